@@ -1,0 +1,211 @@
+"""Headline benchmark: env-steps/sec of the servo vecenv.
+
+One step = the tensor-API loop of test10_servo_vecenv.py:376-456 with the host
+controller replaced by a bank of pre-generated random actions already resident
+in HBM:
+    root[:, 3:10] = actions[k]                     (quat + linear velocity, all 2N actors)
+    gym.set_actor_root_state_tensor(sim, root)      (teleport)
+    gym.simulate(sim); gym.fetch_results(sim, False)
+    gym.refresh_actor_root_state_tensor(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    gym.refresh_dof_state_tensor(sim)               (0 DOFs in S1)
+Weak scaling: every rank owns 4096 envs on its own GPU (one process per GPU,
+launched by torch.distributed.run); envs never interact, so there is no
+collective on the data path. --allgather adds the optional RCCL
+all-gather of the root-state observation.
+
+Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel
+(k_rigid_step, one launch per simulate) at SURVEY.md §8d's algorithmic bytes:
+376 B per env per simulate (2 bodies x (state in 52 + state out 52 + mass
+properties 44 + shape 40)), over its average duration measured with HIP events
+recorded on the simulate stream around every launch of the timed region.
+`cpu_baseline` times the C restatement (oracle/, single thread, "port") on a
+bounded sample of the same workload.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from isaacgym import gymapi, gymtorch  # noqa: E402
+from test_isaacgym_amd import _native as N  # noqa: E402
+from test_isaacgym_amd import scenes  # noqa: E402
+
+METRIC = "env-steps/sec (whole node), 4096 servo envs; 1/2/4/8-GPU scaling"
+ENVS_PER_GPU = 4096
+SIM_BYTES_PER_ENV = 376          # simulate share of the 688 B/env-step
+STEP_BYTES_PER_ENV = 688         # whole tensor-API step
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def cpu_baseline(seconds=10.0):
+    """The oracle (C restatement, one thread) on the same 4096-env scene."""
+    import oracle
+    gym = gymapi.acquire_gym()
+    sim, _ = scenes.servo_scene(gym, ENVS_PER_GPU, use_gpu_pipeline=False)
+    sim.build_model()
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    roots = sim.model_arrays["actor_root_body"]
+    acts = scenes.servo_actions(ENVS_PER_GPU, 16, "cpu", seed=0).numpy()
+    dof = np.zeros((0, 2), np.float32)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        st[roots, 3:10] = acts[steps % len(acts)]
+        oracle.step(p, m, st, dof)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and steps >= 5:
+            break
+    return {"value": ENVS_PER_GPU * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": "%d simulate() steps of the 4096-env servo scene with random root teleports, "
+                      "oracle/migym_oracle.c single-threaded (%.1f s)" % (steps, el)}
+
+
+def load_traffic():
+    """HBM bytes per k_rigid_step launch from the committed rocprofv3 PMC pass
+    (profiles/*pmc*.json, written by profiles/collect_pmc.py), else None."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_rigid.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=600)
+    ap.add_argument("--warmup", type=int, default=60)
+    ap.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
+    ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of the root state every step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    gym = gymapi.acquire_gym()
+    n = args.envs
+    sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=local)
+    gym.prepare_sim(sim)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    gym.acquire_rigid_body_state_tensor(sim)
+    gym.acquire_dof_state_tensor(sim)
+    acts = scenes.servo_actions(n, 64, dev, seed=rank)
+    gathered = None
+    if args.allgather and world > 1:
+        gathered = torch.empty((world,) + tuple(root.shape), dtype=root.dtype, device=dev)
+
+    def step(k):
+        root[:, 3:10] = acts[k % acts.shape[0]]
+        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.simulate(sim)
+        gym.fetch_results(sim, False)
+        gym.refresh_actor_root_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_dof_state_tensor(sim)
+        if gathered is not None:
+            dist.all_gather_into_tensor(gathered, root)
+
+    gym.refresh_actor_root_state_tensor(sim)
+    for k in range(args.warmup):
+        step(k)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # live kernel timing of the timed region's simulate() launches (HIP events)
+    avg = ctypes.c_float()
+    lo = ctypes.c_float()
+    hi = ctypes.c_float()
+    used = N.lib.mg_step_time_stats(sim.native, min(args.steps, 512), ctypes.byref(avg), ctypes.byref(lo),
+                                    ctypes.byref(hi))
+    kern_ms = avg.value if used > 0 else float("nan")
+
+    ms_per_step = 1e3 * el / args.steps
+    value = world * n * args.steps / el
+    bytes_launch = SIM_BYTES_PER_ENV * n
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if used > 0 else None
+    traffic = load_traffic()
+    out = None
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded random root-state teleports, SURVEY.md §8d S1)",
+            "config": {
+                "workload": "S1 servo vecenv: test10_servo_vecenv.py scene (UAV + ground vehicle per env, "
+                            "ground plane, dt 1/60, 2 substeps, TGS 6/1), random quat + linvel teleports "
+                            "every step, full tensor-API loop",
+                "envs_per_gpu": n,
+                "global_envs": world * n,
+                "parallelism": "env-sharded, one process per GPU%s" % (", RCCL all-gather of root state"
+                                                                        if gathered is not None else
+                                                                        ", no collectives"),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_rigid_step",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": bytes_launch,
+                "kernel_ms_avg": kern_ms,
+                "kernel_ms_min": lo.value if used > 0 else None,
+                "kernel_launches_timed": int(used),
+                "note": "working set of 4096 envs (~2.8 MB) sits in L2/MALL: the step is launch/latency "
+                        "bound at this size (SURVEY.md §0.10)",
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            out["cpu_baseline"]["cores"] = 1
+        print(json.dumps(out), flush=True)
+    gym.destroy_sim(sim)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

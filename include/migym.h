@@ -1,0 +1,217 @@
+/*
+ * migym.h — C ABI of libmigym.so, the MI355X-native rigid-body engine that sits
+ * behind the isaacgym.gymapi / gymtorch tensor API.
+ *
+ * This is the drop-in boundary of the hot path. The reference
+ * binds these operations through Isaac Gym's closed pybind11 module; each entry
+ * point below names the reference call site it replaces. The Python mirror
+ * (test_isaacgym_amd/gymapi.py) binds them with ctypes; INTEGRATION.md shows the
+ * binding stub.
+ *
+ * Conventions
+ *   - plain pointers and sizes only; no torch types cross this boundary;
+ *   - every function returns an int status (MG_OK == 0, negative on error) unless
+ *     it returns a handle (NULL on failure), like Isaac Gym's creators returning
+ *     None; mg_last_error() gives the message;
+ *   - `stream` is a hipStream_t passed as void* (0 = the null stream); every
+ *     device operation is enqueued on it, so it orders with the caller's torch
+ *     work on the same stream;
+ *   - `*_host` flags say whether a tensor pointer is host memory (CPU pipeline,
+ *     use_gpu_pipeline=False) or device memory (GPU pipeline);
+ *   - tensor layouts are those of Isaac Gym's tensor API:
+ *       actor root state  (num_actors, 13)  [p.xyz, q.xyzw, v.xyz, w.xyz]
+ *       rigid body state  (num_bodies, 13)  same columns
+ *       dof state         (num_dofs, 2)     [pos, vel]
+ *       net contact force (num_bodies, 3)
+ *     rows are env-major, then actor creation order, then body/DOF tree order.
+ */
+#ifndef MIGYM_H
+#define MIGYM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MG_ABI_VERSION 1
+
+/* status codes */
+#define MG_OK              0
+#define MG_ERR_ARG        -1
+#define MG_ERR_DEVICE     -2
+#define MG_ERR_STATE      -3
+#define MG_ERR_UNSUPPORTED -4
+
+/* shape record types (mg_model.shapes[i*MG_SHAPE_STRIDE + 0]) */
+#define MG_SHAPE_SPHERE   0
+#define MG_SHAPE_BOX      1
+#define MG_SHAPE_CAPSULE  2
+
+/* body kinds (mg_model.body_kind) */
+#define MG_BODY_FREE      0   /* single-body dynamic actor: free-body kernel */
+#define MG_BODY_STATIC    1   /* fixed single-body actor: never integrated */
+#define MG_BODY_LINK      2   /* link of an articulation: articulation kernel */
+
+/* joint types (mg_model.tmpl_link_i[l*4 + 1]) — values of gymapi.JointType */
+#define MG_JOINT_FIXED     0
+#define MG_JOINT_REVOLUTE  1
+#define MG_JOINT_PRISMATIC 2
+
+/* DOF drive modes — values of gymapi.DofDriveMode */
+#define MG_DOF_MODE_NONE   0
+#define MG_DOF_MODE_POS    1
+#define MG_DOF_MODE_VEL    2
+#define MG_DOF_MODE_EFFORT 3
+
+/* record strides (floats / int32 per record) */
+#define MG_STATE_N        13  /* body/root state columns */
+#define MG_MASS_N         12  /* inv_mass, inv_I[3] (principal), iq[4] (principal frame, xyzw), com[3], mass */
+#define MG_TBODY_F_N       8  /* lin_damp, ang_damp, max_lin_vel, max_ang_vel, gravity_on, pad[3] */
+#define MG_TBODY_I_N       4  /* shape_start, shape_count, pad, pad */
+#define MG_SHAPE_STRIDE   16  /* type, size[3], p[3], q[4], friction, restitution, pad[3] */
+#define MG_DOFPROP_N      12  /* mode, kp, kd, effort, max_vel, lower, upper, has_limits, armature, friction, pad[2] */
+#define MG_LINK_F_N       16  /* joint origin p[3], q[4] (parent link frame), axis[3] (joint frame), pad[6] */
+#define MG_LINK_I_N        4  /* parent (local, -1 root), joint type, dof (local, -1 none), pad */
+#define MG_ARTIC_I_N       4  /* first_body, first_dof, tmpl, pad */
+#define MG_ATMPL_I_N       4  /* first_link (into tmpl_link_*), num_links, num_dofs, fixed_base */
+
+/* Simulation parameters: gymapi.SimParams + PhysXParams + the ground plane
+ * (reference: test10_servo_vecenv.py:117-144 and :198-206). */
+typedef struct mg_sim_params {
+    float   dt;                         /* SimParams.dt */
+    int32_t substeps;                   /* SimParams.substeps */
+    float   gravity[3];                 /* SimParams.gravity */
+    int32_t up_axis;                    /* 0 = Y, 1 = Z */
+    int32_t num_position_iterations;    /* PhysXParams.num_position_iterations */
+    int32_t num_velocity_iterations;    /* PhysXParams.num_velocity_iterations */
+    float   contact_offset;             /* PhysXParams.contact_offset */
+    float   rest_offset;                /* PhysXParams.rest_offset */
+    float   bounce_threshold_velocity;  /* PhysXParams.bounce_threshold_velocity */
+    float   max_depenetration_velocity; /* PhysXParams.max_depenetration_velocity */
+    int32_t has_ground;                 /* gym.add_ground called */
+    float   ground_normal[3];           /* PlaneParams.normal (normalised) */
+    float   ground_distance;            /* plane: dot(n, x) + distance = 0 */
+    float   ground_static_friction;
+    float   ground_dynamic_friction;
+    float   ground_restitution;
+    int32_t reserved[8];
+} mg_sim_params;
+
+/* The packed scene, built by the host scene builder at prepare_sim / first
+ * tensor access (reference: create_env/create_actor, test10_servo_vecenv.py:
+ * 300-323; indexing semantics SURVEY.md §8a rows a2-a5). All pointers are host
+ * memory; mg_upload_model copies them to HBM. */
+typedef struct mg_model {
+    int32_t num_envs, num_actors, num_bodies, num_dofs;
+    int32_t num_tmpl_bodies, num_shapes;
+    int32_t num_artics, num_artic_tmpls, num_tmpl_links;
+    int32_t reserved_i[7];
+
+    const float*   body_state0;   /* [num_bodies][13] initial state, AoS */
+    const float*   body_mass;     /* [num_bodies][MG_MASS_N] */
+    const int32_t* body_kind;     /* [num_bodies] MG_BODY_* */
+    const int32_t* body_tmpl;     /* [num_bodies] index into tmpl_body_* */
+    const float*   tmpl_body_f;   /* [num_tmpl_bodies][MG_TBODY_F_N] */
+    const int32_t* tmpl_body_i;   /* [num_tmpl_bodies][MG_TBODY_I_N] */
+    const float*   shapes;        /* [num_shapes][MG_SHAPE_STRIDE] */
+    const int32_t* actor_root_body; /* [num_actors] global body index of each actor's root */
+    const int32_t* actor_dof;     /* [num_actors+1] first global DOF of each actor (CSR) */
+
+    const float*   dof_state0;    /* [num_dofs][2] */
+    const float*   dof_props;     /* [num_dofs][MG_DOFPROP_N] */
+    const int32_t* artic_i;       /* [num_artics][MG_ARTIC_I_N] */
+    const int32_t* artic_tmpl_i;  /* [num_artic_tmpls][MG_ATMPL_I_N] */
+    const float*   tmpl_link_f;   /* [num_tmpl_links][MG_LINK_F_N] */
+    const int32_t* tmpl_link_i;   /* [num_tmpl_links][MG_LINK_I_N] */
+    const void*    reserved_p[3];
+} mg_model;
+
+typedef struct mg_sim mg_sim;
+
+/* ---- library / device ---------------------------------------------------- */
+int32_t     mg_abi_version(void);
+const char* mg_last_error(void);
+int32_t     mg_device_count(void);           /* HIP devices visible; 0 on a host without a GPU */
+
+/* ---- sim lifetime ---------------------------------------------------------
+ * gym.create_sim (test10_servo_vecenv.py:185) / gym.destroy_sim (:474).
+ * Returns NULL when no HIP device is usable — the Python layer then returns
+ * None, as Isaac Gym does (:187-189). */
+mg_sim*     mg_create_sim(int32_t device, const mg_sim_params* params);
+void        mg_destroy_sim(mg_sim* sim);
+int32_t     mg_set_sim_params(mg_sim* sim, const mg_sim_params* params);
+/* gym.prepare_sim (examples/franka_cube_ik_osc.py:288), or the lazy first
+ * tensor access of test10 (which never calls prepare_sim). */
+int32_t     mg_upload_model(mg_sim* sim, const mg_model* model);
+
+/* ---- stepping --------------------------------------------------------------
+ * gym.simulate(sim) (test10_servo_vecenv.py:380): one frame of dt as
+ * `substeps` TGS substeps, one fused kernel per body class. Asynchronous. */
+int32_t     mg_simulate(mg_sim* sim, void* stream);
+/* gym.fetch_results(sim, wait) (:381): waits for the last simulate when wait. */
+int32_t     mg_fetch_results(mg_sim* sim, int32_t wait);
+
+/* ---- tensor API: refresh (state -> user tensor) ----------------------------
+ * gym.refresh_actor_root_state_tensor (:394), refresh_rigid_body_state_tensor
+ * (:395), refresh_dof_state_tensor (:396), refresh_net_contact_force_tensor
+ * (test12_add_joint.py.py:131). `dst` is the persistent tensor handed out by
+ * acquire_*; a host dst is written synchronously. */
+int32_t     mg_refresh_actor_root_state(mg_sim* sim, float* dst, int32_t dst_host, void* stream);
+int32_t     mg_refresh_rigid_body_state(mg_sim* sim, float* dst, int32_t dst_host, void* stream);
+int32_t     mg_refresh_dof_state(mg_sim* sim, float* dst, int32_t dst_host, void* stream);
+int32_t     mg_refresh_net_contact_force(mg_sim* sim, float* dst, int32_t dst_host, void* stream);
+
+/* ---- tensor API: set (user tensor -> state, applied at the next simulate) --
+ * gym.set_actor_root_state_tensor (test10_servo_vecenv.py:456) and the
+ * _indexed variant: `src` is (num_actors, 13); when `idx` is non-NULL only the
+ * n_idx actor rows it lists are applied (idx is int32, host or device like src).
+ * src is consumed in stream order, so the caller may reuse it right away. */
+int32_t     mg_set_actor_root_state(mg_sim* sim, const float* src, int32_t src_host,
+                                    const int32_t* idx, int32_t n_idx, void* stream);
+/* gym.set_rigid_body_state_tensor (test/test05_isaacgym_vel_batch.py:367-385):
+ * free bodies only (articulation links follow their joints). */
+int32_t     mg_set_rigid_body_state(mg_sim* sim, const float* src, int32_t src_host, void* stream);
+/* gym.set_dof_state_tensor[_indexed], set_dof_position_target_tensor,
+ * set_dof_velocity_target_tensor, set_dof_actuation_force_tensor
+ * (examples/franka_cube_ik_osc.py:409-410). idx lists actor indices. */
+int32_t     mg_set_dof_state(mg_sim* sim, const float* src, int32_t src_host,
+                             const int32_t* idx, int32_t n_idx, void* stream);
+int32_t     mg_set_dof_position_target(mg_sim* sim, const float* src, int32_t src_host,
+                                       const int32_t* idx, int32_t n_idx, void* stream);
+int32_t     mg_set_dof_velocity_target(mg_sim* sim, const float* src, int32_t src_host,
+                                       const int32_t* idx, int32_t n_idx, void* stream);
+int32_t     mg_set_dof_actuation_force(mg_sim* sim, const float* src, int32_t src_host,
+                                       const int32_t* idx, int32_t n_idx, void* stream);
+/* DOF drive properties of every DOF, [num_dofs][MG_DOFPROP_N] host array
+ * (gym.set_actor_dof_properties after prepare_sim). */
+int32_t     mg_set_dof_props(mg_sim* sim, const float* props_host);
+/* gym.apply_rigid_body_force_tensors(sim, forces, torques, space): (num_bodies,3)
+ * each or NULL; space 0 = global (ENV_SPACE/GLOBAL), 1 = local (LOCAL_SPACE).
+ * Applied at the body's centre of mass during the next simulate only. */
+int32_t     mg_apply_rigid_body_force(mg_sim* sim, const float* force, const float* torque,
+                                      int32_t space, int32_t src_host, void* stream);
+
+/* ---- Jacobian / mass matrix (examples/franka_cube_ik_osc.py:305-316,345-346) */
+/* Writes the articulation template `tmpl`'s Jacobian (num_instances, L-1 or L, 6, D)
+ * and mass matrix (num_instances, D, D) for fixed-base articulations.  */
+int32_t     mg_refresh_jacobian(mg_sim* sim, int32_t tmpl, float* dst, int32_t dst_host, void* stream);
+int32_t     mg_refresh_mass_matrix(mg_sim* sim, int32_t tmpl, float* dst, int32_t dst_host, void* stream);
+
+/* ---- introspection for tests and the bench ------------------------------- */
+/* Duration in ms of the last simulate()'s kernels (HIP events on `stream`),
+ * -1 when unavailable. Synchronises on the step's end event. */
+float       mg_last_step_ms(mg_sim* sim);
+/* Average / min / max duration in ms of the step kernels of the last n
+ * simulate() calls (a ring of HIP event pairs recorded on the simulate stream
+ * around the kernel launches; at most 512). Returns the count used, or < 0. */
+int32_t     mg_step_time_stats(mg_sim* sim, int32_t n, float* avg_ms, float* min_ms, float* max_ms);
+/* Number of bodies advanced by the free-body kernel / articulations by the
+ * articulation kernel in one simulate. */
+int32_t     mg_num_free_bodies(mg_sim* sim);
+int32_t     mg_num_articulations(mg_sim* sim);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIGYM_H */

@@ -1,0 +1,69 @@
+"""TEST INFRASTRUCTURE ONLY — the CPU restatement of the engine step
+(oracle/migym_oracle.c) as a parity checker. Imported by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg; never by the product
+package test_isaacgym_amd. Physics parity with PhysX is UNPINNED (the
+reference engine is a closed binary absent from the reference tree); see the
+header of migym_oracle.c and DESIGN.md §4.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "liboracle.so")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def _load():
+    if not os.path.exists(LIB):
+        build()
+    lib = ctypes.CDLL(LIB)
+    vp = ctypes.c_void_p
+    lib.oracle_step.restype = ctypes.c_int
+    lib.oracle_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def step(sim_params, model, state, dof, tgt=None, props=None, ext=None, cforce=None, body_range=None):
+    """One gym.simulate() on the host, in place.
+
+    sim_params: _native.MgSimParams; model: _native.MgModel (its arrays alive);
+    state [nb,13] f32, dof [nd,2] f32 (updated in place); tgt [nd,3]; props [nd,12];
+    ext [nb,6]; cforce [nb,3] (written). Returns cforce.
+    """
+    nb = state.shape[0]
+    nd = dof.shape[0]
+    assert state.dtype == np.float32 and state.flags.c_contiguous and state.shape[1] == 13
+    assert dof.dtype == np.float32 and dof.flags.c_contiguous
+    if tgt is None:
+        tgt = np.zeros((max(nd, 1), 3), dtype=np.float32)
+    if cforce is None:
+        cforce = np.zeros((nb, 3), dtype=np.float32)
+    b0, b1 = body_range if body_range is not None else (0, -1)
+    rc = lib().oracle_step(ctypes.addressof(sim_params), ctypes.addressof(model), _ptr(state), _ptr(dof),
+                           _ptr(np.ascontiguousarray(tgt, dtype=np.float32)),
+                           _ptr(None if props is None else np.ascontiguousarray(props, dtype=np.float32)),
+                           _ptr(None if ext is None else np.ascontiguousarray(ext, dtype=np.float32)),
+                           _ptr(cforce), int(b0), int(b1))
+    if rc != 0:
+        raise RuntimeError("oracle_step: unsupported model")
+    return cforce

@@ -1,0 +1,564 @@
+/*
+ * migym_oracle.c — TEST INFRASTRUCTURE ONLY. CPU restatement of the engine's
+ * step, used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * as the checker. Never linked into, or called by, the product path
+ * (test_isaacgym_amd/), which fails loudly without its HIP library.
+ *
+ * What it restates. The reference engine behind gym.simulate() is NVIDIA Isaac
+ * Gym / PhysX, a closed binary that is not in /root/reference (SURVEY.md §0.1,
+ * §8c), so there is no reference source to follow line by line: PHYSICS PARITY
+ * WITH PHYSX IS UNPINNED. This file restates the algorithm DESIGN.md §3 states,
+ * fixed by the reference's call sites:
+ *   - sim parameters: test10_servo_vecenv.py:117-144 (dt 1/60, 2 substeps, TGS
+ *     solver_type=1, 6 position / 1 velocity iterations, contact_offset 0.01,
+ *     rest_offset 0), ground plane :198-206;
+ *   - teleport semantics of set_actor_root_state_tensor: :451-456;
+ *   - drive law of set_actor_dof_properties: examples/dof_controls.py:89-150,
+ *     test13_camera_spherical_joint.py:197-205;
+ *   - the articulated-body algorithm: Featherstone, RBDA Table 7.1.
+ * It is pinned to the device by construction of the test, not to PhysX: the
+ * arithmetic is written in the same evaluation order as the HIP kernels
+ * (test_isaacgym_amd/csrc/mg_rigid.hip, mg_artic.hip), and both sides are
+ * compiled with -ffp-contract=off, so parity is expected bit for bit. Analytic
+ * known-answer tests (tests/test_oracle_kat.py) pin it to physics.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fno-fast-math).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/migym.h"
+
+#define OR_MAXC 8
+#define OR_MAXL 16
+
+typedef struct { float x, y, z; } v3_t;
+typedef struct { float x, y, z, w; } q4_t;
+typedef struct { v3_t c0, c1, c2; } m3_t;
+
+static v3_t V(float x, float y, float z) { v3_t r; r.x = x; r.y = y; r.z = z; return r; }
+static v3_t add3(v3_t a, v3_t b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static v3_t sub3(v3_t a, v3_t b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static v3_t mul3(v3_t a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+static float dot3(v3_t a, v3_t b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static v3_t cross3(v3_t a, v3_t b) { return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static v3_t mad3(v3_t a, v3_t b, float s) { return V(a.x + b.x * s, a.y + b.y * s, a.z + b.z * s); }
+
+static q4_t Q(float x, float y, float z, float w) { q4_t r; r.x = x; r.y = y; r.z = z; r.w = w; return r; }
+static q4_t qmul_(q4_t a, q4_t b) {
+    return Q(a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y,
+             a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x,
+             a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w,
+             a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z);
+}
+static q4_t qnorm_(q4_t a) {
+    float n2 = a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+    float inv;
+    if (!(n2 > 0.0f)) return Q(0.0f, 0.0f, 0.0f, 1.0f);
+    inv = 1.0f / sqrtf(n2);
+    return Q(a.x * inv, a.y * inv, a.z * inv, a.w * inv);
+}
+static v3_t qrot_(q4_t q, v3_t v) {
+    float tx = 2.0f * (q.y * v.z - q.z * v.y);
+    float ty = 2.0f * (q.z * v.x - q.x * v.z);
+    float tz = 2.0f * (q.x * v.y - q.y * v.x);
+    return V(v.x + q.w * tx + (q.y * tz - q.z * ty),
+             v.y + q.w * ty + (q.z * tx - q.x * tz),
+             v.z + q.w * tz + (q.x * ty - q.y * tx));
+}
+static m3_t qmat_(q4_t q) {
+    float xx = q.x * q.x, yy = q.y * q.y, zz = q.z * q.z;
+    float xy = q.x * q.y, xz = q.x * q.z, yz = q.y * q.z;
+    float wx = q.w * q.x, wy = q.w * q.y, wz = q.w * q.z;
+    m3_t m;
+    m.c0 = V(1.0f - 2.0f * (yy + zz), 2.0f * (xy + wz), 2.0f * (xz - wy));
+    m.c1 = V(2.0f * (xy - wz), 1.0f - 2.0f * (xx + zz), 2.0f * (yz + wx));
+    m.c2 = V(2.0f * (xz + wy), 2.0f * (yz - wx), 1.0f - 2.0f * (xx + yy));
+    return m;
+}
+static v3_t mv_(m3_t m, v3_t u) {
+    return V(m.c0.x * u.x + m.c1.x * u.y + m.c2.x * u.z,
+             m.c0.y * u.x + m.c1.y * u.y + m.c2.y * u.z,
+             m.c0.z * u.x + m.c1.z * u.y + m.c2.z * u.z);
+}
+static v3_t mtv_(m3_t m, v3_t v) { return V(dot3(m.c0, v), dot3(m.c1, v), dot3(m.c2, v)); }
+static v3_t invI_world(m3_t Rp, v3_t invI, v3_t v) {
+    v3_t u = mtv_(Rp, v);
+    u = V(u.x * invI.x, u.y * invI.y, u.z * invI.z);
+    return mv_(Rp, u);
+}
+/* sin/cos by Taylor + double angle */
+static void sincos_(float x, float* so, float* co) {
+    int k = 0, i;
+    float x2, s, c;
+    while (x > 0.5f && k < 24) { x = x * 0.5f; k = k + 1; }
+    x2 = x * x;
+    s = x * (1.0f - x2 * (1.0f / 6.0f) * (1.0f - x2 * (1.0f / 20.0f) * (1.0f - x2 * (1.0f / 42.0f) * (1.0f - x2 * (1.0f / 72.0f)))));
+    c = 1.0f - x2 * 0.5f * (1.0f - x2 * (1.0f / 12.0f) * (1.0f - x2 * (1.0f / 30.0f) * (1.0f - x2 * (1.0f / 56.0f) * (1.0f - x2 * (1.0f / 90.0f)))));
+    for (i = 0; i < k; ++i) {
+        float s2 = 2.0f * s * c;
+        float c2 = c * c - s * s;
+        s = s2; c = c2;
+    }
+    *so = s; *co = c;
+}
+static q4_t qint_(q4_t q, v3_t dth) {
+    float th2 = dot3(dth, dth), th, s, c, k;
+    if (!(th2 > 0.0f)) return q;
+    th = sqrtf(th2);
+    sincos_(0.5f * th, &s, &c);
+    k = s / th;
+    return qnorm_(qmul_(Q(dth.x * k, dth.y * k, dth.z * k, c), q));
+}
+
+/* ---- step constants ---------------------------------- */
+typedef struct {
+    float h, sub, inv_sub, inv_h, inv_dt, g[3];
+    int substeps, npos, nvel;
+    float co, ro, maxdep, bounce;
+    int ground;
+    v3_t n, t1, t2;
+    float pd, mu_g, e_g;
+} step_t;
+
+static step_t make_step_(const mg_sim_params* p) {
+    step_t P;
+    int ss = p->substeps > 0 ? p->substeps : 1;
+    int np = p->num_position_iterations > 0 ? p->num_position_iterations : 1;
+    float nx = p->ground_normal[0], ny = p->ground_normal[1], nz = p->ground_normal[2];
+    float ax = 1.0f, ay = 0.0f, az = 0.0f, t1x, t1y, t1z, inv;
+    memset(&P, 0, sizeof P);
+    P.substeps = ss; P.npos = np;
+    P.nvel = p->num_velocity_iterations > 0 ? p->num_velocity_iterations : 0;
+    P.h = p->dt / (float)ss;
+    P.sub = P.h / (float)np;
+    P.inv_sub = 1.0f / P.sub;
+    P.inv_h = 1.0f / P.h;
+    P.inv_dt = 1.0f / p->dt;
+    P.g[0] = p->gravity[0]; P.g[1] = p->gravity[1]; P.g[2] = p->gravity[2];
+    P.co = p->contact_offset; P.ro = p->rest_offset;
+    P.maxdep = p->max_depenetration_velocity; P.bounce = p->bounce_threshold_velocity;
+    P.ground = p->has_ground;
+    P.n = V(nx, ny, nz);
+    P.pd = p->ground_distance;
+    if (!(fabsf(nx) < 0.9f)) { ax = 0.0f; ay = 1.0f; }
+    t1x = ny * az - nz * ay; t1y = nz * ax - nx * az; t1z = nx * ay - ny * ax;
+    inv = 1.0f / sqrtf(t1x * t1x + t1y * t1y + t1z * t1z);
+    t1x = t1x * inv; t1y = t1y * inv; t1z = t1z * inv;
+    P.t1 = V(t1x, t1y, t1z);
+    P.t2 = V(ny * t1z - nz * t1y, nz * t1x - nx * t1z, nx * t1y - ny * t1x);
+    P.mu_g = p->ground_dynamic_friction;
+    P.e_g = p->ground_restitution;
+    return P;
+}
+
+/* ---- free body --------------------------------------- */
+typedef struct {
+    v3_t r; float s0, mu, e, kn, kt1, kt2; v3_t In, It1, It2; float ln, lt1, lt2, vn0;
+} slot_t;
+
+static void contact_normal(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float invm, float tgt) {
+    v3_t rn = cross3(c->r, P->n);
+    float vn = dot3(P->n, *v) + dot3(*w, rn);
+    float dl = c->kn * (tgt - vn);
+    float nl = fmaxf(c->ln + dl, 0.0f);
+    dl = nl - c->ln;
+    c->ln = nl;
+    *v = mad3(*v, P->n, dl * invm);
+    *w = mad3(*w, c->In, dl);
+}
+
+static void contact_friction(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float invm) {
+    v3_t r1 = cross3(c->r, P->t1), r2 = cross3(c->r, P->t2);
+    float vt1 = dot3(P->t1, *v) + dot3(*w, r1);
+    float vt2 = dot3(P->t2, *v) + dot3(*w, r2);
+    float n1 = c->lt1 - c->kt1 * vt1;
+    float n2 = c->lt2 - c->kt2 * vt2;
+    float lim = c->mu * c->ln;
+    float m2 = n1 * n1 + n2 * n2, d1, d2;
+    if (m2 > lim * lim) {
+        float sc = lim / sqrtf(m2);
+        n1 = n1 * sc; n2 = n2 * sc;
+    }
+    d1 = n1 - c->lt1; d2 = n2 - c->lt2;
+    c->lt1 = n1; c->lt2 = n2;
+    *v = mad3(mad3(*v, P->t1, d1 * invm), P->t2, d2 * invm);
+    *w = mad3(mad3(*w, c->It1, d1), c->It2, d2);
+}
+
+static void push_(slot_t* sl, int* nc, v3_t r, float s0, float mu, float e) {
+    if (*nc >= OR_MAXC) return;
+    sl[*nc].r = r; sl[*nc].s0 = s0; sl[*nc].mu = mu; sl[*nc].e = e;
+    *nc = *nc + 1;
+}
+
+static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st, const float* ext, float* cf) {
+    const float* M = m->body_mass + (size_t)b * MG_MASS_N;
+    const int tb = m->body_tmpl[b];
+    const float* tf = m->tmpl_body_f + (size_t)tb * MG_TBODY_F_N;
+    const int sh0 = m->tmpl_body_i[tb * MG_TBODY_I_N + 0], nsh = m->tmpl_body_i[tb * MG_TBODY_I_N + 1];
+    v3_t x = V(st[0], st[1], st[2]);
+    q4_t q = Q(st[3], st[4], st[5], st[6]);
+    v3_t v = V(st[7], st[8], st[9]);
+    v3_t w = V(st[10], st[11], st[12]);
+    const float invm = M[0];
+    const v3_t invI = V(M[1], M[2], M[3]);
+    const q4_t iq = Q(M[4], M[5], M[6], M[7]);
+    const v3_t com = V(M[8], M[9], M[10]);
+    const float h = P->h;
+    const float lin_keep = 1.0f - fminf(tf[0] * h, 1.0f);
+    const float ang_keep = 1.0f - fminf(tf[1] * h, 1.0f);
+    const float max_lv2 = tf[2] * tf[2], max_av2 = tf[3] * tf[3];
+    v3_t fext = V(0.0f, 0.0f, 0.0f), text = V(0.0f, 0.0f, 0.0f), fsum = V(0.0f, 0.0f, 0.0f);
+    int s_, st_;
+    if (ext) { fext = V(ext[0], ext[1], ext[2]); text = V(ext[3], ext[4], ext[5]); }
+    q = qnorm_(q);
+    for (st_ = 0; st_ < P->substeps; ++st_) {
+        const m3_t Rp = qmat_(qmul_(q, iq));
+        const v3_t xc = add3(x, qrot_(q, com));
+        slot_t sl[OR_MAXC];
+        int nc = 0, j, it;
+        v3_t dx = V(0.0f, 0.0f, 0.0f), dth = V(0.0f, 0.0f, 0.0f);
+        if (tf[4] != 0.0f) v = mad3(v, V(P->g[0], P->g[1], P->g[2]), h);
+        v = mad3(v, fext, invm * h);
+        w = mad3(w, invI_world(Rp, invI, text), h);
+        v = mul3(v, lin_keep);
+        w = mul3(w, ang_keep);
+        {
+            float v2 = dot3(v, v), w2;
+            if (v2 > max_lv2) v = mul3(v, sqrtf(max_lv2 / v2));
+            w2 = dot3(w, w);
+            if (w2 > max_av2) w = mul3(w, sqrtf(max_av2 / w2));
+        }
+        if (P->ground) {
+            for (s_ = sh0; s_ < sh0 + nsh; ++s_) {
+                const float* sh = m->shapes + (size_t)s_ * MG_SHAPE_STRIDE;
+                const int type = (int)sh[0];
+                const q4_t qs = qmul_(q, Q(sh[7], sh[8], sh[9], sh[10]));
+                const v3_t cs = add3(x, qrot_(q, V(sh[4], sh[5], sh[6])));
+                const float mu = 0.5f * (sh[11] + P->mu_g);
+                const float e = 0.5f * (sh[12] + P->e_g);
+                if (type == MG_SHAPE_BOX) {
+                    const m3_t Rs = qmat_(qs);
+                    const v3_t a0 = mul3(Rs.c0, sh[1]), a1 = mul3(Rs.c1, sh[2]), a2 = mul3(Rs.c2, sh[3]);
+                    int k;
+                    for (k = 0; k < 8; ++k) {
+                        const float sx = (k & 1) ? 1.0f : -1.0f;
+                        const float sy = (k & 2) ? 1.0f : -1.0f;
+                        const float sz = (k & 4) ? 1.0f : -1.0f;
+                        const v3_t p = add3(add3(add3(cs, mul3(a0, sx)), mul3(a1, sy)), mul3(a2, sz));
+                        const float sep = dot3(P->n, p) + P->pd;
+                        if (sep < P->co) push_(sl, &nc, sub3(p, xc), sep - P->ro, mu, e);
+                    }
+                } else if (type == MG_SHAPE_SPHERE) {
+                    const float sep = dot3(P->n, cs) + P->pd - sh[1];
+                    if (sep < P->co) push_(sl, &nc, sub3(sub3(cs, mul3(P->n, sh[1])), xc), sep - P->ro, mu, e);
+                } else if (type == MG_SHAPE_CAPSULE) {
+                    const v3_t ax = mul3(qrot_(qs, V(1.0f, 0.0f, 0.0f)), sh[2]);
+                    int k;
+                    for (k = 0; k < 2; ++k) {
+                        const v3_t c = k ? add3(cs, ax) : sub3(cs, ax);
+                        const float sep = dot3(P->n, c) + P->pd - sh[1];
+                        if (sep < P->co) push_(sl, &nc, sub3(sub3(c, mul3(P->n, sh[1])), xc), sep - P->ro, mu, e);
+                    }
+                }
+            }
+        }
+        for (j = 0; j < nc; ++j) {
+            const v3_t rn = cross3(sl[j].r, P->n), r1 = cross3(sl[j].r, P->t1), r2 = cross3(sl[j].r, P->t2);
+            sl[j].In = invI_world(Rp, invI, rn);
+            sl[j].It1 = invI_world(Rp, invI, r1);
+            sl[j].It2 = invI_world(Rp, invI, r2);
+            sl[j].kn = 1.0f / (invm + dot3(rn, sl[j].In));
+            sl[j].kt1 = 1.0f / (invm + dot3(r1, sl[j].It1));
+            sl[j].kt2 = 1.0f / (invm + dot3(r2, sl[j].It2));
+            sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
+            sl[j].vn0 = dot3(P->n, v) + dot3(w, rn);
+        }
+        for (it = 0; it < P->npos; ++it) {
+            for (j = 0; j < nc; ++j) {
+                const v3_t rn = cross3(sl[j].r, P->n);
+                const float s = sl[j].s0 + dot3(P->n, dx) + dot3(dth, rn);
+                float tgt = -s * P->inv_sub;
+                if (s < 0.0f) tgt = fminf(tgt, P->maxdep);
+                contact_normal(P, &sl[j], &v, &w, invm, tgt);
+            }
+            for (j = 0; j < nc; ++j) contact_friction(P, &sl[j], &v, &w, invm);
+            dx = mad3(dx, v, P->sub);
+            dth = mad3(dth, w, P->sub);
+        }
+        for (it = 0; it < P->nvel; ++it) {
+            for (j = 0; j < nc; ++j) {
+                const v3_t rn = cross3(sl[j].r, P->n);
+                const float s = sl[j].s0 + dot3(P->n, dx) + dot3(dth, rn);
+                float tgt = s > 0.0f ? -s * P->inv_h : 0.0f;
+                if (sl[j].e > 0.0f && sl[j].vn0 < -P->bounce) tgt = fmaxf(tgt, -sl[j].e * sl[j].vn0);
+                contact_normal(P, &sl[j], &v, &w, invm, tgt);
+            }
+            for (j = 0; j < nc; ++j) contact_friction(P, &sl[j], &v, &w, invm);
+        }
+        for (j = 0; j < nc; ++j) {
+            fsum = mad3(fsum, P->n, sl[j].ln);
+            fsum = mad3(fsum, P->t1, sl[j].lt1);
+            fsum = mad3(fsum, P->t2, sl[j].lt2);
+        }
+        {
+            const v3_t xc1 = add3(xc, dx);
+            q = qint_(q, dth);
+            x = sub3(xc1, qrot_(q, com));
+        }
+    }
+    st[0] = x.x; st[1] = x.y; st[2] = x.z;
+    st[3] = q.x; st[4] = q.y; st[5] = q.z; st[6] = q.w;
+    st[7] = v.x; st[8] = v.y; st[9] = v.z;
+    st[10] = w.x; st[11] = w.y; st[12] = w.z;
+    cf[0] = fsum.x * P->inv_dt; cf[1] = fsum.y * P->inv_dt; cf[2] = fsum.z * P->inv_dt;
+}
+
+/* ---- spatial algebra ----------------------------------- */
+typedef struct { v3_t w, v; } sv_t;
+typedef struct { m3_t A, B, C; } si_t;
+
+static sv_t SVc(v3_t w, v3_t v) { sv_t r; r.w = w; r.v = v; return r; }
+static sv_t sv0(void) { return SVc(V(0.0f, 0.0f, 0.0f), V(0.0f, 0.0f, 0.0f)); }
+static sv_t svadd_(sv_t a, sv_t b) { return SVc(add3(a.w, b.w), add3(a.v, b.v)); }
+static sv_t svmul_(sv_t a, float s) { return SVc(mul3(a.w, s), mul3(a.v, s)); }
+static float svdot_(sv_t a, sv_t b) { return dot3(a.w, b.w) + dot3(a.v, b.v); }
+static sv_t crm_(sv_t a, sv_t b) { return SVc(cross3(a.w, b.w), add3(cross3(a.w, b.v), cross3(a.v, b.w))); }
+static sv_t crf_(sv_t a, sv_t f) { return SVc(add3(cross3(a.w, f.w), cross3(a.v, f.v)), cross3(a.w, f.v)); }
+static m3_t M3c(v3_t c0, v3_t c1, v3_t c2) { m3_t m; m.c0 = c0; m.c1 = c1; m.c2 = c2; return m; }
+static m3_t madd_(m3_t a, m3_t b) { return M3c(add3(a.c0, b.c0), add3(a.c1, b.c1), add3(a.c2, b.c2)); }
+static m3_t msub_(m3_t a, m3_t b) { return M3c(sub3(a.c0, b.c0), sub3(a.c1, b.c1), sub3(a.c2, b.c2)); }
+static m3_t mmul_(m3_t a, m3_t b) { return M3c(mv_(a, b.c0), mv_(a, b.c1), mv_(a, b.c2)); }
+static m3_t mt_(m3_t a) { return M3c(V(a.c0.x, a.c1.x, a.c2.x), V(a.c0.y, a.c1.y, a.c2.y), V(a.c0.z, a.c1.z, a.c2.z)); }
+static m3_t mskew_(v3_t r) { return M3c(V(0.0f, r.z, -r.y), V(-r.z, 0.0f, r.x), V(r.y, -r.x, 0.0f)); }
+static m3_t mouter_(v3_t a, v3_t b, float s) { return M3c(mul3(a, b.x * s), mul3(a, b.y * s), mul3(a, b.z * s)); }
+static sv_t simul_(si_t I, sv_t m) { return SVc(add3(mv_(I.A, m.w), mv_(I.B, m.v)), add3(mtv_(I.B, m.w), mv_(I.C, m.v))); }
+static sv_t xmot_(m3_t E, v3_t r, sv_t m) { return SVc(mv_(E, m.w), mv_(E, sub3(m.v, cross3(r, m.w)))); }
+static sv_t xfrc_t_(m3_t E, v3_t r, sv_t f) {
+    v3_t n = mtv_(E, f.w), fo = mtv_(E, f.v);
+    return SVc(add3(n, cross3(r, fo)), fo);
+}
+static si_t xin_t_(m3_t E, v3_t r, si_t I) {
+    m3_t Et = mt_(E);
+    m3_t A = mmul_(mmul_(Et, I.A), E), B = mmul_(mmul_(Et, I.B), E), C = mmul_(mmul_(Et, I.C), E);
+    m3_t rx = mskew_(r);
+    si_t o;
+    o.A = madd_(msub_(A, mmul_(B, rx)), msub_(mmul_(rx, mt_(B)), mmul_(mmul_(rx, C), rx)));
+    o.B = madd_(B, mmul_(rx, C));
+    o.C = C;
+    return o;
+}
+static si_t siadd_(si_t a, si_t b) { si_t o; o.A = madd_(a.A, b.A); o.B = madd_(a.B, b.B); o.C = madd_(a.C, b.C); return o; }
+static si_t sirigid_(float m, v3_t c, m3_t Ic) {
+    si_t o;
+    float cc = dot3(c, c);
+    m3_t ccT = mouter_(c, c, m);
+    m3_t dg = M3c(V(m * cc, 0.0f, 0.0f), V(0.0f, m * cc, 0.0f), V(0.0f, 0.0f, m * cc));
+    o.A = madd_(Ic, msub_(dg, ccT));
+    o.B = mskew_(mul3(c, m));
+    o.C = M3c(V(m, 0.0f, 0.0f), V(0.0f, m, 0.0f), V(0.0f, 0.0f, m));
+    return o;
+}
+static q4_t qaxang_(v3_t a, float th) {
+    float s, c, half = 0.5f * th, ah = half < 0.0f ? -half : half;
+    sincos_(ah, &s, &c);
+    if (half < 0.0f) s = -s;
+    return Q(a.x * s, a.y * s, a.z * s, c);
+}
+
+/* joint transform of link l at (q, qd): relative rotation/translation, S, vJ */
+static void joint_(const float* lf, int jt, float qj, q4_t* qrel, v3_t* rr, sv_t* S) {
+    const v3_t po = V(lf[0], lf[1], lf[2]);
+    const q4_t qo = Q(lf[3], lf[4], lf[5], lf[6]);
+    const v3_t ax = V(lf[7], lf[8], lf[9]);
+    *qrel = qo; *rr = po; *S = sv0();
+    if (jt == MG_JOINT_REVOLUTE) {
+        *qrel = qmul_(qo, qaxang_(ax, qj));
+        *S = SVc(ax, V(0.0f, 0.0f, 0.0f));
+    } else if (jt == MG_JOINT_PRISMATIC) {
+        *rr = add3(po, qrot_(qo, mul3(ax, qj)));
+        *S = SVc(V(0.0f, 0.0f, 0.0f), ax);
+    }
+}
+
+/* ---- articulation: Featherstone ABA, implicit drives ---- */
+static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* state /*[nb][13]*/,
+                      float* dof /*[nd][2]*/, const float* tgt /*[nd][3]*/, const float* props /*[nd][12]*/,
+                      float* cforce) {
+    const int b0 = ai[0], d0 = ai[1], t = ai[2];
+    const int* ti = m->artic_tmpl_i + (size_t)t * MG_ATMPL_I_N;
+    const int fl = ti[0], L = ti[1], D = ti[2], fixed_base = ti[3];
+    const float* LF = m->tmpl_link_f + (size_t)fl * MG_LINK_F_N;
+    const int* LI = m->tmpl_link_i + (size_t)fl * MG_LINK_I_N;
+    const float h = P->h;
+    float q[OR_MAXL], qd[OR_MAXL], qdd[OR_MAXL], Dl[OR_MAXL], ul[OR_MAXL];
+    m3_t E[OR_MAXL];
+    v3_t r[OR_MAXL];
+    sv_t Sj[OR_MAXL], v[OR_MAXL], c[OR_MAXL], pA[OR_MAXL], U[OR_MAXL], a[OR_MAXL];
+    si_t IA[OR_MAXL];
+    q4_t ql[OR_MAXL];
+    v3_t xl[OR_MAXL];
+    const float* s0 = state + (size_t)b0 * MG_STATE_N;
+    const v3_t x0 = V(s0[0], s0[1], s0[2]);
+    const q4_t q0 = qnorm_(Q(s0[3], s0[4], s0[5], s0[6]));
+    const float grav_on = m->tmpl_body_f[(size_t)m->body_tmpl[b0] * MG_TBODY_F_N + 4];
+    const v3_t gw = grav_on != 0.0f ? V(P->g[0], P->g[1], P->g[2]) : V(0.0f, 0.0f, 0.0f);
+    const v3_t gb = qrot_(Q(-q0.x, -q0.y, -q0.z, q0.w), gw);
+    int d, l, st_;
+    if (!fixed_base || L > OR_MAXL) return -1;
+    for (d = 0; d < D; ++d) { q[d] = dof[(d0 + d) * 2 + 0]; qd[d] = dof[(d0 + d) * 2 + 1]; qdd[d] = 0.0f; }
+    for (st_ = 0; st_ < P->substeps; ++st_) {
+        for (l = 0; l < L; ++l) {
+            const int p = LI[l * MG_LINK_I_N + 0], jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
+            const float* M = m->body_mass + (size_t)(b0 + l) * MG_MASS_N;
+            if (p < 0) {
+                E[l] = M3c(V(1.0f, 0.0f, 0.0f), V(0.0f, 1.0f, 0.0f), V(0.0f, 0.0f, 1.0f));
+                r[l] = V(0.0f, 0.0f, 0.0f);
+                Sj[l] = sv0(); v[l] = sv0(); c[l] = sv0();
+            } else {
+                q4_t qrel; v3_t rr; sv_t s, vJ;
+                const float qj = dj >= 0 ? q[dj] : 0.0f, qdj = dj >= 0 ? qd[dj] : 0.0f;
+                joint_(LF + l * MG_LINK_F_N, jt, qj, &qrel, &rr, &s);
+                E[l] = mt_(qmat_(qrel));
+                r[l] = rr;
+                Sj[l] = s;
+                vJ = svmul_(s, qdj);
+                v[l] = svadd_(xmot_(E[l], rr, v[p]), vJ);
+                c[l] = crm_(v[l], vJ);
+            }
+            {
+                const float mass = M[11];
+                const v3_t com = V(M[8], M[9], M[10]);
+                const q4_t iq = Q(M[4], M[5], M[6], M[7]);
+                const v3_t Id = V(M[1] > 0.0f ? 1.0f / M[1] : 0.0f, M[2] > 0.0f ? 1.0f / M[2] : 0.0f,
+                                  M[3] > 0.0f ? 1.0f / M[3] : 0.0f);
+                const m3_t Rq = qmat_(iq);
+                const m3_t Ic = mmul_(mmul_(Rq, M3c(V(Id.x, 0.0f, 0.0f), V(0.0f, Id.y, 0.0f), V(0.0f, 0.0f, Id.z))), mt_(Rq));
+                IA[l] = sirigid_(mass, com, Ic);
+                pA[l] = crf_(v[l], simul_(IA[l], v[l]));
+            }
+        }
+        for (l = L - 1; l >= 1; --l) {
+            const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
+            si_t Ia = IA[l];
+            sv_t pa;
+            if (dj >= 0) {
+                const float* pr = props + (size_t)(d0 + dj) * MG_DOFPROP_N;
+                const float* tg = tgt + (size_t)(d0 + dj) * 3;
+                const int mode = (int)pr[0];
+                const float kp = pr[1], kd = pr[2], eff = pr[3], arm = pr[8];
+                float tau = 0.0f, imp = 0.0f, invD;
+                if (mode == MG_DOF_MODE_POS) {
+                    tau = kp * (tg[0] - q[dj] - h * qd[dj]) + kd * (tg[1] - qd[dj]);
+                    imp = h * kd + h * h * kp;
+                } else if (mode == MG_DOF_MODE_VEL) {
+                    tau = kd * (tg[1] - qd[dj]);
+                    imp = h * kd;
+                } else if (mode == MG_DOF_MODE_EFFORT) {
+                    tau = tg[2];
+                }
+                if (eff > 0.0f && (tau > eff || tau < -eff)) {
+                    tau = tau > eff ? eff : -eff;
+                    imp = 0.0f;
+                }
+                U[l] = simul_(Ia, Sj[l]);
+                Dl[l] = svdot_(Sj[l], U[l]) + arm + imp;
+                ul[l] = tau - svdot_(Sj[l], pA[l]);
+                invD = 1.0f / Dl[l];
+                Ia.A = msub_(Ia.A, mouter_(U[l].w, U[l].w, invD));
+                Ia.B = msub_(Ia.B, mouter_(U[l].w, U[l].v, invD));
+                Ia.C = msub_(Ia.C, mouter_(U[l].v, U[l].v, invD));
+                pa = svadd_(svadd_(pA[l], simul_(Ia, c[l])), svmul_(U[l], ul[l] * invD));
+            } else {
+                pa = svadd_(pA[l], simul_(Ia, c[l]));
+            }
+            if (p > 0 || (p == 0 && !fixed_base)) {
+                IA[p] = siadd_(IA[p], xin_t_(E[l], r[l], Ia));
+                pA[p] = svadd_(pA[p], xfrc_t_(E[l], r[l], pa));
+            }
+        }
+        a[0] = SVc(V(0.0f, 0.0f, 0.0f), mul3(gb, -1.0f));
+        for (l = 1; l < L; ++l) {
+            const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
+            sv_t ap = svadd_(xmot_(E[l], r[l], a[p]), c[l]);
+            if (dj >= 0) {
+                const float acc = (ul[l] - svdot_(U[l], ap)) / Dl[l];
+                qdd[dj] = acc;
+                ap = svadd_(ap, svmul_(Sj[l], acc));
+            }
+            a[l] = ap;
+        }
+        for (d = 0; d < D; ++d) {
+            const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
+            const float maxv = pr[4];
+            float wv = qd[d] + h * qdd[d], xv;
+            if (maxv > 0.0f) wv = fminf(fmaxf(wv, -maxv), maxv);
+            xv = q[d] + h * wv;
+            if (pr[7] != 0.0f) {
+                const float lo = pr[5], hi = pr[6];
+                if (xv < lo) { xv = lo; if (wv < 0.0f) wv = 0.0f; }
+                if (xv > hi) { xv = hi; if (wv > 0.0f) wv = 0.0f; }
+            }
+            q[d] = xv; qd[d] = wv;
+        }
+    }
+    for (d = 0; d < D; ++d) { dof[(d0 + d) * 2 + 0] = q[d]; dof[(d0 + d) * 2 + 1] = qd[d]; }
+    for (l = 0; l < L; ++l) {
+        const int p = LI[l * MG_LINK_I_N + 0], jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
+        const float* M = m->body_mass + (size_t)(b0 + l) * MG_MASS_N;
+        float* so = state + (size_t)(b0 + l) * MG_STATE_N;
+        v3_t ww, vw, com = V(M[8], M[9], M[10]);
+        if (p < 0) {
+            ql[l] = q0; xl[l] = x0; v[l] = sv0();
+        } else {
+            q4_t qrel; v3_t rr; sv_t s;
+            const float qj = dj >= 0 ? q[dj] : 0.0f, qdj = dj >= 0 ? qd[dj] : 0.0f;
+            joint_(LF + l * MG_LINK_F_N, jt, qj, &qrel, &rr, &s);
+            ql[l] = qnorm_(qmul_(ql[p], qrel));
+            xl[l] = add3(xl[p], qrot_(ql[p], rr));
+            v[l] = svadd_(xmot_(mt_(qmat_(qrel)), rr, v[p]), svmul_(s, qdj));
+        }
+        ww = qrot_(ql[l], v[l].w);
+        vw = qrot_(ql[l], add3(v[l].v, cross3(v[l].w, com)));
+        so[0] = xl[l].x; so[1] = xl[l].y; so[2] = xl[l].z;
+        so[3] = ql[l].x; so[4] = ql[l].y; so[5] = ql[l].z; so[6] = ql[l].w;
+        so[7] = vw.x; so[8] = vw.y; so[9] = vw.z;
+        so[10] = ww.x; so[11] = ww.y; so[12] = ww.z;
+        cforce[(size_t)(b0 + l) * 3 + 0] = 0.0f;
+        cforce[(size_t)(b0 + l) * 3 + 1] = 0.0f;
+        cforce[(size_t)(b0 + l) * 3 + 2] = 0.0f;
+    }
+    return 0;
+}
+
+/* ---- entry point --------------------------------------------------------
+ * One gym.simulate() over the whole model, AoS host arrays:
+ *   state [nb][13] in/out, dof [nd][2] in/out, tgt [nd][3] (target pos, target
+ *   vel, actuation force), props [nd][12] (NULL = model->dof_props),
+ *   ext [nb][6] world force/torque at the COM or NULL, cforce [nb][3] out.
+ * Bodies in [body_begin, body_end) only (a bounded CPU-baseline sample);
+ * articulations are stepped when their root lies in that range. Returns 0, or
+ * -1 for an unsupported model. */
+int oracle_step(const mg_sim_params* p, const mg_model* m, float* state, float* dof, const float* tgt,
+                const float* props, const float* ext, float* cforce, int body_begin, int body_end) {
+    step_t P = make_step_(p);
+    int b, k;
+    if (!props) props = m->dof_props;
+    if (body_end < 0 || body_end > m->num_bodies) body_end = m->num_bodies;
+    for (k = 0; k < m->num_artics; ++k) {
+        const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;
+        if (ai[0] < body_begin || ai[0] >= body_end) continue;
+        if (artic_step(&P, m, ai, state, dof, tgt, props, cforce) != 0) return -1;
+    }
+    for (b = body_begin; b < body_end; ++b) {
+        if (m->body_kind[b] != MG_BODY_FREE) continue;
+        rigid_body_step(&P, m, b, state + (size_t)b * MG_STATE_N, ext ? ext + (size_t)b * 6 : NULL,
+                        cforce + (size_t)b * 3);
+    }
+    return 0;
+}
+
+int oracle_abi_version(void) { return MG_ABI_VERSION; }

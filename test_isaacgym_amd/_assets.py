@@ -1,0 +1,534 @@
+"""Asset import: URDF files and primitive assets, mass properties, body / joint /
+DOF ordering.
+
+Reference behaviour this mirrors (SURVEY.md §2 "URDF/MJCF/mesh importer", §8a a10):
+  - gym.load_asset(sim, root, file, AssetOptions) -> Asset, or None on failure
+    (test10_servo_vecenv.py:230-234);
+  - gym.create_box(sim, x, y, z, options) (examples/franka_cube_ik_osc.py:156,161),
+    create_sphere / create_capsule;
+  - bodies in kinematic-tree (depth-first) order from the root link; children in
+    the order their joints are declared. dof_test_camera.urdf declares its links
+    out of order (base, camera, camera_y, camera_z) with the tree
+    base -> z -> y -> camera (assets/urdf/dof_test_camera.urdf:98-119), so its
+    bodies come out [base_link, camera_z_link, camera_y_link, camera_link];
+  - a link with no <inertial>, no collision and no visual geometry that hangs on
+    a fixed joint is merged into its parent (franka's panda_link8: the Jacobian
+    of examples/franka_cube_ik_osc.py:306 has 10 = bodies - 1 rows for a fixed
+    base, i.e. 11 bodies);
+  - missing mass properties are computed from the collision shapes at
+    AssetOptions.density; a mass without an inertia tensor (the UAV and ground
+    vehicle, assets/urdf/uav/urdf/rq-1-predator-mae-uav.urdf:4-7) keeps the mass
+    and takes the shape inertia scaled to it.
+Meshes: collision meshes that exist are represented by their axis-aligned box in
+the mesh frame. The servo scene's two meshes are missing from the reference
+(.MISSING_LARGE_BLOBS:7-8); they get the frozen box proxies of MESH_PROXIES,
+expressed in the body frame.
+"""
+import math
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+from . import _types as T
+
+# body-frame full extents of the frozen proxies for meshes absent from the reference
+MESH_PROXIES = {
+    "predator.obj": (16.0, 20.0, 3.0),                 # rq-1-predator, URDF scale 2
+    "predator_without_sphere.obj": (16.0, 20.0, 3.0),
+    "fusch-apc.obj": (7.5, 3.0, 2.5),                  # tpz-fuchs-apc, URDF scale 0.6
+}
+
+SPHERE, BOX, CAPSULE = 0, 1, 2
+
+
+def _quat_from_rpy(r, p, y):
+    # URDF rpy: fixed-axis roll (x), pitch (y), yaw (z) => R = Rz(y) Ry(p) Rx(r)
+    q = T.Quat.from_euler_zyx(r, p, y)
+    return np.array([q.x, q.y, q.z, q.w], dtype=np.float64)
+
+
+def _qmul(a, b):
+    ax, ay, az, aw = a
+    bx, by, bz, bw = b
+    return np.array([aw * bx + ax * bw + ay * bz - az * by,
+                     aw * by - ax * bz + ay * bw + az * bx,
+                     aw * bz + ax * by - ay * bx + az * bw,
+                     aw * bw - ax * bx - ay * by - az * bz])
+
+
+def _qmat(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+def _mat_to_quat(R):
+    t = np.trace(R)
+    if t > 0:
+        s = math.sqrt(t + 1.0) * 2
+        w = 0.25 * s
+        x = (R[2, 1] - R[1, 2]) / s
+        y = (R[0, 2] - R[2, 0]) / s
+        z = (R[1, 0] - R[0, 1]) / s
+    elif R[0, 0] > R[1, 1] and R[0, 0] > R[2, 2]:
+        s = math.sqrt(1.0 + R[0, 0] - R[1, 1] - R[2, 2]) * 2
+        w = (R[2, 1] - R[1, 2]) / s
+        x = 0.25 * s
+        y = (R[0, 1] + R[1, 0]) / s
+        z = (R[0, 2] + R[2, 0]) / s
+    elif R[1, 1] > R[2, 2]:
+        s = math.sqrt(1.0 + R[1, 1] - R[0, 0] - R[2, 2]) * 2
+        w = (R[0, 2] - R[2, 0]) / s
+        x = (R[0, 1] + R[1, 0]) / s
+        y = 0.25 * s
+        z = (R[1, 2] + R[2, 1]) / s
+    else:
+        s = math.sqrt(1.0 + R[2, 2] - R[0, 0] - R[1, 1]) * 2
+        w = (R[1, 0] - R[0, 1]) / s
+        x = (R[0, 2] + R[2, 0]) / s
+        y = (R[1, 2] + R[2, 1]) / s
+        z = 0.25 * s
+    q = np.array([x, y, z, w])
+    q = q / np.linalg.norm(q)
+    return -q if q[3] < 0 else q
+
+
+class Shape:
+    __slots__ = ("type", "size", "p", "q", "friction", "restitution", "source")
+
+    def __init__(self, type_, size, p=None, q=None, source="primitive"):
+        self.type = type_
+        self.size = tuple(float(s) for s in size)
+        self.p = np.zeros(3) if p is None else np.asarray(p, dtype=np.float64)
+        self.q = np.array([0, 0, 0, 1.0]) if q is None else np.asarray(q, dtype=np.float64)
+        self.friction = 1.0
+        self.restitution = 0.0
+        self.source = source
+
+    def volume(self):
+        if self.type == BOX:
+            return 8.0 * self.size[0] * self.size[1] * self.size[2]
+        if self.type == SPHERE:
+            return 4.0 / 3.0 * math.pi * self.size[0] ** 3
+        r, hh = self.size[0], self.size[1]
+        return math.pi * r * r * 2.0 * hh + 4.0 / 3.0 * math.pi * r ** 3
+
+    def inertia_unit_mass(self):
+        """Rotational inertia about the shape centre, shape frame, per unit mass."""
+        if self.type == BOX:
+            a, b, c = (2 * s for s in self.size)
+            return np.diag([(b * b + c * c) / 12.0, (a * a + c * c) / 12.0, (a * a + b * b) / 12.0])
+        if self.type == SPHERE:
+            r = self.size[0]
+            return np.eye(3) * 0.4 * r * r
+        # capsule along x: cylinder (length 2hh) + two hemispheres
+        r, hh = self.size[0], self.size[1]
+        L = 2.0 * hh
+        vc = math.pi * r * r * L
+        vs = 4.0 / 3.0 * math.pi * r ** 3
+        mc, ms = vc / (vc + vs), vs / (vc + vs)
+        ix = mc * 0.5 * r * r + ms * 0.4 * r * r
+        iy = mc * (L * L / 12.0 + 0.25 * r * r) + ms * (0.4 * r * r + L * L / 4.0 + 3.0 * L * r / 8.0)
+        return np.diag([ix, iy, iy])
+
+
+class Body:
+    def __init__(self, name):
+        self.name = name
+        self.mass = None          # from <inertial>
+        self.com = np.zeros(3)
+        self.inertia = None       # 3x3 about COM, link frame
+        self.has_inertial = False
+        self.has_visual = False
+        self.shapes = []
+
+
+class Joint:
+    def __init__(self, name, jtype, parent, child):
+        self.name = name
+        self.type = jtype
+        self.parent = parent      # body index (after ordering)
+        self.child = child
+        self.p = np.zeros(3)
+        self.q = np.array([0, 0, 0, 1.0])
+        self.axis = np.array([1.0, 0, 0])
+        self.has_limits = False
+        self.lower = 0.0
+        self.upper = 0.0
+        self.effort = 0.0
+        self.velocity = 0.0
+        self.damping = 0.0
+        self.friction = 0.0
+
+    @property
+    def has_dof(self):
+        return self.type in (T.JOINT_REVOLUTE, T.JOINT_PRISMATIC)
+
+
+class MassProps:
+    __slots__ = ("mass", "com", "inertia")
+
+    def __init__(self, mass, com, inertia):
+        self.mass = float(mass)
+        self.com = np.asarray(com, dtype=np.float64)
+        self.inertia = np.asarray(inertia, dtype=np.float64)
+
+    def principal(self):
+        """(inv_mass, inv principal moments[3], principal frame quat xyzw)."""
+        I = 0.5 * (self.inertia + self.inertia.T)
+        w, V = np.linalg.eigh(I)
+        if np.linalg.det(V) < 0:
+            V[:, 2] = -V[:, 2]
+        q = _mat_to_quat(V)
+        invm = 1.0 / self.mass if self.mass > 0 else 0.0
+        invI = np.array([1.0 / x if x > 1e-12 else 0.0 for x in w])
+        return invm, invI, q
+
+
+class Asset:
+    """A loaded asset: bodies in tree order, one joint per non-root body."""
+
+    def __init__(self, name, options):
+        self.name = name
+        self.options = options
+        self.bodies = []
+        self.joints = []          # joints[k] attaches bodies[k + 1] (tree order)
+        self.mass_props = []
+        self.dof_props = None
+        self.shape_props = []
+
+    # ---- derived structure
+    @property
+    def dof_joints(self):
+        return [j for j in self.joints if j.has_dof]
+
+    @property
+    def num_dofs(self):
+        return len(self.dof_joints)
+
+    def dof_of_body(self, b):
+        """local DOF index driven by body b's joint, or -1."""
+        if b == 0:
+            return -1
+        d = 0
+        for k, j in enumerate(self.joints):
+            if k + 1 == b:
+                return d if j.has_dof else -1
+            if j.has_dof:
+                d += 1
+        return -1
+
+    @property
+    def is_articulation(self):
+        return len(self.bodies) > 1 or self.options.fix_base_link
+
+    def finalize(self):
+        opts = self.options
+        self.mass_props = [compute_mass_props(b, opts.density) for b in self.bodies]
+        n = self.num_dofs
+        props = np.zeros(n, dtype=T.DOF_PROPERTIES_DTYPE)
+        for d, j in enumerate(self.dof_joints):
+            props[d]["hasLimits"] = j.has_limits
+            props[d]["lower"] = j.lower
+            props[d]["upper"] = j.upper
+            props[d]["driveMode"] = opts.default_dof_drive_mode
+            props[d]["velocity"] = j.velocity
+            props[d]["effort"] = j.effort
+            props[d]["stiffness"] = 0.0
+            props[d]["damping"] = j.damping
+            props[d]["friction"] = j.friction
+            props[d]["armature"] = opts.armature
+        self.dof_props = props
+        self.shape_props = []
+        for b in self.bodies:
+            for s in b.shapes:
+                sp = T.RigidShapeProperties()
+                sp.friction = s.friction
+                sp.restitution = s.restitution
+                self.shape_props.append(sp)
+        return self
+
+
+def compute_mass_props(body, density):
+    """Mass, COM and inertia about the COM (link frame) of a body."""
+    shapes = body.shapes
+    vols = [s.volume() for s in shapes]
+    vtot = sum(vols)
+    if body.has_inertial and body.inertia is not None and body.mass is not None:
+        return MassProps(body.mass, body.com, body.inertia)
+    if vtot > 0:
+        m_shape = density * vtot
+        com = sum(s.p * v for s, v in zip(shapes, vols)) / vtot
+        I = np.zeros((3, 3))
+        for s, v in zip(shapes, vols):
+            ms = density * v
+            R = _qmat(s.q)
+            Ic = R @ (s.inertia_unit_mass() * ms) @ R.T
+            d = s.p - com
+            I += Ic + ms * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
+        if body.mass is not None:             # mass given, inertia missing: scale the shape inertia
+            scale = body.mass / m_shape
+            com_out = body.com if body.has_inertial else com
+            return MassProps(body.mass, com_out, I * scale)
+        return MassProps(m_shape, com, I)
+    mass = body.mass if body.mass is not None else 1.0
+    return MassProps(mass, body.com, np.eye(3) * 0.01 * mass)
+
+
+# ------------------------------------------------------------------ primitives
+def _primitive_asset(name, shape, options):
+    a = Asset(name, options)
+    b = Body(name)
+    b.shapes.append(shape)
+    b.has_visual = True
+    a.bodies.append(b)
+    return a.finalize()
+
+
+def create_box(width, height, depth, options):
+    return _primitive_asset("box", Shape(BOX, (0.5 * width, 0.5 * height, 0.5 * depth)), options)
+
+
+def create_sphere(radius, options):
+    return _primitive_asset("sphere", Shape(SPHERE, (radius,)), options)
+
+
+def create_capsule(radius, length, options):
+    return _primitive_asset("capsule", Shape(CAPSULE, (radius, 0.5 * length)), options)
+
+
+# ------------------------------------------------------------------ meshes
+def _mesh_vertices(path):
+    ext = os.path.splitext(path)[1].lower()
+    if ext == ".obj":
+        vs = []
+        with open(path, "r", errors="ignore") as f:
+            for line in f:
+                if line.startswith("v "):
+                    parts = line.split()
+                    vs.append([float(parts[1]), float(parts[2]), float(parts[3])])
+        return np.array(vs, dtype=np.float64).reshape(-1, 3)
+    if ext == ".stl":
+        with open(path, "rb") as f:
+            data = f.read()
+        if data[:5].lower() == b"solid" and b"facet" in data[:400]:
+            vs = [[float(t) for t in ln.split()[1:4]] for ln in data.decode(errors="ignore").splitlines()
+                  if ln.strip().startswith("vertex")]
+            return np.array(vs, dtype=np.float64).reshape(-1, 3)
+        n = int(np.frombuffer(data[80:84], dtype="<u4")[0])
+        rec = np.frombuffer(data[84:84 + 50 * n], dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)),
+                                                                   ("a", "<u2")]))
+        return rec["v"].reshape(-1, 3).astype(np.float64)
+    return np.zeros((0, 3))
+
+
+def _resolve(filename, urdf_dir, asset_root):
+    if filename.startswith("package://"):
+        rest = filename[len("package://"):]
+        d = urdf_dir
+        for _ in range(6):
+            cand = os.path.join(d, rest)
+            if os.path.exists(cand):
+                return cand
+            parent = os.path.dirname(d)
+            cand = os.path.join(parent, rest)
+            if os.path.exists(cand):
+                return cand
+            if parent == d:
+                break
+            d = parent
+        return os.path.join(asset_root, rest)
+    if filename.startswith("file://"):
+        filename = filename[len("file://"):]
+    return filename if os.path.isabs(filename) else os.path.join(urdf_dir, filename)
+
+
+def _floats(s, n, default):
+    if s is None:
+        return list(default)
+    v = [float(t) for t in s.split()]
+    return v if len(v) == n else list(default)
+
+
+def _origin(el):
+    o = el.find("origin") if el is not None else None
+    if o is None:
+        return np.zeros(3), np.array([0, 0, 0, 1.0])
+    xyz = _floats(o.get("xyz"), 3, (0, 0, 0))
+    rpy = _floats(o.get("rpy"), 3, (0, 0, 0))
+    return np.array(xyz, dtype=np.float64), _quat_from_rpy(*rpy)
+
+
+def _geometry_shapes(col, urdf_dir, asset_root, options, warnings):
+    geo = col.find("geometry")
+    if geo is None:
+        return []
+    p, q = _origin(col)
+    out = []
+    for g in geo:
+        if g.tag == "box":
+            sx, sy, sz = _floats(g.get("size"), 3, (1, 1, 1))
+            out.append(Shape(BOX, (0.5 * sx, 0.5 * sy, 0.5 * sz), p, q, "box"))
+        elif g.tag == "sphere":
+            out.append(Shape(SPHERE, (float(g.get("radius", 1.0)),), p, q, "sphere"))
+        elif g.tag == "cylinder":
+            r, l = float(g.get("radius", 1.0)), float(g.get("length", 1.0))
+            if options.replace_cylinder_with_capsule:
+                # URDF cylinders run along z, capsules along x
+                qc = _qmul(q, _quat_from_rpy(0.0, -0.5 * math.pi, 0.0))
+                out.append(Shape(CAPSULE, (r, max(0.5 * l - r, 0.0)), p, qc, "cylinder->capsule"))
+            else:
+                out.append(Shape(BOX, (r, r, 0.5 * l), p, q, "cylinder->box"))
+        elif g.tag == "mesh":
+            fn = g.get("filename", "")
+            scale = _floats(g.get("scale"), 3, (1, 1, 1))
+            path = _resolve(fn, urdf_dir, asset_root)
+            base = os.path.basename(fn)
+            if os.path.exists(path):
+                vs = _mesh_vertices(path) * np.array(scale)
+                if len(vs):
+                    lo, hi = vs.min(0), vs.max(0)
+                    c = 0.5 * (lo + hi)
+                    he = np.maximum(0.5 * (hi - lo), 1e-4)
+                    out.append(Shape(BOX, tuple(he), p + _qmat(q) @ c, q, "mesh-aabb:" + base))
+                else:
+                    warnings.append("mesh %s has no vertices" % fn)
+            elif base in MESH_PROXIES:
+                ex = MESH_PROXIES[base]
+                out.append(Shape(BOX, (0.5 * ex[0], 0.5 * ex[1], 0.5 * ex[2]), None, None, "proxy:" + base))
+            else:
+                warnings.append("mesh %s not found; shape skipped" % fn)
+    return out
+
+
+_URDF_JOINT = {"revolute": T.JOINT_REVOLUTE, "continuous": T.JOINT_REVOLUTE, "prismatic": T.JOINT_PRISMATIC,
+               "fixed": T.JOINT_FIXED, "floating": T.JOINT_FLOATING, "planar": T.JOINT_PLANAR}
+
+
+def load_urdf(asset_root, filename, options):
+    path = filename if os.path.isabs(filename) else os.path.join(asset_root, filename)
+    if not os.path.exists(path):
+        raise FileNotFoundError(path)
+    root = ET.parse(path).getroot()
+    urdf_dir = os.path.dirname(os.path.abspath(path))
+    warnings = []
+    links = {}
+    order = []
+    for le in root.findall("link"):
+        b = Body(le.get("name"))
+        ine = le.find("inertial")
+        if ine is not None:
+            b.has_inertial = True
+            p, q = _origin(ine)
+            b.com = p
+            m = ine.find("mass")
+            if m is not None:
+                b.mass = float(m.get("value", 0.0))
+            it = ine.find("inertia")
+            if it is not None:
+                g = lambda k: float(it.get(k, 0.0))  # noqa: E731
+                I = np.array([[g("ixx"), g("ixy"), g("ixz")], [g("ixy"), g("iyy"), g("iyz")],
+                              [g("ixz"), g("iyz"), g("izz")]])
+                R = _qmat(q)
+                b.inertia = R @ I @ R.T
+        b.has_visual = le.find("visual") is not None
+        for col in le.findall("collision"):
+            b.shapes.extend(_geometry_shapes(col, urdf_dir, asset_root, options, warnings))
+        links[b.name] = b
+        order.append(b.name)
+
+    joints = []
+    for je in root.findall("joint"):
+        jt = _URDF_JOINT.get(je.get("type", "fixed"), T.JOINT_FIXED)
+        parent = je.find("parent").get("link")
+        child = je.find("child").get("link")
+        j = Joint(je.get("name"), jt, parent, child)
+        j.p, j.q = _origin(je)
+        ax = je.find("axis")
+        if ax is not None:
+            a = np.array(_floats(ax.get("xyz"), 3, (1, 0, 0)))
+            n = np.linalg.norm(a)
+            j.axis = a / n if n > 0 else np.array([1.0, 0, 0])
+        lim = je.find("limit")
+        if lim is not None:
+            j.effort = float(lim.get("effort", 0.0))
+            j.velocity = float(lim.get("velocity", 0.0))
+            if je.get("type") in ("revolute", "prismatic"):
+                j.has_limits = True
+                j.lower = float(lim.get("lower", 0.0))
+                j.upper = float(lim.get("upper", 0.0))
+        dyn = je.find("dynamics")
+        if dyn is not None:
+            j.damping = float(dyn.get("damping", 0.0))
+            j.friction = float(dyn.get("friction", 0.0))
+        joints.append(j)
+
+    # merge empty links hanging on fixed joints (and all fixed joints if collapse_fixed_joints)
+    changed = True
+    while changed:
+        changed = False
+        for j in joints:
+            if j.type != T.JOINT_FIXED:
+                continue
+            c = links[j.child]
+            empty = not c.has_inertial and not c.shapes and not c.has_visual
+            if not (empty or options.collapse_fixed_joints):
+                continue
+            par = links[j.parent]
+            R = _qmat(j.q)
+            for s in c.shapes:
+                s.p = j.p + R @ s.p
+                s.q = _qmul(j.q, s.q)
+                par.shapes.append(s)
+            if c.has_inertial and c.mass:
+                mp_p = compute_mass_props(par, options.density)
+                mp_c = compute_mass_props(c, options.density)
+                cc = j.p + R @ mp_c.com
+                Ic = R @ mp_c.inertia @ R.T
+                M = mp_p.mass + mp_c.mass
+                com = (mp_p.com * mp_p.mass + cc * mp_c.mass) / M
+                I = np.zeros((3, 3))
+                for (mm, cm, Im) in ((mp_p.mass, mp_p.com, mp_p.inertia), (mp_c.mass, cc, Ic)):
+                    d = cm - com
+                    I += Im + mm * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
+                par.mass, par.com, par.inertia, par.has_inertial = M, com, I, True
+            for k in joints:
+                if k.parent == c.name:
+                    k.p = j.p + R @ k.p
+                    k.q = _qmul(j.q, k.q)
+                    k.parent = j.parent
+            joints.remove(j)
+            order.remove(c.name)
+            del links[c.name]
+            changed = True
+            break
+
+    children = {n: [] for n in order}
+    is_child = set()
+    for j in joints:
+        children[j.parent].append(j)
+        is_child.add(j.child)
+    roots = [n for n in order if n not in is_child]
+    if len(roots) != 1:
+        raise ValueError("URDF %s: expected one root link, found %s" % (path, roots))
+
+    asset = Asset(root.get("name", os.path.basename(path)), options)
+    index = {}
+
+    def visit(name, via):
+        index[name] = len(asset.bodies)
+        asset.bodies.append(links[name])
+        if via is not None:
+            asset.joints.append(via)
+        for j in children[name]:
+            visit(j.child, j)
+
+    visit(roots[0], None)
+    for j in asset.joints:
+        j.parent = index[j.parent]
+        j.child = index[j.child]
+    asset.warnings = warnings
+    asset.path = path
+    return asset.finalize()

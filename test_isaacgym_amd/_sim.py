@@ -1,0 +1,372 @@
+"""Sim / Env / actor bookkeeping, the packed model handed to libmigym, and the
+persistent tensors of the tensor API.
+
+Index maps (bit-exact contract):
+  actor (DOMAIN_SIM)  = env-major, then actor creation order in the env
+                        (test10_servo_vecenv.py:373 views (num_envs, 2, 13));
+  rigid body          = env-major, actor order, body tree order
+                        (examples/franka_cube_ik_osc.py:255,277);
+  DOF                 = env-major, actor order, DOF tree order
+                        (examples/franka_cube_ik_osc.py:323-326 views (num_envs, 9, 1)).
+Tensor frame: global sim frame; env i's origin is its grid cell.
+"""
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import _types as T
+from ._assets import _qmat, _qmul
+
+
+class Env:
+    __slots__ = ("sim", "index", "lower", "upper", "per_row", "origin", "actors", "num_bodies", "num_dofs",
+                 "cameras")
+
+    def __init__(self, sim, index, lower, upper, per_row):
+        self.sim = sim
+        self.index = index
+        self.lower = lower
+        self.upper = upper
+        self.per_row = max(int(per_row), 1)
+        col = index % self.per_row
+        row = index // self.per_row
+        dx = upper.x - lower.x
+        if sim.params.up_axis == T.UP_AXIS_Z:
+            self.origin = np.array([col * dx, row * (upper.y - lower.y), 0.0])
+        else:
+            self.origin = np.array([col * dx, 0.0, row * (upper.z - lower.z)])
+        self.actors = []
+        self.num_bodies = 0
+        self.num_dofs = 0
+        self.cameras = []
+
+    def __repr__(self):
+        return "Env(%d)" % self.index
+
+
+class Actor:
+    def __init__(self, env, asset, pose, name, group, filter_, seg):
+        self.env = env
+        self.asset = asset
+        self.pose = T.Transform(pose.p, pose.r)
+        self.name = name
+        self.group = group
+        self.filter = filter_
+        self.segmentation_id = seg
+        self.handle = len(env.actors)
+        self.body_offset = env.num_bodies          # env-domain first body
+        self.dof_offset = env.num_dofs             # env-domain first DOF
+        self.global_index = -1
+        self.global_body = -1
+        self.global_dof = -1
+        self.dof_props = asset.dof_props.copy()
+        nd = asset.num_dofs
+        self.dof_state = np.zeros((nd, 2), dtype=np.float32)
+        self.dof_targets = np.zeros((nd, 3), dtype=np.float32)   # pos, vel, effort
+        self.shape_props = [_copy_shape_props(sp) for sp in asset.shape_props]
+        self.mass_props = list(asset.mass_props)
+        self.body_colors = {}
+        self.scale = 1.0
+
+    @property
+    def num_bodies(self):
+        return len(self.asset.bodies)
+
+    @property
+    def num_dofs(self):
+        return self.asset.num_dofs
+
+
+def _copy_shape_props(sp):
+    c = T.RigidShapeProperties()
+    c.__dict__.update(sp.__dict__)
+    return c
+
+
+class Viewer:
+    """Headless viewer: a non-None handle whose window 'closes' after
+    MIGYM_VIEWER_FRAMES draws (default 60), so the reference's
+    `while not gym.query_viewer_has_closed(viewer)` loops terminate."""
+
+    def __init__(self, sim, props):
+        self.sim = sim
+        self.props = props
+        self.frames = 0
+        self.max_frames = int(os.environ.get("MIGYM_VIEWER_FRAMES", "60"))
+        self.cam_transform = T.Transform(T.Vec3(0, -5, 5), T.Quat())
+
+
+class CameraSensor:
+    def __init__(self, env, props, handle):
+        self.env = env
+        self.props = props
+        self.handle = handle
+        self.local = T.Transform()
+        self.body = None          # env-domain body handle when attached
+        self.follow = T.FOLLOW_TRANSFORM
+        self.transform = T.Transform()   # env-frame transform when not attached
+
+
+class Sim:
+    def __init__(self, compute_device, graphics_device, engine, params):
+        self.compute_device = int(compute_device)
+        self.graphics_device = graphics_device
+        self.engine = engine
+        self.params = params
+        self.plane = None
+        self.envs = []
+        self.assets = []
+        self.finalized = False
+        self.native = None
+        self.frame = 0
+        self.time = 0.0
+        self.use_gpu_pipeline = bool(params.use_gpu_pipeline)
+        self.device = torch.device("cuda", self.compute_device) if self.use_gpu_pipeline else torch.device("cpu")
+        self.tensors = {}
+        self.jacobians = {}
+        self.mass_matrices = {}
+
+    # ------------------------------------------------------------ params
+    def mg_params(self):
+        p = self.params
+        px = p.physx
+        mp = N.MgSimParams()
+        mp.dt = float(p.dt)
+        mp.substeps = int(p.substeps)
+        mp.gravity[:] = [p.gravity.x, p.gravity.y, p.gravity.z]
+        mp.up_axis = int(p.up_axis)
+        mp.num_position_iterations = int(px.num_position_iterations)
+        mp.num_velocity_iterations = int(px.num_velocity_iterations)
+        mp.contact_offset = float(px.contact_offset)
+        mp.rest_offset = float(px.rest_offset)
+        mp.bounce_threshold_velocity = float(px.bounce_threshold_velocity)
+        mp.max_depenetration_velocity = float(px.max_depenetration_velocity)
+        if self.plane is not None:
+            n = self.plane.normal.normalize()
+            mp.has_ground = 1
+            mp.ground_normal[:] = [n.x, n.y, n.z]
+            mp.ground_distance = float(self.plane.distance)
+            mp.ground_static_friction = float(self.plane.static_friction)
+            mp.ground_dynamic_friction = float(self.plane.dynamic_friction)
+            mp.ground_restitution = float(self.plane.restitution)
+        return mp
+
+    # ------------------------------------------------------------ layout
+    @property
+    def actors(self):
+        for e in self.envs:
+            for a in e.actors:
+                yield a
+
+    def _assign_indices(self):
+        ai = bi = di = 0
+        for e in self.envs:
+            for a in e.actors:
+                a.global_index = ai
+                a.global_body = bi
+                a.global_dof = di
+                ai += 1
+                bi += a.num_bodies
+                di += a.num_dofs
+        self.num_actors, self.num_bodies, self.num_dofs = ai, bi, di
+
+    def actor_world_body_poses(self, a):
+        """Initial world poses (p[3], q[4]) of an actor's bodies by forward kinematics."""
+        asset = a.asset
+        root_p = a.env.origin + np.array([a.pose.p.x, a.pose.p.y, a.pose.p.z])
+        root_q = np.array([a.pose.r.x, a.pose.r.y, a.pose.r.z, a.pose.r.w])
+        root_q = root_q / np.linalg.norm(root_q)
+        ps = [root_p]
+        qs = [root_q]
+        for k, j in enumerate(asset.joints):
+            b = k + 1
+            d = asset.dof_of_body(b)
+            qj = float(a.dof_state[d, 0]) if d >= 0 else 0.0
+            qrel = j.q.copy()
+            rr = j.p.copy()
+            if j.type == T.JOINT_REVOLUTE:
+                s, c = np.sin(0.5 * qj), np.cos(0.5 * qj)
+                qrel = _qmul(j.q, np.array([j.axis[0] * s, j.axis[1] * s, j.axis[2] * s, c]))
+            elif j.type == T.JOINT_PRISMATIC:
+                rr = j.p + _qmat(j.q) @ (j.axis * qj)
+            pp, pq = ps[j.parent], qs[j.parent]
+            qn = _qmul(pq, qrel)
+            qs.append(qn / np.linalg.norm(qn))
+            ps.append(pp + _qmat(pq) @ rr)
+        return ps, qs
+
+    def build_model(self):
+        """Pack the scene into the arrays of mg_model (include/migym.h)."""
+        self._assign_indices()
+        nb, na, nd = self.num_bodies, self.num_actors, self.num_dofs
+        st = np.zeros((nb, N.MG_STATE_N), dtype=np.float32)
+        mass = np.zeros((nb, N.MG_MASS_N), dtype=np.float32)
+        kind = np.zeros(nb, dtype=np.int32)
+        btmpl = np.zeros(nb, dtype=np.int32)
+        root = np.zeros(na, dtype=np.int32)
+        adof = np.zeros(na + 1, dtype=np.int32)
+        dof0 = np.zeros((nd, 2), dtype=np.float32)
+        dprops = np.zeros((nd, N.MG_DOFPROP_N), dtype=np.float32)
+        tbf, tbi, shapes = [], [], []
+        tb_key = {}
+        artic, atmpl, lf, li = [], [], [], []
+        atmpl_key = {}
+        for a in self.actors:
+            asset = a.asset
+            opts = asset.options
+            root[a.global_index] = a.global_body
+            adof[a.global_index + 1] = a.global_dof + a.num_dofs
+            ps, qs = self.actor_world_body_poses(a)
+            multi = len(asset.bodies) > 1
+            for b, body in enumerate(asset.bodies):
+                g = a.global_body + b
+                st[g, 0:3] = ps[b]
+                st[g, 3:7] = qs[b]
+                mp = a.mass_props[b]
+                invm, invI, iq = mp.principal()
+                mass[g, 0] = invm
+                mass[g, 1:4] = invI
+                mass[g, 4:8] = iq
+                mass[g, 8:11] = mp.com
+                mass[g, 11] = mp.mass
+                if multi:
+                    kind[g] = N.MG_BODY_LINK
+                elif opts.fix_base_link:
+                    kind[g] = N.MG_BODY_STATIC
+                else:
+                    kind[g] = N.MG_BODY_FREE
+                # template body: asset body + its shape materials + body options
+                sidx = sum(len(x.shapes) for x in asset.bodies[:b])
+                mats = tuple((a.shape_props[sidx + k].friction, a.shape_props[sidx + k].restitution)
+                             for k in range(len(body.shapes)))
+                key = (id(asset), b, mats)
+                if key not in tb_key:
+                    tb_key[key] = len(tbf)
+                    tbf.append([opts.linear_damping, opts.angular_damping, opts.max_linear_velocity,
+                                opts.max_angular_velocity, 0.0 if opts.disable_gravity else 1.0, 0, 0, 0])
+                    tbi.append([len(shapes), len(body.shapes), 0, 0])
+                    for k, s in enumerate(body.shapes):
+                        rec = np.zeros(N.MG_SHAPE_STRIDE, dtype=np.float32)
+                        rec[0] = s.type
+                        rec[1:1 + len(s.size)] = s.size
+                        rec[4:7] = s.p
+                        rec[7:11] = s.q
+                        rec[11] = mats[k][0]
+                        rec[12] = mats[k][1]
+                        shapes.append(rec)
+                btmpl[g] = tb_key[key]
+            for d in range(a.num_dofs):
+                gd = a.global_dof + d
+                dof0[gd] = a.dof_state[d]
+                p = a.dof_props[d]
+                dprops[gd, :10] = [p["driveMode"], p["stiffness"], p["damping"], p["effort"], p["velocity"],
+                                   p["lower"], p["upper"], 1.0 if p["hasLimits"] else 0.0, p["armature"],
+                                   p["friction"]]
+            if multi:
+                if id(asset) not in atmpl_key:
+                    atmpl_key[id(asset)] = len(atmpl)
+                    atmpl.append([len(lf), len(asset.bodies), asset.num_dofs, 1 if opts.fix_base_link else 0])
+                    for b in range(len(asset.bodies)):
+                        f = np.zeros(N.MG_LINK_F_N, dtype=np.float32)
+                        ii = [-1, 0, -1, 0]
+                        if b > 0:
+                            j = asset.joints[b - 1]
+                            f[0:3] = j.p
+                            f[3:7] = j.q
+                            f[7:10] = j.axis
+                            ii = [j.parent, j.type if j.type in (T.JOINT_FIXED, T.JOINT_REVOLUTE,
+                                                                 T.JOINT_PRISMATIC) else T.JOINT_FIXED,
+                                  asset.dof_of_body(b), 0]
+                        lf.append(f)
+                        li.append(ii)
+                artic.append([a.global_body, a.global_dof, atmpl_key[id(asset)], 0])
+        self.model_arrays = dict(
+            body_state0=st, body_mass=mass, body_kind=kind, body_tmpl=btmpl,
+            tmpl_body_f=np.array(tbf, dtype=np.float32).reshape(-1, N.MG_TBODY_F_N),
+            tmpl_body_i=np.array(tbi, dtype=np.int32).reshape(-1, N.MG_TBODY_I_N),
+            shapes=np.array(shapes, dtype=np.float32).reshape(-1, N.MG_SHAPE_STRIDE),
+            actor_root_body=root, actor_dof=adof, dof_state0=dof0, dof_props=dprops,
+            artic_i=np.array(artic, dtype=np.int32).reshape(-1, N.MG_ARTIC_I_N),
+            artic_tmpl_i=np.array(atmpl, dtype=np.int32).reshape(-1, N.MG_ATMPL_I_N),
+            tmpl_link_f=np.array(lf, dtype=np.float32).reshape(-1, N.MG_LINK_F_N),
+            tmpl_link_i=np.array(li, dtype=np.int32).reshape(-1, N.MG_LINK_I_N),
+        )
+        return self.model_arrays
+
+    def mg_model(self, arrays=None):
+        """ctypes mg_model over the packed arrays (kept alive by self._model_keep)."""
+        A = arrays if arrays is not None else self.model_arrays
+        m = N.MgModel()
+        m.num_envs = len(self.envs)
+        m.num_actors = len(A["actor_root_body"])
+        m.num_bodies = len(A["body_kind"])
+        m.num_dofs = len(A["dof_state0"])
+        m.num_tmpl_bodies = len(A["tmpl_body_f"])
+        m.num_shapes = len(A["shapes"])
+        m.num_artics = len(A["artic_i"])
+        m.num_artic_tmpls = len(A["artic_tmpl_i"])
+        m.num_tmpl_links = len(A["tmpl_link_f"])
+        keep = {}
+        for name in ("body_state0", "body_mass", "tmpl_body_f", "shapes", "dof_state0", "dof_props", "tmpl_link_f"):
+            arr = np.ascontiguousarray(A[name], dtype=np.float32)
+            keep[name] = arr
+            setattr(m, name, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        for name in ("body_kind", "body_tmpl", "tmpl_body_i", "actor_root_body", "actor_dof", "artic_i",
+                     "artic_tmpl_i", "tmpl_link_i"):
+            arr = np.ascontiguousarray(A[name], dtype=np.int32)
+            keep[name] = arr
+            setattr(m, name, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        self._model_keep = keep
+        return m
+
+    # ------------------------------------------------------------ finalize
+    def finalize(self):
+        if self.finalized:
+            return
+        A = self.build_model()
+        dev = self.device
+        self.tensors["root"] = torch.from_numpy(A["body_state0"][A["actor_root_body"]].copy()).to(dev)
+        self.tensors["rb"] = torch.from_numpy(A["body_state0"].copy()).to(dev)
+        self.tensors["dof"] = torch.from_numpy(A["dof_state0"].copy()).to(dev)
+        self.tensors["ncf"] = torch.zeros((self.num_bodies, 3), dtype=torch.float32, device=dev)
+        if N.device_count() > 0:
+            handle = N.lib.mg_create_sim(self.compute_device, ctypes.byref(self.mg_params()))
+            if not handle:
+                raise N.MigymError("mg_create_sim: " + N.last_error())
+            self.native = handle
+            N.check(N.lib.mg_upload_model(handle, ctypes.byref(self.mg_model())), "mg_upload_model")
+            # actor DOF targets / props set before prepare
+            self._push_dof_targets_all()
+        self.finalized = True
+
+    def _push_dof_targets_all(self):
+        if self.num_dofs == 0:
+            return
+        tgt = np.zeros((self.num_dofs, 3), dtype=np.float32)
+        for a in self.actors:
+            tgt[a.global_dof:a.global_dof + a.num_dofs] = a.dof_targets
+        for col, fn in ((0, N.lib.mg_set_dof_position_target), (1, N.lib.mg_set_dof_velocity_target),
+                        (2, N.lib.mg_set_dof_actuation_force)):
+            c = np.ascontiguousarray(tgt[:, col])
+            N.check(fn(self.native, c.ctypes.data, 1, None, 0, self.stream()), "set dof targets")
+
+    def require_native(self, what):
+        self.finalize()
+        if self.native is None:
+            raise N.MigymError(
+                "%s needs a HIP device: libmigym found %d GPUs (no CPU engine exists; run on an MI355X)"
+                % (what, N.device_count()))
+        return self.native
+
+    def stream(self):
+        if torch.cuda.is_available():
+            return torch.cuda.current_stream(self.compute_device).cuda_stream
+        return None
+
+    def destroy(self):
+        if self.native:
+            N.lib.mg_destroy_sim(self.native)
+            self.native = None

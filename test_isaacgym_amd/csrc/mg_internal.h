@@ -1,0 +1,82 @@
+// mg_internal.h — internal structures shared by the host side (migym_capi.cpp)
+// and the HIP kernels (mg_rigid.hip, mg_artic.hip, mg_tensor.hip).
+//
+// Numerics contract: every kernel is compiled with -ffp-contract=off and uses no
+// library transcendental in the step, so that the CPU restatement in
+// oracle/migym_oracle.c (compiled the same way) reproduces it bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/migym.h"
+
+#define MG_MAX_CONTACTS 8     // contact slots per free body per substep
+#define MG_MAX_LINKS    16    // articulation links handled per lane
+#define MG_MAX_DOFS     16
+
+// Per-simulate constants derived on the host from mg_sim_params
+// (one copy, passed by value as a kernel argument).
+struct MgStep {
+    float h;          // substep length dt / substeps
+    float sub;        // TGS position sub-iteration length h / npos
+    float inv_sub;    // 1 / sub
+    float inv_h;      // 1 / h
+    float inv_dt;     // 1 / dt (contact impulse -> force)
+    float g[3];       // gravity
+    int   substeps, npos, nvel;
+    float contact_offset, rest_offset, max_depen, bounce_thresh;
+    int   has_ground;
+    float n[3];       // ground normal
+    float pd;         // ground plane offset: dot(n, x) + pd = 0
+    float t1[3], t2[3];   // ground tangent basis
+    float mu_ground, e_ground;
+};
+
+// Kernel argument block of the free-body step (SoA arrays, stride = nb).
+struct MgRigidArgs {
+    int          nf;          // number of free bodies
+    int          nb;          // SoA stride (total bodies)
+    const int*   free_ids;    // [nf] global body ids
+    float*       state;       // [13][nb]
+    const float* mass;        // [12][nb]
+    const int*   body_tmpl;   // [nb]
+    const float* tbf;         // [ntb][8]
+    const int*   tbi;         // [ntb][4]
+    const float* shapes;      // [ns][16]
+    const float* ext;         // [6][nb] world force/torque at COM, or null
+    float*       cforce;      // [3][nb] net contact force out
+};
+
+// Articulation step arguments (lane = articulation instance).
+struct MgArticArgs {
+    int          na;          // articulation instances in this launch
+    int          nb, nd;      // SoA strides
+    const int*   artic_i;     // [na][4] first_body, first_dof, tmpl, pad
+    int          tmpl;        // template id handled by this launch
+    int          nl, ndof;    // links / dofs of the template
+    int          fixed_base;
+    const float* link_f;      // [nl][16] template link constants
+    const int*   link_i;      // [nl][4]
+    float*       state;       // [13][nb]  link states (root = primary, others FK output)
+    const float* mass;        // [12][nb]
+    const int*   body_tmpl;
+    const float* tbf;
+    float*       dof_pos;     // [nd]
+    float*       dof_vel;     // [nd]
+    const float* dof_tpos;    // [nd]
+    const float* dof_tvel;    // [nd]
+    const float* dof_force;   // [nd]
+    const float* dof_props;   // [12][nd]
+    const float* ext;         // [6][nb] or null
+    float*       cforce;      // [3][nb]
+};
+
+// launchers (defined in the .hip files)
+hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream_t s);
+hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream_t s);
+hipError_t mg_launch_gather_rows(const float* soa, int stride, int ncol, const int* ids, int n,
+                                 float* aos, hipStream_t s);
+hipError_t mg_launch_scatter_rows(const float* aos, int ncol, const int* ids, const int* sel,
+                                  int n, float* soa, int stride, hipStream_t s);
+hipError_t mg_launch_scatter_dofs(const float* aos, int ncol, const int* actor_dof, const int* sel,
+                                  int nsel, int max_dofs, float* const* dst, hipStream_t s);
+hipError_t mg_launch_jacobian(const MgArticArgs& A, float* jac, float* mm, hipStream_t s);

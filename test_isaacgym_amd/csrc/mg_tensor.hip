@@ -1,0 +1,84 @@
+// mg_tensor.hip — the tensor-API copy kernels: SoA engine state <-> the AoS
+// tensors Isaac Gym hands out (refresh_* / set_*).
+//
+// One thread per output element, so the AoS side (the user's tensor) is read or
+// written fully coalesced; the SoA side is a per-field stride walk that the L2
+// absorbs (13 fields x 4 B per row).
+#include "mg_internal.h"
+
+namespace {
+
+// aos[i][f] = soa[f][ids ? ids[i] : i]
+__global__ void k_gather_rows(const float* __restrict__ soa, int stride, int ncol,
+                              const int* __restrict__ ids, int n, float* __restrict__ aos) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long total = (long)n * ncol;
+    if (t >= total) return;
+    const int i = (int)(t / ncol);
+    const int f = (int)(t - (long)i * ncol);
+    const int r = ids ? ids[i] : i;
+    aos[t] = soa[(long)f * stride + r];
+}
+
+// for k < n: i = sel ? sel[k] : k;  soa[f][ids ? ids[i] : i] = aos[i][f]
+__global__ void k_scatter_rows(const float* __restrict__ aos, int ncol, const int* __restrict__ ids,
+                               const int* __restrict__ sel, int n, float* __restrict__ soa, int stride) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long total = (long)n * ncol;
+    if (t >= total) return;
+    const int k = (int)(t / ncol);
+    const int f = (int)(t - (long)k * ncol);
+    const int i = sel ? sel[k] : k;
+    const int r = ids ? ids[i] : i;
+    soa[(long)f * stride + r] = aos[(long)i * ncol + f];
+}
+
+// DOF rows selected by actor: for k < nsel, a = sel[k], j < count(a):
+//   d = actor_dof[a] + j;  dst[c][d] = src[d][c]   (c < ncol)
+// sel == null: every DOF row (nsel = num_dofs, max_dofs = 1, actor_dof unused).
+__global__ void k_scatter_dofs(const float* __restrict__ src, int ncol, const int* __restrict__ actor_dof,
+                               const int* __restrict__ sel, int nsel, int max_dofs, float* dst0, float* dst1) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)nsel * max_dofs) return;
+    int d;
+    if (sel) {
+        const int k = (int)(t / max_dofs);
+        const int j = (int)(t - (long)k * max_dofs);
+        const int a = sel[k];
+        const int d0 = actor_dof[a], d1 = actor_dof[a + 1];
+        if (d0 + j >= d1) return;
+        d = d0 + j;
+    } else {
+        d = (int)t;
+    }
+    dst0[d] = src[(long)d * ncol + 0];
+    if (ncol > 1) dst1[d] = src[(long)d * ncol + 1];
+}
+
+inline int nblocks(long total, int bs) { return (int)((total + bs - 1) / bs); }
+
+}  // namespace
+
+hipError_t mg_launch_gather_rows(const float* soa, int stride, int ncol, const int* ids, int n,
+                                 float* aos, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_rows, dim3(nblocks((long)n * ncol, 256)), dim3(256), 0, s,
+                       soa, stride, ncol, ids, n, aos);
+    return hipGetLastError();
+}
+
+hipError_t mg_launch_scatter_rows(const float* aos, int ncol, const int* ids, const int* sel, int n,
+                                  float* soa, int stride, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scatter_rows, dim3(nblocks((long)n * ncol, 256)), dim3(256), 0, s,
+                       aos, ncol, ids, sel, n, soa, stride);
+    return hipGetLastError();
+}
+
+hipError_t mg_launch_scatter_dofs(const float* src, int ncol, const int* actor_dof, const int* sel,
+                                  int nsel, int max_dofs, float* const* dst, hipStream_t s) {
+    if (nsel <= 0 || max_dofs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scatter_dofs, dim3(nblocks((long)nsel * max_dofs, 256)), dim3(256), 0, s,
+                       src, ncol, actor_dof, sel, nsel, max_dofs, dst[0], dst[1]);
+    return hipGetLastError();
+}

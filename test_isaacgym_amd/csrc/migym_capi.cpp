@@ -1,0 +1,577 @@
+// migym_capi.cpp — host side of libmigym.so: the C ABI declared in
+// include/migym.h. Owns the engine state in HBM (SoA, env index as the
+// coalesced axis), launches the step kernels and the tensor-API copy kernels on
+// the caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdarg>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mg_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(MG_ERR_DEVICE, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    return hipMalloc((void**)p, n * sizeof(T));
+}
+
+// host AoS [n][ncol] -> device SoA [ncol][n]
+template <class T>
+std::vector<T> to_soa(const T* aos, int n, int ncol) {
+    std::vector<T> soa((size_t)n * ncol);
+    for (int i = 0; i < n; ++i)
+        for (int f = 0; f < ncol; ++f) soa[(size_t)f * n + i] = aos[(size_t)i * ncol + f];
+    return soa;
+}
+
+struct ArticGroup {
+    int tmpl, first_link, nl, ndof, fixed_base;
+    int offset, count;   // into the template-sorted instance list
+};
+
+}  // namespace
+
+struct mg_sim {
+    int device = 0;
+    mg_sim_params params{};
+    bool uploaded = false;
+
+    int nenv = 0, na = 0, nb = 0, nd = 0, ntb = 0, ns = 0, nf = 0, nartic = 0, ntl = 0;
+    int max_actor_dofs = 0;
+
+    float* d_state = nullptr;     // [13][nb]
+    float* d_mass = nullptr;      // [12][nb]
+    int* d_body_tmpl = nullptr;   // [nb]
+    int* d_free = nullptr;        // [nf]
+    float* d_tbf = nullptr;
+    int* d_tbi = nullptr;
+    float* d_shapes = nullptr;
+    int* d_actor_root = nullptr;  // [na]
+    int* d_actor_dof = nullptr;   // [na+1]
+    float* d_cforce = nullptr;    // [3][nb]
+    float* d_ext = nullptr;       // [6][nb]
+    bool ext_pending = false;
+
+    float* d_dof = nullptr;       // [2][nd]: pos, vel
+    float* d_dof_tgt = nullptr;   // [3][nd]: target pos, target vel, actuation force
+    float* d_dof_props = nullptr; // [12][nd]
+    int* d_artic = nullptr;       // [nartic][4] sorted by template
+    float* d_link_f = nullptr;
+    int* d_link_i = nullptr;
+    std::vector<ArticGroup> groups;
+
+    float* d_stage = nullptr;     // host-transfer staging (floats)
+    size_t stage_n = 0;
+    int* d_stage_idx = nullptr;
+    size_t stage_idx_n = 0;
+
+    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    bool stepped = false;
+    // ring of per-simulate event pairs for live kernel timing (bench.py roofline)
+    static constexpr int kRing = 512;
+    hipEvent_t ring_b[kRing] = {}, ring_e[kRing] = {};
+    long long ring_n = 0;
+};
+
+namespace {
+
+MgStep make_step(const mg_sim_params& p) {
+    MgStep P{};
+    const int ss = p.substeps > 0 ? p.substeps : 1;
+    const int np = p.num_position_iterations > 0 ? p.num_position_iterations : 1;
+    P.substeps = ss;
+    P.npos = np;
+    P.nvel = p.num_velocity_iterations > 0 ? p.num_velocity_iterations : 0;
+    P.h = p.dt / (float)ss;
+    P.sub = P.h / (float)np;
+    P.inv_sub = 1.0f / P.sub;
+    P.inv_h = 1.0f / P.h;
+    P.inv_dt = 1.0f / p.dt;
+    for (int k = 0; k < 3; ++k) P.g[k] = p.gravity[k];
+    P.contact_offset = p.contact_offset;
+    P.rest_offset = p.rest_offset;
+    P.max_depen = p.max_depenetration_velocity;
+    P.bounce_thresh = p.bounce_threshold_velocity;
+    P.has_ground = p.has_ground;
+    const float nx = p.ground_normal[0], ny = p.ground_normal[1], nz = p.ground_normal[2];
+    P.n[0] = nx; P.n[1] = ny; P.n[2] = nz;
+    P.pd = p.ground_distance;
+    // tangent basis: t1 = normalize(n x a), t2 = n x t1
+    float ax = 1.0f, ay = 0.0f, az = 0.0f;
+    if (!(std::fabs(nx) < 0.9f)) { ax = 0.0f; ay = 1.0f; }
+    float t1x = ny * az - nz * ay, t1y = nz * ax - nx * az, t1z = nx * ay - ny * ax;
+    const float inv = 1.0f / std::sqrt(t1x * t1x + t1y * t1y + t1z * t1z);
+    t1x = t1x * inv; t1y = t1y * inv; t1z = t1z * inv;
+    P.t1[0] = t1x; P.t1[1] = t1y; P.t1[2] = t1z;
+    P.t2[0] = ny * t1z - nz * t1y;
+    P.t2[1] = nz * t1x - nx * t1z;
+    P.t2[2] = nx * t1y - ny * t1x;
+    P.mu_ground = p.ground_dynamic_friction;
+    P.e_ground = p.ground_restitution;
+    return P;
+}
+
+int ensure_stage(mg_sim* s, size_t nfloat, size_t nidx) {
+    if (nfloat > s->stage_n) {
+        if (s->d_stage) (void)hipFree(s->d_stage);
+        s->d_stage = nullptr;
+        HIP_TRY(dalloc(&s->d_stage, nfloat));
+        s->stage_n = nfloat;
+    }
+    if (nidx > s->stage_idx_n) {
+        if (s->d_stage_idx) (void)hipFree(s->d_stage_idx);
+        s->d_stage_idx = nullptr;
+        HIP_TRY(dalloc(&s->d_stage_idx, nidx));
+        s->stage_idx_n = nidx;
+    }
+    return MG_OK;
+}
+
+// gather `n` rows of `ncol` SoA fields into dst (host or device)
+int refresh_rows(mg_sim* s, const float* soa, int stride, int ncol, const int* ids, int n, float* dst,
+                 int dst_host, hipStream_t st) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (!dst && n > 0) return fail(MG_ERR_ARG, "null destination");
+    HIP_TRY(hipSetDevice(s->device));
+    if (n == 0) return MG_OK;
+    if (!dst_host) {
+        HIP_TRY(mg_launch_gather_rows(soa, stride, ncol, ids, n, dst, st));
+        return MG_OK;
+    }
+    int rc = ensure_stage(s, (size_t)n * ncol, 0);
+    if (rc) return rc;
+    HIP_TRY(mg_launch_gather_rows(soa, stride, ncol, ids, n, s->d_stage, st));
+    HIP_TRY(hipMemcpyAsync(dst, s->d_stage, (size_t)n * ncol * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return MG_OK;
+}
+
+// stage a host source (and optional index list) to the device
+int stage_src(mg_sim* s, const float* src, int src_host, size_t nfloat, const int* idx, int n_idx,
+              hipStream_t st, const float** dsrc, const int** didx) {
+    *dsrc = src;
+    *didx = idx;
+    if (!src_host) return MG_OK;
+    int rc = ensure_stage(s, nfloat, idx ? (size_t)n_idx : 0);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(s->d_stage, src, nfloat * sizeof(float), hipMemcpyHostToDevice, st));
+    *dsrc = s->d_stage;
+    if (idx && n_idx > 0) {
+        HIP_TRY(hipMemcpyAsync(s->d_stage_idx, idx, (size_t)n_idx * sizeof(int), hipMemcpyHostToDevice, st));
+        *didx = s->d_stage_idx;
+    }
+    return MG_OK;
+}
+
+int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* dst0, float* dst1,
+                    const int* idx, int n_idx, hipStream_t st) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (s->nd == 0) return MG_OK;
+    if (!src) return fail(MG_ERR_ARG, "null source tensor");
+    HIP_TRY(hipSetDevice(s->device));
+    const float* dsrc;
+    const int* didx;
+    int rc = stage_src(s, src, src_host, (size_t)s->nd * ncol, idx, n_idx, st, &dsrc, &didx);
+    if (rc) return rc;
+    float* dst[2] = {dst0, dst1};
+    if (idx)
+        HIP_TRY(mg_launch_scatter_dofs(dsrc, ncol, s->d_actor_dof, didx, n_idx, s->max_actor_dofs, dst, st));
+    else
+        HIP_TRY(mg_launch_scatter_dofs(dsrc, ncol, nullptr, nullptr, s->nd, 1, dst, st));
+    return MG_OK;
+}
+
+void free_all(mg_sim* s) {
+    void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free, s->d_tbf, s->d_tbi, s->d_shapes,
+                    s->d_actor_root, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
+                    s->d_dof_props, s->d_artic, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t mg_abi_version(void) { return MG_ABI_VERSION; }
+const char* mg_last_error(void) { return g_err.c_str(); }
+
+int32_t mg_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+mg_sim* mg_create_sim(int32_t device, const mg_sim_params* params) {
+    if (!params) { fail(MG_ERR_ARG, "null params"); return nullptr; }
+    int n = mg_device_count();
+    if (n <= 0) { fail(MG_ERR_DEVICE, "no HIP device available (libmigym needs an MI355X)"); return nullptr; }
+    if (device < 0 || device >= n) { fail(MG_ERR_DEVICE, "device %d out of range (%d visible)", device, n); return nullptr; }
+    if (hipSetDevice(device) != hipSuccess) { fail(MG_ERR_DEVICE, "hipSetDevice(%d) failed", device); return nullptr; }
+    mg_sim* s = new mg_sim();
+    s->device = device;
+    s->params = *params;
+    for (int k = 0; k < mg_sim::kRing; ++k) {
+        if (hipEventCreate(&s->ring_b[k]) != hipSuccess || hipEventCreate(&s->ring_e[k]) != hipSuccess) {
+            fail(MG_ERR_DEVICE, "hipEventCreate failed");
+            mg_destroy_sim(s);
+            return nullptr;
+        }
+    }
+    return s;
+}
+
+void mg_destroy_sim(mg_sim* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    (void)hipDeviceSynchronize();
+    free_all(s);
+    for (int k = 0; k < mg_sim::kRing; ++k) {
+        if (s->ring_b[k]) (void)hipEventDestroy(s->ring_b[k]);
+        if (s->ring_e[k]) (void)hipEventDestroy(s->ring_e[k]);
+    }
+    delete s;
+}
+
+int32_t mg_set_sim_params(mg_sim* s, const mg_sim_params* p) {
+    if (!s || !p) return fail(MG_ERR_ARG, "null argument");
+    s->params = *p;
+    return MG_OK;
+}
+
+int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
+    if (!s || !m) return fail(MG_ERR_ARG, "null argument");
+    if (s->uploaded) return fail(MG_ERR_STATE, "model already uploaded");
+    if (m->num_bodies < 0 || m->num_actors < 0 || m->num_dofs < 0) return fail(MG_ERR_ARG, "negative sizes");
+    HIP_TRY(hipSetDevice(s->device));
+    const int nb = m->num_bodies, na = m->num_actors, nd = m->num_dofs;
+    s->nenv = m->num_envs; s->na = na; s->nb = nb; s->nd = nd;
+    s->ntb = m->num_tmpl_bodies; s->ns = m->num_shapes;
+    s->nartic = m->num_artics; s->ntl = m->num_tmpl_links;
+
+    // validate indices on the host before anything reaches a kernel
+    for (int b = 0; b < nb; ++b) {
+        const int t = m->body_tmpl[b];
+        if (t < 0 || t >= s->ntb) return fail(MG_ERR_ARG, "body %d: template %d out of range", b, t);
+        const int s0 = m->tmpl_body_i[t * MG_TBODY_I_N + 0], sc = m->tmpl_body_i[t * MG_TBODY_I_N + 1];
+        if (s0 < 0 || sc < 0 || s0 + sc > s->ns) return fail(MG_ERR_ARG, "template body %d: bad shape range", t);
+    }
+    for (int a = 0; a < na; ++a) {
+        if (m->actor_root_body[a] < 0 || m->actor_root_body[a] >= nb) return fail(MG_ERR_ARG, "actor %d: bad root", a);
+        if (m->actor_dof[a] > m->actor_dof[a + 1]) return fail(MG_ERR_ARG, "actor_dof not monotone");
+        s->max_actor_dofs = std::max(s->max_actor_dofs, m->actor_dof[a + 1] - m->actor_dof[a]);
+    }
+    if (na > 0 && (m->actor_dof[0] != 0 || m->actor_dof[na] != nd)) return fail(MG_ERR_ARG, "actor_dof must span [0, num_dofs]");
+
+    std::vector<int> free_ids;
+    for (int b = 0; b < nb; ++b)
+        if (m->body_kind[b] == MG_BODY_FREE) free_ids.push_back(b);
+    s->nf = (int)free_ids.size();
+
+    // articulation instances grouped by template
+    s->groups.clear();
+    std::vector<int> artic_sorted;
+    for (int t = 0; t < m->num_artic_tmpls; ++t) {
+        ArticGroup g;
+        g.tmpl = t;
+        g.first_link = m->artic_tmpl_i[t * MG_ATMPL_I_N + 0];
+        g.nl = m->artic_tmpl_i[t * MG_ATMPL_I_N + 1];
+        g.ndof = m->artic_tmpl_i[t * MG_ATMPL_I_N + 2];
+        g.fixed_base = m->artic_tmpl_i[t * MG_ATMPL_I_N + 3];
+        if (g.nl < 1 || g.nl > MG_MAX_LINKS || g.ndof > g.nl || g.first_link < 0 || g.first_link + g.nl > s->ntl)
+            return fail(MG_ERR_UNSUPPORTED, "articulation template %d: %d links / %d dofs unsupported", t, g.nl, g.ndof);
+        if (!g.fixed_base)
+            return fail(MG_ERR_UNSUPPORTED, "articulation template %d: floating-base articulations are not supported yet", t);
+        for (int l = 0; l < g.nl; ++l) {
+            const int* li = m->tmpl_link_i + (size_t)(g.first_link + l) * MG_LINK_I_N;
+            if (li[0] >= l || (l > 0 && li[0] < 0) || (l == 0 && li[0] != -1))
+                return fail(MG_ERR_ARG, "articulation template %d: links not in topological order", t);
+            if (li[2] >= g.ndof) return fail(MG_ERR_ARG, "articulation template %d: bad dof index", t);
+        }
+        g.offset = (int)artic_sorted.size() / MG_ARTIC_I_N;
+        g.count = 0;
+        for (int k = 0; k < m->num_artics; ++k) {
+            const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;
+            if (ai[2] != t) continue;
+            if (ai[0] < 0 || ai[0] + g.nl > nb || ai[1] < 0 || ai[1] + g.ndof > nd)
+                return fail(MG_ERR_ARG, "articulation %d out of range", k);
+            for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_sorted.push_back(ai[j]);
+            g.count++;
+        }
+        s->groups.push_back(g);
+    }
+
+    // device buffers
+    HIP_TRY(dalloc(&s->d_state, (size_t)nb * MG_STATE_N));
+    HIP_TRY(dalloc(&s->d_mass, (size_t)nb * MG_MASS_N));
+    HIP_TRY(dalloc(&s->d_body_tmpl, nb));
+    HIP_TRY(dalloc(&s->d_free, s->nf));
+    HIP_TRY(dalloc(&s->d_tbf, (size_t)s->ntb * MG_TBODY_F_N));
+    HIP_TRY(dalloc(&s->d_tbi, (size_t)s->ntb * MG_TBODY_I_N));
+    HIP_TRY(dalloc(&s->d_shapes, (size_t)s->ns * MG_SHAPE_STRIDE));
+    HIP_TRY(dalloc(&s->d_actor_root, na));
+    HIP_TRY(dalloc(&s->d_actor_dof, na + 1));
+    HIP_TRY(dalloc(&s->d_cforce, (size_t)nb * 3));
+    HIP_TRY(dalloc(&s->d_ext, (size_t)nb * 6));
+    HIP_TRY(dalloc(&s->d_dof, (size_t)nd * 2));
+    HIP_TRY(dalloc(&s->d_dof_tgt, (size_t)nd * 3));
+    HIP_TRY(dalloc(&s->d_dof_props, (size_t)nd * MG_DOFPROP_N));
+    HIP_TRY(dalloc(&s->d_artic, artic_sorted.size()));
+    HIP_TRY(dalloc(&s->d_link_f, (size_t)s->ntl * MG_LINK_F_N));
+    HIP_TRY(dalloc(&s->d_link_i, (size_t)s->ntl * MG_LINK_I_N));
+
+    auto h2d = [](void* d, const void* h, size_t bytes) -> hipError_t {
+        if (bytes == 0 || !h) return hipSuccess;
+        return hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
+    };
+    std::vector<float> st = to_soa(m->body_state0, nb, MG_STATE_N);
+    std::vector<float> ms = to_soa(m->body_mass, nb, MG_MASS_N);
+    HIP_TRY(h2d(s->d_state, st.data(), st.size() * sizeof(float)));
+    HIP_TRY(h2d(s->d_mass, ms.data(), ms.size() * sizeof(float)));
+    HIP_TRY(h2d(s->d_body_tmpl, m->body_tmpl, (size_t)nb * sizeof(int)));
+    HIP_TRY(h2d(s->d_free, free_ids.data(), free_ids.size() * sizeof(int)));
+    HIP_TRY(h2d(s->d_tbf, m->tmpl_body_f, (size_t)s->ntb * MG_TBODY_F_N * sizeof(float)));
+    HIP_TRY(h2d(s->d_tbi, m->tmpl_body_i, (size_t)s->ntb * MG_TBODY_I_N * sizeof(int)));
+    HIP_TRY(h2d(s->d_shapes, m->shapes, (size_t)s->ns * MG_SHAPE_STRIDE * sizeof(float)));
+    HIP_TRY(h2d(s->d_actor_root, m->actor_root_body, (size_t)na * sizeof(int)));
+    HIP_TRY(h2d(s->d_actor_dof, m->actor_dof, (size_t)(na + 1) * sizeof(int)));
+    HIP_TRY(hipMemset(s->d_cforce, 0, (size_t)nb * 3 * sizeof(float)));
+    HIP_TRY(hipMemset(s->d_ext, 0, (size_t)nb * 6 * sizeof(float)));
+    if (nd > 0) {
+        std::vector<float> ds = to_soa(m->dof_state0, nd, 2);
+        HIP_TRY(h2d(s->d_dof, ds.data(), ds.size() * sizeof(float)));
+        HIP_TRY(hipMemset(s->d_dof_tgt, 0, (size_t)nd * 3 * sizeof(float)));
+        std::vector<float> dp = to_soa(m->dof_props, nd, MG_DOFPROP_N);
+        HIP_TRY(h2d(s->d_dof_props, dp.data(), dp.size() * sizeof(float)));
+    }
+    HIP_TRY(h2d(s->d_artic, artic_sorted.data(), artic_sorted.size() * sizeof(int)));
+    HIP_TRY(h2d(s->d_link_f, m->tmpl_link_f, (size_t)s->ntl * MG_LINK_F_N * sizeof(float)));
+    HIP_TRY(h2d(s->d_link_i, m->tmpl_link_i, (size_t)s->ntl * MG_LINK_I_N * sizeof(int)));
+    HIP_TRY(hipDeviceSynchronize());
+    s->uploaded = true;
+    return MG_OK;
+}
+
+int32_t mg_simulate(mg_sim* s, void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "simulate before the model was uploaded");
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)stream;
+    const MgStep P = make_step(s->params);
+    const int slot = (int)(s->ring_n % mg_sim::kRing);
+    s->ev_begin = s->ring_b[slot];
+    s->ev_end = s->ring_e[slot];
+    HIP_TRY(hipEventRecord(s->ev_begin, st));
+    for (const ArticGroup& g : s->groups) {
+        if (g.count == 0) continue;
+        MgArticArgs A{};
+        A.na = g.count; A.nb = s->nb; A.nd = s->nd;
+        A.artic_i = s->d_artic + (size_t)g.offset * MG_ARTIC_I_N;
+        A.tmpl = g.tmpl; A.nl = g.nl; A.ndof = g.ndof; A.fixed_base = g.fixed_base;
+        A.link_f = s->d_link_f + (size_t)g.first_link * MG_LINK_F_N;
+        A.link_i = s->d_link_i + (size_t)g.first_link * MG_LINK_I_N;
+        A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl; A.tbf = s->d_tbf;
+        A.dof_pos = s->d_dof; A.dof_vel = s->d_dof + s->nd;
+        A.dof_tpos = s->d_dof_tgt; A.dof_tvel = s->d_dof_tgt + s->nd; A.dof_force = s->d_dof_tgt + 2 * (size_t)s->nd;
+        A.dof_props = s->d_dof_props;
+        A.ext = s->ext_pending ? s->d_ext : nullptr;
+        A.cforce = s->d_cforce;
+        hipError_t e = mg_launch_artic_step(P, A, st);
+        if (e != hipSuccess) return fail(MG_ERR_DEVICE, "articulation step launch: %s", hipGetErrorString(e));
+    }
+    if (s->nf > 0) {
+        MgRigidArgs A{};
+        A.nf = s->nf; A.nb = s->nb; A.free_ids = s->d_free;
+        A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
+        A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes;
+        A.ext = s->ext_pending ? s->d_ext : nullptr;
+        A.cforce = s->d_cforce;
+        HIP_TRY(mg_launch_rigid_step(P, A, st));
+    }
+    if (s->ext_pending) {
+        HIP_TRY(hipMemsetAsync(s->d_ext, 0, (size_t)s->nb * 6 * sizeof(float), st));
+        s->ext_pending = false;
+    }
+    HIP_TRY(hipEventRecord(s->ev_end, st));
+    s->ring_n++;
+    s->stepped = true;
+    return MG_OK;
+}
+
+int32_t mg_fetch_results(mg_sim* s, int32_t wait) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    if (wait && s->stepped) HIP_TRY(hipEventSynchronize(s->ev_end));
+    return MG_OK;
+}
+
+float mg_last_step_ms(mg_sim* s) {
+    if (!s || !s->stepped) return -1.0f;
+    if (hipEventSynchronize(s->ev_end) != hipSuccess) return -1.0f;
+    float ms = -1.0f;
+    if (hipEventElapsedTime(&ms, s->ev_begin, s->ev_end) != hipSuccess) return -1.0f;
+    return ms;
+}
+
+int32_t mg_step_time_stats(mg_sim* s, int32_t n, float* avg_ms, float* min_ms, float* max_ms) {
+    if (!s || n <= 0) return fail(MG_ERR_ARG, "bad arguments");
+    if (s->ring_n == 0) return fail(MG_ERR_STATE, "no simulate() recorded");
+    long long avail = s->ring_n < mg_sim::kRing ? s->ring_n : mg_sim::kRing;
+    if (n > avail) n = (int32_t)avail;
+    double sum = 0.0;
+    float lo = 1e30f, hi = 0.0f;
+    for (int32_t k = 0; k < n; ++k) {
+        const int slot = (int)((s->ring_n - 1 - k) % mg_sim::kRing);
+        HIP_TRY(hipEventSynchronize(s->ring_e[slot]));
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, s->ring_b[slot], s->ring_e[slot]));
+        sum += ms;
+        lo = ms < lo ? ms : lo;
+        hi = ms > hi ? ms : hi;
+    }
+    if (avg_ms) *avg_ms = (float)(sum / n);
+    if (min_ms) *min_ms = lo;
+    if (max_ms) *max_ms = hi;
+    return n;
+}
+
+int32_t mg_num_free_bodies(mg_sim* s) { return s ? s->nf : 0; }
+int32_t mg_num_articulations(mg_sim* s) { return s ? s->nartic : 0; }
+
+int32_t mg_refresh_actor_root_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    return refresh_rows(s, s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, dst, dst_host, (hipStream_t)stream);
+}
+int32_t mg_refresh_rigid_body_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    return refresh_rows(s, s->d_state, s->nb, MG_STATE_N, nullptr, s->nb, dst, dst_host, (hipStream_t)stream);
+}
+int32_t mg_refresh_dof_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    return refresh_rows(s, s->d_dof, s->nd, 2, nullptr, s->nd, dst, dst_host, (hipStream_t)stream);
+}
+int32_t mg_refresh_net_contact_force(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    return refresh_rows(s, s->d_cforce, s->nb, 3, nullptr, s->nb, dst, dst_host, (hipStream_t)stream);
+}
+
+int32_t mg_set_actor_root_state(mg_sim* s, const float* src, int32_t src_host, const int32_t* idx,
+                                int32_t n_idx, void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (!src) return fail(MG_ERR_ARG, "null source tensor");
+    if (idx && n_idx < 0) return fail(MG_ERR_ARG, "negative index count");
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)stream;
+    const float* dsrc;
+    const int* didx;
+    int rc = stage_src(s, src, src_host, (size_t)s->na * MG_STATE_N, idx, n_idx, st, &dsrc, &didx);
+    if (rc) return rc;
+    HIP_TRY(mg_launch_scatter_rows(dsrc, MG_STATE_N, s->d_actor_root, didx, idx ? n_idx : s->na, s->d_state,
+                                   s->nb, st));
+    return MG_OK;
+}
+
+int32_t mg_set_rigid_body_state(mg_sim* s, const float* src, int32_t src_host, void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (!src) return fail(MG_ERR_ARG, "null source tensor");
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)stream;
+    const float* dsrc;
+    const int* didx;
+    int rc = stage_src(s, src, src_host, (size_t)s->nb * MG_STATE_N, nullptr, 0, st, &dsrc, &didx);
+    if (rc) return rc;
+    // free bodies only: rows are selected through the free-body list
+    HIP_TRY(mg_launch_scatter_rows(dsrc, MG_STATE_N, nullptr, s->d_free, s->nf, s->d_state, s->nb, st));
+    return MG_OK;
+}
+
+int32_t mg_set_dof_state(mg_sim* s, const float* src, int32_t src_host, const int32_t* idx, int32_t n_idx,
+                         void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    return set_dof_columns(s, src, src_host, 2, s->d_dof, s->d_dof + s->nd, idx, n_idx, (hipStream_t)stream);
+}
+int32_t mg_set_dof_position_target(mg_sim* s, const float* src, int32_t src_host, const int32_t* idx,
+                                   int32_t n_idx, void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    return set_dof_columns(s, src, src_host, 1, s->d_dof_tgt, nullptr, idx, n_idx, (hipStream_t)stream);
+}
+int32_t mg_set_dof_velocity_target(mg_sim* s, const float* src, int32_t src_host, const int32_t* idx,
+                                   int32_t n_idx, void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    return set_dof_columns(s, src, src_host, 1, s->d_dof_tgt + s->nd, nullptr, idx, n_idx, (hipStream_t)stream);
+}
+int32_t mg_set_dof_actuation_force(mg_sim* s, const float* src, int32_t src_host, const int32_t* idx,
+                                   int32_t n_idx, void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    return set_dof_columns(s, src, src_host, 1, s->d_dof_tgt + 2 * (size_t)s->nd, nullptr, idx, n_idx,
+                           (hipStream_t)stream);
+}
+
+int32_t mg_set_dof_props(mg_sim* s, const float* props_host) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (s->nd == 0) return MG_OK;
+    if (!props_host) return fail(MG_ERR_ARG, "null props");
+    HIP_TRY(hipSetDevice(s->device));
+    std::vector<float> dp = to_soa(props_host, s->nd, MG_DOFPROP_N);
+    HIP_TRY(hipMemcpy(s->d_dof_props, dp.data(), dp.size() * sizeof(float), hipMemcpyHostToDevice));
+    return MG_OK;
+}
+
+int32_t mg_apply_rigid_body_force(mg_sim* s, const float* force, const float* torque, int32_t space,
+                                  int32_t src_host, void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (space != 0) return fail(MG_ERR_UNSUPPORTED, "only global-space forces are supported");
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)stream;
+    const float* parts[2] = {force, torque};
+    for (int k = 0; k < 2; ++k) {
+        if (!parts[k]) continue;
+        const float* dsrc;
+        const int* didx;
+        int rc = stage_src(s, parts[k], src_host, (size_t)s->nb * 3, nullptr, 0, st, &dsrc, &didx);
+        if (rc) return rc;
+        HIP_TRY(mg_launch_scatter_rows(dsrc, 3, nullptr, nullptr, s->nb, s->d_ext + (size_t)k * 3 * s->nb, s->nb, st));
+        if (src_host) HIP_TRY(hipStreamSynchronize(st));  // staging buffer is reused by the next part
+    }
+    s->ext_pending = true;
+    return MG_OK;
+}
+
+int32_t mg_refresh_jacobian(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_host, void* stream) {
+    (void)tmpl; (void)dst; (void)dst_host; (void)stream;
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    return fail(MG_ERR_UNSUPPORTED, "jacobian tensors are not implemented yet");
+}
+int32_t mg_refresh_mass_matrix(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_host, void* stream) {
+    (void)tmpl; (void)dst; (void)dst_host; (void)stream;
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    return fail(MG_ERR_UNSUPPORTED, "mass matrix tensors are not implemented yet");
+}
+
+}  // extern "C"

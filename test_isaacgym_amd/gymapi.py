@@ -1,0 +1,1023 @@
+"""isaacgym.gymapi mirror over libmigym (MI355X).
+
+`acquire_gym()` returns the Gym singleton whose methods the reference's scripts
+call (the hot loop is test10_servo_vecenv.py:376-471 and
+examples/franka_cube_ik_osc.py:336-415). The physics path — simulate, refresh_*,
+set_* — is libmigym's HIP kernels; everything here is scene bookkeeping and
+argument marshalling. Error behaviour follows Isaac Gym: creators return None,
+setters return False, lookups return INVALID_HANDLE (-1).
+
+Out of scope: rendering and the viewer. Camera and viewer calls
+are headless stubs that keep the reference scripts running (§8b last row).
+"""
+import ctypes
+import math
+import sys
+import time
+
+import numpy as np
+import torch
+
+from . import _assets
+from . import _native as N
+from ._sim import Actor, CameraSensor, Env, Sim, Viewer
+from ._types import *  # noqa: F401,F403
+from ._types import (_DOF_TYPE_STRINGS, _JOINT_TYPE_STRINGS, DOF_PROPERTIES_DTYPE, DofState, Quat,
+                     RigidBodyProperties, RigidBodyState, Transform, Vec3)
+from . import _types as _T
+
+
+class Tensor:
+    """Non-owning tensor descriptor (gymapi.Tensor): what acquire_* returns and
+    gymtorch.unwrap_tensor builds (examples/interop_torch.py:133-142)."""
+
+    def __init__(self, torch_tensor):
+        self._t = torch_tensor
+        self.data_address = torch_tensor.data_ptr()
+        self.shape = tuple(torch_tensor.shape)
+        self.device = -1 if torch_tensor.device.type == "cpu" else int(torch_tensor.device.index or 0)
+        self.dtype = _T.DTYPE_FLOAT32 if torch_tensor.dtype == torch.float32 else _T.DTYPE_UINT32
+        self.own_data = False
+        self.ndim = torch_tensor.dim()
+
+    @property
+    def is_host(self):
+        return self.device < 0
+
+    def __repr__(self):
+        return "gymapi.Tensor(shape=%s, device=%d, data_address=0x%x)" % (self.shape, self.device, self.data_address)
+
+
+def _as_tensor_arg(t, name):
+    if isinstance(t, Tensor):
+        tt = t._t
+    elif isinstance(t, torch.Tensor):
+        tt = t
+    else:
+        raise TypeError("%s: expected a gymapi.Tensor (gymtorch.unwrap_tensor)" % name)
+    if not tt.is_contiguous():
+        raise ValueError("%s: tensor must be contiguous" % name)
+    return tt
+
+
+class Gym:
+    def __init__(self):
+        self._sims = []
+        self._t0 = time.time()
+
+    # ================================================================ sim
+    def create_sim(self, compute_device=0, graphics_device=0, type=_T.SIM_PHYSX, params=None):
+        """test10_servo_vecenv.py:185. Returns a Sim, or None (Isaac Gym style)."""
+        if params is None:
+            params = _T.SimParams()
+        if type != _T.SIM_PHYSX:
+            print("*** migym: only the PhysX-style rigid solver is available (SIM_FLEX requested)", file=sys.stderr)
+            return None
+        sim = Sim(compute_device, graphics_device, type, params)
+        self._sims.append(sim)
+        return sim
+
+    def destroy_sim(self, sim):
+        if sim is not None:
+            sim.destroy()
+            if sim in self._sims:
+                self._sims.remove(sim)
+
+    def get_sim_params(self, sim):
+        return sim.params
+
+    def set_sim_params(self, sim, params):
+        sim.params = params
+        if sim.native:
+            N.check(N.lib.mg_set_sim_params(sim.native, ctypes.byref(sim.mg_params())), "mg_set_sim_params")
+
+    def add_ground(self, sim, params):
+        sim.plane = params
+        if sim.native:
+            N.check(N.lib.mg_set_sim_params(sim.native, ctypes.byref(sim.mg_params())), "mg_set_sim_params")
+
+    def prepare_sim(self, sim):
+        """examples/franka_cube_ik_osc.py:288. Uploads the scene to HBM."""
+        sim.finalize()
+        return True
+
+    def simulate(self, sim):
+        """One frame (test10_servo_vecenv.py:380): the fused HIP step kernels."""
+        h = sim.require_native("gym.simulate")
+        N.check(N.lib.mg_simulate(h, sim.stream()), "mg_simulate")
+        sim.frame += 1
+        sim.time += sim.params.dt
+
+    def fetch_results(self, sim, wait=True):
+        if sim.native:
+            N.check(N.lib.mg_fetch_results(sim.native, 1 if wait else 0), "mg_fetch_results")
+        return True
+
+    def get_sim_time(self, sim):
+        return sim.time
+
+    def get_frame_count(self, sim):
+        return sim.frame
+
+    def get_elapsed_time(self, sim):
+        return time.time() - self._t0
+
+    def get_sim_actor_count(self, sim):
+        return sum(len(e.actors) for e in sim.envs)
+
+    def get_sim_rigid_body_count(self, sim):
+        return sum(e.num_bodies for e in sim.envs)
+
+    def get_sim_dof_count(self, sim):
+        return sum(e.num_dofs for e in sim.envs)
+
+    def get_env_count(self, sim):
+        return len(sim.envs)
+
+    def get_env(self, sim, index):
+        return sim.envs[index]
+
+    # ================================================================ assets
+    def load_asset(self, sim, rootpath, filename, options=None):
+        """test10_servo_vecenv.py:230. None on failure (:232-234)."""
+        options = options if options is not None else _T.AssetOptions()
+        try:
+            if filename.lower().endswith(".urdf"):
+                asset = _assets.load_urdf(rootpath, filename, _copy_options(options))
+            else:
+                print("*** migym: unsupported asset format: %s" % filename, file=sys.stderr)
+                return None
+        except (OSError, ValueError) as e:
+            print("*** migym: failed to load asset %s: %s" % (filename, e), file=sys.stderr)
+            return None
+        for w in getattr(asset, "warnings", []):
+            print("migym: %s" % w, file=sys.stderr)
+        sim.assets.append(asset)
+        return asset
+
+    load_urdf = load_asset
+
+    def create_box(self, sim, width, height, depth, options=None):
+        a = _assets.create_box(width, height, depth, _copy_options(options or _T.AssetOptions()))
+        sim.assets.append(a)
+        return a
+
+    def create_sphere(self, sim, radius, options=None):
+        a = _assets.create_sphere(radius, _copy_options(options or _T.AssetOptions()))
+        sim.assets.append(a)
+        return a
+
+    def create_capsule(self, sim, radius, length, options=None):
+        a = _assets.create_capsule(radius, length, _copy_options(options or _T.AssetOptions()))
+        sim.assets.append(a)
+        return a
+
+    def get_asset_rigid_body_count(self, asset):
+        return len(asset.bodies)
+
+    def get_asset_rigid_body_name(self, asset, i):
+        return asset.bodies[i].name if 0 <= i < len(asset.bodies) else None
+
+    def get_asset_rigid_body_names(self, asset):
+        return [b.name for b in asset.bodies]
+
+    def get_asset_rigid_body_dict(self, asset):
+        return {b.name: i for i, b in enumerate(asset.bodies)}
+
+    def find_asset_rigid_body_index(self, asset, name):
+        return self.get_asset_rigid_body_dict(asset).get(name, _T.INVALID_HANDLE)
+
+    def get_asset_joint_count(self, asset):
+        return len(asset.joints)
+
+    def get_asset_joint_name(self, asset, i):
+        return asset.joints[i].name
+
+    def get_asset_joint_names(self, asset):
+        return [j.name for j in asset.joints]
+
+    def get_asset_joint_dict(self, asset):
+        return {j.name: i for i, j in enumerate(asset.joints)}
+
+    def get_asset_joint_type(self, asset, i):
+        return asset.joints[i].type
+
+    def find_asset_joint_index(self, asset, name):
+        return self.get_asset_joint_dict(asset).get(name, _T.INVALID_HANDLE)
+
+    def get_asset_dof_count(self, asset):
+        return asset.num_dofs
+
+    def get_asset_dof_name(self, asset, i):
+        return asset.dof_joints[i].name
+
+    def get_asset_dof_names(self, asset):
+        return [j.name for j in asset.dof_joints]
+
+    def get_asset_dof_dict(self, asset):
+        return {j.name: i for i, j in enumerate(asset.dof_joints)}
+
+    def find_asset_dof_index(self, asset, name):
+        return self.get_asset_dof_dict(asset).get(name, _T.INVALID_HANDLE)
+
+    def get_asset_dof_type(self, asset, i):
+        j = asset.dof_joints[i]
+        return _T.DOF_ROTATION if j.type == _T.JOINT_REVOLUTE else _T.DOF_TRANSLATION
+
+    def get_asset_dof_properties(self, asset):
+        return asset.dof_props.copy()
+
+    def get_asset_rigid_shape_count(self, asset):
+        return sum(len(b.shapes) for b in asset.bodies)
+
+    def get_asset_rigid_shape_properties(self, asset):
+        return list(asset.shape_props)
+
+    def set_asset_rigid_shape_properties(self, asset, props):
+        asset.shape_props = list(props)
+        return True
+
+    def get_asset_rigid_body_shape_indices(self, asset):
+        out, s = [], 0
+        for b in asset.bodies:
+            out.append((s, len(b.shapes)))
+            s += len(b.shapes)
+        return out
+
+    def get_joint_type_string(self, jtype):
+        return _JOINT_TYPE_STRINGS.get(jtype, "Invalid")
+
+    def get_dof_type_string(self, dtype):
+        return _DOF_TYPE_STRINGS.get(dtype, "Invalid")
+
+    # ================================================================ envs / actors
+    def create_env(self, sim, lower, upper, num_per_row):
+        """test10_servo_vecenv.py:301."""
+        if sim.finalized:
+            print("*** migym: cannot create envs after prepare_sim / first tensor access", file=sys.stderr)
+            return None
+        env = Env(sim, len(sim.envs), lower, upper, num_per_row)
+        sim.envs.append(env)
+        return env
+
+    def create_actor(self, env, asset, pose, name=None, group=-1, filter=0, segmentationId=0):
+        """test10_servo_vecenv.py:317,323. Returns the env-local actor handle, -1 on failure."""
+        if env.sim.finalized:
+            print("*** migym: cannot create actors after prepare_sim / first tensor access", file=sys.stderr)
+            return _T.INVALID_HANDLE
+        if asset is None:
+            return _T.INVALID_HANDLE
+        a = Actor(env, asset, pose, name if name is not None else asset.name, group, filter, segmentationId)
+        env.actors.append(a)
+        env.num_bodies += a.num_bodies
+        env.num_dofs += a.num_dofs
+        return a.handle
+
+    def _actor(self, env, handle):
+        if handle is None or not (0 <= handle < len(env.actors)):
+            raise IndexError("invalid actor handle %r" % (handle,))
+        return env.actors[handle]
+
+    def get_actor_count(self, env):
+        return len(env.actors)
+
+    def get_actor_handle(self, env, index):
+        return index if 0 <= index < len(env.actors) else _T.INVALID_HANDLE
+
+    def find_actor_handle(self, env, name):
+        for a in env.actors:
+            if a.name == name:
+                return a.handle
+        return _T.INVALID_HANDLE
+
+    def get_actor_name(self, env, handle):
+        return self._actor(env, handle).name
+
+    def get_actor_index(self, env, handle, domain):
+        a = self._actor(env, handle)
+        if domain == _T.DOMAIN_SIM:
+            env.sim._assign_indices()
+            return a.global_index
+        return a.handle
+
+    def get_actor_rigid_body_count(self, env, handle):
+        return self._actor(env, handle).num_bodies
+
+    def get_actor_rigid_body_names(self, env, handle):
+        return [b.name for b in self._actor(env, handle).asset.bodies]
+
+    def get_actor_rigid_body_dict(self, env, handle):
+        return {b.name: i for i, b in enumerate(self._actor(env, handle).asset.bodies)}
+
+    def get_actor_rigid_body_handle(self, env, handle, index):
+        a = self._actor(env, handle)
+        return a.body_offset + index if 0 <= index < a.num_bodies else _T.INVALID_HANDLE
+
+    def find_actor_rigid_body_handle(self, env, handle, name):
+        a = self._actor(env, handle)
+        for i, b in enumerate(a.asset.bodies):
+            if b.name == name:
+                return a.body_offset + i
+        return _T.INVALID_HANDLE
+
+    def get_actor_rigid_body_index(self, env, handle, index, domain):
+        """examples/franka_cube_ik_osc.py:255."""
+        a = self._actor(env, handle)
+        if not 0 <= index < a.num_bodies:
+            return _T.INVALID_HANDLE
+        if domain == _T.DOMAIN_ACTOR:
+            return index
+        if domain == _T.DOMAIN_ENV:
+            return a.body_offset + index
+        env.sim._assign_indices()
+        return a.global_body + index
+
+    def find_actor_rigid_body_index(self, env, handle, name, domain):
+        """examples/franka_cube_ik_osc.py:277."""
+        d = self.get_actor_rigid_body_dict(env, handle)
+        if name not in d:
+            return _T.INVALID_HANDLE
+        return self.get_actor_rigid_body_index(env, handle, d[name], domain)
+
+    def get_rigid_handle(self, env, actor_name, body_name):
+        h = self.find_actor_handle(env, actor_name)
+        return _T.INVALID_HANDLE if h < 0 else self.find_actor_rigid_body_handle(env, h, body_name)
+
+    def get_actor_joint_count(self, env, handle):
+        return len(self._actor(env, handle).asset.joints)
+
+    def get_actor_joint_names(self, env, handle):
+        return [j.name for j in self._actor(env, handle).asset.joints]
+
+    def get_actor_joint_dict(self, env, handle):
+        return {j.name: i for i, j in enumerate(self._actor(env, handle).asset.joints)}
+
+    def get_actor_joint_handle(self, env, handle, index):
+        return index
+
+    def get_actor_dof_count(self, env, handle):
+        return self._actor(env, handle).num_dofs
+
+    def get_actor_dof_names(self, env, handle):
+        return [j.name for j in self._actor(env, handle).asset.dof_joints]
+
+    def get_actor_dof_dict(self, env, handle):
+        return {j.name: i for i, j in enumerate(self._actor(env, handle).asset.dof_joints)}
+
+    def get_actor_dof_handle(self, env, handle, index):
+        a = self._actor(env, handle)
+        return a.dof_offset + index if 0 <= index < a.num_dofs else _T.INVALID_HANDLE
+
+    def find_actor_dof_handle(self, env, handle, name):
+        """test12_add_joint.py.py:100: a missing name gives INVALID_HANDLE, not an error."""
+        d = self.get_actor_dof_dict(env, handle)
+        return self._actor(env, handle).dof_offset + d[name] if name in d else _T.INVALID_HANDLE
+
+    def get_actor_dof_index(self, env, handle, index, domain):
+        a = self._actor(env, handle)
+        if domain == _T.DOMAIN_ACTOR:
+            return index
+        if domain == _T.DOMAIN_ENV:
+            return a.dof_offset + index
+        env.sim._assign_indices()
+        return a.global_dof + index
+
+    def find_actor_dof_index(self, env, handle, name, domain):
+        d = self.get_actor_dof_dict(env, handle)
+        return self.get_actor_dof_index(env, handle, d[name], domain) if name in d else _T.INVALID_HANDLE
+
+    def _dof_owner(self, env, dof_handle):
+        for a in env.actors:
+            if a.dof_offset <= dof_handle < a.dof_offset + a.num_dofs:
+                return a, dof_handle - a.dof_offset
+        raise IndexError("invalid DOF handle %r" % (dof_handle,))
+
+    # ---- DOF properties and targets (non-tensor API)
+    def get_actor_dof_properties(self, env, handle):
+        return self._actor(env, handle).dof_props.copy()
+
+    def set_actor_dof_properties(self, env, handle, props):
+        a = self._actor(env, handle)
+        props = np.asarray(props)
+        for f in DOF_PROPERTIES_DTYPE.names:
+            if props.dtype.names and f in props.dtype.names:
+                a.dof_props[f] = props[f]
+        sim = env.sim
+        if sim.finalized and sim.native:
+            self._push_dof_props(sim)
+        return True
+
+    def _push_dof_props(self, sim):
+        dp = np.zeros((sim.num_dofs, N.MG_DOFPROP_N), dtype=np.float32)
+        for a in sim.actors:
+            for d in range(a.num_dofs):
+                p = a.dof_props[d]
+                dp[a.global_dof + d, :10] = [p["driveMode"], p["stiffness"], p["damping"], p["effort"], p["velocity"],
+                                             p["lower"], p["upper"], 1.0 if p["hasLimits"] else 0.0, p["armature"],
+                                             p["friction"]]
+        N.check(N.lib.mg_set_dof_props(sim.native, dp.ctypes.data), "mg_set_dof_props")
+
+    def _set_actor_dof_column(self, env, handle, values, col):
+        a = self._actor(env, handle)
+        vals = np.asarray(values, dtype=np.float32).reshape(-1)
+        a.dof_targets[:len(vals), col] = vals[:a.num_dofs]
+        sim = env.sim
+        if sim.finalized and sim.native and a.num_dofs:
+            full = np.zeros(sim.num_dofs, dtype=np.float32)
+            full[a.global_dof:a.global_dof + a.num_dofs] = a.dof_targets[:, col]
+            idx = np.array([a.global_index], dtype=np.int32)
+            fn = (N.lib.mg_set_dof_position_target, N.lib.mg_set_dof_velocity_target,
+                  N.lib.mg_set_dof_actuation_force)[col]
+            N.check(fn(sim.native, full.ctypes.data, 1, idx.ctypes.data, 1, sim.stream()), "set dof column")
+        return True
+
+    def set_actor_dof_position_targets(self, env, handle, targets):
+        return self._set_actor_dof_column(env, handle, targets, 0)
+
+    def set_actor_dof_velocity_targets(self, env, handle, targets):
+        return self._set_actor_dof_column(env, handle, targets, 1)
+
+    def get_actor_dof_position_targets(self, env, handle):
+        return self._actor(env, handle).dof_targets[:, 0].copy()
+
+    def get_actor_dof_velocity_targets(self, env, handle):
+        return self._actor(env, handle).dof_targets[:, 1].copy()
+
+    def set_dof_target_position(self, env, dof_handle, target):
+        a, d = self._dof_owner(env, dof_handle)
+        vals = a.dof_targets[:, 0].copy()
+        vals[d] = target
+        return self._set_actor_dof_column(env, a.handle, vals, 0)
+
+    def set_dof_target_velocity(self, env, dof_handle, target):
+        a, d = self._dof_owner(env, dof_handle)
+        vals = a.dof_targets[:, 1].copy()
+        vals[d] = target
+        return self._set_actor_dof_column(env, a.handle, vals, 1)
+
+    def apply_dof_effort(self, env, dof_handle, effort):
+        a, d = self._dof_owner(env, dof_handle)
+        vals = a.dof_targets[:, 2].copy()
+        vals[d] = effort
+        return self._set_actor_dof_column(env, a.handle, vals, 2)
+
+    def apply_actor_dof_efforts(self, env, handle, efforts):
+        return self._set_actor_dof_column(env, handle, efforts, 2)
+
+    # ---- DOF / body states (non-tensor API; slow path)
+    def _host_state(self, sim):
+        """Current (body_state[nb,13], dof_state[nd,2]) on the host."""
+        sim.finalize()
+        if sim.native is None:
+            A = sim.model_arrays
+            return A["body_state0"].copy(), A["dof_state0"].copy()
+        rb = np.zeros((sim.num_bodies, 13), dtype=np.float32)
+        N.check(N.lib.mg_refresh_rigid_body_state(sim.native, rb.ctypes.data, 1, sim.stream()), "refresh")
+        ds = np.zeros((max(sim.num_dofs, 1), 2), dtype=np.float32)
+        if sim.num_dofs:
+            N.check(N.lib.mg_refresh_dof_state(sim.native, ds.ctypes.data, 1, sim.stream()), "refresh")
+        return rb, ds[:sim.num_dofs]
+
+    def get_actor_dof_states(self, env, handle, flags=_T.STATE_ALL):
+        a = self._actor(env, handle)
+        out = np.zeros(a.num_dofs, dtype=DofState.dtype)
+        if not env.sim.finalized:
+            out["pos"], out["vel"] = a.dof_state[:, 0], a.dof_state[:, 1]
+            return out
+        _, ds = self._host_state(env.sim)
+        sl = ds[a.global_dof:a.global_dof + a.num_dofs]
+        out["pos"], out["vel"] = sl[:, 0], sl[:, 1]
+        return out
+
+    def set_actor_dof_states(self, env, handle, states, flags=_T.STATE_ALL):
+        a = self._actor(env, handle)
+        st = np.asarray(states)
+        if flags & _T.STATE_POS:
+            a.dof_state[:, 0] = st["pos"][:a.num_dofs]
+        if flags & _T.STATE_VEL:
+            a.dof_state[:, 1] = st["vel"][:a.num_dofs]
+        sim = env.sim
+        if sim.finalized and sim.native and a.num_dofs:
+            full = np.zeros((sim.num_dofs, 2), dtype=np.float32)
+            full[a.global_dof:a.global_dof + a.num_dofs] = a.dof_state
+            idx = np.array([a.global_index], dtype=np.int32)
+            N.check(N.lib.mg_set_dof_state(sim.native, full.ctypes.data, 1, idx.ctypes.data, 1, sim.stream()),
+                    "mg_set_dof_state")
+        return True
+
+    def get_dof_position(self, env, dof_handle):
+        a, d = self._dof_owner(env, dof_handle)
+        return float(self.get_actor_dof_states(env, a.handle)["pos"][d])
+
+    def get_dof_velocity(self, env, dof_handle):
+        a, d = self._dof_owner(env, dof_handle)
+        return float(self.get_actor_dof_states(env, a.handle)["vel"][d])
+
+    def _rb_struct(self, rows):
+        out = np.zeros(len(rows), dtype=RigidBodyState.dtype)
+        for k, n in enumerate("xyz"):
+            out["pose"]["p"][n] = rows[:, k]
+            out["vel"]["linear"][n] = rows[:, 7 + k]
+            out["vel"]["angular"][n] = rows[:, 10 + k]
+        for k, n in enumerate("xyzw"):
+            out["pose"]["r"][n] = rows[:, 3 + k]
+        return out
+
+    def _rb_rows(self, st):
+        rows = np.zeros((len(st), 13), dtype=np.float32)
+        for k, n in enumerate("xyz"):
+            rows[:, k] = st["pose"]["p"][n]
+            rows[:, 7 + k] = st["vel"]["linear"][n]
+            rows[:, 10 + k] = st["vel"]["angular"][n]
+        for k, n in enumerate("xyzw"):
+            rows[:, 3 + k] = st["pose"]["r"][n]
+        return rows
+
+    def get_actor_rigid_body_states(self, env, handle, flags=_T.STATE_ALL):
+        a = self._actor(env, handle)
+        rb, _ = self._host_state(env.sim)
+        return self._rb_struct(rb[a.global_body:a.global_body + a.num_bodies])
+
+    def get_env_rigid_body_states(self, env, flags=_T.STATE_ALL):
+        rb, _ = self._host_state(env.sim)
+        first = env.actors[0].global_body if env.actors else 0
+        return self._rb_struct(rb[first:first + env.num_bodies])
+
+    def get_sim_rigid_body_states(self, sim, flags=_T.STATE_ALL):
+        rb, _ = self._host_state(sim)
+        return self._rb_struct(rb)
+
+    def _set_root_rows(self, sim, actors_rows):
+        """Teleport actor roots: [(actor, row13)] through the indexed root setter."""
+        sim.finalize()
+        full = np.zeros((sim.num_actors, 13), dtype=np.float32)
+        idx = np.zeros(len(actors_rows), dtype=np.int32)
+        for k, (a, row) in enumerate(actors_rows):
+            full[a.global_index] = row
+            idx[k] = a.global_index
+        if sim.native is None:
+            A = sim.model_arrays
+            for a, row in actors_rows:
+                A["body_state0"][a.global_body] = row
+            return True
+        N.check(N.lib.mg_set_actor_root_state(sim.native, full.ctypes.data, 1, idx.ctypes.data, len(idx),
+                                              sim.stream()), "mg_set_actor_root_state")
+        return True
+
+    def set_actor_rigid_body_states(self, env, handle, states, flags=_T.STATE_ALL):
+        a = self._actor(env, handle)
+        cur = self.get_actor_rigid_body_states(env, handle)
+        new = np.asarray(states)
+        if flags & _T.STATE_POS:
+            cur["pose"] = new["pose"][:len(cur)]
+        if flags & _T.STATE_VEL:
+            cur["vel"] = new["vel"][:len(cur)]
+        return self._set_root_rows(env.sim, [(a, self._rb_rows(cur[:1])[0])])
+
+    def set_sim_rigid_body_states(self, sim, states, flags=_T.STATE_ALL):
+        cur = self.get_sim_rigid_body_states(sim)
+        new = np.asarray(states)
+        if flags & _T.STATE_POS:
+            cur["pose"] = new["pose"]
+        if flags & _T.STATE_VEL:
+            cur["vel"] = new["vel"]
+        rows = self._rb_rows(cur)
+        return self._set_root_rows(sim, [(a, rows[a.global_body]) for a in sim.actors])
+
+    def set_rigid_linear_velocity(self, env, body_handle, vel):
+        a = self._body_owner(env, body_handle)
+        st = self.get_actor_rigid_body_states(env, a.handle)
+        st["vel"]["linear"][0] = (vel.x, vel.y, vel.z)
+        return self.set_actor_rigid_body_states(env, a.handle, st, _T.STATE_ALL)
+
+    def set_rigid_angular_velocity(self, env, body_handle, vel):
+        a = self._body_owner(env, body_handle)
+        st = self.get_actor_rigid_body_states(env, a.handle)
+        st["vel"]["angular"][0] = (vel.x, vel.y, vel.z)
+        return self.set_actor_rigid_body_states(env, a.handle, st, _T.STATE_ALL)
+
+    def set_rigid_transform(self, env, body_handle, transform):
+        a = self._body_owner(env, body_handle)
+        st = self.get_actor_rigid_body_states(env, a.handle)
+        st["pose"]["p"][0] = (transform.p.x, transform.p.y, transform.p.z)
+        st["pose"]["r"][0] = (transform.r.x, transform.r.y, transform.r.z, transform.r.w)
+        return self.set_actor_rigid_body_states(env, a.handle, st, _T.STATE_ALL)
+
+    def _body_owner(self, env, body_handle):
+        for a in env.actors:
+            if a.body_offset <= body_handle < a.body_offset + a.num_bodies:
+                return a
+        raise IndexError("invalid rigid body handle %r" % (body_handle,))
+
+    def get_rigid_transform(self, env, body_handle):
+        """examples/franka_cube_ik_osc.py:272."""
+        a = self._body_owner(env, body_handle)
+        env.sim._assign_indices()
+        if env.sim.finalized:
+            rb, _ = self._host_state(env.sim)
+            r = rb[a.global_body + body_handle - a.body_offset]
+            return Transform(Vec3(*r[0:3]), Quat(*r[3:7]))
+        ps, qs = env.sim.actor_world_body_poses(a)
+        k = body_handle - a.body_offset
+        return Transform(Vec3(*ps[k]), Quat(*qs[k]))
+
+    # ---- rigid body / shape properties
+    def get_actor_rigid_body_properties(self, env, handle):
+        a = self._actor(env, handle)
+        out = []
+        for mp in a.mass_props:
+            p = RigidBodyProperties(mp.mass, Vec3(*mp.com))
+            p.inertia = _T.Mat33(Vec3(*mp.inertia[0]), Vec3(*mp.inertia[1]), Vec3(*mp.inertia[2]))
+            out.append(p)
+        return out
+
+    def set_actor_rigid_body_properties(self, env, handle, props, recomputeInertia=False):
+        a = self._actor(env, handle)
+        if env.sim.finalized:
+            print("*** migym: rigid body properties are frozen after prepare_sim", file=sys.stderr)
+            return False
+        new = []
+        for mp, p in zip(a.mass_props, props):
+            I = mp.inertia
+            if getattr(p, "inertia", None) is not None and not recomputeInertia:
+                I = np.array([[p.inertia.x.x, p.inertia.x.y, p.inertia.x.z], [p.inertia.y.x, p.inertia.y.y,
+                              p.inertia.y.z], [p.inertia.z.x, p.inertia.z.y, p.inertia.z.z]])
+            if recomputeInertia and mp.mass > 0:
+                I = mp.inertia * (p.mass / mp.mass)
+            new.append(_assets.MassProps(p.mass, [p.com.x, p.com.y, p.com.z], I))
+        a.mass_props = new
+        return True
+
+    def get_actor_rigid_shape_properties(self, env, handle):
+        return self._actor(env, handle).shape_props
+
+    def set_actor_rigid_shape_properties(self, env, handle, props):
+        a = self._actor(env, handle)
+        if env.sim.finalized:
+            print("*** migym: shape properties are frozen after prepare_sim", file=sys.stderr)
+            return False
+        a.shape_props = list(props)
+        return True
+
+    def set_rigid_body_color(self, env, handle, body_index, mesh_type, color):
+        self._actor(env, handle).body_colors[body_index] = color
+
+    def get_rigid_body_color(self, env, handle, body_index, mesh_type):
+        return self._actor(env, handle).body_colors.get(body_index, Vec3(1, 1, 1))
+
+    def set_rigid_body_segmentation_id(self, env, handle, body_index, seg):
+        pass
+
+    def set_rigid_body_texture(self, env, handle, body_index, mesh_type, tex):
+        pass
+
+    def set_actor_scale(self, env, handle, scale):
+        self._actor(env, handle).scale = float(scale)
+        return abs(scale - 1.0) < 1e-6
+
+    def get_actor_scale(self, env, handle):
+        return self._actor(env, handle).scale
+
+    # ================================================================ tensor API
+    def _acquire(self, sim, key):
+        sim.finalize()
+        return Tensor(sim.tensors[key])
+
+    def acquire_actor_root_state_tensor(self, sim):
+        """test10_servo_vecenv.py:372,400: the same storage on every call."""
+        return self._acquire(sim, "root")
+
+    def acquire_rigid_body_state_tensor(self, sim):
+        return self._acquire(sim, "rb")
+
+    def acquire_dof_state_tensor(self, sim):
+        return self._acquire(sim, "dof")
+
+    def acquire_net_contact_force_tensor(self, sim):
+        return self._acquire(sim, "ncf")
+
+    def _refresh(self, sim, key, fn, what):
+        sim.finalize()
+        t = sim.tensors[key]
+        if t.numel() == 0:
+            return True
+        h = sim.require_native(what)
+        N.check(fn(h, t.data_ptr(), 1 if t.device.type == "cpu" else 0, sim.stream()), what)
+        return True
+
+    def refresh_actor_root_state_tensor(self, sim):
+        return self._refresh(sim, "root", N.lib.mg_refresh_actor_root_state, "refresh_actor_root_state_tensor")
+
+    def refresh_rigid_body_state_tensor(self, sim):
+        return self._refresh(sim, "rb", N.lib.mg_refresh_rigid_body_state, "refresh_rigid_body_state_tensor")
+
+    def refresh_dof_state_tensor(self, sim):
+        """test10_servo_vecenv.py:396: zero DOFs is an empty tensor, not an error."""
+        return self._refresh(sim, "dof", N.lib.mg_refresh_dof_state, "refresh_dof_state_tensor")
+
+    def refresh_net_contact_force_tensor(self, sim):
+        return self._refresh(sim, "ncf", N.lib.mg_refresh_net_contact_force, "refresh_net_contact_force_tensor")
+
+    def _set(self, sim, tensor, fn, ncols, nrows, what, index=None, count=None):
+        sim.finalize()
+        t = _as_tensor_arg(tensor, what)
+        if t.dtype != torch.float32 or t.numel() != nrows * ncols:
+            print("*** migym: %s: expected a float32 tensor of %d x %d" % (what, nrows, ncols), file=sys.stderr)
+            return False
+        if nrows == 0:
+            return True
+        h = sim.require_native(what)
+        host = 1 if t.device.type == "cpu" else 0
+        if index is not None:
+            it = _as_tensor_arg(index, what + " indices")
+            if it.dtype != torch.int32:
+                print("*** migym: %s: indices must be int32" % what, file=sys.stderr)
+                return False
+            if (it.device.type == "cpu") != (t.device.type == "cpu"):
+                it = it.to(t.device)
+            n = int(count) if count is not None else it.numel()
+            rc = fn(h, t.data_ptr(), host, it.data_ptr(), n, sim.stream())
+        else:
+            rc = fn(h, t.data_ptr(), host, None, 0, sim.stream())
+        if rc != N.MG_OK:
+            print("*** migym: %s: %s" % (what, N.last_error()), file=sys.stderr)
+            return False
+        return True
+
+    def set_actor_root_state_tensor(self, sim, tensor):
+        """test10_servo_vecenv.py:456: teleports all actor roots; returns bool."""
+        return self._set(sim, tensor, N.lib.mg_set_actor_root_state, 13, sim_num(sim, "actors"),
+                         "set_actor_root_state_tensor")
+
+    def set_actor_root_state_tensor_indexed(self, sim, tensor, indices, count):
+        return self._set(sim, tensor, N.lib.mg_set_actor_root_state, 13, sim_num(sim, "actors"),
+                         "set_actor_root_state_tensor_indexed", indices, count)
+
+    def set_rigid_body_state_tensor(self, sim, tensor):
+        sim.finalize()
+        t = _as_tensor_arg(tensor, "set_rigid_body_state_tensor")
+        if t.numel() != sim.num_bodies * 13:
+            return False
+        h = sim.require_native("set_rigid_body_state_tensor")
+        rc = N.lib.mg_set_rigid_body_state(h, t.data_ptr(), 1 if t.device.type == "cpu" else 0, sim.stream())
+        return rc == N.MG_OK
+
+    def set_dof_state_tensor(self, sim, tensor):
+        return self._set(sim, tensor, N.lib.mg_set_dof_state, 2, sim_num(sim, "dofs"), "set_dof_state_tensor")
+
+    def set_dof_state_tensor_indexed(self, sim, tensor, indices, count):
+        return self._set(sim, tensor, N.lib.mg_set_dof_state, 2, sim_num(sim, "dofs"),
+                         "set_dof_state_tensor_indexed", indices, count)
+
+    def set_dof_position_target_tensor(self, sim, tensor):
+        """examples/franka_cube_ik_osc.py:409."""
+        return self._set(sim, tensor, N.lib.mg_set_dof_position_target, 1, sim_num(sim, "dofs"),
+                         "set_dof_position_target_tensor")
+
+    def set_dof_position_target_tensor_indexed(self, sim, tensor, indices, count):
+        return self._set(sim, tensor, N.lib.mg_set_dof_position_target, 1, sim_num(sim, "dofs"),
+                         "set_dof_position_target_tensor_indexed", indices, count)
+
+    def set_dof_velocity_target_tensor(self, sim, tensor):
+        return self._set(sim, tensor, N.lib.mg_set_dof_velocity_target, 1, sim_num(sim, "dofs"),
+                         "set_dof_velocity_target_tensor")
+
+    def set_dof_velocity_target_tensor_indexed(self, sim, tensor, indices, count):
+        return self._set(sim, tensor, N.lib.mg_set_dof_velocity_target, 1, sim_num(sim, "dofs"),
+                         "set_dof_velocity_target_tensor_indexed", indices, count)
+
+    def set_dof_actuation_force_tensor(self, sim, tensor):
+        """examples/franka_cube_ik_osc.py:410."""
+        return self._set(sim, tensor, N.lib.mg_set_dof_actuation_force, 1, sim_num(sim, "dofs"),
+                         "set_dof_actuation_force_tensor")
+
+    def set_dof_actuation_force_tensor_indexed(self, sim, tensor, indices, count):
+        return self._set(sim, tensor, N.lib.mg_set_dof_actuation_force, 1, sim_num(sim, "dofs"),
+                         "set_dof_actuation_force_tensor_indexed", indices, count)
+
+    def apply_rigid_body_force_tensors(self, sim, forceTensor=None, torqueTensor=None, space=_T.ENV_SPACE):
+        sim.finalize()
+        h = sim.require_native("apply_rigid_body_force_tensors")
+        tensors = [_as_tensor_arg(x, "apply_rigid_body_force_tensors") if x is not None else None
+                   for x in (forceTensor, torqueTensor)]
+        host = 1 if any(t is not None and t.device.type == "cpu" for t in tensors) else 0
+        ptr = [t.data_ptr() if t is not None else None for t in tensors]
+        mg_space = 1 if space == _T.LOCAL_SPACE else 0
+        rc = N.lib.mg_apply_rigid_body_force(h, ptr[0], ptr[1], mg_space, host, sim.stream())
+        if rc != N.MG_OK:
+            print("*** migym: apply_rigid_body_force_tensors: %s" % N.last_error(), file=sys.stderr)
+            return False
+        return True
+
+    def _artic_template(self, sim, actor_name):
+        sim.finalize()
+        for a in sim.actors:
+            if a.name == actor_name and len(a.asset.bodies) > 1:
+                A = sim.model_arrays
+                for k, row in enumerate(A["artic_i"]):
+                    if row[0] == a.global_body:
+                        return int(row[2]), a.asset
+        raise KeyError("no articulated actor named %r" % (actor_name,))
+
+    def acquire_jacobian_tensor(self, sim, actor_name):
+        """examples/franka_cube_ik_osc.py:305: (num_envs, links-1, 6, dofs) for a fixed base."""
+        t, asset = self._artic_template(sim, actor_name)
+        if actor_name not in sim.jacobians:
+            n = sum(1 for a in sim.actors if a.name == actor_name)
+            fixed = asset.options.fix_base_link
+            nl = len(asset.bodies) - (1 if fixed else 0)
+            nd = asset.num_dofs + (0 if fixed else 6)
+            sim.jacobians[actor_name] = (t, torch.zeros((n, nl, 6, nd), dtype=torch.float32, device=sim.device))
+        return Tensor(sim.jacobians[actor_name][1])
+
+    def acquire_mass_matrix_tensor(self, sim, actor_name):
+        """examples/franka_cube_ik_osc.py:315: (num_envs, dofs, dofs) for a fixed base."""
+        t, asset = self._artic_template(sim, actor_name)
+        if actor_name not in sim.mass_matrices:
+            n = sum(1 for a in sim.actors if a.name == actor_name)
+            nd = asset.num_dofs + (0 if asset.options.fix_base_link else 6)
+            sim.mass_matrices[actor_name] = (t, torch.zeros((n, nd, nd), dtype=torch.float32, device=sim.device))
+        return Tensor(sim.mass_matrices[actor_name][1])
+
+    def refresh_jacobian_tensors(self, sim):
+        h = sim.require_native("refresh_jacobian_tensors")
+        for name, (t, ten) in sim.jacobians.items():
+            N.check(N.lib.mg_refresh_jacobian(h, t, ten.data_ptr(), 1 if ten.device.type == "cpu" else 0,
+                                              sim.stream()), "refresh_jacobian_tensors(%s)" % name)
+        return True
+
+    def refresh_mass_matrix_tensors(self, sim):
+        h = sim.require_native("refresh_mass_matrix_tensors")
+        for name, (t, ten) in sim.mass_matrices.items():
+            N.check(N.lib.mg_refresh_mass_matrix(h, t, ten.data_ptr(), 1 if ten.device.type == "cpu" else 0,
+                                                 sim.stream()), "refresh_mass_matrix_tensors(%s)" % name)
+        return True
+
+    # ================================================================ viewer (headless)
+    def create_viewer(self, sim, props):
+        return Viewer(sim, props)
+
+    def destroy_viewer(self, viewer):
+        pass
+
+    def query_viewer_has_closed(self, viewer):
+        return viewer is None or viewer.frames >= viewer.max_frames
+
+    def draw_viewer(self, viewer, sim, render_collision=False):
+        if viewer is not None:
+            viewer.frames += 1
+
+    def step_graphics(self, sim):
+        pass
+
+    def sync_frame_time(self, sim):
+        """Real-time throttle in Isaac Gym (test10_servo_vecenv.py:392): a no-op here."""
+
+    def poll_viewer_events(self, viewer):
+        pass
+
+    def viewer_camera_look_at(self, viewer, env, pos, target):
+        if viewer is not None:
+            viewer.cam_transform = Transform(pos, Quat())
+
+    def get_viewer_camera_transform(self, viewer, env):
+        return viewer.cam_transform if viewer is not None else Transform()
+
+    def get_viewer_size(self, viewer):
+        return Vec3(_T.DEFAULT_VIEWER_WIDTH, _T.DEFAULT_VIEWER_HEIGHT, 0)
+
+    def get_viewer_mouse_position(self, viewer):
+        return Vec3(0.5, 0.5, 0)
+
+    def subscribe_viewer_keyboard_event(self, viewer, key, action):
+        pass
+
+    def subscribe_viewer_mouse_event(self, viewer, button, action):
+        pass
+
+    def query_viewer_action_events(self, viewer):
+        return []
+
+    def add_lines(self, viewer, env, num_lines, vertices, colors):
+        pass
+
+    def clear_lines(self, viewer):
+        pass
+
+    def set_light_parameters(self, sim, light_index, intensity, ambient, direction):
+        pass
+
+    def draw_env_rigid_contacts(self, viewer, env, color, scale, flag):
+        pass
+
+    # ================================================================ cameras (headless)
+    def create_camera_sensor(self, env, props):
+        """Per-env 0-based handles (test11's aliased list needs that)."""
+        cam = CameraSensor(env, props, len(env.cameras))
+        env.cameras.append(cam)
+        return cam.handle
+
+    def destroy_camera_sensor(self, sim, env, handle):
+        pass
+
+    def set_camera_location(self, handle, env, pos, target):
+        cam = env.cameras[handle]
+        cam.transform = _look_at(pos, target)
+
+    def set_camera_transform(self, handle, env, transform):
+        env.cameras[handle].transform = Transform(transform.p, transform.r)
+
+    def attach_camera_to_body(self, handle, env, body_handle, local_transform, follow_mode):
+        cam = env.cameras[handle]
+        cam.body = body_handle
+        cam.local = Transform(local_transform.p, local_transform.r)
+        cam.follow = follow_mode
+
+    def get_camera_transform(self, sim, env, handle):
+        cam = env.cameras[handle]
+        if cam.body is None:
+            o = env.origin
+            return Transform(Vec3(o[0], o[1], o[2]), Quat()) * cam.transform
+        return self.get_rigid_transform(env, cam.body) * cam.local
+
+    def get_camera_view_matrix(self, sim, env, handle):
+        t = self.get_camera_transform(sim, env, handle)
+        inv = t.inverse()
+        R = _assets._qmat(np.array([inv.r.x, inv.r.y, inv.r.z, inv.r.w]))
+        m = np.eye(4, dtype=np.float32)
+        m[:3, :3] = R.T
+        m[3, :3] = [inv.p.x, inv.p.y, inv.p.z]
+        return m
+
+    def get_camera_proj_matrix(self, sim, env, handle):
+        p = env.cameras[handle].props
+        fx = 1.0 / math.tan(math.radians(p.horizontal_fov) * 0.5)
+        fy = fx * p.width / p.height
+        n, f = p.near_plane, p.far_plane
+        m = np.zeros((4, 4), dtype=np.float32)
+        m[0, 0], m[1, 1] = fx, fy
+        m[2, 2] = 0.0
+        m[2, 3] = -1.0
+        m[3, 2] = n
+        return m
+
+    def set_camera_proj_matrix(self, *args):
+        pass
+
+    def render_all_camera_sensors(self, sim):
+        pass
+
+    def start_access_image_tensors(self, sim):
+        pass
+
+    def end_access_image_tensors(self, sim):
+        pass
+
+    def get_camera_image(self, sim, env, handle, image_type):
+        p = env.cameras[handle].props
+        if image_type == _T.IMAGE_COLOR:
+            return np.zeros((p.height, p.width * 4), dtype=np.uint8)
+        if image_type == _T.IMAGE_SEGMENTATION:
+            return np.zeros((p.height, p.width), dtype=np.int32)
+        return np.zeros((p.height, p.width), dtype=np.float32)
+
+    def get_camera_image_gpu_tensor(self, sim, env, handle, image_type):
+        p = env.cameras[handle].props
+        shape = (p.height, p.width, 4) if image_type == _T.IMAGE_COLOR else (p.height, p.width)
+        dtype = torch.uint8 if image_type == _T.IMAGE_COLOR else torch.float32
+        return Tensor(torch.zeros(shape, dtype=dtype, device=sim.device))
+
+    def write_camera_image_to_file(self, sim, env, handle, image_type, filename):
+        return True
+
+    def write_viewer_image_to_file(self, viewer, filename):
+        return True
+
+
+def sim_num(sim, what):
+    sim.finalize()
+    return {"actors": sim.num_actors, "bodies": sim.num_bodies, "dofs": sim.num_dofs}[what]
+
+
+def _look_at(pos, target):
+    f = (target - pos).normalize()
+    yaw = math.atan2(f.y, f.x)
+    pitch = -math.asin(max(-1.0, min(1.0, f.z)))
+    return Transform(pos, Quat.from_euler_zyx(0.0, pitch, yaw))
+
+
+def _copy_options(o):
+    c = _T.AssetOptions()
+    c.__dict__.update(o.__dict__)
+    return c
+
+
+_GYM = None
+
+
+def acquire_gym():
+    """gymapi.acquire_gym() (test10_servo_vecenv.py:177): the singleton Gym."""
+    global _GYM
+    if _GYM is None:
+        _GYM = Gym()
+    return _GYM

@@ -1,0 +1,224 @@
+"""GPU parity: the HIP step kernels (through the C ABI, driven by the gymapi
+tensor API exactly like test10_servo_vecenv.py:376-456) against the C
+restatement in oracle/ on the same inputs.
+
+Tolerance: the device and the oracle evaluate the same fp32 expressions in the
+same order with FMA contraction off, so the expected difference is zero; the
+hard assertion is |gpu - oracle| <= 1e-5 * max(1, |x|) per element (positions
+up to ~1e3 m, velocities up to 1e3 m/s), and bit-exactness is asserted
+separately so a drift in either build shows up by name.
+"""
+import numpy as np
+import pytest
+import torch
+
+from isaacgym import gymapi, gymtorch
+from test_isaacgym_amd import scenes
+import oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+RTOL = 1e-5
+
+
+def _close(a, b):
+    return np.abs(a - b) <= RTOL * np.maximum(1.0, np.abs(b))
+
+
+def _tensors(gym, sim):
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))
+    return root, rb, dof, ncf
+
+
+def test_servo_single_step_parity(gym):
+    """Every step starts the oracle from the device's own state (after the
+    root teleport), so each simulate() is compared on identical inputs."""
+    n, steps = 256, 40
+    sim, _ = scenes.servo_scene(gym, n)
+    gym.prepare_sim(sim)
+    root, rb, _, ncf = _tensors(gym, sim)
+    acts = scenes.servo_actions(n, steps, DEV, seed=1)
+    p, m = sim.mg_params(), sim.mg_model()
+    gym.refresh_actor_root_state_tensor(sim)
+    worst = 0.0
+    exact = True
+    for k in range(steps):
+        root[:, 3:10] = acts[k]
+        assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.refresh_rigid_body_state_tensor(sim)
+        inp = rb.cpu().numpy().copy()
+        gym.simulate(sim)
+        gym.fetch_results(sim, True)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_net_contact_force_tensor(sim)
+        gym.refresh_actor_root_state_tensor(sim)
+        got = rb.cpu().numpy()
+        cf = oracle.step(p, m, inp, np.zeros((0, 2), np.float32))
+        assert np.all(_close(got, inp)), "step %d: max |diff| %g" % (k, np.abs(got - inp).max())
+        assert np.all(_close(ncf.cpu().numpy(), cf))
+        worst = max(worst, float(np.abs(got - inp).max()))
+        exact = exact and np.array_equal(got, inp) and np.array_equal(ncf.cpu().numpy(), cf)
+    assert exact, "within tolerance but not bit-exact (max |diff| %g)" % worst
+
+
+def test_servo_trajectory_bitexact(gym):
+    """A 120-frame rollout with a random root teleport every frame, device vs
+    oracle from the same initial state: no re-synchronisation."""
+    n, steps = 128, 120
+    sim, _ = scenes.servo_scene(gym, n)
+    gym.prepare_sim(sim)
+    root, rb, _, _ = _tensors(gym, sim)
+    acts = scenes.servo_actions(n, steps, DEV, seed=2)
+    acts_h = acts.cpu().numpy()
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    roots = sim.model_arrays["actor_root_body"]
+    gym.refresh_actor_root_state_tensor(sim)
+    for k in range(steps):
+        root[:, 3:10] = acts[k]
+        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.simulate(sim)
+        gym.refresh_actor_root_state_tensor(sim)
+        # oracle: the same teleport of every root row, then the step
+        st[roots, 3:10] = acts_h[k]
+        oracle.step(p, m, st, np.zeros((0, 2), np.float32))
+    gym.refresh_rigid_body_state_tensor(sim)
+    got = rb.cpu().numpy()
+    assert np.all(np.isfinite(got))
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+
+
+def test_primitive_drops_parity(gym):
+    """Boxes, spheres and capsules dropped at random orientations onto the
+    ground: every contact branch of the kernel, 240 frames, bit for bit."""
+    sp = scenes.servo_sim_params(True)
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    plane.restitution = 0.5
+    gym.add_ground(sim, plane)
+    assets = [gym.create_box(sim, 1.0, 0.5, 0.3, gymapi.AssetOptions()),
+              gym.create_sphere(sim, 0.3, gymapi.AssetOptions()),
+              gym.create_capsule(sim, 0.2, 0.8, gymapi.AssetOptions())]
+    rng = np.random.RandomState(42)
+    for i in range(96):
+        env = gym.create_env(sim, gymapi.Vec3(-2, -2, 0), gymapi.Vec3(2, 2, 2), 10)
+        q = gymapi.Quat(*rng.randn(4)).normalize()
+        pose = gymapi.Transform(gymapi.Vec3(0, 0, 0.5 + 2 * rng.rand()), q)
+        gym.create_actor(env, assets[i % 3], pose, "obj", i, 0)
+    gym.prepare_sim(sim)
+    _, rb, _, ncf = _tensors(gym, sim)
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    for _ in range(240):
+        gym.simulate(sim)
+        cf = oracle.step(p, m, st, np.zeros((0, 2), np.float32))
+    gym.refresh_rigid_body_state_tensor(sim)
+    gym.refresh_net_contact_force_tensor(sim)
+    got = rb.cpu().numpy()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+    assert np.array_equal(ncf.cpu().numpy(), cf)
+    # physics sanity: everything came to rest on the ground
+    assert np.all(got[:, 2] > 0.05) and np.all(got[:, 2] < 0.6)
+
+
+def test_gimbal_parity(gym):
+    """S2: the 3-DOF camera gimbal under random PD position targets."""
+    n, steps = 256, 60
+    sim, _ = scenes.gimbal_scene(gym, n)
+    gym.prepare_sim(sim)
+    _, rb, dof, _ = _tensors(gym, sim)
+    tg = scenes.gimbal_targets(n, steps, DEV, seed=3)
+    tg_h = tg.cpu().numpy()
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    ds = sim.model_arrays["dof_state0"].copy()
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+    for k in range(steps):
+        t = tg[k].contiguous()
+        assert gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(t))
+        gym.simulate(sim)
+        tgt[:, 0] = tg_h[k]
+        oracle.step(p, m, st, ds, tgt=tgt)
+    gym.refresh_dof_state_tensor(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    got_d = dof.cpu().numpy()
+    got = rb.cpu().numpy()
+    assert np.all(np.isfinite(got_d))
+    assert np.all(_close(got_d, ds)) and np.all(_close(got, st))
+    assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+
+
+def test_tensor_api_semantics(gym):
+    """acquire returns one persistent storage (test10 :372 vs :400); refresh
+    publishes the step; the _indexed setter touches only the listed actors; the
+    CPU pipeline (host tensors, test10's mode) gives the same numbers."""
+    n = 64
+    sims = {}
+    for gpu_pipe in (True, False):
+        sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=gpu_pipe)
+        gym.prepare_sim(sim)
+        t1 = gym.acquire_actor_root_state_tensor(sim)
+        t2 = gym.acquire_actor_root_state_tensor(sim)
+        assert t1.data_address == t2.data_address
+        root = gymtorch.wrap_tensor(t1)
+        assert root.data_ptr() == t1.data_address
+        assert root.device.type == ("cuda" if gpu_pipe else "cpu")
+        before = root.clone()
+        gym.simulate(sim)
+        assert torch.equal(root, before)        # not refreshed yet
+        gym.refresh_actor_root_state_tensor(sim)
+        assert not torch.equal(root, before)    # the vehicles fell
+        sims[gpu_pipe] = (sim, root)
+    assert np.array_equal(sims[True][1].cpu().numpy(), sims[False][1].numpy())
+
+    sim, root = sims[True]
+    gym.refresh_actor_root_state_tensor(sim)
+    new = root.clone()
+    new[:, 2] += 5.0
+    idx = torch.tensor([3, 10, 11], dtype=torch.int32, device=DEV)
+    assert gym.set_actor_root_state_tensor_indexed(sim, gymtorch.unwrap_tensor(new), gymtorch.unwrap_tensor(idx), 3)
+    expect = root.clone()
+    expect[idx.long()] = new[idx.long()]
+    gym.refresh_actor_root_state_tensor(sim)
+    assert torch.equal(root, expect)
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    assert dof.shape == (0, 2)
+    assert gym.refresh_dof_state_tensor(sim)
+
+
+def test_servo_4096_properties(gym):
+    """The bench workload (4096 envs): determinism across two sims, finite
+    state, unit quaternions, and the vehicles come to rest on the ground 15 s
+    after the random teleports stop."""
+    n = 4096
+    outs = []
+    for _ in range(2):
+        sim, _ = scenes.servo_scene(gym, n)
+        gym.prepare_sim(sim)
+        root, rb, _, _ = _tensors(gym, sim)
+        acts = scenes.servo_actions(n, 30, DEV, seed=4)
+        gym.refresh_actor_root_state_tensor(sim)
+        for k in range(30):
+            root[:, 3:10] = acts[k]
+            gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+            gym.simulate(sim)
+            gym.refresh_actor_root_state_tensor(sim)
+        for _ in range(900):
+            gym.simulate(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        outs.append(rb.cpu().numpy().copy())
+        gym.destroy_sim(sim)
+    a, b = outs
+    assert np.array_equal(a, b)
+    assert np.all(np.isfinite(a))
+    qn = np.linalg.norm(a[:, 3:7], axis=1)
+    assert np.all(np.abs(qn - 1) < 1e-5)
+    car = a[1::2]
+    # at rest on one of its faces (half extents 3.75 / 1.5 / 1.25 m)
+    assert np.all((car[:, 2] > 1.2) & (car[:, 2] < 3.8)), (car[:, 2].min(), car[:, 2].max())
+    assert np.all(np.abs(car[:, 7:10]) < 0.05), np.abs(car[:, 7:10]).max()
