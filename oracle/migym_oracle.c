@@ -84,10 +84,23 @@ static v3_t mv_(m3_t m, v3_t u) {
              m.c0.z * u.x + m.c1.z * u.y + m.c2.z * u.z);
 }
 static v3_t mtv_(m3_t m, v3_t v) { return V(dot3(m.c0, v), dot3(m.c1, v), dot3(m.c2, v)); }
-static v3_t invI_world(m3_t Rp, v3_t invI, v3_t v) {
-    v3_t u = mtv_(Rp, v);
-    u = V(u.x * invI.x, u.y * invI.y, u.z * invI.z);
-    return mv_(Rp, u);
+/* symmetric world inverse inertia: Rp diag(d) Rp^T */
+typedef struct { float xx, yy, zz, xy, xz, yz; } s3_t;
+static s3_t sym_rdrt_(m3_t Rp, v3_t d) {
+    v3_t u0 = mul3(Rp.c0, d.x), u1 = mul3(Rp.c1, d.y), u2 = mul3(Rp.c2, d.z);
+    s3_t s;
+    s.xx = u0.x * Rp.c0.x + u1.x * Rp.c1.x + u2.x * Rp.c2.x;
+    s.yy = u0.y * Rp.c0.y + u1.y * Rp.c1.y + u2.y * Rp.c2.y;
+    s.zz = u0.z * Rp.c0.z + u1.z * Rp.c1.z + u2.z * Rp.c2.z;
+    s.xy = u0.x * Rp.c0.y + u1.x * Rp.c1.y + u2.x * Rp.c2.y;
+    s.xz = u0.x * Rp.c0.z + u1.x * Rp.c1.z + u2.x * Rp.c2.z;
+    s.yz = u0.y * Rp.c0.z + u1.y * Rp.c1.z + u2.y * Rp.c2.z;
+    return s;
+}
+static v3_t symmul_(s3_t s, v3_t v) {
+    return V(s.xx * v.x + s.xy * v.y + s.xz * v.z,
+             s.xy * v.x + s.yy * v.y + s.yz * v.z,
+             s.xz * v.x + s.yz * v.y + s.zz * v.z);
 }
 /* sin/cos by Taylor + double angle */
 static void sincos_(float x, float* so, float* co) {
@@ -156,10 +169,10 @@ static step_t make_step_(const mg_sim_params* p) {
 
 /* ---- free body --------------------------------------- */
 typedef struct {
-    v3_t r; float s0, mu, e, kn, kt1, kt2; v3_t In, It1, It2; float ln, lt1, lt2, vn0;
+    v3_t r; float s0, mu, e, kn, kt1, kt2, ln, lt1, lt2, vn0;
 } slot_t;
 
-static void contact_normal(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float invm, float tgt) {
+static void contact_normal(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw, float tgt) {
     v3_t rn = cross3(c->r, P->n);
     float vn = dot3(P->n, *v) + dot3(*w, rn);
     float dl = c->kn * (tgt - vn);
@@ -167,10 +180,10 @@ static void contact_normal(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float i
     dl = nl - c->ln;
     c->ln = nl;
     *v = mad3(*v, P->n, dl * invm);
-    *w = mad3(*w, c->In, dl);
+    *w = mad3(*w, symmul_(*Iw, rn), dl);
 }
 
-static void contact_friction(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float invm) {
+static void contact_friction(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw) {
     v3_t r1 = cross3(c->r, P->t1), r2 = cross3(c->r, P->t2);
     float vt1 = dot3(P->t1, *v) + dot3(*w, r1);
     float vt2 = dot3(P->t2, *v) + dot3(*w, r2);
@@ -185,12 +198,15 @@ static void contact_friction(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float
     d1 = n1 - c->lt1; d2 = n2 - c->lt2;
     c->lt1 = n1; c->lt2 = n2;
     *v = mad3(mad3(*v, P->t1, d1 * invm), P->t2, d2 * invm);
-    *w = mad3(mad3(*w, c->It1, d1), c->It2, d2);
+    *w = mad3(mad3(*w, symmul_(*Iw, r1), d1), symmul_(*Iw, r2), d2);
 }
 
+/* candidates are held newest-first (slot 0 = latest accepted); at most OR_MAXC */
 static void push_(slot_t* sl, int* nc, v3_t r, float s0, float mu, float e) {
+    int j;
     if (*nc >= OR_MAXC) return;
-    sl[*nc].r = r; sl[*nc].s0 = s0; sl[*nc].mu = mu; sl[*nc].e = e;
+    for (j = *nc; j > 0; --j) sl[j] = sl[j - 1];
+    sl[0].r = r; sl[0].s0 = s0; sl[0].mu = mu; sl[0].e = e;
     *nc = *nc + 1;
 }
 
@@ -216,14 +232,14 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
     if (ext) { fext = V(ext[0], ext[1], ext[2]); text = V(ext[3], ext[4], ext[5]); }
     q = qnorm_(q);
     for (st_ = 0; st_ < P->substeps; ++st_) {
-        const m3_t Rp = qmat_(qmul_(q, iq));
+        const s3_t Iw = sym_rdrt_(qmat_(qmul_(q, iq)), invI);
         const v3_t xc = add3(x, qrot_(q, com));
         slot_t sl[OR_MAXC];
         int nc = 0, j, it;
         v3_t dx = V(0.0f, 0.0f, 0.0f), dth = V(0.0f, 0.0f, 0.0f);
         if (tf[4] != 0.0f) v = mad3(v, V(P->g[0], P->g[1], P->g[2]), h);
         v = mad3(v, fext, invm * h);
-        w = mad3(w, invI_world(Rp, invI, text), h);
+        w = mad3(w, symmul_(Iw, text), h);
         v = mul3(v, lin_keep);
         w = mul3(w, ang_keep);
         {
@@ -268,12 +284,9 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
         }
         for (j = 0; j < nc; ++j) {
             const v3_t rn = cross3(sl[j].r, P->n), r1 = cross3(sl[j].r, P->t1), r2 = cross3(sl[j].r, P->t2);
-            sl[j].In = invI_world(Rp, invI, rn);
-            sl[j].It1 = invI_world(Rp, invI, r1);
-            sl[j].It2 = invI_world(Rp, invI, r2);
-            sl[j].kn = 1.0f / (invm + dot3(rn, sl[j].In));
-            sl[j].kt1 = 1.0f / (invm + dot3(r1, sl[j].It1));
-            sl[j].kt2 = 1.0f / (invm + dot3(r2, sl[j].It2));
+            sl[j].kn = 1.0f / (invm + dot3(rn, symmul_(Iw, rn)));
+            sl[j].kt1 = 1.0f / (invm + dot3(r1, symmul_(Iw, r1)));
+            sl[j].kt2 = 1.0f / (invm + dot3(r2, symmul_(Iw, r2)));
             sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
             sl[j].vn0 = dot3(P->n, v) + dot3(w, rn);
         }
@@ -283,9 +296,9 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                 const float s = sl[j].s0 + dot3(P->n, dx) + dot3(dth, rn);
                 float tgt = -s * P->inv_sub;
                 if (s < 0.0f) tgt = fminf(tgt, P->maxdep);
-                contact_normal(P, &sl[j], &v, &w, invm, tgt);
+                contact_normal(P, &sl[j], &v, &w, invm, &Iw, tgt);
             }
-            for (j = 0; j < nc; ++j) contact_friction(P, &sl[j], &v, &w, invm);
+            for (j = 0; j < nc; ++j) contact_friction(P, &sl[j], &v, &w, invm, &Iw);
             dx = mad3(dx, v, P->sub);
             dth = mad3(dth, w, P->sub);
         }
@@ -295,9 +308,9 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                 const float s = sl[j].s0 + dot3(P->n, dx) + dot3(dth, rn);
                 float tgt = s > 0.0f ? -s * P->inv_h : 0.0f;
                 if (sl[j].e > 0.0f && sl[j].vn0 < -P->bounce) tgt = fmaxf(tgt, -sl[j].e * sl[j].vn0);
-                contact_normal(P, &sl[j], &v, &w, invm, tgt);
+                contact_normal(P, &sl[j], &v, &w, invm, &Iw, tgt);
             }
-            for (j = 0; j < nc; ++j) contact_friction(P, &sl[j], &v, &w, invm);
+            for (j = 0; j < nc; ++j) contact_friction(P, &sl[j], &v, &w, invm, &Iw);
         }
         for (j = 0; j < nc; ++j) {
             fsum = mad3(fsum, P->n, sl[j].ln);

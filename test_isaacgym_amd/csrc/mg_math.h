@@ -71,6 +71,26 @@ MG_HD V3 inv_inertia_w(M3 Rp, V3 invI, V3 v) {
     return mmul(Rp, u);
 }
 
+// symmetric 3x3 (world inverse inertia)
+struct S3 { float xx, yy, zz, xy, xz, yz; };
+// Rp diag(d) Rp^T, Rp given by its columns
+MG_HD S3 sym_rdrt(M3 Rp, V3 d) {
+    const V3 u0 = vscale(Rp.c0, d.x), u1 = vscale(Rp.c1, d.y), u2 = vscale(Rp.c2, d.z);
+    S3 s;
+    s.xx = u0.x * Rp.c0.x + u1.x * Rp.c1.x + u2.x * Rp.c2.x;
+    s.yy = u0.y * Rp.c0.y + u1.y * Rp.c1.y + u2.y * Rp.c2.y;
+    s.zz = u0.z * Rp.c0.z + u1.z * Rp.c1.z + u2.z * Rp.c2.z;
+    s.xy = u0.x * Rp.c0.y + u1.x * Rp.c1.y + u2.x * Rp.c2.y;
+    s.xz = u0.x * Rp.c0.z + u1.x * Rp.c1.z + u2.x * Rp.c2.z;
+    s.yz = u0.y * Rp.c0.z + u1.y * Rp.c1.z + u2.y * Rp.c2.z;
+    return s;
+}
+MG_HD V3 symmul(S3 s, V3 v) {
+    return v3(s.xx * v.x + s.xy * v.y + s.xz * v.z,
+              s.xy * v.x + s.yy * v.y + s.yz * v.z,
+              s.xz * v.x + s.yz * v.y + s.zz * v.z);
+}
+
 // sin / cos of a half angle by Taylor series on |x| <= 0.5 with double-angle
 // reconstruction: only + - * / so host and device round identically.
 MG_HD void mg_sincos(float x, float* s_out, float* c_out) {

@@ -21,28 +21,41 @@
 
 namespace {
 
+// 14 floats per contact slot: the world inverse inertia is one symmetric matrix
+// per substep, re-applied to (r x dir) in every row instead of being cached per
+// slot, which keeps the 8 slots in VGPRs (no scratch spills).
 struct Slot {
     V3 r;        // contact point - centre of mass (world)
     float s0;    // separation minus rest offset at substep start
     float mu, e; // combined friction / restitution
     float kn, kt1, kt2;   // effective masses
-    V3 In, It1, It2;      // world inverse inertia times (r x dir)
     float ln, lt1, lt2;   // accumulated impulses
     float vn0;            // pre-solve normal velocity (restitution)
 };
 
+// Insert a contact candidate at slot 0 and shift the others up (static indices
+// only: a select chain on `j == nc` is folded by the compiler into a dynamically
+// indexed store, which forces the slot array into scratch memory). Slots hold
+// the candidates newest-first; once MG_MAX_CONTACTS are held, later candidates
+// are dropped.
 __device__ __forceinline__ void push_candidate(Slot (&sl)[MG_MAX_CONTACTS], int& nc, V3 r, float s0,
                                                float mu, float e) {
+    if (nc >= MG_MAX_CONTACTS) return;
 #pragma unroll
-    for (int j = 0; j < MG_MAX_CONTACTS; ++j) {
-        if (j == nc) {
-            sl[j].r = r; sl[j].s0 = s0; sl[j].mu = mu; sl[j].e = e;
-        }
+    for (int j = MG_MAX_CONTACTS - 1; j > 0; --j) {
+        sl[j].r = sl[j - 1].r; sl[j].s0 = sl[j - 1].s0; sl[j].mu = sl[j - 1].mu; sl[j].e = sl[j - 1].e;
     }
-    if (nc < MG_MAX_CONTACTS) nc = nc + 1;
+    sl[0].r = r; sl[0].s0 = s0; sl[0].mu = mu; sl[0].e = e;
+    nc = nc + 1;
 }
 
-__device__ __forceinline__ void contact_normal(Slot& c, V3 n, V3& v, V3& w, float invm, float tgt) {
+// The empty asm makes the lever arm opaque to loop-invariant code motion, so
+// (r x n), Iw (r x n) ... are recomputed per row instead of being hoisted for all
+// 8 slots out of the iteration loop (which spilled 176 B/lane to scratch).
+#define MG_OPAQUE3(v) asm volatile("" : "+v"((v).x), "+v"((v).y), "+v"((v).z))
+
+__device__ __forceinline__ void contact_normal(Slot& c, V3 n, V3& v, V3& w, float invm, const S3& Iw, float tgt) {
+    MG_OPAQUE3(c.r);
     const V3 rn = vcross(c.r, n);
     const float vn = vdot(n, v) + vdot(w, rn);
     float dl = c.kn * (tgt - vn);
@@ -50,11 +63,12 @@ __device__ __forceinline__ void contact_normal(Slot& c, V3 n, V3& v, V3& w, floa
     dl = nl - c.ln;
     c.ln = nl;
     v = vmad(v, n, dl * invm);
-    w = vmad(w, c.In, dl);
+    w = vmad(w, symmul(Iw, rn), dl);
 }
 
 // Coulomb friction on a circular cone |lt| <= mu * ln
-__device__ __forceinline__ void contact_friction(Slot& c, V3 t1, V3 t2, V3& v, V3& w, float invm) {
+__device__ __forceinline__ void contact_friction(Slot& c, V3 t1, V3 t2, V3& v, V3& w, float invm, const S3& Iw) {
+    MG_OPAQUE3(c.r);
     const V3 r1 = vcross(c.r, t1);
     const V3 r2 = vcross(c.r, t2);
     const float vt1 = vdot(t1, v) + vdot(w, r1);
@@ -70,7 +84,7 @@ __device__ __forceinline__ void contact_friction(Slot& c, V3 t1, V3 t2, V3& v, V
     const float d1 = n1 - c.lt1, d2 = n2 - c.lt2;
     c.lt1 = n1; c.lt2 = n2;
     v = vmad(vmad(v, t1, d1 * invm), t2, d2 * invm);
-    w = vmad(vmad(w, c.It1, d1), c.It2, d2);
+    w = vmad(vmad(w, symmul(Iw, r1), d1), symmul(Iw, r2), d2);
 }
 
 __global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
@@ -119,13 +133,13 @@ __global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
     V3 fsum = v3(0.0f, 0.0f, 0.0f);
 
     for (int st = 0; st < P.substeps; ++st) {
-        const M3 Rp = qmat(qmul(q, iq));
+        const S3 Iw = sym_rdrt(qmat(qmul(q, iq)), invI);
         const V3 xc = vadd(x, qrot(q, com));
 
         // 1. unconstrained velocity
         if (grav_on != 0.0f) v = vmad(v, v3(P.g[0], P.g[1], P.g[2]), h);
         v = vmad(v, fext, invm * h);
-        w = vmad(w, inv_inertia_w(Rp, invI, text), h);
+        w = vmad(w, symmul(Iw, text), h);
         v = vscale(v, lin_keep);
         w = vscale(w, ang_keep);
         {
@@ -188,12 +202,9 @@ __global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
                 const V3 rn = vcross(sl[j].r, n);
                 const V3 r1 = vcross(sl[j].r, t1);
                 const V3 r2 = vcross(sl[j].r, t2);
-                sl[j].In = inv_inertia_w(Rp, invI, rn);
-                sl[j].It1 = inv_inertia_w(Rp, invI, r1);
-                sl[j].It2 = inv_inertia_w(Rp, invI, r2);
-                sl[j].kn = 1.0f / (invm + vdot(rn, sl[j].In));
-                sl[j].kt1 = 1.0f / (invm + vdot(r1, sl[j].It1));
-                sl[j].kt2 = 1.0f / (invm + vdot(r2, sl[j].It2));
+                sl[j].kn = 1.0f / (invm + vdot(rn, symmul(Iw, rn)));
+                sl[j].kt1 = 1.0f / (invm + vdot(r1, symmul(Iw, r1)));
+                sl[j].kt2 = 1.0f / (invm + vdot(r2, symmul(Iw, r2)));
                 sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
                 sl[j].vn0 = vdot(n, v) + vdot(w, rn);
             }
@@ -209,12 +220,12 @@ __global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
                     const float s = sl[j].s0 + vdot(n, dx) + vdot(dth, rn);
                     float tgt = -s * P.inv_sub;
                     if (s < 0.0f) tgt = fminf(tgt, P.max_depen);
-                    contact_normal(sl[j], n, v, w, invm, tgt);
+                    contact_normal(sl[j], n, v, w, invm, Iw, tgt);
                 }
             }
 #pragma unroll
             for (int j = 0; j < MG_MAX_CONTACTS; ++j)
-                if (j < nc) contact_friction(sl[j], t1, t2, v, w, invm);
+                if (j < nc) contact_friction(sl[j], t1, t2, v, w, invm, Iw);
             dx = vmad(dx, v, P.sub);
             dth = vmad(dth, w, P.sub);
         }
@@ -227,12 +238,12 @@ __global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
                     const float s = sl[j].s0 + vdot(n, dx) + vdot(dth, rn);
                     float tgt = s > 0.0f ? -s * P.inv_h : 0.0f;
                     if (sl[j].e > 0.0f && sl[j].vn0 < -P.bounce_thresh) tgt = fmaxf(tgt, -sl[j].e * sl[j].vn0);
-                    contact_normal(sl[j], n, v, w, invm, tgt);
+                    contact_normal(sl[j], n, v, w, invm, Iw, tgt);
                 }
             }
 #pragma unroll
             for (int j = 0; j < MG_MAX_CONTACTS; ++j)
-                if (j < nc) contact_friction(sl[j], t1, t2, v, w, invm);
+                if (j < nc) contact_friction(sl[j], t1, t2, v, w, invm, Iw);
         }
 #pragma unroll
         for (int j = 0; j < MG_MAX_CONTACTS; ++j) {

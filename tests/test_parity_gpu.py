@@ -192,9 +192,10 @@ def test_tensor_api_semantics(gym):
 
 
 def test_servo_4096_properties(gym):
-    """The bench workload (4096 envs): determinism across two sims, finite
-    state, unit quaternions, and the vehicles come to rest on the ground 15 s
-    after the random teleports stop."""
+    """The bench workload (4096 envs): 30 frames of random teleports, then every
+    root is stopped (v = w = 0) with the vehicles levelled; 15 s later the
+    vehicles rest flat on the ground (box proxy half-height 1.25 m). Two sims
+    must agree bit for bit; state stays finite with unit quaternions."""
     n = 4096
     outs = []
     for _ in range(2):
@@ -208,6 +209,9 @@ def test_servo_4096_properties(gym):
             gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
             gym.simulate(sim)
             gym.refresh_actor_root_state_tensor(sim)
+        root[:, 7:13] = 0.0
+        root[1::2, 3:7] = acts[29, 1::2, 0:4]          # vehicle: yaw-only attitude
+        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
         for _ in range(900):
             gym.simulate(sim)
         gym.refresh_rigid_body_state_tensor(sim)
@@ -219,6 +223,5 @@ def test_servo_4096_properties(gym):
     qn = np.linalg.norm(a[:, 3:7], axis=1)
     assert np.all(np.abs(qn - 1) < 1e-5)
     car = a[1::2]
-    # at rest on one of its faces (half extents 3.75 / 1.5 / 1.25 m)
-    assert np.all((car[:, 2] > 1.2) & (car[:, 2] < 3.8)), (car[:, 2].min(), car[:, 2].max())
-    assert np.all(np.abs(car[:, 7:10]) < 0.05), np.abs(car[:, 7:10]).max()
+    assert np.all(np.abs(car[:, 2] - 1.25) < 0.01), (car[:, 2].min(), car[:, 2].max())
+    assert np.all(np.abs(car[:, 7:10]) < 0.01), np.abs(car[:, 7:10]).max()
