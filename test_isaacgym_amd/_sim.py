@@ -66,8 +66,8 @@ class Actor:
         nd = asset.num_dofs
         self.dof_state = np.zeros((nd, 2), dtype=np.float32)
         self.dof_targets = np.zeros((nd, 3), dtype=np.float32)   # pos, vel, effort
-        self.shape_props = [_copy_shape_props(sp) for sp in asset.shape_props]
-        self.mass_props = list(asset.mass_props)
+        self.shape_props = asset.shape_props      # copy-on-write (set_actor_rigid_shape_properties)
+        self.mass_props = asset.mass_props        # copy-on-write (set_actor_rigid_body_properties)
         self.body_colors = {}
         self.scale = 1.0
 
@@ -176,9 +176,15 @@ class Sim:
     def actor_world_body_poses(self, a):
         """Initial world poses (p[3], q[4]) of an actor's bodies by forward kinematics."""
         asset = a.asset
-        root_p = a.env.origin + np.array([a.pose.p.x, a.pose.p.y, a.pose.p.z])
-        root_q = np.array([a.pose.r.x, a.pose.r.y, a.pose.r.z, a.pose.r.w])
-        root_q = root_q / np.linalg.norm(root_q)
+        o = a.env.origin
+        root_p = (o[0] + a.pose.p.x, o[1] + a.pose.p.y, o[2] + a.pose.p.z)
+        r = a.pose.r
+        nq = (r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w) ** 0.5
+        root_q = (r.x / nq, r.y / nq, r.z / nq, r.w / nq)
+        if not asset.joints:
+            return [root_p], [root_q]
+        root_p = np.array(root_p)
+        root_q = np.array(root_q)
         ps = [root_p]
         qs = [root_q]
         for k, j in enumerate(asset.joints):
@@ -214,50 +220,63 @@ class Sim:
         tb_key = {}
         artic, atmpl, lf, li = [], [], [], []
         atmpl_key = {}
+        blocks = {}        # per (asset, mass props, shape props): mass rows, kinds, template ids
         for a in self.actors:
             asset = a.asset
             opts = asset.options
-            root[a.global_index] = a.global_body
+            nba = a.num_bodies
+            g0 = a.global_body
+            root[a.global_index] = g0
             adof[a.global_index + 1] = a.global_dof + a.num_dofs
             ps, qs = self.actor_world_body_poses(a)
-            multi = len(asset.bodies) > 1
-            for b, body in enumerate(asset.bodies):
-                g = a.global_body + b
-                st[g, 0:3] = ps[b]
-                st[g, 3:7] = qs[b]
-                mp = a.mass_props[b]
-                invm, invI, iq = mp.principal()
-                mass[g, 0] = invm
-                mass[g, 1:4] = invI
-                mass[g, 4:8] = iq
-                mass[g, 8:11] = mp.com
-                mass[g, 11] = mp.mass
+            multi = nba > 1
+            for b in range(nba):
+                st[g0 + b, 0:3] = ps[b]
+                st[g0 + b, 3:7] = qs[b]
+            bkey = (id(asset), id(a.mass_props), id(a.shape_props))
+            blk = blocks.get(bkey)
+            if blk is None:
+                bm = np.zeros((nba, N.MG_MASS_N), dtype=np.float32)
+                bt = np.zeros(nba, dtype=np.int32)
+                for b, body in enumerate(asset.bodies):
+                    mp = a.mass_props[b]
+                    invm, invI, iq = mp.principal()
+                    bm[b, 0] = invm
+                    bm[b, 1:4] = invI
+                    bm[b, 4:8] = iq
+                    bm[b, 8:11] = mp.com
+                    bm[b, 11] = mp.mass
+                    # template body: asset body + its shape materials + body options
+                    sidx = sum(len(x.shapes) for x in asset.bodies[:b])
+                    mats = tuple((a.shape_props[sidx + k].friction, a.shape_props[sidx + k].restitution)
+                                 for k in range(len(body.shapes)))
+                    key = (id(asset), b, mats)
+                    if key not in tb_key:
+                        tb_key[key] = len(tbf)
+                        tbf.append([opts.linear_damping, opts.angular_damping, opts.max_linear_velocity,
+                                    opts.max_angular_velocity, 0.0 if opts.disable_gravity else 1.0, 0, 0, 0])
+                        tbi.append([len(shapes), len(body.shapes), 0, 0])
+                        for k, sh in enumerate(body.shapes):
+                            rec = np.zeros(N.MG_SHAPE_STRIDE, dtype=np.float32)
+                            rec[0] = sh.type
+                            rec[1:1 + len(sh.size)] = sh.size
+                            rec[4:7] = sh.p
+                            rec[7:11] = sh.q
+                            rec[11] = mats[k][0]
+                            rec[12] = mats[k][1]
+                            shapes.append(rec)
+                    bt[b] = tb_key[key]
                 if multi:
-                    kind[g] = N.MG_BODY_LINK
+                    bk = N.MG_BODY_LINK
                 elif opts.fix_base_link:
-                    kind[g] = N.MG_BODY_STATIC
+                    bk = N.MG_BODY_STATIC
                 else:
-                    kind[g] = N.MG_BODY_FREE
-                # template body: asset body + its shape materials + body options
-                sidx = sum(len(x.shapes) for x in asset.bodies[:b])
-                mats = tuple((a.shape_props[sidx + k].friction, a.shape_props[sidx + k].restitution)
-                             for k in range(len(body.shapes)))
-                key = (id(asset), b, mats)
-                if key not in tb_key:
-                    tb_key[key] = len(tbf)
-                    tbf.append([opts.linear_damping, opts.angular_damping, opts.max_linear_velocity,
-                                opts.max_angular_velocity, 0.0 if opts.disable_gravity else 1.0, 0, 0, 0])
-                    tbi.append([len(shapes), len(body.shapes), 0, 0])
-                    for k, s in enumerate(body.shapes):
-                        rec = np.zeros(N.MG_SHAPE_STRIDE, dtype=np.float32)
-                        rec[0] = s.type
-                        rec[1:1 + len(s.size)] = s.size
-                        rec[4:7] = s.p
-                        rec[7:11] = s.q
-                        rec[11] = mats[k][0]
-                        rec[12] = mats[k][1]
-                        shapes.append(rec)
-                btmpl[g] = tb_key[key]
+                    bk = N.MG_BODY_FREE
+                blk = blocks[bkey] = (bm, bt, bk)
+            bm, bt, bk = blk
+            mass[g0:g0 + nba] = bm
+            btmpl[g0:g0 + nba] = bt
+            kind[g0:g0 + nba] = bk
             for d in range(a.num_dofs):
                 gd = a.global_dof + d
                 dof0[gd] = a.dof_state[d]

@@ -645,18 +645,18 @@ class Gym:
             if recomputeInertia and mp.mass > 0:
                 I = mp.inertia * (p.mass / mp.mass)
             new.append(_assets.MassProps(p.mass, [p.com.x, p.com.y, p.com.z], I))
-        a.mass_props = new
+        a.mass_props = new          # a private list: the actor no longer shares the asset's
         return True
 
     def get_actor_rigid_shape_properties(self, env, handle):
-        return self._actor(env, handle).shape_props
+        return [_copy_shape(sp) for sp in self._actor(env, handle).shape_props]
 
     def set_actor_rigid_shape_properties(self, env, handle, props):
         a = self._actor(env, handle)
         if env.sim.finalized:
             print("*** migym: shape properties are frozen after prepare_sim", file=sys.stderr)
             return False
-        a.shape_props = list(props)
+        a.shape_props = [_copy_shape(sp) for sp in props]
         return True
 
     def set_rigid_body_color(self, env, handle, body_index, mesh_type, color):
@@ -1004,6 +1004,12 @@ def _look_at(pos, target):
     yaw = math.atan2(f.y, f.x)
     pitch = -math.asin(max(-1.0, min(1.0, f.z)))
     return Transform(pos, Quat.from_euler_zyx(0.0, pitch, yaw))
+
+
+def _copy_shape(sp):
+    c = _T.RigidShapeProperties()
+    c.__dict__.update(sp.__dict__)
+    return c
 
 
 def _copy_options(o):
