@@ -168,25 +168,38 @@ static step_t make_step_(const mg_sim_params* p) {
 }
 
 /* ---- free body --------------------------------------- */
+/* Ground basis: the general (n, t1, t2), or the +Z basis n = z, t1 = y, t2 = -x
+ * written out explicitly (as the device's BasisZ specialisation). */
+typedef struct { int upz; v3_t n, t1, t2; } basis_t;
+static float b_dn(const basis_t* B, v3_t v) { return B->upz ? v.z : dot3(B->n, v); }
+static float b_d1(const basis_t* B, v3_t v) { return B->upz ? v.y : dot3(B->t1, v); }
+static float b_d2(const basis_t* B, v3_t v) { return B->upz ? -v.x : dot3(B->t2, v); }
+static v3_t b_cn(const basis_t* B, v3_t r) { return B->upz ? V(r.y, -r.x, 0.0f) : cross3(r, B->n); }
+static v3_t b_c1(const basis_t* B, v3_t r) { return B->upz ? V(-r.z, 0.0f, r.x) : cross3(r, B->t1); }
+static v3_t b_c2(const basis_t* B, v3_t r) { return B->upz ? V(0.0f, -r.z, r.y) : cross3(r, B->t2); }
+static v3_t b_addn(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x, v.y, v.z + s) : mad3(v, B->n, s); }
+static v3_t b_add1(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x, v.y + s, v.z) : mad3(v, B->t1, s); }
+static v3_t b_add2(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x - s, v.y, v.z) : mad3(v, B->t2, s); }
+
 typedef struct {
-    v3_t r; float s0, mu, e, kn, kt1, kt2, ln, lt1, lt2, vn0;
+    v3_t r; float s0, mu, e, kn, kt1, kt2, ln, lt1, lt2, vn0; int on;
 } slot_t;
 
-static void contact_normal(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw, float tgt) {
-    v3_t rn = cross3(c->r, P->n);
-    float vn = dot3(P->n, *v) + dot3(*w, rn);
+static void contact_normal(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw, float tgt) {
+    v3_t rn = b_cn(B, c->r);
+    float vn = b_dn(B, *v) + dot3(*w, rn);
     float dl = c->kn * (tgt - vn);
     float nl = fmaxf(c->ln + dl, 0.0f);
     dl = nl - c->ln;
     c->ln = nl;
-    *v = mad3(*v, P->n, dl * invm);
+    *v = b_addn(B, *v, dl * invm);
     *w = mad3(*w, symmul_(*Iw, rn), dl);
 }
 
-static void contact_friction(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw) {
-    v3_t r1 = cross3(c->r, P->t1), r2 = cross3(c->r, P->t2);
-    float vt1 = dot3(P->t1, *v) + dot3(*w, r1);
-    float vt2 = dot3(P->t2, *v) + dot3(*w, r2);
+static void contact_friction(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw) {
+    v3_t r1 = b_c1(B, c->r), r2 = b_c2(B, c->r);
+    float vt1 = b_d1(B, *v) + dot3(*w, r1);
+    float vt2 = b_d2(B, *v) + dot3(*w, r2);
     float n1 = c->lt1 - c->kt1 * vt1;
     float n2 = c->lt2 - c->kt2 * vt2;
     float lim = c->mu * c->ln;
@@ -197,17 +210,55 @@ static void contact_friction(const step_t* P, slot_t* c, v3_t* v, v3_t* w, float
     }
     d1 = n1 - c->lt1; d2 = n2 - c->lt2;
     c->lt1 = n1; c->lt2 = n2;
-    *v = mad3(mad3(*v, P->t1, d1 * invm), P->t2, d2 * invm);
+    *v = b_add2(B, b_add1(B, *v, d1 * invm), d2 * invm);
     *w = mad3(mad3(*w, symmul_(*Iw, r1), d1), symmul_(*Iw, r2), d2);
 }
 
-/* candidates are held newest-first (slot 0 = latest accepted); at most OR_MAXC */
-static void push_(slot_t* sl, int* nc, v3_t r, float s0, float mu, float e) {
-    int j;
-    if (*nc >= OR_MAXC) return;
-    for (j = *nc; j > 0; --j) sl[j] = sl[j - 1];
-    sl[0].r = r; sl[0].s0 = s0; sl[0].mu = mu; sl[0].e = e;
-    *nc = *nc + 1;
+/* Contact candidates of one shape: (static index k, point, separation). */
+typedef struct { int k; v3_t p; float sep; } cand_t;
+static int shape_candidates(const step_t* P, const basis_t* B, const float* sh, q4_t q, v3_t x, cand_t* out,
+                            float* mu, float* e) {
+    const int type = (int)sh[0];
+    const q4_t qs = qmul_(q, Q(sh[7], sh[8], sh[9], sh[10]));
+    const v3_t cs = add3(x, qrot_(q, V(sh[4], sh[5], sh[6])));
+    int k, n = 0;
+    *mu = 0.5f * (sh[11] + P->mu_g);
+    *e = 0.5f * (sh[12] + P->e_g);
+    if (type == MG_SHAPE_BOX) {
+        /* the 4 corners of the face most opposed to n (first axis on ties) */
+        const m3_t Rs = qmat_(qs);
+        const float d0 = b_dn(B, Rs.c0), d1 = b_dn(B, Rs.c1), d2 = b_dn(B, Rs.c2);
+        const float ad0 = fabsf(d0), ad1 = fabsf(d1), ad2 = fabsf(d2);
+        const v3_t a0 = mul3(Rs.c0, sh[1]), a1 = mul3(Rs.c1, sh[2]), a2 = mul3(Rs.c2, sh[3]);
+        int ia = 0;
+        float best = ad0, di;
+        v3_t ai, e1, e2, u, cu;
+        if (ad1 > best) { ia = 1; best = ad1; }
+        if (ad2 > best) ia = 2;
+        di = ia == 0 ? d0 : (ia == 1 ? d1 : d2);
+        ai = ia == 0 ? a0 : (ia == 1 ? a1 : a2);
+        e1 = ia == 0 ? a1 : a0;
+        e2 = ia == 2 ? a1 : a2;
+        u = mul3(ai, di > 0.0f ? -1.0f : 1.0f);
+        cu = add3(cs, u);
+        for (k = 0; k < 4; ++k) {
+            const float sx = (k & 1) ? 1.0f : -1.0f;
+            const float sy = (k & 2) ? 1.0f : -1.0f;
+            const v3_t p = add3(add3(cu, mul3(e1, sx)), mul3(e2, sy));
+            out[n].k = k; out[n].p = p; out[n].sep = b_dn(B, p) + P->pd; n++;
+        }
+    } else if (type == MG_SHAPE_SPHERE) {
+        const float rad = sh[1];
+        out[n].k = 0; out[n].p = b_addn(B, cs, -rad); out[n].sep = b_dn(B, cs) + P->pd - rad; n++;
+    } else if (type == MG_SHAPE_CAPSULE) {
+        const float rad = sh[1];
+        const v3_t ax = mul3(qrot_(qs, V(1.0f, 0.0f, 0.0f)), sh[2]);
+        for (k = 0; k < 2; ++k) {
+            const v3_t c = k ? add3(cs, ax) : sub3(cs, ax);
+            out[n].k = k; out[n].p = b_addn(B, c, -rad); out[n].sep = b_dn(B, c) + P->pd - rad; n++;
+        }
+    }
+    return n;
 }
 
 static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st, const float* ext, float* cf) {
@@ -228,14 +279,18 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
     const float ang_keep = 1.0f - fminf(tf[1] * h, 1.0f);
     const float max_lv2 = tf[2] * tf[2], max_av2 = tf[3] * tf[3];
     v3_t fext = V(0.0f, 0.0f, 0.0f), text = V(0.0f, 0.0f, 0.0f), fsum = V(0.0f, 0.0f, 0.0f);
+    basis_t B;
     int s_, st_;
+    B.n = P->n; B.t1 = P->t1; B.t2 = P->t2;
+    B.upz = P->n.x == 0.0f && P->n.y == 0.0f && P->n.z == 1.0f && P->t1.x == 0.0f && P->t1.y == 1.0f &&
+            P->t1.z == 0.0f && P->t2.x == -1.0f && P->t2.y == 0.0f && P->t2.z == 0.0f;
     if (ext) { fext = V(ext[0], ext[1], ext[2]); text = V(ext[3], ext[4], ext[5]); }
     q = qnorm_(q);
     for (st_ = 0; st_ < P->substeps; ++st_) {
         const s3_t Iw = sym_rdrt_(qmat_(qmul_(q, iq)), invI);
         const v3_t xc = add3(x, qrot_(q, com));
         slot_t sl[OR_MAXC];
-        int nc = 0, j, it;
+        int j, it;
         v3_t dx = V(0.0f, 0.0f, 0.0f), dth = V(0.0f, 0.0f, 0.0f);
         if (tf[4] != 0.0f) v = mad3(v, V(P->g[0], P->g[1], P->g[2]), h);
         v = mad3(v, fext, invm * h);
@@ -248,74 +303,69 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
             w2 = dot3(w, w);
             if (w2 > max_av2) w = mul3(w, sqrtf(max_av2 / w2));
         }
+        for (j = 0; j < OR_MAXC; ++j) sl[j].on = 0;
         if (P->ground) {
+            int nc = 0;
             for (s_ = sh0; s_ < sh0 + nsh; ++s_) {
-                const float* sh = m->shapes + (size_t)s_ * MG_SHAPE_STRIDE;
-                const int type = (int)sh[0];
-                const q4_t qs = qmul_(q, Q(sh[7], sh[8], sh[9], sh[10]));
-                const v3_t cs = add3(x, qrot_(q, V(sh[4], sh[5], sh[6])));
-                const float mu = 0.5f * (sh[11] + P->mu_g);
-                const float e = 0.5f * (sh[12] + P->e_g);
-                if (type == MG_SHAPE_BOX) {
-                    const m3_t Rs = qmat_(qs);
-                    const v3_t a0 = mul3(Rs.c0, sh[1]), a1 = mul3(Rs.c1, sh[2]), a2 = mul3(Rs.c2, sh[3]);
-                    int k;
-                    for (k = 0; k < 8; ++k) {
-                        const float sx = (k & 1) ? 1.0f : -1.0f;
-                        const float sy = (k & 2) ? 1.0f : -1.0f;
-                        const float sz = (k & 4) ? 1.0f : -1.0f;
-                        const v3_t p = add3(add3(add3(cs, mul3(a0, sx)), mul3(a1, sy)), mul3(a2, sz));
-                        const float sep = dot3(P->n, p) + P->pd;
-                        if (sep < P->co) push_(sl, &nc, sub3(p, xc), sep - P->ro, mu, e);
-                    }
-                } else if (type == MG_SHAPE_SPHERE) {
-                    const float sep = dot3(P->n, cs) + P->pd - sh[1];
-                    if (sep < P->co) push_(sl, &nc, sub3(sub3(cs, mul3(P->n, sh[1])), xc), sep - P->ro, mu, e);
-                } else if (type == MG_SHAPE_CAPSULE) {
-                    const v3_t ax = mul3(qrot_(qs, V(1.0f, 0.0f, 0.0f)), sh[2]);
-                    int k;
-                    for (k = 0; k < 2; ++k) {
-                        const v3_t c = k ? add3(cs, ax) : sub3(cs, ax);
-                        const float sep = dot3(P->n, c) + P->pd - sh[1];
-                        if (sep < P->co) push_(sl, &nc, sub3(sub3(c, mul3(P->n, sh[1])), xc), sep - P->ro, mu, e);
+                cand_t cd[8];
+                float mu, e;
+                int k, n = shape_candidates(P, &B, m->shapes + (size_t)s_ * MG_SHAPE_STRIDE, q, x, cd, &mu, &e);
+                for (k = 0; k < n; ++k) {
+                    slot_t ns;
+                    if (!(cd[k].sep < P->co)) continue;
+                    ns.r = sub3(cd[k].p, xc); ns.s0 = cd[k].sep - P->ro; ns.mu = mu; ns.e = e; ns.on = 1;
+                    if (nsh == 1) {
+                        sl[cd[k].k] = ns;          /* static slot: candidate k -> slot k (of 4) */
+                    } else if (nc < OR_MAXC) {     /* shift register: newest in slot 0 */
+                        for (j = OR_MAXC - 1; j > 0; --j) sl[j] = sl[j - 1];
+                        sl[0] = ns;
+                        nc = nc + 1;
                     }
                 }
             }
         }
-        for (j = 0; j < nc; ++j) {
-            const v3_t rn = cross3(sl[j].r, P->n), r1 = cross3(sl[j].r, P->t1), r2 = cross3(sl[j].r, P->t2);
-            sl[j].kn = 1.0f / (invm + dot3(rn, symmul_(Iw, rn)));
-            sl[j].kt1 = 1.0f / (invm + dot3(r1, symmul_(Iw, r1)));
-            sl[j].kt2 = 1.0f / (invm + dot3(r2, symmul_(Iw, r2)));
-            sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
-            sl[j].vn0 = dot3(P->n, v) + dot3(w, rn);
+        for (j = 0; j < OR_MAXC; ++j) {
+            if (!sl[j].on) continue;
+            {
+                const v3_t rn = b_cn(&B, sl[j].r), r1 = b_c1(&B, sl[j].r), r2 = b_c2(&B, sl[j].r);
+                sl[j].kn = 1.0f / (invm + dot3(rn, symmul_(Iw, rn)));
+                sl[j].kt1 = 1.0f / (invm + dot3(r1, symmul_(Iw, r1)));
+                sl[j].kt2 = 1.0f / (invm + dot3(r2, symmul_(Iw, r2)));
+                sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
+                sl[j].vn0 = b_dn(&B, v) + dot3(w, rn);
+            }
         }
         for (it = 0; it < P->npos; ++it) {
-            for (j = 0; j < nc; ++j) {
-                const v3_t rn = cross3(sl[j].r, P->n);
-                const float s = sl[j].s0 + dot3(P->n, dx) + dot3(dth, rn);
-                float tgt = -s * P->inv_sub;
+            for (j = 0; j < OR_MAXC; ++j) {
+                float s, tgt;
+                if (!sl[j].on) continue;
+                s = sl[j].s0 + b_dn(&B, dx) + dot3(dth, b_cn(&B, sl[j].r));
+                tgt = -s * P->inv_sub;
                 if (s < 0.0f) tgt = fminf(tgt, P->maxdep);
-                contact_normal(P, &sl[j], &v, &w, invm, &Iw, tgt);
+                contact_normal(&B, &sl[j], &v, &w, invm, &Iw, tgt);
             }
-            for (j = 0; j < nc; ++j) contact_friction(P, &sl[j], &v, &w, invm, &Iw);
+            for (j = 0; j < OR_MAXC; ++j)
+                if (sl[j].on) contact_friction(&B, &sl[j], &v, &w, invm, &Iw);
             dx = mad3(dx, v, P->sub);
             dth = mad3(dth, w, P->sub);
         }
         for (it = 0; it < P->nvel; ++it) {
-            for (j = 0; j < nc; ++j) {
-                const v3_t rn = cross3(sl[j].r, P->n);
-                const float s = sl[j].s0 + dot3(P->n, dx) + dot3(dth, rn);
-                float tgt = s > 0.0f ? -s * P->inv_h : 0.0f;
+            for (j = 0; j < OR_MAXC; ++j) {
+                float s, tgt;
+                if (!sl[j].on) continue;
+                s = sl[j].s0 + b_dn(&B, dx) + dot3(dth, b_cn(&B, sl[j].r));
+                tgt = s > 0.0f ? -s * P->inv_h : 0.0f;
                 if (sl[j].e > 0.0f && sl[j].vn0 < -P->bounce) tgt = fmaxf(tgt, -sl[j].e * sl[j].vn0);
-                contact_normal(P, &sl[j], &v, &w, invm, &Iw, tgt);
+                contact_normal(&B, &sl[j], &v, &w, invm, &Iw, tgt);
             }
-            for (j = 0; j < nc; ++j) contact_friction(P, &sl[j], &v, &w, invm, &Iw);
+            for (j = 0; j < OR_MAXC; ++j)
+                if (sl[j].on) contact_friction(&B, &sl[j], &v, &w, invm, &Iw);
         }
-        for (j = 0; j < nc; ++j) {
-            fsum = mad3(fsum, P->n, sl[j].ln);
-            fsum = mad3(fsum, P->t1, sl[j].lt1);
-            fsum = mad3(fsum, P->t2, sl[j].lt2);
+        for (j = 0; j < OR_MAXC; ++j) {
+            if (!sl[j].on) continue;
+            fsum = b_addn(&B, fsum, sl[j].ln);
+            fsum = b_add1(&B, fsum, sl[j].lt1);
+            fsum = b_add2(&B, fsum, sl[j].lt2);
         }
         {
             const v3_t xc1 = add3(xc, dx);

@@ -11,7 +11,9 @@ import os
 import torch  # noqa: F401  -- load torch's HIP runtime first, so libmigym binds to the same one
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmigym.so")
+# MIGYM_LIB selects another build of the same library (kernel A/B experiments:
+# tools/kbench.py); the default is the in-tree libmigym.so.
+LIB_PATH = os.environ.get("MIGYM_LIB") or os.path.join(_HERE, "libmigym.so")
 
 MG_OK = 0
 MG_STATE_N = 13

@@ -34,6 +34,7 @@ struct MgStep {
 // Kernel argument block of the free-body step (SoA arrays, stride = nb).
 struct MgRigidArgs {
     int          nf;          // number of free bodies
+    int          nf1;         // of which single-shape (listed first in free_ids)
     int          nb;          // SoA stride (total bodies)
     const int*   free_ids;    // [nf] global body ids
     float*       state;       // [13][nb]

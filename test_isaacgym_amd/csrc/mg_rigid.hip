@@ -15,15 +15,50 @@
 // the two actors of an env do not collide, so lanes never communicate: no
 // atomics, no LDS, no grid sync. State is SoA [field][body] so every load and
 // store of a wavefront is one coalesced 256-B transaction per field.
-// The C restatement is oracle/migym_oracle.c:oracle_rigid_step.
+//
+// Issue-bound design notes (one wave per SIMD at 4096 envs, so the frame time
+// is the instruction stream of one wave):
+//   - a box contributes the 4 corners of its face most opposed to the ground
+//     normal; single-shape bodies (one launch) keep 4 static slots with the
+//     world-inertia products cached per slot, multi-shape bodies (a second
+//     launch) use 8 shift-register slots (static indices only);
+//   - the +Z ground (make_step's basis n = z, t1 = y, t2 = -x) is a template
+//     specialisation with the cross / dot products written out;
+//   - free bodies are ordered by template on upload, so bodies that are in the
+//     air (no contacts) and bodies on the ground fill different waves.
+// The C restatement is oracle/migym_oracle.c:rigid_body_step (same slot order,
+// same specialisation, same evaluation order).
 #include "mg_internal.h"
 #include "mg_math.h"
 
 namespace {
 
-// 14 floats per contact slot: the world inverse inertia is one symmetric matrix
-// per substep, re-applied to (r x dir) in every row instead of being cached per
-// slot, which keeps the 8 slots in VGPRs (no scratch spills).
+// ---- ground basis: general (n, t1, t2) or the +Z specialisation -----------
+struct BasisGen {
+    V3 n, t1, t2;
+    __device__ __forceinline__ float dn(V3 v) const { return vdot(n, v); }
+    __device__ __forceinline__ float d1(V3 v) const { return vdot(t1, v); }
+    __device__ __forceinline__ float d2(V3 v) const { return vdot(t2, v); }
+    __device__ __forceinline__ V3 cn(V3 r) const { return vcross(r, n); }
+    __device__ __forceinline__ V3 c1(V3 r) const { return vcross(r, t1); }
+    __device__ __forceinline__ V3 c2(V3 r) const { return vcross(r, t2); }
+    __device__ __forceinline__ V3 addn(V3 v, float s) const { return vmad(v, n, s); }
+    __device__ __forceinline__ V3 add1(V3 v, float s) const { return vmad(v, t1, s); }
+    __device__ __forceinline__ V3 add2(V3 v, float s) const { return vmad(v, t2, s); }
+};
+// n = (0,0,1), t1 = (0,1,0), t2 = (-1,0,0)
+struct BasisZ {
+    __device__ __forceinline__ float dn(V3 v) const { return v.z; }
+    __device__ __forceinline__ float d1(V3 v) const { return v.y; }
+    __device__ __forceinline__ float d2(V3 v) const { return -v.x; }
+    __device__ __forceinline__ V3 cn(V3 r) const { return v3(r.y, -r.x, 0.0f); }
+    __device__ __forceinline__ V3 c1(V3 r) const { return v3(-r.z, 0.0f, r.x); }
+    __device__ __forceinline__ V3 c2(V3 r) const { return v3(0.0f, -r.z, r.y); }
+    __device__ __forceinline__ V3 addn(V3 v, float s) const { return v3(v.x, v.y, v.z + s); }
+    __device__ __forceinline__ V3 add1(V3 v, float s) const { return v3(v.x, v.y + s, v.z); }
+    __device__ __forceinline__ V3 add2(V3 v, float s) const { return v3(v.x - s, v.y, v.z); }
+};
+
 struct Slot {
     V3 r;        // contact point - centre of mass (world)
     float s0;    // separation minus rest offset at substep start
@@ -31,48 +66,37 @@ struct Slot {
     float kn, kt1, kt2;   // effective masses
     float ln, lt1, lt2;   // accumulated impulses
     float vn0;            // pre-solve normal velocity (restitution)
+    V3 In, I1, I2;        // Iw (r x n), Iw (r x t1), Iw (r x t2): cached when CACHE
+    bool on;
 };
-
-// Insert a contact candidate at slot 0 and shift the others up (static indices
-// only: a select chain on `j == nc` is folded by the compiler into a dynamically
-// indexed store, which forces the slot array into scratch memory). Slots hold
-// the candidates newest-first; once MG_MAX_CONTACTS are held, later candidates
-// are dropped.
-__device__ __forceinline__ void push_candidate(Slot (&sl)[MG_MAX_CONTACTS], int& nc, V3 r, float s0,
-                                               float mu, float e) {
-    if (nc >= MG_MAX_CONTACTS) return;
-#pragma unroll
-    for (int j = MG_MAX_CONTACTS - 1; j > 0; --j) {
-        sl[j].r = sl[j - 1].r; sl[j].s0 = sl[j - 1].s0; sl[j].mu = sl[j - 1].mu; sl[j].e = sl[j - 1].e;
-    }
-    sl[0].r = r; sl[0].s0 = s0; sl[0].mu = mu; sl[0].e = e;
-    nc = nc + 1;
-}
 
 // The empty asm makes the lever arm opaque to loop-invariant code motion, so
 // (r x n), Iw (r x n) ... are recomputed per row instead of being hoisted for all
-// 8 slots out of the iteration loop (which spilled 176 B/lane to scratch).
+// 8 slots out of the iteration loop (which spilled to scratch).
 #define MG_OPAQUE3(v) asm volatile("" : "+v"((v).x), "+v"((v).y), "+v"((v).z))
 
-__device__ __forceinline__ void contact_normal(Slot& c, V3 n, V3& v, V3& w, float invm, const S3& Iw, float tgt) {
-    MG_OPAQUE3(c.r);
-    const V3 rn = vcross(c.r, n);
-    const float vn = vdot(n, v) + vdot(w, rn);
+template <bool CACHE, class B>
+__device__ __forceinline__ void contact_normal(const B& G, Slot& c, V3& v, V3& w, float invm, const S3& Iw,
+                                               float tgt) {
+    if (!CACHE) MG_OPAQUE3(c.r);
+    const V3 rn = G.cn(c.r);
+    const float vn = G.dn(v) + vdot(w, rn);
     float dl = c.kn * (tgt - vn);
     const float nl = fmaxf(c.ln + dl, 0.0f);
     dl = nl - c.ln;
     c.ln = nl;
-    v = vmad(v, n, dl * invm);
-    w = vmad(w, symmul(Iw, rn), dl);
+    v = G.addn(v, dl * invm);
+    w = vmad(w, CACHE ? c.In : symmul(Iw, rn), dl);
 }
 
 // Coulomb friction on a circular cone |lt| <= mu * ln
-__device__ __forceinline__ void contact_friction(Slot& c, V3 t1, V3 t2, V3& v, V3& w, float invm, const S3& Iw) {
-    MG_OPAQUE3(c.r);
-    const V3 r1 = vcross(c.r, t1);
-    const V3 r2 = vcross(c.r, t2);
-    const float vt1 = vdot(t1, v) + vdot(w, r1);
-    const float vt2 = vdot(t2, v) + vdot(w, r2);
+template <bool CACHE, class B>
+__device__ __forceinline__ void contact_friction(const B& G, Slot& c, V3& v, V3& w, float invm, const S3& Iw) {
+    if (!CACHE) MG_OPAQUE3(c.r);
+    const V3 r1 = G.c1(c.r);
+    const V3 r2 = G.c2(c.r);
+    const float vt1 = G.d1(v) + vdot(w, r1);
+    const float vt2 = G.d2(v) + vdot(w, r2);
     float n1 = c.lt1 - c.kt1 * vt1;
     float n2 = c.lt2 - c.kt2 * vt2;
     const float lim = c.mu * c.ln;
@@ -83,14 +107,65 @@ __device__ __forceinline__ void contact_friction(Slot& c, V3 t1, V3 t2, V3& v, V
     }
     const float d1 = n1 - c.lt1, d2 = n2 - c.lt2;
     c.lt1 = n1; c.lt2 = n2;
-    v = vmad(vmad(v, t1, d1 * invm), t2, d2 * invm);
-    w = vmad(vmad(w, symmul(Iw, r1), d1), symmul(Iw, r2), d2);
+    v = G.add2(G.add1(v, d1 * invm), d2 * invm);
+    w = vmad(vmad(w, CACHE ? c.I1 : symmul(Iw, r1), d1), CACHE ? c.I2 : symmul(Iw, r2), d2);
 }
 
-__global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= A.nf) return;
-    const int b = A.free_ids[i];
+// Candidates of one shape: emit(k, point, separation, mu, e) with k the static
+// candidate index within the shape (box corner bits zyx, capsule end 0/1).
+template <class B, class F>
+__device__ __forceinline__ void shape_candidates(const B& G, const MgStep& P, const float* sh, Q4 q, V3 x, F&& emit) {
+    const int type = (int)sh[0];
+    const Q4 qs = qmul(q, q4(sh[7], sh[8], sh[9], sh[10]));
+    const V3 cs = vadd(x, qrot(q, v3(sh[4], sh[5], sh[6])));
+    const float mu = 0.5f * (sh[11] + P.mu_ground);
+    const float e = 0.5f * (sh[12] + P.e_ground);
+    if (type == MG_SHAPE_BOX) {
+        // the face whose outward normal is most opposed to n: axis i* maximises
+        // |n . axis_i| (first index on ties), side s* = -sign(n . axis_i*); its 4
+        // corners are the candidates k = 0..3 (signs of the two other axes)
+        const M3 Rs = qmat(qs);
+        const float d0 = G.dn(Rs.c0), d1 = G.dn(Rs.c1), d2 = G.dn(Rs.c2);
+        const float ad0 = fabsf(d0), ad1 = fabsf(d1), ad2 = fabsf(d2);
+        int ia = 0;
+        float best = ad0;
+        if (ad1 > best) { ia = 1; best = ad1; }
+        if (ad2 > best) ia = 2;
+        const V3 a0 = vscale(Rs.c0, sh[1]);
+        const V3 a1 = vscale(Rs.c1, sh[2]);
+        const V3 a2 = vscale(Rs.c2, sh[3]);
+        const float di = ia == 0 ? d0 : (ia == 1 ? d1 : d2);
+        const V3 ai = ia == 0 ? a0 : (ia == 1 ? a1 : a2);
+        const V3 e1 = ia == 0 ? a1 : a0;
+        const V3 e2 = ia == 2 ? a1 : a2;
+        const V3 u = vscale(ai, di > 0.0f ? -1.0f : 1.0f);
+        const V3 cu = vadd(cs, u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float sx = (k & 1) ? 1.0f : -1.0f;
+            const float sy = (k & 2) ? 1.0f : -1.0f;
+            const V3 p = vadd(vadd(cu, vscale(e1, sx)), vscale(e2, sy));
+            emit(k, p, G.dn(p) + P.pd, mu, e);
+        }
+    } else if (type == MG_SHAPE_SPHERE) {
+        const float rad = sh[1];
+        emit(0, G.addn(cs, -rad), G.dn(cs) + P.pd - rad, mu, e);
+    } else if (type == MG_SHAPE_CAPSULE) {
+        const float rad = sh[1];
+        const V3 ax = vscale(qrot(qs, v3(1.0f, 0.0f, 0.0f)), sh[2]);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const V3 c = k ? vadd(cs, ax) : vsub(cs, ax);
+            emit(k, G.addn(c, -rad), G.dn(c) + P.pd - rad, mu, e);
+        }
+    }
+}
+
+// MULTI = false: bodies with one shape, static slots (candidate k -> slot k),
+// cached inertia vectors; MULTI = true: several shapes, shift-register slots.
+template <int MAXC, bool MULTI, class B>
+__device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const MgRigidArgs& A, int b) {
+    constexpr bool CACHE = !MULTI;
     const int nb = A.nb;
     float* S = A.state;
 
@@ -120,9 +195,6 @@ __global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
         text = v3(A.ext[3 * nb + b], A.ext[4 * nb + b], A.ext[5 * nb + b]);
     }
 
-    const V3 n = v3(P.n[0], P.n[1], P.n[2]);
-    const V3 t1 = v3(P.t1[0], P.t1[1], P.t1[2]);
-    const V3 t2 = v3(P.t2[0], P.t2[1], P.t2[2]);
     const float h = P.h;
     const float lin_keep = 1.0f - fminf(lin_damp * h, 1.0f);
     const float ang_keep = 1.0f - fminf(ang_damp * h, 1.0f);
@@ -150,63 +222,58 @@ __global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
         }
 
         // 2. contacts against the ground plane
-        Slot sl[MG_MAX_CONTACTS];
-        int nc = 0;
+        Slot sl[MAXC];
+#pragma unroll
+        for (int j = 0; j < MAXC; ++j) sl[j].on = false;
         if (P.has_ground) {
-            for (int s = sh0; s < sh0 + nsh; ++s) {
-                const float* sh = A.shapes + s * MG_SHAPE_STRIDE;
-                const int type = (int)sh[0];
-                const Q4 qs = qmul(q, q4(sh[7], sh[8], sh[9], sh[10]));
-                const V3 cs = vadd(x, qrot(q, v3(sh[4], sh[5], sh[6])));
-                const float mu = 0.5f * (sh[11] + P.mu_ground);
-                const float e = 0.5f * (sh[12] + P.e_ground);
-                if (type == MG_SHAPE_BOX) {
-                    const M3 Rs = qmat(qs);
-                    const V3 a0 = vscale(Rs.c0, sh[1]);
-                    const V3 a1 = vscale(Rs.c1, sh[2]);
-                    const V3 a2 = vscale(Rs.c2, sh[3]);
+            if constexpr (!MULTI) {
+                // static slots: candidate k of the only shape lives in slot k
+                if (nsh == 1)
+                shape_candidates(G, P, A.shapes + sh0 * MG_SHAPE_STRIDE, q, x,
+                                 [&](int k, V3 p, float sep, float mu, float e) {
+                                     if (sep < P.contact_offset) {
+                                         sl[k].on = true;
+                                         sl[k].r = vsub(p, xc);
+                                         sl[k].s0 = sep - P.rest_offset;
+                                         sl[k].mu = mu;
+                                         sl[k].e = e;
+                                     }
+                                 });
+            } else {
+                // several shapes: shift-register insert, newest candidate in slot 0
+                int nc = 0;
+                for (int s = sh0; s < sh0 + nsh; ++s) {
+                    shape_candidates(G, P, A.shapes + s * MG_SHAPE_STRIDE, q, x,
+                                     [&](int, V3 p, float sep, float mu, float e) {
+                                         if (sep < P.contact_offset && nc < MAXC) {
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const float sx = (k & 1) ? 1.0f : -1.0f;
-                        const float sy = (k & 2) ? 1.0f : -1.0f;
-                        const float sz = (k & 4) ? 1.0f : -1.0f;
-                        const V3 p = vadd(vadd(vadd(cs, vscale(a0, sx)), vscale(a1, sy)), vscale(a2, sz));
-                        const float sep = vdot(n, p) + P.pd;
-                        if (sep < P.contact_offset)
-                            push_candidate(sl, nc, vsub(p, xc), sep - P.rest_offset, mu, e);
-                    }
-                } else if (type == MG_SHAPE_SPHERE) {
-                    const float sep = vdot(n, cs) + P.pd - sh[1];
-                    if (sep < P.contact_offset) {
-                        const V3 p = vsub(cs, vscale(n, sh[1]));
-                        push_candidate(sl, nc, vsub(p, xc), sep - P.rest_offset, mu, e);
-                    }
-                } else if (type == MG_SHAPE_CAPSULE) {
-                    const V3 ax = vscale(qrot(qs, v3(1.0f, 0.0f, 0.0f)), sh[2]);
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        const V3 c = k ? vadd(cs, ax) : vsub(cs, ax);
-                        const float sep = vdot(n, c) + P.pd - sh[1];
-                        if (sep < P.contact_offset) {
-                            const V3 p = vsub(c, vscale(n, sh[1]));
-                            push_candidate(sl, nc, vsub(p, xc), sep - P.rest_offset, mu, e);
-                        }
-                    }
+                                             for (int j = MAXC - 1; j > 0; --j) {
+                                                 sl[j].r = sl[j - 1].r; sl[j].s0 = sl[j - 1].s0;
+                                                 sl[j].mu = sl[j - 1].mu; sl[j].e = sl[j - 1].e;
+                                                 sl[j].on = sl[j - 1].on;
+                                             }
+                                             sl[0].r = vsub(p, xc); sl[0].s0 = sep - P.rest_offset;
+                                             sl[0].mu = mu; sl[0].e = e; sl[0].on = true;
+                                             nc = nc + 1;
+                                         }
+                                     });
                 }
             }
         }
         // contact constants
 #pragma unroll
-        for (int j = 0; j < MG_MAX_CONTACTS; ++j) {
-            if (j < nc) {
-                const V3 rn = vcross(sl[j].r, n);
-                const V3 r1 = vcross(sl[j].r, t1);
-                const V3 r2 = vcross(sl[j].r, t2);
-                sl[j].kn = 1.0f / (invm + vdot(rn, symmul(Iw, rn)));
-                sl[j].kt1 = 1.0f / (invm + vdot(r1, symmul(Iw, r1)));
-                sl[j].kt2 = 1.0f / (invm + vdot(r2, symmul(Iw, r2)));
+        for (int j = 0; j < MAXC; ++j) {
+            if (sl[j].on) {
+                const V3 rn = G.cn(sl[j].r);
+                const V3 r1 = G.c1(sl[j].r);
+                const V3 r2 = G.c2(sl[j].r);
+                const V3 In = symmul(Iw, rn), I1 = symmul(Iw, r1), I2 = symmul(Iw, r2);
+                if (CACHE) { sl[j].In = In; sl[j].I1 = I1; sl[j].I2 = I2; }
+                sl[j].kn = 1.0f / (invm + vdot(rn, In));
+                sl[j].kt1 = 1.0f / (invm + vdot(r1, I1));
+                sl[j].kt2 = 1.0f / (invm + vdot(r2, I2));
                 sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
-                sl[j].vn0 = vdot(n, v) + vdot(w, rn);
+                sl[j].vn0 = G.dn(v) + vdot(w, rn);
             }
         }
 
@@ -214,43 +281,41 @@ __global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
         V3 dx = v3(0.0f, 0.0f, 0.0f), dth = v3(0.0f, 0.0f, 0.0f);
         for (int it = 0; it < P.npos; ++it) {
 #pragma unroll
-            for (int j = 0; j < MG_MAX_CONTACTS; ++j) {
-                if (j < nc) {
-                    const V3 rn = vcross(sl[j].r, n);
-                    const float s = sl[j].s0 + vdot(n, dx) + vdot(dth, rn);
+            for (int j = 0; j < MAXC; ++j) {
+                if (sl[j].on) {
+                    const float s = sl[j].s0 + G.dn(dx) + vdot(dth, G.cn(sl[j].r));
                     float tgt = -s * P.inv_sub;
                     if (s < 0.0f) tgt = fminf(tgt, P.max_depen);
-                    contact_normal(sl[j], n, v, w, invm, Iw, tgt);
+                    contact_normal<CACHE>(G, sl[j], v, w, invm, Iw, tgt);
                 }
             }
 #pragma unroll
-            for (int j = 0; j < MG_MAX_CONTACTS; ++j)
-                if (j < nc) contact_friction(sl[j], t1, t2, v, w, invm, Iw);
+            for (int j = 0; j < MAXC; ++j)
+                if (sl[j].on) contact_friction<CACHE>(G, sl[j], v, w, invm, Iw);
             dx = vmad(dx, v, P.sub);
             dth = vmad(dth, w, P.sub);
         }
         // velocity iterations (bias removed)
         for (int it = 0; it < P.nvel; ++it) {
 #pragma unroll
-            for (int j = 0; j < MG_MAX_CONTACTS; ++j) {
-                if (j < nc) {
-                    const V3 rn = vcross(sl[j].r, n);
-                    const float s = sl[j].s0 + vdot(n, dx) + vdot(dth, rn);
+            for (int j = 0; j < MAXC; ++j) {
+                if (sl[j].on) {
+                    const float s = sl[j].s0 + G.dn(dx) + vdot(dth, G.cn(sl[j].r));
                     float tgt = s > 0.0f ? -s * P.inv_h : 0.0f;
                     if (sl[j].e > 0.0f && sl[j].vn0 < -P.bounce_thresh) tgt = fmaxf(tgt, -sl[j].e * sl[j].vn0);
-                    contact_normal(sl[j], n, v, w, invm, Iw, tgt);
+                    contact_normal<CACHE>(G, sl[j], v, w, invm, Iw, tgt);
                 }
             }
 #pragma unroll
-            for (int j = 0; j < MG_MAX_CONTACTS; ++j)
-                if (j < nc) contact_friction(sl[j], t1, t2, v, w, invm, Iw);
+            for (int j = 0; j < MAXC; ++j)
+                if (sl[j].on) contact_friction<CACHE>(G, sl[j], v, w, invm, Iw);
         }
 #pragma unroll
-        for (int j = 0; j < MG_MAX_CONTACTS; ++j) {
-            if (j < nc) {
-                fsum = vmad(fsum, n, sl[j].ln);
-                fsum = vmad(fsum, t1, sl[j].lt1);
-                fsum = vmad(fsum, t2, sl[j].lt2);
+        for (int j = 0; j < MAXC; ++j) {
+            if (sl[j].on) {
+                fsum = G.addn(fsum, sl[j].ln);
+                fsum = G.add1(fsum, sl[j].lt1);
+                fsum = G.add2(fsum, sl[j].lt2);
             }
         }
 
@@ -269,11 +334,47 @@ __global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
     A.cforce[2 * nb + b] = fsum.z * P.inv_dt;
 }
 
+template <bool UPZ, int MAXC, bool MULTI>
+__global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= A.nf) return;
+    const int b = A.free_ids[i];
+    if constexpr (UPZ) {
+        rigid_body<MAXC, MULTI>(BasisZ{}, P, A, b);
+    } else {
+        BasisGen G;
+        G.n = v3(P.n[0], P.n[1], P.n[2]);
+        G.t1 = v3(P.t1[0], P.t1[1], P.t1[2]);
+        G.t2 = v3(P.t2[0], P.t2[1], P.t2[2]);
+        rigid_body<MAXC, MULTI>(G, P, A, b);
+    }
+}
+
 }  // namespace
 
+bool mg_step_is_upz(const MgStep& P) {
+    return P.n[0] == 0.0f && P.n[1] == 0.0f && P.n[2] == 1.0f && P.t1[0] == 0.0f && P.t1[1] == 1.0f &&
+           P.t1[2] == 0.0f && P.t2[0] == -1.0f && P.t2[1] == 0.0f && P.t2[2] == 0.0f;
+}
+
+// A.free_ids lists the single-shape bodies first (A.nf1 of them), then the
+// multi-shape ones; each group is its own launch.
 hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream_t s) {
     if (A.nf <= 0) return hipSuccess;
-    const int blocks = (A.nf + 63) / 64;
-    hipLaunchKernelGGL(k_rigid_step, dim3(blocks), dim3(64), 0, s, P, A);
+    const bool upz = mg_step_is_upz(P);
+    MgRigidArgs A1 = A, A2 = A;
+    A1.nf = A.nf1;
+    A2.nf = A.nf - A.nf1;
+    A2.free_ids = A.free_ids + A.nf1;
+    if (A1.nf > 0) {
+        const int blocks = (A1.nf + 63) / 64;
+        if (upz) hipLaunchKernelGGL((k_rigid_step<true, 4, false>), dim3(blocks), dim3(64), 0, s, P, A1);
+        else hipLaunchKernelGGL((k_rigid_step<false, 4, false>), dim3(blocks), dim3(64), 0, s, P, A1);
+    }
+    if (A2.nf > 0) {
+        const int blocks = (A2.nf + 63) / 64;
+        if (upz) hipLaunchKernelGGL((k_rigid_step<true, MG_MAX_CONTACTS, true>), dim3(blocks), dim3(64), 0, s, P, A2);
+        else hipLaunchKernelGGL((k_rigid_step<false, MG_MAX_CONTACTS, true>), dim3(blocks), dim3(64), 0, s, P, A2);
+    }
     return hipGetLastError();
 }

@@ -66,6 +66,7 @@ struct mg_sim {
 
     int nenv = 0, na = 0, nb = 0, nd = 0, ntb = 0, ns = 0, nf = 0, nartic = 0, ntl = 0;
     int max_actor_dofs = 0;
+    int nf1 = 0;   // single-shape free bodies (first in d_free)
 
     float* d_state = nullptr;     // [13][nb]
     float* d_mass = nullptr;      // [12][nb]
@@ -291,9 +292,20 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     }
     if (na > 0 && (m->actor_dof[0] != 0 || m->actor_dof[na] != nd)) return fail(MG_ERR_ARG, "actor_dof must span [0, num_dofs]");
 
+    // free bodies ordered by template body (stable): bodies of one kind share
+    // waves, so e.g. the servo scene's airborne UAVs and grounded vehicles do
+    // not interleave lane by lane (results do not depend on the order)
     std::vector<int> free_ids;
     for (int b = 0; b < nb; ++b)
         if (m->body_kind[b] == MG_BODY_FREE) free_ids.push_back(b);
+    auto nshapes = [m](int b) { return m->tmpl_body_i[m->body_tmpl[b] * MG_TBODY_I_N + 1]; };
+    std::stable_sort(free_ids.begin(), free_ids.end(), [&](int a, int b) {
+        const bool ma = nshapes(a) > 1, mb = nshapes(b) > 1;   // single-shape bodies first
+        if (ma != mb) return !ma;
+        return m->body_tmpl[a] < m->body_tmpl[b];
+    });
+    s->nf1 = 0;
+    for (int b : free_ids) s->nf1 += nshapes(b) <= 1 ? 1 : 0;
     s->nf = (int)free_ids.size();
 
     // articulation instances grouped by template
@@ -408,7 +420,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     }
     if (s->nf > 0) {
         MgRigidArgs A{};
-        A.nf = s->nf; A.nb = s->nb; A.free_ids = s->d_free;
+        A.nf = s->nf; A.nf1 = s->nf1; A.nb = s->nb; A.free_ids = s->d_free;
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
         A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
