@@ -196,22 +196,24 @@ static void contact_normal(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, float 
     *w = mad3(*w, symmul_(*Iw, rn), dl);
 }
 
+/* PhysX-style pyramid friction: tangent rows one after the other, each
+ * accumulated impulse clamped to [-mu ln, mu ln] */
 static void contact_friction(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw) {
-    v3_t r1 = b_c1(B, c->r), r2 = b_c2(B, c->r);
-    float vt1 = b_d1(B, *v) + dot3(*w, r1);
-    float vt2 = b_d2(B, *v) + dot3(*w, r2);
-    float n1 = c->lt1 - c->kt1 * vt1;
-    float n2 = c->lt2 - c->kt2 * vt2;
-    float lim = c->mu * c->ln;
-    float m2 = n1 * n1 + n2 * n2, d1, d2;
-    if (m2 > lim * lim) {
-        float sc = lim / sqrtf(m2);
-        n1 = n1 * sc; n2 = n2 * sc;
-    }
-    d1 = n1 - c->lt1; d2 = n2 - c->lt2;
-    c->lt1 = n1; c->lt2 = n2;
-    *v = b_add2(B, b_add1(B, *v, d1 * invm), d2 * invm);
-    *w = mad3(mad3(*w, symmul_(*Iw, r1), d1), symmul_(*Iw, r2), d2);
+    const float lim = c->mu * c->ln;
+    v3_t r1 = b_c1(B, c->r), r2;
+    float vt1 = b_d1(B, *v) + dot3(*w, r1), vt2, n1, n2, d1, d2;
+    n1 = fminf(fmaxf(c->lt1 - c->kt1 * vt1, -lim), lim);
+    d1 = n1 - c->lt1;
+    c->lt1 = n1;
+    *v = b_add1(B, *v, d1 * invm);
+    *w = mad3(*w, symmul_(*Iw, r1), d1);
+    r2 = b_c2(B, c->r);
+    vt2 = b_d2(B, *v) + dot3(*w, r2);
+    n2 = fminf(fmaxf(c->lt2 - c->kt2 * vt2, -lim), lim);
+    d2 = n2 - c->lt2;
+    c->lt2 = n2;
+    *v = b_add2(B, *v, d2 * invm);
+    *w = mad3(*w, symmul_(*Iw, r2), d2);
 }
 
 /* Contact candidates of one shape: (static index k, point, separation). */

@@ -8,7 +8,7 @@
 //      capsule end caps within contact_offset), at most MG_MAX_CONTACTS slots;
 //   3. TGS: npos position iterations of length h/npos, each a Gauss-Seidel pass
 //      over the normal rows (speculative / depenetration target) then over the
-//      friction rows (Coulomb, circular cone), followed by integrating the
+//      friction rows (Coulomb pyramid, PhysX-style), followed by integrating the
 //      body's motion delta; then nvel velocity iterations with the bias removed;
 //   4. pose update: com += sum of iteration deltas, q = exp(dtheta) q.
 // Envs are independent and (test10_servo_vecenv.py:317,323: group=i, filter=-1)
@@ -89,26 +89,27 @@ __device__ __forceinline__ void contact_normal(const B& G, Slot& c, V3& v, V3& w
     w = vmad(w, CACHE ? c.In : symmul(Iw, rn), dl);
 }
 
-// Coulomb friction on a circular cone |lt| <= mu * ln
+// Coulomb friction, PhysX-style pyramid: the two tangent rows are solved one
+// after the other, each accumulated impulse clamped to [-mu ln, mu ln]
+// (no sqrt / divide on the Gauss-Seidel chain).
 template <bool CACHE, class B>
 __device__ __forceinline__ void contact_friction(const B& G, Slot& c, V3& v, V3& w, float invm, const S3& Iw) {
     if (!CACHE) MG_OPAQUE3(c.r);
-    const V3 r1 = G.c1(c.r);
-    const V3 r2 = G.c2(c.r);
-    const float vt1 = G.d1(v) + vdot(w, r1);
-    const float vt2 = G.d2(v) + vdot(w, r2);
-    float n1 = c.lt1 - c.kt1 * vt1;
-    float n2 = c.lt2 - c.kt2 * vt2;
     const float lim = c.mu * c.ln;
-    const float m2 = n1 * n1 + n2 * n2;
-    if (m2 > lim * lim) {
-        const float sc = lim / sqrtf(m2);
-        n1 = n1 * sc; n2 = n2 * sc;
-    }
-    const float d1 = n1 - c.lt1, d2 = n2 - c.lt2;
-    c.lt1 = n1; c.lt2 = n2;
-    v = G.add2(G.add1(v, d1 * invm), d2 * invm);
-    w = vmad(vmad(w, CACHE ? c.I1 : symmul(Iw, r1), d1), CACHE ? c.I2 : symmul(Iw, r2), d2);
+    const V3 r1 = G.c1(c.r);
+    const float vt1 = G.d1(v) + vdot(w, r1);
+    const float n1 = fminf(fmaxf(c.lt1 - c.kt1 * vt1, -lim), lim);
+    const float d1 = n1 - c.lt1;
+    c.lt1 = n1;
+    v = G.add1(v, d1 * invm);
+    w = vmad(w, CACHE ? c.I1 : symmul(Iw, r1), d1);
+    const V3 r2 = G.c2(c.r);
+    const float vt2 = G.d2(v) + vdot(w, r2);
+    const float n2 = fminf(fmaxf(c.lt2 - c.kt2 * vt2, -lim), lim);
+    const float d2 = n2 - c.lt2;
+    c.lt2 = n2;
+    v = G.add2(v, d2 * invm);
+    w = vmad(w, CACHE ? c.I2 : symmul(Iw, r2), d2);
 }
 
 // Candidates of one shape: emit(k, point, separation, mu, e) with k the static
