@@ -38,7 +38,7 @@ sys.path.insert(0, ROOT)
 
 from isaacgym import gymapi, gymtorch  # noqa: E402
 from test_isaacgym_amd import _native as N  # noqa: E402
-from test_isaacgym_amd import scenes  # noqa: E402
+from test_isaacgym_amd import scenes, sharding  # noqa: E402
 
 METRIC = "env-steps/sec (whole node), 4096 servo envs; 1/2/4/8-GPU scaling"
 ENVS_PER_GPU = 4096
@@ -105,15 +105,15 @@ def main():
 
     gym = gymapi.acquire_gym()
     n = args.envs
-    sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=local)
+    # rank k owns global envs [k n, (k+1) n), placed at their global grid cells
+    sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=local, env_offset=rank * n,
+                                grid_envs=world * n)
     gym.prepare_sim(sim)
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     gym.acquire_rigid_body_state_tensor(sim)
     gym.acquire_dof_state_tensor(sim)
     acts = scenes.servo_actions(n, 64, dev, seed=rank)
-    gathered = None
-    if args.allgather and world > 1:
-        gathered = torch.empty((world,) + tuple(root.shape), dtype=root.dtype, device=dev)
+    gathered = args.allgather and world > 1
 
     def step(k):
         root[:, 3:10] = acts[k % acts.shape[0]]
@@ -123,8 +123,8 @@ def main():
         gym.refresh_actor_root_state_tensor(sim)
         gym.refresh_rigid_body_state_tensor(sim)
         gym.refresh_dof_state_tensor(sim)
-        if gathered is not None:
-            dist.all_gather_into_tensor(gathered, root)
+        if gathered:
+            sharding.all_gather_rows(root)      # RCCL over xGMI: (world * 2n, 13) observation
 
     gym.refresh_actor_root_state_tensor(sim)
     for k in range(args.warmup):
@@ -179,7 +179,7 @@ def main():
                 "envs_per_gpu": n,
                 "global_envs": world * n,
                 "parallelism": "env-sharded, one process per GPU%s" % (", RCCL all-gather of root state"
-                                                                        if gathered is not None else
+                                                                        if gathered else
                                                                         ", no collectives"),
             },
             "roofline": {

@@ -31,8 +31,9 @@ class Env:
         self.lower = lower
         self.upper = upper
         self.per_row = max(int(per_row), 1)
-        col = index % self.per_row
-        row = index // self.per_row
+        g = index + sim.env_offset           # grid cell of the global env index (sharded sims)
+        col = g % self.per_row
+        row = g // self.per_row
         dx = upper.x - lower.x
         if sim.params.up_axis == T.UP_AXIS_Z:
             self.origin = np.array([col * dx, row * (upper.y - lower.y), 0.0])
@@ -117,6 +118,7 @@ class Sim:
         self.engine = engine
         self.params = params
         self.plane = None
+        self.env_offset = 0        # global index of this sim's first env (sharding.shard_sim)
         self.envs = []
         self.assets = []
         self.finalized = False

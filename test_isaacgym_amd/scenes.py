@@ -38,9 +38,12 @@ def servo_sim_params(use_gpu_pipeline=True):
 
 
 def servo_scene(gym, num_envs, use_gpu_pipeline=True, device=0, uav_height=102.0, asset_root=None,
-                asset_files=("servo/uav.urdf", "servo/ground_vehicle.urdf")):
-    """Returns (sim, envs). Actor rows alternate UAV, vehicle (test10 :373-374)."""
+                asset_files=("servo/uav.urdf", "servo/ground_vehicle.urdf"), env_offset=0, grid_envs=None):
+    """Returns (sim, envs). Actor rows alternate UAV, vehicle (test10 :373-374).
+    env_offset / grid_envs: this sim holds envs [env_offset, env_offset +
+    num_envs) of a grid laid out for grid_envs envs (sharding.py)."""
     sim = gym.create_sim(device, device, gymapi.SIM_PHYSX, servo_sim_params(use_gpu_pipeline))
+    sim.env_offset = env_offset
     plane = gymapi.PlaneParams()
     plane.normal = gymapi.Vec3(0, 0, 1)
     plane.distance = 0
@@ -57,7 +60,7 @@ def servo_scene(gym, num_envs, use_gpu_pipeline=True, device=0, uav_height=102.0
         if a is None:
             raise RuntimeError("failed to load %s" % f)
         assets.append(a)
-    per_row = int(math.sqrt(num_envs))
+    per_row = int(math.sqrt(grid_envs or num_envs))
     spacing = 20.0
     lower = gymapi.Vec3(-spacing, -spacing, -spacing)
     upper = gymapi.Vec3(spacing, spacing, spacing)
