@@ -193,8 +193,11 @@ int32_t     mg_apply_rigid_body_force(mg_sim* sim, const float* force, const flo
                                       int32_t space, int32_t src_host, void* stream);
 
 /* ---- Jacobian / mass matrix (examples/franka_cube_ik_osc.py:305-316,345-346) */
-/* Writes the articulation template `tmpl`'s Jacobian (num_instances, L-1 or L, 6, D)
- * and mass matrix (num_instances, D, D) for fixed-base articulations.  */
+/* For the fixed-base articulation template `tmpl` (instances in actor order):
+ * Jacobian (instances, L-1, 6, D) — link 1..L-1, rows [linear velocity of the
+ * link frame origin; angular velocity] in the world frame, one column per DOF;
+ * mass matrix (instances, D, D) — joint-space inertia by the composite-rigid-
+ * body algorithm, joint armature not included. Both at the current DOF state. */
 int32_t     mg_refresh_jacobian(mg_sim* sim, int32_t tmpl, float* dst, int32_t dst_host, void* stream);
 int32_t     mg_refresh_mass_matrix(mg_sim* sim, int32_t tmpl, float* dst, int32_t dst_host, void* stream);
 

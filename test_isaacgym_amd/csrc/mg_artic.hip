@@ -219,7 +219,143 @@ __global__ void __launch_bounds__(64) k_artic_step(MgStep P, MgArticArgs A) {
     }
 }
 
+// ---- Jacobian and joint-space mass matrix (refresh_jacobian_tensors /
+// refresh_mass_matrix_tensors, examples/franka_cube_ik_osc.py:305-316,345-346).
+// One lane = one articulation of the template. For a fixed base the tensors are
+//   J: (instances, L-1, 6, D): link l = 1..L-1, rows [linear xyz of the link
+//      frame origin, angular xyz] in the world frame, column d = DOF d;
+//   M: (instances, D, D): composite-rigid-body algorithm (RBDA Table 6.2) in
+//      link coordinates, without joint armature.
+template <int MAXL>
+__global__ void __launch_bounds__(64) k_artic_jac_mm(MgArticArgs A, float* jac, float* mm) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= A.na) return;
+    const int b0 = A.artic_i[i * MG_ARTIC_I_N + 0];
+    const int d0 = A.artic_i[i * MG_ARTIC_I_N + 1];
+    const int nb = A.nb;
+    const int L = A.nl, D = A.ndof;
+    const float* S = A.state;
+    const V3 x0 = v3(S[0 * nb + b0], S[1 * nb + b0], S[2 * nb + b0]);
+    const Q4 q0 = qnormalize(q4(S[3 * nb + b0], S[4 * nb + b0], S[5 * nb + b0], S[6 * nb + b0]));
+
+    Q4 ql[MAXL];
+    V3 xl[MAXL], axw[MAXL];
+    M3 E[MAXL];
+    V3 r[MAXL];
+    SV Sj[MAXL];
+    SI IC[MAXL];
+    for (int l = 0; l < L; ++l) {
+        const float* lf = A.link_f + l * MG_LINK_F_N;
+        const int* li = A.link_i + l * MG_LINK_I_N;
+        const int p = li[0], jt = li[1], dof = li[2];
+        const int b = b0 + l;
+        if (p < 0) {
+            ql[l] = q0; xl[l] = x0;
+            E[l] = m3cols(v3(1.0f, 0.0f, 0.0f), v3(0.0f, 1.0f, 0.0f), v3(0.0f, 0.0f, 1.0f));
+            r[l] = v3(0.0f, 0.0f, 0.0f);
+            Sj[l] = svzero();
+            axw[l] = v3(0.0f, 0.0f, 0.0f);
+        } else {
+            const V3 po = v3(lf[0], lf[1], lf[2]);
+            const Q4 qo = q4(lf[3], lf[4], lf[5], lf[6]);
+            const V3 ax = v3(lf[7], lf[8], lf[9]);
+            const float qj = dof >= 0 ? A.dof_pos[d0 + dof] : 0.0f;
+            Q4 qrel = qo;
+            V3 rr = po;
+            SV s = svzero();
+            if (jt == MG_JOINT_REVOLUTE) {
+                qrel = qmul(qo, q_axis_angle(ax, qj));
+                s = sv(ax, v3(0.0f, 0.0f, 0.0f));
+            } else if (jt == MG_JOINT_PRISMATIC) {
+                rr = vadd(po, qrot(qo, vscale(ax, qj)));
+                s = sv(v3(0.0f, 0.0f, 0.0f), ax);
+            }
+            ql[l] = qnormalize(qmul(ql[p], qrel));
+            xl[l] = vadd(xl[p], qrot(ql[p], rr));
+            E[l] = m3t(qmat(qrel));
+            r[l] = rr;
+            Sj[l] = s;
+            axw[l] = qrot(ql[l], ax);
+        }
+        const float* M = A.mass;
+        const float m = M[11 * nb + b];
+        const V3 com = v3(M[8 * nb + b], M[9 * nb + b], M[10 * nb + b]);
+        const Q4 iq = q4(M[4 * nb + b], M[5 * nb + b], M[6 * nb + b], M[7 * nb + b]);
+        const V3 invI = v3(M[1 * nb + b], M[2 * nb + b], M[3 * nb + b]);
+        const V3 Id = v3(invI.x > 0.0f ? 1.0f / invI.x : 0.0f, invI.y > 0.0f ? 1.0f / invI.y : 0.0f,
+                         invI.z > 0.0f ? 1.0f / invI.z : 0.0f);
+        const M3 Rq = qmat(iq);
+        IC[l] = si_rigid(m, com, m3mul(m3mul(Rq, m3cols(v3(Id.x, 0.0f, 0.0f), v3(0.0f, Id.y, 0.0f),
+                                                       v3(0.0f, 0.0f, Id.z))), m3t(Rq)));
+    }
+    if (jac) {
+        float* J = jac + (long)i * (L - 1) * 6 * D;
+        for (int l = 1; l < L; ++l) {
+            float* Jl = J + (l - 1) * 6 * D;
+            for (int k = 0; k < 6 * D; ++k) Jl[k] = 0.0f;
+            int j = l;
+            while (j > 0) {
+                const int* lj = A.link_i + j * MG_LINK_I_N;
+                const int dof = lj[2];
+                if (dof >= 0) {
+                    const V3 z = axw[j];
+                    V3 lin, ang;
+                    if (lj[1] == MG_JOINT_REVOLUTE) {
+                        lin = vcross(z, vsub(xl[l], xl[j]));
+                        ang = z;
+                    } else {
+                        lin = z;
+                        ang = v3(0.0f, 0.0f, 0.0f);
+                    }
+                    Jl[0 * D + dof] = lin.x; Jl[1 * D + dof] = lin.y; Jl[2 * D + dof] = lin.z;
+                    Jl[3 * D + dof] = ang.x; Jl[4 * D + dof] = ang.y; Jl[5 * D + dof] = ang.z;
+                }
+                j = lj[0];
+            }
+        }
+    }
+    if (mm) {
+        float* Mo = mm + (long)i * D * D;
+        for (int l = L - 1; l >= 1; --l) {
+            const int p = A.link_i[l * MG_LINK_I_N + 0];
+            if (p > 0) IC[p] = si_add(IC[p], x_inertia_t(E[l], r[l], IC[l]));
+        }
+        for (int l = 1; l < L; ++l) {
+            const int di = A.link_i[l * MG_LINK_I_N + 2];
+            if (di < 0) continue;
+            SV F = si_mul(IC[l], Sj[l]);
+            Mo[di * D + di] = svdot(Sj[l], F);
+            int j = l;
+            while (A.link_i[j * MG_LINK_I_N + 0] > 0) {
+                F = x_force_t(E[j], r[j], F);
+                j = A.link_i[j * MG_LINK_I_N + 0];
+                const int dj = A.link_i[j * MG_LINK_I_N + 2];
+                if (dj >= 0) {
+                    const float h = svdot(F, Sj[j]);
+                    Mo[di * D + dj] = h;
+                    Mo[dj * D + di] = h;
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t mg_launch_jacobian(const MgArticArgs& A, float* jac, float* mm, hipStream_t s) {
+    if (A.na <= 0) return hipSuccess;
+    if (!A.fixed_base) return hipErrorNotSupported;
+    const int blocks = (A.na + 63) / 64;
+    if (A.nl <= 4)
+        hipLaunchKernelGGL(k_artic_jac_mm<4>, dim3(blocks), dim3(64), 0, s, A, jac, mm);
+    else if (A.nl <= 8)
+        hipLaunchKernelGGL(k_artic_jac_mm<8>, dim3(blocks), dim3(64), 0, s, A, jac, mm);
+    else if (A.nl <= MG_MAX_LINKS)
+        hipLaunchKernelGGL(k_artic_jac_mm<MG_MAX_LINKS>, dim3(blocks), dim3(64), 0, s, A, jac, mm);
+    else
+        return hipErrorNotSupported;
+    return hipGetLastError();
+}
 
 hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream_t s) {
     if (A.na <= 0) return hipSuccess;

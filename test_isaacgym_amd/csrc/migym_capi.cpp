@@ -575,15 +575,46 @@ int32_t mg_apply_rigid_body_force(mg_sim* s, const float* force, const float* to
     return MG_OK;
 }
 
+static int refresh_jac_mm(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_host, void* stream, bool jac) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (!dst) return fail(MG_ERR_ARG, "null destination");
+    const ArticGroup* g = nullptr;
+    for (const ArticGroup& x : s->groups)
+        if (x.tmpl == tmpl) g = &x;
+    if (!g) return fail(MG_ERR_ARG, "no articulation template %d", tmpl);
+    if (!g->fixed_base) return fail(MG_ERR_UNSUPPORTED, "jacobian / mass matrix of floating-base articulations");
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)stream;
+    const size_t per = jac ? (size_t)(g->nl - 1) * 6 * g->ndof : (size_t)g->ndof * g->ndof;
+    const size_t total = per * g->count;
+    float* out = dst;
+    if (dst_host) {
+        int rc = ensure_stage(s, total, 0);
+        if (rc) return rc;
+        out = s->d_stage;
+    }
+    MgArticArgs A{};
+    A.na = g->count; A.nb = s->nb; A.nd = s->nd;
+    A.artic_i = s->d_artic + (size_t)g->offset * MG_ARTIC_I_N;
+    A.tmpl = g->tmpl; A.nl = g->nl; A.ndof = g->ndof; A.fixed_base = g->fixed_base;
+    A.link_f = s->d_link_f + (size_t)g->first_link * MG_LINK_F_N;
+    A.link_i = s->d_link_i + (size_t)g->first_link * MG_LINK_I_N;
+    A.state = s->d_state; A.mass = s->d_mass;
+    A.dof_pos = s->d_dof; A.dof_vel = s->d_dof + s->nd;
+    if (total > 0 && !jac) HIP_TRY(hipMemsetAsync(out, 0, total * sizeof(float), st));
+    HIP_TRY(mg_launch_jacobian(A, jac ? out : nullptr, jac ? nullptr : out, st));
+    if (dst_host) {
+        HIP_TRY(hipMemcpyAsync(dst, out, total * sizeof(float), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return MG_OK;
+}
+
 int32_t mg_refresh_jacobian(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_host, void* stream) {
-    (void)tmpl; (void)dst; (void)dst_host; (void)stream;
-    if (!s) return fail(MG_ERR_ARG, "null sim");
-    return fail(MG_ERR_UNSUPPORTED, "jacobian tensors are not implemented yet");
+    return refresh_jac_mm(s, tmpl, dst, dst_host, stream, true);
 }
 int32_t mg_refresh_mass_matrix(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_host, void* stream) {
-    (void)tmpl; (void)dst; (void)dst_host; (void)stream;
-    if (!s) return fail(MG_ERR_ARG, "null sim");
-    return fail(MG_ERR_UNSUPPORTED, "mass matrix tensors are not implemented yet");
+    return refresh_jac_mm(s, tmpl, dst, dst_host, stream, false);
 }
 
 }  // extern "C"

@@ -810,13 +810,19 @@ class Gym:
         return True
 
     def _artic_template(self, sim, actor_name):
+        """(template id, asset) of the articulated actors named actor_name; the
+        tensors cover every instance of that template, in actor order."""
         sim.finalize()
+        A = sim.model_arrays
         for a in sim.actors:
             if a.name == actor_name and len(a.asset.bodies) > 1:
-                A = sim.model_arrays
-                for k, row in enumerate(A["artic_i"]):
+                for row in A["artic_i"]:
                     if row[0] == a.global_body:
-                        return int(row[2]), a.asset
+                        t = int(row[2])
+                        named = sum(1 for b in sim.actors if b.name == actor_name and b.asset is a.asset)
+                        if named != int((A["artic_i"][:, 2] == t).sum()):
+                            raise ValueError("actors named %r must be exactly the instances of one asset" % actor_name)
+                        return t, a.asset
         raise KeyError("no articulated actor named %r" % (actor_name,))
 
     def acquire_jacobian_tensor(self, sim, actor_name):

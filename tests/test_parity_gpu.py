@@ -225,3 +225,107 @@ def test_servo_4096_properties(gym):
     car = a[1::2]
     assert np.all(np.abs(car[:, 2] - 1.25) < 0.01), (car[:, 2].min(), car[:, 2].max())
     assert np.all(np.abs(car[:, 7:10]) < 0.01), np.abs(car[:, 7:10]).max()
+
+
+def _np_quat_mul(a, b):
+    ax, ay, az, aw = a
+    bx, by, bz, bw = b
+    return np.array([aw * bx + ax * bw + ay * bz - az * by, aw * by - ax * bz + ay * bw + az * bx,
+                     aw * bz + ax * by - ay * bx + az * bw, aw * bw - ax * bx - ay * by - az * bz])
+
+
+def _np_rot(q, v):
+    x, y, z, w = q
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                  [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                  [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+    return R @ v
+
+
+def test_gimbal_jacobian_matches_float64_kinematics(gym):
+    """refresh_jacobian_tensors (examples/franka_cube_ik_osc.py:305-311) at random
+    joint angles vs a float64 forward-kinematics Jacobian of the link origins:
+    atol 1e-5 (unit-scale lever arms)."""
+    n = 32
+    sim, envs = scenes.gimbal_scene(gym, n)
+    gym.prepare_sim(sim)
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    jac = gymtorch.wrap_tensor(gym.acquire_jacobian_tensor(sim, "gimbal"))
+    assert tuple(jac.shape) == (n, 3, 6, 3)
+    rng = np.random.RandomState(0)
+    q = rng.uniform(-1.5, 1.5, (n, 3)).astype(np.float32)
+    st = torch.zeros((3 * n, 2), dtype=torch.float32, device=DEV)
+    st[:, 0] = torch.from_numpy(q.reshape(-1)).to(DEV)
+    assert gym.set_dof_state_tensor(sim, gymtorch.unwrap_tensor(st))
+    gym.refresh_jacobian_tensors(sim)
+    J = jac.cpu().numpy()
+    asset = sim.assets[0]
+    base = sim.model_arrays["body_state0"][0::4]
+    for e in range(n):
+        ps, qs, zs = [base[e, 0:3].astype(np.float64)], [base[e, 3:7].astype(np.float64)], [None]
+        for k, j in enumerate(asset.joints):
+            th = float(q[e, k])
+            qrel = _np_quat_mul(j.q, np.r_[j.axis * np.sin(th / 2), np.cos(th / 2)])
+            ps.append(ps[j.parent] + _np_rot(qs[j.parent], j.p))
+            qs.append(_np_quat_mul(qs[j.parent], qrel))
+            zs.append(_np_rot(qs[-1], j.axis))
+        for l in range(1, 4):
+            ref = np.zeros((6, 3))
+            for jl in range(1, l + 1):                 # the gimbal is a chain: ancestors 1..l
+                ref[:3, jl - 1] = np.cross(zs[jl], ps[l] - ps[jl])
+                ref[3:, jl - 1] = zs[jl]
+            np.testing.assert_allclose(J[e, l - 1], ref, atol=1e-5)
+
+
+def test_mass_matrix_consistent_with_aba(gym):
+    """CRBA mass matrix (refresh_mass_matrix_tensors) against the ABA step: from
+    rest, gravity off, one substep of h with unit EFFORT on DOF k gives
+    qd = h (M + diag(armature))^-1 e_k, so M_ab qd / h must be the identity
+    (two independent algorithms; rtol 1e-3 in float32)."""
+    sp = gymapi.SimParams()
+    sp.dt = 1.0 / 600.0
+    sp.substeps = 1
+    sp.up_axis = gymapi.UP_AXIS_Z
+    sp.gravity = gymapi.Vec3(0, 0, 0)
+    sp.use_gpu_pipeline = True
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    opts.armature = 0.002
+    asset = gym.load_asset(sim, scenes.ASSET_ROOT, "servo/gimbal.urdf", opts)
+    n = 3
+    rng = np.random.RandomState(1)
+    q0 = rng.uniform(-1.2, 1.2, (n, 3)).astype(np.float32)
+    for e in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 2)
+        h = gym.create_actor(env, asset, gymapi.Transform(gymapi.Vec3(0, 0, 1)), "gimbal", e, 1)
+        props = gym.get_actor_dof_properties(env, h)
+        props["driveMode"][:] = gymapi.DOF_MODE_EFFORT
+        props["stiffness"][:] = 0
+        props["damping"][:] = 0
+        props["effort"][:] = 0          # no clamp
+        props["velocity"][:] = 0
+        gym.set_actor_dof_properties(env, h, props)
+        ds = np.zeros(3, gymapi.DofState.dtype)
+        ds["pos"] = q0[e]
+        gym.set_actor_dof_states(env, h, ds, gymapi.STATE_ALL)
+    gym.prepare_sim(sim)
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    mm = gymtorch.wrap_tensor(gym.acquire_mass_matrix_tensor(sim, "gimbal"))
+    gym.refresh_mass_matrix_tensors(sim)
+    M = mm.cpu().numpy().astype(np.float64)
+    assert np.allclose(M, np.transpose(M, (0, 2, 1)))
+    Minv = np.zeros((n, 3, 3))
+    init = torch.zeros((3 * n, 2), dtype=torch.float32, device=DEV)
+    init[:, 0] = torch.from_numpy(q0.reshape(-1)).to(DEV)
+    for k in range(3):
+        gym.set_dof_state_tensor(sim, gymtorch.unwrap_tensor(init))
+        tau = torch.zeros(3 * n, dtype=torch.float32, device=DEV)
+        tau[k::3] = 1.0
+        gym.set_dof_actuation_force_tensor(sim, gymtorch.unwrap_tensor(tau))
+        gym.simulate(sim)
+        gym.refresh_dof_state_tensor(sim)
+        Minv[:, :, k] = dof.cpu().numpy()[:, 1].reshape(n, 3) / sp.dt
+    for e in range(n):
+        eye = (M[e] + 0.002 * np.eye(3)) @ Minv[e]
+        np.testing.assert_allclose(eye, np.eye(3), atol=2e-3)
