@@ -72,6 +72,39 @@ def cpu_baseline(seconds=10.0):
                       "oracle/migym_oracle.c single-threaded (%.1f s)" % (steps, el)}
 
 
+def gimbal_rate(n, steps, warmup, dev):
+    """S2 servo-arm: n fixed-base 3-DOF gimbals under random PD
+    position targets; one step = set_dof_position_target_tensor -> simulate ->
+    refresh DOF + rigid-body state. Returns env-steps/s and the step kernel time."""
+    gym = gymapi.acquire_gym()
+    sim, _ = scenes.gimbal_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
+    gym.prepare_sim(sim)
+    gym.acquire_dof_state_tensor(sim)
+    gym.acquire_rigid_body_state_tensor(sim)
+    tg = scenes.gimbal_targets(n, 64, dev, seed=0)
+
+    def step(k):
+        gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[k % 64]))
+        gym.simulate(sim)
+        gym.refresh_dof_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+
+    for k in range(warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    avg = ctypes.c_float()
+    used = N.lib.mg_step_time_stats(sim.native, min(steps, 512), ctypes.byref(avg), None, None)
+    gym.destroy_sim(sim)
+    return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
+            "kernel": "k_artic_step<4>", "kernel_ms_avg": avg.value if used > 0 else None,
+            "algorithmic_bytes_per_env": 532}
+
+
 def load_traffic():
     """HBM bytes per k_rigid_step launch from the committed rocprofv3 PMC pass
     (profiles/*pmc*.json, written by profiles/collect_pmc.py), else None."""
@@ -92,6 +125,7 @@ def main():
     ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of the root state every step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-gimbal", action="store_true", help="skip the secondary S2 servo-arm measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,6 +232,8 @@ def main():
                         "bound at this size (SURVEY.md §0.10)",
             },
         }
+        if world == 1 and not args.no_gimbal:
+            out["s2_servo_arm"] = gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline"]["cores"] = 1

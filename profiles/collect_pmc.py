@@ -1,0 +1,61 @@
+"""Turns rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate runs, as
+MI355X_MICROARCH.md §rocprofv3 PMC slots requires) of `bench.py` into per-launch
+HBM traffic of the step kernel.
+
+Units and gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE / WRITE_SIZE
+are KiB; FETCH_SIZE under-reads wide coalesced loads by exactly 2x and other
+widths are uncalibrated, so the read factor is calibrated here on a kernel of
+the same run with a known read volume and the same access width (dword loads):
+k_scatter_rows of set_actor_root_state reads the (2N, 13) f32 root tensor once
+(fully coalesced) plus its int32 root-body index per row.
+
+usage: python profiles/collect_pmc.py FETCH.csv WRITE.csv ENVS OUT.json
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        name = r["Kernel_Name"]
+        for key in ("k_rigid_step", "k_scatter_rows", "k_gather_rows", "k_artic_step"):
+            if key in name:
+                name = key
+        acc[name].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+
+
+def main():
+    fetch_csv, write_csv, envs, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    f, nf = per_kernel(fetch_csv, "FETCH_SIZE")
+    w, _ = per_kernel(write_csv, "WRITE_SIZE")
+    actors = 2 * envs
+    known_read = actors * 13 * 4 + actors * 4
+    factor = known_read / (f["k_scatter_rows"] * 1024.0)
+    rigid_read = f["k_rigid_step"] * 1024.0 * factor
+    rigid_write = w["k_rigid_step"] * 1024.0
+    res = {
+        "envs": envs,
+        "kernel": "k_rigid_step",
+        "fetch_kib_raw": f["k_rigid_step"],
+        "write_kib_raw": w["k_rigid_step"],
+        "read_factor_calibrated": factor,
+        "calibration": "k_scatter_rows reads %d B per launch; FETCH_SIZE %.1f KiB" % (known_read,
+                                                                                   f["k_scatter_rows"]),
+        "hbm_bytes_per_launch": rigid_read + rigid_write,
+        "algorithmic_bytes_per_launch": 376 * envs,
+        "launches": nf["k_rigid_step"],
+        "all_kernels_fetch_kib": f,
+        "all_kernels_write_kib": w,
+    }
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -21,6 +21,14 @@ from . import _types as T
 from ._assets import _qmat, _qmul
 
 
+def _raw_stream(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+if hasattr(torch._C, "_cuda_getCurrentRawStream"):
+    _raw_stream = torch._C._cuda_getCurrentRawStream      # noqa: F811  (one C call, no Stream object)
+
+
 class Env:
     __slots__ = ("sim", "index", "lower", "upper", "per_row", "origin", "actors", "num_bodies", "num_dofs",
                  "cameras")
@@ -383,9 +391,11 @@ class Sim:
         return self.native
 
     def stream(self):
-        if torch.cuda.is_available():
-            return torch.cuda.current_stream(self.compute_device).cuda_stream
-        return None
+        """torch's current HIP stream on the sim's device (raw handle), so our
+        kernels order with the caller's torch work on the state tensors."""
+        if self.native is None:
+            return None
+        return _raw_stream(self.compute_device)
 
     def destroy(self):
         if self.native:
