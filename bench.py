@@ -105,10 +105,11 @@ def gimbal_rate(n, steps, warmup, dev):
             "algorithmic_bytes_per_env": 532}
 
 
-def load_traffic():
-    """HBM bytes per k_rigid_step launch from the committed rocprofv3 PMC pass
-    (profiles/*pmc*.json, written by profiles/collect_pmc.py), else None."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_rigid.json")
+def load_traffic(envs):
+    """HBM bytes per k_rigid_step launch at this env count from the committed
+    rocprofv3 PMC passes (profiles/r01_pmc_rigid_<envs>.json, written by
+    profiles/collect_pmc.py), else None."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_rigid_%d.json" % envs)
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -190,7 +191,7 @@ def main():
     value = world * n * args.steps / el
     bytes_launch = SIM_BYTES_PER_ENV * n
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if used > 0 else None
-    traffic = load_traffic()
+    traffic = load_traffic(n)
     out = None
     if rank == 0:
         out = {

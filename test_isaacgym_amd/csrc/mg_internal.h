@@ -36,7 +36,7 @@ struct MgRigidArgs {
     int          nf;          // number of free bodies
     int          nf1;         // of which single-shape (listed first in free_ids)
     int          nb;          // SoA stride (total bodies)
-    const int*   free_ids;    // [nf] global body ids
+    const int*   free_ids;    // [nf] storage slots, or null: slot = lane index
     float*       state;       // [13][nb]
     const float* mass;        // [12][nb]
     const int*   body_tmpl;   // [nb]

@@ -339,7 +339,7 @@ template <bool UPZ, int MAXC, bool MULTI>
 __global__ void __launch_bounds__(64) k_rigid_step(MgStep P, MgRigidArgs A) {
     const int i = blockIdx.x * 64 + threadIdx.x;
     if (i >= A.nf) return;
-    const int b = A.free_ids[i];
+    const int b = A.free_ids ? A.free_ids[i] : i;
     if constexpr (UPZ) {
         rigid_body<MAXC, MULTI>(BasisZ{}, P, A, b);
     } else {
@@ -366,7 +366,15 @@ hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream
     MgRigidArgs A1 = A, A2 = A;
     A1.nf = A.nf1;
     A2.nf = A.nf - A.nf1;
-    A2.free_ids = A.free_ids + A.nf1;
+    if (A.free_ids) {
+        A2.free_ids = A.free_ids + A.nf1;
+    } else {   // bodies in storage slots 0..nf-1: the second group starts at slot nf1
+        A2.state = A.state + A.nf1;
+        A2.mass = A.mass + A.nf1;
+        A2.body_tmpl = A.body_tmpl + A.nf1;
+        A2.ext = A.ext ? A.ext + A.nf1 : nullptr;
+        A2.cforce = A.cforce + A.nf1;
+    }
     if (A1.nf > 0) {
         const int blocks = (A1.nf + 63) / 64;
         if (upz) hipLaunchKernelGGL((k_rigid_step<true, 4, false>), dim3(blocks), dim3(64), 0, s, P, A1);

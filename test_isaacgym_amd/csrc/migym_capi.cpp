@@ -66,16 +66,21 @@ struct mg_sim {
 
     int nenv = 0, na = 0, nb = 0, nd = 0, ntb = 0, ns = 0, nf = 0, nartic = 0, ntl = 0;
     int max_actor_dofs = 0;
-    int nf1 = 0;   // single-shape free bodies (first in d_free)
+    int nf1 = 0;   // single-shape free bodies (storage slots 0..nf1-1)
 
     float* d_state = nullptr;     // [13][nb]
     float* d_mass = nullptr;      // [12][nb]
-    int* d_body_tmpl = nullptr;   // [nb]
-    int* d_free = nullptr;        // [nf]
+    // Bodies are stored in an internal order (free bodies first, by launch group
+    // and template; then each articulation's links contiguously; then the rest)
+    // so every kernel's lanes touch contiguous SoA slots. Tensors stay in the
+    // global (Isaac Gym) order: the gather / scatter index maps fold in `perm`.
+    int* d_body_tmpl = nullptr;   // [nb] internal order
+    int* d_free_global = nullptr; // [nf] global ids of the free bodies (internal 0..nf-1)
+    int* d_perm = nullptr;        // [nb] global body -> internal slot
     float* d_tbf = nullptr;
     int* d_tbi = nullptr;
     float* d_shapes = nullptr;
-    int* d_actor_root = nullptr;  // [na]
+    int* d_actor_root = nullptr;  // [na] internal slot of each actor's root body
     int* d_actor_dof = nullptr;   // [na+1]
     float* d_cforce = nullptr;    // [3][nb]
     float* d_ext = nullptr;       // [6][nb]
@@ -211,7 +216,7 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
 }
 
 void free_all(mg_sim* s) {
-    void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free, s->d_tbf, s->d_tbi, s->d_shapes,
+    void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_tbi, s->d_shapes,
                     s->d_actor_root, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
                     s->d_dof_props, s->d_artic, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx};
     for (void* p : ptrs)
@@ -308,6 +313,12 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     for (int b : free_ids) s->nf1 += nshapes(b) <= 1 ? 1 : 0;
     s->nf = (int)free_ids.size();
 
+    // internal storage order: free bodies (as above), articulation links
+    // (instance by instance, template by template), everything else
+    std::vector<int> order(free_ids), perm(nb, -1);
+    std::vector<char> placed(nb, 0);
+    for (int b : free_ids) placed[b] = 1;
+
     // articulation instances grouped by template
     s->groups.clear();
     std::vector<int> artic_sorted;
@@ -336,16 +347,35 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
             if (ai[0] < 0 || ai[0] + g.nl > nb || ai[1] < 0 || ai[1] + g.ndof > nd)
                 return fail(MG_ERR_ARG, "articulation %d out of range", k);
             for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_sorted.push_back(ai[j]);
+            for (int l = 0; l < g.nl; ++l) {
+                if (placed[ai[0] + l]) return fail(MG_ERR_ARG, "articulation %d overlaps another body", k);
+                placed[ai[0] + l] = 1;
+                order.push_back(ai[0] + l);
+            }
             g.count++;
         }
         s->groups.push_back(g);
+    }
+
+    for (int b = 0; b < nb; ++b)
+        if (!placed[b]) order.push_back(b);
+    for (int i = 0; i < nb; ++i) perm[order[i]] = i;
+    for (size_t k = 0; k < artic_sorted.size(); k += MG_ARTIC_I_N) artic_sorted[k] = perm[artic_sorted[k]];
+    std::vector<int> root_int(na), tmpl_int(nb);
+    for (int a = 0; a < na; ++a) root_int[a] = perm[m->actor_root_body[a]];
+    for (int i = 0; i < nb; ++i) tmpl_int[i] = m->body_tmpl[order[i]];
+    std::vector<float> st0((size_t)nb * MG_STATE_N), ms0((size_t)nb * MG_MASS_N);
+    for (int i = 0; i < nb; ++i) {
+        std::memcpy(&st0[(size_t)i * MG_STATE_N], m->body_state0 + (size_t)order[i] * MG_STATE_N, MG_STATE_N * sizeof(float));
+        std::memcpy(&ms0[(size_t)i * MG_MASS_N], m->body_mass + (size_t)order[i] * MG_MASS_N, MG_MASS_N * sizeof(float));
     }
 
     // device buffers
     HIP_TRY(dalloc(&s->d_state, (size_t)nb * MG_STATE_N));
     HIP_TRY(dalloc(&s->d_mass, (size_t)nb * MG_MASS_N));
     HIP_TRY(dalloc(&s->d_body_tmpl, nb));
-    HIP_TRY(dalloc(&s->d_free, s->nf));
+    HIP_TRY(dalloc(&s->d_free_global, s->nf));
+    HIP_TRY(dalloc(&s->d_perm, nb));
     HIP_TRY(dalloc(&s->d_tbf, (size_t)s->ntb * MG_TBODY_F_N));
     HIP_TRY(dalloc(&s->d_tbi, (size_t)s->ntb * MG_TBODY_I_N));
     HIP_TRY(dalloc(&s->d_shapes, (size_t)s->ns * MG_SHAPE_STRIDE));
@@ -364,16 +394,17 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         if (bytes == 0 || !h) return hipSuccess;
         return hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
     };
-    std::vector<float> st = to_soa(m->body_state0, nb, MG_STATE_N);
-    std::vector<float> ms = to_soa(m->body_mass, nb, MG_MASS_N);
+    std::vector<float> st = to_soa(st0.data(), nb, MG_STATE_N);
+    std::vector<float> ms = to_soa(ms0.data(), nb, MG_MASS_N);
     HIP_TRY(h2d(s->d_state, st.data(), st.size() * sizeof(float)));
     HIP_TRY(h2d(s->d_mass, ms.data(), ms.size() * sizeof(float)));
-    HIP_TRY(h2d(s->d_body_tmpl, m->body_tmpl, (size_t)nb * sizeof(int)));
-    HIP_TRY(h2d(s->d_free, free_ids.data(), free_ids.size() * sizeof(int)));
+    HIP_TRY(h2d(s->d_body_tmpl, tmpl_int.data(), (size_t)nb * sizeof(int)));
+    HIP_TRY(h2d(s->d_free_global, free_ids.data(), free_ids.size() * sizeof(int)));
+    HIP_TRY(h2d(s->d_perm, perm.data(), (size_t)nb * sizeof(int)));
     HIP_TRY(h2d(s->d_tbf, m->tmpl_body_f, (size_t)s->ntb * MG_TBODY_F_N * sizeof(float)));
     HIP_TRY(h2d(s->d_tbi, m->tmpl_body_i, (size_t)s->ntb * MG_TBODY_I_N * sizeof(int)));
     HIP_TRY(h2d(s->d_shapes, m->shapes, (size_t)s->ns * MG_SHAPE_STRIDE * sizeof(float)));
-    HIP_TRY(h2d(s->d_actor_root, m->actor_root_body, (size_t)na * sizeof(int)));
+    HIP_TRY(h2d(s->d_actor_root, root_int.data(), (size_t)na * sizeof(int)));
     HIP_TRY(h2d(s->d_actor_dof, m->actor_dof, (size_t)(na + 1) * sizeof(int)));
     HIP_TRY(hipMemset(s->d_cforce, 0, (size_t)nb * 3 * sizeof(float)));
     HIP_TRY(hipMemset(s->d_ext, 0, (size_t)nb * 6 * sizeof(float)));
@@ -420,7 +451,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     }
     if (s->nf > 0) {
         MgRigidArgs A{};
-        A.nf = s->nf; A.nf1 = s->nf1; A.nb = s->nb; A.free_ids = s->d_free;
+        A.nf = s->nf; A.nf1 = s->nf1; A.nb = s->nb; A.free_ids = nullptr;   // internal slots 0..nf-1
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
         A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
@@ -482,7 +513,7 @@ int32_t mg_refresh_actor_root_state(mg_sim* s, float* dst, int32_t dst_host, voi
 }
 int32_t mg_refresh_rigid_body_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
-    return refresh_rows(s, s->d_state, s->nb, MG_STATE_N, nullptr, s->nb, dst, dst_host, (hipStream_t)stream);
+    return refresh_rows(s, s->d_state, s->nb, MG_STATE_N, s->d_perm, s->nb, dst, dst_host, (hipStream_t)stream);
 }
 int32_t mg_refresh_dof_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
@@ -490,7 +521,7 @@ int32_t mg_refresh_dof_state(mg_sim* s, float* dst, int32_t dst_host, void* stre
 }
 int32_t mg_refresh_net_contact_force(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
-    return refresh_rows(s, s->d_cforce, s->nb, 3, nullptr, s->nb, dst, dst_host, (hipStream_t)stream);
+    return refresh_rows(s, s->d_cforce, s->nb, 3, s->d_perm, s->nb, dst, dst_host, (hipStream_t)stream);
 }
 
 int32_t mg_set_actor_root_state(mg_sim* s, const float* src, int32_t src_host, const int32_t* idx,
@@ -519,7 +550,7 @@ int32_t mg_set_rigid_body_state(mg_sim* s, const float* src, int32_t src_host, v
     int rc = stage_src(s, src, src_host, (size_t)s->nb * MG_STATE_N, nullptr, 0, st, &dsrc, &didx);
     if (rc) return rc;
     // free bodies only: rows are selected through the free-body list
-    HIP_TRY(mg_launch_scatter_rows(dsrc, MG_STATE_N, nullptr, s->d_free, s->nf, s->d_state, s->nb, st));
+    HIP_TRY(mg_launch_scatter_rows(dsrc, MG_STATE_N, s->d_perm, s->d_free_global, s->nf, s->d_state, s->nb, st));
     return MG_OK;
 }
 
@@ -568,7 +599,7 @@ int32_t mg_apply_rigid_body_force(mg_sim* s, const float* force, const float* to
         const int* didx;
         int rc = stage_src(s, parts[k], src_host, (size_t)s->nb * 3, nullptr, 0, st, &dsrc, &didx);
         if (rc) return rc;
-        HIP_TRY(mg_launch_scatter_rows(dsrc, 3, nullptr, nullptr, s->nb, s->d_ext + (size_t)k * 3 * s->nb, s->nb, st));
+        HIP_TRY(mg_launch_scatter_rows(dsrc, 3, s->d_perm, nullptr, s->nb, s->d_ext + (size_t)k * 3 * s->nb, s->nb, st));
         if (src_host) HIP_TRY(hipStreamSynchronize(st));  // staging buffer is reused by the next part
     }
     s->ext_pending = true;
