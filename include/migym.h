@@ -75,6 +75,7 @@ extern "C" {
 #define MG_LINK_I_N        4  /* parent (local, -1 root), joint type, dof (local, -1 none), pad */
 #define MG_ARTIC_I_N       4  /* first_body, first_dof, tmpl, pad */
 #define MG_ATMPL_I_N       4  /* first_link (into tmpl_link_*), num_links, num_dofs, fixed_base */
+#define MG_ACOLL_N         4  /* env, collision group, collision filter, pad */
 
 /* Simulation parameters: gymapi.SimParams + PhysXParams + the ground plane
  * (reference: test10_servo_vecenv.py:117-144 and :198-206). */
@@ -124,7 +125,13 @@ typedef struct mg_model {
     const int32_t* artic_tmpl_i;  /* [num_artic_tmpls][MG_ATMPL_I_N] */
     const float*   tmpl_link_f;   /* [num_tmpl_links][MG_LINK_F_N] */
     const int32_t* tmpl_link_i;   /* [num_tmpl_links][MG_LINK_I_N] */
-    const void*    reserved_p[3];
+    /* [num_actors][MG_ACOLL_N]: env, collision group, collision filter, pad
+     * (create_actor's group / filter, test10_servo_vecenv.py:317,323). Two actors
+     * of an env collide when (group_a == group_b or either is -1) and
+     * (filter_a & filter_b) == 0; the ground collides with everything. NULL: no
+     * body-body contacts (every env steps in the uncoupled kernels). */
+    const int32_t* actor_coll;
+    const void*    reserved_p[2];
 } mg_model;
 
 typedef struct mg_sim mg_sim;
@@ -213,6 +220,9 @@ int32_t     mg_step_time_stats(mg_sim* sim, int32_t n, float* avg_ms, float* min
  * articulation kernel in one simulate. */
 int32_t     mg_num_free_bodies(mg_sim* sim);
 int32_t     mg_num_articulations(mg_sim* sim);
+/* Number of envs stepped by the coupled per-env kernel (envs whose bodies can
+ * touch each other under the actor_coll rule, e.g. the Franka cube-pick scene). */
+int32_t     mg_num_coupled_envs(mg_sim* sim);
 
 #ifdef __cplusplus
 }

@@ -67,3 +67,16 @@ def step(sim_params, model, state, dof, tgt=None, props=None, ext=None, cforce=N
     if rc != 0:
         raise RuntimeError("oracle_step: unsupported model")
     return cforce
+
+
+def collide(a, b, margin):
+    """Narrow phase of the coupled step (oracle_collide): a, b = [type, c.xyz,
+    q.xyzw, h.xyz]; returns an (n, 7) array of [point on a, normal b->a, sep]."""
+    L = lib()
+    L.oracle_collide.restype = ctypes.c_int
+    L.oracle_collide.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p]
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    out = np.zeros((4, 7), dtype=np.float32)
+    n = L.oracle_collide(a.ctypes.data, b.ctypes.data, float(margin), out.ctypes.data)
+    return out[:n]

@@ -476,6 +476,11 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
     if (!fixed_base || L > OR_MAXL) return -1;
     for (d = 0; d < D; ++d) { q[d] = dof[(d0 + d) * 2 + 0]; qd[d] = dof[(d0 + d) * 2 + 1]; qdd[d] = 0.0f; }
     for (st_ = 0; st_ < P->substeps; ++st_) {
+      unsigned xmask = 0u, xpos = 0u;
+      float tau0d[OR_MAXL], impd[OR_MAXL];
+      int att;
+      for (att = 0; att < 2; ++att) {
+        unsigned nm;
         for (l = 0; l < L; ++l) {
             const int p = LI[l * MG_LINK_I_N + 0], jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
             const float* M = m->body_mass + (size_t)(b0 + l) * MG_MASS_N;
@@ -525,10 +530,16 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
                 } else if (mode == MG_DOF_MODE_EFFORT) {
                     tau = tg[2];
                 }
-                if (eff > 0.0f && (tau > eff || tau < -eff)) {
-                    tau = tau > eff ? eff : -eff;
-                    imp = 0.0f;
+                if (eff > 0.0f) {
+                    if ((xmask >> dj) & 1u) {
+                        tau = ((xpos >> dj) & 1u) ? eff : -eff;
+                        imp = 0.0f;
+                    } else if (imp == 0.0f) {
+                        tau = fminf(fmaxf(tau, -eff), eff);
+                    }
                 }
+                tau0d[dj] = tau;
+                impd[dj] = imp;
                 U[l] = simul_(Ia, Sj[l]);
                 Dl[l] = svdot_(Sj[l], U[l]) + arm + imp;
                 ul[l] = tau - svdot_(Sj[l], pA[l]);
@@ -556,6 +567,18 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
             }
             a[l] = ap;
         }
+        nm = xmask;
+        for (d = 0; d < D; ++d) {
+            const float eff = props[(size_t)(d0 + d) * MG_DOFPROP_N + 3];
+            if (eff > 0.0f && impd[d] != 0.0f) {
+                const float act = tau0d[d] - impd[d] * qdd[d];
+                if (act > eff) { nm |= 1u << d; xpos |= 1u << d; }
+                else if (act < -eff) nm |= 1u << d;
+            }
+        }
+        if (nm == xmask) break;
+        xmask = nm;
+      }
         for (d = 0; d < D; ++d) {
             const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
             const float maxv = pr[4];
@@ -599,6 +622,8 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
     return 0;
 }
 
+#include "migym_oracle_env.c"
+
 /* ---- entry point --------------------------------------------------------
  * One gym.simulate() over the whole model, AoS host arrays:
  *   state [nb][13] in/out, dof [nd][2] in/out, tgt [nd][3] (target pos, target
@@ -610,20 +635,35 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
 int oracle_step(const mg_sim_params* p, const mg_model* m, float* state, float* dof, const float* tgt,
                 const float* props, const float* ext, float* cforce, int body_begin, int body_end) {
     step_t P = make_step_(p);
-    int b, k;
+    int b, k, ne, rc = 0;
+    oenv_t* envs = NULL;
+    char* owned = NULL;
     if (!props) props = m->dof_props;
     if (body_end < 0 || body_end > m->num_bodies) body_end = m->num_bodies;
+    envs = (oenv_t*)calloc((size_t)(m->num_envs > 0 ? m->num_envs : 1), sizeof(oenv_t));
+    owned = (char*)calloc((size_t)(m->num_bodies > 0 ? m->num_bodies : 1), 1);
+    if (!envs || !owned) { rc = -1; goto done; }
+    ne = classify_envs_(m, envs, owned);
+    if (ne < 0) { rc = -1; goto done; }
+    for (k = 0; k < ne; ++k) {
+        const int first = envs[k].art_body >= 0 ? envs[k].art_body : envs[k].free_b[0];
+        if (first < body_begin || first >= body_end) continue;
+        if (env_step_(&P, m, &envs[k], state, dof, tgt, props, ext, cforce) != 0) { rc = -1; goto done; }
+    }
     for (k = 0; k < m->num_artics; ++k) {
         const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;
-        if (ai[0] < body_begin || ai[0] >= body_end) continue;
-        if (artic_step(&P, m, ai, state, dof, tgt, props, cforce) != 0) return -1;
+        if (ai[0] < body_begin || ai[0] >= body_end || owned[ai[0]]) continue;
+        if (artic_step(&P, m, ai, state, dof, tgt, props, cforce) != 0) { rc = -1; goto done; }
     }
     for (b = body_begin; b < body_end; ++b) {
-        if (m->body_kind[b] != MG_BODY_FREE) continue;
+        if (m->body_kind[b] != MG_BODY_FREE || owned[b]) continue;
         rigid_body_step(&P, m, b, state + (size_t)b * MG_STATE_N, ext ? ext + (size_t)b * 6 : NULL,
                         cforce + (size_t)b * 3);
     }
-    return 0;
+done:
+    free(envs);
+    free(owned);
+    return rc;
 }
 
 int oracle_abi_version(void) { return MG_ABI_VERSION; }

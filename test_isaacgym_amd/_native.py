@@ -26,6 +26,7 @@ MG_LINK_F_N = 16
 MG_LINK_I_N = 4
 MG_ARTIC_I_N = 4
 MG_ATMPL_I_N = 4
+MG_ACOLL_N = 4
 
 MG_SHAPE_SPHERE, MG_SHAPE_BOX, MG_SHAPE_CAPSULE = 0, 1, 2
 MG_BODY_FREE, MG_BODY_STATIC, MG_BODY_LINK = 0, 1, 2
@@ -69,7 +70,8 @@ class MgModel(ctypes.Structure):
         ("actor_root_body", _i32p), ("actor_dof", _i32p),
         ("dof_state0", _f32p), ("dof_props", _f32p),
         ("artic_i", _i32p), ("artic_tmpl_i", _i32p), ("tmpl_link_f", _f32p), ("tmpl_link_i", _i32p),
-        ("reserved_p", ctypes.c_void_p * 3),
+        ("actor_coll", _i32p),
+        ("reserved_p", ctypes.c_void_p * 2),
     ]
 
 
@@ -108,6 +110,7 @@ def _load():
         "mg_step_time_stats": (i32, [vp, i32, vp, vp, vp]),
         "mg_num_free_bodies": (i32, [vp]),
         "mg_num_articulations": (i32, [vp]),
+        "mg_num_coupled_envs": (i32, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -129,6 +132,7 @@ EXPORTED_SYMBOLS = (
     "mg_set_dof_actuation_force", "mg_set_dof_props", "mg_apply_rigid_body_force",
     "mg_refresh_jacobian", "mg_refresh_mass_matrix", "mg_last_step_ms", "mg_step_time_stats", "mg_num_free_bodies",
     "mg_num_articulations",
+    "mg_num_coupled_envs",
 )
 
 

@@ -224,6 +224,7 @@ class Sim:
         btmpl = np.zeros(nb, dtype=np.int32)
         root = np.zeros(na, dtype=np.int32)
         adof = np.zeros(na + 1, dtype=np.int32)
+        acoll = np.zeros((na, N.MG_ACOLL_N), dtype=np.int32)
         dof0 = np.zeros((nd, 2), dtype=np.float32)
         dprops = np.zeros((nd, N.MG_DOFPROP_N), dtype=np.float32)
         tbf, tbi, shapes = [], [], []
@@ -237,6 +238,7 @@ class Sim:
             nba = a.num_bodies
             g0 = a.global_body
             root[a.global_index] = g0
+            acoll[a.global_index, :3] = [a.env.index, a.group, a.filter]
             adof[a.global_index + 1] = a.global_dof + a.num_dofs
             ps, qs = self.actor_world_body_poses(a)
             multi = nba > 1
@@ -317,7 +319,7 @@ class Sim:
             tmpl_body_f=np.array(tbf, dtype=np.float32).reshape(-1, N.MG_TBODY_F_N),
             tmpl_body_i=np.array(tbi, dtype=np.int32).reshape(-1, N.MG_TBODY_I_N),
             shapes=np.array(shapes, dtype=np.float32).reshape(-1, N.MG_SHAPE_STRIDE),
-            actor_root_body=root, actor_dof=adof, dof_state0=dof0, dof_props=dprops,
+            actor_root_body=root, actor_dof=adof, actor_coll=acoll, dof_state0=dof0, dof_props=dprops,
             artic_i=np.array(artic, dtype=np.int32).reshape(-1, N.MG_ARTIC_I_N),
             artic_tmpl_i=np.array(atmpl, dtype=np.int32).reshape(-1, N.MG_ATMPL_I_N),
             tmpl_link_f=np.array(lf, dtype=np.float32).reshape(-1, N.MG_LINK_F_N),
@@ -344,7 +346,7 @@ class Sim:
             keep[name] = arr
             setattr(m, name, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
         for name in ("body_kind", "body_tmpl", "tmpl_body_i", "actor_root_body", "actor_dof", "artic_i",
-                     "artic_tmpl_i", "tmpl_link_i"):
+                     "artic_tmpl_i", "tmpl_link_i", "actor_coll"):
             arr = np.ascontiguousarray(A[name], dtype=np.int32)
             keep[name] = arr
             setattr(m, name, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))

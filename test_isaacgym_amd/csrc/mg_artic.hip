@@ -11,8 +11,9 @@
 //   pass 3 (outward): a_0 = -g (base frame), qdd = (u - U^T a') / D;
 //   semi-implicit Euler on (q, qd), joint-velocity clamp, joint-limit clamp.
 // Drive law: POS tau0 = kp (q* - q - h qd) + kd (qd* - qd),
-// VEL tau0 = kd (qd* - qd), EFFORT tau0 = u; when |tau0| exceeds the effort
-// limit the drive is applied explicitly, clamped, and its implicit term dropped.
+// VEL tau0 = kd (qd* - qd), EFFORT tau0 = u. Effort limit: EFFORT forces are
+// clamped; a PD / velocity drive whose implicit force tau0 - (h kd + h^2 kp) qdd
+// exceeds the limit is re-solved (once, exactly) as a constant force at the limit.
 // Per-template link constants (parent, joint frame, axis) are read with
 // wave-uniform addresses, so they come through the scalar cache once per wave.
 // Restated in C by oracle/migym_oracle.c:oracle_artic_step.
@@ -53,6 +54,12 @@ __global__ void __launch_bounds__(64) k_artic_step(MgStep P, MgArticArgs A) {
     float Dl[MAXL], ul[MAXL];
 
     for (int st = 0; st < P.substeps; ++st) {
+      // Effort limit: a drive whose implicit force tau0 - imp qdd exceeds the
+      // limit is re-solved as a constant force at the limit (xmask / xpos), one
+      // exact ABA re-solve when any joint saturates.
+      unsigned xmask = 0u, xpos = 0u;
+      float tau0d[MAXL], impd[MAXL];
+      for (int att = 0; att < 2; ++att) {
         // ---- pass 1: kinematics, velocities, bias forces
         for (int l = 0; l < L; ++l) {
             const float* lf = A.link_f + l * MG_LINK_F_N;
@@ -122,10 +129,16 @@ __global__ void __launch_bounds__(64) k_artic_step(MgStep P, MgArticArgs A) {
                 } else if (mode == MG_DOF_MODE_EFFORT) {
                     tau = A.dof_force[gd];
                 }
-                if (eff > 0.0f && (tau > eff || tau < -eff)) {
-                    tau = tau > eff ? eff : -eff;
-                    imp = 0.0f;
+                if (eff > 0.0f) {
+                    if ((xmask >> dof) & 1u) {
+                        tau = ((xpos >> dof) & 1u) ? eff : -eff;
+                        imp = 0.0f;
+                    } else if (imp == 0.0f) {
+                        tau = fminf(fmaxf(tau, -eff), eff);
+                    }
                 }
+                tau0d[dof] = tau;
+                impd[dof] = imp;
                 U[l] = si_mul(Ia, Sj[l]);
                 Dl[l] = svdot(Sj[l], U[l]) + arm + imp;
                 ul[l] = tau - svdot(Sj[l], pA[l]);
@@ -155,6 +168,19 @@ __global__ void __launch_bounds__(64) k_artic_step(MgStep P, MgArticArgs A) {
             }
             a[l] = ap;
         }
+        // ---- saturated implicit drives?
+        unsigned nm = xmask;
+        for (int d = 0; d < D; ++d) {
+            const float eff = A.dof_props[3 * nd + d0 + d];
+            if (eff > 0.0f && impd[d] != 0.0f) {
+                const float act = tau0d[d] - impd[d] * qdd[d];
+                if (act > eff) { nm |= 1u << d; xpos |= 1u << d; }
+                else if (act < -eff) nm |= 1u << d;
+            }
+        }
+        if (nm == xmask) break;
+        xmask = nm;
+      }
         // ---- integrate joints
         for (int d = 0; d < D; ++d) {
             const int gd = d0 + d;

@@ -1,0 +1,271 @@
+// mg_collide.h — narrow phase for the per-env step (mg_env.hip): contacts
+// between two convex primitives (box, sphere, capsule) in world space.
+//
+// Output convention: each contact is (point p on shape A, unit normal n pointing
+// from B towards A, separation sep — negative when penetrating). Boxes are
+// (centre, rotation columns, half extents); spheres (centre, radius); capsules
+// are replaced by their two end-cap spheres (documented approximation).
+// Box–box is SAT over the 15 axes (face axes preferred unless an edge axis
+// separates by more than 1e-3 m), then Sutherland–Hodgman clipping of the
+// incident face against the reference face (at most 8 points, the 4 deepest
+// kept, ties by index); edge–edge gives one contact at the closest points.
+// Fixed evaluation order, no FMA: oracle/migym_oracle_env.c restates it.
+#pragma once
+#include "mg_math.h"
+
+#define MG_PAIR_MAXC 4
+
+struct CShape {      // a primitive placed in the world
+    int type;        // MG_SHAPE_*
+    V3 c;            // centre
+    M3 R;            // orientation (columns = local axes)
+    V3 h;            // box half extents | (radius, half height, -) for sphere / capsule
+};
+
+struct PairOut {
+    int n;
+    V3 p[MG_PAIR_MAXC];
+    V3 nrm[MG_PAIR_MAXC];
+    float sep[MG_PAIR_MAXC];
+};
+
+MG_HD float m3c(const M3& R, int i, int k) {      // component k of column i
+    const V3 c = i == 0 ? R.c0 : (i == 1 ? R.c1 : R.c2);
+    return k == 0 ? c.x : (k == 1 ? c.y : c.z);
+}
+MG_HD V3 m3col(const M3& R, int i) { return i == 0 ? R.c0 : (i == 1 ? R.c1 : R.c2); }
+MG_HD float v3c(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+
+MG_HD void pair_push(PairOut& o, V3 p, V3 n, float sep) {
+    if (o.n < MG_PAIR_MAXC) {
+        o.p[o.n] = p; o.nrm[o.n] = n; o.sep[o.n] = sep;
+        o.n = o.n + 1;
+    }
+}
+
+// sphere A (centre a, radius ra) vs sphere B
+MG_HD void sphere_sphere(V3 a, float ra, V3 b, float rb, float margin, PairOut& o) {
+    const V3 d = vsub(a, b);
+    const float l2 = vdot(d, d);
+    const float l = sqrtf(l2);
+    const float sep = l - ra - rb;
+    if (!(sep < margin)) return;
+    V3 n = l > 1e-9f ? vscale(d, 1.0f / l) : v3(0.0f, 0.0f, 1.0f);
+    pair_push(o, vsub(a, vscale(n, ra)), n, sep);
+}
+
+// sphere A vs box B
+MG_HD void sphere_box(V3 s, float r, const CShape& B, float margin, PairOut& o) {
+    const V3 d = vsub(s, B.c);
+    const V3 loc = mtmul(B.R, d);
+    const float hx = B.h.x, hy = B.h.y, hz = B.h.z;
+    const float qx = fminf(fmaxf(loc.x, -hx), hx);
+    const float qy = fminf(fmaxf(loc.y, -hy), hy);
+    const float qz = fminf(fmaxf(loc.z, -hz), hz);
+    const bool inside = loc.x == qx && loc.y == qy && loc.z == qz;
+    V3 n;
+    float sep;
+    if (!inside) {
+        const V3 dq = mmul(B.R, v3(loc.x - qx, loc.y - qy, loc.z - qz));
+        const float l = sqrtf(vdot(dq, dq));
+        sep = l - r;
+        if (!(sep < margin)) return;
+        n = vscale(dq, 1.0f / l);
+    } else {
+        // centre inside: leave through the nearest face
+        const float px = hx - fabsf(loc.x), py = hy - fabsf(loc.y), pz = hz - fabsf(loc.z);
+        int ax = 0;
+        float pen = px;
+        if (py < pen) { ax = 1; pen = py; }
+        if (pz < pen) { ax = 2; pen = pz; }
+        const float sg = v3c(loc, ax) < 0.0f ? -1.0f : 1.0f;
+        n = vscale(m3col(B.R, ax), sg);
+        sep = -pen - r;
+    }
+    pair_push(o, vsub(s, vscale(n, r)), n, sep);
+}
+
+// box A vs box B
+MG_HD void box_box(const CShape& A, const CShape& B, float margin, PairOut& o) {
+    const V3 d = vsub(B.c, A.c);               // A -> B
+    float Rm[3][3], AbsR[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            Rm[i][j] = vdot(m3col(A.R, i), m3col(B.R, j));
+            AbsR[i][j] = fabsf(Rm[i][j]) + 1e-6f;
+        }
+    const float ha[3] = {A.h.x, A.h.y, A.h.z};
+    const float hb[3] = {B.h.x, B.h.y, B.h.z};
+    const float t[3] = {vdot(d, A.R.c0), vdot(d, A.R.c1), vdot(d, A.R.c2)};
+    // face axes
+    float best_face = -1e30f;
+    int face = 0;
+    for (int i = 0; i < 3; ++i) {
+        const float rb = hb[0] * AbsR[i][0] + hb[1] * AbsR[i][1] + hb[2] * AbsR[i][2];
+        const float sep = fabsf(t[i]) - ha[i] - rb;
+        if (sep > best_face) { best_face = sep; face = i; }
+    }
+    for (int j = 0; j < 3; ++j) {
+        const float ra = ha[0] * AbsR[0][j] + ha[1] * AbsR[1][j] + ha[2] * AbsR[2][j];
+        const float tb = t[0] * Rm[0][j] + t[1] * Rm[1][j] + t[2] * Rm[2][j];
+        const float sep = fabsf(tb) - hb[j] - ra;
+        if (sep > best_face) { best_face = sep; face = 3 + j; }
+    }
+    if (!(best_face < margin)) return;
+    // edge axes
+    float best_edge = -1e30f;
+    int ei = -1, ej = -1;
+    V3 eaxis = v3(0.0f, 0.0f, 0.0f);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            V3 ax = vcross(m3col(A.R, i), m3col(B.R, j));
+            const float l2 = vdot(ax, ax);
+            if (!(l2 > 1e-6f)) continue;
+            ax = vscale(ax, 1.0f / sqrtf(l2));
+            const float ra = ha[0] * fabsf(vdot(ax, A.R.c0)) + ha[1] * fabsf(vdot(ax, A.R.c1)) + ha[2] * fabsf(vdot(ax, A.R.c2));
+            const float rb = hb[0] * fabsf(vdot(ax, B.R.c0)) + hb[1] * fabsf(vdot(ax, B.R.c1)) + hb[2] * fabsf(vdot(ax, B.R.c2));
+            const float sep = fabsf(vdot(d, ax)) - ra - rb;
+            if (!(sep < margin)) return;         // a separating axis: no contact
+            if (sep > best_edge) { best_edge = sep; ei = i; ej = j; eaxis = ax; }
+        }
+    if (ei >= 0 && best_edge > best_face + 1e-3f) {
+        // edge-edge: closest points of the two supporting edges
+        V3 ax = eaxis;
+        if (vdot(ax, d) < 0.0f) ax = vscale(ax, -1.0f);      // A -> B
+        V3 pa = A.c, pb = B.c;
+        for (int k = 0; k < 3; ++k) {
+            if (k != ei) pa = vadd(pa, vscale(m3col(A.R, k), vdot(ax, m3col(A.R, k)) > 0.0f ? ha[k] : -ha[k]));
+            if (k != ej) pb = vadd(pb, vscale(m3col(B.R, k), vdot(ax, m3col(B.R, k)) > 0.0f ? -hb[k] : hb[k]));
+        }
+        const V3 ua = m3col(A.R, ei), ub = m3col(B.R, ej);
+        const V3 w = vsub(pa, pb);
+        const float b = vdot(ua, ub), dd = vdot(ua, w), e = vdot(ub, w);
+        const float den = 1.0f - b * b;
+        float sa = 0.0f, sb = 0.0f;
+        if (den > 1e-6f) {
+            sa = (b * e - dd) / den;
+            sb = (e - b * dd) / den;
+        }
+        sa = fminf(fmaxf(sa, -ha[ei]), ha[ei]);
+        sb = fminf(fmaxf(sb, -hb[ej]), hb[ej]);
+        const V3 ca = vadd(pa, vscale(ua, sa));
+        const V3 cb = vadd(pb, vscale(ub, sb));
+        pair_push(o, vscale(vadd(ca, cb), 0.5f), vscale(ax, -1.0f), best_edge);
+        return;
+    }
+    // face contact: reference box / axis, incident box
+    const bool refA = face < 3;
+    const CShape& Rf = refA ? A : B;
+    const CShape& In = refA ? B : A;
+    const int fa = refA ? face : face - 3;
+    const float hr[3] = {Rf.h.x, Rf.h.y, Rf.h.z};
+    const float hi[3] = {In.h.x, In.h.y, In.h.z};
+    V3 nref = m3col(Rf.R, fa);                         // outward normal of the reference face, towards In
+    if (vdot(vsub(In.c, Rf.c), nref) < 0.0f) nref = vscale(nref, -1.0f);
+    // incident face: most anti-parallel to nref
+    int ik = 0;
+    float bestd = 1e30f;
+    for (int k = 0; k < 3; ++k) {
+        const float dk = -fabsf(vdot(nref, m3col(In.R, k)));
+        if (dk < bestd) { bestd = dk; ik = k; }
+    }
+    const V3 iax = m3col(In.R, ik);
+    const V3 ifc = vadd(In.c, vscale(iax, vdot(nref, iax) > 0.0f ? -hi[ik] : hi[ik]));
+    const int iu = ik == 0 ? 1 : 0, iv = ik == 2 ? 1 : 2;
+    const V3 eu = vscale(m3col(In.R, iu), hi[iu]), ev = vscale(m3col(In.R, iv), hi[iv]);
+    // polygon in the reference face frame (u, v): up to 8 vertices
+    const int ru = fa == 0 ? 1 : 0, rv = fa == 2 ? 1 : 2;
+    const V3 U = m3col(Rf.R, ru), W = m3col(Rf.R, rv);
+    const V3 rc = vadd(Rf.c, vscale(nref, hr[fa]));     // reference face centre
+    float px[8], py[8];
+    int np = 4;
+    {
+        const V3 q0 = vsub(vsub(ifc, eu), ev), q1 = vsub(vadd(ifc, eu), ev);
+        const V3 q2 = vadd(vadd(ifc, eu), ev), q3 = vadd(vsub(ifc, eu), ev);
+        px[0] = vdot(vsub(q0, rc), U); py[0] = vdot(vsub(q0, rc), W);
+        px[1] = vdot(vsub(q1, rc), U); py[1] = vdot(vsub(q1, rc), W);
+        px[2] = vdot(vsub(q2, rc), U); py[2] = vdot(vsub(q2, rc), W);
+        px[3] = vdot(vsub(q3, rc), U); py[3] = vdot(vsub(q3, rc), W);
+    }
+    // clip against u <= hu, -u <= hu, v <= hv, -v <= hv
+    for (int side = 0; side < 4; ++side) {
+        const float lim = side < 2 ? hr[ru] : hr[rv];
+        const float sg = (side & 1) ? -1.0f : 1.0f;
+        float ox[8], oy[8];
+        int no = 0;
+        for (int k = 0; k < np; ++k) {
+            const int k2 = k + 1 == np ? 0 : k + 1;
+            const float a0 = sg * (side < 2 ? px[k] : py[k]) - lim;
+            const float a1 = sg * (side < 2 ? px[k2] : py[k2]) - lim;
+            if (a0 <= 0.0f && no < 8) { ox[no] = px[k]; oy[no] = py[k]; no = no + 1; }
+            if ((a0 <= 0.0f) != (a1 <= 0.0f) && no < 8) {
+                const float tt = a0 / (a0 - a1);
+                ox[no] = px[k] + (px[k2] - px[k]) * tt;
+                oy[no] = py[k] + (py[k2] - py[k]) * tt;
+                no = no + 1;
+            }
+        }
+        np = no;
+        for (int k = 0; k < np; ++k) { px[k] = ox[k]; py[k] = oy[k]; }
+        if (np == 0) return;
+    }
+    // depth of each clipped point below the reference face: project onto the
+    // incident face plane along nref to get the point on the incident body
+    const V3 inrm = vscale(iax, vdot(nref, iax) > 0.0f ? -1.0f : 1.0f);
+    const float den = vdot(inrm, nref);
+    float dep[8];
+    V3 pts[8];
+    for (int k = 0; k < np; ++k) {
+        const V3 q = vadd(vadd(rc, vscale(U, px[k])), vscale(W, py[k]));   // on the reference plane
+        float tt = 0.0f;
+        if (fabsf(den) > 1e-6f) tt = vdot(vsub(ifc, q), inrm) / den;
+        pts[k] = vadd(q, vscale(nref, tt));                              // on the incident face
+        dep[k] = tt;                                                     // separation along nref
+    }
+    // keep the (up to) 4 deepest within the margin, lowest index first on ties
+    bool used[8];
+    for (int k = 0; k < 8; ++k) used[k] = false;
+    for (int m = 0; m < MG_PAIR_MAXC; ++m) {
+        int bk = -1;
+        float bd = margin;
+        for (int k = 0; k < np; ++k)
+            if (!used[k] && dep[k] < bd) { bd = dep[k]; bk = k; }
+        if (bk < 0) break;
+        used[bk] = true;
+        // normal from B towards A: nref points from the reference box to the incident box
+        const V3 n = refA ? vscale(nref, -1.0f) : nref;
+        // the point lies on the incident box: on B when A is the reference, on A otherwise
+        const V3 pA = refA ? vsub(pts[bk], vscale(nref, dep[bk])) : pts[bk];
+        pair_push(o, pA, n, dep[bk]);
+    }
+}
+
+// generic dispatch; capsules are two end-cap spheres
+MG_HD void collide(const CShape& A, const CShape& B, float margin, PairOut& o) {
+    V3 ca[2], cb[2];
+    float ra, rb;
+    int na, nbs;
+    if (A.type == MG_SHAPE_BOX && B.type == MG_SHAPE_BOX) { box_box(A, B, margin, o); return; }
+    // sphere-like decomposition
+    na = A.type == MG_SHAPE_CAPSULE ? 2 : 1;
+    nbs = B.type == MG_SHAPE_CAPSULE ? 2 : 1;
+    ra = A.h.x; rb = B.h.x;
+    ca[0] = A.type == MG_SHAPE_CAPSULE ? vsub(A.c, vscale(A.R.c0, A.h.y)) : A.c;
+    ca[1] = vadd(A.c, vscale(A.R.c0, A.h.y));
+    cb[0] = B.type == MG_SHAPE_CAPSULE ? vsub(B.c, vscale(B.R.c0, B.h.y)) : B.c;
+    cb[1] = vadd(B.c, vscale(B.R.c0, B.h.y));
+    if (B.type == MG_SHAPE_BOX) {
+        for (int k = 0; k < na; ++k) sphere_box(ca[k], ra, B, margin, o);
+        return;
+    }
+    if (A.type == MG_SHAPE_BOX) {
+        PairOut t;
+        t.n = 0;
+        for (int k = 0; k < nbs; ++k) sphere_box(cb[k], rb, A, margin, t);
+        for (int k = 0; k < t.n; ++k)     // swap roles: point on A, normal from B to A
+            pair_push(o, vadd(t.p[k], vscale(t.nrm[k], t.sep[k])), vscale(t.nrm[k], -1.0f), t.sep[k]);
+        return;
+    }
+    for (int k = 0; k < na; ++k)
+        for (int m = 0; m < nbs; ++m) sphere_sphere(ca[k], ra, cb[m], rb, margin, o);
+}

@@ -71,7 +71,43 @@ struct MgArticArgs {
     float*       cforce;      // [3][nb]
 };
 
+// Coupled per-env step (mg_env.hip). env_i rows (MG_ENV_I_N int32):
+//   [0] first internal body of the env's articulation or -1, [1] its first DOF,
+//   [2] free bodies nf <= MG_ENV_MAXF, [3..6] their internal slots,
+//   [7] static bodies ns <= MG_ENV_MAXS, [8..11] their internal slots,
+//   [12] collision mask: bit k art-free k, 4+s art-static s, 8+p free pair p
+//        ((0,1),(0,2),(0,3),(1,2),(1,3),(2,3)), 14+4k+s free k-static s.
+#define MG_ENV_I_N    16
+#define MG_ENV_MAXF    4
+#define MG_ENV_MAXS    4
+#define MG_ENV_MAXCT  20     // contacts per env per substep
+#define MG_ENV_FREE0  16     // participant id of free body 0 (links are 0..15)
+
+struct MgEnvArgs {
+    int          ne;          // envs in this launch
+    int          nb, nd;
+    const int*   env_i;       // [ne][MG_ENV_I_N]
+    int          nl, ndof;    // articulation template of this launch (0 links: none)
+    const float* link_f;
+    const int*   link_i;
+    float*       state;
+    const float* mass;
+    const int*   body_tmpl;
+    const float* tbf;
+    const int*   tbi;
+    const float* shapes;
+    float*       dof_pos;
+    float*       dof_vel;
+    const float* dof_tpos;
+    const float* dof_tvel;
+    const float* dof_force;
+    const float* dof_props;
+    const float* ext;
+    float*       cforce;
+};
+
 // launchers (defined in the .hip files)
+hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s);
 hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream_t s);
 hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream_t s);
 hipError_t mg_launch_gather_rows(const float* soa, int stride, int ncol, const int* ids, int n,

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdarg>
@@ -54,7 +55,14 @@ std::vector<T> to_soa(const T* aos, int n, int ncol) {
 
 struct ArticGroup {
     int tmpl, first_link, nl, ndof, fixed_base;
-    int offset, count;   // into the template-sorted instance list
+    int offset, count;             // into the template-sorted instance list (all instances)
+    int step_offset, step_count;   // into the list stepped by k_artic_step (uncoupled envs)
+};
+
+// coupled envs (mg_env.hip) of one articulation template (tmpl -1: none)
+struct EnvGroup {
+    int tmpl, first_link, nl, ndof;
+    int offset, count;   // rows of d_env
 };
 
 }  // namespace
@@ -67,6 +75,7 @@ struct mg_sim {
     int nenv = 0, na = 0, nb = 0, nd = 0, ntb = 0, ns = 0, nf = 0, nartic = 0, ntl = 0;
     int max_actor_dofs = 0;
     int nf1 = 0;   // single-shape free bodies (storage slots 0..nf1-1)
+    int nf_rigid = 0;   // free bodies of uncoupled envs (slots 0..nf_rigid-1), free-body kernel
 
     float* d_state = nullptr;     // [13][nb]
     float* d_mass = nullptr;      // [12][nb]
@@ -93,6 +102,10 @@ struct mg_sim {
     float* d_link_f = nullptr;
     int* d_link_i = nullptr;
     std::vector<ArticGroup> groups;
+    int* d_artic_step = nullptr;  // [..][4] instances stepped by k_artic_step
+    int* d_env = nullptr;         // [n_coupled][MG_ENV_I_N] coupled envs, by group
+    int n_coupled = 0;
+    std::vector<EnvGroup> env_groups;
 
     float* d_stage = nullptr;     // host-transfer staging (floats)
     size_t stage_n = 0;
@@ -218,7 +231,7 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_tbi, s->d_shapes,
                     s->d_actor_root, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
-                    s->d_dof_props, s->d_artic, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx};
+                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -297,12 +310,103 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     }
     if (na > 0 && (m->actor_dof[0] != 0 || m->actor_dof[na] != nd)) return fail(MG_ERR_ARG, "actor_dof must span [0, num_dofs]");
 
+    // ---- coupled envs: envs where two bodies may touch (actor_coll rule, see
+    // migym.h) step in the per-env kernel; everything else in the free-body /
+    // articulation kernels
+    std::vector<char> coupled_body(nb, 0);           // free roots / articulation roots of coupled envs
+    std::vector<std::array<int, MG_ENV_I_N>> env_rows;   // global body ids, converted below
+    std::vector<int> env_tmpl;
+    if (m->actor_coll && na > 0) {
+        for (int a = 0; a + 1 < na; ++a)
+            if (m->actor_root_body[a + 1] <= m->actor_root_body[a])
+                return fail(MG_ERR_ARG, "actor_coll needs actors in body order");
+        std::vector<int> artic_of_root(nb, -1);
+        for (int k = 0; k < m->num_artics; ++k) {
+            const int r0 = m->artic_i[(size_t)k * MG_ARTIC_I_N + 0];
+            if (r0 < 0 || r0 >= nb) return fail(MG_ERR_ARG, "articulation %d: bad first body", k);
+            artic_of_root[r0] = k;
+        }
+        const int ne = m->num_envs;
+        std::vector<std::vector<int>> env_actors(ne > 0 ? ne : 0);
+        for (int a = 0; a < na; ++a) {
+            const int e = m->actor_coll[(size_t)a * MG_ACOLL_N + 0];
+            if (e < 0 || e >= ne) return fail(MG_ERR_ARG, "actor %d: env %d out of range", a, e);
+            env_actors[e].push_back(a);
+        }
+        auto collide = [m](int a, int b) {
+            const int ga = m->actor_coll[(size_t)a * MG_ACOLL_N + 1], gb = m->actor_coll[(size_t)b * MG_ACOLL_N + 1];
+            const int fa = m->actor_coll[(size_t)a * MG_ACOLL_N + 2], fb = m->actor_coll[(size_t)b * MG_ACOLL_N + 2];
+            return (ga == gb || ga == -1 || gb == -1) && (fa & fb) == 0;
+        };
+        for (int e = 0; e < ne; ++e) {
+            std::vector<int> art, fr, stc;
+            for (int a : env_actors[e]) {
+                const int r0 = m->actor_root_body[a];
+                const int kind = m->body_kind[r0];
+                if (kind == MG_BODY_LINK) art.push_back(a);
+                else if (kind == MG_BODY_FREE) fr.push_back(a);
+                else stc.push_back(a);
+            }
+            bool coupled = false;
+            for (size_t i = 0; i < fr.size(); ++i) {
+                for (int t : stc) coupled = coupled || collide(fr[i], t);
+                for (size_t j = i + 1; j < fr.size(); ++j) coupled = coupled || collide(fr[i], fr[j]);
+            }
+            for (int a : art) {
+                for (int t : stc) coupled = coupled || collide(a, t);
+                for (int f : fr) coupled = coupled || collide(a, f);
+            }
+            if (!coupled) continue;
+            if (art.size() > 1 || fr.size() > MG_ENV_MAXF || stc.size() > MG_ENV_MAXS)
+                return fail(MG_ERR_UNSUPPORTED,
+                            "env %d: %zu articulations / %zu free / %zu static bodies in contact range; the "
+                            "coupled step supports 1 / %d / %d", e, art.size(), fr.size(), stc.size(),
+                            MG_ENV_MAXF, MG_ENV_MAXS);
+            std::array<int, MG_ENV_I_N> row;
+            row.fill(0);
+            row[0] = -1;
+            int tmpl = -1;
+            if (!art.empty()) {
+                const int r0 = m->actor_root_body[art[0]];
+                const int k = artic_of_root[r0];
+                if (k < 0) return fail(MG_ERR_ARG, "env %d: articulated actor without articulation record", e);
+                row[0] = r0;
+                row[1] = m->artic_i[(size_t)k * MG_ARTIC_I_N + 1];
+                tmpl = m->artic_i[(size_t)k * MG_ARTIC_I_N + 2];
+                coupled_body[r0] = 1;
+            }
+            row[2] = (int)fr.size();
+            for (size_t i = 0; i < fr.size(); ++i) {
+                row[3 + i] = m->actor_root_body[fr[i]];
+                coupled_body[row[3 + i]] = 1;
+            }
+            row[7] = (int)stc.size();
+            for (size_t i = 0; i < stc.size(); ++i) row[8 + i] = m->actor_root_body[stc[i]];
+            int mask = 0;
+            static const int pair_bit[4][4] = {{-1, 0, 1, 2}, {-1, -1, 3, 4}, {-1, -1, -1, 5}, {-1, -1, -1, -1}};
+            for (size_t i = 0; i < fr.size(); ++i) {
+                if (!art.empty() && collide(art[0], fr[i])) mask |= 1 << i;
+                for (size_t j = i + 1; j < fr.size(); ++j)
+                    if (collide(fr[i], fr[j])) mask |= 1 << (8 + pair_bit[i][j]);
+                for (size_t t = 0; t < stc.size(); ++t)
+                    if (collide(fr[i], stc[t])) mask |= 1 << (14 + 4 * i + t);
+            }
+            for (size_t t = 0; t < stc.size(); ++t)
+                if (!art.empty() && collide(art[0], stc[t])) mask |= 1 << (4 + t);
+            row[12] = mask;
+            row[13] = tmpl;
+            env_rows.push_back(row);
+            env_tmpl.push_back(tmpl);
+        }
+    }
+
     // free bodies ordered by template body (stable): bodies of one kind share
     // waves, so e.g. the servo scene's airborne UAVs and grounded vehicles do
-    // not interleave lane by lane (results do not depend on the order)
-    std::vector<int> free_ids;
+    // not interleave lane by lane (results do not depend on the order). Free
+    // bodies of coupled envs come last (the per-env kernel reads them).
+    std::vector<int> free_ids, free_cpl;
     for (int b = 0; b < nb; ++b)
-        if (m->body_kind[b] == MG_BODY_FREE) free_ids.push_back(b);
+        if (m->body_kind[b] == MG_BODY_FREE) (coupled_body[b] ? free_cpl : free_ids).push_back(b);
     auto nshapes = [m](int b) { return m->tmpl_body_i[m->body_tmpl[b] * MG_TBODY_I_N + 1]; };
     std::stable_sort(free_ids.begin(), free_ids.end(), [&](int a, int b) {
         const bool ma = nshapes(a) > 1, mb = nshapes(b) > 1;   // single-shape bodies first
@@ -311,6 +415,8 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     });
     s->nf1 = 0;
     for (int b : free_ids) s->nf1 += nshapes(b) <= 1 ? 1 : 0;
+    s->nf_rigid = (int)free_ids.size();
+    free_ids.insert(free_ids.end(), free_cpl.begin(), free_cpl.end());
     s->nf = (int)free_ids.size();
 
     // internal storage order: free bodies (as above), articulation links
@@ -321,7 +427,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
 
     // articulation instances grouped by template
     s->groups.clear();
-    std::vector<int> artic_sorted;
+    std::vector<int> artic_sorted, artic_step;
     for (int t = 0; t < m->num_artic_tmpls; ++t) {
         ArticGroup g;
         g.tmpl = t;
@@ -329,7 +435,8 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         g.nl = m->artic_tmpl_i[t * MG_ATMPL_I_N + 1];
         g.ndof = m->artic_tmpl_i[t * MG_ATMPL_I_N + 2];
         g.fixed_base = m->artic_tmpl_i[t * MG_ATMPL_I_N + 3];
-        if (g.nl < 1 || g.nl > MG_MAX_LINKS || g.ndof > g.nl || g.first_link < 0 || g.first_link + g.nl > s->ntl)
+        if (g.nl < 1 || g.nl > MG_MAX_LINKS || g.ndof > g.nl || g.ndof > MG_MAX_DOFS || g.first_link < 0 ||
+            g.first_link + g.nl > s->ntl)
             return fail(MG_ERR_UNSUPPORTED, "articulation template %d: %d links / %d dofs unsupported", t, g.nl, g.ndof);
         if (!g.fixed_base)
             return fail(MG_ERR_UNSUPPORTED, "articulation template %d: floating-base articulations are not supported yet", t);
@@ -341,12 +448,18 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         }
         g.offset = (int)artic_sorted.size() / MG_ARTIC_I_N;
         g.count = 0;
+        g.step_offset = (int)artic_step.size() / MG_ARTIC_I_N;
+        g.step_count = 0;
         for (int k = 0; k < m->num_artics; ++k) {
             const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;
             if (ai[2] != t) continue;
             if (ai[0] < 0 || ai[0] + g.nl > nb || ai[1] < 0 || ai[1] + g.ndof > nd)
                 return fail(MG_ERR_ARG, "articulation %d out of range", k);
             for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_sorted.push_back(ai[j]);
+            if (!coupled_body[ai[0]]) {
+                for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_step.push_back(ai[j]);
+                g.step_count++;
+            }
             for (int l = 0; l < g.nl; ++l) {
                 if (placed[ai[0] + l]) return fail(MG_ERR_ARG, "articulation %d overlaps another body", k);
                 placed[ai[0] + l] = 1;
@@ -361,6 +474,31 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         if (!placed[b]) order.push_back(b);
     for (int i = 0; i < nb; ++i) perm[order[i]] = i;
     for (size_t k = 0; k < artic_sorted.size(); k += MG_ARTIC_I_N) artic_sorted[k] = perm[artic_sorted[k]];
+    for (size_t k = 0; k < artic_step.size(); k += MG_ARTIC_I_N) artic_step[k] = perm[artic_step[k]];
+    // coupled env rows: internal slots, grouped by articulation template (-1 first)
+    std::vector<int> env_flat;
+    s->env_groups.clear();
+    for (int t = -1; t < m->num_artic_tmpls; ++t) {
+        EnvGroup g{};
+        g.tmpl = t;
+        if (t >= 0) {
+            g.first_link = m->artic_tmpl_i[t * MG_ATMPL_I_N + 0];
+            g.nl = m->artic_tmpl_i[t * MG_ATMPL_I_N + 1];
+            g.ndof = m->artic_tmpl_i[t * MG_ATMPL_I_N + 2];
+        }
+        g.offset = (int)env_flat.size() / MG_ENV_I_N;
+        for (size_t r = 0; r < env_rows.size(); ++r) {
+            if (env_tmpl[r] != t) continue;
+            std::array<int, MG_ENV_I_N> row = env_rows[r];
+            if (row[0] >= 0) row[0] = perm[row[0]];
+            for (int i = 0; i < row[2]; ++i) row[3 + i] = perm[row[3 + i]];
+            for (int i = 0; i < row[7]; ++i) row[8 + i] = perm[row[8 + i]];
+            env_flat.insert(env_flat.end(), row.begin(), row.end());
+            g.count++;
+        }
+        if (g.count > 0) s->env_groups.push_back(g);
+    }
+    s->n_coupled = (int)env_rows.size();
     std::vector<int> root_int(na), tmpl_int(nb);
     for (int a = 0; a < na; ++a) root_int[a] = perm[m->actor_root_body[a]];
     for (int i = 0; i < nb; ++i) tmpl_int[i] = m->body_tmpl[order[i]];
@@ -387,6 +525,8 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(dalloc(&s->d_dof_tgt, (size_t)nd * 3));
     HIP_TRY(dalloc(&s->d_dof_props, (size_t)nd * MG_DOFPROP_N));
     HIP_TRY(dalloc(&s->d_artic, artic_sorted.size()));
+    HIP_TRY(dalloc(&s->d_artic_step, artic_step.size()));
+    HIP_TRY(dalloc(&s->d_env, env_flat.size()));
     HIP_TRY(dalloc(&s->d_link_f, (size_t)s->ntl * MG_LINK_F_N));
     HIP_TRY(dalloc(&s->d_link_i, (size_t)s->ntl * MG_LINK_I_N));
 
@@ -416,6 +556,8 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         HIP_TRY(h2d(s->d_dof_props, dp.data(), dp.size() * sizeof(float)));
     }
     HIP_TRY(h2d(s->d_artic, artic_sorted.data(), artic_sorted.size() * sizeof(int)));
+    HIP_TRY(h2d(s->d_artic_step, artic_step.data(), artic_step.size() * sizeof(int)));
+    HIP_TRY(h2d(s->d_env, env_flat.data(), env_flat.size() * sizeof(int)));
     HIP_TRY(h2d(s->d_link_f, m->tmpl_link_f, (size_t)s->ntl * MG_LINK_F_N * sizeof(float)));
     HIP_TRY(h2d(s->d_link_i, m->tmpl_link_i, (size_t)s->ntl * MG_LINK_I_N * sizeof(int)));
     HIP_TRY(hipDeviceSynchronize());
@@ -433,10 +575,10 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     s->ev_end = s->ring_e[slot];
     HIP_TRY(hipEventRecord(s->ev_begin, st));
     for (const ArticGroup& g : s->groups) {
-        if (g.count == 0) continue;
+        if (g.step_count == 0) continue;
         MgArticArgs A{};
-        A.na = g.count; A.nb = s->nb; A.nd = s->nd;
-        A.artic_i = s->d_artic + (size_t)g.offset * MG_ARTIC_I_N;
+        A.na = g.step_count; A.nb = s->nb; A.nd = s->nd;
+        A.artic_i = s->d_artic_step + (size_t)g.step_offset * MG_ARTIC_I_N;
         A.tmpl = g.tmpl; A.nl = g.nl; A.ndof = g.ndof; A.fixed_base = g.fixed_base;
         A.link_f = s->d_link_f + (size_t)g.first_link * MG_LINK_F_N;
         A.link_i = s->d_link_i + (size_t)g.first_link * MG_LINK_I_N;
@@ -449,9 +591,27 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         hipError_t e = mg_launch_artic_step(P, A, st);
         if (e != hipSuccess) return fail(MG_ERR_DEVICE, "articulation step launch: %s", hipGetErrorString(e));
     }
-    if (s->nf > 0) {
+    for (const EnvGroup& g : s->env_groups) {
+        MgEnvArgs A{};
+        A.ne = g.count; A.nb = s->nb; A.nd = s->nd;
+        A.env_i = s->d_env + (size_t)g.offset * MG_ENV_I_N;
+        A.nl = g.tmpl >= 0 ? g.nl : 0;
+        A.ndof = g.tmpl >= 0 ? g.ndof : 0;
+        A.link_f = s->d_link_f + (size_t)(g.tmpl >= 0 ? g.first_link : 0) * MG_LINK_F_N;
+        A.link_i = s->d_link_i + (size_t)(g.tmpl >= 0 ? g.first_link : 0) * MG_LINK_I_N;
+        A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
+        A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes;
+        A.dof_pos = s->d_dof; A.dof_vel = s->d_dof + s->nd;
+        A.dof_tpos = s->d_dof_tgt; A.dof_tvel = s->d_dof_tgt + s->nd; A.dof_force = s->d_dof_tgt + 2 * (size_t)s->nd;
+        A.dof_props = s->d_dof_props;
+        A.ext = s->ext_pending ? s->d_ext : nullptr;
+        A.cforce = s->d_cforce;
+        hipError_t e = mg_launch_env_step(P, A, st);
+        if (e != hipSuccess) return fail(MG_ERR_DEVICE, "coupled env step launch: %s", hipGetErrorString(e));
+    }
+    if (s->nf_rigid > 0) {
         MgRigidArgs A{};
-        A.nf = s->nf; A.nf1 = s->nf1; A.nb = s->nb; A.free_ids = nullptr;   // internal slots 0..nf-1
+        A.nf = s->nf_rigid; A.nf1 = s->nf1; A.nb = s->nb; A.free_ids = nullptr;   // internal slots 0..nf-1
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
         A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
@@ -506,6 +666,7 @@ int32_t mg_step_time_stats(mg_sim* s, int32_t n, float* avg_ms, float* min_ms, f
 
 int32_t mg_num_free_bodies(mg_sim* s) { return s ? s->nf : 0; }
 int32_t mg_num_articulations(mg_sim* s) { return s ? s->nartic : 0; }
+int32_t mg_num_coupled_envs(mg_sim* s) { return s ? s->n_coupled : 0; }
 
 int32_t mg_refresh_actor_root_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
     if (!s) return fail(MG_ERR_ARG, "null sim");

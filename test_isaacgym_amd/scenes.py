@@ -154,3 +154,112 @@ def gimbal_targets(num_envs, num_batches, device, seed=0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     t = (torch.rand(num_batches, 3 * num_envs, generator=g) * 2 - 1) * 1.57
     return t.to(torch.float32).to(device)
+
+
+# ---------------------------------------------------------------- S3 Franka
+FRANKA_TABLE_DIMS = (0.6, 1.0, 0.4)
+FRANKA_BOX_SIZE = 0.045
+
+
+def franka_sim_params(use_gpu_pipeline=True):
+    """examples/franka_cube_ik_osc.py:111-128."""
+    sp = gymapi.SimParams()
+    sp.up_axis = gymapi.UP_AXIS_Z
+    sp.gravity = gymapi.Vec3(0.0, 0.0, -9.8)
+    sp.dt = 1.0 / 60.0
+    sp.substeps = 2
+    sp.use_gpu_pipeline = use_gpu_pipeline
+    sp.physx.solver_type = 1
+    sp.physx.num_position_iterations = 8
+    sp.physx.num_velocity_iterations = 1
+    sp.physx.rest_offset = 0.0
+    sp.physx.contact_offset = 0.001
+    sp.physx.friction_offset_threshold = 0.001
+    sp.physx.friction_correlation_distance = 0.0005
+    sp.physx.use_gpu = True
+    return sp
+
+
+def franka_scene(gym, num_envs, use_gpu_pipeline=True, device=0, controller="osc", seed=42, asset_root=None,
+                 asset_file="franka/franka_proxy.urdf"):
+    """S3: the cube-pick scene of examples/franka_cube_ik_osc.py:150-285 — per env a
+    fixed table (0.6 x 1.0 x 0.4 at x = 0.5), a 4.5 cm cube placed at random on it
+    (np.random.seed(seed), same draws in the same order as :244-249), and a
+    fixed-base, gravity-free Franka (armature 0.01) with OSC effort drives on the
+    arm and 800 / 40 position drives on the fingers; all three in collision group
+    i, the Franka with filter 2. The Franka is assets/franka/franka_proxy.urdf
+    (tools/make_franka_asset.py). Returns (sim, info dict)."""
+    import numpy as np
+    np.random.seed(seed)
+    sim = gym.create_sim(device, device, gymapi.SIM_PHYSX, franka_sim_params(use_gpu_pipeline))
+    tx, ty, tz = FRANKA_TABLE_DIMS
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    table_asset = gym.create_box(sim, tx, ty, tz, opts)
+    opts = gymapi.AssetOptions()
+    box_asset = gym.create_box(sim, FRANKA_BOX_SIZE, FRANKA_BOX_SIZE, FRANKA_BOX_SIZE, opts)
+    opts = gymapi.AssetOptions()
+    opts.armature = 0.01
+    opts.fix_base_link = True
+    opts.disable_gravity = True
+    opts.flip_visual_attachments = True
+    franka_asset = gym.load_asset(sim, asset_root or ASSET_ROOT, asset_file, opts)
+    if franka_asset is None:
+        raise RuntimeError("franka asset %s not found" % asset_file)
+    props = gym.get_asset_dof_properties(franka_asset)
+    lower, upper = props["lower"], props["upper"]
+    mids = 0.3 * (upper + lower)
+    if controller == "ik":
+        props["driveMode"][:7].fill(gymapi.DOF_MODE_POS)
+        props["stiffness"][:7].fill(400.0)
+        props["damping"][:7].fill(40.0)
+    else:
+        props["driveMode"][:7].fill(gymapi.DOF_MODE_EFFORT)
+        props["stiffness"][:7].fill(0.0)
+        props["damping"][:7].fill(0.0)
+    props["driveMode"][7:].fill(gymapi.DOF_MODE_POS)
+    props["stiffness"][7:].fill(800.0)
+    props["damping"][7:].fill(40.0)
+    ndof = gym.get_asset_dof_count(franka_asset)
+    default_pos = np.zeros(ndof, dtype=np.float32)
+    default_pos[:7] = mids[:7]
+    default_pos[7:] = upper[7:]
+    default_state = np.zeros(ndof, gymapi.DofState.dtype)
+    default_state["pos"] = default_pos
+    hand_index = gym.get_asset_rigid_body_dict(franka_asset)["panda_hand"]
+
+    per_row = int(math.sqrt(num_envs))
+    spacing = 1.0
+    lo, hi = gymapi.Vec3(-spacing, -spacing, 0.0), gymapi.Vec3(spacing, spacing, spacing)
+    franka_pose = gymapi.Transform()
+    franka_pose.p = gymapi.Vec3(0, 0, 0)
+    table_pose = gymapi.Transform()
+    table_pose.p = gymapi.Vec3(0.5, 0.0, 0.5 * tz)
+    box_pose = gymapi.Transform()
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim, plane)
+    envs, box_idxs, hand_idxs, init_pos, init_rot = [], [], [], [], []
+    for i in range(num_envs):
+        env = gym.create_env(sim, lo, hi, per_row)
+        envs.append(env)
+        gym.create_actor(env, table_asset, table_pose, "table", i, 0)
+        box_pose.p.x = table_pose.p.x + np.random.uniform(-0.2, 0.1)
+        box_pose.p.y = table_pose.p.y + np.random.uniform(-0.3, 0.3)
+        box_pose.p.z = tz + 0.5 * FRANKA_BOX_SIZE
+        box_pose.r = gymapi.Quat.from_axis_angle(gymapi.Vec3(0, 0, 1), np.random.uniform(-math.pi, math.pi))
+        box = gym.create_actor(env, box_asset, box_pose, "box", i, 0)
+        np.random.uniform(0, 1, 3)          # the script's colour draws (:251), kept for the same sequence
+        box_idxs.append(gym.get_actor_rigid_body_index(env, box, 0, gymapi.DOMAIN_SIM))
+        franka = gym.create_actor(env, franka_asset, franka_pose, "franka", i, 2)
+        gym.set_actor_dof_properties(env, franka, props)
+        gym.set_actor_dof_states(env, franka, default_state, gymapi.STATE_ALL)
+        gym.set_actor_dof_position_targets(env, franka, default_pos)
+        hand = gym.find_actor_rigid_body_handle(env, franka, "panda_hand")
+        hp = gym.get_rigid_transform(env, hand)
+        init_pos.append([hp.p.x, hp.p.y, hp.p.z])
+        init_rot.append([hp.r.x, hp.r.y, hp.r.z, hp.r.w])
+        hand_idxs.append(gym.find_actor_rigid_body_index(env, franka, "panda_hand", gymapi.DOMAIN_SIM))
+    info = dict(envs=envs, box_idxs=box_idxs, hand_idxs=hand_idxs, init_pos=init_pos, init_rot=init_rot,
+                hand_index=hand_index, default_dof_pos=default_pos, num_dofs=ndof, controller=controller)
+    return sim, info

@@ -1,0 +1,133 @@
+"""S3 on the GPU: the Franka cube-pick scene of examples/franka_cube_ik_osc.py
+through the coupled per-env step (mg_env.hip), driven by the script's own OSC
+controller (test_isaacgym_amd.franka_control, restating :348-410) on the
+device Jacobian / mass-matrix tensors.
+
+Parity: every frame's GPU state must equal the C restatement
+(oracle/migym_oracle_env.c) fed the same actions, bit for bit (the same fp32
+expressions in the same order, no FMA contraction on either side).
+Physics: the pick loop lifts cubes (the script's whole point), and the
+Jacobian / mass matrix match float64 textbook kinematics (tests/kinematics64.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from isaacgym import gymapi, gymtorch
+from test_isaacgym_amd import franka_control, scenes
+import kinematics64 as K
+import oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _setup(gym, n, seed=42):
+    sim, info = scenes.franka_scene(gym, n, use_gpu_pipeline=True, seed=seed)
+    gym.prepare_sim(sim)
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    jac = gymtorch.wrap_tensor(gym.acquire_jacobian_tensor(sim, "franka"))
+    mm = gymtorch.wrap_tensor(gym.acquire_mass_matrix_tensor(sim, "franka"))
+    ctl = franka_control.CubePick(n, info["init_pos"], info["init_rot"], info["default_dof_pos"], DEV)
+    return sim, info, rb, dof, jac, mm, ctl
+
+
+def _control(gym, sim, info, rb, dof, jac, mm, ctl, n):
+    gym.refresh_rigid_body_state_tensor(sim)
+    gym.refresh_dof_state_tensor(sim)
+    gym.refresh_jacobian_tensors(sim)
+    gym.refresh_mass_matrix_tensors(sim)
+    h = info["hand_index"]
+    bi = torch.tensor(info["box_idxs"], device=DEV)
+    hi = torch.tensor(info["hand_idxs"], device=DEV)
+    dp = dof[:, 0].view(n, 9, 1)
+    dv = dof[:, 1].view(n, 9, 1)
+    pa, ea = ctl.step(rb, dp, dv, jac[:, h - 1, :, :7], mm[:, :7, :7], bi, hi)
+    gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(pa.contiguous()))
+    gym.set_dof_actuation_force_tensor(sim, gymtorch.unwrap_tensor(ea.contiguous()))
+    return pa, ea
+
+
+def test_franka_env_classification(gym):
+    """Every env is one coupled-step lane (cube + table in group i, filter 0;
+    Franka filter 2): no body goes through the uncoupled kernels."""
+    from test_isaacgym_amd import _native as N
+    sim, info, *_ = _setup(gym, 8)
+    assert N.lib.mg_num_coupled_envs(sim.native) == 8
+
+
+def test_franka_pick_parity_bitexact(gym):
+    """64 envs, 240 frames of the OSC pick loop (approach, grasp contacts,
+    lift): GPU state == oracle state after every frame."""
+    n, frames = 64, 240
+    sim, info, rb, dof, jac, mm, ctl = _setup(gym, n)
+    p, m = sim.mg_params(), sim.mg_model()
+    A = sim.model_arrays
+    st = A["body_state0"].copy()
+    ds = A["dof_state0"].copy()
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+    tgt[:, 0] = ds[:, 0]
+    gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(torch.from_numpy(tgt[:, 0].copy()).to(DEV)))
+    lifted = np.zeros(n, bool)
+    for f in range(frames):
+        gym.simulate(sim)
+        gym.fetch_results(sim, True)
+        oracle.step(p, m, st, ds, tgt=tgt, props=A["dof_props"])
+        pa, ea = _control(gym, sim, info, rb, dof, jac, mm, ctl, n)
+        got, got_d = rb.cpu().numpy(), dof.cpu().numpy()
+        assert np.all(np.isfinite(got))
+        if not (np.array_equal(got, st) and np.array_equal(got_d, ds)):
+            bad = np.argwhere(got != st)
+            pytest.fail("frame %d: first differing body/field %s, max |diff| %g (dof %g)"
+                        % (f, bad[:3].tolist(), np.abs(got - st).max(), np.abs(got_d - ds).max()))
+        tgt[:, 0] = pa.reshape(-1).cpu().numpy()
+        tgt[:, 2] = ea.reshape(-1).cpu().numpy()
+        lifted |= st[info["box_idxs"], 2] > 0.45
+    assert lifted.sum() >= 1      # the window reaches grasp-and-lift contacts
+
+
+def test_franka_pick_lifts_cubes(gym):
+    """256 envs, 600 frames (10 s) of the script's loop: most cubes are grasped
+    and lifted above 0.55 m (the script drops them at 0.6 m, :405)."""
+    n, frames = 256, 600
+    sim, info, rb, dof, jac, mm, ctl = _setup(gym, n)
+    maxz = torch.zeros(n, device=DEV)
+    bi = torch.tensor(info["box_idxs"], device=DEV)
+    for f in range(frames):
+        gym.simulate(sim)
+        gym.fetch_results(sim, True)
+        _control(gym, sim, info, rb, dof, jac, mm, ctl, n)
+        maxz = torch.maximum(maxz, rb[bi, 2])
+    assert torch.isfinite(rb).all()
+    frac = float((maxz > 0.55).float().mean())
+    assert frac >= 0.5, "only %.2f of the cubes were lifted" % frac
+    # nothing sinks through the table or the ground
+    assert float(rb[bi, 2].min()) > 0.0
+
+
+def test_franka_jacobian_mass_matrix_float64(gym):
+    """Device Jacobian (link origins) and CRBA mass matrix of the Franka at
+    random joint configurations vs float64 kinematics64 (rtol 1e-4)."""
+    n = 16
+    sim, info, rb, dof, jac, mm, ctl = _setup(gym, n)
+    A = sim.model_arrays
+    rng = np.random.RandomState(5)
+    props = A["dof_props"][:9]
+    lo, hi = props[:, 5], props[:, 6]
+    q = (lo + (hi - lo) * rng.uniform(0.1, 0.9, (n, 9))).astype(np.float32)
+    init = torch.zeros((9 * n, 2), dtype=torch.float32, device=DEV)
+    init[:, 0] = torch.from_numpy(q.reshape(-1)).to(DEV)
+    gym.set_dof_state_tensor(sim, gymtorch.unwrap_tensor(init))
+    gym.refresh_jacobian_tensors(sim)
+    gym.refresh_mass_matrix_tensors(sim)
+    art = K.Articulation(A, 0)
+    J = jac.cpu().numpy()
+    M = mm.cpu().numpy()
+    for e in range(n):
+        fb = int(A["artic_i"][e, 0])
+        base = A["body_state0"][fb]
+        Jr = art.jacobian(base, q[e].astype(np.float64))
+        Mr = art.mass_matrix(base, q[e].astype(np.float64), fb)
+        assert np.allclose(J[e], Jr, rtol=1e-4, atol=1e-5), np.abs(J[e] - Jr).max()
+        assert np.allclose(M[e], Mr, rtol=1e-4, atol=1e-5), np.abs(M[e] - Mr).max()

@@ -17,7 +17,8 @@ STUBS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "stubs")
 def _exec_script(path, cwd, monkeypatch, frames=3):
     from test_isaacgym_amd import _native as N
     monkeypatch.chdir(cwd)
-    monkeypatch.setattr(sys, "argv", [path])
+    if not any(a == path for a in sys.argv[:1]):
+        monkeypatch.setattr(sys, "argv", [path])
     monkeypatch.setenv("MIGYM_VIEWER_FRAMES", str(frames))
     monkeypatch.syspath_prepend(STUBS)
     monkeypatch.syspath_prepend(REFERENCE)
@@ -73,3 +74,25 @@ def test_test12_gimbal_setup(monkeypatch):
     assert gym.get_asset_dof_names(asset) == ["camera_z_joint", "camera_y_joint", "camera_joint"]
     assert ns["cart_dof_handle"] == -1     # missing DOF name -> INVALID_HANDLE, no exception (:100)
     assert tuple(ns["dof_state"].shape) == (3, 2)
+
+
+@pytest.mark.skipif(has_gpu(), reason="CPU-container variant")
+def test_franka_cube_ik_osc_setup(monkeypatch):
+    """examples/franka_cube_ik_osc.py (S3) unmodified, 16 envs, OSC controller."""
+    path = os.path.join(REFERENCE, "examples", "franka_cube_ik_osc.py")
+    monkeypatch.setattr(sys, "argv", [path, "--num_envs", "16", "--controller", "osc", "--pipeline", "cpu"])
+    ns, err = _exec_script(path, os.path.join(REFERENCE, "examples"), monkeypatch)
+    assert err is not None
+    gym, sim = ns["gym"], ns["sim"]
+    assert len(ns["envs"]) == 16
+    # 13 bodies per env: table, box, 11 Franka links (panda_link8 absent, SURVEY.md §8a a4)
+    assert gym.get_sim_rigid_body_count(sim) == 16 * 13
+    assert ns["franka_hand_index"] == 8
+    assert ns["box_idxs"][:2] == [1, 14] and ns["hand_idxs"][:2] == [10, 23]
+    assert tuple(ns["jacobian"].shape) == (16, 10, 6, 9)
+    assert tuple(ns["mm"].shape) == (16, 7, 7)
+    assert tuple(ns["dof_pos"].shape) == (16, 9, 1)
+    # the packed model routes every env through the coupled per-env step: the
+    # cube and the table share group i (filter 0), the Franka has filter 2
+    A = sim.model_arrays
+    assert (A["actor_coll"][:3, :3] == [[0, 0, 0], [0, 0, 0], [0, 0, 2]]).all()
