@@ -105,6 +105,61 @@ def gimbal_rate(n, steps, warmup, dev):
             "algorithmic_bytes_per_env": 532}
 
 
+def franka_rate(n, steps, warmup, dev):
+    """S3 Franka cube pick: examples/franka_cube_ik_osc.py's
+    loop at n envs, OSC controller: simulate -> fetch_results -> refresh rigid-body /
+    DOF / Jacobian / mass-matrix tensors -> the script's controller on the device
+    (test_isaacgym_amd.franka_control) -> set DOF position targets and efforts.
+    Returns env-steps/s and the coupled-step kernel time."""
+    from test_isaacgym_amd import franka_control
+    gym = gymapi.acquire_gym()
+    sim, info = scenes.franka_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
+    gym.prepare_sim(sim)
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    jac = gymtorch.wrap_tensor(gym.acquire_jacobian_tensor(sim, "franka"))
+    mm = gymtorch.wrap_tensor(gym.acquire_mass_matrix_tensor(sim, "franka"))
+    ctl = franka_control.CubePick(n, info["init_pos"], info["init_rot"], info["default_dof_pos"], dev)
+    h = info["hand_index"]
+    bi = torch.tensor(info["box_idxs"], device=dev)
+    hi = torch.tensor(info["hand_idxs"], device=dev)
+    j_eef = jac[:, h - 1, :, :7]
+    mm7 = mm[:, :7, :7]
+    dp = dof[:, 0].view(n, 9, 1)
+    dv = dof[:, 1].view(n, 9, 1)
+    lifted = torch.zeros(n, dtype=torch.bool, device=dev)
+
+    def step():
+        gym.simulate(sim)
+        gym.fetch_results(sim, False)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_dof_state_tensor(sim)
+        gym.refresh_jacobian_tensors(sim)
+        gym.refresh_mass_matrix_tensors(sim)
+        pa, ea = ctl.step(rb, dp, dv, j_eef, mm7, bi, hi)
+        gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(pa))
+        gym.set_dof_actuation_force_tensor(sim, gymtorch.unwrap_tensor(ea))
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+        lifted |= rb[bi, 2] > 0.55
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    avg = ctypes.c_float()
+    used = N.lib.mg_step_time_stats(sim.native, min(steps, 512), ctypes.byref(avg), None, None)
+    out = {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
+           "kernel": "k_env_step<16,12>", "kernel_ms_avg": avg.value if used > 0 else None,
+           "coupled_envs": int(N.lib.mg_num_coupled_envs(sim.native)),
+           "cubes_lifted_frac": float(lifted.float().mean()),
+           "controller": "OSC (franka_cube_ik_osc.py:59-79,348-410) on the device"}
+    gym.destroy_sim(sim)
+    return out
+
+
 def load_traffic(envs):
     """HBM bytes per k_rigid_step launch at this env count from the committed
     rocprofv3 PMC passes (profiles/r01_pmc_rigid_<envs>.json, written by
@@ -127,6 +182,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-gimbal", action="store_true", help="skip the secondary S2 servo-arm measurement")
+    ap.add_argument("--no-franka", action="store_true", help="skip the secondary S3 Franka cube-pick measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -235,6 +291,8 @@ def main():
         }
         if world == 1 and not args.no_gimbal:
             out["s2_servo_arm"] = gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev)
+        if world == 1 and not args.no_franka:
+            out["s3_franka"] = franka_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline"]["cores"] = 1

@@ -9,9 +9,9 @@
  * the rule in include/migym.h (actor_coll), independently of the library.
  */
 
-#define OE_MAXF 4
+#define OE_MAXF 2
 #define OE_MAXS 4
-#define OE_MAXCT 20
+#define OE_MAXCT 16
 #define OE_F0 16
 #define OE_PMAX 4
 
@@ -284,108 +284,86 @@ static void ground_pair_(const step_t* P, const cshape_t* s, pair_t* o) {
     }
 }
 
-typedef struct {
-    int a, b;
-    v3_t d[3], ra, rb;
-    float s0, mu, e, vn0, k[3], lam[3];
-} ect_t;
-
 /* env description, as the library's env_i row but with global body ids */
 typedef struct {
     int art_body, art_dof, art_tmpl, nf, free_b[OE_MAXF], ns, stat_b[OE_MAXS], mask;
 } oenv_t;
 
-typedef struct {
-    const step_t* P;
-    const mg_model* m;
-    const float* props;
-    const float* tgt;
-    float* state;
-    int L, D;
-    const int* LI;
-    int nct;
-    ect_t ct[OE_MAXCT];
-    float Jr[OE_MAXCT * 3][OR_MAXL], Wr[OE_MAXCT * 3][OR_MAXL];
-    float q[OR_MAXL], qd[OR_MAXL], dq[OR_MAXL];
-    v3_t fv[OE_MAXF], fw[OE_MAXF], fdx[OE_MAXF], fdth[OE_MAXF], fxc[OE_MAXF];
-    float finvm[OE_MAXF];
-    s3_t fIw[OE_MAXF];
-} ectx_t;
+#define OE_G 16
+#define OE_ST0 32
 
-static void eadd_(ectx_t* X, int a, int b, const pair_t* o, float mu, float rest) {
-    int j;
-    for (j = 0; j < o->n; ++j) {
-        ect_t* c;
-        if (X->nct >= OE_MAXCT) return;
-        c = &X->ct[X->nct];
-        c->a = a; c->b = b;
-        c->d[0] = o->nrm[j];
-        tangents_(o->nrm[j], &c->d[1], &c->d[2]);
-        c->ra = a >= OE_F0 ? sub3(o->p[j], X->fxc[a - OE_F0]) : o->p[j];
-        c->rb = b >= OE_F0 ? sub3(o->p[j], X->fxc[b - OE_F0]) : V(0.0f, 0.0f, 0.0f);
-        c->s0 = o->sep[j] - X->P->ro;
-        c->mu = mu; c->e = rest;
-        X->nct = X->nct + 1;
-    }
+/* sum of 16 slots in the device's DPP order (mg_env.hip red16): row_ror 8,
+ * row_ror 4, quad xor 2, quad xor 1; every lane ends with this value */
+static float red16_(const float* v) {
+    float s[16], t[16], u0, u1;
+    int i;
+    for (i = 0; i < 16; ++i) s[i] = v[i] + v[(i + 8) & 15];
+    for (i = 0; i < 4; ++i) t[i] = s[i] + s[(i + 4) & 15];
+    u0 = t[0] + t[2];
+    u1 = t[1] + t[3];
+    return u0 + u1;
+}
+static float red16_prod_(const float* a, const float* b) {
+    float v[16];
+    int i;
+    for (i = 0; i < 16; ++i) v[i] = a[i] * b[i];
+    return red16_(v);
 }
 
-static float erel_(const ectx_t* X, const ect_t* C, int c, int rw, int motion) {
-    const v3_t dir = C->d[rw];
-    float va = 0.0f, vb = 0.0f;
-    int d;
-    if (C->a >= OE_F0) {
-        const int k = C->a - OE_F0;
-        va = motion ? dot3(dir, X->fdx[k]) + dot3(X->fdth[k], cross3(C->ra, dir))
-                    : dot3(dir, X->fv[k]) + dot3(X->fw[k], cross3(C->ra, dir));
-    } else {
-        const float* J = X->Jr[c * 3 + rw];
-        for (d = 0; d < X->D; ++d) va = va + J[d] * (motion ? X->dq[d] : X->qd[d]);
-    }
-    if (C->b >= OE_F0) {
-        const int k = C->b - OE_F0;
-        vb = motion ? dot3(dir, X->fdx[k]) + dot3(X->fdth[k], cross3(C->rb, dir))
-                    : dot3(dir, X->fv[k]) + dot3(X->fw[k], cross3(C->rb, dir));
-    }
-    return va - vb;
-}
+typedef struct { int a, sa, b, sb; } epair_t;
 
-static void eapply_(ectx_t* X, const ect_t* C, int c, int rw, float dl) {
-    const v3_t dir = C->d[rw];
-    int d;
-    if (C->a >= OE_F0) {
-        const int k = C->a - OE_F0;
-        X->fv[k] = mad3(X->fv[k], dir, dl * X->finvm[k]);
-        X->fw[k] = mad3(X->fw[k], symmul_(X->fIw[k], cross3(C->ra, dir)), dl);
-    } else {
-        const float* W = X->Wr[c * 3 + rw];
-        for (d = 0; d < X->D; ++d) X->qd[d] = X->qd[d] + W[d] * dl;
+/* candidate shape pairs of an env, in the device's order (migym_capi.cpp upload) */
+static int env_pairs_(const mg_model* m, const oenv_t* ev, int ground, int L, epair_t* out, int cap) {
+    static const int pb[4][4] = {{-1, 0, 1, 2}, {-1, -1, 3, 4}, {-1, -1, -1, 5}, {-1, -1, -1, -1}};
+    int n = 0, k, j, t, l, sa, sb;
+#define OE_PUSH(A_, SA_, B_, SB_) do { if (n < cap) { out[n].a = (A_); out[n].sa = (SA_); out[n].b = (B_); out[n].sb = (SB_); } n++; } while (0)
+#define OE_SHP(B_, S0_, NS_) do { const int* t_ = m->tmpl_body_i + (size_t)m->body_tmpl[B_] * MG_TBODY_I_N; S0_ = t_[0]; NS_ = t_[1]; } while (0)
+    for (k = 0; k < ev->nf; ++k) {
+        int sa0, nsa;
+        OE_SHP(ev->free_b[k], sa0, nsa);
+        for (sa = sa0; sa < sa0 + nsa; ++sa) {
+            if (ground) OE_PUSH(OE_F0 + k, sa, -1, -1);
+            for (t = 0; t < ev->ns; ++t) {
+                int sb0, nsb;
+                if (!((ev->mask >> (14 + 4 * k + t)) & 1)) continue;
+                OE_SHP(ev->stat_b[t], sb0, nsb);
+                for (sb = sb0; sb < sb0 + nsb; ++sb) OE_PUSH(OE_F0 + k, sa, OE_ST0 + t, sb);
+            }
+            for (j = k + 1; j < ev->nf; ++j) {
+                int sb0, nsb;
+                if (!((ev->mask >> (8 + pb[k][j])) & 1)) continue;
+                OE_SHP(ev->free_b[j], sb0, nsb);
+                for (sb = sb0; sb < sb0 + nsb; ++sb) OE_PUSH(OE_F0 + k, sa, OE_F0 + j, sb);
+            }
+            if (ev->art_body >= 0 && ((ev->mask >> k) & 1)) {
+                int sb0, nsb;
+                OE_SHP(ev->art_body, sb0, nsb);
+                for (sb = sb0; sb < sb0 + nsb; ++sb) OE_PUSH(OE_F0 + k, sa, 0, sb);
+            }
+        }
     }
-    if (C->b >= OE_F0) {
-        const int k = C->b - OE_F0;
-        X->fv[k] = mad3(X->fv[k], dir, -(dl * X->finvm[k]));
-        X->fw[k] = mad3(X->fw[k], symmul_(X->fIw[k], cross3(C->rb, dir)), -dl);
+    for (l = 1; l < L; ++l) {
+        int sa0, nsa;
+        OE_SHP(ev->art_body + l, sa0, nsa);
+        for (sa = sa0; sa < sa0 + nsa; ++sa) {
+            if (ground) OE_PUSH(l, sa, -1, -1);
+            for (t = 0; t < ev->ns; ++t) {
+                int sb0, nsb;
+                if (!((ev->mask >> (4 + t)) & 1)) continue;
+                OE_SHP(ev->stat_b[t], sb0, nsb);
+                for (sb = sb0; sb < sb0 + nsb; ++sb) OE_PUSH(l, sa, OE_ST0 + t, sb);
+            }
+            for (k = 0; k < ev->nf; ++k) {
+                int sb0, nsb;
+                if (!((ev->mask >> k) & 1)) continue;
+                OE_SHP(ev->free_b[k], sb0, nsb);
+                for (sb = sb0; sb < sb0 + nsb; ++sb) OE_PUSH(l, sa, OE_F0 + k, sb);
+            }
+        }
     }
-}
-
-static void enormal_(ectx_t* X, int c, float tgt) {
-    ect_t* C = &X->ct[c];
-    float dl = C->k[0] * (tgt - erel_(X, C, c, 0, 0));
-    const float nl = fmaxf(C->lam[0] + dl, 0.0f);
-    dl = nl - C->lam[0];
-    C->lam[0] = nl;
-    eapply_(X, C, c, 0, dl);
-}
-
-static void efriction_(ectx_t* X, int c) {
-    ect_t* C = &X->ct[c];
-    const float lim = C->mu * C->lam[0];
-    int rw;
-    for (rw = 1; rw < 3; ++rw) {
-        const float nl = fminf(fmaxf(C->lam[rw] - C->k[rw] * erel_(X, C, c, rw, 0), -lim), lim);
-        const float dl = nl - C->lam[rw];
-        C->lam[rw] = nl;
-        eapply_(X, C, c, rw, dl);
-    }
+#undef OE_PUSH
+#undef OE_SHP
+    return n;
 }
 
 static const float* shp_(const mg_model* m, int s) { return m->shapes + (size_t)s * MG_SHAPE_STRIDE; }
@@ -399,32 +377,48 @@ static si_t link_inertia_(const float* M) {
     return sirigid_(mass, com, mmul_(mmul_(Rq, M3c(V(Id.x, 0.0f, 0.0f), V(0.0f, Id.y, 0.0f), V(0.0f, 0.0f, Id.z))), mt_(Rq)));
 }
 
+#define OE_MAXPAIRS 512
+
 static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float* state, float* dof, const float* tgt,
                      const float* props, const float* ext, float* cforce) {
-    static ectx_t X;   /* large scratch; the oracle is single-threaded */
-    const int b0 = ev->art_body, d0 = ev->art_dof, nfr = ev->nf, nst = ev->ns, cmask = ev->mask;
+    const int b0 = ev->art_body, d0 = ev->art_dof, nfr = ev->nf;
     const int* ti = ev->art_tmpl >= 0 ? m->artic_tmpl_i + (size_t)ev->art_tmpl * MG_ATMPL_I_N : NULL;
     const int L = ti ? ti[1] : 0, D = ti ? ti[2] : 0;
     const float* LF = ti ? m->tmpl_link_f + (size_t)ti[0] * MG_LINK_F_N : NULL;
     const int* LI = ti ? m->tmpl_link_i + (size_t)ti[0] * MG_LINK_I_N : NULL;
     const float h = P->h;
     const v3_t gvec = V(P->g[0], P->g[1], P->g[2]);
+    static epair_t pairs[OE_MAXPAIRS];
+    int npair;
     v3_t x0 = V(0.0f, 0.0f, 0.0f), gb = V(0.0f, 0.0f, 0.0f);
     q4_t q0 = Q(0.0f, 0.0f, 0.0f, 1.0f);
-    float mdiag[OR_MAXL], qdd[OR_MAXL], tau0d[OR_MAXL], impd[OR_MAXL];
-    v3_t lsum[OR_MAXL];
-    v3_t fx[OE_MAXF], fcom[OE_MAXF], finvI[OE_MAXF], fsum[OE_MAXF], fext[OE_MAXF], text[OE_MAXF];
-    q4_t fq[OE_MAXF], fiq[OE_MAXF];
-    float lkeep[OE_MAXF], akeep[OE_MAXF], mlv2[OE_MAXF], mav2[OE_MAXF], gon[OE_MAXF];
+    /* slots */
+    float q[OE_G], u[OE_G], dp[OE_G], qdd[OE_G], mdiag[OE_G], tau0d[OE_G], impd[OE_G];
+    /* links */
     m3_t E[OR_MAXL];
-    v3_t r[OR_MAXL], xl[OR_MAXL], zl[OR_MAXL];
+    v3_t r[OR_MAXL], xl[OR_MAXL], zl[OR_MAXL], lsum[OR_MAXL];
+    q4_t ql[OR_MAXL];
     sv_t Sj[OR_MAXL], vl[OR_MAXL], cl[OR_MAXL], pA[OR_MAXL], U[OR_MAXL], al[OR_MAXL];
     si_t IA[OR_MAXL];
-    float Dl[OR_MAXL], ul[OR_MAXL], Mf[OR_MAXL][OR_MAXL], invd[OR_MAXL];
-    q4_t ql[OR_MAXL];
-    int d, l, k, c, st_, it;
-    if (L > OR_MAXL || (ti && !ti[3])) return -1;
-    X.P = P; X.m = m; X.props = props; X.tgt = tgt; X.state = state; X.L = L; X.D = D; X.LI = LI;
+    float Dl[OR_MAXL], ul[OR_MAXL];
+    int amask[OR_MAXL], dlink[OE_G], drev[OE_G];
+    static float Lc[OE_G][OE_G], Mi[OE_G][OE_G];
+    float invd[OE_G];
+    /* free bodies */
+    v3_t fx[OE_MAXF], fxc[OE_MAXF], fcom[OE_MAXF], finvI[OE_MAXF], fext[OE_MAXF], text[OE_MAXF], fsum[OE_MAXF];
+    q4_t fq[OE_MAXF], fiq[OE_MAXF];
+    float finvm[OE_MAXF], lkeep[OE_MAXF], akeep[OE_MAXF], mlv2[OE_MAXF], mav2[OE_MAXF], gon[OE_MAXF];
+    s3_t fIw[OE_MAXF];
+    /* contacts and rows */
+    int ca[OE_MAXCT], cb[OE_MAXCT];
+    v3_t cp[OE_MAXCT], cd[OE_MAXCT][3];
+    float cs0[OE_MAXCT], cmu[OE_MAXCT], ce[OE_MAXCT], cvn0[OE_MAXCT], ck[OE_MAXCT][3], clam[OE_MAXCT][3];
+    static float Jr[OE_MAXCT * 3][OE_G], Wr[OE_MAXCT * 3][OE_G];
+    int d, l, k, c, i, j, st_, it;
+    if (L > OR_MAXL || (ti && !ti[3]) || D + 6 * nfr > OE_G || nfr > OE_MAXF) return -1;
+    npair = env_pairs_(m, ev, P->ground, L, pairs, OE_MAXPAIRS);
+    if (npair > OE_MAXPAIRS) return -1;
+    for (i = 0; i < OE_G; ++i) { q[i] = 0.0f; u[i] = 0.0f; dp[i] = 0.0f; }
     if (L > 0) {
         const float* s0 = state + (size_t)b0 * MG_STATE_N;
         const float grav_on = m->tmpl_body_f[(size_t)m->body_tmpl[b0] * MG_TBODY_F_N + 4];
@@ -432,8 +426,13 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         q0 = qnorm_(Q(s0[3], s0[4], s0[5], s0[6]));
         gb = qrot_(Q(-q0.x, -q0.y, -q0.z, q0.w), grav_on != 0.0f ? gvec : V(0.0f, 0.0f, 0.0f));
     }
-    for (d = 0; d < D; ++d) { X.q[d] = dof[(d0 + d) * 2 + 0]; X.qd[d] = dof[(d0 + d) * 2 + 1]; }
-    for (l = 0; l < L; ++l) lsum[l] = V(0.0f, 0.0f, 0.0f);
+    for (l = 0; l < L; ++l) {
+        const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
+        amask[l] = (p >= 0 ? amask[p] : 0) | (dj >= 0 ? (1 << dj) : 0);
+        if (dj >= 0) { dlink[dj] = l; drev[dj] = LI[l * MG_LINK_I_N + 1] == MG_JOINT_REVOLUTE ? 1 : 0; }
+        lsum[l] = V(0.0f, 0.0f, 0.0f);
+    }
+    for (d = 0; d < D; ++d) { q[d] = dof[(d0 + d) * 2 + 0]; u[d] = dof[(d0 + d) * 2 + 1]; }
     for (k = 0; k < nfr; ++k) {
         const int b = ev->free_b[k];
         const float* s = state + (size_t)b * MG_STATE_N;
@@ -441,9 +440,8 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         const float* tf = m->tmpl_body_f + (size_t)m->body_tmpl[b] * MG_TBODY_F_N;
         fx[k] = V(s[0], s[1], s[2]);
         fq[k] = qnorm_(Q(s[3], s[4], s[5], s[6]));
-        X.fv[k] = V(s[7], s[8], s[9]);
-        X.fw[k] = V(s[10], s[11], s[12]);
-        X.finvm[k] = M[0];
+        for (i = 0; i < 6; ++i) u[D + 6 * k + i] = s[7 + i];
+        finvm[k] = M[0];
         finvI[k] = V(M[1], M[2], M[3]);
         fiq[k] = Q(M[4], M[5], M[6], M[7]);
         fcom[k] = V(M[8], M[9], M[10]);
@@ -462,236 +460,192 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     }
 
     for (st_ = 0; st_ < P->substeps; ++st_) {
-        int first_link_row;
+        int nct = 0, link_rows = 0;
+        /* ---- 1. unconstrained motion */
         if (L > 0) {
-          unsigned xmask = 0u, xpos = 0u;
-          int att;
-          for (att = 0; att < 2; ++att) {
-            unsigned nm;
-            for (l = 0; l < L; ++l) {
-                const int p = LI[l * MG_LINK_I_N + 0], jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
-                if (p < 0) {
-                    E[l] = M3c(V(1.0f, 0.0f, 0.0f), V(0.0f, 1.0f, 0.0f), V(0.0f, 0.0f, 1.0f));
-                    r[l] = V(0.0f, 0.0f, 0.0f);
-                    Sj[l] = sv0(); vl[l] = sv0(); cl[l] = sv0();
-                    ql[l] = q0; xl[l] = x0; zl[l] = V(0.0f, 0.0f, 0.0f);
-                } else {
-                    q4_t qrel; v3_t rr; sv_t s, vJ;
-                    const float* lf = LF + l * MG_LINK_F_N;
-                    const float qj = dj >= 0 ? X.q[dj] : 0.0f, qdj = dj >= 0 ? X.qd[dj] : 0.0f;
-                    joint_(lf, jt, qj, &qrel, &rr, &s);
-                    E[l] = mt_(qmat_(qrel));
-                    r[l] = rr;
-                    Sj[l] = s;
-                    vJ = svmul_(s, qdj);
-                    vl[l] = svadd_(xmot_(E[l], rr, vl[p]), vJ);
-                    cl[l] = crm_(vl[l], vJ);
-                    ql[l] = qnorm_(qmul_(ql[p], qrel));
-                    xl[l] = add3(xl[p], qrot_(ql[p], rr));
-                    zl[l] = qrot_(ql[l], V(lf[7], lf[8], lf[9]));
-                }
-                IA[l] = link_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N);
-                pA[l] = crf_(vl[l], simul_(IA[l], vl[l]));
-            }
-            for (l = L - 1; l >= 1; --l) {
-                const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
-                si_t Ia = IA[l];
-                sv_t pa;
-                if (dj >= 0) {
-                    const float* pr = props + (size_t)(d0 + dj) * MG_DOFPROP_N;
-                    const float* tg = tgt + (size_t)(d0 + dj) * 3;
-                    const int mode = (int)pr[0];
-                    const float kp = pr[1], kd = pr[2], eff = pr[3], arm = pr[8];
-                    float tau = 0.0f, imp = 0.0f, invD;
-                    if (mode == MG_DOF_MODE_POS) {
-                        tau = kp * (tg[0] - X.q[dj] - h * X.qd[dj]) + kd * (tg[1] - X.qd[dj]);
-                        imp = h * kd + h * h * kp;
-                    } else if (mode == MG_DOF_MODE_VEL) {
-                        tau = kd * (tg[1] - X.qd[dj]);
-                        imp = h * kd;
-                    } else if (mode == MG_DOF_MODE_EFFORT) {
-                        tau = tg[2];
+            unsigned xmask = 0u, xpos = 0u;
+            int att;
+            for (att = 0; att < 2; ++att) {
+                unsigned nm;
+                for (l = 0; l < L; ++l) {
+                    const int p = LI[l * MG_LINK_I_N + 0], jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
+                    if (p < 0) {
+                        E[l] = M3c(V(1.0f, 0.0f, 0.0f), V(0.0f, 1.0f, 0.0f), V(0.0f, 0.0f, 1.0f));
+                        r[l] = V(0.0f, 0.0f, 0.0f);
+                        Sj[l] = sv0(); vl[l] = sv0(); cl[l] = sv0();
+                        ql[l] = q0; xl[l] = x0; zl[l] = V(0.0f, 0.0f, 0.0f);
+                    } else {
+                        q4_t qrel; v3_t rr; sv_t sj, vJ;
+                        const float* lf = LF + l * MG_LINK_F_N;
+                        const float qj = dj >= 0 ? q[dj] : 0.0f, qdj = dj >= 0 ? u[dj] : 0.0f;
+                        joint_(lf, jt, qj, &qrel, &rr, &sj);
+                        E[l] = mt_(qmat_(qrel));
+                        r[l] = rr;
+                        Sj[l] = sj;
+                        vJ = svmul_(sj, qdj);
+                        vl[l] = svadd_(xmot_(E[l], rr, vl[p]), vJ);
+                        cl[l] = crm_(vl[l], vJ);
+                        ql[l] = qnorm_(qmul_(ql[p], qrel));
+                        xl[l] = add3(xl[p], qrot_(ql[p], rr));
+                        zl[l] = qrot_(ql[l], V(lf[7], lf[8], lf[9]));
                     }
-                    if (eff > 0.0f) {
-                        if ((xmask >> dj) & 1u) {
-                            tau = ((xpos >> dj) & 1u) ? eff : -eff;
-                            imp = 0.0f;
-                        } else if (imp == 0.0f) {
-                            tau = fminf(fmaxf(tau, -eff), eff);
+                    IA[l] = link_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N);
+                    pA[l] = crf_(vl[l], simul_(IA[l], vl[l]));
+                }
+                for (l = L - 1; l >= 1; --l) {
+                    const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
+                    si_t Ia = IA[l];
+                    sv_t pa;
+                    if (dj >= 0) {
+                        const float* pr = props + (size_t)(d0 + dj) * MG_DOFPROP_N;
+                        const float* tg = tgt + (size_t)(d0 + dj) * 3;
+                        const int mode = (int)pr[0];
+                        const float kp = pr[1], kd = pr[2], eff = pr[3], arm = pr[8];
+                        const float qv = q[dj], uv = u[dj];
+                        float tau = 0.0f, imp = 0.0f, invD;
+                        if (mode == MG_DOF_MODE_POS) {
+                            tau = kp * (tg[0] - qv - h * uv) + kd * (tg[1] - uv);
+                            imp = h * kd + h * h * kp;
+                        } else if (mode == MG_DOF_MODE_VEL) {
+                            tau = kd * (tg[1] - uv);
+                            imp = h * kd;
+                        } else if (mode == MG_DOF_MODE_EFFORT) {
+                            tau = tg[2];
                         }
+                        if (eff > 0.0f) {
+                            if ((xmask >> dj) & 1u) {
+                                tau = ((xpos >> dj) & 1u) ? eff : -eff;
+                                imp = 0.0f;
+                            } else if (imp == 0.0f) {
+                                tau = fminf(fmaxf(tau, -eff), eff);
+                            }
+                        }
+                        tau0d[dj] = tau;
+                        impd[dj] = imp;
+                        mdiag[dj] = arm + imp;
+                        U[l] = simul_(Ia, Sj[l]);
+                        Dl[l] = svdot_(Sj[l], U[l]) + arm + imp;
+                        ul[l] = tau - svdot_(Sj[l], pA[l]);
+                        invD = 1.0f / Dl[l];
+                        Ia.A = msub_(Ia.A, mouter_(U[l].w, U[l].w, invD));
+                        Ia.B = msub_(Ia.B, mouter_(U[l].w, U[l].v, invD));
+                        Ia.C = msub_(Ia.C, mouter_(U[l].v, U[l].v, invD));
+                        pa = svadd_(svadd_(pA[l], simul_(Ia, cl[l])), svmul_(U[l], ul[l] * invD));
+                    } else {
+                        pa = svadd_(pA[l], simul_(Ia, cl[l]));
                     }
-                    tau0d[dj] = tau;
-                    impd[dj] = imp;
-                    mdiag[dj] = arm + imp;
-                    U[l] = simul_(Ia, Sj[l]);
-                    Dl[l] = svdot_(Sj[l], U[l]) + arm + imp;
-                    ul[l] = tau - svdot_(Sj[l], pA[l]);
-                    invD = 1.0f / Dl[l];
-                    Ia.A = msub_(Ia.A, mouter_(U[l].w, U[l].w, invD));
-                    Ia.B = msub_(Ia.B, mouter_(U[l].w, U[l].v, invD));
-                    Ia.C = msub_(Ia.C, mouter_(U[l].v, U[l].v, invD));
-                    pa = svadd_(svadd_(pA[l], simul_(Ia, cl[l])), svmul_(U[l], ul[l] * invD));
-                } else {
-                    pa = svadd_(pA[l], simul_(Ia, cl[l]));
+                    if (p > 0) {
+                        IA[p] = siadd_(IA[p], xin_t_(E[l], r[l], Ia));
+                        pA[p] = svadd_(pA[p], xfrc_t_(E[l], r[l], pa));
+                    }
                 }
-                if (p > 0) {
-                    IA[p] = siadd_(IA[p], xin_t_(E[l], r[l], Ia));
-                    pA[p] = svadd_(pA[p], xfrc_t_(E[l], r[l], pa));
+                al[0] = SVc(V(0.0f, 0.0f, 0.0f), mul3(gb, -1.0f));
+                for (l = 1; l < L; ++l) {
+                    const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
+                    sv_t ap = svadd_(xmot_(E[l], r[l], al[p]), cl[l]);
+                    if (dj >= 0) {
+                        const float acc = (ul[l] - svdot_(U[l], ap)) / Dl[l];
+                        qdd[dj] = acc;
+                        ap = svadd_(ap, svmul_(Sj[l], acc));
+                    }
+                    al[l] = ap;
                 }
-            }
-            al[0] = SVc(V(0.0f, 0.0f, 0.0f), mul3(gb, -1.0f));
-            for (l = 1; l < L; ++l) {
-                const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
-                sv_t ap = svadd_(xmot_(E[l], r[l], al[p]), cl[l]);
-                if (dj >= 0) {
-                    const float acc = (ul[l] - svdot_(U[l], ap)) / Dl[l];
-                    qdd[dj] = acc;
-                    ap = svadd_(ap, svmul_(Sj[l], acc));
+                nm = xmask;
+                for (d = 0; d < D; ++d) {
+                    const float eff = props[(size_t)(d0 + d) * MG_DOFPROP_N + 3];
+                    if (eff > 0.0f && impd[d] != 0.0f) {
+                        const float act = tau0d[d] - impd[d] * qdd[d];
+                        if (act > eff) { nm |= 1u << d; xpos |= 1u << d; }
+                        else if (act < -eff) nm |= 1u << d;
+                    }
                 }
-                al[l] = ap;
-            }
-            nm = xmask;
-            for (d = 0; d < D; ++d) {
-                const float eff = props[(size_t)(d0 + d) * MG_DOFPROP_N + 3];
-                if (eff > 0.0f && impd[d] != 0.0f) {
-                    const float act = tau0d[d] - impd[d] * qdd[d];
-                    if (act > eff) { nm |= 1u << d; xpos |= 1u << d; }
-                    else if (act < -eff) nm |= 1u << d;
-                }
-            }
-            if (nm == xmask) break;
-            xmask = nm;
-          }
-            for (d = 0; d < D; ++d) {
-                const float maxv = props[(size_t)(d0 + d) * MG_DOFPROP_N + 4];
-                float w = X.qd[d] + h * qdd[d];
-                if (maxv > 0.0f) w = fminf(fmaxf(w, -maxv), maxv);
-                X.qd[d] = w;
-                X.dq[d] = 0.0f;
+                if (nm == xmask) break;
+                xmask = nm;
             }
         }
         for (k = 0; k < nfr; ++k) {
-            v3_t v = X.fv[k], w = X.fw[k];
+            const int s0 = D + 6 * k;
+            const s3_t Iw = sym_rdrt_(qmat_(qmul_(fq[k], fiq[k])), finvI[k]);
+            v3_t v = V(u[s0 + 0], u[s0 + 1], u[s0 + 2]), w = V(u[s0 + 3], u[s0 + 4], u[s0 + 5]);
             float v2, w2;
-            X.fIw[k] = sym_rdrt_(qmat_(qmul_(fq[k], fiq[k])), finvI[k]);
-            X.fxc[k] = add3(fx[k], qrot_(fq[k], fcom[k]));
+            fIw[k] = Iw;
+            fxc[k] = add3(fx[k], qrot_(fq[k], fcom[k]));
             if (gon[k] != 0.0f) v = mad3(v, gvec, h);
-            v = mad3(v, fext[k], X.finvm[k] * h);
-            w = mad3(w, symmul_(X.fIw[k], text[k]), h);
+            v = mad3(v, fext[k], finvm[k] * h);
+            w = mad3(w, symmul_(Iw, text[k]), h);
             v = mul3(v, lkeep[k]);
             w = mul3(w, akeep[k]);
             v2 = dot3(v, v);
             if (v2 > mlv2[k]) v = mul3(v, sqrtf(mlv2[k] / v2));
             w2 = dot3(w, w);
             if (w2 > mav2[k]) w = mul3(w, sqrtf(mav2[k] / w2));
-            X.fv[k] = v; X.fw[k] = w;
-            X.fdx[k] = V(0.0f, 0.0f, 0.0f); X.fdth[k] = V(0.0f, 0.0f, 0.0f);
+            u[s0 + 0] = v.x; u[s0 + 1] = v.y; u[s0 + 2] = v.z;
+            u[s0 + 3] = w.x; u[s0 + 4] = w.y; u[s0 + 5] = w.z;
         }
+        for (d = 0; d < D; ++d) {
+            const float maxv = props[(size_t)(d0 + d) * MG_DOFPROP_N + 4];
+            float w = u[d] + h * qdd[d];
+            if (maxv > 0.0f) w = fminf(fmaxf(w, -maxv), maxv);
+            u[d] = w;
+        }
+        for (i = 0; i < OE_G; ++i) dp[i] = 0.0f;
 
-        /* contacts, in the device's pair order */
-        X.nct = 0;
-        for (k = 0; k < nfr; ++k) {
-            const int bk = ev->free_b[k];
-            const int* tk = m->tmpl_body_i + (size_t)m->body_tmpl[bk] * MG_TBODY_I_N;
-            int sa, s, j, sb;
-            for (sa = tk[0]; sa < tk[0] + tk[1]; ++sa) {
-                const float* sha = shp_(m, sa);
-                const cshape_t ca = place_(sha, fx[k], fq[k]);
-                pair_t o;
-                if (P->ground) {
-                    o.n = 0;
-                    ground_pair_(P, &ca, &o);
-                    eadd_(&X, OE_F0 + k, -1, &o, 0.5f * (sha[11] + P->mu_g), 0.5f * (sha[12] + P->e_g));
+        /* ---- 2. narrow phase, pair order */
+        for (i = 0; i < npair; ++i) {
+            const epair_t* pp = &pairs[i];
+            const float* sha = shp_(m, pp->sa);
+            v3_t xa, xb;
+            q4_t qa, qb;
+            cshape_t sA, sB;
+            pair_t o;
+            float mu, rest;
+            if (pp->a >= OE_F0) { xa = fx[pp->a - OE_F0]; qa = fq[pp->a - OE_F0]; }
+            else { xa = xl[pp->a]; qa = ql[pp->a]; }
+            sA = place_(sha, xa, qa);
+            o.n = 0;
+            if (pp->b < 0) {
+                ground_pair_(P, &sA, &o);
+                mu = 0.5f * (sha[11] + P->mu_g);
+                rest = 0.5f * (sha[12] + P->e_g);
+            } else {
+                const float* shb = shp_(m, pp->sb);
+                if (pp->b >= OE_ST0) {
+                    const float* ss = state + (size_t)ev->stat_b[pp->b - OE_ST0] * MG_STATE_N;
+                    xb = V(ss[0], ss[1], ss[2]);
+                    qb = qnorm_(Q(ss[3], ss[4], ss[5], ss[6]));
+                } else if (pp->b >= OE_F0) {
+                    xb = fx[pp->b - OE_F0];
+                    qb = fq[pp->b - OE_F0];
+                } else {
+                    xb = xl[pp->b];
+                    qb = ql[pp->b];
                 }
-                for (s = 0; s < nst; ++s) {
-                    const int bs = ev->stat_b[s];
-                    const float* ss = state + (size_t)bs * MG_STATE_N;
-                    const int* ts = m->tmpl_body_i + (size_t)m->body_tmpl[bs] * MG_TBODY_I_N;
-                    const v3_t xs = V(ss[0], ss[1], ss[2]);
-                    const q4_t qs = qnorm_(Q(ss[3], ss[4], ss[5], ss[6]));
-                    if (!((cmask >> (14 + k * 4 + s)) & 1)) continue;
-                    for (sb = ts[0]; sb < ts[0] + ts[1]; ++sb) {
-                        const float* shb = shp_(m, sb);
-                        const cshape_t cb = place_(shb, xs, qs);
-                        o.n = 0;
-                        collide_(&ca, &cb, P->co, &o);
-                        eadd_(&X, OE_F0 + k, -1, &o, 0.5f * (sha[11] + shb[11]), 0.5f * (sha[12] + shb[12]));
-                    }
-                }
-                for (j = k + 1; j < nfr; ++j) {
-                    const int bit = k == 0 ? j - 1 : (k == 1 ? j + 1 : 5);
-                    const int bj = ev->free_b[j];
-                    const int* tj = m->tmpl_body_i + (size_t)m->body_tmpl[bj] * MG_TBODY_I_N;
-                    if (!((cmask >> (8 + bit)) & 1)) continue;
-                    for (sb = tj[0]; sb < tj[0] + tj[1]; ++sb) {
-                        const float* shb = shp_(m, sb);
-                        const cshape_t cb = place_(shb, fx[j], fq[j]);
-                        o.n = 0;
-                        collide_(&ca, &cb, P->co, &o);
-                        eadd_(&X, OE_F0 + k, OE_F0 + j, &o, 0.5f * (sha[11] + shb[11]), 0.5f * (sha[12] + shb[12]));
-                    }
-                }
-                if (L > 0 && ((cmask >> k) & 1)) {
-                    const int* t0 = m->tmpl_body_i + (size_t)m->body_tmpl[b0] * MG_TBODY_I_N;
-                    for (sb = t0[0]; sb < t0[0] + t0[1]; ++sb) {
-                        const float* shb = shp_(m, sb);
-                        const cshape_t cb = place_(shb, xl[0], ql[0]);
-                        o.n = 0;
-                        collide_(&ca, &cb, P->co, &o);
-                        eadd_(&X, OE_F0 + k, -1, &o, 0.5f * (sha[11] + shb[11]), 0.5f * (sha[12] + shb[12]));
-                    }
-                }
+                sB = place_(shb, xb, qb);
+                collide_(&sA, &sB, P->co, &o);
+                mu = 0.5f * (sha[11] + shb[11]);
+                rest = 0.5f * (sha[12] + shb[12]);
             }
-        }
-        first_link_row = X.nct;
-        for (l = 1; l < L; ++l) {
-            const int* tl = m->tmpl_body_i + (size_t)m->body_tmpl[b0 + l] * MG_TBODY_I_N;
-            int sa, s, sb;
-            for (sa = tl[0]; sa < tl[0] + tl[1]; ++sa) {
-                const float* sha = shp_(m, sa);
-                const cshape_t ca = place_(sha, xl[l], ql[l]);
-                pair_t o;
-                if (P->ground) {
-                    o.n = 0;
-                    ground_pair_(P, &ca, &o);
-                    eadd_(&X, l, -1, &o, 0.5f * (sha[11] + P->mu_g), 0.5f * (sha[12] + P->e_g));
-                }
-                for (s = 0; s < nst; ++s) {
-                    const int bs = ev->stat_b[s];
-                    const float* ss = state + (size_t)bs * MG_STATE_N;
-                    const int* ts = m->tmpl_body_i + (size_t)m->body_tmpl[bs] * MG_TBODY_I_N;
-                    const v3_t xs = V(ss[0], ss[1], ss[2]);
-                    const q4_t qs = qnorm_(Q(ss[3], ss[4], ss[5], ss[6]));
-                    if (!((cmask >> (4 + s)) & 1)) continue;
-                    for (sb = ts[0]; sb < ts[0] + ts[1]; ++sb) {
-                        const float* shb = shp_(m, sb);
-                        const cshape_t cb = place_(shb, xs, qs);
-                        o.n = 0;
-                        collide_(&ca, &cb, P->co, &o);
-                        eadd_(&X, l, -1, &o, 0.5f * (sha[11] + shb[11]), 0.5f * (sha[12] + shb[12]));
-                    }
-                }
-                for (k = 0; k < nfr; ++k) {
-                    const int bk = ev->free_b[k];
-                    const int* tk = m->tmpl_body_i + (size_t)m->body_tmpl[bk] * MG_TBODY_I_N;
-                    if (!((cmask >> k) & 1)) continue;
-                    for (sb = tk[0]; sb < tk[0] + tk[1]; ++sb) {
-                        const float* shb = shp_(m, sb);
-                        const cshape_t cb = place_(shb, fx[k], fq[k]);
-                        o.n = 0;
-                        collide_(&ca, &cb, P->co, &o);
-                        eadd_(&X, l, OE_F0 + k, &o, 0.5f * (sha[11] + shb[11]), 0.5f * (sha[12] + shb[12]));
-                    }
+            for (j = 0; j < o.n; ++j) {
+                if (nct < OE_MAXCT) {
+                    ca[nct] = pp->a;
+                    cb[nct] = pp->b;
+                    cp[nct] = o.p[j];
+                    cd[nct][0] = o.nrm[j];
+                    tangents_(o.nrm[j], &cd[nct][1], &cd[nct][2]);
+                    cs0[nct] = o.sep[j] - P->ro;
+                    cmu[nct] = mu;
+                    ce[nct] = rest;
+                    if (pp->a < OE_F0) link_rows = 1;
+                    nct++;
                 }
             }
         }
 
-        /* rows */
-        if (X.nct > first_link_row) {
-            int i, j;
+        /* ---- 3. rows */
+        if (link_rows) {
             for (l = 0; l < L; ++l) IA[l] = link_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N);
             for (i = 0; i < D; ++i)
-                for (j = 0; j < D; ++j) Mf[i][j] = 0.0f;
+                for (j = 0; j < D; ++j) Lc[i][j] = 0.0f;
             for (l = L - 1; l >= 1; --l) {
                 const int p = LI[l * MG_LINK_I_N + 0];
                 if (p > 0) IA[p] = siadd_(IA[p], xin_t_(E[l], r[l], IA[l]));
@@ -701,7 +655,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 sv_t Fv;
                 if (di < 0) continue;
                 Fv = simul_(IA[l], Sj[l]);
-                Mf[di][di] = svdot_(Sj[l], Fv) + mdiag[di];
+                Lc[di][di] = svdot_(Sj[l], Fv) + mdiag[di];
                 j = l;
                 while (LI[j * MG_LINK_I_N + 0] > 0) {
                     int dj;
@@ -710,119 +664,148 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     dj = LI[j * MG_LINK_I_N + 2];
                     if (dj >= 0) {
                         const float hv = svdot_(Fv, Sj[j]);
-                        Mf[di][dj] = hv;
-                        Mf[dj][di] = hv;
+                        Lc[di][dj] = hv;
+                        Lc[dj][di] = hv;
                     }
                 }
             }
             for (j = 0; j < D; ++j) {
-                float s = Mf[j][j], dj;
-                for (k = 0; k < j; ++k) s = s - Mf[j][k] * Mf[j][k];
-                dj = sqrtf(s);
-                invd[j] = 1.0f / dj;
-                Mf[j][j] = dj;
+                float s = Lc[j][j], djv;
+                for (k = 0; k < j; ++k) s = s - Lc[j][k] * Lc[j][k];
+                djv = sqrtf(s);
+                invd[j] = 1.0f / djv;
+                Lc[j][j] = djv;
                 for (i = j + 1; i < D; ++i) {
-                    float t = Mf[i][j];
-                    for (k = 0; k < j; ++k) t = t - Mf[i][k] * Mf[j][k];
-                    Mf[i][j] = t * invd[j];
+                    float t = Lc[i][j];
+                    for (k = 0; k < j; ++k) t = t - Lc[i][k] * Lc[j][k];
+                    Lc[i][j] = t * invd[j];
+                }
+            }
+            for (j = 0; j < D; ++j) {       /* column j of M_eff^-1 (device lane j) */
+                for (i = 0; i < D; ++i) {
+                    float t = i == j ? 1.0f : 0.0f;
+                    for (k = 0; k < i; ++k) t = t - Lc[i][k] * Mi[k][j];
+                    Mi[i][j] = t * invd[i];
+                }
+                for (i = D - 1; i >= 0; --i) {
+                    float t = Mi[i][j];
+                    for (k = i + 1; k < D; ++k) t = t - Lc[k][i] * Mi[k][j];
+                    Mi[i][j] = t * invd[i];
                 }
             }
         }
-        for (c = 0; c < X.nct; ++c) {
-            ect_t* C = &X.ct[c];
-            const v3_t pw = C->a < OE_F0 ? C->ra : add3(C->ra, X.fxc[C->a - OE_F0]);
+        for (c = 0; c < nct; ++c) {
+            const int a = ca[c], b = cb[c];
+            const v3_t p = cp[c];
             int rw;
             for (rw = 0; rw < 3; ++rw) {
-                const v3_t dir = C->d[rw];
-                float wa = 0.0f, wb = 0.0f;
-                if (C->a >= OE_F0) {
-                    const int kk = C->a - OE_F0;
-                    const v3_t rd = cross3(C->ra, dir);
-                    wa = X.finvm[kk] + dot3(rd, symmul_(X.fIw[kk], rd));
-                } else {
-                    float* J = X.Jr[c * 3 + rw];
-                    float* W = X.Wr[c * 3 + rw];
-                    int j = C->a, i;
-                    for (d = 0; d < D; ++d) J[d] = 0.0f;
-                    while (j > 0) {
-                        const int dof_ = LI[j * MG_LINK_I_N + 2];
-                        if (dof_ >= 0) {
-                            if (LI[j * MG_LINK_I_N + 1] == MG_JOINT_REVOLUTE) J[dof_] = dot3(cross3(zl[j], sub3(pw, xl[j])), dir);
-                            else J[dof_] = dot3(zl[j], dir);
+                const v3_t dir = cd[c][rw];
+                float* J = Jr[c * 3 + rw];
+                float* W = Wr[c * 3 + rw];
+                int ln;
+                for (ln = 0; ln < OE_G; ++ln) {
+                    float Jv = 0.0f, Wv = 0.0f;
+                    if (ln < D) {
+                        if (a < OE_F0 && ((amask[a] >> ln) & 1)) {
+                            const int jl = dlink[ln];
+                            Jv = drev[ln] ? dot3(cross3(zl[jl], sub3(p, xl[jl])), dir) : dot3(zl[jl], dir);
                         }
-                        j = LI[j * MG_LINK_I_N + 0];
+                    } else if ((ln - D) / 6 < nfr) {
+                        const int fk = (ln - D) / 6, fc = (ln - D) % 6;
+                        const float sg = a == OE_F0 + fk ? 1.0f : (b == OE_F0 + fk ? -1.0f : 0.0f);
+                        if (sg != 0.0f) {
+                            const v3_t rd = cross3(sub3(p, fxc[fk]), dir);
+                            if (fc < 3) {
+                                const float dc = fc == 0 ? dir.x : (fc == 1 ? dir.y : dir.z);
+                                Jv = sg * dc;
+                                Wv = sg * (finvm[fk] * dc);
+                            } else {
+                                const v3_t iw = symmul_(fIw[fk], rd);
+                                Jv = sg * (fc == 3 ? rd.x : (fc == 4 ? rd.y : rd.z));
+                                Wv = sg * (fc == 3 ? iw.x : (fc == 4 ? iw.y : iw.z));
+                            }
+                        }
                     }
-                    for (i = 0; i < D; ++i) {
-                        float t = J[i];
-                        for (k = 0; k < i; ++k) t = t - Mf[i][k] * W[k];
-                        W[i] = t * invd[i];
-                    }
-                    for (i = D - 1; i >= 0; --i) {
-                        float t = W[i];
-                        for (k = i + 1; k < D; ++k) t = t - Mf[k][i] * W[k];
-                        W[i] = t * invd[i];
-                    }
-                    for (d = 0; d < D; ++d) wa = wa + J[d] * W[d];
+                    J[ln] = Jv;
+                    W[ln] = Wv;
                 }
-                if (C->b >= OE_F0) {
-                    const int kk = C->b - OE_F0;
-                    const v3_t rd = cross3(C->rb, dir);
-                    wb = X.finvm[kk] + dot3(rd, symmul_(X.fIw[kk], rd));
+                if (link_rows) {
+                    for (ln = 0; ln < D; ++ln) {
+                        float w = 0.0f;
+                        for (k = 0; k < D; ++k) w = w + Mi[ln][k] * J[k];
+                        W[ln] = w;
+                    }
                 }
-                C->k[rw] = 1.0f / (wa + wb);
-                C->lam[rw] = 0.0f;
+                ck[c][rw] = 1.0f / red16_prod_(J, W);
+                clam[c][rw] = 0.0f;
             }
+            cvn0[c] = red16_prod_(Jr[c * 3], u);
         }
-        for (c = 0; c < X.nct; ++c) X.ct[c].vn0 = erel_(&X, &X.ct[c], c, 0, 0);
 
-        for (it = 0; it < P->npos; ++it) {
-            for (c = 0; c < X.nct; ++c) {
-                const float s = X.ct[c].s0 + erel_(&X, &X.ct[c], c, 0, 1);
-                float tg = -s * P->inv_sub;
-                if (s < 0.0f) tg = fminf(tg, P->maxdep);
-                enormal_(&X, c, tg);
+        /* ---- 4. TGS */
+        for (it = 0; it < P->npos + P->nvel; ++it) {
+            const int pos = it < P->npos;
+            int ln;
+            for (c = 0; c < nct; ++c) {
+                const float s = cs0[c] + red16_prod_(Jr[c * 3], dp);
+                float tg, lam, dl, nl;
+                if (pos) {
+                    tg = -s * P->inv_sub;
+                    if (s < 0.0f) tg = fminf(tg, P->maxdep);
+                } else {
+                    tg = s > 0.0f ? -s * P->inv_h : 0.0f;
+                    if (ce[c] > 0.0f && cvn0[c] < -P->bounce) tg = fmaxf(tg, -ce[c] * cvn0[c]);
+                }
+                lam = clam[c][0];
+                dl = ck[c][0] * (tg - red16_prod_(Jr[c * 3], u));
+                nl = fmaxf(lam + dl, 0.0f);
+                dl = nl - lam;
+                for (ln = 0; ln < OE_G; ++ln) u[ln] = u[ln] + Wr[c * 3][ln] * dl;
+                clam[c][0] = nl;
             }
-            for (c = 0; c < X.nct; ++c) efriction_(&X, c);
-            for (d = 0; d < D; ++d) X.dq[d] = X.dq[d] + X.qd[d] * P->sub;
-            for (k = 0; k < nfr; ++k) {
-                X.fdx[k] = mad3(X.fdx[k], X.fv[k], P->sub);
-                X.fdth[k] = mad3(X.fdth[k], X.fw[k], P->sub);
+            for (c = 0; c < nct; ++c) {
+                const float lim = cmu[c] * clam[c][0];
+                int rw;
+                for (rw = 1; rw < 3; ++rw) {
+                    const float lam = clam[c][rw];
+                    const float nl = fminf(fmaxf(lam - ck[c][rw] * red16_prod_(Jr[c * 3 + rw], u), -lim), lim);
+                    const float dl = nl - lam;
+                    for (ln = 0; ln < OE_G; ++ln) u[ln] = u[ln] + Wr[c * 3 + rw][ln] * dl;
+                    clam[c][rw] = nl;
+                }
             }
+            if (pos)
+                for (ln = 0; ln < OE_G; ++ln) dp[ln] = dp[ln] + u[ln] * P->sub;
         }
-        for (it = 0; it < P->nvel; ++it) {
-            for (c = 0; c < X.nct; ++c) {
-                const float s = X.ct[c].s0 + erel_(&X, &X.ct[c], c, 0, 1);
-                float tg = s > 0.0f ? -s * P->inv_h : 0.0f;
-                if (X.ct[c].e > 0.0f && X.ct[c].vn0 < -P->bounce) tg = fmaxf(tg, -X.ct[c].e * X.ct[c].vn0);
-                enormal_(&X, c, tg);
-            }
-            for (c = 0; c < X.nct; ++c) efriction_(&X, c);
-        }
-        for (c = 0; c < X.nct; ++c) {
-            const ect_t* C = &X.ct[c];
-            v3_t imp = mul3(C->d[0], C->lam[0]);
-            imp = mad3(imp, C->d[1], C->lam[1]);
-            imp = mad3(imp, C->d[2], C->lam[2]);
-            if (C->a >= OE_F0) fsum[C->a - OE_F0] = add3(fsum[C->a - OE_F0], imp);
-            else if (C->a >= 0) lsum[C->a] = add3(lsum[C->a], imp);
-            if (C->b >= OE_F0) fsum[C->b - OE_F0] = sub3(fsum[C->b - OE_F0], imp);
-        }
+
+        /* ---- 5. integrate */
         for (d = 0; d < D; ++d) {
             const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
             const float maxv = pr[4];
-            float w = X.qd[d], x;
+            float w = u[d], x;
             if (maxv > 0.0f) w = fminf(fmaxf(w, -maxv), maxv);
-            x = X.q[d] + X.dq[d];
+            x = q[d] + dp[d];
             if (pr[7] != 0.0f) {
                 const float lo = pr[5], hi = pr[6];
                 if (x < lo) { x = lo; if (w < 0.0f) w = 0.0f; }
                 if (x > hi) { x = hi; if (w > 0.0f) w = 0.0f; }
             }
-            X.q[d] = x; X.qd[d] = w;
+            q[d] = x; u[d] = w;
+        }
+        for (c = 0; c < nct; ++c) {
+            v3_t imp = mul3(cd[c][0], clam[c][0]);
+            imp = mad3(imp, cd[c][1], clam[c][1]);
+            imp = mad3(imp, cd[c][2], clam[c][2]);
+            if (ca[c] >= OE_F0) fsum[ca[c] - OE_F0] = add3(fsum[ca[c] - OE_F0], imp);
+            else lsum[ca[c]] = add3(lsum[ca[c]], imp);
+            if (cb[c] >= OE_F0 && cb[c] < OE_ST0) fsum[cb[c] - OE_F0] = sub3(fsum[cb[c] - OE_F0], imp);
         }
         for (k = 0; k < nfr; ++k) {
-            const v3_t xc1 = add3(X.fxc[k], X.fdx[k]);
-            fq[k] = qint_(fq[k], X.fdth[k]);
+            const int s0 = D + 6 * k;
+            const v3_t dx = V(dp[s0 + 0], dp[s0 + 1], dp[s0 + 2]);
+            const v3_t dth = V(dp[s0 + 3], dp[s0 + 4], dp[s0 + 5]);
+            const v3_t xc1 = add3(fxc[k], dx);
+            fq[k] = qint_(fq[k], dth);
             fx[k] = sub3(xc1, qrot_(fq[k], fcom[k]));
         }
     }
@@ -832,14 +815,13 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         float* s = state + (size_t)b * MG_STATE_N;
         s[0] = fx[k].x; s[1] = fx[k].y; s[2] = fx[k].z;
         s[3] = fq[k].x; s[4] = fq[k].y; s[5] = fq[k].z; s[6] = fq[k].w;
-        s[7] = X.fv[k].x; s[8] = X.fv[k].y; s[9] = X.fv[k].z;
-        s[10] = X.fw[k].x; s[11] = X.fw[k].y; s[12] = X.fw[k].z;
+        for (i = 0; i < 6; ++i) s[7 + i] = u[D + 6 * k + i];
         cforce[(size_t)b * 3 + 0] = fsum[k].x * P->inv_dt;
         cforce[(size_t)b * 3 + 1] = fsum[k].y * P->inv_dt;
         cforce[(size_t)b * 3 + 2] = fsum[k].z * P->inv_dt;
     }
     if (L == 0) return 0;
-    for (d = 0; d < D; ++d) { dof[(d0 + d) * 2 + 0] = X.q[d]; dof[(d0 + d) * 2 + 1] = X.qd[d]; }
+    for (d = 0; d < D; ++d) { dof[(d0 + d) * 2 + 0] = q[d]; dof[(d0 + d) * 2 + 1] = u[d]; }
     for (l = 0; l < L; ++l) {
         const int p = LI[l * MG_LINK_I_N + 0], jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
         const float* M = m->body_mass + (size_t)(b0 + l) * MG_MASS_N;
@@ -848,12 +830,12 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         if (p < 0) {
             ql[l] = q0; xl[l] = x0; vl[l] = sv0();
         } else {
-            q4_t qrel; v3_t rr; sv_t s;
-            const float qj = dj >= 0 ? X.q[dj] : 0.0f, qdj = dj >= 0 ? X.qd[dj] : 0.0f;
-            joint_(LF + l * MG_LINK_F_N, jt, qj, &qrel, &rr, &s);
+            q4_t qrel; v3_t rr; sv_t sj;
+            const float qj = dj >= 0 ? q[dj] : 0.0f, qdj = dj >= 0 ? u[dj] : 0.0f;
+            joint_(LF + l * MG_LINK_F_N, jt, qj, &qrel, &rr, &sj);
             ql[l] = qnorm_(qmul_(ql[p], qrel));
             xl[l] = add3(xl[p], qrot_(ql[p], rr));
-            vl[l] = svadd_(xmot_(mt_(qmat_(qrel)), rr, vl[p]), svmul_(s, qdj));
+            vl[l] = svadd_(xmot_(mt_(qmat_(qrel)), rr, vl[p]), svmul_(sj, qdj));
         }
         ww = qrot_(ql[l], vl[l].w);
         vw = qrot_(ql[l], add3(vl[l].v, cross3(vl[l].w, com)));

@@ -71,22 +71,31 @@ struct MgArticArgs {
     float*       cforce;      // [3][nb]
 };
 
-// Coupled per-env step (mg_env.hip). env_i rows (MG_ENV_I_N int32):
+// Coupled per-env step (mg_env.hip): MG_ENV_G lanes per env, one lane per
+// generalized-velocity slot (articulation DOFs first, then 6 per free body),
+// so D + 6 nf <= MG_ENV_G. env_i rows (MG_ENV_I_N int32):
 //   [0] first internal body of the env's articulation or -1, [1] its first DOF,
 //   [2] free bodies nf <= MG_ENV_MAXF, [3..6] their internal slots,
 //   [7] static bodies ns <= MG_ENV_MAXS, [8..11] their internal slots,
 //   [12] collision mask: bit k art-free k, 4+s art-static s, 8+p free pair p
-//        ((0,1),(0,2),(0,3),(1,2),(1,3),(2,3)), 14+4k+s free k-static s.
+//        ((0,1),(0,2),(0,3),(1,2),(1,3),(2,3)), 14+4k+s free k-static s,
+//   [13] articulation template or -1, [14] first pair, [15] pair count.
+// Pairs ([4] int32): a, shape of a, b, shape of b (-1: ground). Participants:
+// link l = l (link 0, the fixed base, only as b), free body k = MG_ENV_FREE0 + k,
+// static body s = MG_ENV_STATIC0 + s, ground = -1.
 #define MG_ENV_I_N    16
-#define MG_ENV_MAXF    4
+#define MG_ENV_G      16     // lanes per env
+#define MG_ENV_MAXF    2
 #define MG_ENV_MAXS    4
-#define MG_ENV_MAXCT  20     // contacts per env per substep
-#define MG_ENV_FREE0  16     // participant id of free body 0 (links are 0..15)
+#define MG_ENV_MAXCT  16     // contacts per env per substep
+#define MG_ENV_FREE0  16
+#define MG_ENV_STATIC0 32
 
 struct MgEnvArgs {
     int          ne;          // envs in this launch
     int          nb, nd;
     const int*   env_i;       // [ne][MG_ENV_I_N]
+    const int*   pairs;       // [..][4] candidate shape pairs (env_i[14], [15])
     int          nl, ndof;    // articulation template of this launch (0 links: none)
     const float* link_f;
     const int*   link_i;

@@ -104,6 +104,7 @@ struct mg_sim {
     std::vector<ArticGroup> groups;
     int* d_artic_step = nullptr;  // [..][4] instances stepped by k_artic_step
     int* d_env = nullptr;         // [n_coupled][MG_ENV_I_N] coupled envs, by group
+    int* d_pairs = nullptr;       // [..][4] candidate shape pairs of the coupled envs
     int n_coupled = 0;
     std::vector<EnvGroup> env_groups;
 
@@ -231,7 +232,7 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_tbi, s->d_shapes,
                     s->d_actor_root, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
-                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx};
+                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -316,6 +317,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     std::vector<char> coupled_body(nb, 0);           // free roots / articulation roots of coupled envs
     std::vector<std::array<int, MG_ENV_I_N>> env_rows;   // global body ids, converted below
     std::vector<int> env_tmpl;
+    std::vector<int> pairs;                              // [..][4] shape pairs of the coupled envs
     if (m->actor_coll && na > 0) {
         for (int a = 0; a + 1 < na; ++a)
             if (m->actor_root_body[a + 1] <= m->actor_root_body[a])
@@ -362,6 +364,17 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                             "env %d: %zu articulations / %zu free / %zu static bodies in contact range; the "
                             "coupled step supports 1 / %d / %d", e, art.size(), fr.size(), stc.size(),
                             MG_ENV_MAXF, MG_ENV_MAXS);
+            int art_nl = 0, art_nd = 0;
+            if (!art.empty()) {
+                const int k = artic_of_root[m->actor_root_body[art[0]]];
+                const int t = k >= 0 ? m->artic_i[(size_t)k * MG_ARTIC_I_N + 2] : -1;
+                if (t < 0 || t >= m->num_artic_tmpls) return fail(MG_ERR_ARG, "env %d: bad articulation", e);
+                art_nl = m->artic_tmpl_i[t * MG_ATMPL_I_N + 1];
+                art_nd = m->artic_tmpl_i[t * MG_ATMPL_I_N + 2];
+            }
+            if (art_nd + 6 * (int)fr.size() > MG_ENV_G)
+                return fail(MG_ERR_UNSUPPORTED, "env %d: %d DOFs + %zu free bodies exceed the %d velocity slots of "
+                            "the coupled step", e, art_nd, fr.size(), MG_ENV_G);
             std::array<int, MG_ENV_I_N> row;
             row.fill(0);
             row[0] = -1;
@@ -395,6 +408,62 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                 if (!art.empty() && collide(art[0], stc[t])) mask |= 1 << (4 + t);
             row[12] = mask;
             row[13] = tmpl;
+            // candidate shape pairs, in the order the step solves them
+            auto shp = [m](int b, int* s0, int* ns) {
+                const int* t = m->tmpl_body_i + (size_t)m->body_tmpl[b] * MG_TBODY_I_N;
+                *s0 = t[0];
+                *ns = t[1];
+            };
+            auto push = [&pairs](int a, int sa, int b, int sb) {
+                pairs.push_back(a); pairs.push_back(sa); pairs.push_back(b); pairs.push_back(sb);
+            };
+            static const int pbit[4][4] = {{-1, 0, 1, 2}, {-1, -1, 3, 4}, {-1, -1, -1, 5}, {-1, -1, -1, -1}};
+            const bool ground = s->params.has_ground != 0;
+            row[14] = (int)(pairs.size() / 4);
+            for (int k = 0; k < (int)fr.size(); ++k) {
+                int sa0, nsa;
+                shp(row[3 + k], &sa0, &nsa);
+                for (int sa = sa0; sa < sa0 + nsa; ++sa) {
+                    if (ground) push(MG_ENV_FREE0 + k, sa, -1, -1);
+                    for (int t = 0; t < (int)stc.size(); ++t) {
+                        if (!((mask >> (14 + 4 * k + t)) & 1)) continue;
+                        int sb0, nsb;
+                        shp(row[8 + t], &sb0, &nsb);
+                        for (int sb = sb0; sb < sb0 + nsb; ++sb) push(MG_ENV_FREE0 + k, sa, MG_ENV_STATIC0 + t, sb);
+                    }
+                    for (int j = k + 1; j < (int)fr.size(); ++j) {
+                        if (!((mask >> (8 + pbit[k][j])) & 1)) continue;
+                        int sb0, nsb;
+                        shp(row[3 + j], &sb0, &nsb);
+                        for (int sb = sb0; sb < sb0 + nsb; ++sb) push(MG_ENV_FREE0 + k, sa, MG_ENV_FREE0 + j, sb);
+                    }
+                    if (row[0] >= 0 && ((mask >> k) & 1)) {
+                        int sb0, nsb;
+                        shp(row[0], &sb0, &nsb);
+                        for (int sb = sb0; sb < sb0 + nsb; ++sb) push(MG_ENV_FREE0 + k, sa, 0, sb);
+                    }
+                }
+            }
+            for (int l = 1; l < art_nl; ++l) {
+                int sa0, nsa;
+                shp(row[0] + l, &sa0, &nsa);
+                for (int sa = sa0; sa < sa0 + nsa; ++sa) {
+                    if (ground) push(l, sa, -1, -1);
+                    for (int t = 0; t < (int)stc.size(); ++t) {
+                        if (!((mask >> (4 + t)) & 1)) continue;
+                        int sb0, nsb;
+                        shp(row[8 + t], &sb0, &nsb);
+                        for (int sb = sb0; sb < sb0 + nsb; ++sb) push(l, sa, MG_ENV_STATIC0 + t, sb);
+                    }
+                    for (int k = 0; k < (int)fr.size(); ++k) {
+                        if (!((mask >> k) & 1)) continue;
+                        int sb0, nsb;
+                        shp(row[3 + k], &sb0, &nsb);
+                        for (int sb = sb0; sb < sb0 + nsb; ++sb) push(l, sa, MG_ENV_FREE0 + k, sb);
+                    }
+                }
+            }
+            row[15] = (int)(pairs.size() / 4) - row[14];
             env_rows.push_back(row);
             env_tmpl.push_back(tmpl);
         }
@@ -527,6 +596,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(dalloc(&s->d_artic, artic_sorted.size()));
     HIP_TRY(dalloc(&s->d_artic_step, artic_step.size()));
     HIP_TRY(dalloc(&s->d_env, env_flat.size()));
+    HIP_TRY(dalloc(&s->d_pairs, pairs.size()));
     HIP_TRY(dalloc(&s->d_link_f, (size_t)s->ntl * MG_LINK_F_N));
     HIP_TRY(dalloc(&s->d_link_i, (size_t)s->ntl * MG_LINK_I_N));
 
@@ -558,6 +628,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(h2d(s->d_artic, artic_sorted.data(), artic_sorted.size() * sizeof(int)));
     HIP_TRY(h2d(s->d_artic_step, artic_step.data(), artic_step.size() * sizeof(int)));
     HIP_TRY(h2d(s->d_env, env_flat.data(), env_flat.size() * sizeof(int)));
+    HIP_TRY(h2d(s->d_pairs, pairs.data(), pairs.size() * sizeof(int)));
     HIP_TRY(h2d(s->d_link_f, m->tmpl_link_f, (size_t)s->ntl * MG_LINK_F_N * sizeof(float)));
     HIP_TRY(h2d(s->d_link_i, m->tmpl_link_i, (size_t)s->ntl * MG_LINK_I_N * sizeof(int)));
     HIP_TRY(hipDeviceSynchronize());
@@ -595,6 +666,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         MgEnvArgs A{};
         A.ne = g.count; A.nb = s->nb; A.nd = s->nd;
         A.env_i = s->d_env + (size_t)g.offset * MG_ENV_I_N;
+        A.pairs = s->d_pairs;
         A.nl = g.tmpl >= 0 ? g.nl : 0;
         A.ndof = g.tmpl >= 0 ? g.ndof : 0;
         A.link_f = s->d_link_f + (size_t)(g.tmpl >= 0 ? g.first_link : 0) * MG_LINK_F_N;

@@ -1,0 +1,51 @@
+"""Kernel microbenchmark of the coupled per-env step (k_env_step): the S3
+Franka cube-pick loop (OSC controller) at n envs; warm frames bring the arms to
+the cubes (grasp contacts), then the average simulate() kernel time over the
+timed frames (HIP events). Library from MIGYM_LIB (default in-tree)."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from isaacgym import gymapi, gymtorch  # noqa: E402
+from test_isaacgym_amd import _native as N, franka_control, scenes  # noqa: E402
+
+
+def run(n, warm=150, steps=100):
+    gym = gymapi.acquire_gym()
+    sim, info = scenes.franka_scene(gym, n)
+    gym.prepare_sim(sim)
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    jac = gymtorch.wrap_tensor(gym.acquire_jacobian_tensor(sim, "franka"))
+    mm = gymtorch.wrap_tensor(gym.acquire_mass_matrix_tensor(sim, "franka"))
+    ctl = franka_control.CubePick(n, info["init_pos"], info["init_rot"], info["default_dof_pos"], "cuda:0")
+    h = info["hand_index"]
+    bi = torch.tensor(info["box_idxs"], device="cuda:0")
+    hi = torch.tensor(info["hand_idxs"], device="cuda:0")
+    for k in range(warm + steps):
+        gym.simulate(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_dof_state_tensor(sim)
+        gym.refresh_jacobian_tensors(sim)
+        gym.refresh_mass_matrix_tensors(sim)
+        pa, ea = ctl.step(rb, dof[:, 0].view(n, 9, 1), dof[:, 1].view(n, 9, 1), jac[:, h - 1, :, :7],
+                          mm[:, :7, :7], bi, hi)
+        gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(pa))
+        gym.set_dof_actuation_force_tensor(sim, gymtorch.unwrap_tensor(ea))
+    torch.cuda.synchronize()
+    avg, lo = ctypes.c_float(), ctypes.c_float()
+    used = N.lib.mg_step_time_stats(sim.native, steps, ctypes.byref(avg), ctypes.byref(lo), None)
+    gym.destroy_sim(sim)
+    return {"lib": os.path.basename(N.LIB_PATH), "envs": n, "kernel_us_avg": 1e3 * avg.value,
+            "kernel_us_min": 1e3 * lo.value, "launches": used}
+
+
+if __name__ == "__main__":
+    sizes = [int(x) for x in (sys.argv[1:] or ["4096"])]
+    for n in sizes:
+        print(json.dumps(run(n)), flush=True)
