@@ -291,6 +291,7 @@ typedef struct {
 
 #define OE_G 16
 #define OE_ST0 32
+#define OE_LIM0 64
 
 /* sum of 16 slots in the device's DPP order (mg_env.hip red16): row_ror 8,
  * row_ror 4, quad xor 2, quad xor 1; every lane ends with this value */
@@ -368,16 +369,38 @@ static int env_pairs_(const mg_model* m, const oenv_t* ev, int ground, int L, ep
 
 static const float* shp_(const mg_model* m, int s) { return m->shapes + (size_t)s * MG_SHAPE_STRIDE; }
 
-static si_t link_inertia_(const float* M) {
-    const float mass = M[11];
+
+#define OE_MAXPAIRS 512
+
+static float dot6_(const float* a, const float* b) {
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+static sv_t sv6_(const float* a) { return SVc(V(a[0], a[1], a[2]), V(a[3], a[4], a[5])); }
+static void put6_(float* a, sv_t s) { a[0] = s.w.x; a[1] = s.w.y; a[2] = s.w.z; a[3] = s.v.x; a[4] = s.v.y; a[5] = s.v.z; }
+
+/* world-frame spatial inertia about O (mg_env.hip world_inertia) */
+static void world_inertia_(const float* M, q4_t ql, v3_t xl, v3_t O, float* I) {
+    const float m = M[11];
     const v3_t com = V(M[8], M[9], M[10]);
     const q4_t iq = Q(M[4], M[5], M[6], M[7]);
     const v3_t Id = V(M[1] > 0.0f ? 1.0f / M[1] : 0.0f, M[2] > 0.0f ? 1.0f / M[2] : 0.0f, M[3] > 0.0f ? 1.0f / M[3] : 0.0f);
-    const m3_t Rq = qmat_(iq);
-    return sirigid_(mass, com, mmul_(mmul_(Rq, M3c(V(Id.x, 0.0f, 0.0f), V(0.0f, Id.y, 0.0f), V(0.0f, 0.0f, Id.z))), mt_(Rq)));
+    const s3_t Ic = sym_rdrt_(qmat_(qmul_(ql, iq)), Id);
+    const v3_t c = sub3(add3(xl, qrot_(ql, com)), O);
+    const float cc2 = dot3(c, c);
+    const float ic[9] = {Ic.xx, Ic.xy, Ic.xz, Ic.xy, Ic.yy, Ic.yz, Ic.xz, Ic.yz, Ic.zz};
+    const float cv[3] = {c.x, c.y, c.z};
+    const v3_t mc = mul3(c, m);
+    const float sk[9] = {0.0f, -mc.z, mc.y, mc.z, 0.0f, -mc.x, -mc.y, mc.x, 0.0f};
+    int i, k;
+    for (i = 0; i < 3; ++i)
+        for (k = 0; k < 3; ++k) {
+            const float dg = i == k ? m * cc2 : 0.0f;
+            I[i * 6 + k] = ic[i * 3 + k] + (dg - cv[i] * (cv[k] * m));
+            I[i * 6 + 3 + k] = sk[i * 3 + k];
+            I[(3 + i) * 6 + k] = sk[k * 3 + i];
+            I[(3 + i) * 6 + 3 + k] = i == k ? m : 0.0f;
+        }
 }
-
-#define OE_MAXPAIRS 512
 
 static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float* state, float* dof, const float* tgt,
                      const float* props, const float* ext, float* cforce) {
@@ -390,17 +413,16 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     const v3_t gvec = V(P->g[0], P->g[1], P->g[2]);
     static epair_t pairs[OE_MAXPAIRS];
     int npair;
-    v3_t x0 = V(0.0f, 0.0f, 0.0f), gb = V(0.0f, 0.0f, 0.0f);
+    v3_t x0 = V(0.0f, 0.0f, 0.0f), gw = V(0.0f, 0.0f, 0.0f);
     q4_t q0 = Q(0.0f, 0.0f, 0.0f, 1.0f);
     /* slots */
     float q[OE_G], u[OE_G], dp[OE_G], qdd[OE_G], mdiag[OE_G], tau0d[OE_G], impd[OE_G];
     /* links */
-    m3_t E[OR_MAXL];
-    v3_t r[OR_MAXL], xl[OR_MAXL], zl[OR_MAXL], lsum[OR_MAXL];
-    q4_t ql[OR_MAXL];
-    sv_t Sj[OR_MAXL], vl[OR_MAXL], cl[OR_MAXL], pA[OR_MAXL], U[OR_MAXL], al[OR_MAXL];
-    si_t IA[OR_MAXL];
-    float Dl[OR_MAXL], ul[OR_MAXL];
+    v3_t xl[OR_MAXL], zl[OR_MAXL], lsum[OR_MAXL], rrl[OR_MAXL];
+    q4_t ql[OR_MAXL], qrl[OR_MAXL];
+    sv_t vl[OR_MAXL];
+    static float Iw[OR_MAXL][36];
+    float xi[OR_MAXL][6], va[OR_MAXL][6], ccv[OR_MAXL][6], pav[OR_MAXL][6], Ua[OR_MAXL][6], Dd[OR_MAXL], uu[OR_MAXL];
     int amask[OR_MAXL], dlink[OE_G], drev[OE_G];
     static float Lc[OE_G][OE_G], Mi[OE_G][OE_G];
     float invd[OE_G];
@@ -424,7 +446,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         const float grav_on = m->tmpl_body_f[(size_t)m->body_tmpl[b0] * MG_TBODY_F_N + 4];
         x0 = V(s0[0], s0[1], s0[2]);
         q0 = qnorm_(Q(s0[3], s0[4], s0[5], s0[6]));
-        gb = qrot_(Q(-q0.x, -q0.y, -q0.z, q0.w), grav_on != 0.0f ? gvec : V(0.0f, 0.0f, 0.0f));
+        gw = grav_on != 0.0f ? gvec : V(0.0f, 0.0f, 0.0f);
     }
     for (l = 0; l < L; ++l) {
         const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
@@ -461,48 +483,69 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
 
     for (st_ = 0; st_ < P->substeps; ++st_) {
         int nct = 0, link_rows = 0;
-        /* ---- 1. unconstrained motion */
+        /* ---- 1. unconstrained motion: world-frame ABA about x0 (mg_env.hip aba_world) */
         if (L > 0) {
             unsigned xmask = 0u, xpos = 0u;
             int att;
             for (att = 0; att < 2; ++att) {
                 unsigned nm;
+                for (l = 1; l < L; ++l) {
+                    const float* lf = LF + l * MG_LINK_F_N;
+                    const int jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
+                    const v3_t po = V(lf[0], lf[1], lf[2]), ax = V(lf[7], lf[8], lf[9]);
+                    const q4_t qo = Q(lf[3], lf[4], lf[5], lf[6]);
+                    const float qj = dj >= 0 ? q[dj] : 0.0f;
+                    qrl[l] = qo; rrl[l] = po;
+                    if (jt == MG_JOINT_REVOLUTE) qrl[l] = qmul_(qo, qaxang_(ax, qj));
+                    else if (jt == MG_JOINT_PRISMATIC) rrl[l] = add3(po, qrot_(qo, mul3(ax, qj)));
+                }
                 for (l = 0; l < L; ++l) {
-                    const int p = LI[l * MG_LINK_I_N + 0], jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
-                    if (p < 0) {
-                        E[l] = M3c(V(1.0f, 0.0f, 0.0f), V(0.0f, 1.0f, 0.0f), V(0.0f, 0.0f, 1.0f));
-                        r[l] = V(0.0f, 0.0f, 0.0f);
-                        Sj[l] = sv0(); vl[l] = sv0(); cl[l] = sv0();
-                        ql[l] = q0; xl[l] = x0; zl[l] = V(0.0f, 0.0f, 0.0f);
-                    } else {
-                        q4_t qrel; v3_t rr; sv_t sj, vJ;
+                    const int p = LI[l * MG_LINK_I_N + 0];
+                    if (p < 0) { ql[l] = q0; xl[l] = x0; zl[l] = V(0.0f, 0.0f, 0.0f); }
+                    else {
                         const float* lf = LF + l * MG_LINK_F_N;
-                        const float qj = dj >= 0 ? q[dj] : 0.0f, qdj = dj >= 0 ? u[dj] : 0.0f;
-                        joint_(lf, jt, qj, &qrel, &rr, &sj);
-                        E[l] = mt_(qmat_(qrel));
-                        r[l] = rr;
-                        Sj[l] = sj;
-                        vJ = svmul_(sj, qdj);
-                        vl[l] = svadd_(xmot_(E[l], rr, vl[p]), vJ);
-                        cl[l] = crm_(vl[l], vJ);
-                        ql[l] = qnorm_(qmul_(ql[p], qrel));
-                        xl[l] = add3(xl[p], qrot_(ql[p], rr));
+                        ql[l] = qnorm_(qmul_(ql[p], qrl[l]));
+                        xl[l] = add3(xl[p], qrot_(ql[p], rrl[l]));
                         zl[l] = qrot_(ql[l], V(lf[7], lf[8], lf[9]));
                     }
-                    IA[l] = link_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N);
-                    pA[l] = crf_(vl[l], simul_(IA[l], vl[l]));
+                }
+                for (l = 0; l < L; ++l) {
+                    const int jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
+                    sv_t x = sv0();
+                    if (l > 0 && dj >= 0) {
+                        if (jt == MG_JOINT_REVOLUTE) x = SVc(zl[l], cross3(sub3(xl[l], x0), zl[l]));
+                        else x = SVc(V(0.0f, 0.0f, 0.0f), zl[l]);
+                    }
+                    put6_(xi[l], x);
+                    world_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N, ql[l], xl[l], x0, Iw[l]);
+                }
+                for (i = 0; i < 6; ++i) va[0][i] = 0.0f;
+                for (l = 1; l < L; ++l) {
+                    const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
+                    const float qd = dj >= 0 ? u[dj] : 0.0f;
+                    for (i = 0; i < 6; ++i) va[l][i] = va[p][i] + xi[l][i] * qd;
+                }
+                for (l = 0; l < L; ++l) {
+                    const int dj = LI[l * MG_LINK_I_N + 2];
+                    const float qd = dj >= 0 ? u[dj] : 0.0f;
+                    const sv_t v = sv6_(va[l]);
+                    const sv_t vJ = svmul_(sv6_(xi[l]), qd);
+                    float Iv[6];
+                    for (i = 0; i < 6; ++i) Iv[i] = dot6_(&Iw[l][i * 6], va[l]);
+                    put6_(ccv[l], crm_(v, vJ));
+                    put6_(pav[l], crf_(v, sv6_(Iv)));
                 }
                 for (l = L - 1; l >= 1; --l) {
                     const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
-                    si_t Ia = IA[l];
-                    sv_t pa;
+                    float uinvD = 0.0f;
                     if (dj >= 0) {
                         const float* pr = props + (size_t)(d0 + dj) * MG_DOFPROP_N;
                         const float* tg = tgt + (size_t)(d0 + dj) * 3;
                         const int mode = (int)pr[0];
                         const float kp = pr[1], kd = pr[2], eff = pr[3], arm = pr[8];
                         const float qv = q[dj], uv = u[dj];
-                        float tau = 0.0f, imp = 0.0f, invD;
+                        float tau = 0.0f, imp = 0.0f, Dv, uvv, invD;
+                        for (i = 0; i < 6; ++i) Ua[l][i] = dot6_(&Iw[l][i * 6], xi[l]);
                         if (mode == MG_DOF_MODE_POS) {
                             tau = kp * (tg[0] - qv - h * uv) + kd * (tg[1] - uv);
                             imp = h * kd + h * h * kp;
@@ -520,43 +563,48 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                                 tau = fminf(fmaxf(tau, -eff), eff);
                             }
                         }
+                        Dv = dot6_(xi[l], Ua[l]) + arm + imp;
+                        uvv = tau - dot6_(xi[l], pav[l]);
+                        invD = 1.0f / Dv;
+                        uinvD = uvv * invD;
+                        for (i = 0; i < 36; ++i) Iw[l][i] = Iw[l][i] - Ua[l][i / 6] * (Ua[l][i % 6] * invD);
+                        Dd[l] = Dv;
+                        uu[l] = uvv;
+                        mdiag[dj] = arm + imp;
                         tau0d[dj] = tau;
                         impd[dj] = imp;
-                        mdiag[dj] = arm + imp;
-                        U[l] = simul_(Ia, Sj[l]);
-                        Dl[l] = svdot_(Sj[l], U[l]) + arm + imp;
-                        ul[l] = tau - svdot_(Sj[l], pA[l]);
-                        invD = 1.0f / Dl[l];
-                        Ia.A = msub_(Ia.A, mouter_(U[l].w, U[l].w, invD));
-                        Ia.B = msub_(Ia.B, mouter_(U[l].w, U[l].v, invD));
-                        Ia.C = msub_(Ia.C, mouter_(U[l].v, U[l].v, invD));
-                        pa = svadd_(svadd_(pA[l], simul_(Ia, cl[l])), svmul_(U[l], ul[l] * invD));
-                    } else {
-                        pa = svadd_(pA[l], simul_(Ia, cl[l]));
                     }
                     if (p > 0) {
-                        IA[p] = siadd_(IA[p], xin_t_(E[l], r[l], Ia));
-                        pA[p] = svadd_(pA[p], xfrc_t_(E[l], r[l], pa));
+                        for (i = 0; i < 6; ++i) {
+                            float pv = pav[l][i] + dot6_(&Iw[l][i * 6], ccv[l]);
+                            if (dj >= 0) pv = pv + Ua[l][i] * uinvD;
+                            pav[p][i] = pav[p][i] + pv;
+                        }
+                        for (i = 0; i < 36; ++i) Iw[p][i] = Iw[p][i] + Iw[l][i];
                     }
                 }
-                al[0] = SVc(V(0.0f, 0.0f, 0.0f), mul3(gb, -1.0f));
+                va[0][0] = 0.0f; va[0][1] = 0.0f; va[0][2] = 0.0f;
+                va[0][3] = -gw.x; va[0][4] = -gw.y; va[0][5] = -gw.z;
                 for (l = 1; l < L; ++l) {
                     const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
-                    sv_t ap = svadd_(xmot_(E[l], r[l], al[p]), cl[l]);
+                    float a6[6];
+                    for (i = 0; i < 6; ++i) a6[i] = va[p][i] + ccv[l][i];
                     if (dj >= 0) {
-                        const float acc = (ul[l] - svdot_(U[l], ap)) / Dl[l];
+                        float t16[16], acc;
+                        for (i = 0; i < 16; ++i) t16[i] = i < 6 ? Ua[l][i] * a6[i] : 0.0f;
+                        acc = (uu[l] - red16_(t16)) / Dd[l];
+                        for (i = 0; i < 6; ++i) a6[i] = a6[i] + xi[l][i] * acc;
                         qdd[dj] = acc;
-                        ap = svadd_(ap, svmul_(Sj[l], acc));
                     }
-                    al[l] = ap;
+                    for (i = 0; i < 6; ++i) va[l][i] = a6[i];
                 }
                 nm = xmask;
                 for (d = 0; d < D; ++d) {
                     const float eff = props[(size_t)(d0 + d) * MG_DOFPROP_N + 3];
                     if (eff > 0.0f && impd[d] != 0.0f) {
-                        const float act = tau0d[d] - impd[d] * qdd[d];
-                        if (act > eff) { nm |= 1u << d; xpos |= 1u << d; }
-                        else if (act < -eff) nm |= 1u << d;
+                        const float actf = tau0d[d] - impd[d] * qdd[d];
+                        if (actf > eff) { nm |= 1u << d; xpos |= 1u << d; }
+                        else if (actf < -eff) nm |= 1u << d;
                     }
                 }
                 if (nm == xmask) break;
@@ -641,32 +689,56 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             }
         }
 
+        /* joint-limit rows (mg_env.hip): DOF order, after the contacts */
+        for (d = 0; d < D; ++d) {
+            const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
+            if (pr[7] != 0.0f) {
+                const float lo = pr[5], hi = pr[6];
+                const float q1 = q[d] + h * u[d];
+                const float mg = 0.05f * (hi - lo);
+                if (q1 - lo < mg || hi - q1 < mg) {
+                    const int sgn = (q1 - lo) < (hi - q1) ? 1 : -1;
+                    if (nct < OE_MAXCT) {
+                        ca[nct] = OE_LIM0 + d;
+                        cb[nct] = sgn;
+                        cp[nct] = V(0.0f, 0.0f, 0.0f);
+                        cd[nct][0] = V(0.0f, 0.0f, 0.0f);
+                        cd[nct][1] = V(0.0f, 0.0f, 0.0f);
+                        cd[nct][2] = V(0.0f, 0.0f, 0.0f);
+                        cs0[nct] = sgn > 0 ? q[d] - lo : hi - q[d];
+                        cmu[nct] = 0.0f;
+                        ce[nct] = 0.0f;
+                        link_rows = 1;
+                        nct++;
+                    }
+                }
+            }
+        }
         /* ---- 3. rows */
         if (link_rows) {
-            for (l = 0; l < L; ++l) IA[l] = link_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N);
-            for (i = 0; i < D; ++i)
-                for (j = 0; j < D; ++j) Lc[i][j] = 0.0f;
+            for (l = 0; l < L; ++l) world_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N, ql[l], xl[l], x0, Iw[l]);
             for (l = L - 1; l >= 1; --l) {
                 const int p = LI[l * MG_LINK_I_N + 0];
-                if (p > 0) IA[p] = siadd_(IA[p], xin_t_(E[l], r[l], IA[l]));
+                if (p > 0)
+                    for (i = 0; i < 36; ++i) Iw[p][i] = Iw[p][i] + Iw[l][i];
             }
-            for (l = 1; l < L; ++l) {
-                const int di = LI[l * MG_LINK_I_N + 2];
-                sv_t Fv;
-                if (di < 0) continue;
-                Fv = simul_(IA[l], Sj[l]);
-                Lc[di][di] = svdot_(Sj[l], Fv) + mdiag[di];
-                j = l;
-                while (LI[j * MG_LINK_I_N + 0] > 0) {
-                    int dj;
-                    Fv = xfrc_t_(E[j], r[j], Fv);
-                    j = LI[j * MG_LINK_I_N + 0];
-                    dj = LI[j * MG_LINK_I_N + 2];
+            for (i = 0; i < D; ++i)
+                for (j = 0; j < D; ++j) Lc[i][j] = 0.0f;
+            for (i = 0; i < D; ++i) {
+                const int li_ = dlink[i];
+                float F[6];
+                int r6, jl;
+                for (r6 = 0; r6 < 6; ++r6) F[r6] = dot6_(&Iw[li_][r6 * 6], xi[li_]);
+                Lc[i][i] = dot6_(xi[li_], F) + mdiag[i];
+                jl = LI[li_ * MG_LINK_I_N + 0];
+                while (jl > 0) {
+                    const int dj = LI[jl * MG_LINK_I_N + 2];
                     if (dj >= 0) {
-                        const float hv = svdot_(Fv, Sj[j]);
-                        Lc[di][dj] = hv;
-                        Lc[dj][di] = hv;
+                        const float hv = dot6_(xi[jl], F);
+                        Lc[i][dj] = hv;
+                        Lc[dj][i] = hv;
                     }
+                    jl = LI[jl * MG_LINK_I_N + 0];
                 }
             }
             for (j = 0; j < D; ++j) {
@@ -705,7 +777,9 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 int ln;
                 for (ln = 0; ln < OE_G; ++ln) {
                     float Jv = 0.0f, Wv = 0.0f;
-                    if (ln < D) {
+                    if (a >= OE_LIM0) {
+                        if (rw == 0 && ln == a - OE_LIM0) Jv = (float)b;
+                    } else if (ln < D) {
                         if (a < OE_F0 && ((amask[a] >> ln) & 1)) {
                             const int jl = dlink[ln];
                             Jv = drev[ln] ? dot3(cross3(zl[jl], sub3(p, xl[jl])), dir) : dot3(zl[jl], dir);
@@ -736,7 +810,10 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                         W[ln] = w;
                     }
                 }
-                ck[c][rw] = 1.0f / red16_prod_(J, W);
+                {
+                    const float den = red16_prod_(J, W);
+                    ck[c][rw] = den > 0.0f ? 1.0f / den : 0.0f;
+                }
                 clam[c][rw] = 0.0f;
             }
             cvn0[c] = red16_prod_(Jr[c * 3], u);
@@ -793,7 +870,9 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             q[d] = x; u[d] = w;
         }
         for (c = 0; c < nct; ++c) {
-            v3_t imp = mul3(cd[c][0], clam[c][0]);
+            v3_t imp;
+            if (ca[c] >= OE_LIM0) continue;
+            imp = mul3(cd[c][0], clam[c][0]);
             imp = mad3(imp, cd[c][1], clam[c][1]);
             imp = mad3(imp, cd[c][2], clam[c][2]);
             if (ca[c] >= OE_F0) fsum[ca[c] - OE_F0] = add3(fsum[ca[c] - OE_F0], imp);

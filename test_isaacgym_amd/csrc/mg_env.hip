@@ -28,6 +28,24 @@
 #include "mg_spatial.h"
 #include "mg_collide.h"
 
+#ifdef MG_ENV_PHASE_TIMING
+// profiling build only: per-phase shader-clock cycles summed over waves
+__device__ unsigned long long g_env_phase[8];
+#define PH_T0() unsigned long long ph_t = clock64()
+#define PH_MARK(k) do { const unsigned long long t_ = clock64(); \
+    if (threadIdx.x == 0) atomicAdd(&g_env_phase[k], t_ - ph_t); ph_t = t_; } while (0)
+extern "C" int mg_debug_env_phase(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_env_phase), sizeof(g_env_phase)) == hipSuccess ? 0 : -1;
+}
+extern "C" int mg_debug_env_phase_reset(void) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_env_phase), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#else
+#define PH_T0() do { } while (0)
+#define PH_MARK(k) do { } while (0)
+#endif
+
 namespace {
 
 constexpr int G = MG_ENV_G;
@@ -36,6 +54,7 @@ constexpr int MAXCT = MG_ENV_MAXCT;
 constexpr int MAXF = MG_ENV_MAXF;
 constexpr int F0 = MG_ENV_FREE0;
 constexpr int ST0 = MG_ENV_STATIC0;
+constexpr int LIM0 = MG_ENV_LIMIT0;
 
 struct EnvLds {
     float q[G], u[G], qdd[G], dpos[G], mdiag[G];
@@ -56,6 +75,17 @@ struct EnvLds {
     float cs0[MAXCT], cmu[MAXCT], ce[MAXCT], cvn0[MAXCT];
     float ck[MAXCT][3], clam[MAXCT][3];
     int nct, link_rows;
+    // world-frame articulated-body quantities (about the base origin x0)
+    float Iw[MG_MAX_LINKS][36];      // spatial inertia -> articulated / composite inertia, row-major 6x6
+    float xi[MG_MAX_LINKS][6];       // joint motion axis (w, v at x0)
+    float va[MG_MAX_LINKS][6];       // link velocity, then acceleration
+    float cc[MG_MAX_LINKS][6];       // velocity-product acceleration
+    float pa[MG_MAX_LINKS][6];       // bias force
+    float Ua[MG_MAX_LINKS][6];       // IA xi
+    float Dd[MG_MAX_LINKS], uu[MG_MAX_LINKS];
+    Q4 qr[MG_MAX_LINKS];             // joint rotation / offset relative to the parent
+    V3 rr[MG_MAX_LINKS];
+    float tau0[G], imp[G];
 };
 
 // sum over the 16 lanes of a DPP row, the same value in every lane:
@@ -139,70 +169,132 @@ MG_HD SI link_inertia(const float* Ms, int nb, int b) {
                                   m3t(Rq)));
 }
 
-// Lane 0: ABA with implicit drives (effort limit: one exact re-solve when a
-// drive's implicit force saturates) from S.q / S.u; writes S.qdd, S.mdiag and
-// the substep-start link frames S.xl / S.ql / S.zl; keeps E, r, Sj for CRBA.
+MG_HD float dot6(const float* a, const float* b) {
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+MG_HD SV sv6(const float* a) { return sv(v3(a[0], a[1], a[2]), v3(a[3], a[4], a[5])); }
+MG_HD void put6(float* a, SV s) { a[0] = s.w.x; a[1] = s.w.y; a[2] = s.w.z; a[3] = s.v.x; a[4] = s.v.y; a[5] = s.v.z; }
+
+// world-frame spatial inertia of link body b about the point O: row-major 6x6
+// [A B; B^T C] with A = Ic + m (|c|^2 1 - c c^T), B = [m c]x, C = m 1
+// (c = COM - O, Ic the rotational inertia about the COM in world axes)
+MG_HD void world_inertia(const float* Ms, int nb, int b, Q4 ql, V3 xl, V3 O, float* I) {
+    const float m = Ms[11 * nb + b];
+    const V3 com = v3(Ms[8 * nb + b], Ms[9 * nb + b], Ms[10 * nb + b]);
+    const Q4 iq = q4(Ms[4 * nb + b], Ms[5 * nb + b], Ms[6 * nb + b], Ms[7 * nb + b]);
+    const V3 invI = v3(Ms[1 * nb + b], Ms[2 * nb + b], Ms[3 * nb + b]);
+    const V3 Id = v3(invI.x > 0.0f ? 1.0f / invI.x : 0.0f, invI.y > 0.0f ? 1.0f / invI.y : 0.0f,
+                     invI.z > 0.0f ? 1.0f / invI.z : 0.0f);
+    const S3 Ic = sym_rdrt(qmat(qmul(ql, iq)), Id);
+    const V3 c = vsub(vadd(xl, qrot(ql, com)), O);
+    const float cc2 = vdot(c, c);
+    const float ic[9] = {Ic.xx, Ic.xy, Ic.xz, Ic.xy, Ic.yy, Ic.yz, Ic.xz, Ic.yz, Ic.zz};
+    const float cv[3] = {c.x, c.y, c.z};
+    const V3 mc = vscale(c, m);
+    const float sk[9] = {0.0f, -mc.z, mc.y, mc.z, 0.0f, -mc.x, -mc.y, mc.x, 0.0f};   // [m c]x, row-major
+    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) {
+            const float dg = i == k ? m * cc2 : 0.0f;
+            I[i * 6 + k] = ic[i * 3 + k] + (dg - cv[i] * (cv[k] * m));
+            I[i * 6 + 3 + k] = sk[i * 3 + k];
+            I[(3 + i) * 6 + k] = sk[k * 3 + i];
+            I[(3 + i) * 6 + 3 + k] = i == k ? m : 0.0f;
+        }
+}
+
+// Articulated-body algorithm in the world frame about the base origin x0 (RBDA
+// ch. 7 with all quantities in one frame: no spatial transforms in the inward
+// pass). Every lane of the workgroup calls it (the barriers are shared); `act`
+// selects the envs that do work. Lane l computes link l's joint transform,
+// axis and inertia; lanes 0..5 own one spatial component in the outward scans;
+// lane ln owns entries {ln, ln+16, ln+32} of every 6x6 in the inward pass.
+// Implicit drives (h kd + h^2 kp added to D); a drive whose implicit force
+// exceeds its effort limit is re-solved at the limit (xmask / xpos).
 template <int MAXL>
-__device__ void aba_lane0(const MgStep& P, const MgEnvArgs& A, EnvLds& S, int b0, int d0, int L, int D, V3 x0,
-                          Q4 q0, V3 gb, M3* E, V3* r, SV* Sj) {
+__device__ void aba_world(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool act, int ln, int b0, int d0, int LA,
+                          int DA, V3 x0, Q4 q0, V3 gw, unsigned& xmask, unsigned& xpos) {
     const int nb = A.nb, nd = A.nd;
     const float h = P.h;
     const float* pr = A.dof_props;
-    const float* Ms = A.mass;
-    SV vl[MAXL], cl[MAXL], pA[MAXL], U[MAXL], al[MAXL];
-    SI IA[MAXL];
-    float Dl[MAXL], ul[MAXL], tau0d[MAXL], impd[MAXL];
-    unsigned xmask = 0u, xpos = 0u;
-    for (int att = 0; att < 2; ++att) {
-        for (int l = 0; l < L; ++l) {
-            const float* lf = A.link_f + l * MG_LINK_F_N;
-            const int* li = A.link_i + l * MG_LINK_I_N;
-            const int p = li[0], jt = li[1], dof = li[2];
+    // ---- joint transforms (lane l)
+    if (act && ln < LA && ln > 0) {
+        const float* lf = A.link_f + ln * MG_LINK_F_N;
+        const int* li = A.link_i + ln * MG_LINK_I_N;
+        const int jt = li[1], dof = li[2];
+        const V3 po = v3(lf[0], lf[1], lf[2]);
+        const Q4 qo = q4(lf[3], lf[4], lf[5], lf[6]);
+        const V3 ax = v3(lf[7], lf[8], lf[9]);
+        const float qj = dof >= 0 ? S.q[dof] : 0.0f;
+        Q4 qrel = qo;
+        V3 rr = po;
+        if (jt == MG_JOINT_REVOLUTE) qrel = qmul(qo, q_axis_angle(ax, qj));
+        else if (jt == MG_JOINT_PRISMATIC) rr = vadd(po, qrot(qo, vscale(ax, qj)));
+        S.qr[ln] = qrel;
+        S.rr[ln] = rr;
+    }
+    __syncthreads();
+    // ---- forward kinematics (lane 0)
+    if (act && ln == 0) {
+        for (int l = 0; l < LA; ++l) {
+            const int p = A.link_i[l * MG_LINK_I_N + 0];
             if (p < 0) {
-                E[l] = m3cols(v3(1.0f, 0.0f, 0.0f), v3(0.0f, 1.0f, 0.0f), v3(0.0f, 0.0f, 1.0f));
-                r[l] = v3(0.0f, 0.0f, 0.0f);
-                Sj[l] = svzero();
-                vl[l] = svzero();
-                cl[l] = svzero();
                 S.ql[l] = q0;
                 S.xl[l] = x0;
                 S.zl[l] = v3(0.0f, 0.0f, 0.0f);
             } else {
-                const V3 po = v3(lf[0], lf[1], lf[2]);
-                const Q4 qo = q4(lf[3], lf[4], lf[5], lf[6]);
-                const V3 ax = v3(lf[7], lf[8], lf[9]);
-                const float qj = dof >= 0 ? S.q[dof] : 0.0f;
-                const float qdj = dof >= 0 ? S.u[dof] : 0.0f;
-                Q4 qrel = qo;
-                V3 rr = po;
-                SV s = svzero();
-                if (jt == MG_JOINT_REVOLUTE) {
-                    qrel = qmul(qo, q_axis_angle(ax, qj));
-                    s = sv(ax, v3(0.0f, 0.0f, 0.0f));
-                } else if (jt == MG_JOINT_PRISMATIC) {
-                    rr = vadd(po, qrot(qo, vscale(ax, qj)));
-                    s = sv(v3(0.0f, 0.0f, 0.0f), ax);
-                }
-                E[l] = m3t(qmat(qrel));
-                r[l] = rr;
-                Sj[l] = s;
-                const SV vJ = svscale(s, qdj);
-                vl[l] = svadd(x_motion(E[l], rr, vl[p]), vJ);
-                cl[l] = crm(vl[l], vJ);
+                const float* lf = A.link_f + l * MG_LINK_F_N;
                 const Q4 qp = S.ql[p];
-                S.ql[l] = qnormalize(qmul(qp, qrel));
-                S.xl[l] = vadd(S.xl[p], qrot(qp, rr));
-                S.zl[l] = qrot(S.ql[l], ax);
+                S.ql[l] = qnormalize(qmul(qp, S.qr[l]));
+                S.xl[l] = vadd(S.xl[p], qrot(qp, S.rr[l]));
+                S.zl[l] = qrot(S.ql[l], v3(lf[7], lf[8], lf[9]));
             }
-            IA[l] = link_inertia(Ms, nb, b0 + l);
-            pA[l] = crf(vl[l], si_mul(IA[l], vl[l]));
         }
-        for (int l = L - 1; l >= 1; --l) {
-            const int* li = A.link_i + l * MG_LINK_I_N;
-            const int p = li[0], dof = li[2];
-            SI Ia = IA[l];
-            SV pa;
-            if (dof >= 0) {
+    }
+    __syncthreads();
+    // ---- axes and inertias (lane l)
+    if (act && ln < LA) {
+        const int* li = A.link_i + ln * MG_LINK_I_N;
+        const int jt = li[1], dof = li[2];
+        SV x = svzero();
+        if (ln > 0 && dof >= 0) {
+            const V3 z = S.zl[ln];
+            if (jt == MG_JOINT_REVOLUTE) x = sv(z, vcross(vsub(S.xl[ln], x0), z));
+            else x = sv(v3(0.0f, 0.0f, 0.0f), z);
+        }
+        put6(S.xi[ln], x);
+        world_inertia(A.mass, nb, b0 + ln, S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
+    }
+    __syncthreads();
+    // ---- velocities (lanes 0..5, one component each)
+    if (act && ln < 6) {
+        S.va[0][ln] = 0.0f;
+        for (int l = 1; l < LA; ++l) {
+            const int p = A.link_i[l * MG_LINK_I_N + 0], dof = A.link_i[l * MG_LINK_I_N + 2];
+            const float qd = dof >= 0 ? S.u[dof] : 0.0f;
+            S.va[l][ln] = S.va[p][ln] + S.xi[l][ln] * qd;
+        }
+    }
+    __syncthreads();
+    // ---- velocity-product terms (lane l)
+    if (act && ln < LA) {
+        const int dof = A.link_i[ln * MG_LINK_I_N + 2];
+        const float qd = dof >= 0 ? S.u[dof] : 0.0f;
+        const SV v = sv6(S.va[ln]);
+        const SV vJ = svscale(sv6(S.xi[ln]), qd);
+        float Iv[6];
+        for (int i = 0; i < 6; ++i) Iv[i] = dot6(&S.Iw[ln][i * 6], S.va[ln]);
+        put6(S.cc[ln], crm(v, vJ));
+        put6(S.pa[ln], crf(v, sv6(Iv)));
+    }
+    __syncthreads();
+    // ---- inward pass: articulated inertias and bias forces
+    for (int l = LA - 1; l >= 1; --l) {
+        const int p = A.link_i[l * MG_LINK_I_N + 0], dof = A.link_i[l * MG_LINK_I_N + 2];
+        float uinvD = 0.0f;
+        if (dof >= 0) {
+            if (act && ln < 6) S.Ua[l][ln] = dot6(&S.Iw[l][ln * 6], S.xi[l]);
+            __syncthreads();
+            if (act) {
                 const int gd = d0 + dof;
                 const int mode = (int)pr[0 * nd + gd];
                 const float kp = pr[1 * nd + gd], kd = pr[2 * nd + gd], eff = pr[3 * nd + gd];
@@ -226,92 +318,114 @@ __device__ void aba_lane0(const MgStep& P, const MgEnvArgs& A, EnvLds& S, int b0
                         tau = fminf(fmaxf(tau, -eff), eff);
                     }
                 }
-                tau0d[dof] = tau;
-                impd[dof] = imp;
-                S.mdiag[dof] = arm + imp;
-                U[l] = si_mul(Ia, Sj[l]);
-                Dl[l] = svdot(Sj[l], U[l]) + arm + imp;
-                ul[l] = tau - svdot(Sj[l], pA[l]);
-                const float invD = 1.0f / Dl[l];
-                Ia.A = m3sub(Ia.A, m3outer(U[l].w, U[l].w, invD));
-                Ia.B = m3sub(Ia.B, m3outer(U[l].w, U[l].v, invD));
-                Ia.C = m3sub(Ia.C, m3outer(U[l].v, U[l].v, invD));
-                pa = svadd(svadd(pA[l], si_mul(Ia, cl[l])), svscale(U[l], ul[l] * invD));
-            } else {
-                pa = svadd(pA[l], si_mul(Ia, cl[l]));
+                const float Dv = dot6(S.xi[l], S.Ua[l]) + arm + imp;
+                const float uvv = tau - dot6(S.xi[l], S.pa[l]);
+                const float invD = 1.0f / Dv;
+                uinvD = uvv * invD;
+                for (int e = ln; e < 36; e += G) {
+                    const int i = e / 6, k = e % 6;
+                    S.Iw[l][e] = S.Iw[l][e] - S.Ua[l][i] * (S.Ua[l][k] * invD);
+                }
+                if (ln == 0) {
+                    S.Dd[l] = Dv;
+                    S.uu[l] = uvv;
+                    S.mdiag[dof] = arm + imp;
+                    S.tau0[dof] = tau;
+                    S.imp[dof] = imp;
+                }
             }
-            if (p > 0) {
-                IA[p] = si_add(IA[p], x_inertia_t(E[l], r[l], Ia));
-                pA[p] = svadd(pA[p], x_force_t(E[l], r[l], pa));
-            }
+            __syncthreads();
         }
-        al[0] = sv(v3(0.0f, 0.0f, 0.0f), vscale(gb, -1.0f));
-        for (int l = 1; l < L; ++l) {
-            const int* li = A.link_i + l * MG_LINK_I_N;
-            const int p = li[0], dof = li[2];
-            SV ap = svadd(x_motion(E[l], r[l], al[p]), cl[l]);
-            if (dof >= 0) {
-                const float acc = (ul[l] - svdot(U[l], ap)) / Dl[l];
-                S.qdd[dof] = acc;
-                ap = svadd(ap, svscale(Sj[l], acc));
-            }
-            al[l] = ap;
+        if (act && ln < 6 && p > 0) {
+            float pv = S.pa[l][ln] + dot6(&S.Iw[l][ln * 6], S.cc[l]);
+            if (dof >= 0) pv = pv + S.Ua[l][ln] * uinvD;
+            S.pa[p][ln] = S.pa[p][ln] + pv;
         }
-        unsigned nm = xmask;
-        for (int d = 0; d < D; ++d) {
-            const float eff = pr[3 * nd + d0 + d];
-            if (eff > 0.0f && impd[d] != 0.0f) {
-                const float act = tau0d[d] - impd[d] * S.qdd[d];
-                if (act > eff) { nm |= 1u << d; xpos |= 1u << d; }
-                else if (act < -eff) nm |= 1u << d;
-            }
-        }
-        if (nm == xmask) break;
-        xmask = nm;
+        if (act && p > 0)
+            for (int e = ln; e < 36; e += G) S.Iw[p][e] = S.Iw[p][e] + S.Iw[l][e];
+        __syncthreads();
     }
+    // ---- outward pass: accelerations (lanes 0..5, one component each)
+    if (act && ln < 6) S.va[0][ln] = ln < 3 ? 0.0f : -(ln == 3 ? gw.x : (ln == 4 ? gw.y : gw.z));
+    for (int l = 1; l < LA; ++l) {
+        const int p = A.link_i[l * MG_LINK_I_N + 0], dof = A.link_i[l * MG_LINK_I_N + 2];
+        float a = 0.0f;
+        if (act && ln < 6) a = S.va[p][ln] + S.cc[l][ln];
+        if (dof >= 0) {
+            const float t = red16(act && ln < 6 ? S.Ua[l][ln] * a : 0.0f);
+            if (act) {
+                const float acc = (S.uu[l] - t) / S.Dd[l];
+                if (ln < 6) a = a + S.xi[l][ln] * acc;
+                if (ln == 0) S.qdd[dof] = acc;
+            }
+        }
+        if (act && ln < 6) S.va[l][ln] = a;
+    }
+    __syncthreads();
 }
 
-// Lane 0: M_eff = CRBA (link coordinates) + S.mdiag, Cholesky into S.Lc / S.invd.
+// M_eff = joint-space inertia + S.mdiag from world-frame composite inertias
+// (entrywise subtree sums of the link inertias; M_ij = xi_j . IC_i xi_i for j
+// on the path of i), then Cholesky on lane 0 and the columns of M_eff^-1 on
+// lanes 0..D-1. Called by every lane; `act` selects the envs that work.
 template <int MAXL>
-__device__ void crba_chol_lane0(const MgEnvArgs& A, EnvLds& S, int b0, int L, int D, const M3* E, const V3* r,
-                                const SV* Sj) {
-    SI IC[MAXL];
-    for (int l = 0; l < L; ++l) IC[l] = link_inertia(A.mass, A.nb, b0 + l);
-    for (int i = 0; i < D; ++i)
-        for (int j = 0; j < D; ++j) S.Lc[i][j] = 0.0f;
-    for (int l = L - 1; l >= 1; --l) {
-        const int p = A.link_i[l * MG_LINK_I_N + 0];
-        if (p > 0) IC[p] = si_add(IC[p], x_inertia_t(E[l], r[l], IC[l]));
-    }
-    for (int l = 1; l < L; ++l) {
-        const int di = A.link_i[l * MG_LINK_I_N + 2];
-        if (di < 0) continue;
-        SV Fv = si_mul(IC[l], Sj[l]);
-        S.Lc[di][di] = svdot(Sj[l], Fv) + S.mdiag[di];
-        int j = l;
-        while (A.link_i[j * MG_LINK_I_N + 0] > 0) {
-            Fv = x_force_t(E[j], r[j], Fv);
-            j = A.link_i[j * MG_LINK_I_N + 0];
+__device__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int b0, int LA, int DA, V3 x0) {
+    if (act && ln < LA) world_inertia(A.mass, A.nb, b0 + ln, S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
+    __syncthreads();
+    if (act)
+        for (int l = LA - 1; l >= 1; --l) {
+            const int p = A.link_i[l * MG_LINK_I_N + 0];
+            if (p > 0)
+                for (int e = ln; e < 36; e += G) S.Iw[p][e] = S.Iw[p][e] + S.Iw[l][e];
+        }
+    if (act && ln < DA)
+        for (int j = 0; j < DA; ++j) S.Lc[ln][j] = 0.0f;
+    __syncthreads();
+    if (act && ln < DA) {
+        const int l = S.dlink[ln];
+        float F[6];
+        for (int r = 0; r < 6; ++r) F[r] = dot6(&S.Iw[l][r * 6], S.xi[l]);
+        S.Lc[ln][ln] = dot6(S.xi[l], F) + S.mdiag[ln];
+        int j = A.link_i[l * MG_LINK_I_N + 0];
+        while (j > 0) {
             const int dj = A.link_i[j * MG_LINK_I_N + 2];
             if (dj >= 0) {
-                const float hv = svdot(Fv, Sj[j]);
-                S.Lc[di][dj] = hv;
-                S.Lc[dj][di] = hv;
+                const float hv = dot6(S.xi[j], F);
+                S.Lc[ln][dj] = hv;
+                S.Lc[dj][ln] = hv;
+            }
+            j = A.link_i[j * MG_LINK_I_N + 0];
+        }
+    }
+    __syncthreads();
+    if (act && ln == 0) {
+        for (int j = 0; j < DA; ++j) {
+            float s = S.Lc[j][j];
+            for (int k = 0; k < j; ++k) s = s - S.Lc[j][k] * S.Lc[j][k];
+            const float dj = sqrtf(s);
+            S.invd[j] = 1.0f / dj;
+            S.Lc[j][j] = dj;
+            for (int i = j + 1; i < DA; ++i) {
+                float t = S.Lc[i][j];
+                for (int k = 0; k < j; ++k) t = t - S.Lc[i][k] * S.Lc[j][k];
+                S.Lc[i][j] = t * S.invd[j];
             }
         }
     }
-    for (int j = 0; j < D; ++j) {
-        float s = S.Lc[j][j];
-        for (int k = 0; k < j; ++k) s = s - S.Lc[j][k] * S.Lc[j][k];
-        const float dj = sqrtf(s);
-        S.invd[j] = 1.0f / dj;
-        S.Lc[j][j] = dj;
-        for (int i = j + 1; i < D; ++i) {
-            float t = S.Lc[i][j];
-            for (int k = 0; k < j; ++k) t = t - S.Lc[i][k] * S.Lc[j][k];
-            S.Lc[i][j] = t * S.invd[j];
+    __syncthreads();
+    if (act && ln < DA) {
+        for (int i = 0; i < DA; ++i) {
+            float t = i == ln ? 1.0f : 0.0f;
+            for (int k = 0; k < i; ++k) t = t - S.Lc[i][k] * S.Mi[k][ln];
+            S.Mi[i][ln] = t * S.invd[i];
+        }
+        for (int i = DA - 1; i >= 0; --i) {
+            float t = S.Mi[i][ln];
+            for (int k = i + 1; k < DA; ++k) t = t - S.Lc[k][i] * S.Mi[k][ln];
+            S.Mi[i][ln] = t * S.invd[i];
         }
     }
+    __syncthreads();
 }
 
 template <int MAXL>
@@ -341,21 +455,20 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     const bool is_free = fk < nfr;
 
     // ---- substep-invariant setup
-    V3 x0 = v3(0.0f, 0.0f, 0.0f), gb = v3(0.0f, 0.0f, 0.0f);
+    V3 x0 = v3(0.0f, 0.0f, 0.0f);
     Q4 q0 = q4(0.0f, 0.0f, 0.0f, 1.0f);
-    // lane 0 private: free-body constants, contact force sums, ABA frames
+    // lane 0 private: free-body constants, contact force sums
     V3 fcom[MAXF], finvI[MAXF], fext[MAXF], text[MAXF], fsum[MAXF];
     Q4 fiq[MAXF];
     float lkeep[MAXF], akeep[MAXF], mlv2[MAXF], mav2[MAXF], gon[MAXF];
     V3 lsum[MAXL];
-    M3 E[MAXL];
-    V3 r[MAXL];
-    SV Sj[MAXL];
+    V3 gw = v3(0.0f, 0.0f, 0.0f);
+    const int LA = A.nl, DA = A.ndof;           // launch-uniform loop bounds (barriers inside)
     if (L > 0) {
         x0 = v3(St[0 * nb + b0], St[1 * nb + b0], St[2 * nb + b0]);
         q0 = qnormalize(q4(St[3 * nb + b0], St[4 * nb + b0], St[5 * nb + b0], St[6 * nb + b0]));
         const float grav_on = A.tbf[A.body_tmpl[b0] * MG_TBODY_F_N + 4];
-        gb = qrot_inv(q0, grav_on != 0.0f ? gvec : v3(0.0f, 0.0f, 0.0f));
+        gw = grav_on != 0.0f ? gvec : v3(0.0f, 0.0f, 0.0f);
     }
     if (ln == 0 && live) {
         for (int l = 0; l < L; ++l) {
@@ -402,14 +515,40 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         uv = St[(7 + fc) * nb + b];
     }
     float Jr[MAXCT * 3], Wr[MAXCT * 3];
+    PH_T0();
+    PH_MARK(6);
 
     for (int st = 0; st < P.substeps; ++st) {
         // ================= 1. unconstrained motion (lane 0)
         S.q[ln] = qv;
         S.u[ln] = uv;
         __syncthreads();
+        if (LA > 0) {
+            unsigned xmask = 0u, xpos = 0u;
+            bool redo = live && L > 0;
+            for (int att = 0; att < 2; ++att) {
+                if (!__any(redo)) break;
+                aba_world<MAXL>(P, A, S, redo, ln, b0, d0, LA, DA, x0, q0, gw, xmask, xpos);
+                // drives whose implicit force exceeds the effort limit (same masks in every lane)
+                bool again = false;
+                if (redo) {
+                    unsigned nm = xmask;
+                    for (int d = 0; d < D; ++d) {
+                        const float eff = pr[3 * nd + d0 + d];
+                        if (eff > 0.0f && S.imp[d] != 0.0f) {
+                            const float actf = S.tau0[d] - S.imp[d] * S.qdd[d];
+                            if (actf > eff) { nm |= 1u << d; xpos |= 1u << d; }
+                            else if (actf < -eff) nm |= 1u << d;
+                        }
+                    }
+                    again = nm != xmask;
+                    xmask = nm;
+                }
+                __syncthreads();
+                redo = again;
+            }
+        }
         if (ln == 0 && live) {
-            if (L > 0) aba_lane0<MAXL>(P, A, S, b0, d0, L, D, x0, q0, gb, E, r, Sj);
             for (int k = 0; k < nfr; ++k) {
                 const int s0 = D + 6 * k;
                 const S3 Iw = sym_rdrt(qmat(qmul(S.fq[k], fiq[k])), finvI[k]);
@@ -441,10 +580,15 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             uv = S.u[ln];
         }
         dp = 0.0f;
+        PH_MARK(0);
 
         // ================= 2. narrow phase: one pair per lane per round
         int base = 0;
+#ifdef MG_ENV_ABLATE_NP
+        for (int rb = 0; rb < 0; rb += G) {
+#else
         for (int rb = 0; __any(rb < npair); rb += G) {
+#endif
             const int pi = rb + ln;
             PairOut o;
             o.n = 0;
@@ -511,27 +655,55 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             }
             base += total;
         }
+        // joint-limit rows (PhysX solves limits as constraints): a DOF whose
+        // predicted position q + h u lies within 5% of its range of a limit gets
+        // one unilateral row towards the nearer limit, after the contacts
+        {
+            int need = 0, sgn = 0;
+            float s0 = 0.0f;
+            if (live && is_dof) {
+                const int gd = d0 + ln;
+                if (pr[7 * nd + gd] != 0.0f) {
+                    const float lo = pr[5 * nd + gd], hi = pr[6 * nd + gd];
+                    const float q1 = qv + h * uv;
+                    const float mg = 0.05f * (hi - lo);
+                    if (q1 - lo < mg || hi - q1 < mg) {
+                        need = 1;
+                        sgn = (q1 - lo) < (hi - q1) ? 1 : -1;
+                        s0 = sgn > 0 ? qv - lo : hi - qv;
+                    }
+                }
+            }
+            int incl = need;
+#pragma unroll
+            for (int off = 1; off < G; off <<= 1) {
+                const int t = __shfl_up(incl, off, G);
+                if (ln >= off) incl += t;
+            }
+            const int total = __shfl(incl, G - 1, G);
+            const int c = base + incl - need;
+            if (need && c < MAXCT) {
+                S.ca[c] = LIM0 + ln;
+                S.cb[c] = sgn;
+                S.cp[c] = v3(0.0f, 0.0f, 0.0f);
+                S.cd[c][0] = v3(0.0f, 0.0f, 0.0f);
+                S.cd[c][1] = v3(0.0f, 0.0f, 0.0f);
+                S.cd[c][2] = v3(0.0f, 0.0f, 0.0f);
+                S.cs0[c] = s0;
+                S.cmu[c] = 0.0f;
+                S.ce[c] = 0.0f;
+                S.link_rows = 1;
+            }
+            base += total;
+        }
         const int nct = base < MAXCT ? base : MAXCT;
         __syncthreads();
+        PH_MARK(1);
 
         // ================= 3. rows
-        const bool link_rows = S.link_rows != 0;
-        if (ln == 0 && live && link_rows) crba_chol_lane0<MAXL>(A, S, b0, L, D, E, r, Sj);
-        __syncthreads();
-        if (link_rows && is_dof) {
-            // column ln of M_eff^-1: forward then backward substitution, in place in LDS
-            for (int i = 0; i < D; ++i) {
-                float t = i == ln ? 1.0f : 0.0f;
-                for (int k = 0; k < i; ++k) t = t - S.Lc[i][k] * S.Mi[k][ln];
-                S.Mi[i][ln] = t * S.invd[i];
-            }
-            for (int i = D - 1; i >= 0; --i) {
-                float t = S.Mi[i][ln];
-                for (int k = i + 1; k < D; ++k) t = t - S.Lc[k][i] * S.Mi[k][ln];
-                S.Mi[i][ln] = t * S.invd[i];
-            }
-        }
-        __syncthreads();
+        const bool link_rows = live && S.link_rows != 0;
+        if (LA > 0 && __any(link_rows)) meff_world<MAXL>(A, S, link_rows, ln, b0, LA, DA, x0);
+        PH_MARK(2);
 #pragma unroll
         for (int c = 0; c < MAXCT; ++c) {
 #pragma unroll
@@ -546,7 +718,9 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 for (int rw = 0; rw < 3; ++rw) {
                     const V3 dir = S.cd[c][rw];
                     float J = 0.0f, W = 0.0f;
-                    if (is_dof) {
+                    if (a >= LIM0) {
+                        if (rw == 0 && ln == a - LIM0) J = (float)b;
+                    } else if (is_dof) {
                         if (a < F0 && ((S.amask[a] >> ln) & 1)) {
                             const int j = S.dlink[ln];
                             J = S.drev[ln] ? vdot(vcross(S.zl[j], vsub(p, S.xl[j])), dir) : vdot(S.zl[j], dir);
@@ -574,7 +748,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     }
                     Jr[c * 3 + rw] = J;
                     Wr[c * 3 + rw] = W;
-                    const float kk = 1.0f / red16(J * W);
+                    const float den = red16(J * W);
+                    const float kk = den > 0.0f ? 1.0f / den : 0.0f;
                     if (ln == 0) {
                         S.ck[c][rw] = kk;
                         S.clam[c][rw] = 0.0f;
@@ -585,10 +760,15 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             }
         }
         __syncthreads();
+        PH_MARK(3);
 
         // ================= 4. TGS (the lambdas are kept by lane 0 in LDS; every
         // lane of the env computes the same value)
+#ifdef MG_ENV_ABLATE_TGS
+        for (int it = 0; it < 0; ++it) {
+#else
         for (int it = 0; it < P.npos + P.nvel; ++it) {
+#endif
             const bool pos = it < P.npos;
 #pragma unroll
             for (int c = 0; c < MAXCT; ++c) {
@@ -632,6 +812,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             if (pos) dp = dp + uv * P.sub;
         }
         __syncthreads();
+        PH_MARK(4);
 
         // ================= 5. integrate
         if (is_dof) {
@@ -656,6 +837,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 imp = vmad(imp, S.cd[c][1], S.clam[c][1]);
                 imp = vmad(imp, S.cd[c][2], S.clam[c][2]);
                 const int a = S.ca[c], b = S.cb[c];
+                if (a >= LIM0) continue;
                 if (a >= F0) fsum[a - F0] = vadd(fsum[a - F0], imp);
                 else lsum[a] = vadd(lsum[a], imp);
                 if (b >= F0 && b < ST0) fsum[b - F0] = vsub(fsum[b - F0], imp);
@@ -670,6 +852,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             }
         }
         __syncthreads();
+        PH_MARK(5);
     }
 
     // ---- outputs

@@ -90,6 +90,7 @@ struct MgArticArgs {
 #define MG_ENV_MAXCT  16     // contacts per env per substep
 #define MG_ENV_FREE0  16
 #define MG_ENV_STATIC0 32
+#define MG_ENV_LIMIT0  64     // joint-limit row of DOF d: a = MG_ENV_LIMIT0 + d, b = +1 lower / -1 upper
 
 struct MgEnvArgs {
     int          ne;          // envs in this launch

@@ -37,12 +37,22 @@ def run(n, warm=150, steps=100):
                           mm[:, :7, :7], bi, hi)
         gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(pa))
         gym.set_dof_actuation_force_tensor(sim, gymtorch.unwrap_tensor(ea))
+        if k == warm - 1 and hasattr(N.lib, "mg_debug_env_phase_reset"):
+            torch.cuda.synchronize()
+            N.lib.mg_debug_env_phase_reset()
     torch.cuda.synchronize()
+    phases = None
+    if hasattr(N.lib, "mg_debug_env_phase"):
+        buf = (ctypes.c_ulonglong * 8)()
+        N.lib.mg_debug_env_phase(buf)
+        waves = (n + 3) // 4
+        names = ["unconstrained", "narrowphase", "crba_minv", "rows", "tgs", "integrate", "setup"]
+        phases = {nm: buf[i] / waves / steps for i, nm in enumerate(names)}   # cycles per wave per frame
     avg, lo = ctypes.c_float(), ctypes.c_float()
     used = N.lib.mg_step_time_stats(sim.native, steps, ctypes.byref(avg), ctypes.byref(lo), None)
     gym.destroy_sim(sim)
     return {"lib": os.path.basename(N.LIB_PATH), "envs": n, "kernel_us_avg": 1e3 * avg.value,
-            "kernel_us_min": 1e3 * lo.value, "launches": used}
+            "kernel_us_min": 1e3 * lo.value, "launches": used, "phase_cycles_per_wave": phases}
 
 
 if __name__ == "__main__":
