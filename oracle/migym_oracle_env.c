@@ -116,85 +116,100 @@ static void box_box_(const cshape_t* A, const cshape_t* B, float margin, pair_t*
             sa = (b * e - dd) / den;
             sb = (e - b * dd) / den;
         }
-        sa = fminf(fmaxf(sa, -ha[ei]), ha[ei]);
-        sb = fminf(fmaxf(sb, -hb[ej]), hb[ej]);
+        sa = fminf(fmaxf(sa, -vc_(A->h, ei)), vc_(A->h, ei));
+        sb = fminf(fmaxf(sb, -vc_(B->h, ej)), vc_(B->h, ej));
         ca = add3(pa, mul3(ua, sa));
         cb = add3(pb, mul3(ub, sb));
         ppush_(o, mul3(add3(ca, cb), 0.5f), mul3(ax, -1.0f), best_edge);
         return;
     }
     {
+        /* face contact (mg_collide.h): candidate set in the reference face's
+         * (u, v) frame — incident corners inside the rectangle (0..3), rectangle
+         * corners inside the quad (4..7), edge k x side j crossings (8 + 4k + j);
+         * the 4 deepest within the margin, lowest index on ties */
         const int refA = face < 3;
         const cshape_t* Rf = refA ? A : B;
         const cshape_t* In = refA ? B : A;
         const int fa = refA ? face : face - 3;
-        const float hr[3] = {Rf->h.x, Rf->h.y, Rf->h.z}, hi[3] = {In->h.x, In->h.y, In->h.z};
-        v3_t nref = mcol_(Rf->R, fa), iax, ifc, eu, ev, U, W, rc, inrm;
-        int ik = 0, iu, iv, ru, rv, np = 4, side, m, used[8];
-        float bestd = 1e30f, px[8], py[8], dep[8], den;
-        v3_t pts[8];
+        v3_t nref = mcol_(Rf->R, fa), iax, ifc, eu, ev, U, W, rc, inrm, nn;
+        int ik = 0, iu, iv, ru, rv, m, c;
+        float bestd = 1e30f, hik, hu, hv, qx[4], qy[4], cx[24], cy[24], cdep[24], den;
+        unsigned cvalid = 0u, used = 0u;
         if (dot3(sub3(In->c, Rf->c), nref) < 0.0f) nref = mul3(nref, -1.0f);
         for (k = 0; k < 3; ++k) {
             const float dk = -fabsf(dot3(nref, mcol_(In->R, k)));
             if (dk < bestd) { bestd = dk; ik = k; }
         }
         iax = mcol_(In->R, ik);
-        ifc = add3(In->c, mul3(iax, dot3(nref, iax) > 0.0f ? -hi[ik] : hi[ik]));
+        hik = vc_(In->h, ik);
+        ifc = add3(In->c, mul3(iax, dot3(nref, iax) > 0.0f ? -hik : hik));
         iu = ik == 0 ? 1 : 0; iv = ik == 2 ? 1 : 2;
-        eu = mul3(mcol_(In->R, iu), hi[iu]); ev = mul3(mcol_(In->R, iv), hi[iv]);
+        eu = mul3(mcol_(In->R, iu), vc_(In->h, iu)); ev = mul3(mcol_(In->R, iv), vc_(In->h, iv));
         ru = fa == 0 ? 1 : 0; rv = fa == 2 ? 1 : 2;
         U = mcol_(Rf->R, ru); W = mcol_(Rf->R, rv);
-        rc = add3(Rf->c, mul3(nref, hr[fa]));
+        hu = vc_(Rf->h, ru); hv = vc_(Rf->h, rv);
+        rc = add3(Rf->c, mul3(nref, vc_(Rf->h, fa)));
         {
             const v3_t q0 = sub3(sub3(ifc, eu), ev), q1 = sub3(add3(ifc, eu), ev);
             const v3_t q2 = add3(add3(ifc, eu), ev), q3 = add3(sub3(ifc, eu), ev);
-            px[0] = dot3(sub3(q0, rc), U); py[0] = dot3(sub3(q0, rc), W);
-            px[1] = dot3(sub3(q1, rc), U); py[1] = dot3(sub3(q1, rc), W);
-            px[2] = dot3(sub3(q2, rc), U); py[2] = dot3(sub3(q2, rc), W);
-            px[3] = dot3(sub3(q3, rc), U); py[3] = dot3(sub3(q3, rc), W);
+            qx[0] = dot3(sub3(q0, rc), U); qy[0] = dot3(sub3(q0, rc), W);
+            qx[1] = dot3(sub3(q1, rc), U); qy[1] = dot3(sub3(q1, rc), W);
+            qx[2] = dot3(sub3(q2, rc), U); qy[2] = dot3(sub3(q2, rc), W);
+            qx[3] = dot3(sub3(q3, rc), U); qy[3] = dot3(sub3(q3, rc), W);
         }
-        for (side = 0; side < 4; ++side) {
-            const float lim = side < 2 ? hr[ru] : hr[rv];
-            const float sg = (side & 1) ? -1.0f : 1.0f;
-            float ox[8], oy[8];
-            int no = 0;
-            for (k = 0; k < np; ++k) {
-                const int k2 = k + 1 == np ? 0 : k + 1;
-                const float a0 = sg * (side < 2 ? px[k] : py[k]) - lim;
-                const float a1 = sg * (side < 2 ? px[k2] : py[k2]) - lim;
-                if (a0 <= 0.0f && no < 8) { ox[no] = px[k]; oy[no] = py[k]; no = no + 1; }
-                if ((a0 <= 0.0f) != (a1 <= 0.0f) && no < 8) {
-                    const float tt = a0 / (a0 - a1);
-                    ox[no] = px[k] + (px[k2] - px[k]) * tt;
-                    oy[no] = py[k] + (py[k2] - py[k]) * tt;
-                    no = no + 1;
-                }
+        for (k = 0; k < 4; ++k) {
+            cx[k] = qx[k]; cy[k] = qy[k];
+            if (fabsf(qx[k]) <= hu && fabsf(qy[k]) <= hv) cvalid |= 1u << k;
+        }
+        for (m = 0; m < 4; ++m) {
+            const float X = (m & 1) ? hu : -hu, Y = (m & 2) ? hv : -hv;
+            int pos = 1, neg = 1;
+            for (k = 0; k < 4; ++k) {
+                const int k2 = (k + 1) & 3;
+                const float sk = (qx[k2] - qx[k]) * (Y - qy[k]) - (qy[k2] - qy[k]) * (X - qx[k]);
+                pos = pos && sk >= 0.0f;
+                neg = neg && sk <= 0.0f;
             }
-            np = no;
-            for (k = 0; k < np; ++k) { px[k] = ox[k]; py[k] = oy[k]; }
-            if (np == 0) return;
+            cx[4 + m] = X; cy[4 + m] = Y;
+            if (pos || neg) cvalid |= 1u << (4 + m);
+        }
+        for (k = 0; k < 4; ++k) {
+            const int k2 = (k + 1) & 3;
+            int j;
+            for (j = 0; j < 4; ++j) {
+                const int ci = 8 + 4 * k + j;
+                const int xs = j < 2;
+                const float lim = xs ? (j == 0 ? hu : -hu) : (j == 2 ? hv : -hv);
+                const float a0 = xs ? qx[k] : qy[k], a1 = xs ? qx[k2] : qy[k2];
+                const float o0 = xs ? qy[k] : qx[k], o1 = xs ? qy[k2] : qx[k2];
+                const float da = a0 - lim, db = a1 - lim;
+                const int ok = (da < 0.0f) != (db < 0.0f);
+                const float t = ok ? da / (da - db) : 0.0f;
+                const float ov = o0 + (o1 - o0) * t;
+                cx[ci] = xs ? lim : ov;
+                cy[ci] = xs ? ov : lim;
+                if (ok && fabsf(ov) <= (xs ? hv : hu)) cvalid |= 1u << ci;
+            }
         }
         inrm = mul3(iax, dot3(nref, iax) > 0.0f ? -1.0f : 1.0f);
         den = dot3(inrm, nref);
-        for (k = 0; k < np; ++k) {
-            const v3_t qq = add3(add3(rc, mul3(U, px[k])), mul3(W, py[k]));
-            float tt = 0.0f;
-            if (fabsf(den) > 1e-6f) tt = dot3(sub3(ifc, qq), inrm) / den;
-            pts[k] = add3(qq, mul3(nref, tt));
-            dep[k] = tt;
+        for (c = 0; c < 24; ++c) {
+            const v3_t qq = add3(add3(rc, mul3(U, cx[c])), mul3(W, cy[c]));
+            cdep[c] = fabsf(den) > 1e-6f ? dot3(sub3(ifc, qq), inrm) / den : 0.0f;
         }
-        for (k = 0; k < 8; ++k) used[k] = 0;
+        nn = refA ? mul3(nref, -1.0f) : nref;
         for (m = 0; m < OE_PMAX; ++m) {
             int bk = -1;
-            float bd = margin;
-            for (k = 0; k < np; ++k)
-                if (!used[k] && dep[k] < bd) { bd = dep[k]; bk = k; }
-            if (bk < 0) break;
-            used[bk] = 1;
-            {
-                const v3_t n = refA ? mul3(nref, -1.0f) : nref;
-                const v3_t pA = refA ? sub3(pts[bk], mul3(nref, dep[bk])) : pts[bk];
-                ppush_(o, pA, n, dep[bk]);
+            float bd = margin, x = 0.0f, y = 0.0f;
+            for (c = 0; c < 24; ++c)
+                if (((cvalid & ~used) >> c) & 1u)
+                    if (cdep[c] < bd) { bd = cdep[c]; bk = c; x = cx[c]; y = cy[c]; }
+            if (bk >= 0) {
+                const v3_t qq = add3(add3(rc, mul3(U, x)), mul3(W, y));
+                const v3_t pt = add3(qq, mul3(nref, bd));
+                used |= 1u << bk;
+                ppush_(o, refA ? sub3(pt, mul3(nref, bd)) : pt, nn, bd);
             }
         }
     }

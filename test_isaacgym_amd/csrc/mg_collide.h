@@ -36,11 +36,12 @@ MG_HD float m3c(const M3& R, int i, int k) {      // component k of column i
 MG_HD V3 m3col(const M3& R, int i) { return i == 0 ? R.c0 : (i == 1 ? R.c1 : R.c2); }
 MG_HD float v3c(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
+// static slot writes (no dynamic indexing: the record stays in registers)
 MG_HD void pair_push(PairOut& o, V3 p, V3 n, float sep) {
-    if (o.n < MG_PAIR_MAXC) {
-        o.p[o.n] = p; o.nrm[o.n] = n; o.sep[o.n] = sep;
-        o.n = o.n + 1;
-    }
+#pragma unroll
+    for (int k = 0; k < MG_PAIR_MAXC; ++k)
+        if (o.n == k) { o.p[k] = p; o.nrm[k] = n; o.sep[k] = sep; }
+    if (o.n < MG_PAIR_MAXC) o.n = o.n + 1;
 }
 
 // sphere A (centre a, radius ra) vs sphere B
@@ -146,97 +147,120 @@ MG_HD void box_box(const CShape& A, const CShape& B, float margin, PairOut& o) {
             sa = (b * e - dd) / den;
             sb = (e - b * dd) / den;
         }
-        sa = fminf(fmaxf(sa, -ha[ei]), ha[ei]);
-        sb = fminf(fmaxf(sb, -hb[ej]), hb[ej]);
+        const float hae = v3c(A.h, ei), hbe = v3c(B.h, ej);
+        sa = fminf(fmaxf(sa, -hae), hae);
+        sb = fminf(fmaxf(sb, -hbe), hbe);
         const V3 ca = vadd(pa, vscale(ua, sa));
         const V3 cb = vadd(pb, vscale(ub, sb));
         pair_push(o, vscale(vadd(ca, cb), 0.5f), vscale(ax, -1.0f), best_edge);
         return;
     }
-    // face contact: reference box / axis, incident box
+    // face contact: reference box / axis, incident box. The contact polygon is
+    // the intersection of the incident face with the reference face, taken from a
+    // fixed candidate set in the reference face's (u, v) frame: the incident
+    // quad's corners inside the reference rectangle (0..3), the rectangle's
+    // corners inside the quad (4..7), the crossings of quad edge k with
+    // rectangle side j (8 + 4k + j); the 4 deepest within the margin are kept,
+    // lowest index first on ties.
     const bool refA = face < 3;
     const CShape& Rf = refA ? A : B;
     const CShape& In = refA ? B : A;
     const int fa = refA ? face : face - 3;
-    const float hr[3] = {Rf.h.x, Rf.h.y, Rf.h.z};
-    const float hi[3] = {In.h.x, In.h.y, In.h.z};
     V3 nref = m3col(Rf.R, fa);                         // outward normal of the reference face, towards In
     if (vdot(vsub(In.c, Rf.c), nref) < 0.0f) nref = vscale(nref, -1.0f);
-    // incident face: most anti-parallel to nref
     int ik = 0;
     float bestd = 1e30f;
+#pragma unroll
     for (int k = 0; k < 3; ++k) {
         const float dk = -fabsf(vdot(nref, m3col(In.R, k)));
         if (dk < bestd) { bestd = dk; ik = k; }
     }
     const V3 iax = m3col(In.R, ik);
-    const V3 ifc = vadd(In.c, vscale(iax, vdot(nref, iax) > 0.0f ? -hi[ik] : hi[ik]));
+    const float hik = v3c(In.h, ik);
+    const V3 ifc = vadd(In.c, vscale(iax, vdot(nref, iax) > 0.0f ? -hik : hik));
     const int iu = ik == 0 ? 1 : 0, iv = ik == 2 ? 1 : 2;
-    const V3 eu = vscale(m3col(In.R, iu), hi[iu]), ev = vscale(m3col(In.R, iv), hi[iv]);
-    // polygon in the reference face frame (u, v): up to 8 vertices
+    const V3 eu = vscale(m3col(In.R, iu), v3c(In.h, iu)), ev = vscale(m3col(In.R, iv), v3c(In.h, iv));
     const int ru = fa == 0 ? 1 : 0, rv = fa == 2 ? 1 : 2;
     const V3 U = m3col(Rf.R, ru), W = m3col(Rf.R, rv);
-    const V3 rc = vadd(Rf.c, vscale(nref, hr[fa]));     // reference face centre
-    float px[8], py[8];
-    int np = 4;
+    const float hu = v3c(Rf.h, ru), hv = v3c(Rf.h, rv);
+    const V3 rc = vadd(Rf.c, vscale(nref, v3c(Rf.h, fa)));     // reference face centre
+    float qx[4], qy[4];
     {
         const V3 q0 = vsub(vsub(ifc, eu), ev), q1 = vsub(vadd(ifc, eu), ev);
         const V3 q2 = vadd(vadd(ifc, eu), ev), q3 = vadd(vsub(ifc, eu), ev);
-        px[0] = vdot(vsub(q0, rc), U); py[0] = vdot(vsub(q0, rc), W);
-        px[1] = vdot(vsub(q1, rc), U); py[1] = vdot(vsub(q1, rc), W);
-        px[2] = vdot(vsub(q2, rc), U); py[2] = vdot(vsub(q2, rc), W);
-        px[3] = vdot(vsub(q3, rc), U); py[3] = vdot(vsub(q3, rc), W);
+        qx[0] = vdot(vsub(q0, rc), U); qy[0] = vdot(vsub(q0, rc), W);
+        qx[1] = vdot(vsub(q1, rc), U); qy[1] = vdot(vsub(q1, rc), W);
+        qx[2] = vdot(vsub(q2, rc), U); qy[2] = vdot(vsub(q2, rc), W);
+        qx[3] = vdot(vsub(q3, rc), U); qy[3] = vdot(vsub(q3, rc), W);
     }
-    // clip against u <= hu, -u <= hu, v <= hv, -v <= hv
-    for (int side = 0; side < 4; ++side) {
-        const float lim = side < 2 ? hr[ru] : hr[rv];
-        const float sg = (side & 1) ? -1.0f : 1.0f;
-        float ox[8], oy[8];
-        int no = 0;
-        for (int k = 0; k < np; ++k) {
-            const int k2 = k + 1 == np ? 0 : k + 1;
-            const float a0 = sg * (side < 2 ? px[k] : py[k]) - lim;
-            const float a1 = sg * (side < 2 ? px[k2] : py[k2]) - lim;
-            if (a0 <= 0.0f && no < 8) { ox[no] = px[k]; oy[no] = py[k]; no = no + 1; }
-            if ((a0 <= 0.0f) != (a1 <= 0.0f) && no < 8) {
-                const float tt = a0 / (a0 - a1);
-                ox[no] = px[k] + (px[k2] - px[k]) * tt;
-                oy[no] = py[k] + (py[k2] - py[k]) * tt;
-                no = no + 1;
-            }
+    float cx[24], cy[24];
+    unsigned cvalid = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        cx[k] = qx[k];
+        cy[k] = qy[k];
+        if (fabsf(qx[k]) <= hu && fabsf(qy[k]) <= hv) cvalid |= 1u << k;
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const float X = (m & 1) ? hu : -hu, Y = (m & 2) ? hv : -hv;
+        bool pos = true, neg = true;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int k2 = (k + 1) & 3;
+            const float sk = (qx[k2] - qx[k]) * (Y - qy[k]) - (qy[k2] - qy[k]) * (X - qx[k]);
+            pos = pos && sk >= 0.0f;
+            neg = neg && sk <= 0.0f;
         }
-        np = no;
-        for (int k = 0; k < np; ++k) { px[k] = ox[k]; py[k] = oy[k]; }
-        if (np == 0) return;
+        cx[4 + m] = X;
+        cy[4 + m] = Y;
+        if (pos || neg) cvalid |= 1u << (4 + m);
     }
-    // depth of each clipped point below the reference face: project onto the
-    // incident face plane along nref to get the point on the incident body
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int k2 = (k + 1) & 3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = 8 + 4 * k + j;
+            const bool xs = j < 2;
+            const float lim = xs ? (j == 0 ? hu : -hu) : (j == 2 ? hv : -hv);
+            const float a0 = xs ? qx[k] : qy[k], a1 = xs ? qx[k2] : qy[k2];
+            const float o0 = xs ? qy[k] : qx[k], o1 = xs ? qy[k2] : qx[k2];
+            const float da = a0 - lim, db = a1 - lim;
+            const bool ok = (da < 0.0f) != (db < 0.0f);
+            const float t = ok ? da / (da - db) : 0.0f;
+            const float ov = o0 + (o1 - o0) * t;
+            cx[c] = xs ? lim : ov;
+            cy[c] = xs ? ov : lim;
+            if (ok && fabsf(ov) <= (xs ? hv : hu)) cvalid |= 1u << c;
+        }
+    }
+    // depth of each candidate below the reference face (along nref, to the incident plane)
     const V3 inrm = vscale(iax, vdot(nref, iax) > 0.0f ? -1.0f : 1.0f);
     const float den = vdot(inrm, nref);
-    float dep[8];
-    V3 pts[8];
-    for (int k = 0; k < np; ++k) {
-        const V3 q = vadd(vadd(rc, vscale(U, px[k])), vscale(W, py[k]));   // on the reference plane
-        float tt = 0.0f;
-        if (fabsf(den) > 1e-6f) tt = vdot(vsub(ifc, q), inrm) / den;
-        pts[k] = vadd(q, vscale(nref, tt));                              // on the incident face
-        dep[k] = tt;                                                     // separation along nref
+    float cdep[24];
+#pragma unroll
+    for (int c = 0; c < 24; ++c) {
+        const V3 q = vadd(vadd(rc, vscale(U, cx[c])), vscale(W, cy[c]));
+        cdep[c] = fabsf(den) > 1e-6f ? vdot(vsub(ifc, q), inrm) / den : 0.0f;
     }
-    // keep the (up to) 4 deepest within the margin, lowest index first on ties
-    bool used[8];
-    for (int k = 0; k < 8; ++k) used[k] = false;
+    const V3 n = refA ? vscale(nref, -1.0f) : nref;    // from B towards A
+    unsigned used = 0u;
+#pragma unroll
     for (int m = 0; m < MG_PAIR_MAXC; ++m) {
         int bk = -1;
-        float bd = margin;
-        for (int k = 0; k < np; ++k)
-            if (!used[k] && dep[k] < bd) { bd = dep[k]; bk = k; }
-        if (bk < 0) break;
-        used[bk] = true;
-        // normal from B towards A: nref points from the reference box to the incident box
-        const V3 n = refA ? vscale(nref, -1.0f) : nref;
-        // the point lies on the incident box: on B when A is the reference, on A otherwise
-        const V3 pA = refA ? vsub(pts[bk], vscale(nref, dep[bk])) : pts[bk];
-        pair_push(o, pA, n, dep[bk]);
+        float bd = margin, x = 0.0f, y = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 24; ++c)
+            if (((cvalid & ~used) >> c) & 1u)
+                if (cdep[c] < bd) { bd = cdep[c]; bk = c; x = cx[c]; y = cy[c]; }
+        if (bk >= 0) {
+            used |= 1u << bk;
+            const V3 q = vadd(vadd(rc, vscale(U, x)), vscale(W, y));     // on the reference plane
+            const V3 pt = vadd(q, vscale(nref, bd));                    // on the incident face
+            // the point lies on the incident box: on B when A is the reference, on A otherwise
+            pair_push(o, refA ? vsub(pt, vscale(nref, bd)) : pt, n, bd);
+        }
     }
 }
 
@@ -262,8 +286,9 @@ MG_HD void collide(const CShape& A, const CShape& B, float margin, PairOut& o) {
         PairOut t;
         t.n = 0;
         for (int k = 0; k < nbs; ++k) sphere_box(cb[k], rb, A, margin, t);
-        for (int k = 0; k < t.n; ++k)     // swap roles: point on A, normal from B to A
-            pair_push(o, vadd(t.p[k], vscale(t.nrm[k], t.sep[k])), vscale(t.nrm[k], -1.0f), t.sep[k]);
+#pragma unroll
+        for (int k = 0; k < MG_PAIR_MAXC; ++k)     // swap roles: point on A, normal from B to A
+            if (k < t.n) pair_push(o, vadd(t.p[k], vscale(t.nrm[k], t.sep[k])), vscale(t.nrm[k], -1.0f), t.sep[k]);
         return;
     }
     for (int k = 0; k < na; ++k)

@@ -157,17 +157,14 @@ MG_HD void ground_pair(const MgStep& P, const CShape& s, PairOut& o) {
     }
 }
 
-MG_HD SI link_inertia(const float* Ms, int nb, int b) {
-    const float m = Ms[11 * nb + b];
-    const V3 com = v3(Ms[8 * nb + b], Ms[9 * nb + b], Ms[10 * nb + b]);
-    const Q4 iq = q4(Ms[4 * nb + b], Ms[5 * nb + b], Ms[6 * nb + b], Ms[7 * nb + b]);
-    const V3 invI = v3(Ms[1 * nb + b], Ms[2 * nb + b], Ms[3 * nb + b]);
-    const V3 Id = v3(invI.x > 0.0f ? 1.0f / invI.x : 0.0f, invI.y > 0.0f ? 1.0f / invI.y : 0.0f,
-                     invI.z > 0.0f ? 1.0f / invI.z : 0.0f);
-    const M3 Rq = qmat(iq);
-    return si_rigid(m, com, m3mul(m3mul(Rq, m3cols(v3(Id.x, 0.0f, 0.0f), v3(0.0f, Id.y, 0.0f), v3(0.0f, 0.0f, Id.z))),
-                                  m3t(Rq)));
+// radius of a sphere around the shape centre enclosing the shape
+MG_HD float bound_radius(const float* sh) {
+    const int t = (int)sh[0];
+    if (t == MG_SHAPE_BOX) return sqrtf(sh[1] * sh[1] + sh[2] * sh[2] + sh[3] * sh[3]);
+    if (t == MG_SHAPE_CAPSULE) return sh[1] + sh[2];
+    return sh[1];
 }
+
 
 MG_HD float dot6(const float* a, const float* b) {
     return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
@@ -605,15 +602,18 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 Q4 qa;
                 if (pa >= F0) { xa = S.fx[pa - F0]; qa = S.fq[pa - F0]; }
                 else { xa = S.xl[pa]; qa = S.ql[pa]; }
-                const CShape ca = place_shape(sha, xa, qa);
+                // bounding-sphere rejection (conservative: a rejected pair has no
+                // contact within the margin, so the result is unchanged)
+                const V3 cA = vadd(xa, qrot(qa, v3(sha[4], sha[5], sha[6])));
+                const float rA = bound_radius(sha);
+                bool near = true;
+                V3 xb = v3(0.0f, 0.0f, 0.0f);
+                Q4 qbb = q4(0.0f, 0.0f, 0.0f, 1.0f);
+                const float* shb = sha;
                 if (pb < 0) {
-                    ground_pair(P, ca, o);
-                    mu = 0.5f * (sha[11] + P.mu_ground);
-                    rest = 0.5f * (sha[12] + P.e_ground);
+                    near = vdot(v3(P.n[0], P.n[1], P.n[2]), cA) + P.pd - rA < P.contact_offset;
                 } else {
-                    const float* shb = A.shapes + sb * MG_SHAPE_STRIDE;
-                    V3 xb;
-                    Q4 qbb;
+                    shb = A.shapes + sb * MG_SHAPE_STRIDE;
                     if (pb >= ST0) {
                         const int bs = ei[8 + pb - ST0];
                         xb = v3(St[0 * nb + bs], St[1 * nb + bs], St[2 * nb + bs]);
@@ -625,9 +625,21 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         xb = S.xl[pb];
                         qbb = S.ql[pb];
                     }
-                    collide(ca, place_shape(shb, xb, qbb), P.contact_offset, o);
-                    mu = 0.5f * (sha[11] + shb[11]);
-                    rest = 0.5f * (sha[12] + shb[12]);
+                    const V3 d = vsub(vadd(xb, qrot(qbb, v3(shb[4], shb[5], shb[6]))), cA);
+                    const float rr = rA + bound_radius(shb) + P.contact_offset;
+                    near = vdot(d, d) < rr * rr * 1.0001f + 1e-6f;
+                }
+                if (near) {
+                    const CShape ca = place_shape(sha, xa, qa);
+                    if (pb < 0) {
+                        ground_pair(P, ca, o);
+                        mu = 0.5f * (sha[11] + P.mu_ground);
+                        rest = 0.5f * (sha[12] + P.e_ground);
+                    } else {
+                        collide(ca, place_shape(shb, xb, qbb), P.contact_offset, o);
+                        mu = 0.5f * (sha[11] + shb[11]);
+                        rest = 0.5f * (sha[12] + shb[12]);
+                    }
                 }
             }
             // exclusive prefix sum of the counts over the 16 lanes
@@ -639,9 +651,10 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             }
             const int total = __shfl(incl, G - 1, G);
             const int slot0 = base + incl - o.n;
-            for (int j = 0; j < o.n; ++j) {
+#pragma unroll
+            for (int j = 0; j < MG_PAIR_MAXC; ++j) {
                 const int c = slot0 + j;
-                if (c < MAXCT) {
+                if (j < o.n && c < MAXCT) {
                     S.ca[c] = pa;
                     S.cb[c] = pb;
                     S.cp[c] = o.p[j];
