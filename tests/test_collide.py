@@ -1,0 +1,146 @@
+"""Narrow phase of the coupled per-env step (mg_collide.h, restated by
+oracle/migym_oracle_env.c:collide_) against independent float64 geometry.
+
+Box-box: existence of contacts must agree with a float64 separating-axis test
+(15 axes) outside a +-1e-4 m band around the margin; normals are unit length and
+point from B towards A; every reported point lies on box A's surface shell and
+within |sep| + 1e-3 m of box B. Known answers: a box resting on a larger box
+(4 bottom corners, normal +z, zero separation), a sphere above a box face, an
+edge-edge crossing. Parity of the device narrow phase with this restatement is
+covered bit for bit by tests/test_franka_gpu.py.
+"""
+import math
+
+import numpy as np
+
+import oracle
+
+BOX, SPHERE, CAPSULE = 1, 0, 2
+
+
+def _quat(axis, ang):
+    axis = np.asarray(axis, np.float64)
+    axis = axis / np.linalg.norm(axis)
+    s = math.sin(0.5 * ang)
+    return np.array([axis[0] * s, axis[1] * s, axis[2] * s, math.cos(0.5 * ang)])
+
+
+def _rot(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+def _shape(t, c, q, h):
+    return np.array([t, *c, *q, *h], np.float32)
+
+
+def _sat(c1, R1, h1, c2, R2, h2):
+    d = c2 - c1
+    axes = [R1[:, i] for i in range(3)] + [R2[:, i] for i in range(3)]
+    axes += [np.cross(R1[:, i], R2[:, j]) for i in range(3) for j in range(3)]
+    best = -1e30
+    for ax in axes:
+        n = np.linalg.norm(ax)
+        if n < 1e-6:
+            continue
+        ax = ax / n
+        r1 = sum(h1[k] * abs(ax @ R1[:, k]) for k in range(3))
+        r2 = sum(h2[k] * abs(ax @ R2[:, k]) for k in range(3))
+        best = max(best, abs(d @ ax) - r1 - r2)
+    return best
+
+
+def _box_dist(p, c, R, h):
+    """signed distance from p to the box surface (negative inside)."""
+    loc = R.T @ (p - c)
+    q = np.abs(loc) - h
+    outside = np.linalg.norm(np.maximum(q, 0.0))
+    return outside + min(max(q[0], q[1], q[2]), 0.0)
+
+
+def test_box_box_random_against_float64_sat():
+    rng = np.random.RandomState(7)
+    margin = 0.01
+    checked = contacts = 0
+    for _ in range(3000):
+        h1 = rng.uniform(0.05, 0.5, 3)
+        h2 = rng.uniform(0.05, 0.5, 3)
+        q1 = _quat(rng.normal(size=3), rng.uniform(-math.pi, math.pi))
+        q2 = _quat(rng.normal(size=3), rng.uniform(-math.pi, math.pi))
+        c1 = rng.uniform(-0.2, 0.2, 3)
+        c2 = c1 + rng.normal(size=3) * rng.uniform(0.1, 1.0)
+        A = _shape(BOX, c1, q1, h1)
+        B = _shape(BOX, c2, q2, h2)
+        # the device works in float32: compare against the float32-rounded inputs
+        c1, c2 = A[1:4].astype(np.float64), B[1:4].astype(np.float64)
+        R1, R2 = _rot(A[4:8].astype(np.float64)), _rot(B[4:8].astype(np.float64))
+        h1, h2 = A[8:11].astype(np.float64), B[8:11].astype(np.float64)
+        sep = _sat(c1, R1, h1, c2, R2, h2)
+        out = oracle.collide(A, B, margin)
+        if sep > margin + 1e-4:
+            assert len(out) == 0, (sep, out)
+        elif sep < margin - 1e-4:
+            assert len(out) >= 1, sep
+        checked += 1
+        for p in out:
+            pt, n, s = p[0:3].astype(np.float64), p[3:6].astype(np.float64), float(p[6])
+            assert abs(np.linalg.norm(n) - 1.0) < 1e-5
+            assert s < margin
+            # the point is on A's surface shell and within |sep| of B
+            assert abs(_box_dist(pt, c1, R1, h1)) < 2e-3 + abs(s), (_box_dist(pt, c1, R1, h1), s)
+            assert _box_dist(pt, c2, R2, h2) < abs(s) + 2e-3
+            contacts += 1
+    assert checked == 3000 and contacts > 500
+
+
+def test_box_resting_on_box_four_corners():
+    table = _shape(BOX, (0.5, 0.0, 0.2), (0, 0, 0, 1), (0.3, 0.5, 0.2))
+    for yaw in (0.0, 0.3, -1.1):
+        cube = _shape(BOX, (0.45, 0.1, 0.4 + 0.0225), _quat((0, 0, 1), yaw), (0.0225, 0.0225, 0.0225))
+        out = oracle.collide(cube, table, 0.001)
+        assert len(out) == 4
+        assert np.allclose(out[:, 3:6], [0, 0, 1], atol=1e-6)        # from the table towards the cube
+        assert np.allclose(out[:, 6], 0.0, atol=1e-6)
+        assert np.allclose(out[:, 2], 0.4, atol=1e-6)                # bottom face of the cube
+        # the four bottom corners of the cube
+        R = _rot(cube[4:8].astype(np.float64))
+        corners = np.array(sorted([tuple((cube[1:4] + R @ np.array([sx, sy, -1]) * 0.0225)[:2])
+                                   for sx in (-1, 1) for sy in (-1, 1)]))
+        got = np.array(sorted([tuple(p[:2].astype(np.float64)) for p in out]))
+        assert np.allclose(got, corners, atol=1e-5)
+
+
+def test_sphere_above_box_face():
+    box = _shape(BOX, (0, 0, 0), (0, 0, 0, 1), (1, 1, 1))
+    sph = _shape(SPHERE, (0.2, -0.3, 1.5), (0, 0, 0, 1), (0.49, 0, 0))
+    out = oracle.collide(sph, box, 0.02)
+    assert len(out) == 1
+    assert np.allclose(out[0, 3:6], [0, 0, 1])
+    assert abs(out[0, 6] - 0.01) < 1e-6
+    assert np.allclose(out[0, 0:3], [0.2, -0.3, 1.01], atol=1e-6)
+    assert len(oracle.collide(sph, box, 0.005)) == 0
+    # box as A: same contact seen from the other side
+    out2 = oracle.collide(box, sph, 0.02)
+    assert len(out2) == 1 and np.allclose(out2[0, 3:6], [0, 0, -1]) and abs(out2[0, 6] - 0.01) < 1e-6
+
+
+def test_edge_edge_crossing():
+    # two long thin boxes crossing at right angles, edges overlapping by 1 mm
+    a = _shape(BOX, (0, 0, 0), _quat((1, 0, 0), math.pi / 4), (1.0, 0.1, 0.1))
+    b = _shape(BOX, (0, 0, 2 * 0.1 * math.sqrt(2) - 0.001), _quat((0, 1, 0), math.pi / 4), (0.1, 1.0, 0.1))
+    out = oracle.collide(a, b, 0.01)
+    assert len(out) == 1
+    n = out[0, 3:6]
+    assert abs(abs(n[2]) - 1.0) < 1e-4 and n[2] < 0       # pushes a down, away from b
+    assert abs(out[0, 6] + 0.001) < 1e-4
+
+
+def test_capsule_as_two_spheres():
+    cap = _shape(CAPSULE, (0, 0, 0.05), (0, 0, 0, 1), (0.05, 0.2, 0))
+    box = _shape(BOX, (0, 0, -0.5), (0, 0, 0, 1), (1, 1, 0.5))
+    out = oracle.collide(cap, box, 0.01)
+    assert len(out) == 2
+    assert np.allclose(out[:, 6], 0.0, atol=1e-6)
+    assert np.allclose(sorted(out[:, 0]), [-0.2, 0.2], atol=1e-6)

@@ -131,3 +131,49 @@ def test_franka_jacobian_mass_matrix_float64(gym):
         Mr = art.mass_matrix(base, q[e].astype(np.float64), fb)
         assert np.allclose(J[e], Jr, rtol=1e-4, atol=1e-5), np.abs(J[e] - Jr).max()
         assert np.allclose(M[e], Mr, rtol=1e-4, atol=1e-5), np.abs(M[e] - Mr).max()
+
+
+def test_box_stacks_parity_bitexact(gym):
+    """Coupled envs without an articulation (the no-articulation launch group):
+    per env a fixed table, a cube on it and a second cube dropped onto the
+    first with a random spin (free-static and free-free rows, ground rows);
+    150 frames, GPU == oracle bit for bit after every frame."""
+    n, frames = 96, 150
+    sp = scenes.franka_sim_params(True)
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim, plane)
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    table = gym.create_box(sim, 0.6, 1.0, 0.4, opts)
+    cube = gym.create_box(sim, 0.06, 0.06, 0.06, gymapi.AssetOptions())
+    rng = np.random.RandomState(11)
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 10)
+        gym.create_actor(env, table, gymapi.Transform(gymapi.Vec3(0.5, 0, 0.2)), "table", i, 0)
+        p1 = gymapi.Transform(gymapi.Vec3(0.5 + rng.uniform(-0.1, 0.1), rng.uniform(-0.2, 0.2), 0.43))
+        p1.r = gymapi.Quat.from_axis_angle(gymapi.Vec3(0, 0, 1), rng.uniform(-3, 3))
+        gym.create_actor(env, cube, p1, "c1", i, 0)
+        p2 = gymapi.Transform(gymapi.Vec3(p1.p.x + rng.uniform(-0.02, 0.02), p1.p.y, 0.6))
+        p2.r = gymapi.Quat.from_axis_angle(gymapi.Vec3(rng.normal(), rng.normal(), 1.0), rng.uniform(-1, 1))
+        gym.create_actor(env, cube, p2, "c2", i, 0)
+    gym.prepare_sim(sim)
+    from test_isaacgym_amd import _native as N
+    assert N.lib.mg_num_coupled_envs(sim.native) == n
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    ds = sim.model_arrays["dof_state0"].copy()
+    for f in range(frames):
+        gym.simulate(sim)
+        gym.fetch_results(sim, True)
+        gym.refresh_rigid_body_state_tensor(sim)
+        oracle.step(p, m, st, ds)
+        got = rb.cpu().numpy()
+        if not np.array_equal(got, st):
+            bad = np.argwhere(got != st)
+            pytest.fail("frame %d: first differing body/field %s, max |diff| %g" % (f, bad[:3].tolist(),
+                                                                                 np.abs(got - st).max()))
+    # the dropped cubes end on the first ones or on the table, none below the table top
+    assert np.all(st[2::3, 2] > 0.39)
