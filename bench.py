@@ -105,7 +105,7 @@ def gimbal_rate(n, steps, warmup, dev):
             "algorithmic_bytes_per_env": 532}
 
 
-def franka_rate(n, steps, warmup, dev):
+def franka_rate(n, steps, warmup, dev, use_graph=True):
     """S3 Franka cube pick: examples/franka_cube_ik_osc.py's
     loop at n envs, OSC controller: simulate -> fetch_results -> refresh rigid-body /
     DOF / Jacobian / mass-matrix tensors -> the script's controller on the device
@@ -139,23 +139,50 @@ def franka_rate(n, steps, warmup, dev):
         pa, ea = ctl.step(rb, dp, dv, j_eef, mm7, bi, hi)
         gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(pa))
         gym.set_dof_actuation_force_tensor(sim, gymtorch.unwrap_tensor(ea))
+        lifted.logical_or_(rb[bi, 2] > 0.55)
 
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
+    avg = ctypes.c_float()
+    used = N.lib.mg_step_time_stats(sim.native, min(warmup, 512), ctypes.byref(avg), None, None)
+    t_e = time.perf_counter()
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize(dev)
+    eager_ms = 1e3 * (time.perf_counter() - t_e) / 10
+    graph = None
+    if use_graph:
+        try:
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            graph.replay()
+        except Exception as ex:
+            print("*** bench: S3 hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
+            graph = None
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
-        lifted |= rb[bi, 2] > 0.55
+        if graph is not None:
+            graph.replay()
+        else:
+            step()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    avg = ctypes.c_float()
-    used = N.lib.mg_step_time_stats(sim.native, min(steps, 512), ctypes.byref(avg), None, None)
     out = {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
-           "kernel": "k_env_step<16,12>", "kernel_ms_avg": avg.value if used > 0 else None,
+           "kernel": "k_env_step<16>", "kernel_ms_avg": avg.value if used > 0 else None,
            "coupled_envs": int(N.lib.mg_num_coupled_envs(sim.native)),
            "cubes_lifted_frac": float(lifted.float().mean()),
-           "controller": "OSC (franka_cube_ik_osc.py:59-79,348-410) on the device"}
+           "controller": "OSC (franka_cube_ik_osc.py:59-79,348-410) on the device",
+           "timed_loop": "hipGraph replay" if graph is not None else "eager Python loop",
+           "eager_ms_per_step": eager_ms}
     gym.destroy_sim(sim)
     return out
 
@@ -183,6 +210,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-gimbal", action="store_true", help="skip the secondary S2 servo-arm measurement")
     ap.add_argument("--no-franka", action="store_true", help="skip the secondary S3 Franka cube-pick measurement")
+    ap.add_argument("--eager", action="store_true",
+                    help="time the Python loop itself instead of a hipGraph replay of the step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -217,15 +246,63 @@ def main():
         if gathered:
             sharding.all_gather_rows(root)      # RCCL over xGMI: (world * 2n, 13) observation
 
+    # the same step with the action index on the device, for hipGraph capture
+    kdev = torch.zeros(1, dtype=torch.long, device=dev)     # in [0, acts.shape[0]) at every step
+
+    def step_dev():
+        root[:, 3:10] = acts.index_select(0, kdev).squeeze(0)
+        kdev.add_(1)
+        kdev.remainder_(acts.shape[0])
+        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.simulate(sim)
+        gym.fetch_results(sim, False)
+        gym.refresh_actor_root_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_dof_state_tensor(sim)
+
     gym.refresh_actor_root_state_tensor(sim)
     for k in range(args.warmup):
         step(k)
+    # eager reference timing (the warmup's last half) and the kernel durations
+    torch.cuda.synchronize(dev)
+    t_e = time.perf_counter()
+    neager = max(args.warmup // 2, 1)
+    for k in range(neager):
+        step(args.warmup + k)
+    torch.cuda.synchronize(dev)
+    eager_ms = 1e3 * (time.perf_counter() - t_e) / neager
+    avg = ctypes.c_float()
+    lo = ctypes.c_float()
+    hi = ctypes.c_float()
+    used = N.lib.mg_step_time_stats(sim.native, min(neager, 512), ctypes.byref(avg),
+                                    ctypes.byref(lo), ctypes.byref(hi))
+    graph = None
+    if not args.eager and not gathered:
+        try:
+            kdev.fill_((args.warmup + neager) % acts.shape[0])
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    step_dev()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step_dev()
+            for _ in range(3):
+                graph.replay()
+        except Exception as ex:          # capture unsupported here: time the eager loop
+            print("*** bench: hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
+            graph = None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(args.warmup + k)
+        if graph is not None:
+            graph.replay()
+        else:
+            step(args.warmup + neager + k)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -234,13 +311,10 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    if graph is None:
+        used = N.lib.mg_step_time_stats(sim.native, min(args.steps, 512), ctypes.byref(avg), ctypes.byref(lo),
+                                        ctypes.byref(hi))
 
-    # live kernel timing of the timed region's simulate() launches (HIP events)
-    avg = ctypes.c_float()
-    lo = ctypes.c_float()
-    hi = ctypes.c_float()
-    used = N.lib.mg_step_time_stats(sim.native, min(args.steps, 512), ctypes.byref(avg), ctypes.byref(lo),
-                                    ctypes.byref(hi))
     kern_ms = avg.value if used > 0 else float("nan")
 
     ms_per_step = 1e3 * el / args.steps
@@ -272,6 +346,9 @@ def main():
                 "parallelism": "env-sharded, one process per GPU%s" % (", RCCL all-gather of root state"
                                                                         if gathered else
                                                                         ", no collectives"),
+                "timed_loop": "hipGraph replay of the captured tensor-API step" if graph is not None
+                              else "eager Python loop",
+                "eager_ms_per_step": eager_ms,
             },
             "roofline": {
                 "bound": "hbm",
@@ -285,6 +362,9 @@ def main():
                 "kernel_ms_avg": kern_ms,
                 "kernel_ms_min": lo.value if used > 0 else None,
                 "kernel_launches_timed": int(used),
+                "kernel_timing": "HIP events around each simulate() of the eager %s" % (
+                    "segment after the warmup (graph replays carry no events)" if graph is not None
+                    else "timed loop"),
                 "note": "working set of 4096 envs (~2.8 MB) sits in L2/MALL: the step is launch/latency "
                         "bound at this size (SURVEY.md §0.10)",
             },
@@ -292,7 +372,7 @@ def main():
         if world == 1 and not args.no_gimbal:
             out["s2_servo_arm"] = gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev)
         if world == 1 and not args.no_franka:
-            out["s3_franka"] = franka_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev)
+            out["s3_franka"] = franka_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline"]["cores"] = 1

@@ -207,6 +207,11 @@ int32_t     mg_apply_rigid_body_force(mg_sim* sim, const float* force, const flo
  * body algorithm, joint armature not included. Both at the current DOF state. */
 int32_t     mg_refresh_jacobian(mg_sim* sim, int32_t tmpl, float* dst, int32_t dst_host, void* stream);
 int32_t     mg_refresh_mass_matrix(mg_sim* sim, int32_t tmpl, float* dst, int32_t dst_host, void* stream);
+/* Both in one launch (one forward-kinematics pass): refresh_jacobian_tensors
+ * followed by refresh_mass_matrix_tensors at the same state. Either pointer may
+ * be NULL; both are device memory, or both host memory when dst_host. */
+int32_t     mg_refresh_jacobian_mass_matrix(mg_sim* sim, int32_t tmpl, float* jac, float* mm, int32_t dst_host,
+                                            void* stream);
 
 /* ---- introspection for tests and the bench ------------------------------- */
 /* Duration in ms of the last simulate()'s kernels (HIP events on `stream`),

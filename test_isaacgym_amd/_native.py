@@ -106,6 +106,7 @@ def _load():
         "mg_apply_rigid_body_force": (i32, [vp, vp, vp, i32, i32, vp]),
         "mg_refresh_jacobian": (i32, [vp, i32, vp, i32, vp]),
         "mg_refresh_mass_matrix": (i32, [vp, i32, vp, i32, vp]),
+        "mg_refresh_jacobian_mass_matrix": (i32, [vp, i32, vp, vp, i32, vp]),
         "mg_last_step_ms": (ctypes.c_float, [vp]),
         "mg_step_time_stats": (i32, [vp, i32, vp, vp, vp]),
         "mg_num_free_bodies": (i32, [vp]),
@@ -132,7 +133,7 @@ EXPORTED_SYMBOLS = (
     "mg_set_dof_actuation_force", "mg_set_dof_props", "mg_apply_rigid_body_force",
     "mg_refresh_jacobian", "mg_refresh_mass_matrix", "mg_last_step_ms", "mg_step_time_stats", "mg_num_free_bodies",
     "mg_num_articulations",
-    "mg_num_coupled_envs",
+    "mg_num_coupled_envs", "mg_refresh_jacobian_mass_matrix",
 )
 
 

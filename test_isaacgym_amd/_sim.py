@@ -138,6 +138,10 @@ class Sim:
         self.tensors = {}
         self.jacobians = {}
         self.mass_matrices = {}
+        # state epoch: bumped by simulate and every state setter; the mass matrix
+        # computed alongside the Jacobian is reused while the epoch is unchanged
+        self.epoch = 0
+        self.mm_cache = {}
 
     # ------------------------------------------------------------ params
     def mg_params(self):

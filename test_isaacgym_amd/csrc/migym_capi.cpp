@@ -115,6 +115,7 @@ struct mg_sim {
 
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
     bool stepped = false;
+    bool capturing = false;       // the last simulate was recorded into a graph
     // ring of per-simulate event pairs for live kernel timing (bench.py roofline)
     static constexpr int kRing = 512;
     hipEvent_t ring_b[kRing] = {}, ring_e[kRing] = {};
@@ -358,6 +359,9 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                 for (int t : stc) coupled = coupled || collide(a, t);
                 for (int f : fr) coupled = coupled || collide(a, f);
             }
+#ifdef MG_COUPLE_ARTICULATIONS
+            coupled = coupled || !art.empty();
+#endif
             if (!coupled) continue;
             if (art.size() > 1 || fr.size() > MG_ENV_MAXF || stc.size() > MG_ENV_MAXS)
                 return fail(MG_ERR_UNSUPPORTED,
@@ -641,10 +645,18 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
     const MgStep P = make_step(s->params);
-    const int slot = (int)(s->ring_n % mg_sim::kRing);
-    s->ev_begin = s->ring_b[slot];
-    s->ev_end = s->ring_e[slot];
-    HIP_TRY(hipEventRecord(s->ev_begin, st));
+    // Under HIP stream capture (a hipGraph of the tensor-API step) the launches
+    // are recorded as graph nodes; the timing events are left out (they would
+    // become fixed nodes of the graph) and fetch_results does not block.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(st, &cap));
+    s->capturing = cap != hipStreamCaptureStatusNone;
+    if (!s->capturing) {
+        const int slot = (int)(s->ring_n % mg_sim::kRing);
+        s->ev_begin = s->ring_b[slot];
+        s->ev_end = s->ring_e[slot];
+        HIP_TRY(hipEventRecord(s->ev_begin, st));
+    }
     for (const ArticGroup& g : s->groups) {
         if (g.step_count == 0) continue;
         MgArticArgs A{};
@@ -694,15 +706,17 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         HIP_TRY(hipMemsetAsync(s->d_ext, 0, (size_t)s->nb * 6 * sizeof(float), st));
         s->ext_pending = false;
     }
-    HIP_TRY(hipEventRecord(s->ev_end, st));
-    s->ring_n++;
-    s->stepped = true;
+    if (!s->capturing) {
+        HIP_TRY(hipEventRecord(s->ev_end, st));
+        s->ring_n++;
+        s->stepped = true;
+    }
     return MG_OK;
 }
 
 int32_t mg_fetch_results(mg_sim* s, int32_t wait) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
-    if (wait && s->stepped) HIP_TRY(hipEventSynchronize(s->ev_end));
+    if (wait && s->stepped && !s->capturing) HIP_TRY(hipEventSynchronize(s->ev_end));
     return MG_OK;
 }
 
@@ -839,9 +853,9 @@ int32_t mg_apply_rigid_body_force(mg_sim* s, const float* force, const float* to
     return MG_OK;
 }
 
-static int refresh_jac_mm(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_host, void* stream, bool jac) {
+static int refresh_jac_mm(mg_sim* s, int32_t tmpl, float* jdst, float* mdst, int32_t dst_host, void* stream) {
     if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
-    if (!dst) return fail(MG_ERR_ARG, "null destination");
+    if (!jdst && !mdst) return fail(MG_ERR_ARG, "null destination");
     const ArticGroup* g = nullptr;
     for (const ArticGroup& x : s->groups)
         if (x.tmpl == tmpl) g = &x;
@@ -849,13 +863,15 @@ static int refresh_jac_mm(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_host,
     if (!g->fixed_base) return fail(MG_ERR_UNSUPPORTED, "jacobian / mass matrix of floating-base articulations");
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
-    const size_t per = jac ? (size_t)(g->nl - 1) * 6 * g->ndof : (size_t)g->ndof * g->ndof;
-    const size_t total = per * g->count;
-    float* out = dst;
+    const size_t jper = (size_t)(g->nl - 1) * 6 * g->ndof, mper = (size_t)g->ndof * g->ndof;
+    const size_t jtot = jdst ? jper * g->count : 0, mtot = mdst ? mper * g->count : 0;
+    float* jout = jdst;
+    float* mout = mdst;
     if (dst_host) {
-        int rc = ensure_stage(s, total, 0);
+        int rc = ensure_stage(s, jtot + mtot, 0);
         if (rc) return rc;
-        out = s->d_stage;
+        jout = jdst ? s->d_stage : nullptr;
+        mout = mdst ? s->d_stage + jtot : nullptr;
     }
     MgArticArgs A{};
     A.na = g->count; A.nb = s->nb; A.nd = s->nd;
@@ -865,20 +881,27 @@ static int refresh_jac_mm(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_host,
     A.link_i = s->d_link_i + (size_t)g->first_link * MG_LINK_I_N;
     A.state = s->d_state; A.mass = s->d_mass;
     A.dof_pos = s->d_dof; A.dof_vel = s->d_dof + s->nd;
-    if (total > 0 && !jac) HIP_TRY(hipMemsetAsync(out, 0, total * sizeof(float), st));
-    HIP_TRY(mg_launch_jacobian(A, jac ? out : nullptr, jac ? nullptr : out, st));
+    if (mtot > 0) HIP_TRY(hipMemsetAsync(mout, 0, mtot * sizeof(float), st));
+    HIP_TRY(mg_launch_jacobian(A, jout, mout, st));
     if (dst_host) {
-        HIP_TRY(hipMemcpyAsync(dst, out, total * sizeof(float), hipMemcpyDeviceToHost, st));
+        if (jtot) HIP_TRY(hipMemcpyAsync(jdst, jout, jtot * sizeof(float), hipMemcpyDeviceToHost, st));
+        if (mtot) HIP_TRY(hipMemcpyAsync(mdst, mout, mtot * sizeof(float), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
     return MG_OK;
 }
 
 int32_t mg_refresh_jacobian(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_host, void* stream) {
-    return refresh_jac_mm(s, tmpl, dst, dst_host, stream, true);
+    if (!dst) return fail(MG_ERR_ARG, "null destination");
+    return refresh_jac_mm(s, tmpl, dst, nullptr, dst_host, stream);
 }
 int32_t mg_refresh_mass_matrix(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_host, void* stream) {
-    return refresh_jac_mm(s, tmpl, dst, dst_host, stream, false);
+    if (!dst) return fail(MG_ERR_ARG, "null destination");
+    return refresh_jac_mm(s, tmpl, nullptr, dst, dst_host, stream);
+}
+int32_t mg_refresh_jacobian_mass_matrix(mg_sim* s, int32_t tmpl, float* jac, float* mm, int32_t dst_host,
+                                        void* stream) {
+    return refresh_jac_mm(s, tmpl, jac, mm, dst_host, stream);
 }
 
 }  // extern "C"

@@ -16,6 +16,19 @@ import torch
 from .torch_utils import quat_conjugate, quat_mul, quat_rotate
 
 
+def _inv(a):
+    """torch.inverse without the host-side singularity check (linalg.inv_ex), so
+    the controller can be captured into a hipGraph; same values."""
+    return torch.linalg.inv_ex(a)[0]
+
+
+def _bmm(a, b):
+    """Batched product of tiny matrices, (n, i, k) x (n, k, j), as one broadcast
+    multiply and a reduction: rocBLAS batched GEMM tiles cost ~58 us per call at
+    4096 x 7x7 on MI355X, this ~5 us."""
+    return (a.unsqueeze(-1) * b.unsqueeze(-3)).sum(-2)
+
+
 def quat_axis(q, axis=0):
     """franka_cube_ik_osc.py:28-31."""
     basis = torch.zeros(q.shape[0], 3, device=q.device, dtype=q.dtype)
@@ -77,19 +90,19 @@ class CubePick:
         """franka_cube_ik_osc.py:51-56."""
         j_t = torch.transpose(j_eef, 1, 2)
         lmbda = torch.eye(6, device=j_eef.device) * (self.damping ** 2)
-        return (j_t @ torch.inverse(j_eef @ j_t + lmbda) @ dpose).view(self.n, 7)
+        return _bmm(_bmm(j_t, _inv(_bmm(j_eef, j_t) + lmbda)), dpose).view(self.n, 7)
 
     def control_osc(self, j_eef, mm, dpose, hand_vel, dof_pos, dof_vel):
         """franka_cube_ik_osc.py:59-79."""
-        mm_inv = torch.inverse(mm)
+        mm_inv = _inv(mm)
         j_t = torch.transpose(j_eef, 1, 2)
-        m_eef = torch.inverse(j_eef @ mm_inv @ j_t)
-        u = j_t @ m_eef @ (self.kp * dpose - self.kd * hand_vel.unsqueeze(-1))
-        j_eef_inv = m_eef @ j_eef @ mm_inv
+        m_eef = _inv(_bmm(_bmm(j_eef, mm_inv), j_t))
+        u = _bmm(_bmm(j_t, m_eef), self.kp * dpose - self.kd * hand_vel.unsqueeze(-1))
+        j_eef_inv = _bmm(_bmm(m_eef, j_eef), mm_inv)
         u_null = self.kd_null * -dof_vel + self.kp_null * (
             (self.default_dof_pos.view(1, -1, 1) - dof_pos + np.pi) % (2 * np.pi) - np.pi)
-        u_null = mm @ u_null[:, :7]
-        u = u + (self.eye7 - j_t @ j_eef_inv) @ u_null
+        u_null = _bmm(mm, u_null[:, :7])
+        u = u + _bmm(self.eye7 - _bmm(j_t, j_eef_inv), u_null)
         return u.squeeze(-1)
 
     def step(self, rb_states, dof_pos, dof_vel, j_eef, mm, box_idxs, hand_idxs):
@@ -105,7 +118,7 @@ class CubePick:
         to_box = box_pos - hand_pos
         box_dist = torch.norm(to_box, dim=-1).unsqueeze(-1)
         box_dir = to_box / box_dist
-        box_dot = box_dir @ self.down_dir.view(3, 1)
+        box_dot = (box_dir * self.down_dir).sum(-1, keepdim=True)
         grasp_offset = 0.11 if self.controller == "ik" else 0.10
 
         gripper_sep = dof_pos[:, 7] + dof_pos[:, 8]
@@ -114,11 +127,12 @@ class CubePick:
         yaw_q = cube_grasping_yaw(box_rot, self.corners)
         box_yaw_dir = quat_axis(yaw_q, 0)
         hand_yaw_dir = quat_axis(hand_rot, 0)
-        yaw_dot = torch.bmm(box_yaw_dir.view(self.n, 1, 3), hand_yaw_dir.view(self.n, 3, 1)).squeeze(-1)
+        yaw_dot = (box_yaw_dir * hand_yaw_dir).sum(-1, keepdim=True)
 
         to_init = self.init_pos - hand_pos
         init_dist = torch.norm(to_init, dim=-1)
-        self.hand_restart = (self.hand_restart & (init_dist > 0.02)).squeeze(-1)
+        # in-place state updates: the step can be captured into a hipGraph and replayed
+        self.hand_restart.copy_(self.hand_restart & (init_dist > 0.02))
         return_to_start = (self.hand_restart | gripped.squeeze(-1)).unsqueeze(-1)
 
         above_box = ((box_dot >= 0.99) & (yaw_dot >= 0.95) & (box_dist < grasp_offset * 3)).squeeze(-1)
@@ -138,7 +152,7 @@ class CubePick:
             self.effort_action[:, :7] = self.control_osc(j_eef, mm, dpose, hand_vel, dof_pos, dof_vel)
 
         close_gripper = (box_dist < grasp_offset + 0.02) | gripped
-        self.hand_restart = self.hand_restart | (box_pos[:, 2] > 0.6)
+        self.hand_restart.copy_(self.hand_restart | (box_pos[:, 2] > 0.6))
         keep_going = torch.logical_not(self.hand_restart)
         close_gripper = close_gripper & keep_going.unsqueeze(-1)
         self.pos_action[:, 7:9] = torch.where(close_gripper, self.grip_closed, self.grip_open)

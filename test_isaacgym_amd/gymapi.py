@@ -105,6 +105,7 @@ class Gym:
         """One frame (test10_servo_vecenv.py:380): the fused HIP step kernels."""
         h = sim.require_native("gym.simulate")
         N.check(N.lib.mg_simulate(h, sim.stream()), "mg_simulate")
+        sim.epoch += 1
         sim.frame += 1
         sim.time += sim.params.dt
 
@@ -501,6 +502,7 @@ class Gym:
             full = np.zeros((sim.num_dofs, 2), dtype=np.float32)
             full[a.global_dof:a.global_dof + a.num_dofs] = a.dof_state
             idx = np.array([a.global_index], dtype=np.int32)
+            sim.epoch += 1
             N.check(N.lib.mg_set_dof_state(sim.native, full.ctypes.data, 1, idx.ctypes.data, 1, sim.stream()),
                     "mg_set_dof_state")
         return True
@@ -560,6 +562,7 @@ class Gym:
             for a, row in actors_rows:
                 A["body_state0"][a.global_body] = row
             return True
+        sim.epoch += 1
         N.check(N.lib.mg_set_actor_root_state(sim.native, full.ctypes.data, 1, idx.ctypes.data, len(idx),
                                               sim.stream()), "mg_set_actor_root_state")
         return True
@@ -720,6 +723,7 @@ class Gym:
 
     def _set(self, sim, tensor, fn, ncols, nrows, what, index=None, count=None):
         sim.finalize()
+        sim.epoch += 1
         t = _as_tensor_arg(tensor, what)
         if t.dtype != torch.float32 or t.numel() != nrows * ncols:
             print("*** migym: %s: expected a float32 tensor of %d x %d" % (what, nrows, ncols), file=sys.stderr)
@@ -759,6 +763,7 @@ class Gym:
         if t.numel() != sim.num_bodies * 13:
             return False
         h = sim.require_native("set_rigid_body_state_tensor")
+        sim.epoch += 1
         rc = N.lib.mg_set_rigid_body_state(h, t.data_ptr(), 1 if t.device.type == "cpu" else 0, sim.stream())
         return rc == N.MG_OK
 
@@ -846,15 +851,33 @@ class Gym:
         return Tensor(sim.mass_matrices[actor_name][1])
 
     def refresh_jacobian_tensors(self, sim):
+        """examples/franka_cube_ik_osc.py:345. When the actor's mass-matrix tensor is
+        acquired too, one launch also computes it (same kinematics) into a cache that
+        refresh_mass_matrix_tensors copies from while the state is unchanged."""
         h = sim.require_native("refresh_jacobian_tensors")
         for name, (t, ten) in sim.jacobians.items():
-            N.check(N.lib.mg_refresh_jacobian(h, t, ten.data_ptr(), 1 if ten.device.type == "cpu" else 0,
-                                              sim.stream()), "refresh_jacobian_tensors(%s)" % name)
+            host = 1 if ten.device.type == "cpu" else 0
+            if name in sim.mass_matrices:
+                mm = sim.mass_matrices[name][1]
+                cache = sim.mm_cache.get(name)
+                if cache is None or cache[1].shape != mm.shape or cache[1].device != mm.device:
+                    cache = (None, torch.empty_like(mm))
+                N.check(N.lib.mg_refresh_jacobian_mass_matrix(h, t, ten.data_ptr(), cache[1].data_ptr(), host,
+                                                              sim.stream()), "refresh_jacobian_tensors(%s)" % name)
+                sim.mm_cache[name] = (sim.epoch, cache[1])
+            else:
+                N.check(N.lib.mg_refresh_jacobian(h, t, ten.data_ptr(), host, sim.stream()),
+                        "refresh_jacobian_tensors(%s)" % name)
         return True
 
     def refresh_mass_matrix_tensors(self, sim):
+        """examples/franka_cube_ik_osc.py:346."""
         h = sim.require_native("refresh_mass_matrix_tensors")
         for name, (t, ten) in sim.mass_matrices.items():
+            cache = sim.mm_cache.get(name)
+            if cache is not None and cache[0] == sim.epoch:
+                ten.copy_(cache[1])
+                continue
             N.check(N.lib.mg_refresh_mass_matrix(h, t, ten.data_ptr(), 1 if ten.device.type == "cpu" else 0,
                                                  sim.stream()), "refresh_mass_matrix_tensors(%s)" % name)
         return True

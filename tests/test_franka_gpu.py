@@ -177,3 +177,44 @@ def test_box_stacks_parity_bitexact(gym):
                                                                                  np.abs(got - st).max()))
     # the dropped cubes end on the first ones or on the table, none below the table top
     assert np.all(st[2::3, 2] > 0.39)
+
+
+def test_franka_loop_hipgraph_matches_eager(gym):
+    """The whole S3 frame (simulate, refreshes incl. Jacobian / mass matrix, the
+    torch OSC controller, DOF target / effort setters) captured into a hipGraph
+    and replayed gives the same states as the eager loop, bit for bit."""
+    n, steps = 64, 40
+    outs = []
+    for mode in ("eager", "graph"):
+        sim, info, rb, dof, jac, mm, ctl = _setup(gym, n)
+        h = info["hand_index"]
+        bi = torch.tensor(info["box_idxs"], device=DEV)
+        hi = torch.tensor(info["hand_idxs"], device=DEV)
+        j_eef, mm7 = jac[:, h - 1, :, :7], mm[:, :7, :7]
+        dp, dv = dof[:, 0].view(n, 9, 1), dof[:, 1].view(n, 9, 1)
+
+        def frame():
+            gym.simulate(sim)
+            gym.fetch_results(sim, True)
+            gym.refresh_rigid_body_state_tensor(sim)
+            gym.refresh_dof_state_tensor(sim)
+            gym.refresh_jacobian_tensors(sim)
+            gym.refresh_mass_matrix_tensors(sim)
+            pa, ea = ctl.step(rb, dp, dv, j_eef, mm7, bi, hi)
+            gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(pa))
+            gym.set_dof_actuation_force_tensor(sim, gymtorch.unwrap_tensor(ea))
+
+        if mode == "eager":
+            for _ in range(steps):
+                frame()
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                frame()
+            for _ in range(steps):
+                g.replay()
+        torch.cuda.synchronize()
+        outs.append((rb.cpu().numpy().copy(), dof.cpu().numpy().copy()))
+        gym.destroy_sim(sim)
+    assert np.array_equal(outs[0][0], outs[1][0]), np.abs(outs[0][0] - outs[1][0]).max()
+    assert np.array_equal(outs[0][1], outs[1][1])

@@ -1,0 +1,36 @@
+"""Kernel microbenchmark of the S2 gimbal step: 4096 gimbals
+under random PD position targets; average simulate() kernel time (HIP events).
+Library from MIGYM_LIB (default in-tree)."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from isaacgym import gymapi, gymtorch  # noqa: E402
+from test_isaacgym_amd import _native as N, scenes  # noqa: E402
+
+
+def run(n, steps=200, warm=20):
+    gym = gymapi.acquire_gym()
+    sim, _ = scenes.gimbal_scene(gym, n)
+    gym.prepare_sim(sim)
+    tg = scenes.gimbal_targets(n, 64, "cuda:0", seed=0)
+    for k in range(warm + steps):
+        gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[k % 64]))
+        gym.simulate(sim)
+    torch.cuda.synchronize()
+    avg, lo = ctypes.c_float(), ctypes.c_float()
+    used = N.lib.mg_step_time_stats(sim.native, steps, ctypes.byref(avg), ctypes.byref(lo), None)
+    out = {"lib": os.path.basename(N.LIB_PATH), "envs": n, "kernel_us_avg": 1e3 * avg.value,
+           "kernel_us_min": 1e3 * lo.value, "coupled_envs": int(N.lib.mg_num_coupled_envs(sim.native))}
+    gym.destroy_sim(sim)
+    return out
+
+
+if __name__ == "__main__":
+    for n in [int(x) for x in (sys.argv[1:] or ["4096"])]:
+        print(json.dumps(run(n)), flush=True)
