@@ -134,7 +134,7 @@ static void box_box_(const cshape_t* A, const cshape_t* B, float margin, pair_t*
         const int fa = refA ? face : face - 3;
         v3_t nref = mcol_(Rf->R, fa), iax, ifc, eu, ev, U, W, rc, inrm, nn;
         int ik = 0, iu, iv, ru, rv, m, c;
-        float bestd = 1e30f, hik, hu, hv, qx[4], qy[4], cx[24], cy[24], cdep[24], den;
+        float bestd = 1e30f, hik, hu, hv, qx[4], qy[4], cx[24], cy[24], cdep[24], den, iden;
         unsigned cvalid = 0u, used = 0u;
         if (dot3(sub3(In->c, Rf->c), nref) < 0.0f) nref = mul3(nref, -1.0f);
         for (k = 0; k < 3; ++k) {
@@ -194,9 +194,10 @@ static void box_box_(const cshape_t* A, const cshape_t* B, float margin, pair_t*
         }
         inrm = mul3(iax, dot3(nref, iax) > 0.0f ? -1.0f : 1.0f);
         den = dot3(inrm, nref);
+        iden = fabsf(den) > 1e-6f ? 1.0f / den : 0.0f;
         for (c = 0; c < 24; ++c) {
             const v3_t qq = add3(add3(rc, mul3(U, cx[c])), mul3(W, cy[c]));
-            cdep[c] = fabsf(den) > 1e-6f ? dot3(sub3(ifc, qq), inrm) / den : 0.0f;
+            cdep[c] = dot3(sub3(ifc, qq), inrm) * iden;
         }
         nn = refA ? mul3(nref, -1.0f) : nref;
         for (m = 0; m < OE_PMAX; ++m) {
@@ -821,7 +822,8 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 if (link_rows) {
                     for (ln = 0; ln < D; ++ln) {
                         float w = 0.0f;
-                        for (k = 0; k < D; ++k) w = w + Mi[ln][k] * J[k];
+                        /* column ln of M_eff^-1 (the solve lane ln ran), entry k */
+                        for (k = 0; k < D; ++k) w = w + Mi[k][ln] * J[k];
                         W[ln] = w;
                     }
                 }

@@ -238,11 +238,12 @@ MG_HD void box_box(const CShape& A, const CShape& B, float margin, PairOut& o) {
     // depth of each candidate below the reference face (along nref, to the incident plane)
     const V3 inrm = vscale(iax, vdot(nref, iax) > 0.0f ? -1.0f : 1.0f);
     const float den = vdot(inrm, nref);
+    const float iden = fabsf(den) > 1e-6f ? 1.0f / den : 0.0f;
     float cdep[24];
 #pragma unroll
     for (int c = 0; c < 24; ++c) {
         const V3 q = vadd(vadd(rc, vscale(U, cx[c])), vscale(W, cy[c]));
-        cdep[c] = fabsf(den) > 1e-6f ? vdot(vsub(ifc, q), inrm) / den : 0.0f;
+        cdep[c] = vdot(vsub(ifc, q), inrm) * iden;
     }
     const V3 n = refA ? vscale(nref, -1.0f) : nref;    // from B towards A
     unsigned used = 0u;

@@ -55,6 +55,7 @@ constexpr int MAXF = MG_ENV_MAXF;
 constexpr int F0 = MG_ENV_FREE0;
 constexpr int ST0 = MG_ENV_STATIC0;
 constexpr int LIM0 = MG_ENV_LIMIT0;
+constexpr int NPB = 64;               // candidate pairs per screening block
 
 struct EnvLds {
     float q[G], u[G], qdd[G], dpos[G], mdiag[G];
@@ -67,9 +68,7 @@ struct EnvLds {
     Q4 fq[MAXF];
     float finvm[MAXF];
     S3 fIw[MAXF];
-    float Lc[G][G];                  // Cholesky factor of M_eff (lower)
-    float Mi[G][G];                  // M_eff^-1
-    float invd[G];
+    float Lc[G][G];                  // M_eff, assembled by the DOF lanes
     int ca[MAXCT], cb[MAXCT];
     V3 cp[MAXCT], cd[MAXCT][3];      // point, (n, t1, t2)
     float cs0[MAXCT], cmu[MAXCT], ce[MAXCT], cvn0[MAXCT];
@@ -85,7 +84,10 @@ struct EnvLds {
     float Dd[MG_MAX_LINKS], uu[MG_MAX_LINKS];
     Q4 qr[MG_MAX_LINKS];             // joint rotation / offset relative to the parent
     V3 rr[MG_MAX_LINKS];
-    float tau0[G], imp[G];
+    float tau0[G], imp[G], arm[G];
+    int npl[NPB];                    // candidate pairs that passed the screen
+    V3 sx[MG_ENV_MAXS];              // static bodies: pose (they do not move in the step)
+    Q4 sq[MG_ENV_MAXS];
 };
 
 // sum over the 16 lanes of a DPP row, the same value in every lane:
@@ -100,6 +102,40 @@ __device__ __forceinline__ float red16(float v) {
     v = v + dpp<0x4E>(v);    // quad_perm [2,3,0,1]
     v = v + dpp<0xB1>(v);    // quad_perm [1,0,3,2]
     return v;
+}
+// lane k of the 16-lane row, to every lane of the row (DPP row_newbcast:k,
+// a VALU operand modifier on gfx950: no LDS round trip). k must fold to a
+// constant (fully unrolled loops).
+__device__ __forceinline__ float bcast16(float v, int k) {
+    switch (k) {
+    case 0: return dpp<0x150>(v);  case 1: return dpp<0x151>(v);
+    case 2: return dpp<0x152>(v);  case 3: return dpp<0x153>(v);
+    case 4: return dpp<0x154>(v);  case 5: return dpp<0x155>(v);
+    case 6: return dpp<0x156>(v);  case 7: return dpp<0x157>(v);
+    case 8: return dpp<0x158>(v);  case 9: return dpp<0x159>(v);
+    case 10: return dpp<0x15A>(v); case 11: return dpp<0x15B>(v);
+    case 12: return dpp<0x15C>(v); case 13: return dpp<0x15D>(v);
+    case 14: return dpp<0x15E>(v); default: return dpp<0x15F>(v);
+    }
+}
+
+// substep-invariant per-lane constants: lane l < L holds link l's mass
+// properties, lane d < D holds DOF d's drive properties and targets
+struct LinkC {
+    float m, Idx, Idy, Idz;
+    V3 com;
+    Q4 iq;
+};
+struct DofC {
+    int mode, haslim;
+    float kp, kd, eff, maxv, lo, hi, arm, tpos, tvel, force;
+};
+
+// pose of a pair participant: link l (< F0), free body F0 + k, static body ST0 + s
+__device__ __forceinline__ void pair_pose(const EnvLds& S, int id, V3& x, Q4& q) {
+    if (id >= ST0) { x = S.sx[id - ST0]; q = S.sq[id - ST0]; }
+    else if (id >= F0) { x = S.fx[id - F0]; q = S.fq[id - F0]; }
+    else { x = S.xl[id]; q = S.ql[id]; }
 }
 
 MG_HD void env_tangents(V3 n, V3* t1, V3* t2) {
@@ -175,13 +211,23 @@ MG_HD void put6(float* a, SV s) { a[0] = s.w.x; a[1] = s.w.y; a[2] = s.w.z; a[3]
 // world-frame spatial inertia of link body b about the point O: row-major 6x6
 // [A B; B^T C] with A = Ic + m (|c|^2 1 - c c^T), B = [m c]x, C = m 1
 // (c = COM - O, Ic the rotational inertia about the COM in world axes)
-MG_HD void world_inertia(const float* Ms, int nb, int b, Q4 ql, V3 xl, V3 O, float* I) {
-    const float m = Ms[11 * nb + b];
-    const V3 com = v3(Ms[8 * nb + b], Ms[9 * nb + b], Ms[10 * nb + b]);
-    const Q4 iq = q4(Ms[4 * nb + b], Ms[5 * nb + b], Ms[6 * nb + b], Ms[7 * nb + b]);
-    const V3 invI = v3(Ms[1 * nb + b], Ms[2 * nb + b], Ms[3 * nb + b]);
-    const V3 Id = v3(invI.x > 0.0f ? 1.0f / invI.x : 0.0f, invI.y > 0.0f ? 1.0f / invI.y : 0.0f,
-                     invI.z > 0.0f ? 1.0f / invI.z : 0.0f);
+__device__ LinkC load_link(const float* Ms, int nb, int b) {
+    LinkC k;
+    k.m = Ms[11 * nb + b];
+    k.com = v3(Ms[8 * nb + b], Ms[9 * nb + b], Ms[10 * nb + b]);
+    k.iq = q4(Ms[4 * nb + b], Ms[5 * nb + b], Ms[6 * nb + b], Ms[7 * nb + b]);
+    const float ix = Ms[1 * nb + b], iy = Ms[2 * nb + b], iz = Ms[3 * nb + b];
+    k.Idx = ix > 0.0f ? 1.0f / ix : 0.0f;
+    k.Idy = iy > 0.0f ? 1.0f / iy : 0.0f;
+    k.Idz = iz > 0.0f ? 1.0f / iz : 0.0f;
+    return k;
+}
+
+MG_HD void world_inertia(const LinkC& K, Q4 ql, V3 xl, V3 O, float* I) {
+    const float m = K.m;
+    const V3 com = K.com;
+    const Q4 iq = K.iq;
+    const V3 Id = v3(K.Idx, K.Idy, K.Idz);
     const S3 Ic = sym_rdrt(qmat(qmul(ql, iq)), Id);
     const V3 c = vsub(vadd(xl, qrot(ql, com)), O);
     const float cc2 = vdot(c, c);
@@ -208,11 +254,36 @@ MG_HD void world_inertia(const float* Ms, int nb, int b, Q4 ql, V3 xl, V3 O, flo
 // Implicit drives (h kd + h^2 kp added to D); a drive whose implicit force
 // exceeds its effort limit is re-solved at the limit (xmask / xpos).
 template <int MAXL>
-__device__ void aba_world(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool act, int ln, int b0, int d0, int LA,
-                          int DA, V3 x0, Q4 q0, V3 gw, unsigned& xmask, unsigned& xpos) {
-    const int nb = A.nb, nd = A.nd;
+__device__ __forceinline__ void aba_world(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0, Q4 q0,
+                          V3 gw, const LinkC& lk, const DofC& dc, bool is_dof, bool xm, bool xp) {
     const float h = P.h;
-    const float* pr = A.dof_props;
+    // ---- drive terms (lane d): implicit PD force and its h-derivative; a DOF
+    // flagged by the effort-limit test (xm) runs at constant +-effort
+    if (act && is_dof) {
+        const float qv = S.q[ln], uv = S.u[ln];
+        float tau = 0.0f, imp = 0.0f;
+        if (dc.mode == MG_DOF_MODE_POS) {
+            tau = dc.kp * (dc.tpos - qv - h * uv) + dc.kd * (dc.tvel - uv);
+            imp = h * dc.kd + h * h * dc.kp;
+        } else if (dc.mode == MG_DOF_MODE_VEL) {
+            tau = dc.kd * (dc.tvel - uv);
+            imp = h * dc.kd;
+        } else if (dc.mode == MG_DOF_MODE_EFFORT) {
+            tau = dc.force;
+        }
+        if (dc.eff > 0.0f) {
+            if (xm) {
+                tau = xp ? dc.eff : -dc.eff;
+                imp = 0.0f;
+            } else if (imp == 0.0f) {
+                tau = fminf(fmaxf(tau, -dc.eff), dc.eff);
+            }
+        }
+        S.tau0[ln] = tau;
+        S.imp[ln] = imp;
+        S.mdiag[ln] = dc.arm + imp;
+        S.arm[ln] = dc.arm;
+    }
     // ---- joint transforms (lane l)
     if (act && ln < LA && ln > 0) {
         const float* lf = A.link_f + ln * MG_LINK_F_N;
@@ -259,7 +330,7 @@ __device__ void aba_world(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool a
             else x = sv(v3(0.0f, 0.0f, 0.0f), z);
         }
         put6(S.xi[ln], x);
-        world_inertia(A.mass, nb, b0 + ln, S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
+        world_inertia(lk, S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
     }
     __syncthreads();
     // ---- velocities (lanes 0..5, one component each)
@@ -292,31 +363,8 @@ __device__ void aba_world(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool a
             if (act && ln < 6) S.Ua[l][ln] = dot6(&S.Iw[l][ln * 6], S.xi[l]);
             __syncthreads();
             if (act) {
-                const int gd = d0 + dof;
-                const int mode = (int)pr[0 * nd + gd];
-                const float kp = pr[1 * nd + gd], kd = pr[2 * nd + gd], eff = pr[3 * nd + gd];
-                const float arm = pr[8 * nd + gd];
-                const float qv = S.q[dof], uv = S.u[dof];
-                float tau = 0.0f, imp = 0.0f;
-                if (mode == MG_DOF_MODE_POS) {
-                    tau = kp * (A.dof_tpos[gd] - qv - h * uv) + kd * (A.dof_tvel[gd] - uv);
-                    imp = h * kd + h * h * kp;
-                } else if (mode == MG_DOF_MODE_VEL) {
-                    tau = kd * (A.dof_tvel[gd] - uv);
-                    imp = h * kd;
-                } else if (mode == MG_DOF_MODE_EFFORT) {
-                    tau = A.dof_force[gd];
-                }
-                if (eff > 0.0f) {
-                    if ((xmask >> dof) & 1u) {
-                        tau = ((xpos >> dof) & 1u) ? eff : -eff;
-                        imp = 0.0f;
-                    } else if (imp == 0.0f) {
-                        tau = fminf(fmaxf(tau, -eff), eff);
-                    }
-                }
-                const float Dv = dot6(S.xi[l], S.Ua[l]) + arm + imp;
-                const float uvv = tau - dot6(S.xi[l], S.pa[l]);
+                const float Dv = dot6(S.xi[l], S.Ua[l]) + S.arm[dof] + S.imp[dof];
+                const float uvv = S.tau0[dof] - dot6(S.xi[l], S.pa[l]);
                 const float invD = 1.0f / Dv;
                 uinvD = uvv * invD;
                 for (int e = ln; e < 36; e += G) {
@@ -326,9 +374,6 @@ __device__ void aba_world(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool a
                 if (ln == 0) {
                     S.Dd[l] = Dv;
                     S.uu[l] = uvv;
-                    S.mdiag[dof] = arm + imp;
-                    S.tau0[dof] = tau;
-                    S.imp[dof] = imp;
                 }
             }
             __syncthreads();
@@ -363,11 +408,15 @@ __device__ void aba_world(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool a
 
 // M_eff = joint-space inertia + S.mdiag from world-frame composite inertias
 // (entrywise subtree sums of the link inertias; M_ij = xi_j . IC_i xi_i for j
-// on the path of i), then Cholesky on lane 0 and the columns of M_eff^-1 on
-// lanes 0..D-1. Called by every lane; `act` selects the envs that work.
-template <int MAXL>
-__device__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int b0, int LA, int DA, V3 x0) {
-    if (act && ln < LA) world_inertia(A.mass, A.nb, b0 + ln, S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
+// on the path of i), then its Cholesky factor and M_eff^-1, both in registers:
+// lane i holds row i of the factor (right-looking, column j broadcast by DPP;
+// every entry sees the same subtractions in the same order as the left-looking
+// loops of the oracle), lane j solves column j of M_eff^-1 into mcol[].
+// Called by every lane; `act` selects the envs that work. ND: static bound on D.
+template <int MAXL, int ND>
+__device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, int DA, V3 x0, const LinkC& lk,
+                           float (&mcol)[ND]) {
+    if (act && ln < LA) world_inertia(lk, S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
     __syncthreads();
     if (act)
         for (int l = LA - 1; l >= 1; --l) {
@@ -395,34 +444,48 @@ __device__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int 
         }
     }
     __syncthreads();
-    if (act && ln == 0) {
-        for (int j = 0; j < DA; ++j) {
-            float s = S.Lc[j][j];
-            for (int k = 0; k < j; ++k) s = s - S.Lc[j][k] * S.Lc[j][k];
-            const float dj = sqrtf(s);
-            S.invd[j] = 1.0f / dj;
-            S.Lc[j][j] = dj;
-            for (int i = j + 1; i < DA; ++i) {
-                float t = S.Lc[i][j];
-                for (int k = 0; k < j; ++k) t = t - S.Lc[i][k] * S.Lc[j][k];
-                S.Lc[i][j] = t * S.invd[j];
-            }
+    // all 64 lanes run the register phases (DPP reads neighbouring lanes);
+    // envs that are not `act` compute on stale data and discard it
+    float a[ND], invd[ND];
+    const int row = ln < DA ? ln : 0;
+#pragma unroll
+    for (int k = 0; k < ND; ++k) a[k] = k < DA ? S.Lc[row][k] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+        if (j < DA) {
+            const float dj = bcast16(sqrtf(a[j]), j);
+            invd[j] = 1.0f / dj;
+            if (ln == j) a[j] = dj;
+            else if (ln > j) a[j] = a[j] * invd[j];
+            const float col = a[j];                          // L[ln][j]
+#pragma unroll
+            for (int k = j + 1; k < ND; ++k)
+                if (k < DA) {
+                    const float lk = bcast16(col, k);        // L[k][j]
+                    if (ln >= k) a[k] = a[k] - col * lk;
+                }
         }
     }
-    __syncthreads();
-    if (act && ln < DA) {
-        for (int i = 0; i < DA; ++i) {
+    // column ln of M_eff^-1: forward then backward substitution, L[i][k] from lane i
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+        if (i < DA) {
             float t = i == ln ? 1.0f : 0.0f;
-            for (int k = 0; k < i; ++k) t = t - S.Lc[i][k] * S.Mi[k][ln];
-            S.Mi[i][ln] = t * S.invd[i];
-        }
-        for (int i = DA - 1; i >= 0; --i) {
-            float t = S.Mi[i][ln];
-            for (int k = i + 1; k < DA; ++k) t = t - S.Lc[k][i] * S.Mi[k][ln];
-            S.Mi[i][ln] = t * S.invd[i];
+#pragma unroll
+            for (int k = 0; k < i; ++k) t = t - bcast16(a[k], i) * mcol[k];
+            mcol[i] = t * invd[i];
         }
     }
-    __syncthreads();
+#pragma unroll
+    for (int i = ND - 1; i >= 0; --i) {
+        if (i < DA) {
+            float t = mcol[i];
+#pragma unroll
+            for (int k = i + 1; k < ND; ++k)
+                if (k < DA) t = t - bcast16(a[i], k) * mcol[k];
+            mcol[i] = t * invd[i];
+        }
+    }
 }
 
 template <int MAXL>
@@ -478,6 +541,11 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             }
             lsum[l] = v3(0.0f, 0.0f, 0.0f);
         }
+        for (int k = 0; k < ei[7]; ++k) {
+            const int b = ei[8 + k];
+            S.sx[k] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
+            S.sq[k] = qnormalize(q4(St[3 * nb + b], St[4 * nb + b], St[5 * nb + b], St[6 * nb + b]));
+        }
         for (int k = 0; k < nfr; ++k) {
             const int b = ei[3 + k];
             S.fx[k] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
@@ -504,14 +572,38 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     }
     // slot registers
     float qv = 0.0f, uv = 0.0f, dp = 0.0f;
+    DofC dc = {};
     if (is_dof) {
-        qv = A.dof_pos[d0 + ln];
-        uv = A.dof_vel[d0 + ln];
+        const int gd = d0 + ln;
+        qv = A.dof_pos[gd];
+        uv = A.dof_vel[gd];
+        dc.mode = (int)pr[0 * nd + gd];
+        dc.kp = pr[1 * nd + gd];
+        dc.kd = pr[2 * nd + gd];
+        dc.eff = pr[3 * nd + gd];
+        dc.maxv = pr[4 * nd + gd];
+        dc.lo = pr[5 * nd + gd];
+        dc.hi = pr[6 * nd + gd];
+        dc.haslim = pr[7 * nd + gd] != 0.0f;
+        dc.arm = pr[8 * nd + gd];
+        dc.tpos = A.dof_tpos[gd];
+        dc.tvel = A.dof_tvel[gd];
+        dc.force = A.dof_force[gd];
     } else if (is_free) {
         const int b = ei[3 + fk];
         uv = St[(7 + fc) * nb + b];
     }
-    float Jr[MAXCT * 3], Wr[MAXCT * 3];
+    LinkC lk = {};
+    if (ln < L) lk = load_link(A.mass, nb, b0 + ln);
+    __syncthreads();
+    // the DOF lane's joint: link, revolute flag
+    const int mylink = is_dof ? S.dlink[ln] : 0;
+    const bool myrev = is_dof && S.drev[ln] != 0;
+    constexpr int ND = MAXL <= 4 ? 4 : G;
+    float mcol[ND];                  // column ln of M_eff^-1 (DOF lanes)
+#pragma unroll
+    for (int k = 0; k < ND; ++k) mcol[k] = 0.0f;
+    float Jr[MAXCT * 3], Wr[MAXCT * 3], lam[MAXCT * 3];
     PH_T0();
     PH_MARK(6);
 
@@ -521,28 +613,21 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         S.u[ln] = uv;
         __syncthreads();
         if (LA > 0) {
-            unsigned xmask = 0u, xpos = 0u;
+            bool xm = false, xp = false;     // this DOF runs at constant +-effort
             bool redo = live && L > 0;
             for (int att = 0; att < 2; ++att) {
                 if (!__any(redo)) break;
-                aba_world<MAXL>(P, A, S, redo, ln, b0, d0, LA, DA, x0, q0, gw, xmask, xpos);
-                // drives whose implicit force exceeds the effort limit (same masks in every lane)
-                bool again = false;
-                if (redo) {
-                    unsigned nm = xmask;
-                    for (int d = 0; d < D; ++d) {
-                        const float eff = pr[3 * nd + d0 + d];
-                        if (eff > 0.0f && S.imp[d] != 0.0f) {
-                            const float actf = S.tau0[d] - S.imp[d] * S.qdd[d];
-                            if (actf > eff) { nm |= 1u << d; xpos |= 1u << d; }
-                            else if (actf < -eff) nm |= 1u << d;
-                        }
-                    }
-                    again = nm != xmask;
-                    xmask = nm;
+                aba_world<MAXL>(P, A, S, redo, ln, LA, x0, q0, gw, lk, dc, is_dof, xm, xp);
+                // drives whose implicit force exceeds the effort limit
+                bool flip = false;
+                if (redo && is_dof && dc.eff > 0.0f && S.imp[ln] != 0.0f) {
+                    const float actf = S.tau0[ln] - S.imp[ln] * S.qdd[ln];
+                    if (actf > dc.eff) { xm = true; xp = true; flip = true; }
+                    else if (actf < -dc.eff) { xm = true; flip = true; }
                 }
+                const unsigned long long fb = __ballot(flip);
+                redo = ((fb >> (gi * G)) & 0xFFFFull) != 0ull;
                 __syncthreads();
-                redo = again;
             }
         }
         if (ln == 0 && live) {
@@ -569,7 +654,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         }
         __syncthreads();
         if (is_dof) {
-            const float maxv = pr[4 * nd + d0 + ln];
+            const float maxv = dc.maxv;
             float w = uv + h * S.qdd[ln];
             if (maxv > 0.0f) w = fminf(fmaxf(w, -maxv), maxv);
             uv = w;
@@ -579,94 +664,104 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         dp = 0.0f;
         PH_MARK(0);
 
-        // ================= 2. narrow phase: one pair per lane per round
+        // ================= 2. narrow phase, per block of NPB candidate pairs:
+        // (a) bounding-sphere screen, one pair per lane, survivors compacted in
+        //     pair order into S.npl (the screen is conservative: a rejected pair
+        //     has no contact within the margin);
+        // (b) the full pair test on the survivors, one per lane per round,
+        //     contacts placed by a 16-lane prefix sum in pair order.
         int base = 0;
 #ifdef MG_ENV_ABLATE_NP
-        for (int rb = 0; rb < 0; rb += G) {
+        for (int blk = 0; blk < 0; blk += NPB) {
 #else
-        for (int rb = 0; __any(rb < npair); rb += G) {
+        for (int blk = 0; __any(blk < npair); blk += NPB) {
 #endif
-            const int pi = rb + ln;
-            PairOut o;
-            o.n = 0;
-            float mu = 0.0f, rest = 0.0f;
-            int pa = 0, pb = -1;
-            if (pi < npair) {
-                const int* pp = A.pairs + (size_t)(pair0 + pi) * 4;
-                pa = pp[0];
-                const int sa = pp[1];
-                pb = pp[2];
-                const int sb = pp[3];
-                const float* sha = A.shapes + sa * MG_SHAPE_STRIDE;
-                V3 xa;
-                Q4 qa;
-                if (pa >= F0) { xa = S.fx[pa - F0]; qa = S.fq[pa - F0]; }
-                else { xa = S.xl[pa]; qa = S.ql[pa]; }
-                // bounding-sphere rejection (conservative: a rejected pair has no
-                // contact within the margin, so the result is unchanged)
-                const V3 cA = vadd(xa, qrot(qa, v3(sha[4], sha[5], sha[6])));
-                const float rA = bound_radius(sha);
-                bool near = true;
-                V3 xb = v3(0.0f, 0.0f, 0.0f);
-                Q4 qbb = q4(0.0f, 0.0f, 0.0f, 1.0f);
-                const float* shb = sha;
-                if (pb < 0) {
-                    near = vdot(v3(P.n[0], P.n[1], P.n[2]), cA) + P.pd - rA < P.contact_offset;
-                } else {
-                    shb = A.shapes + sb * MG_SHAPE_STRIDE;
-                    if (pb >= ST0) {
-                        const int bs = ei[8 + pb - ST0];
-                        xb = v3(St[0 * nb + bs], St[1 * nb + bs], St[2 * nb + bs]);
-                        qbb = qnormalize(q4(St[3 * nb + bs], St[4 * nb + bs], St[5 * nb + bs], St[6 * nb + bs]));
-                    } else if (pb >= F0) {
-                        xb = S.fx[pb - F0];
-                        qbb = S.fq[pb - F0];
+            int nnear = 0;
+#pragma unroll
+            for (int r = 0; r < NPB; r += G) {
+                const int pi = blk + r + ln;
+                bool near = false;
+                if (pi < npair) {
+                    const int* pp = A.pairs + (size_t)(pair0 + pi) * 4;
+                    const int pa = pp[0], sa = pp[1], pb = pp[2], sb = pp[3];
+                    const float* sha = A.shapes + sa * MG_SHAPE_STRIDE;
+                    V3 xa, xb;
+                    Q4 qa, qb;
+                    pair_pose(S, pa, xa, qa);
+                    const V3 cA = vadd(xa, qrot(qa, v3(sha[4], sha[5], sha[6])));
+                    const float rA = bound_radius(sha);
+                    if (pb < 0) {
+                        near = vdot(v3(P.n[0], P.n[1], P.n[2]), cA) + P.pd - rA < P.contact_offset;
                     } else {
-                        xb = S.xl[pb];
-                        qbb = S.ql[pb];
+                        const float* shb = A.shapes + sb * MG_SHAPE_STRIDE;
+                        pair_pose(S, pb, xb, qb);
+                        const V3 d = vsub(vadd(xb, qrot(qb, v3(shb[4], shb[5], shb[6]))), cA);
+                        const float rr = rA + bound_radius(shb) + P.contact_offset;
+                        near = vdot(d, d) < rr * rr * 1.0001f + 1e-6f;
                     }
-                    const V3 d = vsub(vadd(xb, qrot(qbb, v3(shb[4], shb[5], shb[6]))), cA);
-                    const float rr = rA + bound_radius(shb) + P.contact_offset;
-                    near = vdot(d, d) < rr * rr * 1.0001f + 1e-6f;
                 }
-                if (near) {
+                const unsigned gm = (unsigned)((__ballot(near) >> (gi * G)) & 0xFFFFull);
+                if (near) S.npl[nnear + __popc(gm & ((1u << ln) - 1u))] = pi;
+                nnear += __popc(gm);
+            }
+            __syncthreads();
+            for (int rb = 0; __any(rb < nnear); rb += G) {
+                PairOut o;
+                o.n = 0;
+                float mu = 0.0f, rest = 0.0f;
+                int pa = 0, pb = -1;
+                if (rb + ln < nnear) {
+                    const int* pp = A.pairs + (size_t)(pair0 + S.npl[rb + ln]) * 4;
+                    pa = pp[0];
+                    const int sa = pp[1];
+                    pb = pp[2];
+                    const int sb = pp[3];
+                    const float* sha = A.shapes + sa * MG_SHAPE_STRIDE;
+                    V3 xa;
+                    Q4 qa;
+                    pair_pose(S, pa, xa, qa);
                     const CShape ca = place_shape(sha, xa, qa);
                     if (pb < 0) {
                         ground_pair(P, ca, o);
                         mu = 0.5f * (sha[11] + P.mu_ground);
                         rest = 0.5f * (sha[12] + P.e_ground);
                     } else {
-                        collide(ca, place_shape(shb, xb, qbb), P.contact_offset, o);
+                        const float* shb = A.shapes + sb * MG_SHAPE_STRIDE;
+                        V3 xb;
+                        Q4 qb;
+                        pair_pose(S, pb, xb, qb);
+                        collide(ca, place_shape(shb, xb, qb), P.contact_offset, o);
                         mu = 0.5f * (sha[11] + shb[11]);
                         rest = 0.5f * (sha[12] + shb[12]);
                     }
                 }
-            }
-            // exclusive prefix sum of the counts over the 16 lanes
-            int incl = o.n;
+                // exclusive prefix sum of the counts over the 16 lanes
+                int incl = o.n;
 #pragma unroll
-            for (int off = 1; off < G; off <<= 1) {
-                const int t = __shfl_up(incl, off, G);
-                if (ln >= off) incl += t;
-            }
-            const int total = __shfl(incl, G - 1, G);
-            const int slot0 = base + incl - o.n;
-#pragma unroll
-            for (int j = 0; j < MG_PAIR_MAXC; ++j) {
-                const int c = slot0 + j;
-                if (j < o.n && c < MAXCT) {
-                    S.ca[c] = pa;
-                    S.cb[c] = pb;
-                    S.cp[c] = o.p[j];
-                    S.cd[c][0] = o.nrm[j];
-                    env_tangents(o.nrm[j], &S.cd[c][1], &S.cd[c][2]);
-                    S.cs0[c] = o.sep[j] - P.rest_offset;
-                    S.cmu[c] = mu;
-                    S.ce[c] = rest;
-                    if (pa < F0) S.link_rows = 1;
+                for (int off = 1; off < G; off <<= 1) {
+                    const int t = __shfl_up(incl, off, G);
+                    if (ln >= off) incl += t;
                 }
+                const int total = __shfl(incl, G - 1, G);
+                const int slot0 = base + incl - o.n;
+#pragma unroll
+                for (int j = 0; j < MG_PAIR_MAXC; ++j) {
+                    const int c = slot0 + j;
+                    if (j < o.n && c < MAXCT) {
+                        S.ca[c] = pa;
+                        S.cb[c] = pb;
+                        S.cp[c] = o.p[j];
+                        S.cd[c][0] = o.nrm[j];
+                        env_tangents(o.nrm[j], &S.cd[c][1], &S.cd[c][2]);
+                        S.cs0[c] = o.sep[j] - P.rest_offset;
+                        S.cmu[c] = mu;
+                        S.ce[c] = rest;
+                        if (pa < F0) S.link_rows = 1;
+                    }
+                }
+                base += total;
             }
-            base += total;
+            __syncthreads();
         }
         // joint-limit rows (PhysX solves limits as constraints): a DOF whose
         // predicted position q + h u lies within 5% of its range of a limit gets
@@ -675,9 +770,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             int need = 0, sgn = 0;
             float s0 = 0.0f;
             if (live && is_dof) {
-                const int gd = d0 + ln;
-                if (pr[7 * nd + gd] != 0.0f) {
-                    const float lo = pr[5 * nd + gd], hi = pr[6 * nd + gd];
+                if (dc.haslim) {
+                    const float lo = dc.lo, hi = dc.hi;
                     const float q1 = qv + h * uv;
                     const float mg = 0.05f * (hi - lo);
                     if (q1 - lo < mg || hi - q1 < mg) {
@@ -715,14 +809,17 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 
         // ================= 3. rows
         const bool link_rows = live && S.link_rows != 0;
-        if (LA > 0 && __any(link_rows)) meff_world<MAXL>(A, S, link_rows, ln, b0, LA, DA, x0);
+        if (LA > 0 && __any(link_rows)) meff_world<MAXL, ND>(A, S, link_rows, ln, LA, DA, x0, lk, mcol);
         PH_MARK(2);
+        // this DOF lane's joint axis and origin at the substep start
+        const V3 myz = S.zl[mylink], myx = S.xl[mylink];
 #pragma unroll
         for (int c = 0; c < MAXCT; ++c) {
 #pragma unroll
             for (int rw = 0; rw < 3; ++rw) {
                 Jr[c * 3 + rw] = 0.0f;
                 Wr[c * 3 + rw] = 0.0f;
+                lam[c * 3 + rw] = 0.0f;
             }
             if (c < nct) {
                 const int a = S.ca[c], b = S.cb[c];
@@ -734,10 +831,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     if (a >= LIM0) {
                         if (rw == 0 && ln == a - LIM0) J = (float)b;
                     } else if (is_dof) {
-                        if (a < F0 && ((S.amask[a] >> ln) & 1)) {
-                            const int j = S.dlink[ln];
-                            J = S.drev[ln] ? vdot(vcross(S.zl[j], vsub(p, S.xl[j])), dir) : vdot(S.zl[j], dir);
-                        }
+                        if (a < F0 && ((S.amask[a] >> ln) & 1))
+                            J = myrev ? vdot(vcross(myz, vsub(p, myx)), dir) : vdot(myz, dir);
                     } else if (is_free) {
                         const float sg = a == F0 + fk ? 1.0f : (b == F0 + fk ? -1.0f : 0.0f);
                         if (sg != 0.0f) {
@@ -756,17 +851,16 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     if (link_rows) {
                         // W = M_eff^-1 J over the DOF slots (J_k broadcast from lane k)
                         float w = 0.0f;
-                        for (int k = 0; k < D; ++k) w = w + S.Mi[is_dof ? ln : 0][k] * __shfl(J, k, G);
+#pragma unroll
+                        for (int k = 0; k < ND; ++k)
+                            if (k < DA) w = w + mcol[k] * bcast16(J, k);
                         if (is_dof) W = w;
                     }
                     Jr[c * 3 + rw] = J;
                     Wr[c * 3 + rw] = W;
                     const float den = red16(J * W);
                     const float kk = den > 0.0f ? 1.0f / den : 0.0f;
-                    if (ln == 0) {
-                        S.ck[c][rw] = kk;
-                        S.clam[c][rw] = 0.0f;
-                    }
+                    if (ln == 0) S.ck[c][rw] = kk;
                 }
                 const float vn0 = red16(Jr[c * 3] * uv);
                 if (ln == 0) S.cvn0[c] = vn0;
@@ -796,46 +890,52 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         const float ev = S.ce[c], vn0 = S.cvn0[c];
                         if (ev > 0.0f && vn0 < -P.bounce_thresh) tgt = fmaxf(tgt, -ev * vn0);
                     }
-                    const float lam = S.clam[c][0];
+                    // every lane of the env holds the same lambdas (red16 and
+                    // the LDS operands are the same in all 16 lanes)
+                    const float lm = lam[c * 3];
                     float dl = S.ck[c][0] * (tgt - red16(Jr[c * 3] * uv));
-                    const float nl = fmaxf(lam + dl, 0.0f);
-                    dl = nl - lam;
+                    const float nl = fmaxf(lm + dl, 0.0f);
+                    dl = nl - lm;
                     uv = uv + Wr[c * 3] * dl;
-                    __builtin_amdgcn_wave_barrier();
-                    if (ln == 0) S.clam[c][0] = nl;
-                    __builtin_amdgcn_wave_barrier();
+                    lam[c * 3] = nl;
                 }
             }
 #pragma unroll
             for (int c = 0; c < MAXCT; ++c) {
                 if (c < nct) {
-                    const float lim = S.cmu[c] * S.clam[c][0];
+                    const float lim = S.cmu[c] * lam[c * 3];
 #pragma unroll
                     for (int rw = 1; rw < 3; ++rw) {
-                        const float lam = S.clam[c][rw];
-                        const float nl = fminf(fmaxf(lam - S.ck[c][rw] * red16(Jr[c * 3 + rw] * uv), -lim), lim);
-                        const float dl = nl - lam;
+                        const float lm = lam[c * 3 + rw];
+                        const float nl = fminf(fmaxf(lm - S.ck[c][rw] * red16(Jr[c * 3 + rw] * uv), -lim), lim);
+                        const float dl = nl - lm;
                         uv = uv + Wr[c * 3 + rw] * dl;
-                        __builtin_amdgcn_wave_barrier();
-                        if (ln == 0) S.clam[c][rw] = nl;
-                        __builtin_amdgcn_wave_barrier();
+                        lam[c * 3 + rw] = nl;
                     }
                 }
             }
             if (pos) dp = dp + uv * P.sub;
+        }
+        if (ln == 0) {
+#pragma unroll
+            for (int c = 0; c < MAXCT; ++c)
+                if (c < nct) {
+                    S.clam[c][0] = lam[c * 3];
+                    S.clam[c][1] = lam[c * 3 + 1];
+                    S.clam[c][2] = lam[c * 3 + 2];
+                }
         }
         __syncthreads();
         PH_MARK(4);
 
         // ================= 5. integrate
         if (is_dof) {
-            const int gd = d0 + ln;
-            const float maxv = pr[4 * nd + gd];
+            const float maxv = dc.maxv;
             float w = uv;
             if (maxv > 0.0f) w = fminf(fmaxf(w, -maxv), maxv);
             float x = qv + dp;
-            if (pr[7 * nd + gd] != 0.0f) {
-                const float lo = pr[5 * nd + gd], hi = pr[6 * nd + gd];
+            if (dc.haslim) {
+                const float lo = dc.lo, hi = dc.hi;
                 if (x < lo) { x = lo; if (w < 0.0f) w = 0.0f; }
                 if (x > hi) { x = hi; if (w > 0.0f) w = 0.0f; }
             }
