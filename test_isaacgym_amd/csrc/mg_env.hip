@@ -130,6 +130,11 @@ struct DofC {
     int mode, haslim;
     float kp, kd, eff, maxv, lo, hi, arm, tpos, tvel, force;
 };
+struct FreeC {
+    V3 invI, com, fext, text;
+    Q4 iq;
+    float lkeep, akeep, mlv2, mav2, gon;
+};
 
 // pose of a pair participant: link l (< F0), free body F0 + k, static body ST0 + s
 __device__ __forceinline__ void pair_pose(const EnvLds& S, int id, V3& x, Q4& q) {
@@ -515,13 +520,13 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     const bool is_free = fk < nfr;
 
     // ---- substep-invariant setup
+    PH_T0();
     V3 x0 = v3(0.0f, 0.0f, 0.0f);
     Q4 q0 = q4(0.0f, 0.0f, 0.0f, 1.0f);
-    // lane 0 private: free-body constants, contact force sums
-    V3 fcom[MAXF], finvI[MAXF], fext[MAXF], text[MAXF], fsum[MAXF];
-    Q4 fiq[MAXF];
-    float lkeep[MAXF], akeep[MAXF], mlv2[MAXF], mav2[MAXF], gon[MAXF];
-    V3 lsum[MAXL];
+    // lane k < nf: free body k's constants and contact force sum; lane l < L:
+    // link l's contact force sum
+    FreeC fr = {};
+    V3 fsum = v3(0.0f, 0.0f, 0.0f), lsum = v3(0.0f, 0.0f, 0.0f);
     V3 gw = v3(0.0f, 0.0f, 0.0f);
     const int LA = A.nl, DA = A.ndof;           // launch-uniform loop bounds (barriers inside)
     if (L > 0) {
@@ -539,35 +544,33 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 S.dlink[dof] = l;
                 S.drev[dof] = li[1] == MG_JOINT_REVOLUTE ? 1 : 0;
             }
-            lsum[l] = v3(0.0f, 0.0f, 0.0f);
         }
-        for (int k = 0; k < ei[7]; ++k) {
-            const int b = ei[8 + k];
-            S.sx[k] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
-            S.sq[k] = qnormalize(q4(St[3 * nb + b], St[4 * nb + b], St[5 * nb + b], St[6 * nb + b]));
-        }
-        for (int k = 0; k < nfr; ++k) {
-            const int b = ei[3 + k];
-            S.fx[k] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
-            S.fq[k] = qnormalize(q4(St[3 * nb + b], St[4 * nb + b], St[5 * nb + b], St[6 * nb + b]));
-            const float* Ms = A.mass;
-            S.finvm[k] = Ms[0 * nb + b];
-            finvI[k] = v3(Ms[1 * nb + b], Ms[2 * nb + b], Ms[3 * nb + b]);
-            fiq[k] = q4(Ms[4 * nb + b], Ms[5 * nb + b], Ms[6 * nb + b], Ms[7 * nb + b]);
-            fcom[k] = v3(Ms[8 * nb + b], Ms[9 * nb + b], Ms[10 * nb + b]);
-            const float* tf = A.tbf + A.body_tmpl[b] * MG_TBODY_F_N;
-            lkeep[k] = 1.0f - fminf(tf[0] * h, 1.0f);
-            akeep[k] = 1.0f - fminf(tf[1] * h, 1.0f);
-            mlv2[k] = tf[2] * tf[2];
-            mav2[k] = tf[3] * tf[3];
-            gon[k] = tf[4];
-            fext[k] = v3(0.0f, 0.0f, 0.0f);
-            text[k] = v3(0.0f, 0.0f, 0.0f);
-            if (A.ext) {
-                fext[k] = v3(A.ext[0 * nb + b], A.ext[1 * nb + b], A.ext[2 * nb + b]);
-                text[k] = v3(A.ext[3 * nb + b], A.ext[4 * nb + b], A.ext[5 * nb + b]);
-            }
-            fsum[k] = v3(0.0f, 0.0f, 0.0f);
+    }
+    if (live && ln < ei[7]) {
+        const int b = ei[8 + ln];
+        S.sx[ln] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
+        S.sq[ln] = qnormalize(q4(St[3 * nb + b], St[4 * nb + b], St[5 * nb + b], St[6 * nb + b]));
+    }
+    if (live && ln < nfr) {
+        const int b = ei[3 + ln];
+        S.fx[ln] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
+        S.fq[ln] = qnormalize(q4(St[3 * nb + b], St[4 * nb + b], St[5 * nb + b], St[6 * nb + b]));
+        const float* Ms = A.mass;
+        S.finvm[ln] = Ms[0 * nb + b];
+        fr.invI = v3(Ms[1 * nb + b], Ms[2 * nb + b], Ms[3 * nb + b]);
+        fr.iq = q4(Ms[4 * nb + b], Ms[5 * nb + b], Ms[6 * nb + b], Ms[7 * nb + b]);
+        fr.com = v3(Ms[8 * nb + b], Ms[9 * nb + b], Ms[10 * nb + b]);
+        const float* tf = A.tbf + A.body_tmpl[b] * MG_TBODY_F_N;
+        fr.lkeep = 1.0f - fminf(tf[0] * h, 1.0f);
+        fr.akeep = 1.0f - fminf(tf[1] * h, 1.0f);
+        fr.mlv2 = tf[2] * tf[2];
+        fr.mav2 = tf[3] * tf[3];
+        fr.gon = tf[4];
+        fr.fext = v3(0.0f, 0.0f, 0.0f);
+        fr.text = v3(0.0f, 0.0f, 0.0f);
+        if (A.ext) {
+            fr.fext = v3(A.ext[0 * nb + b], A.ext[1 * nb + b], A.ext[2 * nb + b]);
+            fr.text = v3(A.ext[3 * nb + b], A.ext[4 * nb + b], A.ext[5 * nb + b]);
         }
     }
     // slot registers
@@ -604,7 +607,6 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 #pragma unroll
     for (int k = 0; k < ND; ++k) mcol[k] = 0.0f;
     float Jr[MAXCT * 3], Wr[MAXCT * 3], lam[MAXCT * 3];
-    PH_T0();
     PH_MARK(6);
 
     for (int st = 0; st < P.substeps; ++st) {
@@ -630,28 +632,28 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 __syncthreads();
             }
         }
-        if (ln == 0 && live) {
-            for (int k = 0; k < nfr; ++k) {
-                const int s0 = D + 6 * k;
-                const S3 Iw = sym_rdrt(qmat(qmul(S.fq[k], fiq[k])), finvI[k]);
-                S.fIw[k] = Iw;
-                S.fxc[k] = vadd(S.fx[k], qrot(S.fq[k], fcom[k]));
-                V3 v = v3(S.u[s0 + 0], S.u[s0 + 1], S.u[s0 + 2]);
-                V3 w = v3(S.u[s0 + 3], S.u[s0 + 4], S.u[s0 + 5]);
-                if (gon[k] != 0.0f) v = vmad(v, gvec, h);
-                v = vmad(v, fext[k], S.finvm[k] * h);
-                w = vmad(w, symmul(Iw, text[k]), h);
-                v = vscale(v, lkeep[k]);
-                w = vscale(w, akeep[k]);
-                const float v2 = vdot(v, v);
-                if (v2 > mlv2[k]) v = vscale(v, sqrtf(mlv2[k] / v2));
-                const float w2 = vdot(w, w);
-                if (w2 > mav2[k]) w = vscale(w, sqrtf(mav2[k] / w2));
-                S.u[s0 + 0] = v.x; S.u[s0 + 1] = v.y; S.u[s0 + 2] = v.z;
-                S.u[s0 + 3] = w.x; S.u[s0 + 4] = w.y; S.u[s0 + 5] = w.z;
-            }
-            S.link_rows = 0;
+        // free body k (lane k): gravity, external force, damping, speed clamps
+        if (live && ln < nfr) {
+            const int k = ln;
+            const int s0 = D + 6 * k;
+            const S3 Iw = sym_rdrt(qmat(qmul(S.fq[k], fr.iq)), fr.invI);
+            S.fIw[k] = Iw;
+            S.fxc[k] = vadd(S.fx[k], qrot(S.fq[k], fr.com));
+            V3 v = v3(S.u[s0 + 0], S.u[s0 + 1], S.u[s0 + 2]);
+            V3 w = v3(S.u[s0 + 3], S.u[s0 + 4], S.u[s0 + 5]);
+            if (fr.gon != 0.0f) v = vmad(v, gvec, h);
+            v = vmad(v, fr.fext, S.finvm[k] * h);
+            w = vmad(w, symmul(Iw, fr.text), h);
+            v = vscale(v, fr.lkeep);
+            w = vscale(w, fr.akeep);
+            const float v2 = vdot(v, v);
+            if (v2 > fr.mlv2) v = vscale(v, sqrtf(fr.mlv2 / v2));
+            const float w2 = vdot(w, w);
+            if (w2 > fr.mav2) w = vscale(w, sqrtf(fr.mav2 / w2));
+            S.u[s0 + 0] = v.x; S.u[s0 + 1] = v.y; S.u[s0 + 2] = v.z;
+            S.u[s0 + 3] = w.x; S.u[s0 + 4] = w.y; S.u[s0 + 5] = w.z;
         }
+        if (ln == 0) S.link_rows = 0;
         __syncthreads();
         if (is_dof) {
             const float maxv = dc.maxv;
@@ -944,25 +946,32 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         }
         S.dpos[ln] = dp;
         __syncthreads();
-        if (ln == 0 && live) {
+        // contact impulse sums in contact order: link l on lane l, free body k on lane k
+        if (live && (ln < L || ln < nfr)) {
             for (int c = 0; c < nct; ++c) {
-                V3 imp = vscale(S.cd[c][0], S.clam[c][0]);
-                imp = vmad(imp, S.cd[c][1], S.clam[c][1]);
-                imp = vmad(imp, S.cd[c][2], S.clam[c][2]);
                 const int a = S.ca[c], b = S.cb[c];
                 if (a >= LIM0) continue;
-                if (a >= F0) fsum[a - F0] = vadd(fsum[a - F0], imp);
-                else lsum[a] = vadd(lsum[a], imp);
-                if (b >= F0 && b < ST0) fsum[b - F0] = vsub(fsum[b - F0], imp);
+                const bool on_link = ln < L && a == ln;
+                const bool on_fa = ln < nfr && a == F0 + ln;
+                const bool on_fb = ln < nfr && b == F0 + ln;
+                if (on_link || on_fa || on_fb) {
+                    V3 imp = vscale(S.cd[c][0], S.clam[c][0]);
+                    imp = vmad(imp, S.cd[c][1], S.clam[c][1]);
+                    imp = vmad(imp, S.cd[c][2], S.clam[c][2]);
+                    if (on_link) lsum = vadd(lsum, imp);
+                    if (on_fa) fsum = vadd(fsum, imp);
+                    if (on_fb) fsum = vsub(fsum, imp);
+                }
             }
-            for (int k = 0; k < nfr; ++k) {
-                const int s0 = D + 6 * k;
-                const V3 dx = v3(S.dpos[s0 + 0], S.dpos[s0 + 1], S.dpos[s0 + 2]);
-                const V3 dth = v3(S.dpos[s0 + 3], S.dpos[s0 + 4], S.dpos[s0 + 5]);
-                const V3 xc1 = vadd(S.fxc[k], dx);
-                S.fq[k] = qintegrate(S.fq[k], dth);
-                S.fx[k] = vsub(xc1, qrot(S.fq[k], fcom[k]));
-            }
+        }
+        if (live && ln < nfr) {
+            const int k = ln;
+            const int s0 = D + 6 * k;
+            const V3 dx = v3(S.dpos[s0 + 0], S.dpos[s0 + 1], S.dpos[s0 + 2]);
+            const V3 dth = v3(S.dpos[s0 + 3], S.dpos[s0 + 4], S.dpos[s0 + 5]);
+            const V3 xc1 = vadd(S.fxc[k], dx);
+            S.fq[k] = qintegrate(S.fq[k], dth);
+            S.fx[k] = vsub(xc1, qrot(S.fq[k], fr.com));
         }
         __syncthreads();
         PH_MARK(5);
@@ -976,8 +985,66 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         A.dof_vel[d0 + ln] = uv;
     }
     __syncthreads();
-    if (!(ln == 0 && live)) return;
-    for (int k = 0; k < nfr; ++k) {
+    // joint transforms (lane l)
+    if (live && ln < L && ln > 0) {
+        const float* lf = A.link_f + ln * MG_LINK_F_N;
+        const int* li = A.link_i + ln * MG_LINK_I_N;
+        const int jt = li[1], dof = li[2];
+        const V3 po = v3(lf[0], lf[1], lf[2]);
+        const Q4 qo = q4(lf[3], lf[4], lf[5], lf[6]);
+        const V3 ax = v3(lf[7], lf[8], lf[9]);
+        const float qj = dof >= 0 ? S.q[dof] : 0.0f;
+        Q4 qrel = qo;
+        V3 rr = po;
+        if (jt == MG_JOINT_REVOLUTE) qrel = qmul(qo, q_axis_angle(ax, qj));
+        else if (jt == MG_JOINT_PRISMATIC) rr = vadd(po, qrot(qo, vscale(ax, qj)));
+        S.qr[ln] = qrel;
+        S.rr[ln] = rr;
+    }
+    __syncthreads();
+    // forward kinematics and link velocities (lane 0, body frames, LDS)
+    if (live && ln == 0) {
+        for (int l = 0; l < L; ++l) {
+            const int* li = A.link_i + l * MG_LINK_I_N;
+            const int p = li[0], jt = li[1], dof = li[2];
+            if (p < 0) {
+                S.ql[l] = q0;
+                S.xl[l] = x0;
+                put6(S.va[l], svzero());
+            } else {
+                const V3 ax = v3(A.link_f[l * MG_LINK_F_N + 7], A.link_f[l * MG_LINK_F_N + 8],
+                                 A.link_f[l * MG_LINK_F_N + 9]);
+                const float qdj = dof >= 0 ? S.u[dof] : 0.0f;
+                const Q4 qrel = S.qr[l];
+                const V3 rr = S.rr[l];
+                SV sj = svzero();
+                if (jt == MG_JOINT_REVOLUTE) sj = sv(ax, v3(0.0f, 0.0f, 0.0f));
+                else if (jt == MG_JOINT_PRISMATIC) sj = sv(v3(0.0f, 0.0f, 0.0f), ax);
+                const Q4 qp = S.ql[p];
+                S.ql[l] = qnormalize(qmul(qp, qrel));
+                S.xl[l] = vadd(S.xl[p], qrot(qp, rr));
+                put6(S.va[l], svadd(x_motion(m3t(qmat(qrel)), rr, sv6(S.va[p])), svscale(sj, qdj)));
+            }
+        }
+    }
+    __syncthreads();
+    if (live && ln < L) {
+        const int b = b0 + ln;
+        const Q4 ql = S.ql[ln];
+        const V3 xl = S.xl[ln];
+        const SV vl = sv6(S.va[ln]);
+        const V3 ww = qrot(ql, vl.w);
+        const V3 vw = qrot(ql, vadd(vl.v, vcross(vl.w, lk.com)));
+        St[0 * nb + b] = xl.x; St[1 * nb + b] = xl.y; St[2 * nb + b] = xl.z;
+        St[3 * nb + b] = ql.x; St[4 * nb + b] = ql.y; St[5 * nb + b] = ql.z; St[6 * nb + b] = ql.w;
+        St[7 * nb + b] = vw.x; St[8 * nb + b] = vw.y; St[9 * nb + b] = vw.z;
+        St[10 * nb + b] = ww.x; St[11 * nb + b] = ww.y; St[12 * nb + b] = ww.z;
+        A.cforce[0 * nb + b] = lsum.x * P.inv_dt;
+        A.cforce[1 * nb + b] = lsum.y * P.inv_dt;
+        A.cforce[2 * nb + b] = lsum.z * P.inv_dt;
+    }
+    if (live && ln < nfr) {
+        const int k = ln;
         const int b = ei[3 + k];
         const int s0 = D + 6 * k;
         const V3 x = S.fx[k];
@@ -985,56 +1052,11 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         St[0 * nb + b] = x.x; St[1 * nb + b] = x.y; St[2 * nb + b] = x.z;
         St[3 * nb + b] = q.x; St[4 * nb + b] = q.y; St[5 * nb + b] = q.z; St[6 * nb + b] = q.w;
         for (int c = 0; c < 6; ++c) St[(7 + c) * nb + b] = S.u[s0 + c];
-        A.cforce[0 * nb + b] = fsum[k].x * P.inv_dt;
-        A.cforce[1 * nb + b] = fsum[k].y * P.inv_dt;
-        A.cforce[2 * nb + b] = fsum[k].z * P.inv_dt;
+        A.cforce[0 * nb + b] = fsum.x * P.inv_dt;
+        A.cforce[1 * nb + b] = fsum.y * P.inv_dt;
+        A.cforce[2 * nb + b] = fsum.z * P.inv_dt;
     }
-    SV vl[MAXL];
-    for (int l = 0; l < L; ++l) {
-        const float* lf = A.link_f + l * MG_LINK_F_N;
-        const int* li = A.link_i + l * MG_LINK_I_N;
-        const int p = li[0], jt = li[1], dof = li[2];
-        const int b = b0 + l;
-        Q4 ql;
-        V3 xl;
-        if (p < 0) {
-            ql = q0;
-            xl = x0;
-            vl[l] = svzero();
-        } else {
-            const V3 po = v3(lf[0], lf[1], lf[2]);
-            const Q4 qo = q4(lf[3], lf[4], lf[5], lf[6]);
-            const V3 ax = v3(lf[7], lf[8], lf[9]);
-            const float qj = dof >= 0 ? S.q[dof] : 0.0f;
-            const float qdj = dof >= 0 ? S.u[dof] : 0.0f;
-            Q4 qrel = qo;
-            V3 rr = po;
-            SV s = svzero();
-            if (jt == MG_JOINT_REVOLUTE) {
-                qrel = qmul(qo, q_axis_angle(ax, qj));
-                s = sv(ax, v3(0.0f, 0.0f, 0.0f));
-            } else if (jt == MG_JOINT_PRISMATIC) {
-                rr = vadd(po, qrot(qo, vscale(ax, qj)));
-                s = sv(v3(0.0f, 0.0f, 0.0f), ax);
-            }
-            const Q4 qp = S.ql[p];
-            ql = qnormalize(qmul(qp, qrel));
-            xl = vadd(S.xl[p], qrot(qp, rr));
-            vl[l] = svadd(x_motion(m3t(qmat(qrel)), rr, vl[p]), svscale(s, qdj));
-        }
-        S.ql[l] = ql;
-        S.xl[l] = xl;
-        const V3 com = v3(A.mass[8 * nb + b], A.mass[9 * nb + b], A.mass[10 * nb + b]);
-        const V3 ww = qrot(ql, vl[l].w);
-        const V3 vw = qrot(ql, vadd(vl[l].v, vcross(vl[l].w, com)));
-        St[0 * nb + b] = xl.x; St[1 * nb + b] = xl.y; St[2 * nb + b] = xl.z;
-        St[3 * nb + b] = ql.x; St[4 * nb + b] = ql.y; St[5 * nb + b] = ql.z; St[6 * nb + b] = ql.w;
-        St[7 * nb + b] = vw.x; St[8 * nb + b] = vw.y; St[9 * nb + b] = vw.z;
-        St[10 * nb + b] = ww.x; St[11 * nb + b] = ww.y; St[12 * nb + b] = ww.z;
-        A.cforce[0 * nb + b] = lsum[l].x * P.inv_dt;
-        A.cforce[1 * nb + b] = lsum[l].y * P.inv_dt;
-        A.cforce[2 * nb + b] = lsum[l].z * P.inv_dt;
-    }
+    PH_MARK(7);
 }
 
 }  // namespace
