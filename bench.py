@@ -72,7 +72,7 @@ def cpu_baseline(seconds=10.0):
                       "oracle/migym_oracle.c single-threaded (%.1f s)" % (steps, el)}
 
 
-def gimbal_rate(n, steps, warmup, dev):
+def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     """S2 servo-arm: n fixed-base 3-DOF gimbals under random PD
     position targets; one step = set_dof_position_target_tensor -> simulate ->
     refresh DOF + rigid-body state. Returns env-steps/s and the step kernel time."""
@@ -92,15 +92,37 @@ def gimbal_rate(n, steps, warmup, dev):
     for k in range(warmup):
         step(k)
     torch.cuda.synchronize(dev)
+    avg = ctypes.c_float()
+    used = N.lib.mg_step_time_stats(sim.native, min(warmup // 2, 512), ctypes.byref(avg), None, None)
+    # hipGraph replay, one captured step per target slot (as the S1 loop)
+    graphs = None
+    if use_graph:
+        try:
+            graphs, pool = [], None
+            for j in range(tg.shape[0]):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    step(j)
+                pool = g.pool()
+                graphs.append(g)
+            for j in range(3):
+                graphs[(warmup + j) % len(graphs)].replay()
+        except Exception as ex:
+            print("*** bench: S2 hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
+            graphs = None
+    base = warmup + 3
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(steps):
-        step(k)
+        if graphs is not None:
+            graphs[(base + k) % len(graphs)].replay()
+        else:
+            step(base + k)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    avg = ctypes.c_float()
-    used = N.lib.mg_step_time_stats(sim.native, min(steps, 512), ctypes.byref(avg), None, None)
     gym.destroy_sim(sim)
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
+            "timed_loop": "hipGraph replay" if graphs is not None else "eager Python loop",
             "kernel": "k_artic_step<4>", "kernel_ms_avg": avg.value if used > 0 else None,
             "algorithmic_bytes_per_env": 532}
 
@@ -145,7 +167,7 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
         step()
     torch.cuda.synchronize(dev)
     avg = ctypes.c_float()
-    used = N.lib.mg_step_time_stats(sim.native, min(warmup, 512), ctypes.byref(avg), None, None)
+    used = N.lib.mg_step_time_stats(sim.native, min(warmup // 2, 512), ctypes.byref(avg), None, None)
     t_e = time.perf_counter()
     for _ in range(10):
         step()
@@ -246,20 +268,6 @@ def main():
         if gathered:
             sharding.all_gather_rows(root)      # RCCL over xGMI: (world * 2n, 13) observation
 
-    # the same step with the action index on the device, for hipGraph capture
-    kdev = torch.zeros(1, dtype=torch.long, device=dev)     # in [0, acts.shape[0]) at every step
-
-    def step_dev():
-        root[:, 3:10] = acts.index_select(0, kdev).squeeze(0)
-        kdev.add_(1)
-        kdev.remainder_(acts.shape[0])
-        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
-        gym.simulate(sim)
-        gym.fetch_results(sim, False)
-        gym.refresh_actor_root_state_tensor(sim)
-        gym.refresh_rigid_body_state_tensor(sim)
-        gym.refresh_dof_state_tensor(sim)
-
     gym.refresh_actor_root_state_tensor(sim)
     for k in range(args.warmup):
         step(k)
@@ -276,31 +284,41 @@ def main():
     hi = ctypes.c_float()
     used = N.lib.mg_step_time_stats(sim.native, min(neager, 512), ctypes.byref(avg),
                                     ctypes.byref(lo), ctypes.byref(hi))
-    graph = None
+    # hipGraph replay: one captured step per action slot j (the step that applies
+    # acts[j]), sharing one memory pool; step k replays graph k % slots, so the
+    # replayed sequence is exactly step(k)'s
+    graphs = None
     if not args.eager and not gathered:
         try:
-            kdev.fill_((args.warmup + neager) % acts.shape[0])
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
-                for _ in range(3):
-                    step_dev()
+                for j in range(3):
+                    step(args.warmup + neager + j)
             torch.cuda.current_stream(dev).wait_stream(side)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                step_dev()
-            for _ in range(3):
-                graph.replay()
+            base = args.warmup + neager + 3
+            graphs = []
+            pool = None
+            for j in range(acts.shape[0]):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    step(j)
+                pool = g.pool()
+                graphs.append(g)
+            # capture does not run the work: replay three steps to settle
+            for j in range(3):
+                graphs[(base + j) % len(graphs)].replay()
+            base += 3
         except Exception as ex:          # capture unsupported here: time the eager loop
             print("*** bench: hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
-            graph = None
+            graphs = None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        if graph is not None:
-            graph.replay()
+        if graphs is not None:
+            graphs[(base + k) % len(graphs)].replay()
         else:
             step(args.warmup + neager + k)
     torch.cuda.synchronize(dev)
@@ -311,7 +329,7 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    if graph is None:
+    if graphs is None:
         used = N.lib.mg_step_time_stats(sim.native, min(args.steps, 512), ctypes.byref(avg), ctypes.byref(lo),
                                         ctypes.byref(hi))
 
@@ -346,7 +364,7 @@ def main():
                 "parallelism": "env-sharded, one process per GPU%s" % (", RCCL all-gather of root state"
                                                                         if gathered else
                                                                         ", no collectives"),
-                "timed_loop": "hipGraph replay of the captured tensor-API step" if graph is not None
+                "timed_loop": "hipGraph replay: one captured tensor-API step per action slot" if graphs is not None
                               else "eager Python loop",
                 "eager_ms_per_step": eager_ms,
             },
@@ -363,14 +381,14 @@ def main():
                 "kernel_ms_min": lo.value if used > 0 else None,
                 "kernel_launches_timed": int(used),
                 "kernel_timing": "HIP events around each simulate() of the eager %s" % (
-                    "segment after the warmup (graph replays carry no events)" if graph is not None
+                    "segment after the warmup (graph replays carry no events)" if graphs is not None
                     else "timed loop"),
                 "note": "working set of 4096 envs (~2.8 MB) sits in L2/MALL: the step is launch/latency "
                         "bound at this size (SURVEY.md §0.10)",
             },
         }
         if world == 1 and not args.no_gimbal:
-            out["s2_servo_arm"] = gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev)
+            out["s2_servo_arm"] = gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
         if world == 1 and not args.no_franka:
             out["s3_franka"] = franka_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
         if world == 1 and not args.no_cpu_baseline:
