@@ -172,8 +172,6 @@ static step_t make_step_(const mg_sim_params* p) {
  * written out explicitly (as the device's BasisZ specialisation). */
 typedef struct { int upz; v3_t n, t1, t2; } basis_t;
 static float b_dn(const basis_t* B, v3_t v) { return B->upz ? v.z : dot3(B->n, v); }
-static float b_d1(const basis_t* B, v3_t v) { return B->upz ? v.y : dot3(B->t1, v); }
-static float b_d2(const basis_t* B, v3_t v) { return B->upz ? -v.x : dot3(B->t2, v); }
 static v3_t b_cn(const basis_t* B, v3_t r) { return B->upz ? V(r.y, -r.x, 0.0f) : cross3(r, B->n); }
 static v3_t b_c1(const basis_t* B, v3_t r) { return B->upz ? V(-r.z, 0.0f, r.x) : cross3(r, B->t1); }
 static v3_t b_c2(const basis_t* B, v3_t r) { return B->upz ? V(0.0f, -r.z, r.y) : cross3(r, B->t2); }
@@ -181,19 +179,45 @@ static v3_t b_addn(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x, v
 static v3_t b_add1(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x, v.y + s, v.z) : mad3(v, B->t1, s); }
 static v3_t b_add2(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x - s, v.y, v.z) : mad3(v, B->t2, s); }
 
+/* Gauss-Seidel row kernels with explicit fused multiply-adds, as the device
+ * (mg_rigid.hip BasisGen / BasisZ vn, v1, v2, ps, fn, f1, f2) */
+static float fdot3_(v3_t a, v3_t b, float acc) { return fmaf(a.z, b.z, fmaf(a.y, b.y, fmaf(a.x, b.x, acc))); }
+static v3_t fmad3_(v3_t v, v3_t d, float s) { return V(fmaf(d.x, s, v.x), fmaf(d.y, s, v.y), fmaf(d.z, s, v.z)); }
+static float b_vn(const basis_t* B, v3_t v, v3_t w, v3_t r) {
+    return B->upz ? fmaf(w.y, -r.x, fmaf(w.x, r.y, v.z)) : fdot3_(w, cross3(r, B->n), dot3(B->n, v));
+}
+static float b_v1(const basis_t* B, v3_t v, v3_t w, v3_t r) {
+    return B->upz ? fmaf(w.z, r.x, fmaf(w.x, -r.z, v.y)) : fdot3_(w, cross3(r, B->t1), dot3(B->t1, v));
+}
+static float b_v2(const basis_t* B, v3_t v, v3_t w, v3_t r) {
+    return B->upz ? fmaf(w.z, r.y, fmaf(w.y, -r.z, -v.x)) : fdot3_(w, cross3(r, B->t2), dot3(B->t2, v));
+}
+static float b_ps(const basis_t* B, float s0, v3_t dx, v3_t dth, v3_t r) {
+    return B->upz ? fmaf(dth.y, -r.x, fmaf(dth.x, r.y, s0 + dx.z)) : fdot3_(dth, cross3(r, B->n), s0 + dot3(B->n, dx));
+}
+static v3_t b_fn(const basis_t* B, v3_t v, float dl, float invm) {
+    return B->upz ? V(v.x, v.y, fmaf(dl, invm, v.z)) : fmad3_(v, B->n, dl * invm);
+}
+static v3_t b_f1(const basis_t* B, v3_t v, float dl, float invm) {
+    return B->upz ? V(v.x, fmaf(dl, invm, v.y), v.z) : fmad3_(v, B->t1, dl * invm);
+}
+static v3_t b_f2(const basis_t* B, v3_t v, float dl, float invm) {
+    return B->upz ? V(fmaf(-dl, invm, v.x), v.y, v.z) : fmad3_(v, B->t2, dl * invm);
+}
+
 typedef struct {
     v3_t r; float s0, mu, e, kn, kt1, kt2, ln, lt1, lt2, vn0; int on;
 } slot_t;
 
 static void contact_normal(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw, float tgt) {
     v3_t rn = b_cn(B, c->r);
-    float vn = b_dn(B, *v) + dot3(*w, rn);
+    float vn = b_vn(B, *v, *w, c->r);
     float dl = c->kn * (tgt - vn);
     float nl = fmaxf(c->ln + dl, 0.0f);
     dl = nl - c->ln;
     c->ln = nl;
-    *v = b_addn(B, *v, dl * invm);
-    *w = mad3(*w, symmul_(*Iw, rn), dl);
+    *v = b_fn(B, *v, dl, invm);
+    *w = fmad3_(*w, symmul_(*Iw, rn), dl);
 }
 
 /* PhysX-style pyramid friction: tangent rows one after the other, each
@@ -201,19 +225,19 @@ static void contact_normal(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, float 
 static void contact_friction(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw) {
     const float lim = c->mu * c->ln;
     v3_t r1 = b_c1(B, c->r), r2;
-    float vt1 = b_d1(B, *v) + dot3(*w, r1), vt2, n1, n2, d1, d2;
+    float vt1 = b_v1(B, *v, *w, c->r), vt2, n1, n2, d1, d2;
     n1 = fminf(fmaxf(c->lt1 - c->kt1 * vt1, -lim), lim);
     d1 = n1 - c->lt1;
     c->lt1 = n1;
-    *v = b_add1(B, *v, d1 * invm);
-    *w = mad3(*w, symmul_(*Iw, r1), d1);
+    *v = b_f1(B, *v, d1, invm);
+    *w = fmad3_(*w, symmul_(*Iw, r1), d1);
     r2 = b_c2(B, c->r);
-    vt2 = b_d2(B, *v) + dot3(*w, r2);
+    vt2 = b_v2(B, *v, *w, c->r);
     n2 = fminf(fmaxf(c->lt2 - c->kt2 * vt2, -lim), lim);
     d2 = n2 - c->lt2;
     c->lt2 = n2;
-    *v = b_add2(B, *v, d2 * invm);
-    *w = mad3(*w, symmul_(*Iw, r2), d2);
+    *v = b_f2(B, *v, d2, invm);
+    *w = fmad3_(*w, symmul_(*Iw, r2), d2);
 }
 
 /* Contact candidates of one shape: (static index k, point, separation). */
@@ -334,28 +358,28 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                 sl[j].kt1 = 1.0f / (invm + dot3(r1, symmul_(Iw, r1)));
                 sl[j].kt2 = 1.0f / (invm + dot3(r2, symmul_(Iw, r2)));
                 sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
-                sl[j].vn0 = b_dn(&B, v) + dot3(w, rn);
+                sl[j].vn0 = b_vn(&B, v, w, sl[j].r);
             }
         }
         for (it = 0; it < P->npos; ++it) {
             for (j = 0; j < OR_MAXC; ++j) {
                 float s, tgt;
                 if (!sl[j].on) continue;
-                s = sl[j].s0 + b_dn(&B, dx) + dot3(dth, b_cn(&B, sl[j].r));
+                s = b_ps(&B, sl[j].s0, dx, dth, sl[j].r);
                 tgt = -s * P->inv_sub;
                 if (s < 0.0f) tgt = fminf(tgt, P->maxdep);
                 contact_normal(&B, &sl[j], &v, &w, invm, &Iw, tgt);
             }
             for (j = 0; j < OR_MAXC; ++j)
                 if (sl[j].on) contact_friction(&B, &sl[j], &v, &w, invm, &Iw);
-            dx = mad3(dx, v, P->sub);
-            dth = mad3(dth, w, P->sub);
+            dx = fmad3_(dx, v, P->sub);
+            dth = fmad3_(dth, w, P->sub);
         }
         for (it = 0; it < P->nvel; ++it) {
             for (j = 0; j < OR_MAXC; ++j) {
                 float s, tgt;
                 if (!sl[j].on) continue;
-                s = sl[j].s0 + b_dn(&B, dx) + dot3(dth, b_cn(&B, sl[j].r));
+                s = b_ps(&B, sl[j].s0, dx, dth, sl[j].r);
                 tgt = s > 0.0f ? -s * P->inv_h : 0.0f;
                 if (sl[j].e > 0.0f && sl[j].vn0 < -P->bounce) tgt = fmaxf(tgt, -sl[j].e * sl[j].vn0);
                 contact_normal(&B, &sl[j], &v, &w, invm, &Iw, tgt);

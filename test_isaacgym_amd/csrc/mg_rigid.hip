@@ -34,6 +34,16 @@
 namespace {
 
 // ---- ground basis: general (n, t1, t2) or the +Z specialisation -----------
+// Row kernels of the Gauss-Seidel chain use explicit fused multiply-adds
+// (fmaf, correctly rounded like the oracle's C fmaf); everything else is built
+// with -ffp-contract=off. vn / v1 / v2: velocity of the contact point along the
+// row direction d (d . v + w . (r x d)); ps: separation s0 + n . dx + dth . (r x n).
+__device__ __forceinline__ float fdot3(V3 a, V3 b, float acc) {
+    return fmaf(a.z, b.z, fmaf(a.y, b.y, fmaf(a.x, b.x, acc)));
+}
+__device__ __forceinline__ V3 fmad3(V3 v, V3 d, float s) {
+    return v3(fmaf(d.x, s, v.x), fmaf(d.y, s, v.y), fmaf(d.z, s, v.z));
+}
 struct BasisGen {
     V3 n, t1, t2;
     __device__ __forceinline__ float dn(V3 v) const { return vdot(n, v); }
@@ -45,6 +55,15 @@ struct BasisGen {
     __device__ __forceinline__ V3 addn(V3 v, float s) const { return vmad(v, n, s); }
     __device__ __forceinline__ V3 add1(V3 v, float s) const { return vmad(v, t1, s); }
     __device__ __forceinline__ V3 add2(V3 v, float s) const { return vmad(v, t2, s); }
+    __device__ __forceinline__ float vn(V3 v, V3 w, V3 r) const { return fdot3(w, cn(r), vdot(n, v)); }
+    __device__ __forceinline__ float v1(V3 v, V3 w, V3 r) const { return fdot3(w, c1(r), vdot(t1, v)); }
+    __device__ __forceinline__ float v2(V3 v, V3 w, V3 r) const { return fdot3(w, c2(r), vdot(t2, v)); }
+    __device__ __forceinline__ float ps(float s0, V3 dx, V3 dth, V3 r) const {
+        return fdot3(dth, cn(r), s0 + vdot(n, dx));
+    }
+    __device__ __forceinline__ V3 fn(V3 v, float dl, float invm) const { return fmad3(v, n, dl * invm); }
+    __device__ __forceinline__ V3 f1(V3 v, float dl, float invm) const { return fmad3(v, t1, dl * invm); }
+    __device__ __forceinline__ V3 f2(V3 v, float dl, float invm) const { return fmad3(v, t2, dl * invm); }
 };
 // n = (0,0,1), t1 = (0,1,0), t2 = (-1,0,0)
 struct BasisZ {
@@ -57,6 +76,16 @@ struct BasisZ {
     __device__ __forceinline__ V3 addn(V3 v, float s) const { return v3(v.x, v.y, v.z + s); }
     __device__ __forceinline__ V3 add1(V3 v, float s) const { return v3(v.x, v.y + s, v.z); }
     __device__ __forceinline__ V3 add2(V3 v, float s) const { return v3(v.x - s, v.y, v.z); }
+    // r x n = (r.y, -r.x, 0), r x t1 = (-r.z, 0, r.x), r x t2 = (0, -r.z, r.y): zero terms dropped
+    __device__ __forceinline__ float vn(V3 v, V3 w, V3 r) const { return fmaf(w.y, -r.x, fmaf(w.x, r.y, v.z)); }
+    __device__ __forceinline__ float v1(V3 v, V3 w, V3 r) const { return fmaf(w.z, r.x, fmaf(w.x, -r.z, v.y)); }
+    __device__ __forceinline__ float v2(V3 v, V3 w, V3 r) const { return fmaf(w.z, r.y, fmaf(w.y, -r.z, -v.x)); }
+    __device__ __forceinline__ float ps(float s0, V3 dx, V3 dth, V3 r) const {
+        return fmaf(dth.y, -r.x, fmaf(dth.x, r.y, s0 + dx.z));
+    }
+    __device__ __forceinline__ V3 fn(V3 v, float dl, float invm) const { return v3(v.x, v.y, fmaf(dl, invm, v.z)); }
+    __device__ __forceinline__ V3 f1(V3 v, float dl, float invm) const { return v3(v.x, fmaf(dl, invm, v.y), v.z); }
+    __device__ __forceinline__ V3 f2(V3 v, float dl, float invm) const { return v3(fmaf(-dl, invm, v.x), v.y, v.z); }
 };
 
 struct Slot {
@@ -79,14 +108,13 @@ template <bool CACHE, class B>
 __device__ __forceinline__ void contact_normal(const B& G, Slot& c, V3& v, V3& w, float invm, const S3& Iw,
                                                float tgt) {
     if (!CACHE) MG_OPAQUE3(c.r);
-    const V3 rn = G.cn(c.r);
-    const float vn = G.dn(v) + vdot(w, rn);
+    const float vn = G.vn(v, w, c.r);
     float dl = c.kn * (tgt - vn);
     const float nl = fmaxf(c.ln + dl, 0.0f);
     dl = nl - c.ln;
     c.ln = nl;
-    v = G.addn(v, dl * invm);
-    w = vmad(w, CACHE ? c.In : symmul(Iw, rn), dl);
+    v = G.fn(v, dl, invm);
+    w = fmad3(w, CACHE ? c.In : symmul(Iw, G.cn(c.r)), dl);
 }
 
 // Coulomb friction, PhysX-style pyramid: the two tangent rows are solved one
@@ -96,20 +124,18 @@ template <bool CACHE, class B>
 __device__ __forceinline__ void contact_friction(const B& G, Slot& c, V3& v, V3& w, float invm, const S3& Iw) {
     if (!CACHE) MG_OPAQUE3(c.r);
     const float lim = c.mu * c.ln;
-    const V3 r1 = G.c1(c.r);
-    const float vt1 = G.d1(v) + vdot(w, r1);
+    const float vt1 = G.v1(v, w, c.r);
     const float n1 = fminf(fmaxf(c.lt1 - c.kt1 * vt1, -lim), lim);
     const float d1 = n1 - c.lt1;
     c.lt1 = n1;
-    v = G.add1(v, d1 * invm);
-    w = vmad(w, CACHE ? c.I1 : symmul(Iw, r1), d1);
-    const V3 r2 = G.c2(c.r);
-    const float vt2 = G.d2(v) + vdot(w, r2);
+    v = G.f1(v, d1, invm);
+    w = fmad3(w, CACHE ? c.I1 : symmul(Iw, G.c1(c.r)), d1);
+    const float vt2 = G.v2(v, w, c.r);
     const float n2 = fminf(fmaxf(c.lt2 - c.kt2 * vt2, -lim), lim);
     const float d2 = n2 - c.lt2;
     c.lt2 = n2;
-    v = G.add2(v, d2 * invm);
-    w = vmad(w, CACHE ? c.I2 : symmul(Iw, r2), d2);
+    v = G.f2(v, d2, invm);
+    w = fmad3(w, CACHE ? c.I2 : symmul(Iw, G.c2(c.r)), d2);
 }
 
 // Candidates of one shape: emit(k, point, separation, mu, e) with k the static
@@ -274,7 +300,7 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
                 sl[j].kt1 = 1.0f / (invm + vdot(r1, I1));
                 sl[j].kt2 = 1.0f / (invm + vdot(r2, I2));
                 sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
-                sl[j].vn0 = G.dn(v) + vdot(w, rn);
+                sl[j].vn0 = G.vn(v, w, sl[j].r);
             }
         }
 
@@ -284,7 +310,7 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
 #pragma unroll
             for (int j = 0; j < MAXC; ++j) {
                 if (sl[j].on) {
-                    const float s = sl[j].s0 + G.dn(dx) + vdot(dth, G.cn(sl[j].r));
+                    const float s = G.ps(sl[j].s0, dx, dth, sl[j].r);
                     float tgt = -s * P.inv_sub;
                     if (s < 0.0f) tgt = fminf(tgt, P.max_depen);
                     contact_normal<CACHE>(G, sl[j], v, w, invm, Iw, tgt);
@@ -293,15 +319,15 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
 #pragma unroll
             for (int j = 0; j < MAXC; ++j)
                 if (sl[j].on) contact_friction<CACHE>(G, sl[j], v, w, invm, Iw);
-            dx = vmad(dx, v, P.sub);
-            dth = vmad(dth, w, P.sub);
+            dx = fmad3(dx, v, P.sub);
+            dth = fmad3(dth, w, P.sub);
         }
         // velocity iterations (bias removed)
         for (int it = 0; it < P.nvel; ++it) {
 #pragma unroll
             for (int j = 0; j < MAXC; ++j) {
                 if (sl[j].on) {
-                    const float s = sl[j].s0 + G.dn(dx) + vdot(dth, G.cn(sl[j].r));
+                    const float s = G.ps(sl[j].s0, dx, dth, sl[j].r);
                     float tgt = s > 0.0f ? -s * P.inv_h : 0.0f;
                     if (sl[j].e > 0.0f && sl[j].vn0 < -P.bounce_thresh) tgt = fmaxf(tgt, -sl[j].e * sl[j].vn0);
                     contact_normal<CACHE>(G, sl[j], v, w, invm, Iw, tgt);
