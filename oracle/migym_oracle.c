@@ -473,6 +473,13 @@ static void joint_(const float* lf, int jt, float qj, q4_t* qrel, v3_t* rr, sv_t
     }
 }
 
+#include "migym_oracle_env.c"
+
+/* Templates of at most OR_WORLD_MAXL links take the world-frame ABA (aba_world_,
+ * as mg_artic.hip k_artic_world); larger ones the body-frame ABA below
+ * (mg_artic.hip k_artic_step). */
+#define OR_WORLD_MAXL 4
+
 /* ---- articulation: Featherstone ABA, implicit drives ---- */
 static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* state /*[nb][13]*/,
                       float* dof /*[nd][2]*/, const float* tgt /*[nd][3]*/, const float* props /*[nd][12]*/,
@@ -503,6 +510,11 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
       unsigned xmask = 0u, xpos = 0u;
       float tau0d[OR_MAXL], impd[OR_MAXL];
       int att;
+      if (L <= OR_WORLD_MAXL) {
+          static aba_ws_t W;
+          float mdiag[OR_MAXL];
+          aba_world_(P, m, LF, LI, L, D, b0, d0, q, qd, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd);
+      } else
       for (att = 0; att < 2; ++att) {
         unsigned nm;
         for (l = 0; l < L; ++l) {
@@ -646,7 +658,6 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
     return 0;
 }
 
-#include "migym_oracle_env.c"
 
 /* ---- entry point --------------------------------------------------------
  * One gym.simulate() over the whole model, AoS host arrays:

@@ -388,8 +388,8 @@ static const float* shp_(const mg_model* m, int s) { return m->shapes + (size_t)
 
 #define OE_MAXPAIRS 512
 
-static float dot6_(const float* a, const float* b) {
-    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+static float dot6_(const float* a, const float* b) {   /* fused chain, as mg_world.h dot6 */
+    return fmaf(a[5], b[5], fmaf(a[4], b[4], fmaf(a[3], b[3], fmaf(a[2], b[2], fmaf(a[1], b[1], a[0] * b[0])))));
 }
 static sv_t sv6_(const float* a) { return SVc(V(a[0], a[1], a[2]), V(a[3], a[4], a[5])); }
 static void put6_(float* a, sv_t s) { a[0] = s.w.x; a[1] = s.w.y; a[2] = s.w.z; a[3] = s.v.x; a[4] = s.v.y; a[5] = s.v.z; }
@@ -418,6 +418,159 @@ static void world_inertia_(const float* M, q4_t ql, v3_t xl, v3_t O, float* I) {
         }
 }
 
+/* World-frame articulated-body algorithm about the base origin x0 (RBDA ch. 7,
+ * every quantity in one frame; mg_env.hip aba_world, mg_artic.hip
+ * k_artic_world): unconstrained joint accelerations qdd with implicit drives
+ * and the effort-limit re-solve. Sets W (kinematics, motion axes, inertias),
+ * mdiag (armature + implicit drive term), tau0d / impd (drive force, implicit
+ * coefficient) for the final attempt. Shared by env_step_ and artic_step. */
+typedef struct {
+    q4_t ql[OR_MAXL], qrl[OR_MAXL];
+    v3_t xl[OR_MAXL], zl[OR_MAXL], rrl[OR_MAXL];
+    float Iw[OR_MAXL][36], xi[OR_MAXL][6], va[OR_MAXL][6], ccv[OR_MAXL][6], pav[OR_MAXL][6], Ua[OR_MAXL][6];
+    float Dd[OR_MAXL], uu[OR_MAXL];
+} aba_ws_t;
+
+static void aba_world_(const step_t* P, const mg_model* m, const float* LF, const int* LI, int L, int D, int b0,
+                       int d0, const float* q, const float* u, const float* props, const float* tgt, v3_t x0, q4_t q0,
+                       v3_t gw, aba_ws_t* W, float* qdd, float* mdiag, float* tau0d, float* impd) {
+    const float h = P->h;
+    q4_t* ql = W->ql; q4_t* qrl = W->qrl;
+    v3_t* xl = W->xl; v3_t* zl = W->zl; v3_t* rrl = W->rrl;
+    float (*Iw)[36] = W->Iw;
+    float (*xi)[6] = W->xi; float (*va)[6] = W->va; float (*ccv)[6] = W->ccv; float (*pav)[6] = W->pav;
+    float (*Ua)[6] = W->Ua;
+    float* Dd = W->Dd; float* uu = W->uu;
+    int l, i, d;
+    if (L > 0) {
+        unsigned xmask = 0u, xpos = 0u;
+        int att;
+        for (att = 0; att < 2; ++att) {
+            unsigned nm;
+            for (l = 1; l < L; ++l) {
+                const float* lf = LF + l * MG_LINK_F_N;
+                const int jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
+                const v3_t po = V(lf[0], lf[1], lf[2]), ax = V(lf[7], lf[8], lf[9]);
+                const q4_t qo = Q(lf[3], lf[4], lf[5], lf[6]);
+                const float qj = dj >= 0 ? q[dj] : 0.0f;
+                qrl[l] = qo; rrl[l] = po;
+                if (jt == MG_JOINT_REVOLUTE) qrl[l] = qmul_(qo, qaxang_(ax, qj));
+                else if (jt == MG_JOINT_PRISMATIC) rrl[l] = add3(po, qrot_(qo, mul3(ax, qj)));
+            }
+            for (l = 0; l < L; ++l) {
+                const int p = LI[l * MG_LINK_I_N + 0];
+                if (p < 0) { ql[l] = q0; xl[l] = x0; zl[l] = V(0.0f, 0.0f, 0.0f); }
+                else {
+                    const float* lf = LF + l * MG_LINK_F_N;
+                    ql[l] = qnorm_(qmul_(ql[p], qrl[l]));
+                    xl[l] = add3(xl[p], qrot_(ql[p], rrl[l]));
+                    zl[l] = qrot_(ql[l], V(lf[7], lf[8], lf[9]));
+                }
+            }
+            for (l = 0; l < L; ++l) {
+                const int jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
+                sv_t x = sv0();
+                if (l > 0 && dj >= 0) {
+                    if (jt == MG_JOINT_REVOLUTE) x = SVc(zl[l], cross3(sub3(xl[l], x0), zl[l]));
+                    else x = SVc(V(0.0f, 0.0f, 0.0f), zl[l]);
+                }
+                put6_(xi[l], x);
+                world_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N, ql[l], xl[l], x0, Iw[l]);
+            }
+            for (i = 0; i < 6; ++i) va[0][i] = 0.0f;
+            for (l = 1; l < L; ++l) {
+                const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
+                const float qd = dj >= 0 ? u[dj] : 0.0f;
+                for (i = 0; i < 6; ++i) va[l][i] = va[p][i] + xi[l][i] * qd;
+            }
+            for (l = 0; l < L; ++l) {
+                const int dj = LI[l * MG_LINK_I_N + 2];
+                const float qd = dj >= 0 ? u[dj] : 0.0f;
+                const sv_t v = sv6_(va[l]);
+                const sv_t vJ = svmul_(sv6_(xi[l]), qd);
+                float Iv[6];
+                for (i = 0; i < 6; ++i) Iv[i] = dot6_(&Iw[l][i * 6], va[l]);
+                put6_(ccv[l], crm_(v, vJ));
+                put6_(pav[l], crf_(v, sv6_(Iv)));
+            }
+            for (l = L - 1; l >= 1; --l) {
+                const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
+                float uinvD = 0.0f;
+                if (dj >= 0) {
+                    const float* pr = props + (size_t)(d0 + dj) * MG_DOFPROP_N;
+                    const float* tg = tgt + (size_t)(d0 + dj) * 3;
+                    const int mode = (int)pr[0];
+                    const float kp = pr[1], kd = pr[2], eff = pr[3], arm = pr[8];
+                    const float qv = q[dj], uv = u[dj];
+                    float tau = 0.0f, imp = 0.0f, Dv, uvv, invD;
+                    for (i = 0; i < 6; ++i) Ua[l][i] = dot6_(&Iw[l][i * 6], xi[l]);
+                    if (mode == MG_DOF_MODE_POS) {
+                        tau = kp * (tg[0] - qv - h * uv) + kd * (tg[1] - uv);
+                        imp = h * kd + h * h * kp;
+                    } else if (mode == MG_DOF_MODE_VEL) {
+                        tau = kd * (tg[1] - uv);
+                        imp = h * kd;
+                    } else if (mode == MG_DOF_MODE_EFFORT) {
+                        tau = tg[2];
+                    }
+                    if (eff > 0.0f) {
+                        if ((xmask >> dj) & 1u) {
+                            tau = ((xpos >> dj) & 1u) ? eff : -eff;
+                            imp = 0.0f;
+                        } else if (imp == 0.0f) {
+                            tau = fminf(fmaxf(tau, -eff), eff);
+                        }
+                    }
+                    Dv = dot6_(xi[l], Ua[l]) + arm + imp;
+                    uvv = tau - dot6_(xi[l], pav[l]);
+                    invD = 1.0f / Dv;
+                    uinvD = uvv * invD;
+                    for (i = 0; i < 36; ++i) Iw[l][i] = Iw[l][i] - Ua[l][i / 6] * (Ua[l][i % 6] * invD);
+                    Dd[l] = Dv;
+                    uu[l] = uvv;
+                    mdiag[dj] = arm + imp;
+                    tau0d[dj] = tau;
+                    impd[dj] = imp;
+                }
+                if (p > 0) {
+                    for (i = 0; i < 6; ++i) {
+                        float pv = pav[l][i] + dot6_(&Iw[l][i * 6], ccv[l]);
+                        if (dj >= 0) pv = pv + Ua[l][i] * uinvD;
+                        pav[p][i] = pav[p][i] + pv;
+                    }
+                    for (i = 0; i < 36; ++i) Iw[p][i] = Iw[p][i] + Iw[l][i];
+                }
+            }
+            va[0][0] = 0.0f; va[0][1] = 0.0f; va[0][2] = 0.0f;
+            va[0][3] = -gw.x; va[0][4] = -gw.y; va[0][5] = -gw.z;
+            for (l = 1; l < L; ++l) {
+                const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
+                float a6[6];
+                for (i = 0; i < 6; ++i) a6[i] = va[p][i] + ccv[l][i];
+                if (dj >= 0) {
+                    float t16[16], acc;
+                    for (i = 0; i < 16; ++i) t16[i] = i < 6 ? Ua[l][i] * a6[i] : 0.0f;
+                    acc = (uu[l] - red16_(t16)) / Dd[l];
+                    for (i = 0; i < 6; ++i) a6[i] = a6[i] + xi[l][i] * acc;
+                    qdd[dj] = acc;
+                }
+                for (i = 0; i < 6; ++i) va[l][i] = a6[i];
+            }
+            nm = xmask;
+            for (d = 0; d < D; ++d) {
+                const float eff = props[(size_t)(d0 + d) * MG_DOFPROP_N + 3];
+                if (eff > 0.0f && impd[d] != 0.0f) {
+                    const float actf = tau0d[d] - impd[d] * qdd[d];
+                    if (actf > eff) { nm |= 1u << d; xpos |= 1u << d; }
+                    else if (actf < -eff) nm |= 1u << d;
+                }
+            }
+            if (nm == xmask) break;
+            xmask = nm;
+        }
+    }
+}
+
 static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float* state, float* dof, const float* tgt,
                      const float* props, const float* ext, float* cforce) {
     const int b0 = ev->art_body, d0 = ev->art_dof, nfr = ev->nf;
@@ -434,11 +587,12 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     /* slots */
     float q[OE_G], u[OE_G], dp[OE_G], qdd[OE_G], mdiag[OE_G], tau0d[OE_G], impd[OE_G];
     /* links */
-    v3_t xl[OR_MAXL], zl[OR_MAXL], lsum[OR_MAXL], rrl[OR_MAXL];
-    q4_t ql[OR_MAXL], qrl[OR_MAXL];
+    static aba_ws_t W;
+    v3_t* xl = W.xl; v3_t* zl = W.zl; q4_t* ql = W.ql;
+    v3_t lsum[OR_MAXL];
     sv_t vl[OR_MAXL];
-    static float Iw[OR_MAXL][36];
-    float xi[OR_MAXL][6], va[OR_MAXL][6], ccv[OR_MAXL][6], pav[OR_MAXL][6], Ua[OR_MAXL][6], Dd[OR_MAXL], uu[OR_MAXL];
+    float (*Iw)[36] = W.Iw;
+    float (*xi)[6] = W.xi;
     int amask[OR_MAXL], dlink[OE_G], drev[OE_G];
     static float Lc[OE_G][OE_G], Mi[OE_G][OE_G];
     float invd[OE_G];
@@ -500,133 +654,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     for (st_ = 0; st_ < P->substeps; ++st_) {
         int nct = 0, link_rows = 0;
         /* ---- 1. unconstrained motion: world-frame ABA about x0 (mg_env.hip aba_world) */
-        if (L > 0) {
-            unsigned xmask = 0u, xpos = 0u;
-            int att;
-            for (att = 0; att < 2; ++att) {
-                unsigned nm;
-                for (l = 1; l < L; ++l) {
-                    const float* lf = LF + l * MG_LINK_F_N;
-                    const int jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
-                    const v3_t po = V(lf[0], lf[1], lf[2]), ax = V(lf[7], lf[8], lf[9]);
-                    const q4_t qo = Q(lf[3], lf[4], lf[5], lf[6]);
-                    const float qj = dj >= 0 ? q[dj] : 0.0f;
-                    qrl[l] = qo; rrl[l] = po;
-                    if (jt == MG_JOINT_REVOLUTE) qrl[l] = qmul_(qo, qaxang_(ax, qj));
-                    else if (jt == MG_JOINT_PRISMATIC) rrl[l] = add3(po, qrot_(qo, mul3(ax, qj)));
-                }
-                for (l = 0; l < L; ++l) {
-                    const int p = LI[l * MG_LINK_I_N + 0];
-                    if (p < 0) { ql[l] = q0; xl[l] = x0; zl[l] = V(0.0f, 0.0f, 0.0f); }
-                    else {
-                        const float* lf = LF + l * MG_LINK_F_N;
-                        ql[l] = qnorm_(qmul_(ql[p], qrl[l]));
-                        xl[l] = add3(xl[p], qrot_(ql[p], rrl[l]));
-                        zl[l] = qrot_(ql[l], V(lf[7], lf[8], lf[9]));
-                    }
-                }
-                for (l = 0; l < L; ++l) {
-                    const int jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
-                    sv_t x = sv0();
-                    if (l > 0 && dj >= 0) {
-                        if (jt == MG_JOINT_REVOLUTE) x = SVc(zl[l], cross3(sub3(xl[l], x0), zl[l]));
-                        else x = SVc(V(0.0f, 0.0f, 0.0f), zl[l]);
-                    }
-                    put6_(xi[l], x);
-                    world_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N, ql[l], xl[l], x0, Iw[l]);
-                }
-                for (i = 0; i < 6; ++i) va[0][i] = 0.0f;
-                for (l = 1; l < L; ++l) {
-                    const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
-                    const float qd = dj >= 0 ? u[dj] : 0.0f;
-                    for (i = 0; i < 6; ++i) va[l][i] = va[p][i] + xi[l][i] * qd;
-                }
-                for (l = 0; l < L; ++l) {
-                    const int dj = LI[l * MG_LINK_I_N + 2];
-                    const float qd = dj >= 0 ? u[dj] : 0.0f;
-                    const sv_t v = sv6_(va[l]);
-                    const sv_t vJ = svmul_(sv6_(xi[l]), qd);
-                    float Iv[6];
-                    for (i = 0; i < 6; ++i) Iv[i] = dot6_(&Iw[l][i * 6], va[l]);
-                    put6_(ccv[l], crm_(v, vJ));
-                    put6_(pav[l], crf_(v, sv6_(Iv)));
-                }
-                for (l = L - 1; l >= 1; --l) {
-                    const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
-                    float uinvD = 0.0f;
-                    if (dj >= 0) {
-                        const float* pr = props + (size_t)(d0 + dj) * MG_DOFPROP_N;
-                        const float* tg = tgt + (size_t)(d0 + dj) * 3;
-                        const int mode = (int)pr[0];
-                        const float kp = pr[1], kd = pr[2], eff = pr[3], arm = pr[8];
-                        const float qv = q[dj], uv = u[dj];
-                        float tau = 0.0f, imp = 0.0f, Dv, uvv, invD;
-                        for (i = 0; i < 6; ++i) Ua[l][i] = dot6_(&Iw[l][i * 6], xi[l]);
-                        if (mode == MG_DOF_MODE_POS) {
-                            tau = kp * (tg[0] - qv - h * uv) + kd * (tg[1] - uv);
-                            imp = h * kd + h * h * kp;
-                        } else if (mode == MG_DOF_MODE_VEL) {
-                            tau = kd * (tg[1] - uv);
-                            imp = h * kd;
-                        } else if (mode == MG_DOF_MODE_EFFORT) {
-                            tau = tg[2];
-                        }
-                        if (eff > 0.0f) {
-                            if ((xmask >> dj) & 1u) {
-                                tau = ((xpos >> dj) & 1u) ? eff : -eff;
-                                imp = 0.0f;
-                            } else if (imp == 0.0f) {
-                                tau = fminf(fmaxf(tau, -eff), eff);
-                            }
-                        }
-                        Dv = dot6_(xi[l], Ua[l]) + arm + imp;
-                        uvv = tau - dot6_(xi[l], pav[l]);
-                        invD = 1.0f / Dv;
-                        uinvD = uvv * invD;
-                        for (i = 0; i < 36; ++i) Iw[l][i] = Iw[l][i] - Ua[l][i / 6] * (Ua[l][i % 6] * invD);
-                        Dd[l] = Dv;
-                        uu[l] = uvv;
-                        mdiag[dj] = arm + imp;
-                        tau0d[dj] = tau;
-                        impd[dj] = imp;
-                    }
-                    if (p > 0) {
-                        for (i = 0; i < 6; ++i) {
-                            float pv = pav[l][i] + dot6_(&Iw[l][i * 6], ccv[l]);
-                            if (dj >= 0) pv = pv + Ua[l][i] * uinvD;
-                            pav[p][i] = pav[p][i] + pv;
-                        }
-                        for (i = 0; i < 36; ++i) Iw[p][i] = Iw[p][i] + Iw[l][i];
-                    }
-                }
-                va[0][0] = 0.0f; va[0][1] = 0.0f; va[0][2] = 0.0f;
-                va[0][3] = -gw.x; va[0][4] = -gw.y; va[0][5] = -gw.z;
-                for (l = 1; l < L; ++l) {
-                    const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
-                    float a6[6];
-                    for (i = 0; i < 6; ++i) a6[i] = va[p][i] + ccv[l][i];
-                    if (dj >= 0) {
-                        float t16[16], acc;
-                        for (i = 0; i < 16; ++i) t16[i] = i < 6 ? Ua[l][i] * a6[i] : 0.0f;
-                        acc = (uu[l] - red16_(t16)) / Dd[l];
-                        for (i = 0; i < 6; ++i) a6[i] = a6[i] + xi[l][i] * acc;
-                        qdd[dj] = acc;
-                    }
-                    for (i = 0; i < 6; ++i) va[l][i] = a6[i];
-                }
-                nm = xmask;
-                for (d = 0; d < D; ++d) {
-                    const float eff = props[(size_t)(d0 + d) * MG_DOFPROP_N + 3];
-                    if (eff > 0.0f && impd[d] != 0.0f) {
-                        const float actf = tau0d[d] - impd[d] * qdd[d];
-                        if (actf > eff) { nm |= 1u << d; xpos |= 1u << d; }
-                        else if (actf < -eff) nm |= 1u << d;
-                    }
-                }
-                if (nm == xmask) break;
-                xmask = nm;
-            }
-        }
+        if (L > 0) aba_world_(P, m, LF, LI, L, D, b0, d0, q, u, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd);
         for (k = 0; k < nfr; ++k) {
             const int s0 = D + 6 * k;
             const s3_t Iw = sym_rdrt_(qmat_(qmul_(fq[k], fiq[k])), finvI[k]);

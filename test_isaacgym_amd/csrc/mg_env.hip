@@ -27,6 +27,7 @@
 #include "mg_internal.h"
 #include "mg_spatial.h"
 #include "mg_collide.h"
+#include "mg_world.h"
 
 #ifdef MG_ENV_PHASE_TIMING
 // profiling build only: per-phase shader-clock cycles summed over waves
@@ -119,13 +120,8 @@ __device__ __forceinline__ float bcast16(float v, int k) {
     }
 }
 
-// substep-invariant per-lane constants: lane l < L holds link l's mass
-// properties, lane d < D holds DOF d's drive properties and targets
-struct LinkC {
-    float m, Idx, Idy, Idz;
-    V3 com;
-    Q4 iq;
-};
+// substep-invariant per-lane constants: lane d < D holds DOF d's drive
+// properties and targets (link constants: LinkC, mg_world.h)
 struct DofC {
     int mode, haslim;
     float kp, kd, eff, maxv, lo, hi, arm, tpos, tvel, force;
@@ -206,49 +202,6 @@ MG_HD float bound_radius(const float* sh) {
     return sh[1];
 }
 
-
-MG_HD float dot6(const float* a, const float* b) {
-    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
-}
-MG_HD SV sv6(const float* a) { return sv(v3(a[0], a[1], a[2]), v3(a[3], a[4], a[5])); }
-MG_HD void put6(float* a, SV s) { a[0] = s.w.x; a[1] = s.w.y; a[2] = s.w.z; a[3] = s.v.x; a[4] = s.v.y; a[5] = s.v.z; }
-
-// world-frame spatial inertia of link body b about the point O: row-major 6x6
-// [A B; B^T C] with A = Ic + m (|c|^2 1 - c c^T), B = [m c]x, C = m 1
-// (c = COM - O, Ic the rotational inertia about the COM in world axes)
-__device__ LinkC load_link(const float* Ms, int nb, int b) {
-    LinkC k;
-    k.m = Ms[11 * nb + b];
-    k.com = v3(Ms[8 * nb + b], Ms[9 * nb + b], Ms[10 * nb + b]);
-    k.iq = q4(Ms[4 * nb + b], Ms[5 * nb + b], Ms[6 * nb + b], Ms[7 * nb + b]);
-    const float ix = Ms[1 * nb + b], iy = Ms[2 * nb + b], iz = Ms[3 * nb + b];
-    k.Idx = ix > 0.0f ? 1.0f / ix : 0.0f;
-    k.Idy = iy > 0.0f ? 1.0f / iy : 0.0f;
-    k.Idz = iz > 0.0f ? 1.0f / iz : 0.0f;
-    return k;
-}
-
-MG_HD void world_inertia(const LinkC& K, Q4 ql, V3 xl, V3 O, float* I) {
-    const float m = K.m;
-    const V3 com = K.com;
-    const Q4 iq = K.iq;
-    const V3 Id = v3(K.Idx, K.Idy, K.Idz);
-    const S3 Ic = sym_rdrt(qmat(qmul(ql, iq)), Id);
-    const V3 c = vsub(vadd(xl, qrot(ql, com)), O);
-    const float cc2 = vdot(c, c);
-    const float ic[9] = {Ic.xx, Ic.xy, Ic.xz, Ic.xy, Ic.yy, Ic.yz, Ic.xz, Ic.yz, Ic.zz};
-    const float cv[3] = {c.x, c.y, c.z};
-    const V3 mc = vscale(c, m);
-    const float sk[9] = {0.0f, -mc.z, mc.y, mc.z, 0.0f, -mc.x, -mc.y, mc.x, 0.0f};   // [m c]x, row-major
-    for (int i = 0; i < 3; ++i)
-        for (int k = 0; k < 3; ++k) {
-            const float dg = i == k ? m * cc2 : 0.0f;
-            I[i * 6 + k] = ic[i * 3 + k] + (dg - cv[i] * (cv[k] * m));
-            I[i * 6 + 3 + k] = sk[i * 3 + k];
-            I[(3 + i) * 6 + k] = sk[k * 3 + i];
-            I[(3 + i) * 6 + 3 + k] = i == k ? m : 0.0f;
-        }
-}
 
 // Articulated-body algorithm in the world frame about the base origin x0 (RBDA
 // ch. 7 with all quantities in one frame: no spatial transforms in the inward
