@@ -123,7 +123,7 @@ def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     gym.destroy_sim(sim)
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
             "timed_loop": "hipGraph replay" if graphs is not None else "eager Python loop",
-            "kernel": "k_artic_step<4>", "kernel_ms_avg": avg.value if used > 0 else None,
+            "kernel": "k_artic_world<4>", "kernel_ms_avg": avg.value if used > 0 else None,
             "algorithmic_bytes_per_env": 532}
 
 
