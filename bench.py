@@ -209,6 +209,75 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
     return out
 
 
+def camera_rate(n, steps, warmup, dev, use_graph=True, width=1600, height=900):
+    """S5 (config 5, test11_servo_vecenv_camerazoom.py): the S1 servo step plus
+    one 1600x900 camera per env on the UAV (local (5, 0, 0), FOLLOW_TRANSFORM,
+    horizontal FOV 30 degrees) rendered into a GPU color tensor every step by
+    render_all_camera_sensors. Returns env-steps/s and the render kernel's
+    time and write bandwidth (roofline: the kernel streams W*H*4 bytes per
+    camera to HBM; reads are the env's few shapes)."""
+    gym = gymapi.acquire_gym()
+    sim, envs = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
+    imgs = scenes.attach_servo_cameras(gym, sim, envs, width, height, 30.0)
+    gym.prepare_sim(sim)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    gym.acquire_rigid_body_state_tensor(sim)
+    acts = scenes.servo_actions(n, 16, dev, seed=5)
+
+    def step(k):
+        root[:, 3:10] = acts[k % acts.shape[0]]
+        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.simulate(sim)
+        gym.fetch_results(sim, False)
+        gym.refresh_actor_root_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.render_all_camera_sensors(sim)
+
+    gym.refresh_actor_root_state_tensor(sim)
+    rms = []
+    for k in range(warmup):
+        step(k)
+        if k >= warmup // 2:
+            rms.append(N.lib.mg_last_render_ms(sim.native))
+    torch.cuda.synchronize(dev)
+    graphs = None
+    if use_graph:
+        try:
+            graphs, pool = [], None
+            for j in range(acts.shape[0]):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    step(j)
+                pool = g.pool()
+                graphs.append(g)
+            for j in range(2):
+                graphs[(warmup + j) % len(graphs)].replay()
+        except Exception as ex:
+            print("*** bench: S5 hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
+            graphs = None
+    base = warmup + 2
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        if graphs is not None:
+            graphs[(base + k) % len(graphs)].replay()
+        else:
+            step(base + k)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    lit = float((imgs[0][0][..., :3].amax(-1) > 0).float().mean())
+    gym.destroy_sim(sim)
+    rk = float(np.mean(rms)) if rms else float("nan")
+    wbytes = n * width * height * 4
+    ach = wbytes / (rk * 1e-3) / 1e9
+    return {"envs": n, "cameras": n, "resolution": [width, height], "env_steps_per_s": n * steps / el,
+            "ms_per_step": 1e3 * el / steps, "timed_loop": "hipGraph replay" if graphs is not None else "eager",
+            "kernel": "k_render", "kernel_ms_avg": rk, "image_bytes_per_launch": wbytes,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS},
+            "env0_non_sky_fraction": lit}
+
+
 def load_traffic(envs):
     """HBM bytes per k_rigid_step launch at this env count from the committed
     rocprofv3 PMC passes (profiles/r01_pmc_rigid_<envs>.json, written by
@@ -232,6 +301,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-gimbal", action="store_true", help="skip the secondary S2 servo-arm measurement")
     ap.add_argument("--no-franka", action="store_true", help="skip the secondary S3 Franka cube-pick measurement")
+    ap.add_argument("--no-cameras", action="store_true", help="skip the secondary S5 camera-render measurement")
+    ap.add_argument("--camera-envs", type=int, default=1024)
     ap.add_argument("--eager", action="store_true",
                     help="time the Python loop itself instead of a hipGraph replay of the step")
     args = ap.parse_args()
@@ -391,6 +462,8 @@ def main():
             out["s2_servo_arm"] = gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
         if world == 1 and not args.no_franka:
             out["s3_franka"] = franka_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
+        if world == 1 and not args.no_cameras:
+            out["s5_cameras"] = camera_rate(args.camera_envs, min(args.steps, 100), 10, dev, not args.eager)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline"]["cores"] = 1

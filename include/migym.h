@@ -76,6 +76,7 @@ extern "C" {
 #define MG_ARTIC_I_N       4  /* first_body, first_dof, tmpl, pad */
 #define MG_ATMPL_I_N       4  /* first_link (into tmpl_link_*), num_links, num_dofs, fixed_base */
 #define MG_ACOLL_N         4  /* env, collision group, collision filter, pad */
+#define MG_RENDER_MAX_SHAPES 64 /* shapes one camera's env may hold */
 
 /* Simulation parameters: gymapi.SimParams + PhysXParams + the ground plane
  * (reference: test10_servo_vecenv.py:117-144 and :198-206). */
@@ -212,6 +213,46 @@ int32_t     mg_refresh_mass_matrix(mg_sim* sim, int32_t tmpl, float* dst, int32_
  * be NULL; both are device memory, or both host memory when dst_host. */
 int32_t     mg_refresh_jacobian_mass_matrix(mg_sim* sim, int32_t tmpl, float* jac, float* mm, int32_t dst_host,
                                             void* stream);
+
+/* ---- camera sensors (config 5: test11_servo_vecenv_camerazoom.py:327-342,388,
+ * 458-460; examples/interop_torch.py:105-120,173-174) ------------------------
+ * A camera sees its own env's bodies and the ground plane (what Isaac Gym's
+ * camera sensors show: examples/interop_images/ holds no neighbouring env's ball,
+ * DESIGN.md §3.8). Images are ray cast on the device:
+ *   color (H, W, 4) RGBA8, depth (H, W) float32 = -(distance along the view
+ *   axis), -inf where nothing is hit, segmentation (H, W) int32 = the body's
+ *   segmentation id, 0 for ground and sky.
+ * Camera frame: looks along its local +x with the sim's up axis (+z, or +y for
+ * UP_AXIS_Y) as image up; pixel (c, r) is the ray f + a l + b u with
+ * a = (cx - c - 0.5) / fx, b = (cy - r - 0.5) / fy. */
+typedef struct mg_camera {
+    int32_t  env;            /* env index: the scene is that env's bodies + ground */
+    int32_t  width, height;
+    int32_t  body;           /* global rigid-body index the camera is attached to, -1: fixed */
+    int32_t  follow;         /* gymapi.CameraFollowMode: 0 FOLLOW_POSITION, 1 FOLLOW_TRANSFORM */
+    float    fx, fy, cx, cy; /* pinhole intrinsics in pixels */
+    float    near_plane, far_plane;
+    float    p[3], q[4];     /* attached: pose in the body frame; fixed: world pose */
+    int32_t  reserved;
+    uint8_t* color;          /* device (H, W, 4) or NULL (not rendered) */
+    float*   depth;          /* device (H, W) or NULL */
+    int32_t* seg;            /* device (H, W) or NULL */
+} mg_camera;
+
+/* What the renderer draws per body: env_body_first [num_envs + 1] (global body
+ * ranges of each env, CSR), color [num_bodies][3] in 0..1 (set_rigid_body_color),
+ * seg [num_bodies] (segmentation ids). Host arrays; may be called again. */
+int32_t     mg_set_render_bodies(mg_sim* sim, const int32_t* env_body_first, const float* color,
+                                 const int32_t* seg);
+/* gym.render_all_camera_sensors: freeze the body poses the cameras see (a device
+ * copy of the state, in stream order); later renders use this snapshot. */
+int32_t     mg_snapshot_render_state(mg_sim* sim, void* stream);
+/* Render `n` cameras (host array) from the snapshot into their device images,
+ * one launch. The camera table is uploaded when it changes (not allowed while
+ * the stream is being captured into a graph). */
+int32_t     mg_render_cameras(mg_sim* sim, const mg_camera* cams, int32_t n, void* stream);
+/* Duration in ms of the last mg_render_cameras launch (HIP events), -1 if none. */
+float       mg_last_render_ms(mg_sim* sim);
 
 /* ---- introspection for tests and the bench ------------------------------- */
 /* Duration in ms of the last simulate()'s kernels (HIP events on `stream`),

@@ -80,3 +80,27 @@ def collide(a, b, margin):
     out = np.zeros((4, 7), dtype=np.float32)
     n = L.oracle_collide(a.ctypes.data, b.ctypes.data, float(margin), out.ctypes.data)
     return out[:n]
+
+
+def render(sim_params, state, body_tmpl, tbi, shapes, env_body_first, color, seg, cam):
+    """One camera on the host (oracle_render, migym_oracle_render.c): returns
+    (rgba (H, W, 4) uint8, depth (H, W) f32, seg (H, W) int32). state is the
+    rigid-body tensor [nb, 13] (global order); cam a _native.MgCamera (its
+    device pointers are ignored)."""
+    L = lib()
+    vp = ctypes.c_void_p
+    L.oracle_render.restype = ctypes.c_int
+    L.oracle_render.argtypes = [vp] * 12
+    H, W = cam.height, cam.width
+    rgba = np.zeros((H, W, 4), np.uint8)
+    depth = np.zeros((H, W), np.float32)
+    sg = np.zeros((H, W), np.int32)
+    arrs = [np.ascontiguousarray(state, np.float32), np.ascontiguousarray(body_tmpl, np.int32),
+            np.ascontiguousarray(tbi, np.int32), np.ascontiguousarray(shapes, np.float32),
+            np.ascontiguousarray(env_body_first, np.int32), np.ascontiguousarray(color, np.float32),
+            np.ascontiguousarray(seg, np.int32)]
+    rc = L.oracle_render(ctypes.addressof(sim_params), *[a.ctypes.data for a in arrs], ctypes.addressof(cam),
+                         rgba.ctypes.data, depth.ctypes.data, sg.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("oracle_render: too many shapes in the camera's env")
+    return rgba, depth, sg

@@ -474,6 +474,7 @@ static void joint_(const float* lf, int jt, float qj, q4_t* qrel, v3_t* rr, sv_t
 }
 
 #include "migym_oracle_env.c"
+#include "migym_oracle_render.c"
 
 /* Templates of at most OR_WORLD_MAXL links take the world-frame ABA (aba_world_,
  * as mg_artic.hip k_artic_world); larger ones the body-frame ABA below

@@ -1,0 +1,235 @@
+/*
+ * migym_oracle_render.c — TEST INFRASTRUCTURE ONLY (included by
+ * migym_oracle.c). CPU restatement of the camera ray caster
+ * (test_isaacgym_amd/csrc/mg_render.hip), one pixel at a time,
+ * in the kernel's order of operations, without its culling (a culled shape
+ * cannot be the nearest hit, so images agree bit for bit).
+ *
+ * What it is pinned to. Isaac Gym's renderer is closed; its outputs in the
+ * reference tree are examples/interop_images/cam-<frame>-<env>.png (16 envs of
+ * examples/interop_torch.py:56-120 at frames 0..50). tests/test_render.py
+ * checks this restatement against the fixture extracted from them
+ * (tests/golden/interop_fixture.json): the ball's silhouette per frame (camera
+ * placement and projection, examples/interop_torch.py:111, default 90-degree
+ * field of view, gravity and frame cadence), the 1 m ground checker and the
+ * absence of neighbouring envs' balls. Shading values are not pinned.
+ *
+ * Camera frame: looks along local +x, image up = the sim's up axis; pixel
+ * (c, r) -> ray f + a l + b u, a = (cx - c - 0.5)/fx, b = (cy - r - 0.5)/fy.
+ */
+
+typedef struct {
+    int type, seg;
+    float r, g, b;
+    v3_t c;
+    m3_t R;
+    v3_t h;
+} rws_t;
+
+static const float R_INF = __builtin_inff();
+
+static float ray_sphere_(v3_t o, v3_t d, v3_t c, float r, float tmin) {
+    v3_t oc = sub3(o, c);
+    float bb = dot3(oc, d);
+    float cc = dot3(oc, oc) - r * r;
+    float dd = dot3(d, d);
+    float disc = bb * bb - dd * cc;
+    float t;
+    if (!(disc >= 0.0f)) return R_INF;
+    t = (-bb - sqrtf(disc)) / dd;
+    return t >= tmin ? t : R_INF;
+}
+
+static void slab_(float o, float d, float h, float* tn, float* tf) {
+    float inv = 1.0f / d;
+    float t1 = (-h - o) * inv;
+    float t2 = (h - o) * inv;
+    *tn = fmaxf(*tn, fminf(t1, t2));
+    *tf = fminf(*tf, fmaxf(t1, t2));
+}
+
+static float ray_box_(v3_t o, v3_t d, const rws_t* s, float tmin, float tmax) {
+    v3_t ol = mtv_(s->R, sub3(o, s->c));
+    v3_t dl = mtv_(s->R, d);
+    float tn = -R_INF, tf = tmax;   /* entry point only: back faces are not drawn */
+    slab_(ol.x, dl.x, s->h.x, &tn, &tf);
+    slab_(ol.y, dl.y, s->h.y, &tn, &tf);
+    slab_(ol.z, dl.z, s->h.z, &tn, &tf);
+    return (tn <= tf && tn >= tmin) ? tn : R_INF;
+}
+
+static float ray_capsule_(v3_t o, v3_t d, const rws_t* s, float tmin) {
+    float r = s->h.x, hl = s->h.y;
+    v3_t ax = s->R.c0;
+    v3_t pa = sub3(s->c, mul3(ax, hl));
+    v3_t ba = mul3(ax, 2.0f * hl);
+    v3_t oa = sub3(o, pa);
+    float baba = dot3(ba, ba), bard = dot3(ba, d), baoa = dot3(ba, oa);
+    float rdoa = dot3(d, oa), oaoa = dot3(oa, oa), dd = dot3(d, d);
+    float a = baba * dd - bard * bard;
+    float b = baba * rdoa - baoa * bard;
+    float c = baba * oaoa - baoa * baoa - r * r * baba;
+    float hh = b * b - a * c;
+    float t = R_INF, t0, t1;
+    if (!(hh >= 0.0f)) return R_INF;
+    if (a > 0.0f) {
+        float tb = (-b - sqrtf(hh)) / a;
+        float y = baoa + tb * bard;
+        if (y > 0.0f && y < baba && tb >= tmin) t = tb;
+    }
+    t0 = ray_sphere_(o, d, pa, r, tmin);
+    t1 = ray_sphere_(o, d, add3(pa, ba), r, tmin);
+    t = t0 < t ? t0 : t;
+    t = t1 < t ? t1 : t;
+    return t;
+}
+
+static float ray_shape_(v3_t o, v3_t d, const rws_t* s, float tmin, float tmax) {
+    if (s->type == MG_SHAPE_BOX) return ray_box_(o, d, s, tmin, tmax);
+    if (s->type == MG_SHAPE_SPHERE) return ray_sphere_(o, d, s->c, s->h.x, tmin);
+    return ray_capsule_(o, d, s, tmin);
+}
+
+static v3_t shape_normal_(const rws_t* s, v3_t p) {
+    v3_t dp = sub3(p, s->c);
+    float t;
+    if (s->type == MG_SHAPE_SPHERE) return mul3(dp, 1.0f / s->h.x);
+    if (s->type == MG_SHAPE_BOX) {
+        v3_t pl = mtv_(s->R, dp), axis;
+        float qx = fabsf(pl.x) / s->h.x, qy = fabsf(pl.y) / s->h.y, qz = fabsf(pl.z) / s->h.z;
+        float best = qx, comp;
+        int k = 0;
+        if (qy > best) { k = 1; best = qy; }
+        if (qz > best) k = 2;
+        axis = k == 0 ? s->R.c0 : (k == 1 ? s->R.c1 : s->R.c2);
+        comp = k == 0 ? pl.x : (k == 1 ? pl.y : pl.z);
+        return mul3(axis, comp < 0.0f ? -1.0f : 1.0f);
+    }
+    t = dot3(dp, s->R.c0);
+    t = fminf(fmaxf(t, -s->h.y), s->h.y);
+    return mul3(sub3(dp, mul3(s->R.c0, t)), 1.0f / s->h.x);
+}
+
+static unsigned q8_(float x) { return (unsigned)(fminf(fmaxf(x, 0.0f), 1.0f) * 255.0f + 0.5f); }
+
+/* One camera. state: AoS [nb][13] in global body order; body_tmpl [nb];
+ * tbi [ntb][MG_TBODY_I_N]; shapes [ns][MG_SHAPE_STRIDE]; env_body_first
+ * [num_envs+1]; color [nb][3]; seg [nb]. Outputs may be NULL. */
+int oracle_render(const mg_sim_params* p, const float* state, const int32_t* body_tmpl, const int32_t* tbi,
+                  const float* shapes, const int32_t* env_body_first, const float* color, const int32_t* seg,
+                  const mg_camera* cam, uint8_t* rgba_out, float* depth_out, int32_t* seg_out) {
+    rws_t ws[MG_RENDER_MAX_SHAPES];
+    int ns = 0, b, k, row, col;
+    v3_t o, f, l, u, upv, leftv, L, gn;
+    q4_t q;
+    float ifx, ify, lx = 0.3f, ly = 0.2f, lz = 1.0f, inv;
+    int up_axis = p->up_axis == 0 ? 0 : 1;
+
+    /* the env's shapes in the world frame */
+    for (b = env_body_first[cam->env]; b < env_body_first[cam->env + 1]; ++b) {
+        const float* st = state + (size_t)b * MG_STATE_N;
+        v3_t pb = V(st[0], st[1], st[2]);
+        q4_t qb = Q(st[3], st[4], st[5], st[6]);
+        int t = body_tmpl[b];
+        int sh0 = tbi[t * MG_TBODY_I_N + 0], nsh = tbi[t * MG_TBODY_I_N + 1];
+        for (k = 0; k < nsh; ++k) {
+            const float* sh = shapes + (size_t)(sh0 + k) * MG_SHAPE_STRIDE;
+            rws_t* w;
+            if (ns >= MG_RENDER_MAX_SHAPES) return -1;
+            w = &ws[ns++];
+            w->type = (int)sh[0];
+            w->seg = seg[b];
+            w->r = color[3 * b + 0]; w->g = color[3 * b + 1]; w->b = color[3 * b + 2];
+            w->c = add3(pb, qrot_(qb, V(sh[4], sh[5], sh[6])));
+            w->R = qmat_(qmul_(qb, Q(sh[7], sh[8], sh[9], sh[10])));
+            if (w->type == MG_SHAPE_BOX) w->h = V(sh[1], sh[2], sh[3]);
+            else if (w->type == MG_SHAPE_SPHERE) w->h = V(sh[1], 0.0f, 0.0f);
+            else w->h = V(sh[1], sh[2], 0.0f);
+        }
+    }
+
+    /* camera pose and frame */
+    o = V(cam->p[0], cam->p[1], cam->p[2]);
+    q = Q(cam->q[0], cam->q[1], cam->q[2], cam->q[3]);
+    if (cam->body >= 0) {
+        const float* st = state + (size_t)cam->body * MG_STATE_N;
+        v3_t pb = V(st[0], st[1], st[2]);
+        q4_t qb = Q(st[3], st[4], st[5], st[6]);
+        if (cam->follow == 1) {
+            o = add3(pb, qrot_(qb, o));
+            q = qmul_(qb, q);
+        } else {
+            o = add3(pb, o);
+        }
+    }
+    if (up_axis == 1) {
+        upv = V(0.0f, 0.0f, 1.0f);
+        leftv = V(0.0f, 1.0f, 0.0f);
+    } else {
+        upv = V(0.0f, 1.0f, 0.0f);
+        leftv = V(0.0f, 0.0f, -1.0f);
+        ly = 1.0f; lz = 0.2f;
+    }
+    inv = 1.0f / sqrtf(lx * lx + ly * ly + lz * lz);
+    L = V(lx * inv, ly * inv, lz * inv);
+    f = qrot_(q, V(1.0f, 0.0f, 0.0f));
+    l = qrot_(q, leftv);
+    u = qrot_(q, upv);
+    ifx = 1.0f / cam->fx;
+    ify = 1.0f / cam->fy;
+    gn = V(p->ground_normal[0], p->ground_normal[1], p->ground_normal[2]);
+
+    for (row = 0; row < cam->height; ++row) {
+        for (col = 0; col < cam->width; ++col) {
+            size_t px = (size_t)row * cam->width + col;
+            float a = (cam->cx - ((float)col + 0.5f)) * ifx;
+            float bq = (cam->cy - ((float)row + 0.5f)) * ify;
+            v3_t d = add3(add3(f, mul3(l, a)), mul3(u, bq));
+            float best = cam->far_plane;
+            int hit = -2, j, shadow = 0, sgv;
+            unsigned rgba;
+            float cr, cg, cb;
+            v3_t pp, n, ps;
+            if (p->has_ground) {
+                float dn = dot3(gn, d);
+                if (dn < 0.0f) {
+                    float t = -(dot3(gn, o) + p->ground_distance) / dn;
+                    if (t >= cam->near_plane && t < best) { best = t; hit = -1; }
+                }
+            }
+            for (j = 0; j < ns; ++j) {
+                float t = ray_shape_(o, d, &ws[j], cam->near_plane, best);
+                if (t < best) { best = t; hit = j; }
+            }
+            if (hit == -2) {
+                if (rgba_out) memcpy(rgba_out + 4 * px, &(uint32_t){0xFF000000u}, 4);
+                if (depth_out) depth_out[px] = -R_INF;
+                if (seg_out) seg_out[px] = 0;
+                continue;
+            }
+            pp = add3(o, mul3(d, best));
+            n = hit >= 0 ? shape_normal_(&ws[hit], pp) : gn;
+            ps = add3(pp, mul3(n, 1e-3f));
+            for (j = 0; j < ns && !shadow; ++j) shadow = ray_shape_(ps, L, &ws[j], 0.0f, R_INF) < R_INF;
+            if (hit >= 0) {
+                float lam = fmaxf(dot3(n, L), 0.0f);
+                float kk = shadow ? 0.3f : 0.3f + 0.7f * lam;
+                cr = ws[hit].r * kk; cg = ws[hit].g * kk; cb = ws[hit].b * kk;
+                sgv = ws[hit].seg;
+            } else {
+                float uu = pp.x, vv = up_axis == 1 ? pp.y : pp.z;
+                int par = ((int)floorf(uu) + (int)floorf(vv)) & 1;
+                float kk = shadow ? 0.55f : 1.0f;
+                cr = (par ? 108.0f / 255.0f : 143.0f / 255.0f) * kk;
+                cg = cr;
+                cb = (par ? 113.0f / 255.0f : 150.0f / 255.0f) * kk;
+                sgv = 0;
+            }
+            rgba = q8_(cr) | (q8_(cg) << 8) | (q8_(cb) << 16) | 0xFF000000u;
+            if (rgba_out) memcpy(rgba_out + 4 * px, &rgba, 4);
+            if (depth_out) depth_out[px] = -best;
+            if (seg_out) seg_out[px] = sgv;
+        }
+    }
+    return 0;
+}

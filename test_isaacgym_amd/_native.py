@@ -75,6 +75,22 @@ class MgModel(ctypes.Structure):
     ]
 
 
+class MgCamera(ctypes.Structure):
+    """mg_camera (include/migym.h): one camera sensor to render."""
+    _fields_ = [
+        ("env", ctypes.c_int32), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+        ("body", ctypes.c_int32), ("follow", ctypes.c_int32),
+        ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+        ("near_plane", ctypes.c_float), ("far_plane", ctypes.c_float),
+        ("p", ctypes.c_float * 3), ("q", ctypes.c_float * 4),
+        ("reserved", ctypes.c_int32),
+        ("color", ctypes.c_void_p), ("depth", ctypes.c_void_p), ("seg", ctypes.c_void_p),
+    ]
+
+
+MG_RENDER_MAX_SHAPES = 64
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
@@ -112,6 +128,10 @@ def _load():
         "mg_num_free_bodies": (i32, [vp]),
         "mg_num_articulations": (i32, [vp]),
         "mg_num_coupled_envs": (i32, [vp]),
+        "mg_set_render_bodies": (i32, [vp, vp, vp, vp]),
+        "mg_snapshot_render_state": (i32, [vp, vp]),
+        "mg_render_cameras": (i32, [vp, vp, i32, vp]),
+        "mg_last_render_ms": (ctypes.c_float, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -134,6 +154,7 @@ EXPORTED_SYMBOLS = (
     "mg_refresh_jacobian", "mg_refresh_mass_matrix", "mg_last_step_ms", "mg_step_time_stats", "mg_num_free_bodies",
     "mg_num_articulations",
     "mg_num_coupled_envs", "mg_refresh_jacobian_mass_matrix",
+    "mg_set_render_bodies", "mg_snapshot_render_state", "mg_render_cameras", "mg_last_render_ms",
 )
 
 

@@ -78,6 +78,7 @@ class Actor:
         self.shape_props = asset.shape_props      # copy-on-write (set_actor_rigid_shape_properties)
         self.mass_props = asset.mass_props        # copy-on-write (set_actor_rigid_body_properties)
         self.body_colors = {}
+        self.body_segs = {}
         self.scale = 1.0
 
     @property
@@ -117,6 +118,7 @@ class CameraSensor:
         self.body = None          # env-domain body handle when attached
         self.follow = T.FOLLOW_TRANSFORM
         self.transform = T.Transform()   # env-frame transform when not attached
+        self.images = {}                 # IMAGE_* -> persistent device tensor (get_camera_image_gpu_tensor)
 
 
 class Sim:
@@ -142,6 +144,16 @@ class Sim:
         # computed alongside the Jacobian is reused while the epoch is unchanged
         self.epoch = 0
         self.mm_cache = {}
+        self._renderer = None
+        self.cam_version = 0       # bumped by every camera change (render tables are rebuilt)
+        self.render_version = 0    # bumped by body colour / segmentation changes
+
+    @property
+    def renderer(self):
+        if self._renderer is None:
+            from ._render import Renderer
+            self._renderer = Renderer(self)
+        return self._renderer
 
     # ------------------------------------------------------------ params
     def mg_params(self):

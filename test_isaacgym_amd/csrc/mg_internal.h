@@ -116,7 +116,47 @@ struct MgEnvArgs {
     float*       cforce;
 };
 
+// Camera render (mg_render.hip). One device record per camera; a camera's
+// pixels are cut into linear runs of MG_RENDER_RUN pixels (row-major), one run
+// per workgroup; blk0 = first workgroup of the camera (prefix over cameras).
+#define MG_RENDER_LANE_PX 4                      // pixels per lane per pass (one 16-B store)
+#define MG_RENDER_PASSES  4                      // passes per wave
+#define MG_RENDER_WAVES   4                      // waves per workgroup
+#define MG_RENDER_RUN (64 * MG_RENDER_LANE_PX * MG_RENDER_PASSES * MG_RENDER_WAVES)   // 4096 px
+struct MgRenderCam {
+    int   env, w, h, slot;         // slot: internal body slot followed, -1 fixed
+    int   follow, blk0, nblk, vec; // vec: 16-B stores allowed (W*H % 4 == 0 and aligned images)
+    float fx, fy, cx, cy, ifx, ify, near_plane, far_plane;
+    float p[3], q[4];
+    float pad;
+    unsigned char* color;
+    float* depth;
+    int* seg;
+};
+// render shape reference: one per shape of every body, grouped by env
+struct MgRShape {
+    int   slot;                    // internal body slot
+    int   shape;                   // shape record (MG_SHAPE_STRIDE floats)
+    int   seg;
+    float r, g, b;
+    int   pad[2];
+};
+struct MgRenderArgs {
+    int                 ncam, nb;
+    const MgRenderCam*  cams;
+    const float*        state;     // snapshot [13][nb]
+    const float*        shapes;
+    const MgRShape*     rshapes;
+    const int*          env_shape_first;   // [nenv + 1]
+    int                 has_ground;
+    float               gn[3], gpd;        // ground: dot(gn, x) + gpd = 0
+    float               up[3], left[3];    // camera-frame up / left axes (local)
+    int                 up_axis;           // 1: checker on (x, y); 0: on (x, z)
+    float               light[3];          // unit direction towards the light
+};
+
 // launchers (defined in the .hip files)
+hipError_t mg_launch_render(const MgRenderArgs& A, int nblocks, hipStream_t s);
 hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s);
 hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream_t s);
 hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream_t s);

@@ -1,0 +1,347 @@
+// mg_render.hip — camera sensors: gym.render_all_camera_sensors /
+// get_camera_image[_gpu_tensor] (config 5, test11_servo_vecenv_camerazoom.py:
+// 327-342,388,458-460; examples/interop_torch.py:105-120,173-174).
+//
+// Ray casting, not rasterisation: a camera sees one env's handful of convex
+// shapes (boxes, spheres, capsules) and the ground plane, so every pixel is a
+// loop over a short shape list held in LDS — no geometry pipeline, no depth
+// buffer, no atomics. The work is dominated by writing the images (5.76 MB per
+// 1600x900 RGBA camera), so the kernel is shaped as a streaming store:
+//   - a camera's pixels are cut into linear row-major runs of 4096; one
+//     workgroup (4 waves) owns one run and each lane shades 4 consecutive
+//     pixels per pass, so a wave stores 1 KB of color (+1 KB depth, +1 KB
+//     segmentation) contiguously with one 16-B store per lane per image;
+//   - the env's shapes are transformed to the world frame once per workgroup
+//     (one lane per shape) from the pose snapshot taken at
+//     render_all_camera_sensors, and shapes whose bounding sphere cannot
+//     project into the run's rows are culled for the primary rays (shadow rays
+//     still test every shape);
+//   - the camera record is read with uniform (scalar) loads.
+// Shading: Lambert + ambient on bodies, a 1 m checker ground,
+// hard shadows from one directional light, black sky; color quantised to RGBA8.
+// The C restatement is oracle/migym_oracle_render.c (same order of operations,
+// -ffp-contract=off on both sides: images agree bit for bit).
+#include "mg_internal.h"
+#include "mg_math.h"
+
+namespace {
+
+// world-frame shape of the camera's env, staged in LDS
+struct WS {
+    int   type, seg;
+    float r, g, b;
+    V3    c;        // centre
+    M3    R;        // columns: shape axes in the world
+    V3    h;        // box half extents; sphere (radius, 0, 0); capsule (radius, half length, 0)
+    float brad;     // bounding radius
+    float brad2;    // (padded bounding radius)^2 of the per-ray rejection tests
+};
+
+// Conservative per-ray rejection by the bounding sphere (cheap, no division):
+// true only if the half-line o + t d (t >= 0) cannot reach the shape. The
+// slack (padded radius, 1e-5 relative) exceeds the rounding of the test, so a
+// rejected shape is one the exact intersection would have missed as well and
+// the images stay bit-identical to the unculled restatement.
+__device__ __forceinline__ bool ray_misses_bound(V3 o, V3 d, float dd, const WS& s) {
+    const V3 oc = vsub(s.c, o);
+    const float sp = vdot(oc, d);
+    const float oc2 = vdot(oc, oc);
+    if (!(oc2 > s.brad2)) return false;
+    return sp < 0.0f || oc2 * dd - sp * sp > (s.brad2 + 1e-5f * oc2) * dd;
+}
+
+__device__ __forceinline__ float ray_sphere(V3 o, V3 d, V3 c, float r, float tmin) {
+    const V3 oc = vsub(o, c);
+    const float bb = vdot(oc, d);
+    const float cc = vdot(oc, oc) - r * r;
+    const float dd = vdot(d, d);
+    const float disc = bb * bb - dd * cc;
+    if (!(disc >= 0.0f)) return __builtin_inff();
+    const float t = (-bb - sqrtf(disc)) / dd;
+    return t >= tmin ? t : __builtin_inff();
+}
+
+__device__ __forceinline__ void slab(float o, float d, float h, float& tn, float& tf) {
+    const float inv = 1.0f / d;
+    const float t1 = (-h - o) * inv;
+    const float t2 = (h - o) * inv;
+    tn = fmaxf(tn, fminf(t1, t2));
+    tf = fminf(tf, fmaxf(t1, t2));
+}
+
+__device__ __forceinline__ float ray_box(V3 o, V3 d, const WS& s, float tmin, float tmax) {
+    const V3 ol = mtmul(s.R, vsub(o, s.c));
+    const V3 dl = mtmul(s.R, d);
+    // entry point only: a ray that starts inside the box (a camera mounted in
+    // its body's collision box) sees through it, as back faces are not drawn
+    float tn = -__builtin_inff(), tf = tmax;
+    slab(ol.x, dl.x, s.h.x, tn, tf);
+    slab(ol.y, dl.y, s.h.y, tn, tf);
+    slab(ol.z, dl.z, s.h.z, tn, tf);
+    return (tn <= tf && tn >= tmin) ? tn : __builtin_inff();
+}
+
+__device__ __forceinline__ float ray_capsule(V3 o, V3 d, const WS& s, float tmin) {
+    const float r = s.h.x, hl = s.h.y;
+    const V3 ax = s.R.c0;
+    const V3 pa = vsub(s.c, vscale(ax, hl));
+    const V3 ba = vscale(ax, 2.0f * hl);
+    const V3 oa = vsub(o, pa);
+    const float baba = vdot(ba, ba), bard = vdot(ba, d), baoa = vdot(ba, oa);
+    const float rdoa = vdot(d, oa), oaoa = vdot(oa, oa), dd = vdot(d, d);
+    const float a = baba * dd - bard * bard;
+    const float b = baba * rdoa - baoa * bard;
+    const float c = baba * oaoa - baoa * baoa - r * r * baba;
+    const float hh = b * b - a * c;
+    if (!(hh >= 0.0f)) return __builtin_inff();   // the infinite cylinder is missed
+    float t = __builtin_inff();
+    if (a > 0.0f) {
+        const float tb = (-b - sqrtf(hh)) / a;
+        const float y = baoa + tb * bard;
+        if (y > 0.0f && y < baba && tb >= tmin) t = tb;
+    }
+    const float t0 = ray_sphere(o, d, pa, r, tmin);
+    const float t1 = ray_sphere(o, d, vadd(pa, ba), r, tmin);
+    t = t0 < t ? t0 : t;
+    t = t1 < t ? t1 : t;
+    return t;
+}
+
+__device__ __forceinline__ float ray_shape(V3 o, V3 d, const WS& s, float tmin, float tmax) {
+    if (s.type == MG_SHAPE_BOX) return ray_box(o, d, s, tmin, tmax);
+    if (s.type == MG_SHAPE_SPHERE) return ray_sphere(o, d, s.c, s.h.x, tmin);
+    return ray_capsule(o, d, s, tmin);
+}
+
+__device__ __forceinline__ V3 shape_normal(const WS& s, V3 p) {
+    const V3 dp = vsub(p, s.c);
+    if (s.type == MG_SHAPE_SPHERE) return vscale(dp, 1.0f / s.h.x);
+    if (s.type == MG_SHAPE_BOX) {
+        const V3 pl = mtmul(s.R, dp);
+        const float qx = fabsf(pl.x) / s.h.x, qy = fabsf(pl.y) / s.h.y, qz = fabsf(pl.z) / s.h.z;
+        int k = 0;
+        float best = qx;
+        if (qy > best) { k = 1; best = qy; }
+        if (qz > best) k = 2;
+        const V3 axis = k == 0 ? s.R.c0 : (k == 1 ? s.R.c1 : s.R.c2);
+        const float sg = (k == 0 ? pl.x : (k == 1 ? pl.y : pl.z)) < 0.0f ? -1.0f : 1.0f;
+        return vscale(axis, sg);
+    }
+    float t = vdot(dp, s.R.c0);
+    t = fminf(fmaxf(t, -s.h.y), s.h.y);
+    return vscale(vsub(dp, vscale(s.R.c0, t)), 1.0f / s.h.x);
+}
+
+__device__ __forceinline__ unsigned q8(float x) {
+    return (unsigned)(fminf(fmaxf(x, 0.0f), 1.0f) * 255.0f + 0.5f);
+}
+
+struct Cam {
+    V3 o, f, l, u;
+    float cx, cy, ifx, ify, near_plane, far_plane;
+};
+
+// one pixel: nearest hit among ground + the culled shape list, shadow ray
+// against every shape, shading
+__device__ __forceinline__ void shade(const MgRenderArgs& A, const Cam& C, const WS* sws, const int* act, int nact,
+                                      int nall, int col, int row, unsigned& rgba, float& depth, int& seg) {
+    const float a = (C.cx - ((float)col + 0.5f)) * C.ifx;
+    const float b = (C.cy - ((float)row + 0.5f)) * C.ify;
+    const V3 d = vadd(vadd(C.f, vscale(C.l, a)), vscale(C.u, b));
+    const V3 gn = v3(A.gn[0], A.gn[1], A.gn[2]);
+    float best = C.far_plane;
+    int hit = -2;
+    if (A.has_ground) {
+        const float dn = vdot(gn, d);
+        if (dn < 0.0f) {
+            const float t = -(vdot(gn, C.o) + A.gpd) / dn;
+            if (t >= C.near_plane && t < best) { best = t; hit = -1; }
+        }
+    }
+    const float dd = vdot(d, d);
+    for (int j = 0; j < nact; ++j) {
+        const int s = act[j];
+        if (ray_misses_bound(C.o, d, dd, sws[s])) continue;
+        const float t = ray_shape(C.o, d, sws[s], C.near_plane, best);
+        if (t < best) { best = t; hit = s; }
+    }
+    if (hit == -2) {
+        rgba = 0xFF000000u;
+        depth = -__builtin_inff();
+        seg = 0;
+        return;
+    }
+    const V3 p = vadd(C.o, vscale(d, best));
+    const V3 n = hit >= 0 ? shape_normal(sws[hit], p) : gn;
+    const V3 L = v3(A.light[0], A.light[1], A.light[2]);
+    const V3 ps = vadd(p, vscale(n, 1e-3f));
+    bool shadow = false;
+    for (int j = 0; j < nall && !shadow; ++j)
+        shadow = !ray_misses_bound(ps, L, 1.0f, sws[j]) &&
+                 ray_shape(ps, L, sws[j], 0.0f, __builtin_inff()) < __builtin_inff();
+    float cr, cg, cb;
+    if (hit >= 0) {
+        const float lam = fmaxf(vdot(n, L), 0.0f);
+        const float k = shadow ? 0.3f : 0.3f + 0.7f * lam;
+        cr = sws[hit].r * k; cg = sws[hit].g * k; cb = sws[hit].b * k;
+        seg = sws[hit].seg;
+    } else {
+        const float uu = p.x, vv = A.up_axis == 1 ? p.y : p.z;
+        const int par = ((int)floorf(uu) + (int)floorf(vv)) & 1;
+        const float k = shadow ? 0.55f : 1.0f;
+        cr = (par ? 108.0f / 255.0f : 143.0f / 255.0f) * k;
+        cg = cr;
+        cb = (par ? 113.0f / 255.0f : 150.0f / 255.0f) * k;
+        seg = 0;
+    }
+    rgba = q8(cr) | (q8(cg) << 8) | (q8(cb) << 16) | 0xFF000000u;
+    depth = -best;
+}
+
+__global__ void __launch_bounds__(256) k_render(MgRenderArgs A) {
+    __shared__ WS sws[MG_RENDER_MAX_SHAPES];
+    __shared__ int act[MG_RENDER_MAX_SHAPES];
+    __shared__ int s_nact;
+
+    // camera of this workgroup (uniform binary search over the prefix blk0)
+    const int blk = blockIdx.x;
+    int lo = 0, hi = A.ncam - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (A.cams[mid].blk0 <= blk) lo = mid; else hi = mid - 1;
+    }
+    const MgRenderCam& K = A.cams[lo];
+    const int W = K.w, H = K.h;
+    const int npx = W * H;
+    const int px_begin = (blk - K.blk0) * MG_RENDER_RUN;
+    const int px_end = min(px_begin + MG_RENDER_RUN, npx);
+    const int nb = A.nb;
+    const float* S = A.state;
+
+    // camera pose (FOLLOW_TRANSFORM / FOLLOW_POSITION / fixed)
+    Cam C;
+    {
+        V3 o = v3(K.p[0], K.p[1], K.p[2]);
+        Q4 q = q4(K.q[0], K.q[1], K.q[2], K.q[3]);
+        if (K.slot >= 0) {
+            const int i = K.slot;
+            const V3 pb = v3(S[0 * nb + i], S[1 * nb + i], S[2 * nb + i]);
+            const Q4 qb = q4(S[3 * nb + i], S[4 * nb + i], S[5 * nb + i], S[6 * nb + i]);
+            if (K.follow == 1) {
+                o = vadd(pb, qrot(qb, o));
+                q = qmul(qb, q);
+            } else {
+                o = vadd(pb, o);
+            }
+        }
+        C.o = o;
+        C.f = qrot(q, v3(1.0f, 0.0f, 0.0f));
+        C.l = qrot(q, v3(A.left[0], A.left[1], A.left[2]));
+        C.u = qrot(q, v3(A.up[0], A.up[1], A.up[2]));
+        C.cx = K.cx; C.cy = K.cy; C.ifx = K.ifx; C.ify = K.ify;
+        C.near_plane = K.near_plane; C.far_plane = K.far_plane;
+    }
+
+    // the env's shapes in the world frame, one lane per shape
+    const int s0 = A.env_shape_first[K.env];
+    const int ns = A.env_shape_first[K.env + 1] - s0;
+    const int t = threadIdx.x;
+    if (t < 64) {
+        bool keep = false;
+        if (t < ns) {
+            const MgRShape rs = A.rshapes[s0 + t];
+            const int i = rs.slot;
+            const V3 pb = v3(S[0 * nb + i], S[1 * nb + i], S[2 * nb + i]);
+            const Q4 qb = q4(S[3 * nb + i], S[4 * nb + i], S[5 * nb + i], S[6 * nb + i]);
+            const float* sh = A.shapes + (size_t)rs.shape * MG_SHAPE_STRIDE;
+            WS w;
+            w.type = (int)sh[0];
+            w.seg = rs.seg;
+            w.r = rs.r; w.g = rs.g; w.b = rs.b;
+            w.c = vadd(pb, qrot(qb, v3(sh[4], sh[5], sh[6])));
+            w.R = qmat(qmul(qb, q4(sh[7], sh[8], sh[9], sh[10])));
+            if (w.type == MG_SHAPE_BOX) {
+                w.h = v3(sh[1], sh[2], sh[3]);
+                w.brad = sqrtf(vdot(w.h, w.h));
+            } else if (w.type == MG_SHAPE_SPHERE) {
+                w.h = v3(sh[1], 0.0f, 0.0f);
+                w.brad = sh[1];
+            } else {
+                w.h = v3(sh[1], sh[2], 0.0f);
+                w.brad = sh[1] + sh[2];
+            }
+            {
+                const float rp = w.brad * 1.01f + 1e-3f;
+                w.brad2 = rp * rp;
+            }
+            sws[t] = w;
+            // primary-ray culling: rows the bounding sphere can project to
+            const V3 dv = vsub(w.c, C.o);
+            const float z = vdot(dv, C.f), yu = vdot(dv, C.u), R = w.brad * 1.001f + 1e-4f;
+            // a camera strictly inside a box or sphere sees none of it (only
+            // entry points are hits and they all lie behind the near plane)
+            const V3 ol = mtmul(w.R, vsub(C.o, w.c));
+            const V3 os = vsub(C.o, w.c);
+            const bool inside =
+                C.near_plane > 0.0f &&
+                ((w.type == MG_SHAPE_BOX && fabsf(ol.x) < w.h.x && fabsf(ol.y) < w.h.y && fabsf(ol.z) < w.h.z) ||
+                 (w.type == MG_SHAPE_SPHERE && vdot(os, os) - w.h.x * w.h.x < 0.0f));
+            if (inside || z + R < C.near_plane) {
+                keep = false;
+            } else if (z - R <= 0.5f * C.near_plane) {
+                keep = true;
+            } else {
+                const float b_hi = fmaxf((yu + R) / (z - R), (yu + R) / (z + R));
+                const float b_lo = fminf((yu - R) / (z - R), (yu - R) / (z + R));
+                const float fy = 1.0f / C.ify;
+                const float r_top = C.cy - b_hi * fy - 2.0f;
+                const float r_bot = C.cy - b_lo * fy + 2.0f;
+                const int row0 = px_begin / W, row1 = (px_end - 1) / W;
+                keep = !(r_bot < (float)row0 || r_top > (float)(row1 + 1));
+            }
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) act[__popcll(m & ((1ull << t) - 1ull))] = t;
+        if (t == 0) s_nact = __popcll(m);
+    }
+    __syncthreads();
+    const int nact = s_nact;
+    const int nall = ns;
+
+    const int wave = t >> 6, lane = t & 63;
+#pragma unroll 1
+    for (int pass = 0; pass < MG_RENDER_PASSES; ++pass) {
+        const int px0 = px_begin + ((pass * MG_RENDER_WAVES + wave) * 64 + lane) * MG_RENDER_LANE_PX;
+        if (px0 >= px_end) continue;
+        int row = px0 / W;
+        int col = px0 - row * W;
+        unsigned rgba[MG_RENDER_LANE_PX];
+        float dep[MG_RENDER_LANE_PX];
+        int sg[MG_RENDER_LANE_PX];
+#pragma unroll
+        for (int k = 0; k < MG_RENDER_LANE_PX; ++k) {
+            rgba[k] = 0u; dep[k] = 0.0f; sg[k] = 0;
+            if (px0 + k < px_end) shade(A, C, sws, act, nact, nall, col, row, rgba[k], dep[k], sg[k]);
+            if (++col == W) { col = 0; ++row; }
+        }
+        if (K.vec && px0 + MG_RENDER_LANE_PX <= px_end) {
+            if (K.color) *(uint4*)(K.color + (size_t)px0 * 4) = make_uint4(rgba[0], rgba[1], rgba[2], rgba[3]);
+            if (K.depth) *(float4*)(K.depth + px0) = make_float4(dep[0], dep[1], dep[2], dep[3]);
+            if (K.seg) *(int4*)(K.seg + px0) = make_int4(sg[0], sg[1], sg[2], sg[3]);
+        } else {
+            for (int k = 0; k < MG_RENDER_LANE_PX && px0 + k < px_end; ++k) {
+                if (K.color) *(unsigned*)(K.color + (size_t)(px0 + k) * 4) = rgba[k];
+                if (K.depth) K.depth[px0 + k] = dep[k];
+                if (K.seg) K.seg[px0 + k] = sg[k];
+            }
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t mg_launch_render(const MgRenderArgs& A, int nblocks, hipStream_t s) {
+    if (nblocks <= 0 || A.ncam <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_render, dim3(nblocks), dim3(256), 0, s, A);
+    return hipGetLastError();
+}

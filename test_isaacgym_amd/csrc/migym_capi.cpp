@@ -113,6 +113,23 @@ struct mg_sim {
     int* d_stage_idx = nullptr;
     size_t stage_idx_n = 0;
 
+    // host copies kept for the camera renderer's shape lists
+    std::vector<int> h_perm, h_body_tmpl, h_tbi;
+    // camera render (mg_render.hip)
+    float* d_rstate = nullptr;    // [13][nb] pose snapshot of render_all_camera_sensors
+    bool rstate_valid = false;
+    MgRShape* d_rshapes = nullptr;
+    int* d_env_shape_first = nullptr;
+    int n_rshapes = 0;
+    bool render_ready = false;
+    MgRenderCam* d_cams = nullptr;
+    int cam_cap = 0;
+    std::vector<mg_camera> cam_host;      // last uploaded table (as given)
+    std::vector<MgRenderCam> cam_dev;     // its device form
+    int cam_blocks = 0;
+    hipEvent_t rev_b = nullptr, rev_e = nullptr;
+    bool rendered = false;
+
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
     bool stepped = false;
     bool capturing = false;       // the last simulate was recorded into a graph
@@ -233,7 +250,8 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_tbi, s->d_shapes,
                     s->d_actor_root, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
-                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx};
+                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
+                    s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -279,6 +297,8 @@ void mg_destroy_sim(mg_sim* s) {
         if (s->ring_b[k]) (void)hipEventDestroy(s->ring_b[k]);
         if (s->ring_e[k]) (void)hipEventDestroy(s->ring_e[k]);
     }
+    if (s->rev_b) (void)hipEventDestroy(s->rev_b);
+    if (s->rev_e) (void)hipEventDestroy(s->rev_e);
     delete s;
 }
 
@@ -636,6 +656,9 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(h2d(s->d_link_f, m->tmpl_link_f, (size_t)s->ntl * MG_LINK_F_N * sizeof(float)));
     HIP_TRY(h2d(s->d_link_i, m->tmpl_link_i, (size_t)s->ntl * MG_LINK_I_N * sizeof(int)));
     HIP_TRY(hipDeviceSynchronize());
+    s->h_perm = perm;
+    s->h_body_tmpl.assign(m->body_tmpl, m->body_tmpl + nb);
+    s->h_tbi.assign(m->tmpl_body_i, m->tmpl_body_i + (size_t)s->ntb * MG_TBODY_I_N);
     s->uploaded = true;
     return MG_OK;
 }
@@ -902,6 +925,157 @@ int32_t mg_refresh_mass_matrix(mg_sim* s, int32_t tmpl, float* dst, int32_t dst_
 int32_t mg_refresh_jacobian_mass_matrix(mg_sim* s, int32_t tmpl, float* jac, float* mm, int32_t dst_host,
                                         void* stream) {
     return refresh_jac_mm(s, tmpl, jac, mm, dst_host, stream);
+}
+
+
+// ---- camera sensors ---------------------------------------------------------
+
+int32_t mg_set_render_bodies(mg_sim* s, const int32_t* env_body_first, const float* color, const int32_t* seg) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (!env_body_first || !color || !seg) return fail(MG_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(s->device));
+    const int ne = s->nenv;
+    if (env_body_first[0] != 0 || env_body_first[ne] != s->nb) return fail(MG_ERR_ARG, "env_body_first must span [0, num_bodies]");
+    std::vector<MgRShape> rs;
+    std::vector<int> first(ne + 1, 0);
+    for (int e = 0; e < ne; ++e) {
+        first[e] = (int)rs.size();
+        if (env_body_first[e + 1] < env_body_first[e]) return fail(MG_ERR_ARG, "env_body_first not monotone");
+        for (int b = env_body_first[e]; b < env_body_first[e + 1]; ++b) {
+            const int t = s->h_body_tmpl[b];
+            const int sh0 = s->h_tbi[(size_t)t * MG_TBODY_I_N + 0], nsh = s->h_tbi[(size_t)t * MG_TBODY_I_N + 1];
+            for (int k = 0; k < nsh; ++k) {
+                MgRShape r{};
+                r.slot = s->h_perm[b];
+                r.shape = sh0 + k;
+                r.seg = seg[b];
+                r.r = color[3 * (size_t)b + 0]; r.g = color[3 * (size_t)b + 1]; r.b = color[3 * (size_t)b + 2];
+                rs.push_back(r);
+            }
+        }
+        if ((int)rs.size() - first[e] > MG_RENDER_MAX_SHAPES)
+            return fail(MG_ERR_UNSUPPORTED, "env %d has %d shapes; a camera's env may hold at most %d", e,
+                        (int)rs.size() - first[e], MG_RENDER_MAX_SHAPES);
+    }
+    first[ne] = (int)rs.size();
+    if (s->d_rshapes) (void)hipFree(s->d_rshapes);
+    if (s->d_env_shape_first) (void)hipFree(s->d_env_shape_first);
+    s->d_rshapes = nullptr; s->d_env_shape_first = nullptr;
+    HIP_TRY(dalloc(&s->d_rshapes, rs.size()));
+    HIP_TRY(dalloc(&s->d_env_shape_first, (size_t)ne + 1));
+    if (!rs.empty()) HIP_TRY(hipMemcpy(s->d_rshapes, rs.data(), rs.size() * sizeof(MgRShape), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->d_env_shape_first, first.data(), first.size() * sizeof(int), hipMemcpyHostToDevice));
+    s->n_rshapes = (int)rs.size();
+    s->render_ready = true;
+    return MG_OK;
+}
+
+int32_t mg_snapshot_render_state(mg_sim* s, void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    HIP_TRY(hipSetDevice(s->device));
+    if (!s->d_rstate) HIP_TRY(dalloc(&s->d_rstate, (size_t)s->nb * MG_STATE_N));
+    HIP_TRY(hipMemcpyAsync(s->d_rstate, s->d_state, (size_t)s->nb * MG_STATE_N * sizeof(float),
+                           hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    s->rstate_valid = true;
+    return MG_OK;
+}
+
+int32_t mg_render_cameras(mg_sim* s, const mg_camera* cams, int32_t n, void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (!s->render_ready) return fail(MG_ERR_STATE, "mg_set_render_bodies was not called");
+    if (!s->rstate_valid) return fail(MG_ERR_STATE, "no render snapshot (mg_snapshot_render_state)");
+    if (n < 0 || (n > 0 && !cams)) return fail(MG_ERR_ARG, "bad camera list");
+    if (n == 0) return MG_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)stream;
+    const bool same = (int)s->cam_host.size() == n &&
+                      std::memcmp(s->cam_host.data(), cams, (size_t)n * sizeof(mg_camera)) == 0;
+    if (!same) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing(st, &cap));
+        if (cap != hipStreamCaptureStatusNone)
+            return fail(MG_ERR_STATE, "camera table changed while the stream is being captured");
+        std::vector<MgRenderCam> dev((size_t)n);
+        long long blocks = 0;
+        for (int i = 0; i < n; ++i) {
+            const mg_camera& c = cams[i];
+            if (c.env < 0 || c.env >= s->nenv) return fail(MG_ERR_ARG, "camera %d: env %d out of range", i, c.env);
+            if (c.width <= 0 || c.height <= 0 || (long long)c.width * c.height > (1ll << 30))
+                return fail(MG_ERR_ARG, "camera %d: bad size %dx%d", i, c.width, c.height);
+            if (c.body >= s->nb) return fail(MG_ERR_ARG, "camera %d: body %d out of range", i, c.body);
+            if (!(c.fx > 0.0f) || !(c.fy > 0.0f)) return fail(MG_ERR_ARG, "camera %d: bad focal length", i);
+            MgRenderCam& d = dev[i];
+            d.env = c.env; d.w = c.width; d.h = c.height;
+            d.slot = c.body >= 0 ? s->h_perm[c.body] : -1;
+            d.follow = c.follow;
+            d.blk0 = (int)blocks;
+            const long long npx = (long long)c.width * c.height;
+            d.nblk = (int)((npx + MG_RENDER_RUN - 1) / MG_RENDER_RUN);
+            blocks += d.nblk;
+            const auto al16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+            d.vec = (npx % MG_RENDER_LANE_PX == 0) && al16(c.color) && al16(c.depth) && al16(c.seg);
+            d.fx = c.fx; d.fy = c.fy; d.cx = c.cx; d.cy = c.cy;
+            d.ifx = 1.0f / c.fx; d.ify = 1.0f / c.fy;
+            d.near_plane = c.near_plane; d.far_plane = c.far_plane;
+            for (int k = 0; k < 3; ++k) d.p[k] = c.p[k];
+            for (int k = 0; k < 4; ++k) d.q[k] = c.q[k];
+            d.color = c.color; d.depth = c.depth; d.seg = c.seg;
+        }
+        if (blocks > (1ll << 31) - 1) return fail(MG_ERR_ARG, "too many pixels in one render call");
+        if (n > s->cam_cap) {
+            if (s->d_cams) (void)hipFree(s->d_cams);
+            s->d_cams = nullptr;
+            HIP_TRY(dalloc(&s->d_cams, (size_t)n));
+            s->cam_cap = n;
+        }
+        HIP_TRY(hipMemcpy(s->d_cams, dev.data(), (size_t)n * sizeof(MgRenderCam), hipMemcpyHostToDevice));
+        s->cam_host.assign(cams, cams + n);
+        s->cam_dev = dev;
+        s->cam_blocks = (int)blocks;
+    }
+    MgRenderArgs A{};
+    A.ncam = n; A.nb = s->nb; A.cams = s->d_cams; A.state = s->d_rstate; A.shapes = s->d_shapes;
+    A.rshapes = s->d_rshapes; A.env_shape_first = s->d_env_shape_first;
+    const mg_sim_params& p = s->params;
+    A.has_ground = p.has_ground;
+    for (int k = 0; k < 3; ++k) A.gn[k] = p.ground_normal[k];
+    A.gpd = p.ground_distance;
+    // camera frame: forward +x, up = the sim's up axis, left = up x forward;
+    // light from above, a little off the up axis
+    A.up_axis = p.up_axis == 0 ? 0 : 1;
+    float lx = 0.3f, ly = 0.2f, lz = 1.0f;
+    if (A.up_axis == 1) {
+        A.up[0] = 0.0f; A.up[1] = 0.0f; A.up[2] = 1.0f;
+        A.left[0] = 0.0f; A.left[1] = 1.0f; A.left[2] = 0.0f;
+    } else {
+        A.up[0] = 0.0f; A.up[1] = 1.0f; A.up[2] = 0.0f;
+        A.left[0] = 0.0f; A.left[1] = 0.0f; A.left[2] = -1.0f;
+        ly = 1.0f; lz = 0.2f;
+    }
+    const float inv = 1.0f / sqrtf(lx * lx + ly * ly + lz * lz);
+    A.light[0] = lx * inv; A.light[1] = ly * inv; A.light[2] = lz * inv;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(st, &cap));
+    const bool timed = cap == hipStreamCaptureStatusNone;
+    if (timed) {
+        if (!s->rev_b) HIP_TRY(hipEventCreate(&s->rev_b));
+        if (!s->rev_e) HIP_TRY(hipEventCreate(&s->rev_e));
+        HIP_TRY(hipEventRecord(s->rev_b, st));
+    }
+    HIP_TRY(mg_launch_render(A, s->cam_blocks, st));
+    if (timed) {
+        HIP_TRY(hipEventRecord(s->rev_e, st));
+        s->rendered = true;
+    }
+    return MG_OK;
+}
+
+float mg_last_render_ms(mg_sim* s) {
+    if (!s || !s->rendered) return -1.0f;
+    if (hipEventSynchronize(s->rev_e) != hipSuccess) return -1.0f;
+    float ms = -1.0f;
+    if (hipEventElapsedTime(&ms, s->rev_b, s->rev_e) != hipSuccess) return -1.0f;
+    return ms;
 }
 
 }  // extern "C"

@@ -20,6 +20,7 @@ import torch
 
 from . import _assets
 from . import _native as N
+from . import _render
 from ._sim import Actor, CameraSensor, Env, Sim, Viewer
 from ._types import *  # noqa: F401,F403
 from ._types import (_DOF_TYPE_STRINGS, _JOINT_TYPE_STRINGS, DOF_PROPERTIES_DTYPE, DofState, Quat,
@@ -663,13 +664,15 @@ class Gym:
         return True
 
     def set_rigid_body_color(self, env, handle, body_index, mesh_type, color):
-        self._actor(env, handle).body_colors[body_index] = color
+        self._actor(env, handle).body_colors[body_index] = Vec3(color.x, color.y, color.z)
+        env.sim.render_version += 1
 
     def get_rigid_body_color(self, env, handle, body_index, mesh_type):
         return self._actor(env, handle).body_colors.get(body_index, Vec3(1, 1, 1))
 
     def set_rigid_body_segmentation_id(self, env, handle, body_index, seg):
-        pass
+        self._actor(env, handle).body_segs[body_index] = int(seg)
+        env.sim.render_version += 1
 
     def set_rigid_body_texture(self, env, handle, body_index, mesh_type, tex):
         pass
@@ -939,35 +942,49 @@ class Gym:
     def draw_env_rigid_contacts(self, viewer, env, color, scale, flag):
         pass
 
-    # ================================================================ cameras (headless)
+    # ================================================================ cameras (device ray caster)
     def create_camera_sensor(self, env, props):
         """Per-env 0-based handles (test11's aliased list needs that)."""
-        cam = CameraSensor(env, props, len(env.cameras))
+        p = _T.CameraProperties()
+        p.__dict__.update(props.__dict__)          # test11 mutates its props between cameras (:327-329)
+        cam = CameraSensor(env, p, len(env.cameras))
         env.cameras.append(cam)
+        env.sim.cam_version += 1
         return cam.handle
 
     def destroy_camera_sensor(self, sim, env, handle):
         pass
 
     def set_camera_location(self, handle, env, pos, target):
+        """examples/interop_torch.py:111: env-frame position looking at target."""
         cam = env.cameras[handle]
-        cam.transform = _look_at(pos, target)
+        cam.body = None
+        cam.transform = _render.look_at(pos, target, env.sim.params.up_axis)
+        env.sim.cam_version += 1
 
     def set_camera_transform(self, handle, env, transform):
-        env.cameras[handle].transform = Transform(transform.p, transform.r)
+        cam = env.cameras[handle]
+        cam.body = None
+        cam.transform = Transform(transform.p, transform.r)
+        env.sim.cam_version += 1
 
     def attach_camera_to_body(self, handle, env, body_handle, local_transform, follow_mode):
+        """test11_servo_vecenv_camerazoom.py:333-336 (FOLLOW_TRANSFORM)."""
         cam = env.cameras[handle]
         cam.body = body_handle
         cam.local = Transform(local_transform.p, local_transform.r)
         cam.follow = follow_mode
+        env.sim.cam_version += 1
 
     def get_camera_transform(self, sim, env, handle):
         cam = env.cameras[handle]
         if cam.body is None:
             o = env.origin
             return Transform(Vec3(o[0], o[1], o[2]), Quat()) * cam.transform
-        return self.get_rigid_transform(env, cam.body) * cam.local
+        b = self.get_rigid_transform(env, cam.body)
+        if cam.follow == _T.FOLLOW_POSITION:
+            return Transform(b.p + cam.local.p, cam.local.r)
+        return b * cam.local
 
     def get_camera_view_matrix(self, sim, env, handle):
         t = self.get_camera_transform(sim, env, handle)
@@ -982,7 +999,7 @@ class Gym:
         p = env.cameras[handle].props
         fx = 1.0 / math.tan(math.radians(p.horizontal_fov) * 0.5)
         fy = fx * p.width / p.height
-        n, f = p.near_plane, p.far_plane
+        n = p.near_plane
         m = np.zeros((4, 4), dtype=np.float32)
         m[0, 0], m[1, 1] = fx, fy
         m[2, 2] = 0.0
@@ -994,7 +1011,9 @@ class Gym:
         pass
 
     def render_all_camera_sensors(self, sim):
-        pass
+        """test11_servo_vecenv_camerazoom.py:388: freezes the poses the cameras
+        see and renders every camera that has a GPU image tensor (one launch)."""
+        return sim.renderer.render_all()
 
     def start_access_image_tensors(self, sim):
         pass
@@ -1003,18 +1022,20 @@ class Gym:
         pass
 
     def get_camera_image(self, sim, env, handle, image_type):
-        p = env.cameras[handle].props
-        if image_type == _T.IMAGE_COLOR:
-            return np.zeros((p.height, p.width * 4), dtype=np.uint8)
-        if image_type == _T.IMAGE_SEGMENTATION:
-            return np.zeros((p.height, p.width), dtype=np.int32)
-        return np.zeros((p.height, p.width), dtype=np.float32)
+        """test11_servo_vecenv_camerazoom.py:459: host image of the last render
+        (color (H, W*4) uint8, depth (H, W) float32, segmentation (H, W) int32)."""
+        if image_type not in _render.IMAGE_KINDS:
+            p = env.cameras[handle].props
+            return np.zeros((p.height, p.width), dtype=np.float32)
+        return sim.renderer.image(env.cameras[handle], image_type)
 
     def get_camera_image_gpu_tensor(self, sim, env, handle, image_type):
-        p = env.cameras[handle].props
-        shape = (p.height, p.width, 4) if image_type == _T.IMAGE_COLOR else (p.height, p.width)
-        dtype = torch.uint8 if image_type == _T.IMAGE_COLOR else torch.float32
-        return Tensor(torch.zeros(shape, dtype=dtype, device=sim.device))
+        """examples/interop_torch.py:116: the camera's persistent device image,
+        updated by every render_all_camera_sensors."""
+        cam = env.cameras[handle]
+        if image_type not in _render.IMAGE_KINDS:
+            raise ValueError("image type %r is not rendered" % (image_type,))
+        return Tensor(_render.image_tensor(sim, cam, image_type))
 
     def write_camera_image_to_file(self, sim, env, handle, image_type, filename):
         return True
@@ -1026,13 +1047,6 @@ class Gym:
 def sim_num(sim, what):
     sim.finalize()
     return {"actors": sim.num_actors, "bodies": sim.num_bodies, "dofs": sim.num_dofs}[what]
-
-
-def _look_at(pos, target):
-    f = (target - pos).normalize()
-    yaw = math.atan2(f.y, f.x)
-    pitch = -math.asin(max(-1.0, min(1.0, f.z)))
-    return Transform(pos, Quat.from_euler_zyx(0.0, pitch, yaw))
 
 
 def _copy_shape(sp):

@@ -8,6 +8,13 @@ reference scripts build them:
   S2 gimbal  — test12_add_joint.py.py:23-34 (gravity 0, TGS 4/1, 2 substeps),
                :72-88 (fixed base at (0, 2, 3), DOF_MODE_POS), stiffness 50 /
                damping 5 (test13_camera_spherical_joint.py:200-203), filter=1.
+  S5 cameras — test11_servo_vecenv_camerazoom.py:274-336: the S1 scene plus one
+               camera per env on the UAV (local (5, 0, 0), FOLLOW_TRANSFORM),
+               1600x900, horizontal FOV 30 degrees, as a GPU image tensor.
+  interop    — examples/interop_torch.py:30-120 (y-up, a 0.5 m ball dropped
+               from y = 5 per env, 128x128 camera at (5, 1, 0) looking at
+               (0, 1, 0)): the scene of the reference's rendered fixture
+               examples/interop_images/.
 
 and the synthetic random actions of SURVEY.md §8d (seeded torch generators).
 """
@@ -115,6 +122,67 @@ def gimbal_scene(gym, num_envs, use_gpu_pipeline=True, device=0, stiffness=50.0,
         props["damping"][:] = damping
         gym.set_actor_dof_properties(env, h, props)
     return sim, envs
+
+
+def attach_servo_cameras(gym, sim, envs, width=1600, height=900, fov=30.0, image_types=None):
+    """One camera per env on the UAV body (test11_servo_vecenv_camerazoom.py:
+    274-280,327-336: local (5, 0, 0), FOLLOW_TRANSFORM), each with a GPU image
+    tensor per requested type. Returns the list of tensors per env."""
+    from . import gymtorch
+    props = gymapi.CameraProperties()
+    props.width, props.height = width, height
+    props.horizontal_fov = fov
+    props.enable_tensors = True
+    out = []
+    for env in envs:
+        cam = gym.create_camera_sensor(env, props)
+        uav = gym.get_actor_handle(env, 0)
+        body = gym.get_actor_rigid_body_handle(env, uav, 0)
+        local = gymapi.Transform()
+        local.p = gymapi.Vec3(5, 0, 0)
+        local.r = gymapi.Quat.from_euler_zyx(0, 0, 0)
+        gym.attach_camera_to_body(cam, env, body, local, gymapi.FOLLOW_TRANSFORM)
+        out.append([gymtorch.wrap_tensor(gym.get_camera_image_gpu_tensor(sim, env, cam, t))
+                    for t in (image_types or (gymapi.IMAGE_COLOR,))])
+    return out
+
+
+def interop_scene(gym, num_envs=16, device=0, colors=None):
+    """examples/interop_torch.py:30-120: returns (sim, envs, cams)."""
+    sp = gymapi.SimParams()
+    sp.gravity = gymapi.Vec3(0.0, -9.8, 0.0)
+    sp.physx.solver_type = 1
+    sp.physx.num_position_iterations = 4
+    sp.physx.num_velocity_iterations = 1
+    sp.use_gpu_pipeline = True
+    sim = gym.create_sim(device, device, gymapi.SIM_PHYSX, sp)
+    ball = gym.create_sphere(sim, 0.5, None)
+    gym.add_ground(sim, gymapi.PlaneParams())
+    per_row = int(math.sqrt(num_envs))
+    spacing = 2.0
+    lower = gymapi.Vec3(-spacing, 0.0, -spacing)
+    upper = gymapi.Vec3(spacing, spacing, spacing)
+    envs, cams = [], []
+    for i in range(num_envs):
+        env = gym.create_env(sim, lower, upper, per_row)
+        envs.append(env)
+        pose = gymapi.Transform()
+        pose.p = gymapi.Vec3(0.0, 5.0, 0.0)
+        pose.r = gymapi.Quat(0.0, 0.0, 0.0, 1.0)
+        h = gym.create_actor(env, ball, pose, "ball", i, 0)
+        props = gym.get_actor_rigid_shape_properties(env, h)
+        props[0].restitution = 0.9
+        gym.set_actor_rigid_shape_properties(env, h, props)
+        c = colors[i] if colors is not None else (0.75, 0.75, 0.75)
+        gym.set_rigid_body_color(env, h, 0, gymapi.MESH_VISUAL_AND_COLLISION, gymapi.Vec3(*c))
+        cp = gymapi.CameraProperties()
+        cp.width = 128
+        cp.height = 128
+        cp.enable_tensors = True
+        cam = gym.create_camera_sensor(env, cp)
+        gym.set_camera_location(cam, env, gymapi.Vec3(5, 1, 0), gymapi.Vec3(0, 1, 0))
+        cams.append(cam)
+    return sim, envs, cams
 
 
 # ------------------------------------------------------------- random actions
