@@ -17,8 +17,9 @@ all-gather of the root-state observation.
 Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel
 (k_rigid_step, one launch per simulate) at SURVEY.md §8d's algorithmic bytes:
 376 B per env per simulate (2 bodies x (state in 52 + state out 52 + mass
-properties 44 + shape 40)), over its average duration measured with HIP events
-recorded on the simulate stream around every launch of the timed region.
+properties 44 + shape 40)), over its average duration taken from the kernel's own
+dispatch timestamps (hipExtLaunchKernelGGL start / stop events on the simulate
+stream; the interval rocprofv3 reports).
 `cpu_baseline` times the C restatement (oracle/, single thread, "port") on a
 bounded sample of the same workload.
 """
@@ -451,7 +452,8 @@ def main():
                 "kernel_ms_avg": kern_ms,
                 "kernel_ms_min": lo.value if used > 0 else None,
                 "kernel_launches_timed": int(used),
-                "kernel_timing": "HIP events around each simulate() of the eager %s" % (
+                "kernel_timing": "dispatch timestamps of k_rigid_step (hipExtLaunchKernelGGL start/stop events, "
+                                 "the interval rocprofv3 reports) for every simulate() of the eager %s" % (
                     "segment after the warmup (graph replays carry no events)" if graphs is not None
                     else "timed loop"),
                 "note": "working set of 4096 envs (~2.8 MB) sits in L2/MALL: the step is launch/latency "

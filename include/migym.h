@@ -258,9 +258,11 @@ float       mg_last_render_ms(mg_sim* sim);
 /* Duration in ms of the last simulate()'s kernels (HIP events on `stream`),
  * -1 when unavailable. Synchronises on the step's end event. */
 float       mg_last_step_ms(mg_sim* sim);
-/* Average / min / max duration in ms of the step kernels of the last n
- * simulate() calls (a ring of HIP event pairs recorded on the simulate stream
- * around the kernel launches; at most 512). Returns the count used, or < 0. */
+/* Average / min / max over the last n simulate() calls (at most 256; eager
+ * calls only, not graph replays) of the summed duration in ms of that step's
+ * kernels, each taken from its own dispatch timestamps (hipExtLaunchKernelGGL
+ * start / stop events, the interval rocprofv3 reports for the kernel). Returns
+ * the count used, or < 0. */
 int32_t     mg_step_time_stats(mg_sim* sim, int32_t n, float* avg_ms, float* min_ms, float* max_ms);
 /* Number of bodies advanced by the free-body kernel / articulations by the
  * articulation kernel in one simulate. */

@@ -713,11 +713,11 @@ hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream
     if (!A.fixed_base) return hipErrorNotSupported;
     const int blocks = (A.na + 63) / 64;
     if (A.nl <= 4)
-        hipLaunchKernelGGL(k_artic_world<4>, dim3(blocks), dim3(64), 0, s, P, A);
+        MG_LAUNCH(k_artic_world<4>, dim3(blocks), dim3(64), 0, s, P, A);
     else if (A.nl <= 8)
-        hipLaunchKernelGGL(k_artic_step<8>, dim3(blocks), dim3(64), 0, s, P, A);
+        MG_LAUNCH(k_artic_step<8>, dim3(blocks), dim3(64), 0, s, P, A);
     else if (A.nl <= MG_MAX_LINKS)
-        hipLaunchKernelGGL(k_artic_step<MG_MAX_LINKS>, dim3(blocks), dim3(64), 0, s, P, A);
+        MG_LAUNCH(k_artic_step<MG_MAX_LINKS>, dim3(blocks), dim3(64), 0, s, P, A);
     else
         return hipErrorNotSupported;
     return hipGetLastError();

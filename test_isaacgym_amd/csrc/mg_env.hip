@@ -1018,9 +1018,9 @@ hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s
     if (A.ne <= 0) return hipSuccess;
     const int blocks = (A.ne + EPW - 1) / EPW;
     if (A.nl <= 4 && A.ndof <= 4)
-        hipLaunchKernelGGL((k_env_step<4>), dim3(blocks), dim3(64), 0, s, P, A);
+        MG_LAUNCH((k_env_step<4>), dim3(blocks), dim3(64), 0, s, P, A);
     else if (A.nl <= MG_MAX_LINKS && A.ndof <= G)
-        hipLaunchKernelGGL((k_env_step<MG_MAX_LINKS>), dim3(blocks), dim3(64), 0, s, P, A);
+        MG_LAUNCH((k_env_step<MG_MAX_LINKS>), dim3(blocks), dim3(64), 0, s, P, A);
     else
         return hipErrorNotSupported;
     return hipGetLastError();

@@ -6,6 +6,7 @@
 // oracle/migym_oracle.c (compiled the same way) reproduces it bit for bit.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include "../../include/migym.h"
 
@@ -154,6 +155,29 @@ struct MgRenderArgs {
     int                 up_axis;           // 1: checker on (x, y); 0: on (x, z)
     float               light[3];          // unit direction towards the light
 };
+
+// Kernel timing by dispatch timestamps: while mg_timer is set (by mg_simulate,
+// outside stream capture) every step kernel is launched with
+// hipExtLaunchKernelGGL and a (start, stop) event pair from the timer, whose
+// elapsed time is the kernel's own duration (the same begin / end the
+// profiler reports), not the launch overhead around it.
+struct MgKernelTimer {
+    hipEvent_t* start;
+    hipEvent_t* stop;
+    int cap, used;
+};
+extern thread_local MgKernelTimer* mg_timer;
+#define MG_LAUNCH(kernel, grid, block, shmem, stream, ...)                                               \
+    do {                                                                                                \
+        MgKernelTimer* t_ = mg_timer;                                                                   \
+        if (t_ && t_->used < t_->cap) {                                                                 \
+            hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, t_->start[t_->used],                \
+                                  t_->stop[t_->used], 0, __VA_ARGS__);                                  \
+            t_->used++;                                                                                 \
+        } else {                                                                                        \
+            hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                        \
+        }                                                                                               \
+    } while (0)
 
 // launchers (defined in the .hip files)
 hipError_t mg_launch_render(const MgRenderArgs& A, int nblocks, hipStream_t s);

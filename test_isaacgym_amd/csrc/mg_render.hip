@@ -342,6 +342,6 @@ __global__ void __launch_bounds__(256) k_render(MgRenderArgs A) {
 
 hipError_t mg_launch_render(const MgRenderArgs& A, int nblocks, hipStream_t s) {
     if (nblocks <= 0 || A.ncam <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_render, dim3(nblocks), dim3(256), 0, s, A);
+    MG_LAUNCH(k_render, dim3(nblocks), dim3(256), 0, s, A);
     return hipGetLastError();
 }

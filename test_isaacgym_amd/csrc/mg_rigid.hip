@@ -403,13 +403,13 @@ hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream
     }
     if (A1.nf > 0) {
         const int blocks = (A1.nf + 63) / 64;
-        if (upz) hipLaunchKernelGGL((k_rigid_step<true, 4, false>), dim3(blocks), dim3(64), 0, s, P, A1);
-        else hipLaunchKernelGGL((k_rigid_step<false, 4, false>), dim3(blocks), dim3(64), 0, s, P, A1);
+        if (upz) MG_LAUNCH((k_rigid_step<true, 4, false>), dim3(blocks), dim3(64), 0, s, P, A1);
+        else MG_LAUNCH((k_rigid_step<false, 4, false>), dim3(blocks), dim3(64), 0, s, P, A1);
     }
     if (A2.nf > 0) {
         const int blocks = (A2.nf + 63) / 64;
-        if (upz) hipLaunchKernelGGL((k_rigid_step<true, MG_MAX_CONTACTS, true>), dim3(blocks), dim3(64), 0, s, P, A2);
-        else hipLaunchKernelGGL((k_rigid_step<false, MG_MAX_CONTACTS, true>), dim3(blocks), dim3(64), 0, s, P, A2);
+        if (upz) MG_LAUNCH((k_rigid_step<true, MG_MAX_CONTACTS, true>), dim3(blocks), dim3(64), 0, s, P, A2);
+        else MG_LAUNCH((k_rigid_step<false, MG_MAX_CONTACTS, true>), dim3(blocks), dim3(64), 0, s, P, A2);
     }
     return hipGetLastError();
 }

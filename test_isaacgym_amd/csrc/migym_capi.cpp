@@ -15,6 +15,8 @@
 
 #include "mg_internal.h"
 
+thread_local MgKernelTimer* mg_timer = nullptr;
+
 namespace {
 
 thread_local std::string g_err;
@@ -134,8 +136,11 @@ struct mg_sim {
     bool stepped = false;
     bool capturing = false;       // the last simulate was recorded into a graph
     // ring of per-simulate event pairs for live kernel timing (bench.py roofline)
-    static constexpr int kRing = 512;
+    static constexpr int kRing = 256;
+    static constexpr int kKern = 4;   // kernels timed per simulate (dispatch timestamps)
     hipEvent_t ring_b[kRing] = {}, ring_e[kRing] = {};
+    hipEvent_t kern_b[kRing][kKern] = {}, kern_e[kRing][kKern] = {};
+    int kern_n[kRing] = {};
     long long ring_n = 0;
 };
 
@@ -279,7 +284,10 @@ mg_sim* mg_create_sim(int32_t device, const mg_sim_params* params) {
     s->device = device;
     s->params = *params;
     for (int k = 0; k < mg_sim::kRing; ++k) {
-        if (hipEventCreate(&s->ring_b[k]) != hipSuccess || hipEventCreate(&s->ring_e[k]) != hipSuccess) {
+        bool ok = hipEventCreate(&s->ring_b[k]) == hipSuccess && hipEventCreate(&s->ring_e[k]) == hipSuccess;
+        for (int j = 0; j < mg_sim::kKern && ok; ++j)
+            ok = hipEventCreate(&s->kern_b[k][j]) == hipSuccess && hipEventCreate(&s->kern_e[k][j]) == hipSuccess;
+        if (!ok) {
             fail(MG_ERR_DEVICE, "hipEventCreate failed");
             mg_destroy_sim(s);
             return nullptr;
@@ -296,6 +304,10 @@ void mg_destroy_sim(mg_sim* s) {
     for (int k = 0; k < mg_sim::kRing; ++k) {
         if (s->ring_b[k]) (void)hipEventDestroy(s->ring_b[k]);
         if (s->ring_e[k]) (void)hipEventDestroy(s->ring_e[k]);
+        for (int j = 0; j < mg_sim::kKern; ++j) {
+            if (s->kern_b[k][j]) (void)hipEventDestroy(s->kern_b[k][j]);
+            if (s->kern_e[k][j]) (void)hipEventDestroy(s->kern_e[k][j]);
+        }
     }
     if (s->rev_b) (void)hipEventDestroy(s->rev_b);
     if (s->rev_e) (void)hipEventDestroy(s->rev_e);
@@ -674,11 +686,20 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(st, &cap));
     s->capturing = cap != hipStreamCaptureStatusNone;
+    MgKernelTimer timer{};
+    struct TimerScope {
+        ~TimerScope() { mg_timer = nullptr; }
+    } timer_scope;
+    int slot = 0;
     if (!s->capturing) {
-        const int slot = (int)(s->ring_n % mg_sim::kRing);
+        slot = (int)(s->ring_n % mg_sim::kRing);
         s->ev_begin = s->ring_b[slot];
         s->ev_end = s->ring_e[slot];
         HIP_TRY(hipEventRecord(s->ev_begin, st));
+        timer.start = s->kern_b[slot];
+        timer.stop = s->kern_e[slot];
+        timer.cap = mg_sim::kKern;
+        mg_timer = &timer;
     }
     for (const ArticGroup& g : s->groups) {
         if (g.step_count == 0) continue;
@@ -729,8 +750,10 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         HIP_TRY(hipMemsetAsync(s->d_ext, 0, (size_t)s->nb * 6 * sizeof(float), st));
         s->ext_pending = false;
     }
+    mg_timer = nullptr;
     if (!s->capturing) {
         HIP_TRY(hipEventRecord(s->ev_end, st));
+        s->kern_n[slot] = timer.used;
         s->ring_n++;
         s->stepped = true;
     }
@@ -761,8 +784,13 @@ int32_t mg_step_time_stats(mg_sim* s, int32_t n, float* avg_ms, float* min_ms, f
     for (int32_t k = 0; k < n; ++k) {
         const int slot = (int)((s->ring_n - 1 - k) % mg_sim::kRing);
         HIP_TRY(hipEventSynchronize(s->ring_e[slot]));
+        // sum of the step kernels' own durations (dispatch timestamps)
         float ms = 0.0f;
-        HIP_TRY(hipEventElapsedTime(&ms, s->ring_b[slot], s->ring_e[slot]));
+        for (int j = 0; j < s->kern_n[slot]; ++j) {
+            float kms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&kms, s->kern_b[slot][j], s->kern_e[slot][j]));
+            ms += kms;
+        }
         sum += ms;
         lo = ms < lo ? ms : lo;
         hi = ms > hi ? ms : hi;
@@ -1057,16 +1085,19 @@ int32_t mg_render_cameras(mg_sim* s, const mg_camera* cams, int32_t n, void* str
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(st, &cap));
     const bool timed = cap == hipStreamCaptureStatusNone;
+    MgKernelTimer timer{};
     if (timed) {
         if (!s->rev_b) HIP_TRY(hipEventCreate(&s->rev_b));
         if (!s->rev_e) HIP_TRY(hipEventCreate(&s->rev_e));
-        HIP_TRY(hipEventRecord(s->rev_b, st));
+        timer.start = &s->rev_b;
+        timer.stop = &s->rev_e;
+        timer.cap = 1;
+        mg_timer = &timer;      // the launch carries the kernel's dispatch timestamps
     }
-    HIP_TRY(mg_launch_render(A, s->cam_blocks, st));
-    if (timed) {
-        HIP_TRY(hipEventRecord(s->rev_e, st));
-        s->rendered = true;
-    }
+    const hipError_t e = mg_launch_render(A, s->cam_blocks, st);
+    mg_timer = nullptr;
+    HIP_TRY(e);
+    if (timed) s->rendered = true;
     return MG_OK;
 }
 

@@ -96,3 +96,17 @@ def test_franka_cube_ik_osc_setup(monkeypatch):
     # cube and the table share group i (filter 0), the Franka has filter 2
     A = sim.model_arrays
     assert (A["actor_coll"][:3, :3] == [[0, 0, 0], [0, 0, 0], [0, 0, 2]]).all()
+
+
+@pytest.mark.skipif(has_gpu(), reason="CPU-container variant")
+def test_test11_camerazoom_setup(monkeypatch):
+    """Config 5's script: 2 envs x 90 cameras on the UAV (one per FOV 1..90),
+    handles kept in test11's aliased list (:261,327-336)."""
+    ns, err = _exec_script(os.path.join(REFERENCE, "test11_servo_vecenv_camerazoom.py"), REFERENCE, monkeypatch)
+    assert err is not None
+    envs = ns["envs"]
+    assert len(envs) == 2 and all(len(e.cameras) == 90 for e in envs)
+    assert ns["camera_handles"][0] is ns["camera_handles"][1] and len(ns["camera_handles"][0]) == 180
+    cam = envs[1].cameras[29]
+    assert cam.props.horizontal_fov == 30 and cam.props.width == 1600 and cam.body == 0
+    assert (cam.local.p.x, cam.local.p.y, cam.local.p.z) == (5, 0, 0)
