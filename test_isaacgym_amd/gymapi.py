@@ -7,8 +7,9 @@ set_* — is libmigym's HIP kernels; everything here is scene bookkeeping and
 argument marshalling. Error behaviour follows Isaac Gym: creators return None,
 setters return False, lookups return INVALID_HANDLE (-1).
 
-Out of scope: rendering and the viewer. Camera and viewer calls
-are headless stubs that keep the reference scripts running (§8b last row).
+Camera sensors are rendered on the GPU (_render.py, csrc/mg_render.hip: config
+5). The viewer is headless: a handle whose window "closes" after
+MIGYM_VIEWER_FRAMES draws, so the reference scripts' loops end (§8b last row).
 """
 import ctypes
 import math
