@@ -20,7 +20,7 @@ Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel
 properties 44 + shape 40)), over its average duration taken from the kernel's own
 dispatch timestamps (hipExtLaunchKernelGGL start / stop events on the simulate
 stream; the interval rocprofv3 reports).
-`cpu_baseline` times the C restatement (oracle/, single thread, "port") on a
+`cpu_baseline` times the C restatement (oracle/, "port") on the host cores (16 threads on the GPU box) on a
 bounded sample of the same workload.
 """
 import argparse
@@ -48,29 +48,48 @@ STEP_BYTES_PER_ENV = 688         # whole tensor-API step
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def cpu_baseline(seconds=10.0):
-    """The oracle (C restatement, one thread) on the same 4096-env scene."""
+def cpu_baseline(seconds=10.0, threads=None):
+    """The oracle (C restatement) on the same 4096-env scene, on `threads` host
+    cores: each step splits the bodies into contiguous ranges, one per thread
+    (oracle.step's body_range; ctypes releases the GIL, envs are independent),
+    plus a single-thread figure on the same sample for reference."""
+    import concurrent.futures as cf
     import oracle
     gym = gymapi.acquire_gym()
     sim, _ = scenes.servo_scene(gym, ENVS_PER_GPU, use_gpu_pipeline=False)
     sim.build_model()
     p, m = sim.mg_params(), sim.mg_model()
     st = sim.model_arrays["body_state0"].copy()
+    nb = st.shape[0]
     roots = sim.model_arrays["actor_root_body"]
     acts = scenes.servo_actions(ENVS_PER_GPU, 16, "cpu", seed=0).numpy()
     dof = np.zeros((0, 2), np.float32)
-    steps = 0
-    t0 = time.perf_counter()
-    while True:
-        st[roots, 3:10] = acts[steps % len(acts)]
-        oracle.step(p, m, st, dof)
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and steps >= 5:
-            break
-    return {"value": ENVS_PER_GPU * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+    cforce = np.zeros((nb, 3), np.float32)
+    threads = threads or max(1, min(16, os.cpu_count() or 1))    # 16 = the GPU box's CPU share
+
+    def run(nthr, budget):
+        cuts = [nb * k // nthr for k in range(nthr + 1)]
+        cuts = [c - (c % 2) for c in cuts]              # an env's two bodies stay in one range
+        cuts[-1] = nb
+        steps = 0
+        with cf.ThreadPoolExecutor(nthr) as pool:
+            t0 = time.perf_counter()
+            while True:
+                st[roots, 3:10] = acts[steps % len(acts)]
+                list(pool.map(lambda k: oracle.step(p, m, st, dof, cforce=cforce,
+                                                    body_range=(cuts[k], cuts[k + 1])), range(nthr)))
+                steps += 1
+                el = time.perf_counter() - t0
+                if el >= budget and steps >= 5:
+                    return steps, el
+
+    s1, e1 = run(1, seconds * 0.3)
+    sn, en = run(threads, seconds * 0.7) if threads > 1 else (s1, e1)
+    return {"value": ENVS_PER_GPU * sn / en, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "single_thread_value": ENVS_PER_GPU * s1 / e1,
             "sample": "%d simulate() steps of the 4096-env servo scene with random root teleports, "
-                      "oracle/migym_oracle.c single-threaded (%.1f s)" % (steps, el)}
+                      "oracle/migym_oracle.c on %d host threads, bodies split into contiguous ranges (%.1f s); "
+                      "single thread: %d steps (%.1f s)" % (sn, threads, en, s1, e1)}
 
 
 def gimbal_rate(n, steps, warmup, dev, use_graph=True):
@@ -468,7 +487,6 @@ def main():
             out["s5_cameras"] = camera_rate(args.camera_envs, min(args.steps, 100), 10, dev, not args.eager)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-            out["cpu_baseline"]["cores"] = 1
         print(json.dumps(out), flush=True)
     gym.destroy_sim(sim)
     if world > 1:

@@ -15,7 +15,7 @@
  * absence of neighbouring envs' balls. Shading values are not pinned.
  *
  * Camera frame: looks along local +x, image up = the sim's up axis; pixel
- * (c, r) -> ray f + a l + b u, a = (cx - c - 0.5)/fx, b = (cy - r - 0.5)/fy.
+ * (c, r) -> ray fma(l, a, f + u b), a = (cx - c - 0.5)/fx, b = (cy - r - 0.5)/fy.
  */
 
 typedef struct {
@@ -28,12 +28,17 @@ typedef struct {
 
 static const float R_INF = __builtin_inff();
 
+/* explicit fused multiply-adds, as the kernel (fmaf is correctly rounded) */
+static float fdot_(v3_t a, v3_t b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static v3_t fma3_(v3_t a, float s, v3_t c) { return V(fmaf(a.x, s, c.x), fmaf(a.y, s, c.y), fmaf(a.z, s, c.z)); }
+static v3_t fmt_(m3_t R, v3_t v) { return V(fdot_(R.c0, v), fdot_(R.c1, v), fdot_(R.c2, v)); }
+
 static float ray_sphere_(v3_t o, v3_t d, v3_t c, float r, float tmin) {
     v3_t oc = sub3(o, c);
-    float bb = dot3(oc, d);
-    float cc = dot3(oc, oc) - r * r;
-    float dd = dot3(d, d);
-    float disc = bb * bb - dd * cc;
+    float bb = fdot_(oc, d);
+    float cc = fmaf(-r, r, fdot_(oc, oc));
+    float dd = fdot_(d, d);
+    float disc = fmaf(-dd, cc, bb * bb);
     float t;
     if (!(disc >= 0.0f)) return R_INF;
     t = (-bb - sqrtf(disc)) / dd;
@@ -49,8 +54,8 @@ static void slab_(float o, float d, float h, float* tn, float* tf) {
 }
 
 static float ray_box_(v3_t o, v3_t d, const rws_t* s, float tmin, float tmax) {
-    v3_t ol = mtv_(s->R, sub3(o, s->c));
-    v3_t dl = mtv_(s->R, d);
+    v3_t ol = fmt_(s->R, sub3(o, s->c));
+    v3_t dl = fmt_(s->R, d);
     float tn = -R_INF, tf = tmax;   /* entry point only: back faces are not drawn */
     slab_(ol.x, dl.x, s->h.x, &tn, &tf);
     slab_(ol.y, dl.y, s->h.y, &tn, &tf);
@@ -61,20 +66,20 @@ static float ray_box_(v3_t o, v3_t d, const rws_t* s, float tmin, float tmax) {
 static float ray_capsule_(v3_t o, v3_t d, const rws_t* s, float tmin) {
     float r = s->h.x, hl = s->h.y;
     v3_t ax = s->R.c0;
-    v3_t pa = sub3(s->c, mul3(ax, hl));
+    v3_t pa = fma3_(ax, -hl, s->c);
     v3_t ba = mul3(ax, 2.0f * hl);
     v3_t oa = sub3(o, pa);
-    float baba = dot3(ba, ba), bard = dot3(ba, d), baoa = dot3(ba, oa);
-    float rdoa = dot3(d, oa), oaoa = dot3(oa, oa), dd = dot3(d, d);
-    float a = baba * dd - bard * bard;
-    float b = baba * rdoa - baoa * bard;
-    float c = baba * oaoa - baoa * baoa - r * r * baba;
-    float hh = b * b - a * c;
+    float baba = fdot_(ba, ba), bard = fdot_(ba, d), baoa = fdot_(ba, oa);
+    float rdoa = fdot_(d, oa), oaoa = fdot_(oa, oa), dd = fdot_(d, d);
+    float a = fmaf(baba, dd, -(bard * bard));
+    float b = fmaf(baba, rdoa, -(baoa * bard));
+    float c = fmaf(baba, oaoa, -(baoa * baoa)) - r * r * baba;
+    float hh = fmaf(b, b, -(a * c));
     float t = R_INF, t0, t1;
     if (!(hh >= 0.0f)) return R_INF;
     if (a > 0.0f) {
         float tb = (-b - sqrtf(hh)) / a;
-        float y = baoa + tb * bard;
+        float y = fmaf(tb, bard, baoa);
         if (y > 0.0f && y < baba && tb >= tmin) t = tb;
     }
     t0 = ray_sphere_(o, d, pa, r, tmin);
@@ -95,7 +100,7 @@ static v3_t shape_normal_(const rws_t* s, v3_t p) {
     float t;
     if (s->type == MG_SHAPE_SPHERE) return mul3(dp, 1.0f / s->h.x);
     if (s->type == MG_SHAPE_BOX) {
-        v3_t pl = mtv_(s->R, dp), axis;
+        v3_t pl = fmt_(s->R, dp), axis;
         float qx = fabsf(pl.x) / s->h.x, qy = fabsf(pl.y) / s->h.y, qz = fabsf(pl.z) / s->h.z;
         float best = qx, comp;
         int k = 0;
@@ -105,9 +110,9 @@ static v3_t shape_normal_(const rws_t* s, v3_t p) {
         comp = k == 0 ? pl.x : (k == 1 ? pl.y : pl.z);
         return mul3(axis, comp < 0.0f ? -1.0f : 1.0f);
     }
-    t = dot3(dp, s->R.c0);
+    t = fdot_(dp, s->R.c0);
     t = fminf(fmaxf(t, -s->h.y), s->h.y);
-    return mul3(sub3(dp, mul3(s->R.c0, t)), 1.0f / s->h.x);
+    return mul3(fma3_(s->R.c0, -t, dp), 1.0f / s->h.x);
 }
 
 static unsigned q8_(float x) { return (unsigned)(fminf(fmaxf(x, 0.0f), 1.0f) * 255.0f + 0.5f); }
@@ -122,7 +127,7 @@ int oracle_render(const mg_sim_params* p, const float* state, const int32_t* bod
     int ns = 0, b, k, row, col;
     v3_t o, f, l, u, upv, leftv, L, gn;
     q4_t q;
-    float ifx, ify, lx = 0.3f, ly = 0.2f, lz = 1.0f, inv;
+    float ifx, ify, lx = 0.3f, ly = 0.2f, lz = 1.0f, inv, h0;
     int up_axis = p->up_axis == 0 ? 0 : 1;
 
     /* the env's shapes in the world frame */
@@ -179,24 +184,26 @@ int oracle_render(const mg_sim_params* p, const float* state, const int32_t* bod
     ify = 1.0f / cam->fy;
     gn = V(p->ground_normal[0], p->ground_normal[1], p->ground_normal[2]);
 
+    h0 = fdot_(gn, o) + p->ground_distance;
     for (row = 0; row < cam->height; ++row) {
+        v3_t rb = fma3_(u, (cam->cy - ((float)row + 0.5f)) * ify, f);
         for (col = 0; col < cam->width; ++col) {
             size_t px = (size_t)row * cam->width + col;
             float a = (cam->cx - ((float)col + 0.5f)) * ifx;
-            float bq = (cam->cy - ((float)row + 0.5f)) * ify;
-            v3_t d = add3(add3(f, mul3(l, a)), mul3(u, bq));
-            float best = cam->far_plane;
+            v3_t d = fma3_(l, a, rb);
+            float best = cam->far_plane, dd;
             int hit = -2, j, shadow = 0, sgv;
             unsigned rgba;
-            float cr, cg, cb;
             v3_t pp, n, ps;
             if (p->has_ground) {
-                float dn = dot3(gn, d);
+                float dn = fdot_(gn, d);
                 if (dn < 0.0f) {
-                    float t = -(dot3(gn, o) + p->ground_distance) / dn;
+                    float t = -h0 / dn;
                     if (t >= cam->near_plane && t < best) { best = t; hit = -1; }
                 }
             }
+            dd = fdot_(d, d);
+            (void)dd;
             for (j = 0; j < ns; ++j) {
                 float t = ray_shape_(o, d, &ws[j], cam->near_plane, best);
                 if (t < best) { best = t; hit = j; }
@@ -207,25 +214,24 @@ int oracle_render(const mg_sim_params* p, const float* state, const int32_t* bod
                 if (seg_out) seg_out[px] = 0;
                 continue;
             }
-            pp = add3(o, mul3(d, best));
+            pp = fma3_(d, best, o);
             n = hit >= 0 ? shape_normal_(&ws[hit], pp) : gn;
-            ps = add3(pp, mul3(n, 1e-3f));
+            ps = fma3_(n, 1e-3f, pp);
             for (j = 0; j < ns && !shadow; ++j) shadow = ray_shape_(ps, L, &ws[j], 0.0f, R_INF) < R_INF;
             if (hit >= 0) {
-                float lam = fmaxf(dot3(n, L), 0.0f);
-                float kk = shadow ? 0.3f : 0.3f + 0.7f * lam;
-                cr = ws[hit].r * kk; cg = ws[hit].g * kk; cb = ws[hit].b * kk;
+                float lam = fmaxf(fdot_(n, L), 0.0f);
+                float kk = shadow ? 0.3f : fmaf(0.7f, lam, 0.3f);
+                rgba = q8_(ws[hit].r * kk) | (q8_(ws[hit].g * kk) << 8) | (q8_(ws[hit].b * kk) << 16) | 0xFF000000u;
                 sgv = ws[hit].seg;
             } else {
                 float uu = pp.x, vv = up_axis == 1 ? pp.y : pp.z;
                 int par = ((int)floorf(uu) + (int)floorf(vv)) & 1;
                 float kk = shadow ? 0.55f : 1.0f;
-                cr = (par ? 108.0f / 255.0f : 143.0f / 255.0f) * kk;
-                cg = cr;
-                cb = (par ? 113.0f / 255.0f : 150.0f / 255.0f) * kk;
+                float cr = (par ? 108.0f / 255.0f : 143.0f / 255.0f) * kk;
+                float cb = (par ? 113.0f / 255.0f : 150.0f / 255.0f) * kk;
+                rgba = q8_(cr) | (q8_(cr) << 8) | (q8_(cb) << 16) | 0xFF000000u;
                 sgv = 0;
             }
-            rgba = q8_(cr) | (q8_(cg) << 8) | (q8_(cb) << 16) | 0xFF000000u;
             if (rgba_out) memcpy(rgba_out + 4 * px, &rgba, 4);
             if (depth_out) depth_out[px] = -best;
             if (seg_out) seg_out[px] = sgv;

@@ -121,9 +121,9 @@ struct MgEnvArgs {
 // pixels are cut into linear runs of MG_RENDER_RUN pixels (row-major), one run
 // per workgroup; blk0 = first workgroup of the camera (prefix over cameras).
 #define MG_RENDER_LANE_PX 4                      // pixels per lane per pass (one 16-B store)
-#define MG_RENDER_PASSES  4                      // passes per wave
+#define MG_RENDER_PASSES  16                     // passes per wave
 #define MG_RENDER_WAVES   4                      // waves per workgroup
-#define MG_RENDER_RUN (64 * MG_RENDER_LANE_PX * MG_RENDER_PASSES * MG_RENDER_WAVES)   // 4096 px
+#define MG_RENDER_RUN (64 * MG_RENDER_LANE_PX * MG_RENDER_PASSES * MG_RENDER_WAVES)   // 16384 px
 struct MgRenderCam {
     int   env, w, h, slot;         // slot: internal body slot followed, -1 fixed
     int   follow, blk0, nblk, vec; // vec: 16-B stores allowed (W*H % 4 == 0 and aligned images)
@@ -144,6 +144,7 @@ struct MgRShape {
 };
 struct MgRenderArgs {
     int                 ncam, nb;
+    int                 uniform_nblk;      // > 0: every camera has this many runs (camera = block / uniform_nblk)
     const MgRenderCam*  cams;
     const float*        state;     // snapshot [13][nb]
     const float*        shapes;

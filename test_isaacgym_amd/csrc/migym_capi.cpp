@@ -1063,6 +1063,9 @@ int32_t mg_render_cameras(mg_sim* s, const mg_camera* cams, int32_t n, void* str
     }
     MgRenderArgs A{};
     A.ncam = n; A.nb = s->nb; A.cams = s->d_cams; A.state = s->d_rstate; A.shapes = s->d_shapes;
+    A.uniform_nblk = s->cam_dev[0].nblk;
+    for (int i = 1; i < n; ++i)
+        if (s->cam_dev[i].nblk != A.uniform_nblk) { A.uniform_nblk = 0; break; }
     A.rshapes = s->d_rshapes; A.env_shape_first = s->d_env_shape_first;
     const mg_sim_params& p = s->params;
     A.has_ground = p.has_ground;
