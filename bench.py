@@ -290,11 +290,16 @@ def camera_rate(n, steps, warmup, dev, use_graph=True, width=1600, height=900):
     rk = float(np.mean(rms)) if rms else float("nan")
     wbytes = n * width * height * 4
     ach = wbytes / (rk * 1e-3) / 1e9
+    traffic = None        # HBM bytes per launch, committed rocprofv3 WRITE_SIZE pass (tools/gpu_render_pmc.sh)
+    pmc = os.path.join(ROOT, "profiles", "r01_pmc_render_%dx%dx%d.json" % (n, width, height))
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("write_bytes_per_launch_from_WRITE_SIZE_KB")
     return {"envs": n, "cameras": n, "resolution": [width, height], "env_steps_per_s": n * steps / el,
             "ms_per_step": 1e3 * el / steps, "timed_loop": "hipGraph replay" if graphs is not None else "eager",
             "kernel": "k_render", "kernel_ms_avg": rk, "image_bytes_per_launch": wbytes,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS},
+                         "frac": ach / HBM_PEAK_GBS, "traffic": traffic},
             "env0_non_sky_fraction": lit}
 
 
