@@ -47,6 +47,15 @@ extern "C" {
 #define MG_SHAPE_SPHERE   0
 #define MG_SHAPE_BOX      1
 #define MG_SHAPE_CAPSULE  2
+#define MG_SHAPE_CONVEX   3   /* convex hull of a mesh: size[0] = bounding radius about the shape
+                                 origin, size[1] = offset of its record in mg_model.hulls */
+
+/* convex hull record (floats, shape-local frame): nv, nf, 0, 0, then nv vertices
+ * (x, y, z), then nf face planes (n.x, n.y, n.z, d) with unit outward n and
+ * n . x <= d inside */
+#define MG_HULL_HEADER     4
+#define MG_HULL_MAX_VERTS 32
+#define MG_HULL_MAX_FACES 64
 
 /* body kinds (mg_model.body_kind) */
 #define MG_BODY_FREE      0   /* single-body dynamic actor: free-body kernel */
@@ -108,7 +117,8 @@ typedef struct mg_model {
     int32_t num_envs, num_actors, num_bodies, num_dofs;
     int32_t num_tmpl_bodies, num_shapes;
     int32_t num_artics, num_artic_tmpls, num_tmpl_links;
-    int32_t reserved_i[7];
+    int32_t num_hull_floats;      /* length of `hulls` */
+    int32_t reserved_i[6];
 
     const float*   body_state0;   /* [num_bodies][13] initial state, AoS */
     const float*   body_mass;     /* [num_bodies][MG_MASS_N] */
@@ -132,7 +142,9 @@ typedef struct mg_model {
      * (filter_a & filter_b) == 0; the ground collides with everything. NULL: no
      * body-body contacts (every env steps in the uncoupled kernels). */
     const int32_t* actor_coll;
-    const void*    reserved_p[2];
+    /* convex hull records (MG_SHAPE_CONVEX shapes point into it), or NULL */
+    const float*   hulls;
+    const void*    reserved_p[1];
 } mg_model;
 
 typedef struct mg_sim mg_sim;

@@ -69,20 +69,24 @@ def step(sim_params, model, state, dof, tgt=None, props=None, ext=None, cforce=N
     return cforce
 
 
-def collide(a, b, margin):
-    """Narrow phase of the coupled step (oracle_collide): a, b = [type, c.xyz,
-    q.xyzw, h.xyz]; returns an (n, 7) array of [point on a, normal b->a, sep]."""
+def collide(a, b, margin, hull_a=None, hull_b=None):
+    """Narrow phase of the coupled step (oracle_collide2): a, b = [type, c.xyz,
+    q.xyzw, h.xyz] (convex: h = (bounding radius, 0, 0) and its hull record
+    hull_a / hull_b); returns an (n, 7) array of [point on a, normal b->a, sep]."""
     L = lib()
-    L.oracle_collide.restype = ctypes.c_int
-    L.oracle_collide.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p]
+    vp = ctypes.c_void_p
+    L.oracle_collide2.restype = ctypes.c_int
+    L.oracle_collide2.argtypes = [vp, vp, vp, vp, ctypes.c_float, vp]
     a = np.ascontiguousarray(a, dtype=np.float32)
     b = np.ascontiguousarray(b, dtype=np.float32)
+    ha = None if hull_a is None else np.ascontiguousarray(hull_a, dtype=np.float32)
+    hb = None if hull_b is None else np.ascontiguousarray(hull_b, dtype=np.float32)
     out = np.zeros((4, 7), dtype=np.float32)
-    n = L.oracle_collide(a.ctypes.data, b.ctypes.data, float(margin), out.ctypes.data)
+    n = L.oracle_collide2(a.ctypes.data, _ptr(ha), b.ctypes.data, _ptr(hb), float(margin), out.ctypes.data)
     return out[:n]
 
 
-def render(sim_params, state, body_tmpl, tbi, shapes, env_body_first, color, seg, cam):
+def render(sim_params, state, body_tmpl, tbi, shapes, env_body_first, color, seg, cam, hulls=None):
     """One camera on the host (oracle_render, migym_oracle_render.c): returns
     (rgba (H, W, 4) uint8, depth (H, W) f32, seg (H, W) int32). state is the
     rigid-body tensor [nb, 13] (global order); cam a _native.MgCamera (its
@@ -90,7 +94,7 @@ def render(sim_params, state, body_tmpl, tbi, shapes, env_body_first, color, seg
     L = lib()
     vp = ctypes.c_void_p
     L.oracle_render.restype = ctypes.c_int
-    L.oracle_render.argtypes = [vp] * 12
+    L.oracle_render.argtypes = [vp] * 13
     H, W = cam.height, cam.width
     rgba = np.zeros((H, W, 4), np.uint8)
     depth = np.zeros((H, W), np.float32)
@@ -99,8 +103,10 @@ def render(sim_params, state, body_tmpl, tbi, shapes, env_body_first, color, seg
             np.ascontiguousarray(tbi, np.int32), np.ascontiguousarray(shapes, np.float32),
             np.ascontiguousarray(env_body_first, np.int32), np.ascontiguousarray(color, np.float32),
             np.ascontiguousarray(seg, np.int32)]
-    rc = L.oracle_render(ctypes.addressof(sim_params), *[a.ctypes.data for a in arrs], ctypes.addressof(cam),
-                         rgba.ctypes.data, depth.ctypes.data, sg.ctypes.data)
+    hl = np.ascontiguousarray(hulls if hulls is not None and len(hulls) else np.zeros(1), np.float32)
+    ptrs = [a.ctypes.data for a in arrs]
+    rc = L.oracle_render(ctypes.addressof(sim_params), ptrs[0], ptrs[1], ptrs[2], ptrs[3], hl.ctypes.data, ptrs[4],
+                         ptrs[5], ptrs[6], ctypes.addressof(cam), rgba.ctypes.data, depth.ctypes.data, sg.ctypes.data)
     if rc != 0:
         raise RuntimeError("oracle_render: too many shapes in the camera's env")
     return rgba, depth, sg

@@ -243,7 +243,7 @@ static void contact_friction(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, floa
 /* Contact candidates of one shape: (static index k, point, separation). */
 typedef struct { int k; v3_t p; float sep; } cand_t;
 static int shape_candidates(const step_t* P, const basis_t* B, const float* sh, q4_t q, v3_t x, cand_t* out,
-                            float* mu, float* e) {
+                            float* mu, float* e, const float* hulls) {
     const int type = (int)sh[0];
     const q4_t qs = qmul_(q, Q(sh[7], sh[8], sh[9], sh[10]));
     const v3_t cs = add3(x, qrot_(q, V(sh[4], sh[5], sh[6])));
@@ -283,6 +283,27 @@ static int shape_candidates(const step_t* P, const basis_t* B, const float* sh, 
             const v3_t c = k ? add3(cs, ax) : sub3(cs, ax);
             out[n].k = k; out[n].p = b_addn(B, c, -rad); out[n].sep = b_dn(B, c) + P->pd - rad; n++;
         }
+    } else if (type == MG_SHAPE_CONVEX) {
+        /* the 4 deepest hull vertices within the contact offset, ascending
+         * separation, lower vertex index first on ties (as mg_rigid.hip) */
+        const float* hv = hulls + (int)sh[2];
+        const int nv = (int)hv[0];
+        float ks[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        v3_t kp[4];
+        int kn = 0, i, at;
+        for (i = 0; i < nv; ++i) {
+            const float* vv = hv + MG_HULL_HEADER + 3 * i;
+            const v3_t p = add3(cs, qrot_(qs, V(vv[0], vv[1], vv[2])));
+            const float sep = b_dn(B, p) + P->pd;
+            if (!(sep < P->co)) continue;
+            if (kn == 4 && !(sep < ks[3])) continue;
+            at = 0;
+            for (k = 0; k < kn; ++k) if (ks[k] <= sep) at = k + 1;
+            for (k = 3; k > at; --k) { ks[k] = ks[k - 1]; kp[k] = kp[k - 1]; }
+            ks[at] = sep; kp[at] = p;
+            if (kn < 4) kn = kn + 1;
+        }
+        for (k = 0; k < kn; ++k) { out[n].k = k; out[n].p = kp[k]; out[n].sep = ks[k]; n++; }
     }
     return n;
 }
@@ -335,7 +356,8 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
             for (s_ = sh0; s_ < sh0 + nsh; ++s_) {
                 cand_t cd[8];
                 float mu, e;
-                int k, n = shape_candidates(P, &B, m->shapes + (size_t)s_ * MG_SHAPE_STRIDE, q, x, cd, &mu, &e);
+                int k, n = shape_candidates(P, &B, m->shapes + (size_t)s_ * MG_SHAPE_STRIDE, q, x, cd, &mu, &e,
+                                             m->hulls);
                 for (k = 0; k < n; ++k) {
                     slot_t ns;
                     if (!(cd[k].sep < P->co)) continue;

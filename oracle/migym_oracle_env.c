@@ -15,7 +15,7 @@
 #define OE_F0 16
 #define OE_PMAX 4
 
-typedef struct { int type; v3_t c; m3_t R; v3_t h; } cshape_t;
+typedef struct { int type; v3_t c; m3_t R; v3_t h; const float* hv; } cshape_t;
 typedef struct { int n; v3_t p[OE_PMAX]; v3_t nrm[OE_PMAX]; float sep[OE_PMAX]; } pair_t;
 
 static v3_t mcol_(m3_t R, int i) { return i == 0 ? R.c0 : (i == 1 ? R.c1 : R.c2); }
@@ -216,6 +216,95 @@ static void box_box_(const cshape_t* A, const cshape_t* B, float margin, pair_t*
     }
 }
 
+/* ---- convex shapes as vertices + face planes (a box: 8 corners, 6 faces),
+ * vertex penetration both ways (mg_collide.h convex_convex) */
+static int cvx_nv_(const cshape_t* S) { return S->type == MG_SHAPE_BOX ? 8 : (int)S->hv[0]; }
+static int cvx_nf_(const cshape_t* S) { return S->type == MG_SHAPE_BOX ? 6 : (int)S->hv[1]; }
+static v3_t cvx_vertex_(const cshape_t* S, int i) {
+    v3_t l;
+    if (S->type == MG_SHAPE_BOX) {
+        l = V((i & 1) ? S->h.x : -S->h.x, (i & 2) ? S->h.y : -S->h.y, (i & 4) ? S->h.z : -S->h.z);
+    } else {
+        const float* v = S->hv + MG_HULL_HEADER + 3 * i;
+        l = V(v[0], v[1], v[2]);
+    }
+    return add3(S->c, mv_(S->R, l));
+}
+static void cvx_plane_l_(const cshape_t* S, int f, v3_t* nl, float* dl) {
+    if (S->type == MG_SHAPE_BOX) {
+        const int ax = f >> 1;
+        const float sg = (f & 1) ? -1.0f : 1.0f;
+        *nl = V(ax == 0 ? sg : 0.0f, ax == 1 ? sg : 0.0f, ax == 2 ? sg : 0.0f);
+        *dl = vc_(S->h, ax);
+    } else {
+        const float* pl = S->hv + MG_HULL_HEADER + 3 * (int)S->hv[0] + 4 * f;
+        *nl = V(pl[0], pl[1], pl[2]);
+        *dl = pl[3];
+    }
+}
+static float cvx_sd_(const cshape_t* S, v3_t p, int* fbest) {
+    const v3_t pl = mtv_(S->R, sub3(p, S->c));
+    const int nf = cvx_nf_(S);
+    float best = -1e30f;
+    int f;
+    *fbest = 0;
+    for (f = 0; f < nf; ++f) {
+        v3_t nl;
+        float dl, sd;
+        cvx_plane_l_(S, f, &nl, &dl);
+        sd = dot3(nl, pl) - dl;
+        if (sd > best) { best = sd; *fbest = f; }
+    }
+    return best;
+}
+static v3_t cvx_normal_(const cshape_t* S, int f) {
+    v3_t nl;
+    float dl;
+    cvx_plane_l_(S, f, &nl, &dl);
+    return mv_(S->R, nl);
+}
+/* the OE_PMAX deepest candidates, ascending separation, earlier first on ties */
+static void deep4_add_(pair_t* D, float sep, v3_t p, v3_t n) {
+    int at = 0, k;
+    if (D->n == OE_PMAX && !(sep < D->sep[OE_PMAX - 1])) return;
+    for (k = 0; k < D->n; ++k) if (D->sep[k] <= sep) at = k + 1;
+    for (k = OE_PMAX - 1; k > at; --k) { D->sep[k] = D->sep[k - 1]; D->p[k] = D->p[k - 1]; D->nrm[k] = D->nrm[k - 1]; }
+    D->sep[at] = sep; D->p[at] = p; D->nrm[at] = n;
+    if (D->n < OE_PMAX) D->n = D->n + 1;
+}
+static void deep4_emit_(const pair_t* D, pair_t* o) {
+    int k;
+    for (k = 0; k < D->n; ++k) ppush_(o, D->p[k], D->nrm[k], D->sep[k]);
+}
+static void convex_convex_(const cshape_t* A, const cshape_t* B, float margin, pair_t* o) {
+    pair_t D;
+    int i, f;
+    const int na = cvx_nv_(A), nb = cvx_nv_(B);
+    D.n = 0;
+    for (i = 0; i < na; ++i) {
+        const v3_t v = cvx_vertex_(A, i);
+        const float sd = cvx_sd_(B, v, &f);
+        if (sd < margin) deep4_add_(&D, sd, v, cvx_normal_(B, f));
+    }
+    for (i = 0; i < nb; ++i) {
+        const v3_t v = cvx_vertex_(B, i);
+        const float sd = cvx_sd_(A, v, &f);
+        if (sd < margin) {
+            const v3_t nA = cvx_normal_(A, f);
+            deep4_add_(&D, sd, sub3(v, mul3(nA, sd)), mul3(nA, -1.0f));
+        }
+    }
+    deep4_emit_(&D, o);
+}
+static void sph_cvx_(v3_t s, float r, const cshape_t* B, float margin, pair_t* o) {
+    int f;
+    const float sep = cvx_sd_(B, s, &f) - r;
+    v3_t n;
+    if (!(sep < margin)) return;
+    n = cvx_normal_(B, f);
+    ppush_(o, sub3(s, mul3(n, r)), n, sep);
+}
+
 static void collide_(const cshape_t* A, const cshape_t* B, float margin, pair_t* o) {
     v3_t ca[2], cb[2];
     float ra, rb;
@@ -228,6 +317,20 @@ static void collide_(const cshape_t* A, const cshape_t* B, float margin, pair_t*
     ca[1] = add3(A->c, mul3(A->R.c0, A->h.y));
     cb[0] = B->type == MG_SHAPE_CAPSULE ? sub3(B->c, mul3(B->R.c0, B->h.y)) : B->c;
     cb[1] = add3(B->c, mul3(B->R.c0, B->h.y));
+    if (A->type == MG_SHAPE_CONVEX || B->type == MG_SHAPE_CONVEX) {
+        const int pa = A->type == MG_SHAPE_BOX || A->type == MG_SHAPE_CONVEX;
+        const int pb = B->type == MG_SHAPE_BOX || B->type == MG_SHAPE_CONVEX;
+        pair_t t;
+        if (pa && pb) { convex_convex_(A, B, margin, o); return; }
+        if (pb) {
+            for (k = 0; k < na; ++k) sph_cvx_(ca[k], ra, B, margin, o);
+            return;
+        }
+        t.n = 0;
+        for (k = 0; k < nbs; ++k) sph_cvx_(cb[k], rb, A, margin, &t);
+        for (k = 0; k < t.n; ++k) ppush_(o, add3(t.p[k], mul3(t.nrm[k], t.sep[k])), mul3(t.nrm[k], -1.0f), t.sep[k]);
+        return;
+    }
     if (B->type == MG_SHAPE_BOX) {
         for (k = 0; k < na; ++k) sph_box_(ca[k], ra, B, margin, o);
         return;
@@ -254,12 +357,13 @@ static void tangents_(v3_t n, v3_t* t1, v3_t* t2) {
     *t2 = cross3(n, t);
 }
 
-static cshape_t place_(const float* sh, v3_t x, q4_t q) {
+static cshape_t place_(const float* sh, v3_t x, q4_t q, const float* hulls) {
     cshape_t c;
     c.type = (int)sh[0];
     c.c = add3(x, qrot_(q, V(sh[4], sh[5], sh[6])));
     c.R = qmat_(qmul_(q, Q(sh[7], sh[8], sh[9], sh[10])));
     c.h = V(sh[1], sh[2], sh[3]);
+    c.hv = c.type == MG_SHAPE_CONVEX ? hulls + (int)sh[2] : NULL;
     return c;
 }
 
@@ -267,7 +371,17 @@ static void ground_pair_(const step_t* P, const cshape_t* s, pair_t* o) {
     const v3_t n = P->n;
     const float off = P->co;
     int k;
-    if (s->type == MG_SHAPE_BOX) {
+    if (s->type == MG_SHAPE_CONVEX) {
+        pair_t D;
+        const int nv = cvx_nv_(s);
+        D.n = 0;
+        for (k = 0; k < nv; ++k) {
+            const v3_t p = cvx_vertex_(s, k);
+            const float sep = dot3(n, p) + P->pd;
+            if (sep < off) deep4_add_(&D, sep, p, n);
+        }
+        deep4_emit_(&D, o);
+    } else if (s->type == MG_SHAPE_BOX) {
         const float d0 = dot3(n, s->R.c0), d1 = dot3(n, s->R.c1), d2 = dot3(n, s->R.c2);
         const float ad0 = fabsf(d0), ad1 = fabsf(d1), ad2 = fabsf(d2);
         int ia = 0;
@@ -693,7 +807,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             float mu, rest;
             if (pp->a >= OE_F0) { xa = fx[pp->a - OE_F0]; qa = fq[pp->a - OE_F0]; }
             else { xa = xl[pp->a]; qa = ql[pp->a]; }
-            sA = place_(sha, xa, qa);
+            sA = place_(sha, xa, qa, m->hulls);
             o.n = 0;
             if (pp->b < 0) {
                 ground_pair_(P, &sA, &o);
@@ -712,7 +826,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     xb = xl[pp->b];
                     qb = ql[pp->b];
                 }
-                sB = place_(shb, xb, qb);
+                sB = place_(shb, xb, qb, m->hulls);
                 collide_(&sA, &sB, P->co, &o);
                 mu = 0.5f * (sha[11] + shb[11]);
                 rest = 0.5f * (sha[12] + shb[12]);
@@ -1062,12 +1176,14 @@ static int classify_envs_(const mg_model* m, oenv_t* envs, char* owned) {
 /* Narrow phase as a test entry point: shapes given as [type, c.xyz, q.xyzw,
  * h.xyz] (11 floats); out[4][7] = point.xyz, normal.xyz, separation. Returns
  * the contact count. */
-int oracle_collide(const float* a, const float* b, float margin, float* out) {
+int oracle_collide2(const float* a, const float* ha, const float* b, const float* hb, float margin, float* out) {
     cshape_t A, B;
     pair_t o;
     int k;
     A.type = (int)a[0]; A.c = V(a[1], a[2], a[3]); A.R = qmat_(Q(a[4], a[5], a[6], a[7])); A.h = V(a[8], a[9], a[10]);
     B.type = (int)b[0]; B.c = V(b[1], b[2], b[3]); B.R = qmat_(Q(b[4], b[5], b[6], b[7])); B.h = V(b[8], b[9], b[10]);
+    A.hv = ha;
+    B.hv = hb;
     o.n = 0;
     collide_(&A, &B, margin, &o);
     for (k = 0; k < o.n; ++k) {
@@ -1076,4 +1192,9 @@ int oracle_collide(const float* a, const float* b, float margin, float* out) {
         out[k * 7 + 6] = o.sep[k];
     }
     return o.n;
+}
+
+/* test entry: shapes as [type, c.xyz, q.xyzw, h.xyz]; hull records (convex) or NULL */
+int oracle_collide(const float* a, const float* b, float margin, float* out) {
+    return oracle_collide2(a, NULL, b, NULL, margin, out);
 }

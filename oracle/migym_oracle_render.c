@@ -24,6 +24,7 @@ typedef struct {
     v3_t c;
     m3_t R;
     v3_t h;
+    const float* hv;
 } rws_t;
 
 static const float R_INF = __builtin_inff();
@@ -89,7 +90,26 @@ static float ray_capsule_(v3_t o, v3_t d, const rws_t* s, float tmin) {
     return t;
 }
 
+static float ray_convex_(v3_t o, v3_t d, const rws_t* s, float tmin, float tmax) {
+    const v3_t ol = fmt_(s->R, sub3(o, s->c));
+    const v3_t dl = fmt_(s->R, d);
+    const int nv = (int)s->hv[0], nf = (int)s->hv[1];
+    const float* pl = s->hv + MG_HULL_HEADER + 3 * nv;
+    float tn = -R_INF, tf = tmax;
+    int f;
+    for (f = 0; f < nf; ++f) {
+        const v3_t n = V(pl[4 * f + 0], pl[4 * f + 1], pl[4 * f + 2]);
+        const float dist = fdot_(n, ol) - pl[4 * f + 3];
+        const float den = fdot_(n, dl);
+        if (den < 0.0f) tn = fmaxf(tn, -dist / den);
+        else if (den > 0.0f) tf = fminf(tf, -dist / den);
+        else if (dist > 0.0f) return R_INF;
+    }
+    return (tn <= tf && tn >= tmin) ? tn : R_INF;
+}
+
 static float ray_shape_(v3_t o, v3_t d, const rws_t* s, float tmin, float tmax) {
+    if (s->type == MG_SHAPE_CONVEX) return ray_convex_(o, d, s, tmin, tmax);
     if (s->type == MG_SHAPE_BOX) return ray_box_(o, d, s, tmin, tmax);
     if (s->type == MG_SHAPE_SPHERE) return ray_sphere_(o, d, s->c, s->h.x, tmin);
     return ray_capsule_(o, d, s, tmin);
@@ -110,6 +130,20 @@ static v3_t shape_normal_(const rws_t* s, v3_t p) {
         comp = k == 0 ? pl.x : (k == 1 ? pl.y : pl.z);
         return mul3(axis, comp < 0.0f ? -1.0f : 1.0f);
     }
+    if (s->type == MG_SHAPE_CONVEX) {
+        const v3_t pl = fmt_(s->R, dp);
+        const int nv = (int)s->hv[0], nf = (int)s->hv[1];
+        const float* pp = s->hv + MG_HULL_HEADER + 3 * nv;
+        float best = -R_INF;
+        v3_t nl = V(0.0f, 0.0f, 1.0f);
+        int f;
+        for (f = 0; f < nf; ++f) {
+            const v3_t n = V(pp[4 * f + 0], pp[4 * f + 1], pp[4 * f + 2]);
+            const float dist = fdot_(n, pl) - pp[4 * f + 3];
+            if (dist > best) { best = dist; nl = n; }
+        }
+        return fma3_(s->R.c2, nl.z, fma3_(s->R.c1, nl.y, mul3(s->R.c0, nl.x)));
+    }
     t = fdot_(dp, s->R.c0);
     t = fminf(fmaxf(t, -s->h.y), s->h.y);
     return mul3(fma3_(s->R.c0, -t, dp), 1.0f / s->h.x);
@@ -118,11 +152,11 @@ static v3_t shape_normal_(const rws_t* s, v3_t p) {
 static unsigned q8_(float x) { return (unsigned)(fminf(fmaxf(x, 0.0f), 1.0f) * 255.0f + 0.5f); }
 
 /* One camera. state: AoS [nb][13] in global body order; body_tmpl [nb];
- * tbi [ntb][MG_TBODY_I_N]; shapes [ns][MG_SHAPE_STRIDE]; env_body_first
+ * tbi [ntb][MG_TBODY_I_N]; shapes [ns][MG_SHAPE_STRIDE]; hulls (or NULL); env_body_first
  * [num_envs+1]; color [nb][3]; seg [nb]. Outputs may be NULL. */
 int oracle_render(const mg_sim_params* p, const float* state, const int32_t* body_tmpl, const int32_t* tbi,
-                  const float* shapes, const int32_t* env_body_first, const float* color, const int32_t* seg,
-                  const mg_camera* cam, uint8_t* rgba_out, float* depth_out, int32_t* seg_out) {
+                  const float* shapes, const float* hulls, const int32_t* env_body_first, const float* color,
+                  const int32_t* seg, const mg_camera* cam, uint8_t* rgba_out, float* depth_out, int32_t* seg_out) {
     rws_t ws[MG_RENDER_MAX_SHAPES];
     int ns = 0, b, k, row, col;
     v3_t o, f, l, u, upv, leftv, L, gn;
@@ -148,8 +182,9 @@ int oracle_render(const mg_sim_params* p, const float* state, const int32_t* bod
             w->c = add3(pb, qrot_(qb, V(sh[4], sh[5], sh[6])));
             w->R = qmat_(qmul_(qb, Q(sh[7], sh[8], sh[9], sh[10])));
             if (w->type == MG_SHAPE_BOX) w->h = V(sh[1], sh[2], sh[3]);
-            else if (w->type == MG_SHAPE_SPHERE) w->h = V(sh[1], 0.0f, 0.0f);
+            else if (w->type == MG_SHAPE_SPHERE || w->type == MG_SHAPE_CONVEX) w->h = V(sh[1], 0.0f, 0.0f);
             else w->h = V(sh[1], sh[2], 0.0f);
+            w->hv = w->type == MG_SHAPE_CONVEX ? hulls + (int)sh[2] : NULL;
         }
     }
 

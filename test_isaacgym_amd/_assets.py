@@ -19,10 +19,12 @@ Reference behaviour this mirrors (SURVEY.md §2 "URDF/MJCF/mesh importer", §8a 
     AssetOptions.density; a mass without an inertia tensor (the UAV and ground
     vehicle, assets/urdf/uav/urdf/rq-1-predator-mae-uav.urdf:4-7) keeps the mass
     and takes the shape inertia scaled to it.
-Meshes: collision meshes that exist are represented by their axis-aligned box in
-the mesh frame. The servo scene's two meshes are missing from the reference
-(.MISSING_LARGE_BLOBS:7-8); they get the frozen box proxies of MESH_PROXIES,
-expressed in the body frame.
+Meshes: a collision mesh that exists becomes its convex hull (MG_SHAPE_CONVEX,
+as PhysX cooks a convex mesh from it), reduced to at most MG_HULL_MAX_VERTS
+vertices by farthest-point sampling of the hull vertices; its mass properties
+are the hull's at AssetOptions.density. The servo scene's two meshes are missing
+from the reference (.MISSING_LARGE_BLOBS:7-8); they get the frozen box proxies
+of MESH_PROXIES, expressed in the body frame.
 """
 import math
 import os
@@ -39,7 +41,8 @@ MESH_PROXIES = {
     "fusch-apc.obj": (7.5, 3.0, 2.5),                  # tpz-fuchs-apc, URDF scale 0.6
 }
 
-SPHERE, BOX, CAPSULE = 0, 1, 2
+SPHERE, BOX, CAPSULE, CONVEX = 0, 1, 2, 3
+HULL_MAX_VERTS, HULL_MAX_FACES = 32, 64          # MG_HULL_MAX_VERTS / _FACES (include/migym.h)
 
 
 def _quat_from_rpy(r, p, y):
@@ -95,10 +98,79 @@ def _mat_to_quat(R):
     return -q if q[3] < 0 else q
 
 
-class Shape:
-    __slots__ = ("type", "size", "p", "q", "friction", "restitution", "source")
+class Hull:
+    """Convex hull in its shape frame: vertices (nv, 3), face planes (nf, 4) =
+    (unit outward n, d) with n . x <= d inside, and unit-density mass
+    properties (volume, centroid, inertia about the centroid)."""
 
-    def __init__(self, type_, size, p=None, q=None, source="primitive"):
+    def __init__(self, verts, planes, volume, com, inertia):
+        self.verts = verts
+        self.planes = planes
+        self.volume = volume
+        self.com = com
+        self.inertia = inertia
+
+    def record(self):
+        """The MG_HULL record (include/migym.h) as float32."""
+        head = np.array([len(self.verts), len(self.planes), 0, 0], dtype=np.float32)
+        return np.concatenate([head, self.verts.astype(np.float32).reshape(-1),
+                               self.planes.astype(np.float32).reshape(-1)])
+
+
+def _farthest_points(pts, k):
+    """k of pts by farthest-point sampling, starting from the point farthest
+    from their centroid (deterministic)."""
+    c = pts.mean(0)
+    idx = [int(np.argmax(((pts - c) ** 2).sum(1)))]
+    d2 = ((pts - pts[idx[0]]) ** 2).sum(1)
+    while len(idx) < k:
+        j = int(np.argmax(d2))
+        idx.append(j)
+        d2 = np.minimum(d2, ((pts - pts[j]) ** 2).sum(1))
+    return pts[sorted(idx)]
+
+
+def make_hull(verts, max_verts=HULL_MAX_VERTS):
+    """Convex hull of a vertex cloud, at most max_verts vertices; coplanar
+    triangles merged into one face plane. Mass properties by tetrahedra from
+    the vertex centroid."""
+    from scipy.spatial import ConvexHull
+    pts = np.unique(np.asarray(verts, dtype=np.float64), axis=0)
+    h = ConvexHull(pts)
+    pts = pts[h.vertices]
+    nv = min(max_verts, len(pts))
+    while True:
+        cand = _farthest_points(pts, nv) if len(pts) > nv else pts
+        h = ConvexHull(cand)
+        hv = cand[np.sort(h.vertices)]
+        h = ConvexHull(hv)
+        planes = []
+        for eq in h.equations:                     # n . x + e <= 0 inside
+            n, d = eq[:3], -eq[3]
+            if not any(abs(np.dot(n, q[:3]) - 1.0) < 1e-6 and abs(d - q[3]) < 1e-6 for q in planes):
+                planes.append(np.array([n[0], n[1], n[2], d]))
+        if len(planes) <= HULL_MAX_FACES or nv <= 8:
+            break
+        nv -= 2
+    o = hv.mean(0)
+    vol, mom1, C = 0.0, np.zeros(3), np.zeros((3, 3))
+    for tri in h.simplices:
+        a, b, c = hv[tri[0]] - o, hv[tri[1]] - o, hv[tri[2]] - o
+        d6 = abs(float(np.dot(a, np.cross(b, c))))
+        s = a + b + c
+        vol += d6 / 6.0
+        mom1 += d6 / 6.0 * s / 4.0
+        C += d6 / 120.0 * (np.outer(a, a) + np.outer(b, b) + np.outer(c, c) + np.outer(s, s))
+    r = mom1 / vol
+    I_o = np.trace(C) * np.eye(3) - C
+    I_c = I_o - vol * (np.dot(r, r) * np.eye(3) - np.outer(r, r))
+    return Hull(hv, np.array(planes), vol, r + o, I_c)
+
+
+class Shape:
+    __slots__ = ("type", "size", "p", "q", "friction", "restitution", "source", "hull")
+
+    def __init__(self, type_, size, p=None, q=None, source="primitive", hull=None):
         self.type = type_
         self.size = tuple(float(s) for s in size)
         self.p = np.zeros(3) if p is None else np.asarray(p, dtype=np.float64)
@@ -106,8 +178,17 @@ class Shape:
         self.friction = 1.0
         self.restitution = 0.0
         self.source = source
+        self.hull = hull
+
+    def com_body(self):
+        """Centroid of the shape in the body frame."""
+        if self.type == CONVEX:
+            return self.p + _qmat(self.q) @ self.hull.com
+        return self.p
 
     def volume(self):
+        if self.type == CONVEX:
+            return self.hull.volume
         if self.type == BOX:
             return 8.0 * self.size[0] * self.size[1] * self.size[2]
         if self.type == SPHERE:
@@ -116,7 +197,9 @@ class Shape:
         return math.pi * r * r * 2.0 * hh + 4.0 / 3.0 * math.pi * r ** 3
 
     def inertia_unit_mass(self):
-        """Rotational inertia about the shape centre, shape frame, per unit mass."""
+        """Rotational inertia about the shape centroid, shape frame, per unit mass."""
+        if self.type == CONVEX:
+            return self.hull.inertia / self.hull.volume
         if self.type == BOX:
             a, b, c = (2 * s for s in self.size)
             return np.diag([(b * b + c * c) / 12.0, (a * a + c * c) / 12.0, (a * a + b * b) / 12.0])
@@ -260,13 +343,13 @@ def compute_mass_props(body, density):
         return MassProps(body.mass, body.com, body.inertia)
     if vtot > 0:
         m_shape = density * vtot
-        com = sum(s.p * v for s, v in zip(shapes, vols)) / vtot
+        com = sum(s.com_body() * v for s, v in zip(shapes, vols)) / vtot
         I = np.zeros((3, 3))
         for s, v in zip(shapes, vols):
             ms = density * v
             R = _qmat(s.q)
             Ic = R @ (s.inertia_unit_mass() * ms) @ R.T
-            d = s.p - com
+            d = s.com_body() - com
             I += Ic + ms * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
         if body.mass is not None:             # mass given, inertia missing: scale the shape inertia
             scale = body.mass / m_shape
@@ -322,6 +405,29 @@ def _mesh_vertices(path):
                                                                    ("a", "<u2")]))
         return rec["v"].reshape(-1, 3).astype(np.float64)
     return np.zeros((0, 3))
+
+
+_HULL_CACHE = {}
+
+
+def mesh_shape(verts, p, q, source):
+    """A collision mesh (vertices in the geometry frame p, q) as a convex-hull
+    shape whose origin is the hull's box centre; None for a degenerate mesh."""
+    key = (np.asarray(verts, dtype=np.float64).tobytes(),)
+    hull = _HULL_CACHE.get(key)
+    if hull is None:
+        try:
+            hull = make_hull(verts)
+        except Exception:                 # flat / degenerate cloud (scipy QhullError)
+            return None
+        c = 0.5 * (hull.verts.min(0) + hull.verts.max(0))
+        hull = Hull(hull.verts - c, np.concatenate([hull.planes[:, :3], hull.planes[:, 3:] -
+                                                    hull.planes[:, :3] @ c[:, None]], 1),
+                    hull.volume, hull.com - c, hull.inertia)
+        hull.box_centre = c
+        _HULL_CACHE[key] = hull
+    brad = float(np.sqrt((hull.verts ** 2).sum(1).max()))
+    return Shape(CONVEX, (brad,), np.asarray(p) + _qmat(q) @ hull.box_centre, q, source, hull)
 
 
 def _resolve(filename, urdf_dir, asset_root):
@@ -388,13 +494,11 @@ def _geometry_shapes(col, urdf_dir, asset_root, options, warnings):
             base = os.path.basename(fn)
             if os.path.exists(path):
                 vs = _mesh_vertices(path) * np.array(scale)
-                if len(vs):
-                    lo, hi = vs.min(0), vs.max(0)
-                    c = 0.5 * (lo + hi)
-                    he = np.maximum(0.5 * (hi - lo), 1e-4)
-                    out.append(Shape(BOX, tuple(he), p + _qmat(q) @ c, q, "mesh-aabb:" + base))
+                sh = mesh_shape(vs, p, q, "mesh-hull:" + base) if len(vs) >= 4 else None
+                if sh is not None:
+                    out.append(sh)
                 else:
-                    warnings.append("mesh %s has no vertices" % fn)
+                    warnings.append("mesh %s has no volume" % fn)
             elif base in MESH_PROXIES:
                 ex = MESH_PROXIES[base]
                 out.append(Shape(BOX, (0.5 * ex[0], 0.5 * ex[1], 0.5 * ex[2]), None, None, "proxy:" + base))

@@ -28,7 +28,8 @@ MG_ARTIC_I_N = 4
 MG_ATMPL_I_N = 4
 MG_ACOLL_N = 4
 
-MG_SHAPE_SPHERE, MG_SHAPE_BOX, MG_SHAPE_CAPSULE = 0, 1, 2
+MG_SHAPE_SPHERE, MG_SHAPE_BOX, MG_SHAPE_CAPSULE, MG_SHAPE_CONVEX = 0, 1, 2, 3
+MG_HULL_HEADER, MG_HULL_MAX_VERTS, MG_HULL_MAX_FACES = 4, 32, 64
 MG_BODY_FREE, MG_BODY_STATIC, MG_BODY_LINK = 0, 1, 2
 
 _f32p = ctypes.POINTER(ctypes.c_float)
@@ -64,14 +65,16 @@ class MgModel(ctypes.Structure):
         ("num_tmpl_bodies", ctypes.c_int32), ("num_shapes", ctypes.c_int32),
         ("num_artics", ctypes.c_int32), ("num_artic_tmpls", ctypes.c_int32),
         ("num_tmpl_links", ctypes.c_int32),
-        ("reserved_i", ctypes.c_int32 * 7),
+        ("num_hull_floats", ctypes.c_int32),
+        ("reserved_i", ctypes.c_int32 * 6),
         ("body_state0", _f32p), ("body_mass", _f32p), ("body_kind", _i32p), ("body_tmpl", _i32p),
         ("tmpl_body_f", _f32p), ("tmpl_body_i", _i32p), ("shapes", _f32p),
         ("actor_root_body", _i32p), ("actor_dof", _i32p),
         ("dof_state0", _f32p), ("dof_props", _f32p),
         ("artic_i", _i32p), ("artic_tmpl_i", _i32p), ("tmpl_link_f", _f32p), ("tmpl_link_i", _i32p),
         ("actor_coll", _i32p),
-        ("reserved_p", ctypes.c_void_p * 2),
+        ("hulls", _f32p),
+        ("reserved_p", ctypes.c_void_p * 1),
     ]
 
 

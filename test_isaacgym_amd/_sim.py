@@ -244,6 +244,8 @@ class Sim:
         dof0 = np.zeros((nd, 2), dtype=np.float32)
         dprops = np.zeros((nd, N.MG_DOFPROP_N), dtype=np.float32)
         tbf, tbi, shapes = [], [], []
+        hulls, hull_off = [], {}       # MG_HULL records, offset by id(hull)
+        nhull = 0
         tb_key = {}
         artic, atmpl, lf, li = [], [], [], []
         atmpl_key = {}
@@ -288,6 +290,13 @@ class Sim:
                             rec = np.zeros(N.MG_SHAPE_STRIDE, dtype=np.float32)
                             rec[0] = sh.type
                             rec[1:1 + len(sh.size)] = sh.size
+                            if sh.type == N.MG_SHAPE_CONVEX:
+                                if id(sh.hull) not in hull_off:
+                                    r = sh.hull.record()
+                                    hull_off[id(sh.hull)] = nhull
+                                    hulls.append(r)
+                                    nhull += len(r)
+                                rec[2] = hull_off[id(sh.hull)]
                             rec[4:7] = sh.p
                             rec[7:11] = sh.q
                             rec[11] = mats[k][0]
@@ -340,6 +349,7 @@ class Sim:
             artic_tmpl_i=np.array(atmpl, dtype=np.int32).reshape(-1, N.MG_ATMPL_I_N),
             tmpl_link_f=np.array(lf, dtype=np.float32).reshape(-1, N.MG_LINK_F_N),
             tmpl_link_i=np.array(li, dtype=np.int32).reshape(-1, N.MG_LINK_I_N),
+            hulls=np.concatenate(hulls).astype(np.float32) if hulls else np.zeros(0, np.float32),
         )
         return self.model_arrays
 
@@ -357,6 +367,11 @@ class Sim:
         m.num_artic_tmpls = len(A["artic_tmpl_i"])
         m.num_tmpl_links = len(A["tmpl_link_f"])
         keep = {}
+        m.num_hull_floats = len(A.get("hulls", ()))
+        if m.num_hull_floats:
+            arr = np.ascontiguousarray(A["hulls"], dtype=np.float32)
+            keep["hulls"] = arr
+            m.hulls = arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
         for name in ("body_state0", "body_mass", "tmpl_body_f", "shapes", "dof_state0", "dof_props", "tmpl_link_f"):
             arr = np.ascontiguousarray(A[name], dtype=np.float32)
             keep[name] = arr

@@ -5,6 +5,13 @@
 // from B towards A, separation sep — negative when penetrating). Boxes are
 // (centre, rotation columns, half extents); spheres (centre, radius); capsules
 // are replaced by their two end-cap spheres (documented approximation).
+// Convex hulls (MG_SHAPE_CONVEX, the importer's hull of a mesh, at most
+// MG_HULL_MAX_VERTS vertices) against boxes and hulls: vertex penetration both
+// ways — every vertex of one shape within the margin of the other, by the
+// other's face planes (signed distance = the largest plane distance, the face
+// attaining it gives the normal) — the 4 deepest kept; against spheres /
+// capsule caps: the centre's plane distance. Edge-edge crossings without a
+// vertex inside are not detected (documented approximation).
 // Box–box is SAT over the 15 axes (face axes preferred unless an edge axis
 // separates by more than 1e-3 m), then Sutherland–Hodgman clipping of the
 // incident face against the reference face (at most 8 points, the 4 deepest
@@ -20,6 +27,7 @@ struct CShape {      // a primitive placed in the world
     V3 c;            // centre
     M3 R;            // orientation (columns = local axes)
     V3 h;            // box half extents | (radius, half height, -) for sphere / capsule
+    const float* hv; // convex: its hull record (MG_HULL_HEADER + 3 nv + 4 nf floats), else null
 };
 
 struct PairOut {
@@ -265,6 +273,113 @@ MG_HD void box_box(const CShape& A, const CShape& B, float margin, PairOut& o) {
     }
 }
 
+// ---- convex shapes as vertices + face planes (a box: 8 corners, 6 faces)
+MG_HD int cvx_nv(const CShape& S) { return S.type == MG_SHAPE_BOX ? 8 : (int)S.hv[0]; }
+MG_HD int cvx_nf(const CShape& S) { return S.type == MG_SHAPE_BOX ? 6 : (int)S.hv[1]; }
+MG_HD V3 cvx_vertex(const CShape& S, int i) {
+    V3 l;
+    if (S.type == MG_SHAPE_BOX) {
+        l = v3((i & 1) ? S.h.x : -S.h.x, (i & 2) ? S.h.y : -S.h.y, (i & 4) ? S.h.z : -S.h.z);
+    } else {
+        const float* v = S.hv + MG_HULL_HEADER + 3 * i;
+        l = v3(v[0], v[1], v[2]);
+    }
+    return vadd(S.c, mmul(S.R, l));
+}
+// local face plane f: outward unit normal nl, offset dl (n . x <= d inside)
+MG_HD void cvx_plane_l(const CShape& S, int f, V3& nl, float& dl) {
+    if (S.type == MG_SHAPE_BOX) {
+        const int ax = f >> 1;
+        const float sg = (f & 1) ? -1.0f : 1.0f;
+        nl = v3(ax == 0 ? sg : 0.0f, ax == 1 ? sg : 0.0f, ax == 2 ? sg : 0.0f);
+        dl = v3c(S.h, ax);
+    } else {
+        const float* pl = S.hv + MG_HULL_HEADER + 3 * (int)S.hv[0] + 4 * f;
+        nl = v3(pl[0], pl[1], pl[2]);
+        dl = pl[3];
+    }
+}
+// signed distance of world point p to S by its face planes (largest plane
+// distance; first face on ties), and that face
+MG_HD float cvx_sd(const CShape& S, V3 p, int& fbest) {
+    const V3 pl = mtmul(S.R, vsub(p, S.c));
+    const int nf = cvx_nf(S);
+    float best = -1e30f;
+    fbest = 0;
+    for (int f = 0; f < nf; ++f) {
+        V3 nl;
+        float dl;
+        cvx_plane_l(S, f, nl, dl);
+        const float s = vdot(nl, pl) - dl;
+        if (s > best) { best = s; fbest = f; }
+    }
+    return best;
+}
+MG_HD V3 cvx_normal(const CShape& S, int f) {
+    V3 nl;
+    float dl;
+    cvx_plane_l(S, f, nl, dl);
+    return mmul(S.R, nl);
+}
+
+// the MG_PAIR_MAXC deepest candidates, ascending separation, earlier first on ties
+struct Deep4 {
+    int n;
+    float s[MG_PAIR_MAXC];
+    V3 p[MG_PAIR_MAXC], nrm[MG_PAIR_MAXC];
+};
+MG_HD void deep4_add(Deep4& D, float s, V3 p, V3 n) {
+    if (D.n == MG_PAIR_MAXC && !(s < D.s[MG_PAIR_MAXC - 1])) return;
+    int at = 0;
+#pragma unroll
+    for (int k = 0; k < MG_PAIR_MAXC; ++k)
+        if (k < D.n && D.s[k] <= s) at = k + 1;
+#pragma unroll
+    for (int k = MG_PAIR_MAXC - 1; k > 0; --k)
+        if (k > at) { D.s[k] = D.s[k - 1]; D.p[k] = D.p[k - 1]; D.nrm[k] = D.nrm[k - 1]; }
+#pragma unroll
+    for (int k = 0; k < MG_PAIR_MAXC; ++k)
+        if (k == at) { D.s[k] = s; D.p[k] = p; D.nrm[k] = n; }
+    if (D.n < MG_PAIR_MAXC) D.n = D.n + 1;
+}
+MG_HD void deep4_emit(const Deep4& D, PairOut& o) {
+#pragma unroll
+    for (int k = 0; k < MG_PAIR_MAXC; ++k)
+        if (k < D.n) pair_push(o, D.p[k], D.nrm[k], D.s[k]);
+}
+
+// convex A vs convex B (box or hull), vertex penetration both ways
+MG_HD void convex_convex(const CShape& A, const CShape& B, float margin, PairOut& o) {
+    Deep4 D;
+    D.n = 0;
+    const int na = cvx_nv(A), nb = cvx_nv(B);
+    for (int i = 0; i < na; ++i) {           // A's vertices by B's planes: normal = B's face normal
+        const V3 v = cvx_vertex(A, i);
+        int f;
+        const float s = cvx_sd(B, v, f);
+        if (s < margin) deep4_add(D, s, v, cvx_normal(B, f));
+    }
+    for (int i = 0; i < nb; ++i) {           // B's vertices by A's planes: point on A's face, normal = -A's
+        const V3 v = cvx_vertex(B, i);
+        int f;
+        const float s = cvx_sd(A, v, f);
+        if (s < margin) {
+            const V3 na_ = cvx_normal(A, f);
+            deep4_add(D, s, vsub(v, vscale(na_, s)), vscale(na_, -1.0f));
+        }
+    }
+    deep4_emit(D, o);
+}
+
+// sphere A (centre s, radius r) vs convex B
+MG_HD void sphere_convex(V3 s, float r, const CShape& B, float margin, PairOut& o) {
+    int f;
+    const float sep = cvx_sd(B, s, f) - r;
+    if (!(sep < margin)) return;
+    const V3 n = cvx_normal(B, f);
+    pair_push(o, vsub(s, vscale(n, r)), n, sep);
+}
+
 // generic dispatch; capsules are two end-cap spheres
 MG_HD void collide(const CShape& A, const CShape& B, float margin, PairOut& o) {
     V3 ca[2], cb[2];
@@ -279,6 +394,22 @@ MG_HD void collide(const CShape& A, const CShape& B, float margin, PairOut& o) {
     ca[1] = vadd(A.c, vscale(A.R.c0, A.h.y));
     cb[0] = B.type == MG_SHAPE_CAPSULE ? vsub(B.c, vscale(B.R.c0, B.h.y)) : B.c;
     cb[1] = vadd(B.c, vscale(B.R.c0, B.h.y));
+    if (A.type == MG_SHAPE_CONVEX || B.type == MG_SHAPE_CONVEX) {
+        const bool pa = A.type == MG_SHAPE_BOX || A.type == MG_SHAPE_CONVEX;
+        const bool pb = B.type == MG_SHAPE_BOX || B.type == MG_SHAPE_CONVEX;
+        if (pa && pb) { convex_convex(A, B, margin, o); return; }
+        if (pb) {                            // sphere / capsule A vs convex B
+            for (int k = 0; k < na; ++k) sphere_convex(ca[k], ra, B, margin, o);
+            return;
+        }
+        PairOut t;                           // convex A vs sphere / capsule B: swap roles
+        t.n = 0;
+        for (int k = 0; k < nbs; ++k) sphere_convex(cb[k], rb, A, margin, t);
+#pragma unroll
+        for (int k = 0; k < MG_PAIR_MAXC; ++k)
+            if (k < t.n) pair_push(o, vadd(t.p[k], vscale(t.nrm[k], t.sep[k])), vscale(t.nrm[k], -1.0f), t.sep[k]);
+        return;
+    }
     if (B.type == MG_SHAPE_BOX) {
         for (int k = 0; k < na; ++k) sphere_box(ca[k], ra, B, margin, o);
         return;

@@ -149,21 +149,33 @@ MG_HD void env_tangents(V3 n, V3* t1, V3* t2) {
     *t2 = vcross(n, t);
 }
 
-MG_HD CShape place_shape(const float* sh, V3 x, Q4 q) {
+MG_HD CShape place_shape(const float* sh, V3 x, Q4 q, const float* hulls) {
     CShape c;
     c.type = (int)sh[0];
     c.c = vadd(x, qrot(q, v3(sh[4], sh[5], sh[6])));
     c.R = qmat(qmul(q, q4(sh[7], sh[8], sh[9], sh[10])));
     c.h = v3(sh[1], sh[2], sh[3]);
+    c.hv = c.type == MG_SHAPE_CONVEX ? hulls + (int)sh[2] : nullptr;
     return c;
 }
 
 // contacts of a placed shape with the ground plane (as mg_rigid.hip: the four
-// corners of the box face most opposed to n, sphere, capsule end caps)
+// corners of the box face most opposed to n, sphere, capsule end caps, the 4
+// deepest hull vertices)
 MG_HD void ground_pair(const MgStep& P, const CShape& s, PairOut& o) {
     const V3 n = v3(P.n[0], P.n[1], P.n[2]);
     const float off = P.contact_offset;
-    if (s.type == MG_SHAPE_BOX) {
+    if (s.type == MG_SHAPE_CONVEX) {
+        Deep4 D;
+        D.n = 0;
+        const int nv = cvx_nv(s);
+        for (int i = 0; i < nv; ++i) {
+            const V3 p = cvx_vertex(s, i);
+            const float sep = vdot(n, p) + P.pd;
+            if (sep < off) deep4_add(D, sep, p, n);
+        }
+        deep4_emit(D, o);
+    } else if (s.type == MG_SHAPE_BOX) {
         const float d0 = vdot(n, s.R.c0), d1 = vdot(n, s.R.c1), d2 = vdot(n, s.R.c2);
         const float ad0 = fabsf(d0), ad1 = fabsf(d1), ad2 = fabsf(d2);
         int ia = 0;
@@ -675,7 +687,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     V3 xa;
                     Q4 qa;
                     pair_pose(S, pa, xa, qa);
-                    const CShape ca = place_shape(sha, xa, qa);
+                    const CShape ca = place_shape(sha, xa, qa, A.hulls);
                     if (pb < 0) {
                         ground_pair(P, ca, o);
                         mu = 0.5f * (sha[11] + P.mu_ground);
@@ -685,7 +697,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         V3 xb;
                         Q4 qb;
                         pair_pose(S, pb, xb, qb);
-                        collide(ca, place_shape(shb, xb, qb), P.contact_offset, o);
+                        collide(ca, place_shape(shb, xb, qb, A.hulls), P.contact_offset, o);
                         mu = 0.5f * (sha[11] + shb[11]);
                         rest = 0.5f * (sha[12] + shb[12]);
                     }

@@ -44,6 +44,7 @@ struct MgRigidArgs {
     const float* tbf;         // [ntb][8]
     const int*   tbi;         // [ntb][4]
     const float* shapes;      // [ns][16]
+    const float* hulls;       // convex hull records (MG_SHAPE_CONVEX)
     const float* ext;         // [6][nb] world force/torque at COM, or null
     float*       cforce;      // [3][nb] net contact force out
 };
@@ -107,6 +108,7 @@ struct MgEnvArgs {
     const float* tbf;
     const int*   tbi;
     const float* shapes;
+    const float* hulls;       // convex hull records (MG_SHAPE_CONVEX)
     float*       dof_pos;
     float*       dof_vel;
     const float* dof_tpos;
@@ -148,6 +150,7 @@ struct MgRenderArgs {
     const MgRenderCam*  cams;
     const float*        state;     // snapshot [13][nb]
     const float*        shapes;
+    const float*        hulls;
     const MgRShape*     rshapes;
     const int*          env_shape_first;   // [nenv + 1]
     int                 has_ground;

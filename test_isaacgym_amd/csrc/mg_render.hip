@@ -35,6 +35,7 @@ struct WS {
     V3    h;        // box half extents; sphere (radius, 0, 0); capsule (radius, half length, 0)
     float brad;     // bounding radius
     float brad2;    // (padded bounding radius)^2 of the per-ray rejection tests
+    const float* hv;   // convex: hull record
 };
 
 // Per-pixel arithmetic uses explicit fused multiply-adds (fmaf: correctly
@@ -116,7 +117,26 @@ __device__ __forceinline__ float ray_capsule(V3 o, V3 d, const WS& s, float tmin
     return t;
 }
 
+// convex hull: clip the ray by the face planes in the hull frame (entry point only)
+__device__ __forceinline__ float ray_convex(V3 o, V3 d, const WS& s, float tmin, float tmax) {
+    const V3 ol = fmt(s.R, vsub(o, s.c));
+    const V3 dl = fmt(s.R, d);
+    const int nv = (int)s.hv[0], nf = (int)s.hv[1];
+    const float* pl = s.hv + MG_HULL_HEADER + 3 * nv;
+    float tn = -__builtin_inff(), tf = tmax;
+    for (int f = 0; f < nf; ++f) {
+        const V3 n = v3(pl[4 * f + 0], pl[4 * f + 1], pl[4 * f + 2]);
+        const float dist = fdot(n, ol) - pl[4 * f + 3];
+        const float den = fdot(n, dl);
+        if (den < 0.0f) tn = fmaxf(tn, -dist / den);
+        else if (den > 0.0f) tf = fminf(tf, -dist / den);
+        else if (dist > 0.0f) return __builtin_inff();
+    }
+    return (tn <= tf && tn >= tmin) ? tn : __builtin_inff();
+}
+
 __device__ __forceinline__ float ray_shape(V3 o, V3 d, const WS& s, float tmin, float tmax) {
+    if (s.type == MG_SHAPE_CONVEX) return ray_convex(o, d, s, tmin, tmax);
     if (s.type == MG_SHAPE_BOX) return ray_box(o, d, s, tmin, tmax);
     if (s.type == MG_SHAPE_SPHERE) return ray_sphere(o, d, s.c, s.h.x, tmin);
     return ray_capsule(o, d, s, tmin);
@@ -135,6 +155,19 @@ __device__ __forceinline__ V3 shape_normal(const WS& s, V3 p) {
         const V3 axis = k == 0 ? s.R.c0 : (k == 1 ? s.R.c1 : s.R.c2);
         const float sg = (k == 0 ? pl.x : (k == 1 ? pl.y : pl.z)) < 0.0f ? -1.0f : 1.0f;
         return vscale(axis, sg);
+    }
+    if (s.type == MG_SHAPE_CONVEX) {            // the face plane the point is farthest out of
+        const V3 pl = fmt(s.R, dp);
+        const int nv = (int)s.hv[0], nf = (int)s.hv[1];
+        const float* pp = s.hv + MG_HULL_HEADER + 3 * nv;
+        float best = -__builtin_inff();
+        V3 nl = v3(0.0f, 0.0f, 1.0f);
+        for (int f = 0; f < nf; ++f) {
+            const V3 n = v3(pp[4 * f + 0], pp[4 * f + 1], pp[4 * f + 2]);
+            const float dist = fdot(n, pl) - pp[4 * f + 3];
+            if (dist > best) { best = dist; nl = n; }
+        }
+        return fma3(s.R.c2, nl.z, fma3(s.R.c1, nl.y, vscale(s.R.c0, nl.x)));
     }
     float t = fdot(dp, s.R.c0);
     t = fminf(fmaxf(t, -s.h.y), s.h.y);
@@ -312,10 +345,14 @@ __global__ void __launch_bounds__(256) k_render(MgRenderArgs A) {
             } else if (w.type == MG_SHAPE_SPHERE) {
                 w.h = v3(sh[1], 0.0f, 0.0f);
                 w.brad = sh[1];
+            } else if (w.type == MG_SHAPE_CONVEX) {
+                w.h = v3(sh[1], 0.0f, 0.0f);
+                w.brad = sh[1];
             } else {
                 w.h = v3(sh[1], sh[2], 0.0f);
                 w.brad = sh[1] + sh[2];
             }
+            w.hv = w.type == MG_SHAPE_CONVEX ? A.hulls + (int)sh[2] : nullptr;
             {
                 const float rp = w.brad * 1.01f + 1e-3f;
                 w.brad2 = rp * rp;
@@ -326,10 +363,17 @@ __global__ void __launch_bounds__(256) k_render(MgRenderArgs A) {
             // points are hits and they all lie behind the near plane).
             const V3 ol = fmt(w.R, vsub(C.o, w.c));      // as in ray_box / ray_sphere
             const V3 os = vsub(C.o, w.c);
+            bool in_hull = w.type == MG_SHAPE_CONVEX;
+            if (in_hull) {                      // strictly inside every face plane (as ray_convex)
+                const int nv = (int)w.hv[0], nf = (int)w.hv[1];
+                const float* pp = w.hv + MG_HULL_HEADER + 3 * nv;
+                for (int f = 0; f < nf; ++f)
+                    in_hull = in_hull && fdot(v3(pp[4 * f], pp[4 * f + 1], pp[4 * f + 2]), ol) - pp[4 * f + 3] < 0.0f;
+            }
             const bool inside =
                 C.near_plane > 0.0f &&
                 ((w.type == MG_SHAPE_BOX && fabsf(ol.x) < w.h.x && fabsf(ol.y) < w.h.y && fabsf(ol.z) < w.h.z) ||
-                 (w.type == MG_SHAPE_SPHERE && fmaf(-w.h.x, w.h.x, fdot(os, os)) < 0.0f));
+                 (w.type == MG_SHAPE_SPHERE && fmaf(-w.h.x, w.h.x, fdot(os, os)) < 0.0f) || in_hull);
             keep = !inside && in_rows(w.c, w.brad * 1.001f + 1e-4f);
             // ground shadow culling: the ground points whose shadow ray (from 1e-3
             // above the plane, towards L) passes within the bounding radius of

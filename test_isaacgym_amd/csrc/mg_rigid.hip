@@ -139,9 +139,11 @@ __device__ __forceinline__ void contact_friction(const B& G, Slot& c, V3& v, V3&
 }
 
 // Candidates of one shape: emit(k, point, separation, mu, e) with k the static
-// candidate index within the shape (box corner bits zyx, capsule end 0/1).
+// candidate index within the shape (box corner bits zyx, capsule end 0/1, the
+// k-th deepest hull vertex).
 template <class B, class F>
-__device__ __forceinline__ void shape_candidates(const B& G, const MgStep& P, const float* sh, Q4 q, V3 x, F&& emit) {
+__device__ __forceinline__ void shape_candidates(const B& G, const MgStep& P, const float* sh, Q4 q, V3 x,
+                                                 const float* hulls, F&& emit) {
     const int type = (int)sh[0];
     const Q4 qs = qmul(q, q4(sh[7], sh[8], sh[9], sh[10]));
     const V3 cs = vadd(x, qrot(q, v3(sh[4], sh[5], sh[6])));
@@ -185,6 +187,35 @@ __device__ __forceinline__ void shape_candidates(const B& G, const MgStep& P, co
             const V3 c = k ? vadd(cs, ax) : vsub(cs, ax);
             emit(k, G.addn(c, -rad), G.dn(c) + P.pd - rad, mu, e);
         }
+    } else if (type == MG_SHAPE_CONVEX) {
+        // the 4 deepest hull vertices within the contact offset, ascending
+        // separation, lower vertex index first on ties
+        const float* hv = hulls + (int)sh[2];
+        const int nv = (int)hv[0];
+        float ks[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        V3 kp[4];
+        int kn = 0;
+        for (int i = 0; i < nv; ++i) {
+            const float* v = hv + MG_HULL_HEADER + 3 * i;
+            const V3 p = vadd(cs, qrot(qs, v3(v[0], v[1], v[2])));
+            const float sep = G.dn(p) + P.pd;
+            if (!(sep < P.contact_offset)) continue;
+            if (kn == 4 && !(sep < ks[3])) continue;
+            int at = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < kn && ks[k] <= sep) at = k + 1;
+#pragma unroll
+            for (int k = 3; k > 0; --k)
+                if (k > at) { ks[k] = ks[k - 1]; kp[k] = kp[k - 1]; }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k == at) { ks[k] = sep; kp[k] = p; }
+            if (kn < 4) kn = kn + 1;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < kn) emit(k, kp[k], ks[k], mu, e);
     }
 }
 
@@ -256,7 +287,7 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
             if constexpr (!MULTI) {
                 // static slots: candidate k of the only shape lives in slot k
                 if (nsh == 1)
-                shape_candidates(G, P, A.shapes + sh0 * MG_SHAPE_STRIDE, q, x,
+                shape_candidates(G, P, A.shapes + sh0 * MG_SHAPE_STRIDE, q, x, A.hulls,
                                  [&](int k, V3 p, float sep, float mu, float e) {
                                      if (sep < P.contact_offset) {
                                          sl[k].on = true;
@@ -270,7 +301,7 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
                 // several shapes: shift-register insert, newest candidate in slot 0
                 int nc = 0;
                 for (int s = sh0; s < sh0 + nsh; ++s) {
-                    shape_candidates(G, P, A.shapes + s * MG_SHAPE_STRIDE, q, x,
+                    shape_candidates(G, P, A.shapes + s * MG_SHAPE_STRIDE, q, x, A.hulls,
                                      [&](int, V3 p, float sep, float mu, float e) {
                                          if (sep < P.contact_offset && nc < MAXC) {
 #pragma unroll

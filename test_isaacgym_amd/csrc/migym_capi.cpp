@@ -91,6 +91,7 @@ struct mg_sim {
     float* d_tbf = nullptr;
     int* d_tbi = nullptr;
     float* d_shapes = nullptr;
+    float* d_hulls = nullptr;     // convex hull records (MG_SHAPE_CONVEX)
     int* d_actor_root = nullptr;  // [na] internal slot of each actor's root body
     int* d_actor_dof = nullptr;   // [na+1]
     float* d_cforce = nullptr;    // [3][nb]
@@ -253,7 +254,7 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
 }
 
 void free_all(mg_sim* s) {
-    void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_tbi, s->d_shapes,
+    void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_tbi, s->d_shapes, s->d_hulls,
                     s->d_actor_root, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
                     s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
                     s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
@@ -336,6 +337,18 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         if (t < 0 || t >= s->ntb) return fail(MG_ERR_ARG, "body %d: template %d out of range", b, t);
         const int s0 = m->tmpl_body_i[t * MG_TBODY_I_N + 0], sc = m->tmpl_body_i[t * MG_TBODY_I_N + 1];
         if (s0 < 0 || sc < 0 || s0 + sc > s->ns) return fail(MG_ERR_ARG, "template body %d: bad shape range", t);
+    }
+    for (int k = 0; k < s->ns; ++k) {
+        const float* sh = m->shapes + (size_t)k * MG_SHAPE_STRIDE;
+        const int t = (int)sh[0];
+        if (t < MG_SHAPE_SPHERE || t > MG_SHAPE_CONVEX) return fail(MG_ERR_ARG, "shape %d: unknown type %d", k, t);
+        if (t != MG_SHAPE_CONVEX) continue;
+        const long off = (long)sh[2], nh = m->hulls ? m->num_hull_floats : 0;
+        if (off < 0 || off + MG_HULL_HEADER > nh) return fail(MG_ERR_ARG, "shape %d: hull offset %ld out of range", k, off);
+        const int nv = (int)m->hulls[off], nfc = (int)m->hulls[off + 1];
+        if (nv < 4 || nv > MG_HULL_MAX_VERTS || nfc < 4 || nfc > MG_HULL_MAX_FACES ||
+            off + MG_HULL_HEADER + 3L * nv + 4L * nfc > nh)
+            return fail(MG_ERR_ARG, "shape %d: bad hull record (%d vertices, %d faces)", k, nv, nfc);
     }
     for (int a = 0; a < na; ++a) {
         if (m->actor_root_body[a] < 0 || m->actor_root_body[a] >= nb) return fail(MG_ERR_ARG, "actor %d: bad root", a);
@@ -622,6 +635,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(dalloc(&s->d_tbf, (size_t)s->ntb * MG_TBODY_F_N));
     HIP_TRY(dalloc(&s->d_tbi, (size_t)s->ntb * MG_TBODY_I_N));
     HIP_TRY(dalloc(&s->d_shapes, (size_t)s->ns * MG_SHAPE_STRIDE));
+    HIP_TRY(dalloc(&s->d_hulls, (size_t)(m->hulls ? m->num_hull_floats : 0)));
     HIP_TRY(dalloc(&s->d_actor_root, na));
     HIP_TRY(dalloc(&s->d_actor_dof, na + 1));
     HIP_TRY(dalloc(&s->d_cforce, (size_t)nb * 3));
@@ -650,6 +664,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(h2d(s->d_tbf, m->tmpl_body_f, (size_t)s->ntb * MG_TBODY_F_N * sizeof(float)));
     HIP_TRY(h2d(s->d_tbi, m->tmpl_body_i, (size_t)s->ntb * MG_TBODY_I_N * sizeof(int)));
     HIP_TRY(h2d(s->d_shapes, m->shapes, (size_t)s->ns * MG_SHAPE_STRIDE * sizeof(float)));
+    if (m->hulls) HIP_TRY(h2d(s->d_hulls, m->hulls, (size_t)m->num_hull_floats * sizeof(float)));
     HIP_TRY(h2d(s->d_actor_root, root_int.data(), (size_t)na * sizeof(int)));
     HIP_TRY(h2d(s->d_actor_dof, m->actor_dof, (size_t)(na + 1) * sizeof(int)));
     HIP_TRY(hipMemset(s->d_cforce, 0, (size_t)nb * 3 * sizeof(float)));
@@ -728,7 +743,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.link_f = s->d_link_f + (size_t)(g.tmpl >= 0 ? g.first_link : 0) * MG_LINK_F_N;
         A.link_i = s->d_link_i + (size_t)(g.tmpl >= 0 ? g.first_link : 0) * MG_LINK_I_N;
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
-        A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes;
+        A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes; A.hulls = s->d_hulls;
         A.dof_pos = s->d_dof; A.dof_vel = s->d_dof + s->nd;
         A.dof_tpos = s->d_dof_tgt; A.dof_tvel = s->d_dof_tgt + s->nd; A.dof_force = s->d_dof_tgt + 2 * (size_t)s->nd;
         A.dof_props = s->d_dof_props;
@@ -741,7 +756,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         MgRigidArgs A{};
         A.nf = s->nf_rigid; A.nf1 = s->nf1; A.nb = s->nb; A.free_ids = nullptr;   // internal slots 0..nf-1
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
-        A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes;
+        A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes; A.hulls = s->d_hulls;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
         A.cforce = s->d_cforce;
         HIP_TRY(mg_launch_rigid_step(P, A, st));
@@ -1063,6 +1078,7 @@ int32_t mg_render_cameras(mg_sim* s, const mg_camera* cams, int32_t n, void* str
     }
     MgRenderArgs A{};
     A.ncam = n; A.nb = s->nb; A.cams = s->d_cams; A.state = s->d_rstate; A.shapes = s->d_shapes;
+    A.hulls = s->d_hulls;
     A.uniform_nblk = s->cam_dev[0].nblk;
     for (int i = 1; i < n; ++i)
         if (s->cam_dev[i].nblk != A.uniform_nblk) { A.uniform_nblk = 0; break; }

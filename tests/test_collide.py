@@ -144,3 +144,85 @@ def test_capsule_as_two_spheres():
     assert len(out) == 2
     assert np.allclose(out[:, 6], 0.0, atol=1e-6)
     assert np.allclose(sorted(out[:, 0]), [-0.2, 0.2], atol=1e-6)
+
+
+# ---------------------------------------------------------------- convex hulls
+CONVEX = 3
+
+
+def _hull_of_box(h):
+    from test_isaacgym_amd import _assets
+    pts = np.array([[sx * h[0], sy * h[1], sz * h[2]] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)])
+    return _assets.make_hull(pts)
+
+
+def test_hull_mass_properties_match_analytic_box():
+    hull = _hull_of_box((0.1, 0.2, 0.3))
+    a, b, c = 0.2, 0.4, 0.6
+    assert hull.volume == __import__("pytest").approx(a * b * c, rel=1e-12)
+    assert np.allclose(hull.com, 0.0, atol=1e-12)
+    V = a * b * c
+    assert np.allclose(np.diag(hull.inertia), [V * (b * b + c * c) / 12, V * (a * a + c * c) / 12,
+                                               V * (a * a + b * b) / 12], rtol=1e-9)
+    assert len(hull.verts) == 8 and len(hull.planes) == 6          # coplanar triangles merged
+
+
+def test_hull_of_box_matches_box_box_face_contact():
+    """A box as a convex hull against a box: vertex penetration gives the same
+    deepest separation and normal as the SAT / clipping box-box path for a
+    face contact (random tilts of the upper box, small overlaps)."""
+    rng = np.random.RandomState(3)
+    h = np.array([0.05, 0.04, 0.03])
+    rec = _hull_of_box(h).record()
+    for _ in range(50):
+        q = _quat(rng.normal(size=3), rng.uniform(-0.3, 0.3))
+        R = _rot(q)
+        low = np.abs(R[2, :]) @ h                                     # half height of the tilted box
+        c = np.array([rng.uniform(-0.02, 0.02), rng.uniform(-0.02, 0.02), 0.2 + low - rng.uniform(0.0, 0.004)])
+        B = _shape(BOX, (0, 0, 0), (0, 0, 0, 1), (0.3, 0.3, 0.2))
+        A_box = _shape(BOX, c, q, h)
+        A_hull = _shape(CONVEX, c, q, (float(np.linalg.norm(h)), 0, 0))
+        rb = oracle.collide(A_box, B, 0.01)
+        rh = oracle.collide(A_hull, B, 0.01, hull_a=rec)
+        assert len(rb) and len(rh)
+        assert rh[:, 6].min() == __import__("pytest").approx(rb[:, 6].min(), abs=2e-6)
+        assert np.allclose(rh[np.argmin(rh[:, 6]), 3:6], [0, 0, 1], atol=1e-5)
+
+
+def test_hull_against_ground_and_sphere():
+    from test_isaacgym_amd import _assets
+    # octahedron, radius 0.1, one vertex 2 mm into a box below; a sphere resting on a face
+    pts = np.array([[0.1, 0, 0], [-0.1, 0, 0], [0, 0.1, 0], [0, -0.1, 0], [0, 0, 0.1], [0, 0, -0.1]])
+    hull = _assets.make_hull(pts)
+    rec = hull.record()
+    assert len(hull.planes) == 8
+    A = _shape(CONVEX, (0, 0, 0.098), (0, 0, 0, 1), (0.1, 0, 0))
+    B = _shape(BOX, (0, 0, -0.5), (0, 0, 0, 1), (1, 1, 0.5))
+    r = oracle.collide(A, B, 0.001, hull_a=rec)
+    assert len(r) == 1 and r[0, 6] == __import__("pytest").approx(-0.002, abs=1e-6)
+    assert np.allclose(r[0, :3], [0, 0, -0.002], atol=1e-6) and np.allclose(r[0, 3:6], [0, 0, 1])
+    # sphere (A) of radius 0.05 touching face (1,1,1)/sqrt3 of the octahedron (B)
+    n = np.ones(3) / math.sqrt(3)
+    dface = 0.1 / math.sqrt(3)
+    S = _shape(SPHERE, n * (dface + 0.05 - 0.001), (0, 0, 0, 1), (0.05, 0, 0))
+    r = oracle.collide(S, _shape(CONVEX, (0, 0, 0), (0, 0, 0, 1), (0.1, 0, 0)), 0.01, hull_b=rec)
+    assert len(r) == 1 and r[0, 6] == __import__("pytest").approx(-0.001, abs=1e-6)
+    assert np.allclose(r[0, 3:6], n, atol=1e-6)
+
+
+def test_reference_franka_meshes_become_hulls():
+    import os
+    from isaacgym import gymapi
+    from conftest import REFERENCE
+    from test_isaacgym_amd import _assets
+    root = os.path.join(REFERENCE, "assets")
+    if not os.path.isdir(root):
+        __import__("pytest").skip("reference tree not present")
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    a = _assets.load_urdf(root, "urdf/franka_description/robots/franka_panda.urdf", opts)
+    shapes = [s for b in a.bodies for s in b.shapes]
+    assert all(s.type == _assets.CONVEX for s in shapes) and len(shapes) == 11
+    assert all(4 <= len(s.hull.verts) <= 32 and len(s.hull.planes) <= 64 for s in shapes)
+    # mass from the hulls at density 1000 (no <inertial> in the URDF)
+    assert a.mass_props[1].mass == __import__("pytest").approx(1000 * shapes[1].hull.volume, rel=1e-9)

@@ -129,6 +129,10 @@ def test_franka_joint_held_at_limit(gym):
     A = sim.build_model()
     props = A["dof_props"].copy()
     lo, hi = props[3, 5], props[3, 6]
+    # the other arm joints hold their pose (position drives), so the reaction of
+    # joint 4's effort does not swing the arm into the table
+    for j in (0, 1, 2, 4, 5, 6):
+        props[j, 0], props[j, 1], props[j, 2] = 1.0, 400.0, 40.0
     p, m = sim.mg_params(), sim.mg_model()
     st = A["body_state0"].copy()
     dof = A["dof_state0"].copy()

@@ -8,6 +8,8 @@ hard assertion is |gpu - oracle| <= 1e-5 * max(1, |x|) per element (positions
 up to ~1e3 m, velocities up to 1e3 m/s), and bit-exactness is asserted
 separately so a drift in either build shows up by name.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -123,6 +125,58 @@ def test_primitive_drops_parity(gym):
     assert np.array_equal(ncf.cpu().numpy(), cf)
     # physics sanity: everything came to rest on the ground
     assert np.all(got[:, 2] > 0.05) and np.all(got[:, 2] < 0.6)
+
+
+def _mesh_urdf(tmp, name, verts, extra_box=False):
+    """A single-link URDF whose collision is a mesh (vertex-only OBJ) and
+    optionally a box as a second shape."""
+    with open(os.path.join(tmp, name + ".obj"), "w") as f:
+        for v in verts:
+            f.write("v %.9g %.9g %.9g\n" % tuple(v))
+    box = ('<collision><origin xyz="0 0 0.15"/><geometry><box size="0.2 0.1 0.1"/></geometry></collision>'
+           if extra_box else "")
+    with open(os.path.join(tmp, name + ".urdf"), "w") as f:
+        f.write('<robot name="%s"><link name="body"><collision><origin xyz="0.02 0 0" rpy="0.3 0 0"/>'
+                '<geometry><mesh filename="%s.obj"/></geometry></collision>%s</link></robot>' % (name, name, box))
+    return name + ".urdf"
+
+
+def test_hull_drops_parity(gym, tmp_path):
+    """Convex-hull free bodies (random point clouds -> hulls of <= 32 vertices;
+    one single-shape, one hull + box) dropped onto the ground: the hull branch
+    of the free-body kernel (static and shift-register slots), 180 frames, bit
+    for bit."""
+    rng = np.random.RandomState(5)
+    files = []
+    for k in range(3):
+        pts = rng.normal(size=(60, 3)) * np.array([0.15, 0.1, 0.08])
+        files.append(_mesh_urdf(str(tmp_path), "cloud%d" % k, pts, extra_box=(k == 2)))
+    sp = scenes.servo_sim_params(True)
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim, plane)
+    assets = [gym.load_asset(sim, str(tmp_path), f, gymapi.AssetOptions()) for f in files]
+    assert all(a.bodies[0].shapes[0].type == 3 for a in assets)
+    for i in range(48):
+        env = gym.create_env(sim, gymapi.Vec3(-2, -2, 0), gymapi.Vec3(2, 2, 2), 8)
+        q = gymapi.Quat(*rng.randn(4)).normalize()
+        pose = gymapi.Transform(gymapi.Vec3(0, 0, 0.3 + rng.rand()), q)
+        gym.create_actor(env, assets[i % 3], pose, "obj", i, 0)
+    gym.prepare_sim(sim)
+    _, rb, _, ncf = _tensors(gym, sim)
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    for _ in range(180):
+        gym.simulate(sim)
+        cf = oracle.step(p, m, st, np.zeros((0, 2), np.float32))
+    gym.refresh_rigid_body_state_tensor(sim)
+    gym.refresh_net_contact_force_tensor(sim)
+    got = rb.cpu().numpy()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+    assert np.array_equal(ncf.cpu().numpy(), cf)
+    assert np.all(got[:, 2] > 0.0) and np.all(got[:, 2] < 0.5)          # at rest on the ground
+    assert np.all(np.abs(got[:, 7:10]) < 0.05)
 
 
 def test_gimbal_parity(gym):

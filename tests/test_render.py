@@ -46,7 +46,7 @@ def _oracle_image(sim, state, cam):
     first, color, seg = _render.body_render_arrays(sim)
     rec = _render.camera_record(sim, cam)
     return oracle.render(sim.mg_params(), state, A["body_tmpl"], A["tmpl_body_i"], A["shapes"], first, color, seg,
-                         rec)
+                         rec, hulls=A["hulls"])
 
 
 def _ball_features(rgba):
