@@ -346,6 +346,39 @@ static void collide_(const cshape_t* A, const cshape_t* B, float margin, pair_t*
         for (m = 0; m < nbs; ++m) sph_sph_(ca[k], ra, cb[m], rb, margin, o);
 }
 
+/* pair screen (mg_env.hip pair_near): part of the narrow phase's definition */
+static float bound_radius_(const float* sh) {
+    const int t = (int)sh[0];
+    if (t == MG_SHAPE_BOX) return sqrtf(sh[1] * sh[1] + sh[2] * sh[2] + sh[3] * sh[3]);
+    if (t == MG_SHAPE_CAPSULE) return sh[1] + sh[2];
+    return sh[1];
+}
+static int sphere_near_box_(v3_t c, float r, const float* shb, v3_t xb, q4_t qb, float off) {
+    const v3_t cb = add3(xb, qrot_(qb, V(shb[4], shb[5], shb[6])));
+    const m3_t Rb = qmat_(qmul_(qb, Q(shb[7], shb[8], shb[9], shb[10])));
+    const v3_t loc = mtv_(Rb, sub3(c, cb));
+    const v3_t e = V(loc.x - fminf(fmaxf(loc.x, -shb[1]), shb[1]), loc.y - fminf(fmaxf(loc.y, -shb[2]), shb[2]),
+                     loc.z - fminf(fmaxf(loc.z, -shb[3]), shb[3]));
+    const float rr = r + off;
+    return dot3(e, e) < rr * rr * 1.0001f + 1e-6f;
+}
+static int pair_near_(const step_t* P, const float* sha, v3_t xa, q4_t qa, const float* shb, v3_t xb, q4_t qb,
+                      int ground) {
+    const v3_t cA = add3(xa, qrot_(qa, V(sha[4], sha[5], sha[6])));
+    const float rA = bound_radius_(sha);
+    v3_t cB, d;
+    float rB, rr;
+    if (ground) return dot3(P->n, cA) + P->pd - rA < P->co;
+    cB = add3(xb, qrot_(qb, V(shb[4], shb[5], shb[6])));
+    rB = bound_radius_(shb);
+    d = sub3(cB, cA);
+    rr = rA + rB + P->co;
+    if (!(dot3(d, d) < rr * rr * 1.0001f + 1e-6f)) return 0;
+    if ((int)shb[0] == MG_SHAPE_BOX && !sphere_near_box_(cA, rA, shb, xb, qb, P->co)) return 0;
+    if ((int)sha[0] == MG_SHAPE_BOX && !sphere_near_box_(cB, rB, sha, xa, qa, P->co)) return 0;
+    return 1;
+}
+
 static void tangents_(v3_t n, v3_t* t1, v3_t* t2) {
     v3_t a = V(1.0f, 0.0f, 0.0f), t;
     float inv;
@@ -810,6 +843,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             sA = place_(sha, xa, qa, m->hulls);
             o.n = 0;
             if (pp->b < 0) {
+                if (!pair_near_(P, sha, xa, qa, sha, xa, qa, 1)) continue;
                 ground_pair_(P, &sA, &o);
                 mu = 0.5f * (sha[11] + P->mu_g);
                 rest = 0.5f * (sha[12] + P->e_g);
@@ -826,6 +860,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     xb = xl[pp->b];
                     qb = ql[pp->b];
                 }
+                if (!pair_near_(P, sha, xa, qa, shb, xb, qb, 0)) continue;
                 sB = place_(shb, xb, qb, m->hulls);
                 collide_(&sA, &sB, P->co, &o);
                 mu = 0.5f * (sha[11] + shb[11]);

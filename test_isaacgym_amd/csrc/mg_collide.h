@@ -300,18 +300,49 @@ MG_HD void cvx_plane_l(const CShape& S, int f, V3& nl, float& dl) {
     }
 }
 // signed distance of world point p to S by its face planes (largest plane
-// distance; first face on ties), and that face
-MG_HD float cvx_sd(const CShape& S, V3 p, int& fbest) {
+// distance; first face on ties), and that face. Callers only use a result with
+// best - r < margin: the scan stops at the first face that makes that false
+// (the maximum can only grow), which leaves every used result unchanged.
+MG_HD float cvx_sd(const CShape& S, V3 p, int& fbest, float r, float margin) {
     const V3 pl = mtmul(S.R, vsub(p, S.c));
     const int nf = cvx_nf(S);
     float best = -1e30f;
     fbest = 0;
+    if (S.type == MG_SHAPE_CONVEX) {
+        // hull planes in batches of 4: the batch's loads are all in flight
+        // before the in-order scan of its faces
+        const float* P = S.hv + MG_HULL_HEADER + 3 * (int)S.hv[0];
+        for (int f0 = 0; f0 < nf; f0 += 4) {
+            float c[4][4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float* q = P + 4 * (f0 + k < nf ? f0 + k : nf - 1);
+                c[k][0] = q[0]; c[k][1] = q[1]; c[k][2] = q[2]; c[k][3] = q[3];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (f0 + k < nf) {
+                    const float s = vdot(v3(c[k][0], c[k][1], c[k][2]), pl) - c[k][3];
+                    if (s > best) {
+                        best = s;
+                        fbest = f0 + k;
+                        if (!(best - r < margin)) return best;
+                    }
+                }
+            }
+        }
+        return best;
+    }
     for (int f = 0; f < nf; ++f) {
         V3 nl;
         float dl;
         cvx_plane_l(S, f, nl, dl);
         const float s = vdot(nl, pl) - dl;
-        if (s > best) { best = s; fbest = f; }
+        if (s > best) {
+            best = s;
+            fbest = f;
+            if (!(best - r < margin)) break;
+        }
     }
     return best;
 }
@@ -356,13 +387,13 @@ MG_HD void convex_convex(const CShape& A, const CShape& B, float margin, PairOut
     for (int i = 0; i < na; ++i) {           // A's vertices by B's planes: normal = B's face normal
         const V3 v = cvx_vertex(A, i);
         int f;
-        const float s = cvx_sd(B, v, f);
+        const float s = cvx_sd(B, v, f, 0.0f, margin);
         if (s < margin) deep4_add(D, s, v, cvx_normal(B, f));
     }
     for (int i = 0; i < nb; ++i) {           // B's vertices by A's planes: point on A's face, normal = -A's
         const V3 v = cvx_vertex(B, i);
         int f;
-        const float s = cvx_sd(A, v, f);
+        const float s = cvx_sd(A, v, f, 0.0f, margin);
         if (s < margin) {
             const V3 na_ = cvx_normal(A, f);
             deep4_add(D, s, vsub(v, vscale(na_, s)), vscale(na_, -1.0f));
@@ -374,7 +405,7 @@ MG_HD void convex_convex(const CShape& A, const CShape& B, float margin, PairOut
 // sphere A (centre s, radius r) vs convex B
 MG_HD void sphere_convex(V3 s, float r, const CShape& B, float margin, PairOut& o) {
     int f;
-    const float sep = cvx_sd(B, s, f) - r;
+    const float sep = cvx_sd(B, s, f, r, margin) - r;
     if (!(sep < margin)) return;
     const V3 n = cvx_normal(B, f);
     pair_push(o, vsub(s, vscale(n, r)), n, sep);

@@ -215,6 +215,33 @@ MG_HD float bound_radius(const float* sh) {
 }
 
 
+// Pair screen (part of the narrow phase's definition; the oracle applies the
+// same test): a pair can only produce contacts when the bounding sphere of A
+// (centre cA, radius rA) comes within the contact offset of the ground plane,
+// of B's bounding sphere, and — when B (or A) is a box — of that box itself.
+MG_HD bool sphere_near_box(V3 c, float r, const float* shb, V3 xb, Q4 qb, float off) {
+    const V3 cb = vadd(xb, qrot(qb, v3(shb[4], shb[5], shb[6])));
+    const M3 Rb = qmat(qmul(qb, q4(shb[7], shb[8], shb[9], shb[10])));
+    const V3 loc = mtmul(Rb, vsub(c, cb));
+    const V3 e = v3(loc.x - fminf(fmaxf(loc.x, -shb[1]), shb[1]), loc.y - fminf(fmaxf(loc.y, -shb[2]), shb[2]),
+                    loc.z - fminf(fmaxf(loc.z, -shb[3]), shb[3]));
+    const float rr = r + off;
+    return vdot(e, e) < rr * rr * 1.0001f + 1e-6f;
+}
+MG_HD bool pair_near(const MgStep& P, const float* sha, V3 xa, Q4 qa, const float* shb, V3 xb, Q4 qb, bool ground) {
+    const V3 cA = vadd(xa, qrot(qa, v3(sha[4], sha[5], sha[6])));
+    const float rA = bound_radius(sha);
+    if (ground) return vdot(v3(P.n[0], P.n[1], P.n[2]), cA) + P.pd - rA < P.contact_offset;
+    const V3 cB = vadd(xb, qrot(qb, v3(shb[4], shb[5], shb[6])));
+    const float rB = bound_radius(shb);
+    const V3 d = vsub(cB, cA);
+    const float rr = rA + rB + P.contact_offset;
+    if (!(vdot(d, d) < rr * rr * 1.0001f + 1e-6f)) return false;
+    if ((int)shb[0] == MG_SHAPE_BOX && !sphere_near_box(cA, rA, shb, xb, qb, P.contact_offset)) return false;
+    if ((int)sha[0] == MG_SHAPE_BOX && !sphere_near_box(cB, rB, sha, xa, qa, P.contact_offset)) return false;
+    return true;
+}
+
 // Articulated-body algorithm in the world frame about the base origin x0 (RBDA
 // ch. 7 with all quantities in one frame: no spatial transforms in the inward
 // pass). Every lane of the workgroup calls it (the barriers are shared); `act`
@@ -652,20 +679,11 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     const int* pp = A.pairs + (size_t)(pair0 + pi) * 4;
                     const int pa = pp[0], sa = pp[1], pb = pp[2], sb = pp[3];
                     const float* sha = A.shapes + sa * MG_SHAPE_STRIDE;
-                    V3 xa, xb;
-                    Q4 qa, qb;
+                    V3 xa, xb = v3(0.0f, 0.0f, 0.0f);
+                    Q4 qa, qb = q4(0.0f, 0.0f, 0.0f, 1.0f);
                     pair_pose(S, pa, xa, qa);
-                    const V3 cA = vadd(xa, qrot(qa, v3(sha[4], sha[5], sha[6])));
-                    const float rA = bound_radius(sha);
-                    if (pb < 0) {
-                        near = vdot(v3(P.n[0], P.n[1], P.n[2]), cA) + P.pd - rA < P.contact_offset;
-                    } else {
-                        const float* shb = A.shapes + sb * MG_SHAPE_STRIDE;
-                        pair_pose(S, pb, xb, qb);
-                        const V3 d = vsub(vadd(xb, qrot(qb, v3(shb[4], shb[5], shb[6]))), cA);
-                        const float rr = rA + bound_radius(shb) + P.contact_offset;
-                        near = vdot(d, d) < rr * rr * 1.0001f + 1e-6f;
-                    }
+                    if (pb >= 0) pair_pose(S, pb, xb, qb);
+                    near = pair_near(P, sha, xa, qa, pb >= 0 ? A.shapes + sb * MG_SHAPE_STRIDE : sha, xb, qb, pb < 0);
                 }
                 const unsigned gm = (unsigned)((__ballot(near) >> (gi * G)) & 0xFFFFull);
                 if (near) S.npl[nnear + __popc(gm & ((1u << ln) - 1u))] = pi;
