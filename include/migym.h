@@ -83,7 +83,12 @@ extern "C" {
 #define MG_LINK_F_N       16  /* joint origin p[3], q[4] (parent link frame), axis[3] (joint frame), pad[6] */
 #define MG_LINK_I_N        4  /* parent (local, -1 root), joint type, dof (local, -1 none), pad */
 #define MG_ARTIC_I_N       4  /* first_body, first_dof, tmpl, pad */
-#define MG_ATMPL_I_N       4  /* first_link (into tmpl_link_*), num_links, num_dofs, fixed_base */
+/* first_link (into tmpl_link_*), num_links, num_dofs, fixed_base. fixed_base 0: a
+ * floating base (the root link moves freely, e.g. the MJCF ant of
+ * examples/apply_forces.py:67); such an articulation steps in the coupled per-env
+ * kernel (needs actor_coll) with num_dofs + 6 (+ 6 per free body of its env) <= 16
+ * velocity slots; its Jacobian / mass-matrix tensors are not supported. */
+#define MG_ATMPL_I_N       4
 #define MG_ACOLL_N         4  /* env, collision group, collision filter, pad */
 #define MG_RENDER_MAX_SHAPES 64 /* shapes one camera's env may hold */
 
@@ -281,7 +286,8 @@ int32_t     mg_step_time_stats(mg_sim* sim, int32_t n, float* avg_ms, float* min
 int32_t     mg_num_free_bodies(mg_sim* sim);
 int32_t     mg_num_articulations(mg_sim* sim);
 /* Number of envs stepped by the coupled per-env kernel (envs whose bodies can
- * touch each other under the actor_coll rule, e.g. the Franka cube-pick scene). */
+ * touch each other under the actor_coll rule, e.g. the Franka cube-pick scene,
+ * and every env holding a floating-base articulation). */
 int32_t     mg_num_coupled_envs(mg_sim* sim);
 
 #ifdef __cplusplus

@@ -536,7 +536,7 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
       if (L <= OR_WORLD_MAXL) {
           static aba_ws_t W;
           float mdiag[OR_MAXL];
-          aba_world_(P, m, LF, LI, L, D, b0, d0, q, qd, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd);
+          aba_world_(P, m, LF, LI, L, D, b0, d0, q, qd, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd, 0, NULL);
       } else
       for (att = 0; att < 2; ++att) {
         unsigned nm;

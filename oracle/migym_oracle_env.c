@@ -477,7 +477,7 @@ static float red16_prod_(const float* a, const float* b) {
 typedef struct { int a, sa, b, sb; } epair_t;
 
 /* candidate shape pairs of an env, in the device's order (migym_capi.cpp upload) */
-static int env_pairs_(const mg_model* m, const oenv_t* ev, int ground, int L, epair_t* out, int cap) {
+static int env_pairs_(const mg_model* m, const oenv_t* ev, int ground, int L, int fb, epair_t* out, int cap) {
     static const int pb[4][4] = {{-1, 0, 1, 2}, {-1, -1, 3, 4}, {-1, -1, -1, 5}, {-1, -1, -1, -1}};
     int n = 0, k, j, t, l, sa, sb;
 #define OE_PUSH(A_, SA_, B_, SB_) do { if (n < cap) { out[n].a = (A_); out[n].sa = (SA_); out[n].b = (B_); out[n].sb = (SB_); } n++; } while (0)
@@ -499,14 +499,14 @@ static int env_pairs_(const mg_model* m, const oenv_t* ev, int ground, int L, ep
                 OE_SHP(ev->free_b[j], sb0, nsb);
                 for (sb = sb0; sb < sb0 + nsb; ++sb) OE_PUSH(OE_F0 + k, sa, OE_F0 + j, sb);
             }
-            if (ev->art_body >= 0 && ((ev->mask >> k) & 1)) {
+            if (ev->art_body >= 0 && !fb && ((ev->mask >> k) & 1)) {   /* the fixed base (static) */
                 int sb0, nsb;
                 OE_SHP(ev->art_body, sb0, nsb);
                 for (sb = sb0; sb < sb0 + nsb; ++sb) OE_PUSH(OE_F0 + k, sa, 0, sb);
             }
         }
     }
-    for (l = 1; l < L; ++l) {
+    for (l = fb ? 0 : 1; l < L; ++l) {     /* moving links (a floating base moves) */
         int sa0, nsa;
         OE_SHP(ev->art_body + l, sa0, nsa);
         for (sa = sa0; sa < sa0 + nsa; ++sa) {
@@ -565,22 +565,57 @@ static void world_inertia_(const float* M, q4_t ql, v3_t xl, v3_t O, float* I) {
         }
 }
 
+/* x = M^-1 b for a symmetric positive definite 6x6 M (row-major): left-looking
+ * Cholesky, forward and backward substitution (mg_env.hip spd6_solve) */
+static void spd6_solve_(const float* M, const float* b, float* x) {
+    float Lm[36], y[6];
+    int i, j, k;
+    for (j = 0; j < 6; ++j) {
+        float sj = M[j * 6 + j], dj, inv;
+        for (k = 0; k < j; ++k) sj = sj - Lm[j * 6 + k] * Lm[j * 6 + k];
+        dj = sqrtf(sj);
+        inv = 1.0f / dj;
+        Lm[j * 6 + j] = dj;
+        for (i = j + 1; i < 6; ++i) {
+            float t = M[i * 6 + j];
+            for (k = 0; k < j; ++k) t = t - Lm[i * 6 + k] * Lm[j * 6 + k];
+            Lm[i * 6 + j] = t * inv;
+        }
+    }
+    for (i = 0; i < 6; ++i) {
+        float t = b[i];
+        for (k = 0; k < i; ++k) t = t - Lm[i * 6 + k] * y[k];
+        y[i] = t / Lm[i * 6 + i];
+    }
+    for (i = 5; i >= 0; --i) {
+        float t = y[i];
+        for (k = i + 1; k < 6; ++k) t = t - Lm[k * 6 + i] * x[k];
+        x[i] = t / Lm[i * 6 + i];
+    }
+}
+
 /* World-frame articulated-body algorithm about the base origin x0 (RBDA ch. 7,
  * every quantity in one frame; mg_env.hip aba_world, mg_artic.hip
  * k_artic_world): unconstrained joint accelerations qdd with implicit drives
  * and the effort-limit re-solve. Sets W (kinematics, motion axes, inertias),
  * mdiag (armature + implicit drive term), tau0d / impd (drive force, implicit
- * coefficient) for the final attempt. Shared by env_step_ and artic_step. */
+ * coefficient) for the final attempt. Shared by env_step_ and artic_step.
+ * Floating base (fb): the root's spatial velocity (w, v at x0) is u[D..D+5];
+ * the inward pass also folds into link 0, a0 = -IA_0^-1 pA_0 (relative to
+ * gravity) starts the outward pass, and qdd[D..D+5] = (w', a0.v + g + w x v).
+ * ext (AoS [6] per body, world force / torque at the COM) or NULL. */
 typedef struct {
     q4_t ql[OR_MAXL], qrl[OR_MAXL];
     v3_t xl[OR_MAXL], zl[OR_MAXL], rrl[OR_MAXL];
     float Iw[OR_MAXL][36], xi[OR_MAXL][6], va[OR_MAXL][6], ccv[OR_MAXL][6], pav[OR_MAXL][6], Ua[OR_MAXL][6];
     float Dd[OR_MAXL], uu[OR_MAXL];
+    float ru[6];              /* floating root: (w, v_O) after the unconstrained update */
 } aba_ws_t;
 
 static void aba_world_(const step_t* P, const mg_model* m, const float* LF, const int* LI, int L, int D, int b0,
                        int d0, const float* q, const float* u, const float* props, const float* tgt, v3_t x0, q4_t q0,
-                       v3_t gw, aba_ws_t* W, float* qdd, float* mdiag, float* tau0d, float* impd) {
+                       v3_t gw, aba_ws_t* W, float* qdd, float* mdiag, float* tau0d, float* impd, int fb,
+                       const float* ext) {
     const float h = P->h;
     q4_t* ql = W->ql; q4_t* qrl = W->qrl;
     v3_t* xl = W->xl; v3_t* zl = W->zl; v3_t* rrl = W->rrl;
@@ -624,7 +659,7 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
                 put6_(xi[l], x);
                 world_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N, ql[l], xl[l], x0, Iw[l]);
             }
-            for (i = 0; i < 6; ++i) va[0][i] = 0.0f;
+            for (i = 0; i < 6; ++i) va[0][i] = fb ? u[D + i] : 0.0f;
             for (l = 1; l < L; ++l) {
                 const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
                 const float qd = dj >= 0 ? u[dj] : 0.0f;
@@ -638,7 +673,17 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
                 float Iv[6];
                 for (i = 0; i < 6; ++i) Iv[i] = dot6_(&Iw[l][i * 6], va[l]);
                 put6_(ccv[l], crm_(v, vJ));
-                put6_(pav[l], crf_(v, sv6_(Iv)));
+                {
+                    sv_t pb = crf_(v, sv6_(Iv));
+                    if (ext) {
+                        const float* x = ext + (size_t)(b0 + l) * 6;
+                        const float* M = m->body_mass + (size_t)(b0 + l) * MG_MASS_N;
+                        const v3_t f = V(x[0], x[1], x[2]), t = V(x[3], x[4], x[5]);
+                        const v3_t c = sub3(add3(xl[l], qrot_(ql[l], V(M[8], M[9], M[10]))), x0);
+                        pb = SVc(sub3(pb.w, add3(t, cross3(c, f))), sub3(pb.v, f));
+                    }
+                    put6_(pav[l], pb);
+                }
             }
             for (l = L - 1; l >= 1; --l) {
                 const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
@@ -679,7 +724,7 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
                     tau0d[dj] = tau;
                     impd[dj] = imp;
                 }
-                if (p > 0) {
+                if (p > 0 || (fb && p == 0)) {
                     for (i = 0; i < 6; ++i) {
                         float pv = pav[l][i] + dot6_(&Iw[l][i * 6], ccv[l]);
                         if (dj >= 0) pv = pv + Ua[l][i] * uinvD;
@@ -688,8 +733,33 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
                     for (i = 0; i < 36; ++i) Iw[p][i] = Iw[p][i] + Iw[l][i];
                 }
             }
-            va[0][0] = 0.0f; va[0][1] = 0.0f; va[0][2] = 0.0f;
-            va[0][3] = -gw.x; va[0][4] = -gw.y; va[0][5] = -gw.z;
+            if (fb) {
+                float nb6[6], a0[6];
+                v3_t w, vo, av;
+                for (i = 0; i < 6; ++i) nb6[i] = -pav[0][i];
+                spd6_solve_(Iw[0], nb6, a0);
+                for (i = 0; i < 6; ++i) va[0][i] = a0[i];
+                w = V(u[D + 0], u[D + 1], u[D + 2]);
+                vo = V(u[D + 3], u[D + 4], u[D + 5]);
+                av = add3(add3(V(a0[3], a0[4], a0[5]), gw), cross3(w, vo));
+                qdd[D + 0] = a0[0]; qdd[D + 1] = a0[1]; qdd[D + 2] = a0[2];
+                qdd[D + 3] = av.x; qdd[D + 4] = av.y; qdd[D + 5] = av.z;
+                {   /* the root link's damping and speed limits (as a free body's) */
+                    const float* tf = m->tmpl_body_f + (size_t)m->body_tmpl[b0] * MG_TBODY_F_N;
+                    const float lkeep = 1.0f - fminf(tf[0] * h, 1.0f), akeep = 1.0f - fminf(tf[1] * h, 1.0f);
+                    v3_t wn = mul3(mad3(w, V(a0[0], a0[1], a0[2]), h), akeep);
+                    v3_t vn = mul3(mad3(vo, av, h), lkeep);
+                    const float w2 = dot3(wn, wn), mw2 = tf[3] * tf[3];
+                    const float v2 = dot3(vn, vn), mv2 = tf[2] * tf[2];
+                    if (w2 > mw2) wn = mul3(wn, sqrtf(mw2 / w2));
+                    if (v2 > mv2) vn = mul3(vn, sqrtf(mv2 / v2));
+                    W->ru[0] = wn.x; W->ru[1] = wn.y; W->ru[2] = wn.z;
+                    W->ru[3] = vn.x; W->ru[4] = vn.y; W->ru[5] = vn.z;
+                }
+            } else {
+                va[0][0] = 0.0f; va[0][1] = 0.0f; va[0][2] = 0.0f;
+                va[0][3] = -gw.x; va[0][4] = -gw.y; va[0][5] = -gw.z;
+            }
             for (l = 1; l < L; ++l) {
                 const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
                 float a6[6];
@@ -723,6 +793,8 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     const int b0 = ev->art_body, d0 = ev->art_dof, nfr = ev->nf;
     const int* ti = ev->art_tmpl >= 0 ? m->artic_tmpl_i + (size_t)ev->art_tmpl * MG_ATMPL_I_N : NULL;
     const int L = ti ? ti[1] : 0, D = ti ? ti[2] : 0;
+    const int fb = (ti && !ti[3]) ? 1 : 0;     /* floating base: root slots D..D+5 */
+    const int NS = D + 6 * fb;                  /* articulation slots; free bodies follow */
     const float* LF = ti ? m->tmpl_link_f + (size_t)ti[0] * MG_LINK_F_N : NULL;
     const int* LI = ti ? m->tmpl_link_i + (size_t)ti[0] * MG_LINK_I_N : NULL;
     const float h = P->h;
@@ -754,8 +826,8 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     float cs0[OE_MAXCT], cmu[OE_MAXCT], ce[OE_MAXCT], cvn0[OE_MAXCT], ck[OE_MAXCT][3], clam[OE_MAXCT][3];
     static float Jr[OE_MAXCT * 3][OE_G], Wr[OE_MAXCT * 3][OE_G];
     int d, l, k, c, i, j, st_, it;
-    if (L > OR_MAXL || (ti && !ti[3]) || D + 6 * nfr > OE_G || nfr > OE_MAXF) return -1;
-    npair = env_pairs_(m, ev, P->ground, L, pairs, OE_MAXPAIRS);
+    if (L > OR_MAXL || NS + 6 * nfr > OE_G || nfr > OE_MAXF) return -1;
+    npair = env_pairs_(m, ev, P->ground, L, fb, pairs, OE_MAXPAIRS);
     if (npair > OE_MAXPAIRS) return -1;
     for (i = 0; i < OE_G; ++i) { q[i] = 0.0f; u[i] = 0.0f; dp[i] = 0.0f; }
     if (L > 0) {
@@ -772,6 +844,14 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         lsum[l] = V(0.0f, 0.0f, 0.0f);
     }
     for (d = 0; d < D; ++d) { q[d] = dof[(d0 + d) * 2 + 0]; u[d] = dof[(d0 + d) * 2 + 1]; }
+    if (fb) {   /* root slots: w and the velocity of the base origin v_O = v_com - w x (R c) */
+        const float* s0 = state + (size_t)b0 * MG_STATE_N;
+        const float* M0 = m->body_mass + (size_t)b0 * MG_MASS_N;
+        const v3_t w = V(s0[10], s0[11], s0[12]), vc = V(s0[7], s0[8], s0[9]);
+        const v3_t vo = sub3(vc, cross3(w, qrot_(q0, V(M0[8], M0[9], M0[10]))));
+        u[D + 0] = w.x; u[D + 1] = w.y; u[D + 2] = w.z;
+        u[D + 3] = vo.x; u[D + 4] = vo.y; u[D + 5] = vo.z;
+    }
     for (k = 0; k < nfr; ++k) {
         const int b = ev->free_b[k];
         const float* s = state + (size_t)b * MG_STATE_N;
@@ -779,7 +859,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         const float* tf = m->tmpl_body_f + (size_t)m->body_tmpl[b] * MG_TBODY_F_N;
         fx[k] = V(s[0], s[1], s[2]);
         fq[k] = qnorm_(Q(s[3], s[4], s[5], s[6]));
-        for (i = 0; i < 6; ++i) u[D + 6 * k + i] = s[7 + i];
+        for (i = 0; i < 6; ++i) u[NS + 6 * k + i] = s[7 + i];
         finvm[k] = M[0];
         finvI[k] = V(M[1], M[2], M[3]);
         fiq[k] = Q(M[4], M[5], M[6], M[7]);
@@ -801,9 +881,10 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     for (st_ = 0; st_ < P->substeps; ++st_) {
         int nct = 0, link_rows = 0;
         /* ---- 1. unconstrained motion: world-frame ABA about x0 (mg_env.hip aba_world) */
-        if (L > 0) aba_world_(P, m, LF, LI, L, D, b0, d0, q, u, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd);
+        if (L > 0) aba_world_(P, m, LF, LI, L, D, b0, d0, q, u, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd, fb,
+                              ext);
         for (k = 0; k < nfr; ++k) {
-            const int s0 = D + 6 * k;
+            const int s0 = NS + 6 * k;
             const s3_t Iw = sym_rdrt_(qmat_(qmul_(fq[k], fiq[k])), finvI[k]);
             v3_t v = V(u[s0 + 0], u[s0 + 1], u[s0 + 2]), w = V(u[s0 + 3], u[s0 + 4], u[s0 + 5]);
             float v2, w2;
@@ -827,6 +908,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             if (maxv > 0.0f) w = fminf(fmaxf(w, -maxv), maxv);
             u[d] = w;
         }
+        for (d = D; d < NS; ++d) u[d] = W.ru[d - D];
         for (i = 0; i < OE_G; ++i) dp[i] = 0.0f;
 
         /* ---- 2. narrow phase, pair order */
@@ -912,11 +994,13 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             for (l = 0; l < L; ++l) world_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N, ql[l], xl[l], x0, Iw[l]);
             for (l = L - 1; l >= 1; --l) {
                 const int p = LI[l * MG_LINK_I_N + 0];
-                if (p > 0)
+                if (p > 0 || (fb && p == 0))
                     for (i = 0; i < 36; ++i) Iw[p][i] = Iw[p][i] + Iw[l][i];
             }
-            for (i = 0; i < D; ++i)
-                for (j = 0; j < D; ++j) Lc[i][j] = 0.0f;
+            for (i = 0; i < NS; ++i)
+                for (j = 0; j < NS; ++j) Lc[i][j] = 0.0f;
+            for (i = 0; i < 6 * fb; ++i)           /* root block: IC_0 */
+                for (j = 0; j < 6; ++j) Lc[D + i][D + j] = Iw[0][i * 6 + j];
             for (i = 0; i < D; ++i) {
                 const int li_ = dlink[i];
                 float F[6];
@@ -933,28 +1017,32 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     }
                     jl = LI[jl * MG_LINK_I_N + 0];
                 }
+                for (r6 = 0; r6 < 6 * fb; ++r6) {   /* root columns: (IC_l xi_l)[r] */
+                    Lc[i][D + r6] = F[r6];
+                    Lc[D + r6][i] = F[r6];
+                }
             }
-            for (j = 0; j < D; ++j) {
+            for (j = 0; j < NS; ++j) {
                 float s = Lc[j][j], djv;
                 for (k = 0; k < j; ++k) s = s - Lc[j][k] * Lc[j][k];
                 djv = sqrtf(s);
                 invd[j] = 1.0f / djv;
                 Lc[j][j] = djv;
-                for (i = j + 1; i < D; ++i) {
+                for (i = j + 1; i < NS; ++i) {
                     float t = Lc[i][j];
                     for (k = 0; k < j; ++k) t = t - Lc[i][k] * Lc[j][k];
                     Lc[i][j] = t * invd[j];
                 }
             }
-            for (j = 0; j < D; ++j) {       /* column j of M_eff^-1 (device lane j) */
-                for (i = 0; i < D; ++i) {
+            for (j = 0; j < NS; ++j) {       /* column j of M_eff^-1 (device lane j) */
+                for (i = 0; i < NS; ++i) {
                     float t = i == j ? 1.0f : 0.0f;
                     for (k = 0; k < i; ++k) t = t - Lc[i][k] * Mi[k][j];
                     Mi[i][j] = t * invd[i];
                 }
-                for (i = D - 1; i >= 0; --i) {
+                for (i = NS - 1; i >= 0; --i) {
                     float t = Mi[i][j];
-                    for (k = i + 1; k < D; ++k) t = t - Lc[k][i] * Mi[k][j];
+                    for (k = i + 1; k < NS; ++k) t = t - Lc[k][i] * Mi[k][j];
                     Mi[i][j] = t * invd[i];
                 }
             }
@@ -977,8 +1065,10 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                             const int jl = dlink[ln];
                             Jv = drev[ln] ? dot3(cross3(zl[jl], sub3(p, xl[jl])), dir) : dot3(zl[jl], dir);
                         }
-                    } else if ((ln - D) / 6 < nfr) {
-                        const int fk = (ln - D) / 6, fc = (ln - D) % 6;
+                    } else if (ln < NS) {           /* floating root: unit spatial axes at x0 */
+                        if (a < OE_F0) Jv = ln - D < 3 ? vc_(cross3(sub3(p, x0), dir), ln - D) : vc_(dir, ln - D - 3);
+                    } else if ((ln - NS) / 6 < nfr) {
+                        const int fk = (ln - NS) / 6, fc = (ln - NS) % 6;
                         const float sg = a == OE_F0 + fk ? 1.0f : (b == OE_F0 + fk ? -1.0f : 0.0f);
                         if (sg != 0.0f) {
                             const v3_t rd = cross3(sub3(p, fxc[fk]), dir);
@@ -997,10 +1087,10 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     W[ln] = Wv;
                 }
                 if (link_rows) {
-                    for (ln = 0; ln < D; ++ln) {
+                    for (ln = 0; ln < NS; ++ln) {
                         float w = 0.0f;
                         /* column ln of M_eff^-1 (the solve lane ln ran), entry k */
-                        for (k = 0; k < D; ++k) w = w + Mi[k][ln] * J[k];
+                        for (k = 0; k < NS; ++k) w = w + Mi[k][ln] * J[k];
                         W[ln] = w;
                     }
                 }
@@ -1073,8 +1163,12 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             else lsum[ca[c]] = add3(lsum[ca[c]], imp);
             if (cb[c] >= OE_F0 && cb[c] < OE_ST0) fsum[cb[c] - OE_F0] = sub3(fsum[cb[c] - OE_F0], imp);
         }
+        if (fb) {   /* floating root: the origin moves by dpos_v, the orientation turns by dpos_w */
+            x0 = add3(x0, V(dp[D + 3], dp[D + 4], dp[D + 5]));
+            q0 = qint_(q0, V(dp[D + 0], dp[D + 1], dp[D + 2]));
+        }
         for (k = 0; k < nfr; ++k) {
-            const int s0 = D + 6 * k;
+            const int s0 = NS + 6 * k;
             const v3_t dx = V(dp[s0 + 0], dp[s0 + 1], dp[s0 + 2]);
             const v3_t dth = V(dp[s0 + 3], dp[s0 + 4], dp[s0 + 5]);
             const v3_t xc1 = add3(fxc[k], dx);
@@ -1088,7 +1182,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         float* s = state + (size_t)b * MG_STATE_N;
         s[0] = fx[k].x; s[1] = fx[k].y; s[2] = fx[k].z;
         s[3] = fq[k].x; s[4] = fq[k].y; s[5] = fq[k].z; s[6] = fq[k].w;
-        for (i = 0; i < 6; ++i) s[7 + i] = u[D + 6 * k + i];
+        for (i = 0; i < 6; ++i) s[7 + i] = u[NS + 6 * k + i];
         cforce[(size_t)b * 3 + 0] = fsum[k].x * P->inv_dt;
         cforce[(size_t)b * 3 + 1] = fsum[k].y * P->inv_dt;
         cforce[(size_t)b * 3 + 2] = fsum[k].z * P->inv_dt;
@@ -1101,7 +1195,10 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         float* so = state + (size_t)(b0 + l) * MG_STATE_N;
         v3_t ww, vw, com = V(M[8], M[9], M[10]);
         if (p < 0) {
-            ql[l] = q0; xl[l] = x0; vl[l] = sv0();
+            const q4_t qc = Q(-q0.x, -q0.y, -q0.z, q0.w);
+            const v3_t w = fb ? V(u[D + 0], u[D + 1], u[D + 2]) : V(0.0f, 0.0f, 0.0f);
+            const v3_t vo = fb ? V(u[D + 3], u[D + 4], u[D + 5]) : V(0.0f, 0.0f, 0.0f);
+            ql[l] = q0; xl[l] = x0; vl[l] = SVc(qrot_(qc, w), qrot_(qc, vo));
         } else {
             q4_t qrel; v3_t rr; sv_t sj;
             const float qj = dj >= 0 ? q[dj] : 0.0f, qdj = dj >= 0 ? u[dj] : 0.0f;
@@ -1171,8 +1268,13 @@ static int classify_envs_(const mg_model* m, oenv_t* envs, char* owned) {
             for (j = i + 1; j < nf; ++j) coupled |= oe_collide_(m, fr[i], fr[j]);
         }
         for (i = 0; i < nart; ++i) {
+            const int r0 = m->actor_root_body[art[i]];
             for (j = 0; j < ns; ++j) coupled |= oe_collide_(m, art[i], stc[j]);
             for (j = 0; j < nf; ++j) coupled |= oe_collide_(m, art[i], fr[j]);
+            for (j = 0; j < m->num_artics; ++j) {   /* a floating base always steps here */
+                const int* ai = m->artic_i + (size_t)j * MG_ARTIC_I_N;
+                if (ai[0] == r0 && !m->artic_tmpl_i[(size_t)ai[2] * MG_ATMPL_I_N + 3]) coupled = 1;
+            }
         }
         if (!coupled) continue;
         if (nart_all > 1 || nf_all > OE_MAXF || ns_all > OE_MAXS) { n = -1; break; }

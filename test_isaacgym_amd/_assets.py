@@ -42,6 +42,7 @@ MESH_PROXIES = {
 }
 
 SPHERE, BOX, CAPSULE, CONVEX = 0, 1, 2, 3
+MJCF_MAX_JOINT_VELOCITY = 100.0      # PhysX's default articulation joint speed limit (rad/s, m/s)
 HULL_MAX_VERTS, HULL_MAX_FACES = 32, 64          # MG_HULL_MAX_VERTS / _FACES (include/migym.h)
 
 
@@ -168,7 +169,7 @@ def make_hull(verts, max_verts=HULL_MAX_VERTS):
 
 
 class Shape:
-    __slots__ = ("type", "size", "p", "q", "friction", "restitution", "source", "hull")
+    __slots__ = ("type", "size", "p", "q", "friction", "restitution", "source", "hull", "density")
 
     def __init__(self, type_, size, p=None, q=None, source="primitive", hull=None):
         self.type = type_
@@ -179,6 +180,7 @@ class Shape:
         self.restitution = 0.0
         self.source = source
         self.hull = hull
+        self.density = None
 
     def com_body(self):
         """Centroid of the shape in the body frame."""
@@ -244,6 +246,7 @@ class Joint:
         self.velocity = 0.0
         self.damping = 0.0
         self.friction = 0.0
+        self.armature = None      # per-joint armature (MJCF), else AssetOptions.armature
 
     @property
     def has_dof(self):
@@ -322,7 +325,7 @@ class Asset:
             props[d]["stiffness"] = 0.0
             props[d]["damping"] = j.damping
             props[d]["friction"] = j.friction
-            props[d]["armature"] = opts.armature
+            props[d]["armature"] = opts.armature if j.armature is None else j.armature
         self.dof_props = props
         self.shape_props = []
         for b in self.bodies:
@@ -635,4 +638,263 @@ def load_urdf(asset_root, filename, options):
         j.child = index[j.child]
     asset.warnings = warnings
     asset.path = path
+    return asset.finalize()
+
+
+# ------------------------------------------------------------------ MJCF
+def _mj_floats(s, default=None):
+    if s is None:
+        return None if default is None else list(default)
+    return [float(t) for t in s.split()]
+
+
+def _mj_quat(el, angle_deg, default=None):
+    """Orientation of an MJCF element as xyzw: quat (MJCF order w x y z), axisangle,
+    euler (xyz, the MJCF default eulerseq) or zaxis; identity if none."""
+    q = _mj_floats(el.get("quat"))
+    if q is not None:
+        v = np.array([q[1], q[2], q[3], q[0]])
+        return v / np.linalg.norm(v)
+    aa = _mj_floats(el.get("axisangle"))
+    k = math.pi / 180.0 if angle_deg else 1.0
+    if aa is not None:
+        ax = np.array(aa[:3]) / np.linalg.norm(aa[:3])
+        h = 0.5 * aa[3] * k
+        return np.array([*(ax * math.sin(h)), math.cos(h)])
+    eu = _mj_floats(el.get("euler"))
+    if eu is not None:
+        q = np.array([0, 0, 0, 1.0])
+        for i, a in enumerate(eu):                  # intrinsic x, y, z
+            ax = np.zeros(3)
+            ax[i] = 1.0
+            h = 0.5 * a * k
+            q = _qmul(q, np.array([*(ax * math.sin(h)), math.cos(h)]))
+        return q
+    za = _mj_floats(el.get("zaxis"))
+    if za is not None:
+        z = np.array(za) / np.linalg.norm(za)
+        return _quat_between(np.array([0, 0, 1.0]), z)
+    return np.array([0, 0, 0, 1.0]) if default is None else default
+
+
+def _quat_between(a, b):
+    """Shortest-arc rotation taking unit vector a to unit vector b (xyzw)."""
+    c = float(np.dot(a, b))
+    if c < -0.999999:
+        ax = np.cross(a, [1.0, 0, 0])
+        if np.linalg.norm(ax) < 1e-6:
+            ax = np.cross(a, [0, 1.0, 0])
+        ax /= np.linalg.norm(ax)
+        return np.array([*ax, 0.0])
+    v = np.cross(a, b)
+    q = np.array([v[0], v[1], v[2], 1.0 + c])
+    return q / np.linalg.norm(q)
+
+
+class _MjDefaults:
+    """<default> attribute sets: the top level and named classes (one level of
+    nesting inherits from its parent class)."""
+
+    def __init__(self, root):
+        self.cls = {}
+        d = root.find("default")
+        if d is not None:
+            self._read(d, "main", {})
+
+    def _read(self, el, name, inherit):
+        cur = {k: dict(v) for k, v in inherit.items()}
+        for child in el:
+            if child.tag == "default":
+                continue
+            cur.setdefault(child.tag, {}).update(child.attrib)
+        self.cls[name] = cur
+        for child in el.findall("default"):
+            self._read(child, child.get("class", name), cur)
+
+    def attrs(self, el, cls):
+        base = dict(self.cls.get(cls, self.cls.get("main", {})).get(el.tag, {}))
+        base.update(el.attrib)
+        return base
+
+
+def _mj_geom_shape(g, angle_deg, warnings):
+    """One MJCF geom as a Shape (body frame), or None (planes, meshes)."""
+    t = g.get("type", "sphere")
+    size = _mj_floats(g.get("size"), (0.0,))
+    fromto = _mj_floats(g.get("fromto"))
+    p = np.array(_mj_floats(g.get("pos"), (0, 0, 0)), dtype=np.float64)
+    q = _mj_quat(_Attr(g), angle_deg)
+    if t in ("capsule", "cylinder"):
+        if t == "cylinder":
+            warnings.append("MJCF cylinder geom %s represented as a capsule" % g.get("name"))
+        r = size[0]
+        if fromto is not None:
+            a, b = np.array(fromto[:3]), np.array(fromto[3:6])
+            d = b - a
+            ln = float(np.linalg.norm(d))
+            p = 0.5 * (a + b)
+            q = _quat_between(np.array([1.0, 0, 0]), d / ln) if ln > 0 else np.array([0, 0, 0, 1.0])
+            hh = 0.5 * ln
+        else:
+            hh = size[1] if len(size) > 1 else 0.0
+            q = _qmul(q, _quat_between(np.array([1.0, 0, 0]), np.array([0, 0, 1.0])))   # MJCF axis: local z
+        return Shape(CAPSULE, (r, hh), p, q, source="mjcf:" + t)
+    if t == "sphere":
+        return Shape(SPHERE, (size[0],), p, q, source="mjcf:sphere")
+    if t == "box":
+        if fromto is not None:
+            warnings.append("MJCF box %s: fromto ignored" % g.get("name"))
+        return Shape(BOX, tuple(size[:3]), p, q, source="mjcf:box")
+    if t != "plane":
+        warnings.append("MJCF geom type %s (%s) skipped" % (t, g.get("name")))
+    return None
+
+
+class _Attr:
+    """An element view over merged (default + own) attributes."""
+
+    def __init__(self, attrs):
+        self._a = attrs if isinstance(attrs, dict) else dict(attrs.attrib) if hasattr(attrs, "attrib") else attrs
+
+    def get(self, k, d=None):
+        return self._a.get(k, d)
+
+
+def load_mjcf(asset_root, filename, options):
+    """MuJoCo MJCF import (assets/mjcf/nv_ant.xml, examples/apply_forces.py:67):
+    the body tree under <worldbody>, hinge / slide joints (one per body; angles in
+    degrees unless <compiler angle="radian">), a <freejoint> / free joint on the
+    root (a floating base unless AssetOptions.fix_base_link), sphere / capsule /
+    box geoms (fromto capsules; cylinders as capsules), mass properties from the
+    geoms at their density (default 1000) unless the body has an <inertial>,
+    geom friction (sliding coefficient), joint range / damping / armature, and
+    motor actuators' gear x ctrlrange as the DOF effort limit. World geoms (the
+    floor plane) are not part of the asset. A hinge whose anchor is off the body
+    origin moves the child frame to the anchor (geoms and children re-expressed)."""
+    path = filename if os.path.isabs(filename) else os.path.join(asset_root, filename)
+    if not os.path.exists(path):
+        raise FileNotFoundError(path)
+    root = ET.parse(path).getroot()
+    comp = root.find("compiler")
+    angle_deg = comp is None or comp.get("angle", "degree") != "radian"
+    k_ang = math.pi / 180.0 if angle_deg else 1.0
+    defaults = _MjDefaults(root)
+    warnings = []
+    wb = root.find("worldbody")
+    if wb is None:
+        raise ValueError("MJCF %s: no <worldbody>" % path)
+    tops = wb.findall("body")
+    if len(tops) != 1:
+        raise ValueError("MJCF %s: expected one top-level body, found %d" % (path, len(tops)))
+    asset = Asset(root.get("model", os.path.basename(path)), options)
+    joint_of_name = {}
+
+    def geom_shapes(bel, cls, shift):
+        out = []
+        for g in bel.findall("geom"):
+            ga = defaults.attrs(g, g.get("class", cls))
+            sh = _mj_geom_shape(_Attr(ga), angle_deg, warnings)
+            if sh is None:
+                continue
+            sh.p = sh.p - shift
+            fr = _mj_floats(ga.get("friction"))
+            if fr:
+                sh.friction = fr[0]
+            sh.density = float(ga.get("density", 1000.0))
+            out.append(sh)
+        return out
+
+    def visit(bel, parent_idx, parent_shift, cls):
+        cls = bel.get("childclass", cls)
+        idx = len(asset.bodies)
+        body = Body(bel.get("name", "body%d" % idx))
+        bp = np.array(_mj_floats(bel.get("pos"), (0, 0, 0)), dtype=np.float64) - parent_shift
+        bq = _mj_quat(bel, angle_deg)
+        joints = [j for j in bel if j.tag in ("joint", "freejoint")]
+        free = [j for j in joints if j.tag == "freejoint" or
+                defaults.attrs(j, j.get("class", cls)).get("type", "hinge") == "free"]
+        hinge = [j for j in joints if j not in free]
+        if parent_idx is None and hinge:
+            raise ValueError("MJCF %s: joints on the root body other than a free joint" % path)
+        if parent_idx is not None and free:
+            raise ValueError("MJCF %s: free joint below the root" % path)
+        if len(hinge) > 1:
+            raise ValueError("MJCF %s: body %s has %d joints (one per body supported)" % (path, body.name, len(hinge)))
+        shift = np.zeros(3)
+        if parent_idx is not None:
+            jt = T.JOINT_FIXED
+            j = Joint(hinge[0].get("name") if hinge else body.name + "_fixed", jt, parent_idx, idx)
+            j.p, j.q = bp, bq
+            if hinge:
+                ja = defaults.attrs(hinge[0], hinge[0].get("class", cls))
+                typ = ja.get("type", "hinge")
+                if typ not in ("hinge", "slide"):
+                    raise ValueError("MJCF %s: joint type %s unsupported" % (path, typ))
+                j.type = T.JOINT_REVOLUTE if typ == "hinge" else T.JOINT_PRISMATIC
+                ax = np.array(_mj_floats(ja.get("axis"), (0, 0, 1)), dtype=np.float64)
+                j.axis = ax / np.linalg.norm(ax)
+                anchor = np.array(_mj_floats(ja.get("pos"), (0, 0, 0)), dtype=np.float64)
+                if np.any(anchor != 0.0):
+                    shift = anchor
+                    j.p = bp + _qmat(bq) @ anchor
+                rng = _mj_floats(ja.get("range"))
+                limited = ja.get("limited", "auto")
+                if rng is not None and limited in ("true", "auto"):
+                    s = k_ang if typ == "hinge" else 1.0
+                    j.has_limits, j.lower, j.upper = True, rng[0] * s, rng[1] * s
+                j.damping = float(ja.get("damping", 0.0))
+                j.friction = float(ja.get("frictionloss", 0.0))
+                j.velocity = MJCF_MAX_JOINT_VELOCITY
+                if ja.get("armature") is not None:
+                    j.armature = float(ja.get("armature"))
+                joint_of_name[j.name] = j
+            asset.joints.append(j)
+        shapes = geom_shapes(bel, cls, shift)
+        body.shapes = shapes
+        body.has_visual = bool(shapes)
+        ine = bel.find("inertial")
+        if ine is not None:
+            body.has_inertial = True
+            body.mass = float(ine.get("mass", 0.0))
+            body.com = np.array(_mj_floats(ine.get("pos"), (0, 0, 0)), dtype=np.float64) - shift
+            R = _qmat(_mj_quat(ine, angle_deg))
+            di = _mj_floats(ine.get("diaginertia"))
+            fi = _mj_floats(ine.get("fullinertia"))
+            if di is not None:
+                body.inertia = R @ np.diag(di) @ R.T
+            elif fi is not None:
+                xx, yy, zz, xy, xz, yz = fi
+                body.inertia = R @ np.array([[xx, xy, xz], [xy, yy, yz], [xz, yz, zz]]) @ R.T
+        elif shapes:
+            # mass properties from the geoms, each at its own density
+            vols = [s.volume() for s in shapes]
+            ms = [s.density * v for s, v in zip(shapes, vols)]
+            M = sum(ms)
+            if M > 0:
+                com = sum(s.com_body() * m for s, m in zip(shapes, ms)) / M
+                I = np.zeros((3, 3))
+                for s, m in zip(shapes, ms):
+                    R = _qmat(s.q)
+                    d = s.com_body() - com
+                    I += R @ (s.inertia_unit_mass() * m) @ R.T + m * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
+                body.has_inertial, body.mass, body.com, body.inertia = True, M, com, I
+        asset.bodies.append(body)
+        for child in bel.findall("body"):
+            visit(child, idx, shift, cls)
+
+    visit(tops[0], None, np.zeros(3), "main")
+    act = root.find("actuator")
+    if act is not None:
+        for mo in act:
+            if mo.tag not in ("motor", "general"):
+                continue
+            j = joint_of_name.get(mo.get("joint"))
+            cr = _mj_floats(mo.get("ctrlrange"))
+            if j is None or cr is None or mo.get("ctrllimited", "true") == "false":
+                continue
+            gear = _mj_floats(mo.get("gear"), (1.0,))[0]
+            j.effort = abs(gear) * max(abs(cr[0]), abs(cr[1]))
+    asset.warnings = warnings
+    asset.path = path
+    asset.floating_root = True
     return asset.finalize()

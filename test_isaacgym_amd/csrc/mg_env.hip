@@ -31,20 +31,22 @@
 
 #ifdef MG_ENV_PHASE_TIMING
 // profiling build only: per-phase shader-clock cycles summed over waves
-__device__ unsigned long long g_env_phase[8];
+__device__ unsigned long long g_env_phase[12];
 #define PH_T0() unsigned long long ph_t = clock64()
 #define PH_MARK(k) do { const unsigned long long t_ = clock64(); \
     if (threadIdx.x == 0) atomicAdd(&g_env_phase[k], t_ - ph_t); ph_t = t_; } while (0)
+#define PH_COUNT(k, v) atomicAdd(&g_env_phase[k], (unsigned long long)(v))
 extern "C" int mg_debug_env_phase(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_env_phase), sizeof(g_env_phase)) == hipSuccess ? 0 : -1;
 }
 extern "C" int mg_debug_env_phase_reset(void) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_env_phase), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #else
 #define PH_T0() do { } while (0)
 #define PH_MARK(k) do { } while (0)
+#define PH_COUNT(k, v) do { } while (0)
 #endif
 
 namespace {
@@ -86,6 +88,7 @@ struct EnvLds {
     Q4 qr[MG_MAX_LINKS];             // joint rotation / offset relative to the parent
     V3 rr[MG_MAX_LINKS];
     float tau0[G], imp[G], arm[G];
+    float ru[6];                     // floating root: (w, v_O) after the unconstrained update
     int npl[NPB];                    // candidate pairs that passed the screen
     V3 sx[MG_ENV_MAXS];              // static bodies: pose (they do not move in the step)
     Q4 sq[MG_ENV_MAXS];
@@ -242,6 +245,42 @@ MG_HD bool pair_near(const MgStep& P, const float* sha, V3 xa, Q4 qa, const floa
     return true;
 }
 
+// x = M^-1 b for a symmetric positive definite 6x6 M (row-major): left-looking
+// Cholesky, forward and backward substitution (oracle: spd6_solve_)
+MG_HD void spd6_solve(const float* M, const float* b, float* x) {
+    float Lm[36], y[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        float sj = M[j * 6 + j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) sj = sj - Lm[j * 6 + k] * Lm[j * 6 + k];
+        const float dj = sqrtf(sj);
+        const float inv = 1.0f / dj;
+        Lm[j * 6 + j] = dj;
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) {
+            float t = M[i * 6 + j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) t = t - Lm[i * 6 + k] * Lm[j * 6 + k];
+            Lm[i * 6 + j] = t * inv;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        float t = b[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) t = t - Lm[i * 6 + k] * y[k];
+        y[i] = t / Lm[i * 6 + i];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        float t = y[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; ++k) t = t - Lm[k * 6 + i] * x[k];
+        x[i] = t / Lm[i * 6 + i];
+    }
+}
+
 // Articulated-body algorithm in the world frame about the base origin x0 (RBDA
 // ch. 7 with all quantities in one frame: no spatial transforms in the inward
 // pass). Every lane of the workgroup calls it (the barriers are shared); `act`
@@ -250,10 +289,16 @@ MG_HD bool pair_near(const MgStep& P, const float* sha, V3 xa, Q4 qa, const floa
 // lane ln owns entries {ln, ln+16, ln+32} of every 6x6 in the inward pass.
 // Implicit drives (h kd + h^2 kp added to D); a drive whose implicit force
 // exceeds its effort limit is re-solved at the limit (xmask / xpos).
+// Floating base (A.floating): link 0 moves with the root spatial velocity held
+// by slots DA..DA+5; the inward pass also folds into link 0 and the root
+// acceleration solves IA_0 a0 = -pA_0 (a0 relative to gravity, as the fixed
+// base's a0 = -g). External wrenches at link COMs (A.ext) enter the bias forces.
 template <int MAXL>
 __device__ __forceinline__ void aba_world(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0, Q4 q0,
-                          V3 gw, const LinkC& lk, const DofC& dc, bool is_dof, bool xm, bool xp) {
+                          V3 gw, const LinkC& lk, const DofC& dc, bool is_dof, bool xm, bool xp, int b0) {
     const float h = P.h;
+    const bool fb = A.floating != 0;
+    const int DA = A.ndof;
     // ---- drive terms (lane d): implicit PD force and its h-derivative; a DOF
     // flagged by the effort-limit test (xm) runs at constant +-effort
     if (act && is_dof) {
@@ -332,7 +377,7 @@ __device__ __forceinline__ void aba_world(const MgStep& P, const MgEnvArgs& A, E
     __syncthreads();
     // ---- velocities (lanes 0..5, one component each)
     if (act && ln < 6) {
-        S.va[0][ln] = 0.0f;
+        S.va[0][ln] = fb ? S.u[DA + ln] : 0.0f;
         for (int l = 1; l < LA; ++l) {
             const int p = A.link_i[l * MG_LINK_I_N + 0], dof = A.link_i[l * MG_LINK_I_N + 2];
             const float qd = dof >= 0 ? S.u[dof] : 0.0f;
@@ -349,7 +394,16 @@ __device__ __forceinline__ void aba_world(const MgStep& P, const MgEnvArgs& A, E
         float Iv[6];
         for (int i = 0; i < 6; ++i) Iv[i] = dot6(&S.Iw[ln][i * 6], S.va[ln]);
         put6(S.cc[ln], crm(v, vJ));
-        put6(S.pa[ln], crf(v, sv6(Iv)));
+        SV pb = crf(v, sv6(Iv));
+        if (A.ext) {
+            // world force f and torque t at the link COM: the wrench about x0
+            const int b = b0 + ln, nb = A.nb;
+            const V3 f = v3(A.ext[0 * nb + b], A.ext[1 * nb + b], A.ext[2 * nb + b]);
+            const V3 t = v3(A.ext[3 * nb + b], A.ext[4 * nb + b], A.ext[5 * nb + b]);
+            const V3 c = vsub(vadd(S.xl[ln], qrot(S.ql[ln], lk.com)), x0);
+            pb = sv(vsub(pb.w, vadd(t, vcross(c, f))), vsub(pb.v, f));
+        }
+        put6(S.pa[ln], pb);
     }
     __syncthreads();
     // ---- inward pass: articulated inertias and bias forces
@@ -375,17 +429,46 @@ __device__ __forceinline__ void aba_world(const MgStep& P, const MgEnvArgs& A, E
             }
             __syncthreads();
         }
-        if (act && ln < 6 && p > 0) {
+        if (act && ln < 6 && (p > 0 || (fb && p == 0))) {
             float pv = S.pa[l][ln] + dot6(&S.Iw[l][ln * 6], S.cc[l]);
             if (dof >= 0) pv = pv + S.Ua[l][ln] * uinvD;
             S.pa[p][ln] = S.pa[p][ln] + pv;
         }
-        if (act && p > 0)
+        if (act && (p > 0 || (fb && p == 0)))
             for (int e = ln; e < 36; e += G) S.Iw[p][e] = S.Iw[p][e] + S.Iw[l][e];
         __syncthreads();
     }
+    // ---- root: a0 = -IA_0^-1 pA_0 (lane 0); the root slots' accelerations are
+    // w' and the classical acceleration of the base origin, a0.v + g + w x v;
+    // the root link's damping and speed limits (as a free body's) give ru
+    if (fb) {
+        if (act && ln == 0) {
+            float nb6[6], a0[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) nb6[i] = -S.pa[0][i];
+            spd6_solve(S.Iw[0], nb6, a0);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) S.va[0][i] = a0[i];
+            const V3 w = v3(S.u[DA + 0], S.u[DA + 1], S.u[DA + 2]);
+            const V3 vo = v3(S.u[DA + 3], S.u[DA + 4], S.u[DA + 5]);
+            const V3 av = vadd(vadd(v3(a0[3], a0[4], a0[5]), gw), vcross(w, vo));
+            S.qdd[DA + 0] = a0[0]; S.qdd[DA + 1] = a0[1]; S.qdd[DA + 2] = a0[2];
+            S.qdd[DA + 3] = av.x; S.qdd[DA + 4] = av.y; S.qdd[DA + 5] = av.z;
+            const float* tf = A.tbf + A.body_tmpl[b0] * MG_TBODY_F_N;
+            const float lkeep = 1.0f - fminf(tf[0] * h, 1.0f), akeep = 1.0f - fminf(tf[1] * h, 1.0f);
+            V3 wn = vscale(vmad(w, v3(a0[0], a0[1], a0[2]), h), akeep);
+            V3 vn = vscale(vmad(vo, av, h), lkeep);
+            const float w2 = vdot(wn, wn), mw2 = tf[3] * tf[3];
+            if (w2 > mw2) wn = vscale(wn, sqrtf(mw2 / w2));
+            const float v2 = vdot(vn, vn), mv2 = tf[2] * tf[2];
+            if (v2 > mv2) vn = vscale(vn, sqrtf(mv2 / v2));
+            S.ru[0] = wn.x; S.ru[1] = wn.y; S.ru[2] = wn.z;
+            S.ru[3] = vn.x; S.ru[4] = vn.y; S.ru[5] = vn.z;
+        }
+        __syncthreads();
+    }
     // ---- outward pass: accelerations (lanes 0..5, one component each)
-    if (act && ln < 6) S.va[0][ln] = ln < 3 ? 0.0f : -(ln == 3 ? gw.x : (ln == 4 ? gw.y : gw.z));
+    if (act && ln < 6 && !fb) S.va[0][ln] = ln < 3 ? 0.0f : -(ln == 3 ? gw.x : (ln == 4 ? gw.y : gw.z));
     for (int l = 1; l < LA; ++l) {
         const int p = A.link_i[l * MG_LINK_I_N + 0], dof = A.link_i[l * MG_LINK_I_N + 2];
         float a = 0.0f;
@@ -410,20 +493,28 @@ __device__ __forceinline__ void aba_world(const MgStep& P, const MgEnvArgs& A, E
 // every entry sees the same subtractions in the same order as the left-looking
 // loops of the oracle), lane j solves column j of M_eff^-1 into mcol[].
 // Called by every lane; `act` selects the envs that work. ND: static bound on D.
+// Floating base: the root slots DA..DA+5 (unit spatial axes at x0) extend the
+// matrix to NA = DA + 6: M[root r][root c] = IC_0[r][c], M[d][root r] = (IC_l xi_l)[r].
 template <int MAXL, int ND>
 __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, int DA, V3 x0, const LinkC& lk,
                            float (&mcol)[ND]) {
+    const bool fb = A.floating != 0;
+    const int NA = fb ? DA + 6 : DA;
     if (act && ln < LA) world_inertia(lk, S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
     __syncthreads();
     if (act)
         for (int l = LA - 1; l >= 1; --l) {
             const int p = A.link_i[l * MG_LINK_I_N + 0];
-            if (p > 0)
+            if (p > 0 || (fb && p == 0))
                 for (int e = ln; e < 36; e += G) S.Iw[p][e] = S.Iw[p][e] + S.Iw[l][e];
         }
-    if (act && ln < DA)
-        for (int j = 0; j < DA; ++j) S.Lc[ln][j] = 0.0f;
+    if (act && ln < NA)
+        for (int j = 0; j < NA; ++j) S.Lc[ln][j] = 0.0f;
     __syncthreads();
+    if (act && fb && ln >= DA && ln < NA) {
+        const int r = ln - DA;
+        for (int c = 0; c < 6; ++c) S.Lc[ln][DA + c] = S.Iw[0][r * 6 + c];
+    }
     if (act && ln < DA) {
         const int l = S.dlink[ln];
         float F[6];
@@ -439,17 +530,22 @@ __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool a
             }
             j = A.link_i[j * MG_LINK_I_N + 0];
         }
+        if (fb)
+            for (int r = 0; r < 6; ++r) {
+                S.Lc[ln][DA + r] = F[r];
+                S.Lc[DA + r][ln] = F[r];
+            }
     }
     __syncthreads();
     // all 64 lanes run the register phases (DPP reads neighbouring lanes);
     // envs that are not `act` compute on stale data and discard it
     float a[ND], invd[ND];
-    const int row = ln < DA ? ln : 0;
+    const int row = ln < NA ? ln : 0;
 #pragma unroll
-    for (int k = 0; k < ND; ++k) a[k] = k < DA ? S.Lc[row][k] : 0.0f;
+    for (int k = 0; k < ND; ++k) a[k] = k < NA ? S.Lc[row][k] : 0.0f;
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
-        if (j < DA) {
+        if (j < NA) {
             const float dj = bcast16(sqrtf(a[j]), j);
             invd[j] = 1.0f / dj;
             if (ln == j) a[j] = dj;
@@ -457,7 +553,7 @@ __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool a
             const float col = a[j];                          // L[ln][j]
 #pragma unroll
             for (int k = j + 1; k < ND; ++k)
-                if (k < DA) {
+                if (k < NA) {
                     const float lk = bcast16(col, k);        // L[k][j]
                     if (ln >= k) a[k] = a[k] - col * lk;
                 }
@@ -466,7 +562,7 @@ __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool a
     // column ln of M_eff^-1: forward then backward substitution, L[i][k] from lane i
 #pragma unroll
     for (int i = 0; i < ND; ++i) {
-        if (i < DA) {
+        if (i < NA) {
             float t = i == ln ? 1.0f : 0.0f;
 #pragma unroll
             for (int k = 0; k < i; ++k) t = t - bcast16(a[k], i) * mcol[k];
@@ -475,11 +571,11 @@ __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool a
     }
 #pragma unroll
     for (int i = ND - 1; i >= 0; --i) {
-        if (i < DA) {
+        if (i < NA) {
             float t = mcol[i];
 #pragma unroll
             for (int k = i + 1; k < ND; ++k)
-                if (k < DA) t = t - bcast16(a[i], k) * mcol[k];
+                if (k < NA) t = t - bcast16(a[i], k) * mcol[k];
             mcol[i] = t * invd[i];
         }
     }
@@ -505,10 +601,14 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     const float h = P.h;
     const V3 gvec = v3(P.g[0], P.g[1], P.g[2]);
 
-    // slot of this lane
+    // slot of this lane: DOFs, the floating root's (w, v_O), free bodies
+    const int RB = (L > 0 && A.floating) ? 6 : 0;
+    const int NS = D + RB;
     const bool is_dof = ln < D;
-    const int fk = ln >= D ? (ln - D) / 6 : MAXF;
-    const int fc = ln >= D ? (ln - D) % 6 : 0;
+    const bool is_root = ln >= D && ln < NS;
+    const int rc = ln - D;
+    const int fk = ln >= NS ? (ln - NS) / 6 : MAXF;
+    const int fc = ln >= NS ? (ln - NS) % 6 : 0;
     const bool is_free = fk < nfr;
 
     // ---- substep-invariant setup
@@ -521,6 +621,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     V3 fsum = v3(0.0f, 0.0f, 0.0f), lsum = v3(0.0f, 0.0f, 0.0f);
     V3 gw = v3(0.0f, 0.0f, 0.0f);
     const int LA = A.nl, DA = A.ndof;           // launch-uniform loop bounds (barriers inside)
+    const int NA = (LA > 0 && A.floating) ? DA + 6 : DA;   // articulation velocity slots
     if (L > 0) {
         x0 = v3(St[0 * nb + b0], St[1 * nb + b0], St[2 * nb + b0]);
         q0 = qnormalize(q4(St[3 * nb + b0], St[4 * nb + b0], St[5 * nb + b0], St[6 * nb + b0]));
@@ -584,6 +685,13 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         dc.tpos = A.dof_tpos[gd];
         dc.tvel = A.dof_tvel[gd];
         dc.force = A.dof_force[gd];
+    } else if (is_root) {
+        // root slots: w and the velocity of the base origin v_O = v_com - w x (R c)
+        const V3 w = v3(St[10 * nb + b0], St[11 * nb + b0], St[12 * nb + b0]);
+        const V3 vc = v3(St[7 * nb + b0], St[8 * nb + b0], St[9 * nb + b0]);
+        const V3 c0 = v3(A.mass[8 * nb + b0], A.mass[9 * nb + b0], A.mass[10 * nb + b0]);
+        const V3 vo = vsub(vc, vcross(w, qrot(q0, c0)));
+        uv = rc < 3 ? v3c(w, rc) : v3c(vo, rc - 3);
     } else if (is_free) {
         const int b = ei[3 + fk];
         uv = St[(7 + fc) * nb + b];
@@ -611,7 +719,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             bool redo = live && L > 0;
             for (int att = 0; att < 2; ++att) {
                 if (!__any(redo)) break;
-                aba_world<MAXL>(P, A, S, redo, ln, LA, x0, q0, gw, lk, dc, is_dof, xm, xp);
+                aba_world<MAXL>(P, A, S, redo, ln, LA, x0, q0, gw, lk, dc, is_dof, xm, xp, b0);
                 // drives whose implicit force exceeds the effort limit
                 bool flip = false;
                 if (redo && is_dof && dc.eff > 0.0f && S.imp[ln] != 0.0f) {
@@ -627,7 +735,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         // free body k (lane k): gravity, external force, damping, speed clamps
         if (live && ln < nfr) {
             const int k = ln;
-            const int s0 = D + 6 * k;
+            const int s0 = NS + 6 * k;
             const S3 Iw = sym_rdrt(qmat(qmul(S.fq[k], fr.iq)), fr.invI);
             S.fIw[k] = Iw;
             S.fxc[k] = vadd(S.fx[k], qrot(S.fq[k], fr.com));
@@ -652,6 +760,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             float w = uv + h * S.qdd[ln];
             if (maxv > 0.0f) w = fminf(fmaxf(w, -maxv), maxv);
             uv = w;
+        } else if (is_root) {
+            uv = S.ru[rc];
         } else if (is_free) {
             uv = S.u[ln];
         }
@@ -690,12 +800,14 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 nnear += __popc(gm);
             }
             __syncthreads();
+            PH_MARK(8);
             for (int rb = 0; __any(rb < nnear); rb += G) {
                 PairOut o;
                 o.n = 0;
                 float mu = 0.0f, rest = 0.0f;
                 int pa = 0, pb = -1;
                 if (rb + ln < nnear) {
+                    PH_COUNT(10, 1);
                     const int* pp = A.pairs + (size_t)(pair0 + S.npl[rb + ln]) * 4;
                     pa = pp[0];
                     const int sa = pp[1];
@@ -716,6 +828,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         Q4 qb;
                         pair_pose(S, pb, xb, qb);
                         collide(ca, place_shape(shb, xb, qb, A.hulls), P.contact_offset, o);
+                        PH_COUNT(11, ((int)sha[0] == MG_SHAPE_CONVEX || (int)shb[0] == MG_SHAPE_CONVEX) ? 1 : 0);
                         mu = 0.5f * (sha[11] + shb[11]);
                         rest = 0.5f * (sha[12] + shb[12]);
                     }
@@ -747,6 +860,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 base += total;
             }
             __syncthreads();
+            PH_MARK(9);
         }
         // joint-limit rows (PhysX solves limits as constraints): a DOF whose
         // predicted position q + h u lies within 5% of its range of a limit gets
@@ -818,6 +932,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     } else if (is_dof) {
                         if (a < F0 && ((S.amask[a] >> ln) & 1))
                             J = myrev ? vdot(vcross(myz, vsub(p, myx)), dir) : vdot(myz, dir);
+                    } else if (is_root) {
+                        if (a < F0) J = rc < 3 ? v3c(vcross(vsub(p, x0), dir), rc) : v3c(dir, rc - 3);
                     } else if (is_free) {
                         const float sg = a == F0 + fk ? 1.0f : (b == F0 + fk ? -1.0f : 0.0f);
                         if (sg != 0.0f) {
@@ -838,8 +954,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         float w = 0.0f;
 #pragma unroll
                         for (int k = 0; k < ND; ++k)
-                            if (k < DA) w = w + mcol[k] * bcast16(J, k);
-                        if (is_dof) W = w;
+                            if (k < NA) w = w + mcol[k] * bcast16(J, k);
+                        if (is_dof || is_root) W = w;
                     }
                     Jr[c * 3 + rw] = J;
                     Wr[c * 3 + rw] = W;
@@ -947,9 +1063,15 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 }
             }
         }
+        if (RB > 0) {
+            // floating root (every lane keeps x0, q0): the origin moves by dpos_v,
+            // the orientation turns by dpos_w
+            x0 = vadd(x0, v3(S.dpos[D + 3], S.dpos[D + 4], S.dpos[D + 5]));
+            q0 = qintegrate(q0, v3(S.dpos[D + 0], S.dpos[D + 1], S.dpos[D + 2]));
+        }
         if (live && ln < nfr) {
             const int k = ln;
-            const int s0 = D + 6 * k;
+            const int s0 = NS + 6 * k;
             const V3 dx = v3(S.dpos[s0 + 0], S.dpos[s0 + 1], S.dpos[s0 + 2]);
             const V3 dth = v3(S.dpos[s0 + 3], S.dpos[s0 + 4], S.dpos[s0 + 5]);
             const V3 xc1 = vadd(S.fxc[k], dx);
@@ -993,7 +1115,10 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             if (p < 0) {
                 S.ql[l] = q0;
                 S.xl[l] = x0;
-                put6(S.va[l], svzero());
+                // root velocity in the base frame (zero for a fixed base)
+                const V3 w = RB ? v3(S.u[D + 0], S.u[D + 1], S.u[D + 2]) : v3(0.0f, 0.0f, 0.0f);
+                const V3 vo = RB ? v3(S.u[D + 3], S.u[D + 4], S.u[D + 5]) : v3(0.0f, 0.0f, 0.0f);
+                put6(S.va[l], sv(qrot(qconj(q0), w), qrot(qconj(q0), vo)));
             } else {
                 const V3 ax = v3(A.link_f[l * MG_LINK_F_N + 7], A.link_f[l * MG_LINK_F_N + 8],
                                  A.link_f[l * MG_LINK_F_N + 9]);
@@ -1029,7 +1154,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     if (live && ln < nfr) {
         const int k = ln;
         const int b = ei[3 + k];
-        const int s0 = D + 6 * k;
+        const int s0 = NS + 6 * k;
         const V3 x = S.fx[k];
         const Q4 q = S.fq[k];
         St[0 * nb + b] = x.x; St[1 * nb + b] = x.y; St[2 * nb + b] = x.z;
@@ -1047,7 +1172,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s) {
     if (A.ne <= 0) return hipSuccess;
     const int blocks = (A.ne + EPW - 1) / EPW;
-    if (A.nl <= 4 && A.ndof <= 4)
+    if (A.nl <= 4 && A.ndof <= 4 && !A.floating)
         MG_LAUNCH((k_env_step<4>), dim3(blocks), dim3(64), 0, s, P, A);
     else if (A.nl <= MG_MAX_LINKS && A.ndof <= G)
         MG_LAUNCH((k_env_step<MG_MAX_LINKS>), dim3(blocks), dim3(64), 0, s, P, A);

@@ -74,8 +74,9 @@ struct MgArticArgs {
 };
 
 // Coupled per-env step (mg_env.hip): MG_ENV_G lanes per env, one lane per
-// generalized-velocity slot (articulation DOFs first, then 6 per free body),
-// so D + 6 nf <= MG_ENV_G. env_i rows (MG_ENV_I_N int32):
+// generalized-velocity slot (articulation DOFs first, then, for a floating
+// base, the root's spatial velocity (w, v at the base origin), then 6 per free
+// body), so D + 6 fb + 6 nf <= MG_ENV_G. env_i rows (MG_ENV_I_N int32):
 //   [0] first internal body of the env's articulation or -1, [1] its first DOF,
 //   [2] free bodies nf <= MG_ENV_MAXF, [3..6] their internal slots,
 //   [7] static bodies ns <= MG_ENV_MAXS, [8..11] their internal slots,
@@ -100,6 +101,7 @@ struct MgEnvArgs {
     const int*   env_i;       // [ne][MG_ENV_I_N]
     const int*   pairs;       // [..][4] candidate shape pairs (env_i[14], [15])
     int          nl, ndof;    // articulation template of this launch (0 links: none)
+    int          floating;    // the template has a floating base: 6 root velocity slots after the DOFs
     const float* link_f;
     const int*   link_i;
     float*       state;

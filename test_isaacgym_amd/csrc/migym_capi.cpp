@@ -63,7 +63,7 @@ struct ArticGroup {
 
 // coupled envs (mg_env.hip) of one articulation template (tmpl -1: none)
 struct EnvGroup {
-    int tmpl, first_link, nl, ndof;
+    int tmpl, first_link, nl, ndof, floating;
     int offset, count;   // rows of d_env
 };
 
@@ -403,6 +403,11 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
             for (int a : art) {
                 for (int t : stc) coupled = coupled || collide(a, t);
                 for (int f : fr) coupled = coupled || collide(a, f);
+                // a floating-base articulation always steps here (ground contacts,
+                // the root's own dynamics)
+                const int k = artic_of_root[m->actor_root_body[a]];
+                if (k >= 0 && !m->artic_tmpl_i[m->artic_i[(size_t)k * MG_ARTIC_I_N + 2] * MG_ATMPL_I_N + 3])
+                    coupled = true;
             }
 #ifdef MG_COUPLE_ARTICULATIONS
             coupled = coupled || !art.empty();
@@ -413,17 +418,18 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                             "env %d: %zu articulations / %zu free / %zu static bodies in contact range; the "
                             "coupled step supports 1 / %d / %d", e, art.size(), fr.size(), stc.size(),
                             MG_ENV_MAXF, MG_ENV_MAXS);
-            int art_nl = 0, art_nd = 0;
+            int art_nl = 0, art_nd = 0, art_fb = 0;
             if (!art.empty()) {
                 const int k = artic_of_root[m->actor_root_body[art[0]]];
                 const int t = k >= 0 ? m->artic_i[(size_t)k * MG_ARTIC_I_N + 2] : -1;
                 if (t < 0 || t >= m->num_artic_tmpls) return fail(MG_ERR_ARG, "env %d: bad articulation", e);
                 art_nl = m->artic_tmpl_i[t * MG_ATMPL_I_N + 1];
                 art_nd = m->artic_tmpl_i[t * MG_ATMPL_I_N + 2];
+                art_fb = m->artic_tmpl_i[t * MG_ATMPL_I_N + 3] ? 0 : 1;
             }
-            if (art_nd + 6 * (int)fr.size() > MG_ENV_G)
-                return fail(MG_ERR_UNSUPPORTED, "env %d: %d DOFs + %zu free bodies exceed the %d velocity slots of "
-                            "the coupled step", e, art_nd, fr.size(), MG_ENV_G);
+            if (art_nd + 6 * art_fb + 6 * (int)fr.size() > MG_ENV_G)
+                return fail(MG_ERR_UNSUPPORTED, "env %d: %d DOFs%s + %zu free bodies exceed the %d velocity slots of "
+                            "the coupled step", e, art_nd, art_fb ? " + a floating base" : "", fr.size(), MG_ENV_G);
             std::array<int, MG_ENV_I_N> row;
             row.fill(0);
             row[0] = -1;
@@ -486,14 +492,14 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                         shp(row[3 + j], &sb0, &nsb);
                         for (int sb = sb0; sb < sb0 + nsb; ++sb) push(MG_ENV_FREE0 + k, sa, MG_ENV_FREE0 + j, sb);
                     }
-                    if (row[0] >= 0 && ((mask >> k) & 1)) {
+                    if (row[0] >= 0 && !art_fb && ((mask >> k) & 1)) {   // the fixed base (static)
                         int sb0, nsb;
                         shp(row[0], &sb0, &nsb);
                         for (int sb = sb0; sb < sb0 + nsb; ++sb) push(MG_ENV_FREE0 + k, sa, 0, sb);
                     }
                 }
             }
-            for (int l = 1; l < art_nl; ++l) {
+            for (int l = art_fb ? 0 : 1; l < art_nl; ++l) {     // moving links (a floating base moves)
                 int sa0, nsa;
                 shp(row[0] + l, &sa0, &nsa);
                 for (int sa = sa0; sa < sa0 + nsa; ++sa) {
@@ -556,8 +562,6 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         if (g.nl < 1 || g.nl > MG_MAX_LINKS || g.ndof > g.nl || g.ndof > MG_MAX_DOFS || g.first_link < 0 ||
             g.first_link + g.nl > s->ntl)
             return fail(MG_ERR_UNSUPPORTED, "articulation template %d: %d links / %d dofs unsupported", t, g.nl, g.ndof);
-        if (!g.fixed_base)
-            return fail(MG_ERR_UNSUPPORTED, "articulation template %d: floating-base articulations are not supported yet", t);
         for (int l = 0; l < g.nl; ++l) {
             const int* li = m->tmpl_link_i + (size_t)(g.first_link + l) * MG_LINK_I_N;
             if (li[0] >= l || (l > 0 && li[0] < 0) || (l == 0 && li[0] != -1))
@@ -585,6 +589,9 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
             }
             g.count++;
         }
+        if (!g.fixed_base && g.step_count > 0)
+            return fail(MG_ERR_UNSUPPORTED, "articulation template %d: a floating base steps in the coupled "
+                        "per-env kernel, which needs actor_coll", t);
         s->groups.push_back(g);
     }
 
@@ -603,6 +610,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
             g.first_link = m->artic_tmpl_i[t * MG_ATMPL_I_N + 0];
             g.nl = m->artic_tmpl_i[t * MG_ATMPL_I_N + 1];
             g.ndof = m->artic_tmpl_i[t * MG_ATMPL_I_N + 2];
+            g.floating = m->artic_tmpl_i[t * MG_ATMPL_I_N + 3] ? 0 : 1;
         }
         g.offset = (int)env_flat.size() / MG_ENV_I_N;
         for (size_t r = 0; r < env_rows.size(); ++r) {
@@ -740,6 +748,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.pairs = s->d_pairs;
         A.nl = g.tmpl >= 0 ? g.nl : 0;
         A.ndof = g.tmpl >= 0 ? g.ndof : 0;
+        A.floating = g.tmpl >= 0 ? g.floating : 0;
         A.link_f = s->d_link_f + (size_t)(g.tmpl >= 0 ? g.first_link : 0) * MG_LINK_F_N;
         A.link_i = s->d_link_i + (size_t)(g.tmpl >= 0 ? g.first_link : 0) * MG_LINK_I_N;
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;

@@ -147,6 +147,8 @@ class Gym:
         try:
             if filename.lower().endswith(".urdf"):
                 asset = _assets.load_urdf(rootpath, filename, _copy_options(options))
+            elif filename.lower().endswith(".xml") or filename.lower().endswith(".mjcf"):
+                asset = _assets.load_mjcf(rootpath, filename, _copy_options(options))
             else:
                 print("*** migym: unsupported asset format: %s" % filename, file=sys.stderr)
                 return None

@@ -19,6 +19,7 @@ reference scripts build them:
 and the synthetic random actions of SURVEY.md §8d (seeded torch generators).
 """
 import math
+import numpy as np
 import os
 
 import torch
@@ -331,3 +332,45 @@ def franka_scene(gym, num_envs, use_gpu_pipeline=True, device=0, controller="osc
     info = dict(envs=envs, box_idxs=box_idxs, hand_idxs=hand_idxs, init_pos=init_pos, init_rot=init_rot,
                 hand_index=hand_index, default_dof_pos=default_pos, num_dofs=ndof, controller=controller)
     return sim, info
+
+
+def ant_sim_params(use_gpu_pipeline=True):
+    """examples/apply_forces.py:31-41: z-up, g = -9.81, 1 substep, TGS 4/1."""
+    sp = gymapi.SimParams()
+    sp.up_axis = gymapi.UP_AXIS_Z
+    sp.gravity = gymapi.Vec3(0.0, 0.0, -9.81)
+    sp.substeps = 1
+    sp.physx.solver_type = 1
+    sp.physx.num_position_iterations = 4
+    sp.physx.num_velocity_iterations = 1
+    sp.use_gpu_pipeline = use_gpu_pipeline
+    return sp
+
+
+def ant_scene(gym, num_envs, use_gpu_pipeline=True, device=0, asset_root=None, asset_file="mjcf/ant.xml",
+              spacing=2.0, seed=17, height=1.0, sim_params=None, asset_options=None):
+    """examples/apply_forces.py:51-100: the MJCF ant (a floating-base
+    articulation, 9 bodies, 8 hinge DOFs) at z = `height` in a sqrt(n)-per-row
+    grid, collision group i, filter 1, random bright colours; ground plane n = +z.
+    Returns (sim, info) with info["num_bodies"], ["envs"], ["actors"]."""
+    sp = sim_params or ant_sim_params(use_gpu_pipeline)
+    sim = gym.create_sim(device, device, gymapi.SIM_PHYSX, sp)
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim, plane)
+    asset = gym.load_asset(sim, asset_root or ASSET_ROOT, asset_file, asset_options or gymapi.AssetOptions())
+    nb = gym.get_asset_rigid_body_count(asset)
+    pose = gymapi.Transform()
+    pose.p.z = height
+    per_row = max(int(np.sqrt(num_envs)), 1)
+    lo, hi = gymapi.Vec3(-spacing, -spacing, 0.0), gymapi.Vec3(spacing, spacing, spacing)
+    rng = np.random.RandomState(seed)
+    envs, actors = [], []
+    for i in range(num_envs):
+        env = gym.create_env(sim, lo, hi, per_row)
+        c = 0.5 + 0.5 * rng.random_sample(3)
+        a = gym.create_actor(env, asset, pose, "actor", i, 1)
+        gym.set_rigid_body_color(env, a, 0, gymapi.MESH_VISUAL_AND_COLLISION, gymapi.Vec3(*c))
+        envs.append(env)
+        actors.append(a)
+    return sim, {"num_bodies": nb, "envs": envs, "actors": actors, "asset": asset}

@@ -43,10 +43,11 @@ def run(n, warm=150, steps=100):
     torch.cuda.synchronize()
     phases = None
     if hasattr(N.lib, "mg_debug_env_phase"):
-        buf = (ctypes.c_ulonglong * 8)()
+        buf = (ctypes.c_ulonglong * 12)()
         N.lib.mg_debug_env_phase(buf)
         waves = (n + 3) // 4
-        names = ["unconstrained", "narrowphase", "crba_minv", "rows", "tgs", "integrate", "setup", "outputs"]
+        names = ["unconstrained", "narrowphase_rest", "crba_minv", "rows", "tgs", "integrate", "setup", "outputs",
+                 "np_screen", "np_collide", "pairs_tested", "pairs_with_hull"]
         phases = {nm: buf[i] / waves / steps for i, nm in enumerate(names)}   # cycles per wave per frame
     avg, lo = ctypes.c_float(), ctypes.c_float()
     used = N.lib.mg_step_time_stats(sim.native, steps, ctypes.byref(avg), ctypes.byref(lo), None)
