@@ -26,6 +26,7 @@ bounded sample of the same workload.
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -92,6 +93,31 @@ def cpu_baseline(seconds=10.0, threads=None):
                       "single thread: %d steps (%.1f s)" % (sn, threads, en, s1, e1)}
 
 
+GRAPH_CHUNK = 8      # tensor-API steps captured per hipGraph (amortizes the graph launch)
+
+
+def graph_chunk(steps, slots):
+    """Steps per captured graph: GRAPH_CHUNK when it divides both the timed step
+    count and the action-slot cycle, else the largest common divisor."""
+    return math.gcd(math.gcd(steps, slots), GRAPH_CHUNK)
+
+
+def capture_chunks(step, slots, chunk):
+    """hipGraphs of `chunk` consecutive steps each, covering the action slots
+    0..slots-1 in order (graph c runs step(c * chunk) .. step(c * chunk + chunk - 1)),
+    sharing one memory pool. Replaying graph (k / chunk) % len runs exactly the
+    steps the eager loop would run for k .. k + chunk - 1."""
+    graphs, pool = [], None
+    for c in range(slots // chunk):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=pool):
+            for j in range(c * chunk, (c + 1) * chunk):
+                step(j)
+        pool = g.pool()
+        graphs.append(g)
+    return graphs
+
+
 def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     """S2 servo-arm: n fixed-base 3-DOF gimbals under random PD
     position targets; one step = set_dof_position_target_tensor -> simulate ->
@@ -114,35 +140,30 @@ def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     torch.cuda.synchronize(dev)
     avg = ctypes.c_float()
     used = N.lib.mg_step_time_stats(sim.native, min(warmup // 2, 512), ctypes.byref(avg), None, None)
-    # hipGraph replay, one captured step per target slot (as the S1 loop)
+    # hipGraph replay, `chunk` captured steps per graph (as the S1 loop)
     graphs = None
+    chunk = graph_chunk(steps, tg.shape[0])
+    base = -(-(warmup + chunk) // chunk) * chunk       # chunk-aligned slot of the first timed step
     if use_graph:
         try:
-            graphs, pool = [], None
-            for j in range(tg.shape[0]):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
-                    step(j)
-                pool = g.pool()
-                graphs.append(g)
-            for j in range(3):
-                graphs[(warmup + j) % len(graphs)].replay()
+            graphs = capture_chunks(step, tg.shape[0], chunk)
+            graphs[(base // chunk - 1) % len(graphs)].replay()
         except Exception as ex:
             print("*** bench: S2 hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
             graphs = None
-    base = warmup + 3
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(steps):
-        if graphs is not None:
-            graphs[(base + k) % len(graphs)].replay()
-        else:
+    if graphs is not None:
+        for i in range(steps // chunk):
+            graphs[(base // chunk + i) % len(graphs)].replay()
+    else:
+        for k in range(steps):
             step(base + k)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     gym.destroy_sim(sim)
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
-            "timed_loop": "hipGraph replay" if graphs is not None else "eager Python loop",
+            "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graphs is not None else "eager Python loop",
             "kernel": "k_artic_world<4>", "kernel_ms_avg": avg.value if used > 0 else None,
             "algorithmic_bytes_per_env": 532}
 
@@ -194,6 +215,7 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
     torch.cuda.synchronize(dev)
     eager_ms = 1e3 * (time.perf_counter() - t_e) / 10
     graph = None
+    chunk = math.gcd(steps, GRAPH_CHUNK)
     if use_graph:
         try:
             side = torch.cuda.Stream(dev)
@@ -204,17 +226,19 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
             torch.cuda.current_stream(dev).wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                step()
+                for _ in range(chunk):
+                    step()
             graph.replay()
         except Exception as ex:
             print("*** bench: S3 hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
             graph = None
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        if graph is not None:
+    if graph is not None:
+        for _ in range(steps // chunk):
             graph.replay()
-        else:
+    else:
+        for _ in range(steps):
             step()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
@@ -223,7 +247,7 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
            "coupled_envs": int(N.lib.mg_num_coupled_envs(sim.native)),
            "cubes_lifted_frac": float(lifted.float().mean()),
            "controller": "OSC (franka_cube_ik_osc.py:59-79,348-410) on the device",
-           "timed_loop": "hipGraph replay" if graph is not None else "eager Python loop",
+           "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graph is not None else "eager Python loop",
            "eager_ms_per_step": eager_ms}
     gym.destroy_sim(sim)
     return out
@@ -380,10 +404,11 @@ def main():
     hi = ctypes.c_float()
     used = N.lib.mg_step_time_stats(sim.native, min(neager, 512), ctypes.byref(avg),
                                     ctypes.byref(lo), ctypes.byref(hi))
-    # hipGraph replay: one captured step per action slot j (the step that applies
-    # acts[j]), sharing one memory pool; step k replays graph k % slots, so the
-    # replayed sequence is exactly step(k)'s
+    # hipGraph replay: graphs of `chunk` consecutive captured steps (step j applies
+    # acts[j]), sharing one memory pool; the replayed sequence is exactly the eager
+    # loop's, and one graph launch is paid per `chunk` steps instead of per step
     graphs = None
+    chunk = graph_chunk(args.steps, acts.shape[0])
     if not args.eager and not gathered:
         try:
             side = torch.cuda.Stream(dev)
@@ -392,19 +417,12 @@ def main():
                 for j in range(3):
                     step(args.warmup + neager + j)
             torch.cuda.current_stream(dev).wait_stream(side)
-            base = args.warmup + neager + 3
-            graphs = []
-            pool = None
-            for j in range(acts.shape[0]):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
-                    step(j)
-                pool = g.pool()
-                graphs.append(g)
-            # capture does not run the work: replay three steps to settle
-            for j in range(3):
-                graphs[(base + j) % len(graphs)].replay()
-            base += 3
+            graphs = capture_chunks(step, acts.shape[0], chunk)
+            # capture does not run the work: replay one chunk to settle, then
+            # time from the next chunk-aligned slot
+            base = -(-(args.warmup + neager + 3) // chunk) * chunk
+            graphs[(base // chunk) % len(graphs)].replay()
+            base += chunk
         except Exception as ex:          # capture unsupported here: time the eager loop
             print("*** bench: hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
             graphs = None
@@ -412,10 +430,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        if graphs is not None:
-            graphs[(base + k) % len(graphs)].replay()
-        else:
+    if graphs is not None:
+        for i in range(args.steps // chunk):
+            graphs[(base // chunk + i) % len(graphs)].replay()
+    else:
+        for k in range(args.steps):
             step(args.warmup + neager + k)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -460,7 +479,8 @@ def main():
                 "parallelism": "env-sharded, one process per GPU%s" % (", RCCL all-gather of root state"
                                                                         if gathered else
                                                                         ", no collectives"),
-                "timed_loop": "hipGraph replay: one captured tensor-API step per action slot" if graphs is not None
+                "timed_loop": ("hipGraph replay: %d captured tensor-API steps per graph (every step's full "
+                               "kernel sequence, action slot by slot)" % chunk) if graphs is not None
                               else "eager Python loop",
                 "eager_ms_per_step": eager_ms,
             },

@@ -379,26 +379,56 @@ MG_HD void deep4_emit(const Deep4& D, PairOut& o) {
         if (k < D.n) pair_push(o, D.p[k], D.nrm[k], D.s[k]);
 }
 
-// convex A vs convex B (box or hull), vertex penetration both ways
+// local vertex i of a hull (clamped to the last vertex: prefetch beyond the end)
+MG_HD V3 hull_vl(const float* V, int n, int i) {
+    const int j = i < n ? i : n - 1;
+    return v3(V[3 * j], V[3 * j + 1], V[3 * j + 2]);
+}
+
+// the candidates of X's vertices against Y's face planes, in vertex order, into
+// D: a vertex v within the margin (cvx_sd: the largest plane distance s, first
+// face f on ties) gives (s, v, n_f) when the point is taken on X (onY false), or
+// (s, v - n_f s, -n_f) on Y's face. A hull X streams its vertices 4 ahead.
+MG_HD void cvx_vertices_vs(const CShape& X, const CShape& Y, float margin, bool onY, Deep4& D) {
+    const int nx = cvx_nv(X);
+    if (X.type == MG_SHAPE_CONVEX) {
+        const float* V = X.hv + MG_HULL_HEADER;
+        V3 r0 = hull_vl(V, nx, 0), r1 = hull_vl(V, nx, 1), r2 = hull_vl(V, nx, 2), r3 = hull_vl(V, nx, 3);
+        for (int i = 0; i < nx; ++i) {
+            const V3 l = r0;
+            r0 = r1; r1 = r2; r2 = r3;
+            r3 = hull_vl(V, nx, i + 4);
+            const V3 v = vadd(X.c, mmul(X.R, l));            // cvx_vertex(X, i)
+            int f;
+            const float sv = cvx_sd(Y, v, f, 0.0f, margin);
+            if (sv < margin) {
+                const V3 n = cvx_normal(Y, f);
+                if (onY) deep4_add(D, sv, vsub(v, vscale(n, sv)), vscale(n, -1.0f));
+                else deep4_add(D, sv, v, n);
+            }
+        }
+        return;
+    }
+    for (int i = 0; i < nx; ++i) {
+        const V3 v = cvx_vertex(X, i);
+        int f;
+        const float sv = cvx_sd(Y, v, f, 0.0f, margin);
+        if (sv < margin) {
+            const V3 n = cvx_normal(Y, f);
+            if (onY) deep4_add(D, sv, vsub(v, vscale(n, sv)), vscale(n, -1.0f));
+            else deep4_add(D, sv, v, n);
+        }
+    }
+}
+
+// convex A vs convex B (box or hull), vertex penetration both ways: A's vertices
+// by B's planes (normal = B's face normal), then B's vertices by A's planes
+// (point on A's face, normal = -A's)
 MG_HD void convex_convex(const CShape& A, const CShape& B, float margin, PairOut& o) {
     Deep4 D;
     D.n = 0;
-    const int na = cvx_nv(A), nb = cvx_nv(B);
-    for (int i = 0; i < na; ++i) {           // A's vertices by B's planes: normal = B's face normal
-        const V3 v = cvx_vertex(A, i);
-        int f;
-        const float s = cvx_sd(B, v, f, 0.0f, margin);
-        if (s < margin) deep4_add(D, s, v, cvx_normal(B, f));
-    }
-    for (int i = 0; i < nb; ++i) {           // B's vertices by A's planes: point on A's face, normal = -A's
-        const V3 v = cvx_vertex(B, i);
-        int f;
-        const float s = cvx_sd(A, v, f, 0.0f, margin);
-        if (s < margin) {
-            const V3 na_ = cvx_normal(A, f);
-            deep4_add(D, s, vsub(v, vscale(na_, s)), vscale(na_, -1.0f));
-        }
-    }
+    cvx_vertices_vs(A, B, margin, false, D);
+    cvx_vertices_vs(B, A, margin, true, D);
     deep4_emit(D, o);
 }
 

@@ -172,8 +172,13 @@ MG_HD void ground_pair(const MgStep& P, const CShape& s, PairOut& o) {
         Deep4 D;
         D.n = 0;
         const int nv = cvx_nv(s);
+        const float* V = s.hv + MG_HULL_HEADER;           // vertices streamed 4 ahead
+        V3 r0 = hull_vl(V, nv, 0), r1 = hull_vl(V, nv, 1), r2 = hull_vl(V, nv, 2), r3 = hull_vl(V, nv, 3);
         for (int i = 0; i < nv; ++i) {
-            const V3 p = cvx_vertex(s, i);
+            const V3 l = r0;
+            r0 = r1; r1 = r2; r2 = r3;
+            r3 = hull_vl(V, nv, i + 4);
+            const V3 p = vadd(s.c, mmul(s.R, l));          // cvx_vertex(s, i)
             const float sep = vdot(n, p) + P.pd;
             if (sep < off) deep4_add(D, sep, p, n);
         }

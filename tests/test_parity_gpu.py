@@ -388,10 +388,11 @@ def test_mass_matrix_consistent_with_aba(gym):
 def test_hipgraph_replay_matches_eager(gym):
     """The tensor-API step captured into a hipGraph (torch.cuda.graph; the library
     records its kernels into the capture and leaves out its timing events) and
-    replayed 50 times gives the same states, bit for bit, as 50 eager steps."""
+    replayed 50 times gives the same states, bit for bit, as 50 eager steps; so
+    does a graph of 5 consecutive steps replayed 10 times (bench.py's chunks)."""
     n, steps = 256, 50
     outs = []
-    for mode in ("eager", "graph"):
+    for mode in ("eager", "graph", "graph5"):
         sim, _ = scenes.servo_scene(gym, n)
         gym.prepare_sim(sim)
         root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
@@ -414,14 +415,17 @@ def test_hipgraph_replay_matches_eager(gym):
             for _ in range(steps):
                 step()
         else:
+            per = 5 if mode == "graph5" else 1
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                step()
+                for _ in range(per):
+                    step()
             # capture records without executing: replay all the steps
-            for _ in range(steps):
+            for _ in range(steps // per):
                 g.replay()
         torch.cuda.synchronize()
         outs.append(rb.cpu().numpy().copy())
         gym.destroy_sim(sim)
     assert np.all(np.isfinite(outs[0]))
     assert np.array_equal(outs[0], outs[1]), "max |diff| %g" % np.abs(outs[0] - outs[1]).max()
+    assert np.array_equal(outs[0], outs[2]), "max |diff| %g" % np.abs(outs[0] - outs[2]).max()
