@@ -13,7 +13,7 @@ import math
 import numpy as np
 import torch
 
-from .torch_utils import quat_conjugate, quat_mul, quat_rotate
+from .torch_utils import quat_conjugate, quat_mul
 
 
 def _inv(a):
@@ -27,6 +27,19 @@ def _bmm(a, b):
     multiply and a reduction: rocBLAS batched GEMM tiles cost ~58 us per call at
     4096 x 7x7 on MI355X, this ~5 us."""
     return (a.unsqueeze(-1) * b.unsqueeze(-3)).sum(-2)
+
+
+def quat_rotate(q, v):
+    """torch_utils.quat_rotate with the q_vec . v dot product as an elementwise
+    multiply-sum instead of a (n,1,3)x(n,3,1) torch.bmm: same formula, but the
+    bmm dispatches a 256x16 hipBLASLt tile at ~56 us per call on MI355X (three
+    calls per S3 frame, rocprof r01), this ~5 us."""
+    q_w = q[:, -1:]
+    q_vec = q[:, :3]
+    a = v * (2.0 * q_w * q_w - 1.0)
+    b = torch.cross(q_vec, v, dim=-1) * q_w * 2.0
+    c = q_vec * (q_vec * v).sum(-1, keepdim=True) * 2.0
+    return a + b + c
 
 
 def quat_axis(q, axis=0):
