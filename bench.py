@@ -9,53 +9,169 @@ in HBM:
     gym.refresh_actor_root_state_tensor(sim)
     gym.refresh_rigid_body_state_tensor(sim)
     gym.refresh_dof_state_tensor(sim)               (0 DOFs in S1)
-Weak scaling: every rank owns 4096 envs on its own GPU (one process per GPU,
-launched by torch.distributed.run); envs never interact, so there is no
-collective on the data path. --allgather adds the optional RCCL
-all-gather of the root-state observation.
+
+Multi-GPU (BASELINE config 4): one process and one sim per GPU,
+4096 envs per rank (weak scaling). `--gpus N` either runs under
+torch.distributed.run (WORLD_SIZE set) or, without it, starts the N rank
+processes itself (test_isaacgym_amd/launch.py) before anything touches the GPU.
+Envs never interact, so the timed loop has no collective; at N > 1 a second leg
+times the optional RCCL all-gather of the root-state observation over xGMI
+(`allgather`), and `--allgather` puts it inside the timed loop instead.
+
+Timing: W warm-up steps, a kernel-timing segment (>= 100 eager launches with
+dispatch-timestamp events), an eager segment with timing off, then the timed
+region — EXACTLY `--steps` steps replayed as hipGraphs, bracketed by barrier +
+synchronize, repeated `--repeats` times; `value` uses the median repeat of the
+per-repeat maximum over ranks.
 
 Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel
 (k_rigid_step, one launch per simulate) at SURVEY.md §8d's algorithmic bytes:
 376 B per env per simulate (2 bodies x (state in 52 + state out 52 + mass
-properties 44 + shape 40)), over its average duration taken from the kernel's own
+properties 44 + shape 40)), over its average duration from the kernel's own
 dispatch timestamps (hipExtLaunchKernelGGL start / stop events on the simulate
-stream; the interval rocprofv3 reports).
-`cpu_baseline` times the C restatement (oracle/, "port") on the host cores (16 threads on the GPU box) on a
-bounded sample of the same workload.
+stream, the interval rocprofv3 reports). `large_n` repeats that at 262,144 envs,
+where the kernel leaves the latency regime. `cpu_baseline` times the C
+restatement (oracle/, "port") on the host cores on a bounded sample of the same
+workload.
 """
 import argparse
-import ctypes
+import importlib.util
 import json
 import math
 import os
+import statistics
 import sys
 import time
-
-import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from isaacgym import gymapi, gymtorch  # noqa: E402
-from test_isaacgym_amd import _native as N  # noqa: E402
-from test_isaacgym_amd import scenes, sharding  # noqa: E402
-
 METRIC = "env-steps/sec (whole node), 4096 servo envs; 1/2/4/8-GPU scaling"
 ENVS_PER_GPU = 4096
+LARGE_N = 262144
 SIM_BYTES_PER_ENV = 376          # SURVEY.md §8d S1: simulate share of the 688 B/env-step
 STEP_BYTES_PER_ENV = 688         # whole tensor-API step
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+KERNEL_TIMED_LAUNCHES = 128      # eager launches with dispatch timestamps (ring holds 256)
+GRAPH_CHUNK = 8                  # tensor-API steps captured per hipGraph (amortizes the graph launch)
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=600)
+    ap.add_argument("--warmup", type=int, default=60)
+    ap.add_argument("--repeats", type=int, default=5, help="timed regions of --steps steps; value = median")
+    ap.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
+    ap.add_argument("--allgather", action="store_true",
+                    help="RCCL all-gather of the root state inside the timed loop (N > 1)")
+    ap.add_argument("--backend", choices=("auto", "nccl", "gloo"), default="auto",
+                    help="process-group backend for N > 1 (auto: RCCL when every rank has its own GPU)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: ranks build their shards and check the gathered layout over gloo")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-gimbal", action="store_true", help="skip the secondary S2 servo-arm measurement")
+    ap.add_argument("--no-franka", action="store_true", help="skip the secondary S3 Franka cube-pick measurement")
+    ap.add_argument("--no-cameras", action="store_true", help="skip the secondary S5 camera-render measurement")
+    ap.add_argument("--no-large-n", action="store_true", help="skip the 262,144-env S1 kernel leg")
+    ap.add_argument("--large-n", type=int, default=LARGE_N)
+    ap.add_argument("--camera-envs", type=int, default=1024)
+    ap.add_argument("--eager", action="store_true",
+                    help="time the Python loop itself instead of a hipGraph replay of the step")
+    return ap.parse_args(argv)
+
+
+def _launcher():
+    """test_isaacgym_amd/launch.py loaded by path: the parent must not import the
+    package (it loads libmigym.so) before the ranks exist."""
+    spec = importlib.util.spec_from_file_location("_mg_launch", os.path.join(ROOT, "test_isaacgym_amd", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+# --------------------------------------------------------------------------- helpers
+def graph_chunk(steps, slots):
+    """Steps per captured graph: GRAPH_CHUNK when it divides both the timed step
+    count and the action-slot cycle, else the largest common divisor."""
+    return math.gcd(math.gcd(steps, slots), GRAPH_CHUNK)
+
+
+def capture_chunks(step, slots, chunk):
+    """hipGraphs of `chunk` consecutive steps each, covering the action slots
+    0..slots-1 in order (graph c runs step(c * chunk) .. step(c * chunk + chunk - 1)),
+    sharing one memory pool. Replaying graph (k / chunk) % len runs exactly the
+    steps the eager loop would run for k .. k + chunk - 1."""
+    import torch
+    graphs, pool = [], None
+    for c in range(slots // chunk):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=pool):
+            for j in range(c * chunk, (c + 1) * chunk):
+                step(j)
+        pool = g.pool()
+        graphs.append(g)
+    return graphs
+
+
+def kernel_stats(sim, n_launches, run):
+    """Run `run()` (n_launches eager simulate calls) with dispatch-timestamp
+    events on, then return (avg_ms, min_ms, launches) of the step kernels."""
+    import ctypes
+    import torch
+    from test_isaacgym_amd import _native as N
+    N.lib.mg_set_kernel_timing(sim.native, 1)
+    try:
+        run()
+        torch.cuda.synchronize()
+    finally:
+        N.lib.mg_set_kernel_timing(sim.native, 0)
+    avg, lo = ctypes.c_float(), ctypes.c_float()
+    used = N.lib.mg_step_time_stats(sim.native, min(n_launches, 256), ctypes.byref(avg), ctypes.byref(lo), None)
+    if used <= 0:
+        return None, None, 0
+    return avg.value, lo.value, int(used)
+
+
+def load_pmc(name):
+    """Committed rocprofv3 PMC summary (profiles/<round>_pmc_<name>.json, newest
+    round first, written by profiles/collect_pmc.py): (dict, file) or (None, None)."""
+    for rnd in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", "%s_pmc_%s.json" % (rnd, name))
+        if os.path.exists(path):
+            with open(path) as f:
+                return json.load(f), os.path.relpath(path, ROOT)
+    return None, None
+
+
+def rigid_roofline(n, kern_ms, kmin, launches, segment):
+    bytes_launch = SIM_BYTES_PER_ENV * n
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms else None
+    pmc, pmc_file = load_pmc("rigid_%d" % n)
+    return {"bound": "hbm", "kernel": "k_rigid_step",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "traffic_source": pmc_file,
+            "algorithmic_bytes_per_launch": bytes_launch,
+            "algorithmic_bytes_per_env": SIM_BYTES_PER_ENV,
+            "kernel_ms_avg": kern_ms, "kernel_ms_min": kmin, "kernel_launches_timed": launches,
+            "kernel_timing": "dispatch timestamps of every k_rigid_step launch (hipExtLaunchKernelGGL start/stop "
+                             "events, the interval rocprofv3 reports) over %s" % segment}
+
+
+# --------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(seconds=10.0, threads=None):
     """The oracle (C restatement) on the same 4096-env scene, on `threads` host
     cores: each step splits the bodies into contiguous ranges, one per thread
     (oracle.step's body_range; ctypes releases the GIL, envs are independent),
     plus a single-thread figure on the same sample for reference."""
     import concurrent.futures as cf
+    import numpy as np
     import oracle
+    from isaacgym import gymapi
+    from test_isaacgym_amd import scenes
     gym = gymapi.acquire_gym()
     sim, _ = scenes.servo_scene(gym, ENVS_PER_GPU, use_gpu_pipeline=False)
     sim.build_model()
@@ -66,7 +182,9 @@ def cpu_baseline(seconds=10.0, threads=None):
     acts = scenes.servo_actions(ENVS_PER_GPU, 16, "cpu", seed=0).numpy()
     dof = np.zeros((0, 2), np.float32)
     cforce = np.zeros((nb, 3), np.float32)
-    threads = threads or max(1, min(16, os.cpu_count() or 1))    # 16 = the GPU box's CPU share
+    ncpu = os.cpu_count() or 1
+    # 16 = the GPU box's CPU share per GPU (os.cpu_count() there shows the whole machine)
+    threads = threads or max(1, min(16, ncpu))
 
     def run(nthr, budget):
         cuts = [nb * k // nthr for k in range(nthr + 1)]
@@ -87,41 +205,22 @@ def cpu_baseline(seconds=10.0, threads=None):
     s1, e1 = run(1, seconds * 0.3)
     sn, en = run(threads, seconds * 0.7) if threads > 1 else (s1, e1)
     return {"value": ENVS_PER_GPU * sn / en, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "host_cpu_count": ncpu,
             "single_thread_value": ENVS_PER_GPU * s1 / e1,
             "sample": "%d simulate() steps of the 4096-env servo scene with random root teleports, "
-                      "oracle/migym_oracle.c on %d host threads, bodies split into contiguous ranges (%.1f s); "
-                      "single thread: %d steps (%.1f s)" % (sn, threads, en, s1, e1)}
+                      "oracle/migym_oracle.c (CPU restatement, not Isaac Gym) on %d host threads "
+                      "(os.cpu_count() = %d), bodies split into contiguous ranges (%.1f s); "
+                      "single thread: %d steps (%.1f s)" % (sn, threads, ncpu, en, s1, e1)}
 
 
-GRAPH_CHUNK = 8      # tensor-API steps captured per hipGraph (amortizes the graph launch)
-
-
-def graph_chunk(steps, slots):
-    """Steps per captured graph: GRAPH_CHUNK when it divides both the timed step
-    count and the action-slot cycle, else the largest common divisor."""
-    return math.gcd(math.gcd(steps, slots), GRAPH_CHUNK)
-
-
-def capture_chunks(step, slots, chunk):
-    """hipGraphs of `chunk` consecutive steps each, covering the action slots
-    0..slots-1 in order (graph c runs step(c * chunk) .. step(c * chunk + chunk - 1)),
-    sharing one memory pool. Replaying graph (k / chunk) % len runs exactly the
-    steps the eager loop would run for k .. k + chunk - 1."""
-    graphs, pool = [], None
-    for c in range(slots // chunk):
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=pool):
-            for j in range(c * chunk, (c + 1) * chunk):
-                step(j)
-        pool = g.pool()
-        graphs.append(g)
-    return graphs
-
-
+# --------------------------------------------------------------------------- secondary legs (N = 1)
 def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     """S2 servo-arm: n fixed-base 3-DOF gimbals under random PD
     position targets; one step = set_dof_position_target_tensor -> simulate ->
     refresh DOF + rigid-body state. Returns env-steps/s and the step kernel time."""
+    import torch
+    from isaacgym import gymapi, gymtorch
+    from test_isaacgym_amd import scenes
     gym = gymapi.acquire_gym()
     sim, _ = scenes.gimbal_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
     gym.prepare_sim(sim)
@@ -137,13 +236,11 @@ def gimbal_rate(n, steps, warmup, dev, use_graph=True):
 
     for k in range(warmup):
         step(k)
-    torch.cuda.synchronize(dev)
-    avg = ctypes.c_float()
-    used = N.lib.mg_step_time_stats(sim.native, min(warmup // 2, 512), ctypes.byref(avg), None, None)
-    # hipGraph replay, `chunk` captured steps per graph (as the S1 loop)
+    kms, kmin, used = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
+                                   lambda: [step(warmup + k) for k in range(KERNEL_TIMED_LAUNCHES)])
     graphs = None
     chunk = graph_chunk(steps, tg.shape[0])
-    base = -(-(warmup + chunk) // chunk) * chunk       # chunk-aligned slot of the first timed step
+    base = -(-(warmup + KERNEL_TIMED_LAUNCHES + chunk) // chunk) * chunk
     if use_graph:
         try:
             graphs = capture_chunks(step, tg.shape[0], chunk)
@@ -162,10 +259,12 @@ def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     gym.destroy_sim(sim)
+    ach = 532 * n / (kms * 1e-3) / 1e9 if kms else None
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
             "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graphs is not None else "eager Python loop",
-            "kernel": "k_artic_world<4>", "kernel_ms_avg": avg.value if used > 0 else None,
-            "algorithmic_bytes_per_env": 532}
+            "kernel": "S2 articulation step", "kernel_ms_avg": kms, "kernel_ms_min": kmin,
+            "kernel_launches_timed": used, "algorithmic_bytes_per_env": 532,
+            "kernel_achieved_GBs": ach}
 
 
 def franka_rate(n, steps, warmup, dev, use_graph=True):
@@ -174,7 +273,9 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
     DOF / Jacobian / mass-matrix tensors -> the script's controller on the device
     (test_isaacgym_amd.franka_control) -> set DOF position targets and efforts.
     Returns env-steps/s and the coupled-step kernel time."""
-    from test_isaacgym_amd import franka_control
+    import torch
+    from isaacgym import gymapi, gymtorch
+    from test_isaacgym_amd import _native as N, franka_control, scenes
     gym = gymapi.acquire_gym()
     sim, info = scenes.franka_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
     gym.prepare_sim(sim)
@@ -206,9 +307,8 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
 
     for _ in range(warmup):
         step()
+    kms, kmin, used = kernel_stats(sim, 100, lambda: [step() for _ in range(100)])
     torch.cuda.synchronize(dev)
-    avg = ctypes.c_float()
-    used = N.lib.mg_step_time_stats(sim.native, min(warmup // 2, 512), ctypes.byref(avg), None, None)
     t_e = time.perf_counter()
     for _ in range(10):
         step()
@@ -243,7 +343,8 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     out = {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
-           "kernel": "k_env_step<16>", "kernel_ms_avg": avg.value if used > 0 else None,
+           "kernel": "S3 coupled step (k_env_step<16>)", "kernel_ms_avg": kms, "kernel_ms_min": kmin,
+           "kernel_launches_timed": used,
            "coupled_envs": int(N.lib.mg_num_coupled_envs(sim.native)),
            "cubes_lifted_frac": float(lifted.float().mean()),
            "controller": "OSC (franka_cube_ik_osc.py:59-79,348-410) on the device",
@@ -260,6 +361,10 @@ def camera_rate(n, steps, warmup, dev, use_graph=True, width=1600, height=900):
     render_all_camera_sensors. Returns env-steps/s and the render kernel's
     time and write bandwidth (roofline: the kernel streams W*H*4 bytes per
     camera to HBM; reads are the env's few shapes)."""
+    import numpy as np
+    import torch
+    from isaacgym import gymapi, gymtorch
+    from test_isaacgym_amd import _native as N, scenes
     gym = gymapi.acquire_gym()
     sim, envs = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
     imgs = scenes.attach_servo_cameras(gym, sim, envs, width, height, 30.0)
@@ -278,11 +383,14 @@ def camera_rate(n, steps, warmup, dev, use_graph=True, width=1600, height=900):
         gym.render_all_camera_sensors(sim)
 
     gym.refresh_actor_root_state_tensor(sim)
-    rms = []
     for k in range(warmup):
         step(k)
-        if k >= warmup // 2:
-            rms.append(N.lib.mg_last_render_ms(sim.native))
+    rms = []
+    N.lib.mg_set_kernel_timing(sim.native, 1)
+    for k in range(20):
+        step(warmup + k)
+        rms.append(N.lib.mg_last_render_ms(sim.native))
+    N.lib.mg_set_kernel_timing(sim.native, 0)
     torch.cuda.synchronize(dev)
     graphs = None
     if use_graph:
@@ -295,11 +403,11 @@ def camera_rate(n, steps, warmup, dev, use_graph=True, width=1600, height=900):
                 pool = g.pool()
                 graphs.append(g)
             for j in range(2):
-                graphs[(warmup + j) % len(graphs)].replay()
+                graphs[(warmup + 20 + j) % len(graphs)].replay()
         except Exception as ex:
             print("*** bench: S5 hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
             graphs = None
-    base = warmup + 2
+    base = warmup + 22
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(steps):
@@ -310,72 +418,38 @@ def camera_rate(n, steps, warmup, dev, use_graph=True, width=1600, height=900):
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     lit = float((imgs[0][0][..., :3].amax(-1) > 0).float().mean())
+    lit_all = float(np.mean([float((imgs[i][0][..., :3].amax(-1) > 0).float().mean())
+                             for i in range(0, n, max(1, n // 16))]))
     gym.destroy_sim(sim)
+    rms = [r for r in rms if r > 0]
     rk = float(np.mean(rms)) if rms else float("nan")
     wbytes = n * width * height * 4
     ach = wbytes / (rk * 1e-3) / 1e9
-    traffic = None        # HBM bytes per launch, committed rocprofv3 WRITE_SIZE pass (tools/gpu_render_pmc.sh)
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc_render_%dx%dx%d.json" % (n, width, height))
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic = json.load(f).get("write_bytes_per_launch_from_WRITE_SIZE_KB")
+    pmc, pmc_file = load_pmc("render_%dx%dx%d" % (n, width, height))
+    traffic = pmc.get("write_bytes_per_launch_from_WRITE_SIZE_KB") if pmc else None
     return {"envs": n, "cameras": n, "resolution": [width, height], "env_steps_per_s": n * steps / el,
             "ms_per_step": 1e3 * el / steps, "timed_loop": "hipGraph replay" if graphs is not None else "eager",
-            "kernel": "k_render", "kernel_ms_avg": rk, "image_bytes_per_launch": wbytes,
+            "kernel": "k_render", "kernel_ms_avg": rk, "kernel_launches_timed": len(rms),
+            "image_bytes_per_launch": wbytes,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "traffic": traffic},
-            "env0_non_sky_fraction": lit}
+                         "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": pmc_file},
+            "env0_non_sky_fraction": lit, "sampled_cameras_non_sky_fraction": lit_all}
 
 
-def load_traffic(envs):
-    """HBM bytes per k_rigid_step launch at this env count from the committed
-    rocprofv3 PMC passes (profiles/r01_pmc_rigid_<envs>.json, written by
-    profiles/collect_pmc.py), else None."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_rigid_%d.json" % envs)
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_launch")
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=600)
-    ap.add_argument("--warmup", type=int, default=60)
-    ap.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
-    ap.add_argument("--allgather", action="store_true", help="RCCL all-gather of the root state every step")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-gimbal", action="store_true", help="skip the secondary S2 servo-arm measurement")
-    ap.add_argument("--no-franka", action="store_true", help="skip the secondary S3 Franka cube-pick measurement")
-    ap.add_argument("--no-cameras", action="store_true", help="skip the secondary S5 camera-render measurement")
-    ap.add_argument("--camera-envs", type=int, default=1024)
-    ap.add_argument("--eager", action="store_true",
-                    help="time the Python loop itself instead of a hipGraph replay of the step")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
+def large_n_rate(n, steps, dev, use_graph=True):
+    """S1 at `n` envs on one GPU (SURVEY.md §8d's large-N regime point): the same
+    tensor-API step; k_rigid_step's own duration over KERNEL_TIMED_LAUNCHES eager
+    launches, and the graph-replayed step rate."""
+    import torch
+    from isaacgym import gymapi, gymtorch
+    from test_isaacgym_amd import scenes
     gym = gymapi.acquire_gym()
-    n = args.envs
-    # rank k owns global envs [k n, (k+1) n), placed at their global grid cells
-    sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=local, env_offset=rank * n,
-                                grid_envs=world * n)
+    sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
     gym.prepare_sim(sim)
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     gym.acquire_rigid_body_state_tensor(sim)
     gym.acquire_dof_state_tensor(sim)
-    acts = scenes.servo_actions(n, 64, dev, seed=rank)
-    gathered = args.allgather and world > 1
+    acts = scenes.servo_actions(n, 16, dev, seed=1)
 
     def step(k):
         root[:, 3:10] = acts[k % acts.shape[0]]
@@ -385,25 +459,152 @@ def main():
         gym.refresh_actor_root_state_tensor(sim)
         gym.refresh_rigid_body_state_tensor(sim)
         gym.refresh_dof_state_tensor(sim)
-        if gathered:
+
+    gym.refresh_actor_root_state_tensor(sim)
+    for k in range(10):
+        step(k)
+    kms, kmin, used = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
+                                   lambda: [step(10 + k) for k in range(KERNEL_TIMED_LAUNCHES)])
+    chunk = graph_chunk(steps, acts.shape[0])
+    graphs = None
+    base = -(-(10 + KERNEL_TIMED_LAUNCHES) // chunk) * chunk
+    if use_graph:
+        try:
+            graphs = capture_chunks(step, acts.shape[0], chunk)
+            graphs[(base // chunk) % len(graphs)].replay()
+            base += chunk
+        except Exception as ex:
+            print("*** bench: large-N hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
+            graphs = None
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    if graphs is not None:
+        for i in range(steps // chunk):
+            graphs[(base // chunk + i) % len(graphs)].replay()
+    else:
+        for k in range(steps):
+            step(base + k)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    gym.destroy_sim(sim)
+    return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps, "steps": steps,
+            "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graphs is not None else "eager",
+            "roofline": rigid_roofline(n, kms, kmin, used, "%d eager steps after a 10-step warm-up" % used)}
+
+
+# --------------------------------------------------------------------------- dry run (no GPU)
+def dry_run(args, world, rank):
+    """Launcher / sharding rehearsal without a GPU: every rank builds its shard of
+    the servo scene (CPU pipeline, no simulate), the root-state tensors are
+    gathered over gloo, and rank 0 checks them against one sim of all envs."""
+    import numpy as np
+    import torch.distributed as dist
+    from isaacgym import gymapi, gymtorch
+    from test_isaacgym_amd import scenes, sharding
+    gym = gymapi.acquire_gym()
+    n = args.envs
+    sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=False, env_offset=rank * n, grid_envs=world * n)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    g = sharding.all_gather_rows(root) if world > 1 else root
+    if rank == 0:
+        ref, _ = scenes.servo_scene(gym, world * n, use_gpu_pipeline=False)
+        want = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(ref)).numpy()
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "env-steps/s", "n_gpus": world,
+                          "dry_run": True, "backend": dist.get_backend() if world > 1 else None,
+                          "envs_per_rank": n, "gathered_rows": int(g.shape[0]),
+                          "layout_matches_single_sim": bool(np.array_equal(g.numpy(), want))}), flush=True)
+    if world > 1:
+        dist.barrier()
+
+
+# --------------------------------------------------------------------------- main
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not under torch.distributed.run: start one process per GPU ourselves,
+        # before this process touches HIP
+        rc, codes = _launcher().spawn_ranks([os.path.abspath(__file__)] + sys.argv[1:], args.gpus)
+        if rc != 0:
+            print("*** bench: rank exit codes %s" % codes, file=sys.stderr)
+        sys.exit(rc)
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    from test_isaacgym_amd import sharding
+    ndev = 0 if args.dry_run else torch.cuda.device_count()
+    backend = args.backend if args.backend != "auto" else sharding.backend_for(world, ndev)
+    if args.dry_run:
+        backend = "gloo"
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    if args.dry_run:
+        dry_run(args, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if ndev <= 0:
+        raise SystemExit("bench: no GPU visible (use --dry-run for the host rehearsal)")
+    dev_index = local % ndev
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    cdev = dev if backend == "nccl" else torch.device("cpu")      # where collective operands live
+
+    from isaacgym import gymapi, gymtorch
+    from test_isaacgym_amd import scenes
+
+    gym = gymapi.acquire_gym()
+    n = args.envs
+    # rank k owns global envs [k n, (k+1) n), placed at their global grid cells
+    sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=dev_index, env_offset=rank * n,
+                                grid_envs=world * n)
+    gym.prepare_sim(sim)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    gym.acquire_rigid_body_state_tensor(sim)
+    gym.acquire_dof_state_tensor(sim)
+    acts = scenes.servo_actions(n, 64, dev, seed=rank)
+    gathered = args.allgather and world > 1
+
+    def step(k, gather=gathered):
+        root[:, 3:10] = acts[k % acts.shape[0]]
+        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.simulate(sim)
+        gym.fetch_results(sim, False)
+        gym.refresh_actor_root_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_dof_state_tensor(sim)
+        if gather:
             sharding.all_gather_rows(root)      # RCCL over xGMI: (world * 2n, 13) observation
 
     gym.refresh_actor_root_state_tensor(sim)
-    for k in range(args.warmup):
+    k = 0
+    for _ in range(args.warmup):
         step(k)
-    # eager reference timing (the warmup's last half) and the kernel durations
+        k += 1
+    # kernel-timing segment: dispatch timestamps on, >= 100 eager launches
+    k0 = k
+    kern_ms, kmin, used = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
+                                       lambda: [step(k0 + j) for j in range(KERNEL_TIMED_LAUNCHES)])
+    k += KERNEL_TIMED_LAUNCHES
+    # eager segment, timing off: what an unmodified script's Python loop costs
+    neager = 32
     torch.cuda.synchronize(dev)
     t_e = time.perf_counter()
-    neager = max(args.warmup // 2, 1)
-    for k in range(neager):
-        step(args.warmup + k)
+    for _ in range(neager):
+        step(k)
+        k += 1
     torch.cuda.synchronize(dev)
     eager_ms = 1e3 * (time.perf_counter() - t_e) / neager
-    avg = ctypes.c_float()
-    lo = ctypes.c_float()
-    hi = ctypes.c_float()
-    used = N.lib.mg_step_time_stats(sim.native, min(neager, 512), ctypes.byref(avg),
-                                    ctypes.byref(lo), ctypes.byref(hi))
+
     # hipGraph replay: graphs of `chunk` consecutive captured steps (step j applies
     # acts[j]), sharing one memory pool; the replayed sequence is exactly the eager
     # loop's, and one graph launch is paid per `chunk` steps instead of per step
@@ -415,46 +616,72 @@ def main():
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 for j in range(3):
-                    step(args.warmup + neager + j)
+                    step(k + j)
             torch.cuda.current_stream(dev).wait_stream(side)
             graphs = capture_chunks(step, acts.shape[0], chunk)
             # capture does not run the work: replay one chunk to settle, then
             # time from the next chunk-aligned slot
-            base = -(-(args.warmup + neager + 3) // chunk) * chunk
-            graphs[(base // chunk) % len(graphs)].replay()
-            base += chunk
+            k = -(-(k + 3) // chunk) * chunk
+            graphs[(k // chunk) % len(graphs)].replay()
+            k += chunk
         except Exception as ex:          # capture unsupported here: time the eager loop
             print("*** bench: hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
             graphs = None
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    if graphs is not None:
-        for i in range(args.steps // chunk):
-            graphs[(base // chunk + i) % len(graphs)].replay()
-    else:
-        for k in range(args.steps):
-            step(args.warmup + neager + k)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    if graphs is None:
-        used = N.lib.mg_step_time_stats(sim.native, min(args.steps, 512), ctypes.byref(avg), ctypes.byref(lo),
-                                        ctypes.byref(hi))
 
-    kern_ms = avg.value if used > 0 else float("nan")
+    def run_steps(k_first, nsteps):
+        if graphs is not None:
+            for i in range(nsteps // chunk):
+                graphs[(k_first // chunk + i) % len(graphs)].replay()
+        else:
+            for j in range(nsteps):
+                step(k_first + j)
 
-    ms_per_step = 1e3 * el / args.steps
+    def timed(fn, reps):
+        """Each repeat bracketed by barrier + synchronize; returns the per-repeat
+        elapsed seconds of every rank, shape (world, reps)."""
+        els = []
+        for r in range(reps):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            fn(r)
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            els.append(time.perf_counter() - t0)
+        t = torch.tensor(els, dtype=torch.float64, device=cdev)
+        if world > 1:
+            parts = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(parts, t)
+            return [p.cpu().tolist() for p in parts]
+        return [els]
+
+    reps = max(1, args.repeats)
+    per_rank = timed(lambda r: run_steps(k + r * args.steps, args.steps), reps)
+    k += reps * args.steps
+    el_max = [max(per_rank[q][r] for q in range(world)) for r in range(reps)]
+    el = statistics.median(el_max)
     value = world * n * args.steps / el
-    bytes_launch = SIM_BYTES_PER_ENV * n
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if used > 0 else None
-    traffic = load_traffic(n)
+    ms_per_step = 1e3 * el / args.steps
+
+    # optional RCCL all-gather of the observation (N > 1): the gather alone and
+    # the eager step loop with one gather per step
+    gather_leg = None
+    if world > 1 and not gathered:
+        gsteps = max(args.steps, 20)
+        g_el = timed(lambda r: [sharding.all_gather_rows(root) for _ in range(gsteps)], 3)
+        g_ms = 1e3 * statistics.median([max(g_el[q][r] for q in range(world)) for r in range(3)]) / gsteps
+        s_el = timed(lambda r: [step(k + j, gather=True) for j in range(gsteps)], 1)
+        s_ms = 1e3 * max(s_el[q][0] for q in range(world)) / gsteps
+        k += gsteps
+        rb = root.numel() * root.element_size()
+        gather_leg = {"backend": backend, "bytes_per_rank": rb, "bytes_gathered": rb * world,
+                      "ms_per_gather": g_ms, "GB_per_s_received": rb * (world - 1) / (g_ms * 1e-3) / 1e9,
+                      "step_with_gather_ms": s_ms,
+                      "env_steps_per_s_with_gather": world * n / (s_ms * 1e-3),
+                      "loop": "eager Python loop: step + all_gather_into_tensor of the (2n, 13) root state"}
+
     out = None
     if rank == 0:
         out = {
@@ -476,45 +703,41 @@ def main():
                             "every step, full tensor-API loop",
                 "envs_per_gpu": n,
                 "global_envs": world * n,
-                "parallelism": "env-sharded, one process per GPU%s" % (", RCCL all-gather of root state"
-                                                                        if gathered else
-                                                                        ", no collectives"),
+                "parallelism": "env-sharded, one process per GPU (%s)%s" % (
+                    backend if world > 1 else "single rank",
+                    ", all-gather of root state in the loop" if gathered else ", no collectives in the loop"),
                 "timed_loop": ("hipGraph replay: %d captured tensor-API steps per graph (every step's full "
                                "kernel sequence, action slot by slot)" % chunk) if graphs is not None
                               else "eager Python loop",
+                "repeats": reps,
+                "ms_per_step_runs": [1e3 * e / args.steps for e in el_max],
+                "ms_per_step_per_rank": [[1e3 * e / args.steps for e in row] for row in per_rank],
                 "eager_ms_per_step": eager_ms,
+                "eager_note": "eager Python loop with kernel timing off (timing is opt-in: mg_set_kernel_timing)",
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_rigid_step",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": bytes_launch,
-                "kernel_ms_avg": kern_ms,
-                "kernel_ms_min": lo.value if used > 0 else None,
-                "kernel_launches_timed": int(used),
-                "kernel_timing": "dispatch timestamps of k_rigid_step (hipExtLaunchKernelGGL start/stop events, "
-                                 "the interval rocprofv3 reports) for every simulate() of the eager %s" % (
-                    "segment after the warmup (graph replays carry no events)" if graphs is not None
-                    else "timed loop"),
-                "note": "working set of 4096 envs (~2.8 MB) sits in L2/MALL: the step is launch/latency "
-                        "bound at this size (SURVEY.md §0.10)",
-            },
+            "roofline": dict(rigid_roofline(n, kern_ms, kmin, used,
+                                            "a %d-step eager segment after the warm-up" % KERNEL_TIMED_LAUNCHES),
+                             note="working set of 4096 envs (~2.8 MB) sits in L2/MALL: the step is "
+                                  "latency bound at this size (SURVEY.md §0.10); see large_n"),
         }
-        if world == 1 and not args.no_gimbal:
+        if gather_leg:
+            out["allgather"] = gather_leg
+    if world == 1:
+        if not args.no_large_n:
+            out["large_n"] = large_n_rate(args.large_n, 64, dev, not args.eager)
+        if not args.no_gimbal:
             out["s2_servo_arm"] = gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
-        if world == 1 and not args.no_franka:
+        if not args.no_franka:
             out["s3_franka"] = franka_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
-        if world == 1 and not args.no_cameras:
+        if not args.no_cameras:
             out["s5_cameras"] = camera_rate(args.camera_envs, min(args.steps, 100), 10, dev, not args.eager)
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
         print(json.dumps(out), flush=True)
     gym.destroy_sim(sim)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

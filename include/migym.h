@@ -272,7 +272,13 @@ int32_t     mg_render_cameras(mg_sim* sim, const mg_camera* cams, int32_t n, voi
 float       mg_last_render_ms(mg_sim* sim);
 
 /* ---- introspection for tests and the bench ------------------------------- */
-/* Duration in ms of the last simulate()'s kernels (HIP events on `stream`),
+/* Kernel timing is opt-in (default off): while on, every eager simulate() and
+ * render launches its kernels with dispatch-timestamp events (hipExtLaunch-
+ * KernelGGL start / stop) and records begin / end events; while off, simulate
+ * enqueues only its kernels and fetch_results(wait) synchronises the stream.
+ * Stream capture never records events. Returns the previous setting. */
+int32_t     mg_set_kernel_timing(mg_sim* sim, int32_t on);
+/* Duration in ms of the last timed simulate()'s kernels (HIP events on `stream`),
  * -1 when unavailable. Synchronises on the step's end event. */
 float       mg_last_step_ms(mg_sim* sim);
 /* Average / min / max over the last n simulate() calls (at most 256; eager

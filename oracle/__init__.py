@@ -59,11 +59,13 @@ def step(sim_params, model, state, dof, tgt=None, props=None, ext=None, cforce=N
     if cforce is None:
         cforce = np.zeros((nb, 3), dtype=np.float32)
     b0, b1 = body_range if body_range is not None else (0, -1)
+    # converted copies bound to locals so they outlive the call
+    tgt_c = np.ascontiguousarray(tgt, dtype=np.float32)
+    props_c = None if props is None else np.ascontiguousarray(props, dtype=np.float32)
+    ext_c = None if ext is None else np.ascontiguousarray(ext, dtype=np.float32)
+    assert cforce.dtype == np.float32 and cforce.flags.c_contiguous and cforce.shape == (nb, 3)
     rc = lib().oracle_step(ctypes.addressof(sim_params), ctypes.addressof(model), _ptr(state), _ptr(dof),
-                           _ptr(np.ascontiguousarray(tgt, dtype=np.float32)),
-                           _ptr(None if props is None else np.ascontiguousarray(props, dtype=np.float32)),
-                           _ptr(None if ext is None else np.ascontiguousarray(ext, dtype=np.float32)),
-                           _ptr(cforce), int(b0), int(b1))
+                           _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), int(b0), int(b1))
     if rc != 0:
         raise RuntimeError("oracle_step: unsupported model")
     return cforce

@@ -193,7 +193,7 @@ hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream
 hipError_t mg_launch_gather_rows(const float* soa, int stride, int ncol, const int* ids, int n,
                                  float* aos, hipStream_t s);
 hipError_t mg_launch_scatter_rows(const float* aos, int ncol, const int* ids, const int* sel,
-                                  int n, float* soa, int stride, hipStream_t s);
+                                  int n, int nrows, float* soa, int stride, hipStream_t s);
 hipError_t mg_launch_scatter_dofs(const float* aos, int ncol, const int* actor_dof, const int* sel,
-                                  int nsel, int max_dofs, float* const* dst, hipStream_t s);
+                                  int nsel, int nactors, int max_dofs, float* const* dst, hipStream_t s);
 hipError_t mg_launch_jacobian(const MgArticArgs& A, float* jac, float* mm, hipStream_t s);

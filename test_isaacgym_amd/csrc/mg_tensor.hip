@@ -23,13 +23,16 @@ __global__ void k_gather_rows(const float* __restrict__ soa, int stride, int nco
 }
 
 // for k < n: i = sel ? sel[k] : k;  soa[f][ids ? ids[i] : i] = aos[i][f]
+// A selected row outside [0, nrows) is skipped (user indices are not trusted).
 __global__ void k_scatter_rows(const float* __restrict__ aos, int ncol, const int* __restrict__ ids,
-                               const int* __restrict__ sel, int n, float* __restrict__ soa, int stride) {
+                               const int* __restrict__ sel, int n, int nrows, float* __restrict__ soa,
+                               int stride) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n * ncol) return;
     const int k = t / ncol;
     const int f = t - k * ncol;
     const int i = sel ? sel[k] : k;
+    if (i < 0 || i >= nrows) return;
     const int r = ids ? ids[i] : i;
     soa[(long)f * stride + r] = aos[(long)i * ncol + f];
 }
@@ -37,8 +40,10 @@ __global__ void k_scatter_rows(const float* __restrict__ aos, int ncol, const in
 // DOF rows selected by actor: for k < nsel, a = sel[k], j < count(a):
 //   d = actor_dof[a] + j;  dst[c][d] = src[d][c]   (c < ncol)
 // sel == null: every DOF row (nsel = num_dofs, max_dofs = 1, actor_dof unused).
+// A selected actor outside [0, nactors) is skipped.
 __global__ void k_scatter_dofs(const float* __restrict__ src, int ncol, const int* __restrict__ actor_dof,
-                               const int* __restrict__ sel, int nsel, int max_dofs, float* dst0, float* dst1) {
+                               const int* __restrict__ sel, int nsel, int nactors, int max_dofs, float* dst0,
+                               float* dst1) {
     const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (long)nsel * max_dofs) return;
     int d;
@@ -46,6 +51,7 @@ __global__ void k_scatter_dofs(const float* __restrict__ src, int ncol, const in
         const int k = (int)(t / max_dofs);
         const int j = (int)(t - (long)k * max_dofs);
         const int a = sel[k];
+        if (a < 0 || a >= nactors) return;
         const int d0 = actor_dof[a], d1 = actor_dof[a + 1];
         if (d0 + j >= d1) return;
         d = d0 + j;
@@ -70,18 +76,18 @@ hipError_t mg_launch_gather_rows(const float* soa, int stride, int ncol, const i
 }
 
 hipError_t mg_launch_scatter_rows(const float* aos, int ncol, const int* ids, const int* sel, int n,
-                                  float* soa, int stride, hipStream_t s) {
+                                  int nrows, float* soa, int stride, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (ncol <= 0 || (long)n * ncol >= (1L << 31)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_scatter_rows, dim3(nblocks((long)n * ncol, 256)), dim3(256), 0, s,
-                       aos, ncol, ids, sel, n, soa, stride);
+                       aos, ncol, ids, sel, n, nrows, soa, stride);
     return hipGetLastError();
 }
 
 hipError_t mg_launch_scatter_dofs(const float* src, int ncol, const int* actor_dof, const int* sel,
-                                  int nsel, int max_dofs, float* const* dst, hipStream_t s) {
+                                  int nsel, int nactors, int max_dofs, float* const* dst, hipStream_t s) {
     if (nsel <= 0 || max_dofs <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_scatter_dofs, dim3(nblocks((long)nsel * max_dofs, 256)), dim3(256), 0, s,
-                       src, ncol, actor_dof, sel, nsel, max_dofs, dst[0], dst[1]);
+                       src, ncol, actor_dof, sel, nsel, nactors, max_dofs, dst[0], dst[1]);
     return hipGetLastError();
 }

@@ -134,6 +134,9 @@ struct mg_sim {
     bool rendered = false;
 
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    bool timing = false;          // mg_set_kernel_timing: events around eager launches
+    bool timed_step = false;      // the last simulate recorded ev_begin / ev_end
+    hipStream_t last_stream = nullptr;
     bool stepped = false;
     bool capturing = false;       // the last simulate was recorded into a graph
     // ring of per-simulate event pairs for live kernel timing (bench.py roofline)
@@ -240,6 +243,7 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
     if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
     if (s->nd == 0) return MG_OK;
     if (!src) return fail(MG_ERR_ARG, "null source tensor");
+    if (idx && n_idx < 0) return fail(MG_ERR_ARG, "negative index count");
     HIP_TRY(hipSetDevice(s->device));
     const float* dsrc;
     const int* didx;
@@ -247,9 +251,9 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
     if (rc) return rc;
     float* dst[2] = {dst0, dst1};
     if (idx)
-        HIP_TRY(mg_launch_scatter_dofs(dsrc, ncol, s->d_actor_dof, didx, n_idx, s->max_actor_dofs, dst, st));
+        HIP_TRY(mg_launch_scatter_dofs(dsrc, ncol, s->d_actor_dof, didx, n_idx, s->na, s->max_actor_dofs, dst, st));
     else
-        HIP_TRY(mg_launch_scatter_dofs(dsrc, ncol, nullptr, nullptr, s->nd, 1, dst, st));
+        HIP_TRY(mg_launch_scatter_dofs(dsrc, ncol, nullptr, nullptr, s->nd, 0, 1, dst, st));
     return MG_OK;
 }
 
@@ -714,7 +718,8 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         ~TimerScope() { mg_timer = nullptr; }
     } timer_scope;
     int slot = 0;
-    if (!s->capturing) {
+    const bool timed = s->timing && !s->capturing;
+    if (timed) {
         slot = (int)(s->ring_n % mg_sim::kRing);
         s->ev_begin = s->ring_b[slot];
         s->ev_end = s->ring_e[slot];
@@ -776,9 +781,13 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     }
     mg_timer = nullptr;
     if (!s->capturing) {
-        HIP_TRY(hipEventRecord(s->ev_end, st));
-        s->kern_n[slot] = timer.used;
-        s->ring_n++;
+        if (timed) {
+            HIP_TRY(hipEventRecord(s->ev_end, st));
+            s->kern_n[slot] = timer.used;
+            s->ring_n++;
+        }
+        s->timed_step = timed;
+        s->last_stream = st;
         s->stepped = true;
     }
     return MG_OK;
@@ -786,12 +795,22 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
 
 int32_t mg_fetch_results(mg_sim* s, int32_t wait) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
-    if (wait && s->stepped && !s->capturing) HIP_TRY(hipEventSynchronize(s->ev_end));
+    if (wait && s->stepped && !s->capturing) {
+        if (s->timed_step) HIP_TRY(hipEventSynchronize(s->ev_end));
+        else HIP_TRY(hipStreamSynchronize(s->last_stream));
+    }
     return MG_OK;
 }
 
+int32_t mg_set_kernel_timing(mg_sim* s, int32_t on) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    const int32_t prev = s->timing ? 1 : 0;
+    s->timing = on != 0;
+    return prev;
+}
+
 float mg_last_step_ms(mg_sim* s) {
-    if (!s || !s->stepped) return -1.0f;
+    if (!s || !s->stepped || !s->timed_step) return -1.0f;
     if (hipEventSynchronize(s->ev_end) != hipSuccess) return -1.0f;
     float ms = -1.0f;
     if (hipEventElapsedTime(&ms, s->ev_begin, s->ev_end) != hipSuccess) return -1.0f;
@@ -857,8 +876,8 @@ int32_t mg_set_actor_root_state(mg_sim* s, const float* src, int32_t src_host, c
     const int* didx;
     int rc = stage_src(s, src, src_host, (size_t)s->na * MG_STATE_N, idx, n_idx, st, &dsrc, &didx);
     if (rc) return rc;
-    HIP_TRY(mg_launch_scatter_rows(dsrc, MG_STATE_N, s->d_actor_root, didx, idx ? n_idx : s->na, s->d_state,
-                                   s->nb, st));
+    HIP_TRY(mg_launch_scatter_rows(dsrc, MG_STATE_N, s->d_actor_root, didx, idx ? n_idx : s->na, s->na,
+                                   s->d_state, s->nb, st));
     return MG_OK;
 }
 
@@ -872,7 +891,8 @@ int32_t mg_set_rigid_body_state(mg_sim* s, const float* src, int32_t src_host, v
     int rc = stage_src(s, src, src_host, (size_t)s->nb * MG_STATE_N, nullptr, 0, st, &dsrc, &didx);
     if (rc) return rc;
     // free bodies only: rows are selected through the free-body list
-    HIP_TRY(mg_launch_scatter_rows(dsrc, MG_STATE_N, s->d_perm, s->d_free_global, s->nf, s->d_state, s->nb, st));
+    HIP_TRY(mg_launch_scatter_rows(dsrc, MG_STATE_N, s->d_perm, s->d_free_global, s->nf, s->nb, s->d_state,
+                                   s->nb, st));
     return MG_OK;
 }
 
@@ -921,7 +941,8 @@ int32_t mg_apply_rigid_body_force(mg_sim* s, const float* force, const float* to
         const int* didx;
         int rc = stage_src(s, parts[k], src_host, (size_t)s->nb * 3, nullptr, 0, st, &dsrc, &didx);
         if (rc) return rc;
-        HIP_TRY(mg_launch_scatter_rows(dsrc, 3, s->d_perm, nullptr, s->nb, s->d_ext + (size_t)k * 3 * s->nb, s->nb, st));
+        HIP_TRY(mg_launch_scatter_rows(dsrc, 3, s->d_perm, nullptr, s->nb, s->nb, s->d_ext + (size_t)k * 3 * s->nb,
+                                       s->nb, st));
         if (src_host) HIP_TRY(hipStreamSynchronize(st));  // staging buffer is reused by the next part
     }
     s->ext_pending = true;
@@ -1112,7 +1133,7 @@ int32_t mg_render_cameras(mg_sim* s, const mg_camera* cams, int32_t n, void* str
     A.light[0] = lx * inv; A.light[1] = ly * inv; A.light[2] = lz * inv;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(st, &cap));
-    const bool timed = cap == hipStreamCaptureStatusNone;
+    const bool timed = s->timing && cap == hipStreamCaptureStatusNone;
     MgKernelTimer timer{};
     if (timed) {
         if (!s->rev_b) HIP_TRY(hipEventCreate(&s->rev_b));
@@ -1125,7 +1146,7 @@ int32_t mg_render_cameras(mg_sim* s, const mg_camera* cams, int32_t n, void* str
     const hipError_t e = mg_launch_render(A, s->cam_blocks, st);
     mg_timer = nullptr;
     HIP_TRY(e);
-    if (timed) s->rendered = true;
+    s->rendered = timed;
     return MG_OK;
 }
 

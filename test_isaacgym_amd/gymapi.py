@@ -503,12 +503,25 @@ class Gym:
             a.dof_state[:, 1] = st["vel"][:a.num_dofs]
         sim = env.sim
         if sim.finalized and sim.native and a.num_dofs:
+            # start from the actor's current device state, so the column that
+            # `flags` does not select keeps its simulated value (Isaac Gym leaves it
+            # untouched: examples/joint_monkey.py:251 sets STATE_POS every frame)
+            _, ds = self._host_state(sim)
+            cur = ds[a.global_dof:a.global_dof + a.num_dofs].copy()
+            if flags & _T.STATE_POS:
+                cur[:, 0] = a.dof_state[:, 0]
+            if flags & _T.STATE_VEL:
+                cur[:, 1] = a.dof_state[:, 1]
+            a.dof_state[:] = cur
             full = np.zeros((sim.num_dofs, 2), dtype=np.float32)
-            full[a.global_dof:a.global_dof + a.num_dofs] = a.dof_state
+            full[a.global_dof:a.global_dof + a.num_dofs] = cur
             idx = np.array([a.global_index], dtype=np.int32)
             sim.epoch += 1
             N.check(N.lib.mg_set_dof_state(sim.native, full.ctypes.data, 1, idx.ctypes.data, 1, sim.stream()),
                     "mg_set_dof_state")
+        elif sim.finalized and a.num_dofs:
+            # no device (scene-building host): the packed initial state is the state
+            sim.model_arrays["dof_state0"][a.global_dof:a.global_dof + a.num_dofs] = a.dof_state
         return True
 
     def get_dof_position(self, env, dof_handle):
@@ -736,19 +749,33 @@ class Gym:
             return False
         if nrows == 0:
             return True
-        h = sim.require_native(what)
         host = 1 if t.device.type == "cpu" else 0
         if index is not None:
             it = _as_tensor_arg(index, what + " indices")
             if it.dtype != torch.int32:
                 print("*** migym: %s: indices must be int32" % what, file=sys.stderr)
                 return False
+            it = it.reshape(-1)
+            n = int(count) if count is not None else it.numel()
+            if n < 0 or n > it.numel():
+                print("*** migym: %s: count %d outside [0, %d] (index tensor size)" % (what, n, it.numel()),
+                      file=sys.stderr)
+                return False
+            na = sim_num(sim, "actors")
+            # index range check on the host (skipped while a graph is being captured:
+            # the copy kernels skip out-of-range rows on the device as well)
+            if n > 0 and not (it.is_cuda and torch.cuda.is_current_stream_capturing()):
+                lo, hi = int(it[:n].min()), int(it[:n].max())
+                if lo < 0 or hi >= na:
+                    print("*** migym: %s: actor index %d outside [0, %d)" % (what, lo if lo < 0 else hi, na),
+                          file=sys.stderr)
+                    return False
             if (it.device.type == "cpu") != (t.device.type == "cpu"):
                 it = it.to(t.device)
-            n = int(count) if count is not None else it.numel()
-            rc = fn(h, t.data_ptr(), host, it.data_ptr(), n, sim.stream())
+            it = it.contiguous()
+            rc = fn(sim.require_native(what), t.data_ptr(), host, it.data_ptr(), n, sim.stream())
         else:
-            rc = fn(h, t.data_ptr(), host, None, 0, sim.stream())
+            rc = fn(sim.require_native(what), t.data_ptr(), host, None, 0, sim.stream())
         if rc != N.MG_OK:
             print("*** migym: %s: %s" % (what, N.last_error()), file=sys.stderr)
             return False
@@ -811,7 +838,19 @@ class Gym:
         h = sim.require_native("apply_rigid_body_force_tensors")
         tensors = [_as_tensor_arg(x, "apply_rigid_body_force_tensors") if x is not None else None
                    for x in (forceTensor, torqueTensor)]
-        host = 1 if any(t is not None and t.device.type == "cpu" for t in tensors) else 0
+        given = [t for t in tensors if t is not None]
+        if not given:
+            return True
+        if len({t.device for t in given}) > 1:
+            print("*** migym: apply_rigid_body_force_tensors: force and torque tensors on different devices "
+                  "(%s)" % ", ".join(str(t.device) for t in given), file=sys.stderr)
+            return False
+        if any(t.dtype != torch.float32 or t.numel() != sim.num_bodies * 3 for t in given):
+            print("*** migym: apply_rigid_body_force_tensors: expected float32 tensors of %d x 3"
+                  % sim.num_bodies, file=sys.stderr)
+            return False
+        tensors = [t.contiguous() if t is not None else None for t in tensors]
+        host = 1 if given[0].device.type == "cpu" else 0
         ptr = [t.data_ptr() if t is not None else None for t in tensors]
         mg_space = 1 if space == _T.LOCAL_SPACE else 0
         rc = N.lib.mg_apply_rigid_body_force(h, ptr[0], ptr[1], mg_space, host, sim.stream())

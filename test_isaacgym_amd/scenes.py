@@ -86,7 +86,7 @@ def servo_scene(gym, num_envs, use_gpu_pipeline=True, device=0, uav_height=102.0
 
 
 def gimbal_scene(gym, num_envs, use_gpu_pipeline=True, device=0, stiffness=50.0, damping=5.0,
-                 asset_root=None, asset_file="servo/gimbal.urdf"):
+                 asset_root=None, asset_file="servo/gimbal.urdf", drive_mode=None):
     sp = gymapi.SimParams()
     sp.substeps = 2
     sp.dt = 1.0 / 60.0
@@ -118,7 +118,7 @@ def gimbal_scene(gym, num_envs, use_gpu_pipeline=True, device=0, stiffness=50.0,
         pose.p = gymapi.Vec3(0.0, 2.0, 3.0)
         h = gym.create_actor(env, asset, pose, "gimbal", i, 1)
         props = gym.get_actor_dof_properties(env, h)
-        props["driveMode"][:] = gymapi.DOF_MODE_POS
+        props["driveMode"][:] = gymapi.DOF_MODE_POS if drive_mode is None else drive_mode
         props["stiffness"][:] = stiffness
         props["damping"][:] = damping
         gym.set_actor_dof_properties(env, h, props)

@@ -31,6 +31,17 @@ def all_gather_rows(t, group=None):
     must hold equal n_k, the weak-scaling layout). One all_gather_into_tensor:
     a single collective per step, sized n_k x world."""
     world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo":
+        # gloo (host rehearsal, or several ranks sharing one GPU): gather host copies
+        parts = [torch.empty_like(t, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, t.detach().to("cpu").contiguous(), group=group)
+        return torch.cat(parts, 0).to(t.device)
     out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     dist.all_gather_into_tensor(out, t.contiguous(), group=group)
     return out
+
+
+def backend_for(world, device_count):
+    """RCCL ("nccl") when every rank has a GPU of its own; gloo otherwise (host
+    rehearsal, or ranks sharing one GPU, which RCCL does not allow)."""
+    return "nccl" if world > 1 and device_count >= world else "gloo"

@@ -158,3 +158,58 @@ def test_errors_are_isaac_style(gym):
         ok = torch.zeros((4, 13))
         with pytest.raises(N.MigymError):
             gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(ok))
+
+
+def test_indexed_setters_reject_bad_indices_and_counts(gym):
+    """an indexed setter never hands the C ABI a count larger than its
+    index tensor or an actor index outside [0, num_actors); Isaac Gym style, it
+    returns False. (The device copy kernels also skip out-of-range rows.)"""
+    import torch
+    sim, envs = scenes.gimbal_scene(gym, 3, use_gpu_pipeline=False)
+    gym.prepare_sim(sim)
+    root = torch.zeros((3, 13))
+    dofs = torch.zeros((9,))
+    ds = torch.zeros((9, 2))
+    for idx, count in (([0, 3], 2), ([-1], 1), ([0, 1], 3), ([0], -1)):
+        it = gymtorch.unwrap_tensor(torch.tensor(idx, dtype=torch.int32))
+        assert gym.set_actor_root_state_tensor_indexed(sim, gymtorch.unwrap_tensor(root), it, count) is False
+        assert gym.set_dof_position_target_tensor_indexed(sim, gymtorch.unwrap_tensor(dofs), it, count) is False
+        assert gym.set_dof_state_tensor_indexed(sim, gymtorch.unwrap_tensor(ds), it, count) is False
+    bad_dtype = gymtorch.unwrap_tensor(torch.tensor([0], dtype=torch.int64))
+    assert gym.set_dof_velocity_target_tensor_indexed(sim, gymtorch.unwrap_tensor(dofs), bad_dtype, 1) is False
+
+
+def test_force_tensors_on_mixed_devices_are_rejected(gym):
+    import torch
+    from conftest import has_gpu
+    sim, _ = scenes.servo_scene(gym, 2, use_gpu_pipeline=False)
+    gym.prepare_sim(sim)
+    if not has_gpu():
+        with pytest.raises(N.MigymError):
+            gym.apply_rigid_body_force_tensors(sim, gymtorch.unwrap_tensor(torch.zeros(4, 3)), None)
+        return
+    f = torch.zeros(4, 3)
+    t = torch.zeros(4, 3, device="cuda:0")
+    assert gym.apply_rigid_body_force_tensors(sim, gymtorch.unwrap_tensor(f), gymtorch.unwrap_tensor(t)) is False
+
+
+def test_set_actor_dof_states_keeps_unselected_column(gym):
+    """STATE_POS leaves velocities as they are (and STATE_VEL positions)."""
+    sim, envs = scenes.gimbal_scene(gym, 2, use_gpu_pipeline=False)
+    gym.prepare_sim(sim)
+    st = gym.get_actor_dof_states(envs[1], 0, gymapi.STATE_ALL)
+    st["pos"] = [0.1, 0.2, 0.3]
+    st["vel"] = [1.0, 2.0, 3.0]
+    assert gym.set_actor_dof_states(envs[1], 0, st, gymapi.STATE_ALL)
+    st2 = gym.get_actor_dof_states(envs[1], 0, gymapi.STATE_ALL)
+    st2["pos"] = [-0.5, -0.5, -0.5]
+    st2["vel"] = [9.0, 9.0, 9.0]
+    assert gym.set_actor_dof_states(envs[1], 0, st2, gymapi.STATE_POS)
+    got = gym.get_actor_dof_states(envs[1], 0, gymapi.STATE_ALL)
+    assert np.allclose(got["pos"], -0.5) and np.allclose(got["vel"], [1.0, 2.0, 3.0])
+    st2["pos"] = [0.7, 0.7, 0.7]
+    assert gym.set_actor_dof_states(envs[1], 0, st2, gymapi.STATE_VEL)
+    got = gym.get_actor_dof_states(envs[1], 0, gymapi.STATE_ALL)
+    assert np.allclose(got["pos"], -0.5) and np.allclose(got["vel"], 9.0)
+    # env 0 untouched
+    assert np.allclose(gym.get_actor_dof_states(envs[0], 0, gymapi.STATE_ALL)["vel"], 0.0)

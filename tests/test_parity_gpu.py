@@ -207,6 +207,43 @@ def test_gimbal_parity(gym):
     assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
 
 
+def test_gimbal_velocity_drive_parity(gym):
+    """DOF_MODE_VEL (examples/dof_controls.py:89-150: velocity targets, the
+    stiffness is ignored, damping drives the joint speed): random velocity
+    targets through set_dof_velocity_target_tensor, every other frame only the
+    odd envs' targets through the _indexed setter; 60 frames bit for bit."""
+    n, steps = 128, 60
+    sim, _ = scenes.gimbal_scene(gym, n, drive_mode=gymapi.DOF_MODE_VEL, stiffness=50.0, damping=2.0)
+    gym.prepare_sim(sim)
+    _, rb, dof, _ = _tensors(gym, sim)
+    tg = scenes.gimbal_targets(n, steps, DEV, seed=7) * 2.0
+    tg_h = tg.cpu().numpy()
+    odd = torch.arange(1, n, 2, dtype=torch.int32, device=DEV)
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    ds = sim.model_arrays["dof_state0"].copy()
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+    for k in range(steps):
+        t = tg[k].contiguous()
+        if k % 2 == 0:
+            assert gym.set_dof_velocity_target_tensor(sim, gymtorch.unwrap_tensor(t))
+            tgt[:, 1] = tg_h[k]
+        else:
+            assert gym.set_dof_velocity_target_tensor_indexed(sim, gymtorch.unwrap_tensor(t),
+                                                               gymtorch.unwrap_tensor(odd), odd.numel())
+            rows = (np.arange(1, n, 2)[:, None] * 3 + np.arange(3)[None, :]).ravel()
+            tgt[rows, 1] = tg_h[k][rows]
+        gym.simulate(sim)
+        oracle.step(p, m, st, ds, tgt=tgt)
+    gym.refresh_dof_state_tensor(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    got_d = dof.cpu().numpy()
+    got = rb.cpu().numpy()
+    assert np.all(np.isfinite(got_d)) and np.abs(got_d[:, 1]).max() > 0.1       # the drives moved the joints
+    assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+
+
 def test_tensor_api_semantics(gym):
     """acquire returns one persistent storage (test10 :372 vs :400); refresh
     publishes the step; the _indexed setter touches only the listed actors; the

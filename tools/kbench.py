@@ -18,6 +18,7 @@ def run(n, steps=200, warm=20):
     gym = gymapi.acquire_gym()
     sim, _ = scenes.servo_scene(gym, n)
     gym.prepare_sim(sim)
+    N.lib.mg_set_kernel_timing(sim.native, 1)
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     acts = scenes.servo_actions(n, 32, "cuda:0", seed=0)
     gym.refresh_actor_root_state_tensor(sim)

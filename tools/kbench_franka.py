@@ -19,6 +19,7 @@ def run(n, warm=150, steps=100):
     gym = gymapi.acquire_gym()
     sim, info = scenes.franka_scene(gym, n)
     gym.prepare_sim(sim)
+    N.lib.mg_set_kernel_timing(sim.native, 1)
     rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
     dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
     jac = gymtorch.wrap_tensor(gym.acquire_jacobian_tensor(sim, "franka"))

@@ -18,6 +18,7 @@ def run(n, steps=200, warm=20):
     gym = gymapi.acquire_gym()
     sim, _ = scenes.gimbal_scene(gym, n)
     gym.prepare_sim(sim)
+    N.lib.mg_set_kernel_timing(sim.native, 1)
     tg = scenes.gimbal_targets(n, 64, "cuda:0", seed=0)
     for k in range(warm + steps):
         gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[k % 64]))

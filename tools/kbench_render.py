@@ -22,6 +22,7 @@ def run(n, w, h, reps=10):
     sim, envs = scenes.servo_scene(gym, n)
     imgs = scenes.attach_servo_cameras(gym, sim, envs, w, h, 30.0)
     gym.prepare_sim(sim)
+    N.lib.mg_set_kernel_timing(sim.native, 1)
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     acts = scenes.servo_actions(n, 4, "cuda:0", seed=5)
     gym.refresh_actor_root_state_tensor(sim)
