@@ -209,12 +209,24 @@ typedef struct {
     v3_t r; float s0, mu, e, kn, kt1, kt2, ln, lt1, lt2, vn0; int on;
 } slot_t;
 
+/* x clamped to [-lim, lim], lim >= 0 (the device's v_med3_f32) */
+static float clamp_sym_(float x, float lim) { return fminf(fmaxf(x, -lim), lim); }
+/* Row targets (mg_rigid.hip pos_target / vel_target): position iterations
+ * v_n >= -s / sub capped at the maximum depenetration velocity (binding only
+ * while penetrating); velocity iterations v_n >= -s / h while separated, else
+ * 0, raised to the restitution bounce above the bounce threshold. */
+static float pos_target_(const step_t* P, float s) { return fminf(-s * P->inv_sub, P->maxdep); }
+static float vel_target_(const step_t* P, float s, float e, float vn0) {
+    float tgt = fminf(-s * P->inv_h, 0.0f);
+    if (e > 0.0f && vn0 < -P->bounce) tgt = fmaxf(tgt, -e * vn0);
+    return tgt;
+}
+
 static void contact_normal(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw, float tgt) {
     v3_t rn = b_cn(B, c->r);
     float vn = b_vn(B, *v, *w, c->r);
-    float dl = c->kn * (tgt - vn);
-    float nl = fmaxf(c->ln + dl, 0.0f);
-    dl = nl - c->ln;
+    float nl = fmaxf(fmaf(c->kn, tgt - vn, c->ln), 0.0f);
+    float dl = nl - c->ln;
     c->ln = nl;
     *v = b_fn(B, *v, dl, invm);
     *w = fmad3_(*w, symmul_(*Iw, rn), dl);
@@ -226,18 +238,38 @@ static void contact_friction(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, floa
     const float lim = c->mu * c->ln;
     v3_t r1 = b_c1(B, c->r), r2;
     float vt1 = b_v1(B, *v, *w, c->r), vt2, n1, n2, d1, d2;
-    n1 = fminf(fmaxf(c->lt1 - c->kt1 * vt1, -lim), lim);
+    n1 = clamp_sym_(fmaf(-c->kt1, vt1, c->lt1), lim);
     d1 = n1 - c->lt1;
     c->lt1 = n1;
     *v = b_f1(B, *v, d1, invm);
     *w = fmad3_(*w, symmul_(*Iw, r1), d1);
     r2 = b_c2(B, c->r);
     vt2 = b_v2(B, *v, *w, c->r);
-    n2 = fminf(fmaxf(c->lt2 - c->kt2 * vt2, -lim), lim);
+    n2 = clamp_sym_(fmaf(-c->kt2, vt2, c->lt2), lim);
     d2 = n2 - c->lt2;
     c->lt2 = n2;
     *v = b_f2(B, *v, d2, invm);
     *w = fmad3_(*w, symmul_(*Iw, r2), d2);
+}
+
+/* Identity skips (mg_rigid.hip shape_pose_identity / inertia_frame / com_world
+ * / origin_from_com): the composition with an identity pose or a zero offset
+ * is skipped, as on the device. */
+static int shape_pose_identity_(const float* sh) {
+    return sh[4] == 0.0f && sh[5] == 0.0f && sh[6] == 0.0f && sh[7] == 0.0f && sh[8] == 0.0f && sh[9] == 0.0f &&
+           sh[10] == 1.0f;
+}
+static q4_t inertia_frame_(q4_t q, q4_t iq) {
+    if (iq.x == 0.0f && iq.y == 0.0f && iq.z == 0.0f && iq.w == 1.0f) return q;
+    return qmul_(q, iq);
+}
+static v3_t com_world_(v3_t x, q4_t q, v3_t com) {
+    if (com.x == 0.0f && com.y == 0.0f && com.z == 0.0f) return x;
+    return add3(x, qrot_(q, com));
+}
+static v3_t origin_from_com_(v3_t xc, q4_t q, v3_t com) {
+    if (com.x == 0.0f && com.y == 0.0f && com.z == 0.0f) return xc;
+    return sub3(xc, qrot_(q, com));
 }
 
 /* Contact candidates of one shape: (static index k, point, separation). */
@@ -245,9 +277,13 @@ typedef struct { int k; v3_t p; float sep; } cand_t;
 static int shape_candidates(const step_t* P, const basis_t* B, const float* sh, q4_t q, v3_t x, cand_t* out,
                             float* mu, float* e, const float* hulls) {
     const int type = (int)sh[0];
-    const q4_t qs = qmul_(q, Q(sh[7], sh[8], sh[9], sh[10]));
-    const v3_t cs = add3(x, qrot_(q, V(sh[4], sh[5], sh[6])));
+    q4_t qs = q;
+    v3_t cs = x;
     int k, n = 0;
+    if (!shape_pose_identity_(sh)) {
+        qs = qmul_(q, Q(sh[7], sh[8], sh[9], sh[10]));
+        cs = add3(x, qrot_(q, V(sh[4], sh[5], sh[6])));
+    }
     *mu = 0.5f * (sh[11] + P->mu_g);
     *e = 0.5f * (sh[12] + P->e_g);
     if (type == MG_SHAPE_BOX) {
@@ -334,8 +370,8 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
     if (ext) { fext = V(ext[0], ext[1], ext[2]); text = V(ext[3], ext[4], ext[5]); }
     q = qnorm_(q);
     for (st_ = 0; st_ < P->substeps; ++st_) {
-        const s3_t Iw = sym_rdrt_(qmat_(qmul_(q, iq)), invI);
-        const v3_t xc = add3(x, qrot_(q, com));
+        const s3_t Iw = sym_rdrt_(qmat_(inertia_frame_(q, iq)), invI);
+        const v3_t xc = com_world_(x, q, com);
         slot_t sl[OR_MAXC];
         int j, it;
         v3_t dx = V(0.0f, 0.0f, 0.0f), dth = V(0.0f, 0.0f, 0.0f);
@@ -372,8 +408,37 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                 }
             }
         }
+        if (nsh <= 1) {
+            /* single-shape bodies (k_rigid_step1): once any of the 4 static slots
+             * is in contact, all 4 are solved, an inactive one with r = 0, s0 = 0
+             * and zero effective masses (so its rows apply zero impulse) */
+            int any = 0;
+            for (j = 0; j < 4; ++j) any = any || sl[j].on;
+            if (any) {
+                float mu = 0.0f, e = 0.0f;
+                if (nsh == 1) {
+                    const float* sh = m->shapes + (size_t)sh0 * MG_SHAPE_STRIDE;
+                    mu = 0.5f * (sh[11] + P->mu_g);
+                    e = 0.5f * (sh[12] + P->e_g);
+                }
+                for (j = 0; j < 4; ++j) {
+                    const int act = sl[j].on;
+                    if (!act) { sl[j].r = V(0.0f, 0.0f, 0.0f); sl[j].s0 = 0.0f; }
+                    sl[j].mu = mu; sl[j].e = e;
+                    {
+                        const v3_t rn = b_cn(&B, sl[j].r), r1 = b_c1(&B, sl[j].r), r2 = b_c2(&B, sl[j].r);
+                        sl[j].kn = act ? 1.0f / (invm + dot3(rn, symmul_(Iw, rn))) : 0.0f;
+                        sl[j].kt1 = act ? 1.0f / (invm + dot3(r1, symmul_(Iw, r1))) : 0.0f;
+                        sl[j].kt2 = act ? 1.0f / (invm + dot3(r2, symmul_(Iw, r2))) : 0.0f;
+                    }
+                    sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
+                    sl[j].vn0 = b_vn(&B, v, w, sl[j].r);
+                    sl[j].on = 1;
+                }
+            }
+        }
         for (j = 0; j < OR_MAXC; ++j) {
-            if (!sl[j].on) continue;
+            if (!sl[j].on || nsh <= 1) continue;
             {
                 const v3_t rn = b_cn(&B, sl[j].r), r1 = b_c1(&B, sl[j].r), r2 = b_c2(&B, sl[j].r);
                 sl[j].kn = 1.0f / (invm + dot3(rn, symmul_(Iw, rn)));
@@ -385,12 +450,8 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
         }
         for (it = 0; it < P->npos; ++it) {
             for (j = 0; j < OR_MAXC; ++j) {
-                float s, tgt;
                 if (!sl[j].on) continue;
-                s = b_ps(&B, sl[j].s0, dx, dth, sl[j].r);
-                tgt = -s * P->inv_sub;
-                if (s < 0.0f) tgt = fminf(tgt, P->maxdep);
-                contact_normal(&B, &sl[j], &v, &w, invm, &Iw, tgt);
+                contact_normal(&B, &sl[j], &v, &w, invm, &Iw, pos_target_(P, b_ps(&B, sl[j].s0, dx, dth, sl[j].r)));
             }
             for (j = 0; j < OR_MAXC; ++j)
                 if (sl[j].on) contact_friction(&B, &sl[j], &v, &w, invm, &Iw);
@@ -399,12 +460,9 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
         }
         for (it = 0; it < P->nvel; ++it) {
             for (j = 0; j < OR_MAXC; ++j) {
-                float s, tgt;
                 if (!sl[j].on) continue;
-                s = b_ps(&B, sl[j].s0, dx, dth, sl[j].r);
-                tgt = s > 0.0f ? -s * P->inv_h : 0.0f;
-                if (sl[j].e > 0.0f && sl[j].vn0 < -P->bounce) tgt = fmaxf(tgt, -sl[j].e * sl[j].vn0);
-                contact_normal(&B, &sl[j], &v, &w, invm, &Iw, tgt);
+                contact_normal(&B, &sl[j], &v, &w, invm, &Iw,
+                               vel_target_(P, b_ps(&B, sl[j].s0, dx, dth, sl[j].r), sl[j].e, sl[j].vn0));
             }
             for (j = 0; j < OR_MAXC; ++j)
                 if (sl[j].on) contact_friction(&B, &sl[j], &v, &w, invm, &Iw);
@@ -418,7 +476,7 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
         {
             const v3_t xc1 = add3(xc, dx);
             q = qint_(q, dth);
-            x = sub3(xc1, qrot_(q, com));
+            x = origin_from_com_(xc1, q, com);
         }
     }
     st[0] = x.x; st[1] = x.y; st[2] = x.z;

@@ -32,6 +32,12 @@ struct MgStep {
     float mu_ground, e_ground;
 };
 
+// Compact per-template record of the single-shape free-body kernel (built at
+// upload): the MG_TBODY_F_N template floats, then the template's first shape
+// record (type -1 when it has none). Staged in LDS when the table fits.
+#define MG_TREC_N        (MG_TBODY_F_N + MG_SHAPE_STRIDE)
+#define MG_TREC_LDS_MAX  (48 * 1024)
+
 // Kernel argument block of the free-body step (SoA arrays, stride = nb).
 struct MgRigidArgs {
     int          nf;          // number of free bodies
@@ -47,6 +53,8 @@ struct MgRigidArgs {
     const float* hulls;       // convex hull records (MG_SHAPE_CONVEX)
     const float* ext;         // [6][nb] world force/torque at COM, or null
     float*       cforce;      // [3][nb] net contact force out
+    const float* trec;        // [ntb][MG_TREC_N] compact template records
+    int          ntb;         // template bodies
 };
 
 // Articulation step arguments (lane = articulation instance).

@@ -13,19 +13,27 @@
 //   4. pose update: com += sum of iteration deltas, q = exp(dtheta) q.
 // Envs are independent and (test10_servo_vecenv.py:317,323: group=i, filter=-1)
 // the two actors of an env do not collide, so lanes never communicate: no
-// atomics, no LDS, no grid sync. State is SoA [field][body] so every load and
-// store of a wavefront is one coalesced 256-B transaction per field.
+// atomics, no grid sync. State is SoA [field][body] so every load and store of
+// a wavefront is one coalesced 256-B transaction per field.
 //
-// Issue-bound design notes (one wave per SIMD at 4096 envs, so the frame time
-// is the instruction stream of one wave):
-//   - a box contributes the 4 corners of its face most opposed to the ground
-//     normal; single-shape bodies (one launch) keep 4 static slots with the
-//     world-inertia products cached per slot, multi-shape bodies (a second
-//     launch) use 8 shift-register slots (static indices only);
+// At the headline size (4096 envs = 128 waves on 1024 SIMDs) the frame time is
+// one wave's instruction stream plus its memory round trips
+// (tools/kbench_rigid_phases.py: 7.2 us with no contacts, +5.9 us for 10 of the
+// 14 solver iterations), so the single-shape kernel k_rigid_step1 is built for
+// latency:
+//   - template constants (damping, speed limits, gravity flag and the shape
+//     record) are one compact MG_TREC_N-float record per template body, staged
+//     in LDS by the workgroup while the lanes' state loads are in flight: one
+//     HBM round trip instead of body -> template -> shape -> ...;
+//   - the 4 static contact slots are processed without branches: an inactive
+//     slot has zero effective masses and a zero lever arm, so its rows apply
+//     exactly zero impulse; only a wave with no contact at all skips the
+//     solver loops (wave-uniform);
+//   - the row updates fuse the impulse accumulation (fmaf) and clamp the
+//     friction impulse with one v_med3_f32;
 //   - the +Z ground (make_step's basis n = z, t1 = y, t2 = -x) is a template
-//     specialisation with the cross / dot products written out;
-//   - free bodies are ordered by template on upload, so bodies that are in the
-//     air (no contacts) and bodies on the ground fill different waves.
+//     specialisation with the cross / dot products written out.
+// Multi-shape bodies run k_rigid_step (8 shift-register slots, a second launch).
 // The C restatement is oracle/migym_oracle.c:rigid_body_step (same slot order,
 // same specialisation, same evaluation order).
 #include "mg_internal.h"
@@ -88,6 +96,9 @@ struct BasisZ {
     __device__ __forceinline__ V3 f2(V3 v, float dl, float invm) const { return v3(fmaf(-dl, invm, v.x), v.y, v.z); }
 };
 
+// clamp x to [-lim, lim] (lim >= 0): the median of three, one instruction
+__device__ __forceinline__ float clamp_sym(float x, float lim) { return __builtin_amdgcn_fmed3f(x, -lim, lim); }
+
 struct Slot {
     V3 r;        // contact point - centre of mass (world)
     float s0;    // separation minus rest offset at substep start
@@ -109,9 +120,8 @@ __device__ __forceinline__ void contact_normal(const B& G, Slot& c, V3& v, V3& w
                                                float tgt) {
     if (!CACHE) MG_OPAQUE3(c.r);
     const float vn = G.vn(v, w, c.r);
-    float dl = c.kn * (tgt - vn);
-    const float nl = fmaxf(c.ln + dl, 0.0f);
-    dl = nl - c.ln;
+    const float nl = fmaxf(fmaf(c.kn, tgt - vn, c.ln), 0.0f);
+    const float dl = nl - c.ln;
     c.ln = nl;
     v = G.fn(v, dl, invm);
     w = fmad3(w, CACHE ? c.In : symmul(Iw, G.cn(c.r)), dl);
@@ -125,17 +135,52 @@ __device__ __forceinline__ void contact_friction(const B& G, Slot& c, V3& v, V3&
     if (!CACHE) MG_OPAQUE3(c.r);
     const float lim = c.mu * c.ln;
     const float vt1 = G.v1(v, w, c.r);
-    const float n1 = fminf(fmaxf(c.lt1 - c.kt1 * vt1, -lim), lim);
+    const float n1 = clamp_sym(fmaf(-c.kt1, vt1, c.lt1), lim);
     const float d1 = n1 - c.lt1;
     c.lt1 = n1;
     v = G.f1(v, d1, invm);
     w = fmad3(w, CACHE ? c.I1 : symmul(Iw, G.c1(c.r)), d1);
     const float vt2 = G.v2(v, w, c.r);
-    const float n2 = fminf(fmaxf(c.lt2 - c.kt2 * vt2, -lim), lim);
+    const float n2 = clamp_sym(fmaf(-c.kt2, vt2, c.lt2), lim);
     const float d2 = n2 - c.lt2;
     c.lt2 = n2;
     v = G.f2(v, d2, invm);
     w = fmad3(w, CACHE ? c.I2 : symmul(Iw, G.c2(c.r)), d2);
+}
+
+// Row targets. Position iterations: v_n >= -s / sub, capped at the maximum
+// depenetration velocity (the cap only binds while penetrating: for s >= 0 the
+// target is <= 0 <= max_depen). Velocity iterations: v_n >= -s / h while
+// separated, else 0, raised to the restitution bounce -e v_n0 above the
+// bounce threshold.
+__device__ __forceinline__ float pos_target(const MgStep& P, float s) { return fminf(-s * P.inv_sub, P.max_depen); }
+__device__ __forceinline__ float vel_target(const MgStep& P, float s, float e, float vn0) {
+    float tgt = fminf(-s * P.inv_h, 0.0f);
+    if (e > 0.0f && vn0 < -P.bounce_thresh) tgt = fmaxf(tgt, -e * vn0);
+    return tgt;
+}
+
+// Identity skips shared by both kernels and the oracle (the skipped
+// composition with an identity pose / a zero offset returns its input up to
+// the sign of zero terms).
+__device__ __forceinline__ bool shape_pose_identity(const float* sh) {
+    return sh[4] == 0.0f && sh[5] == 0.0f && sh[6] == 0.0f && sh[7] == 0.0f && sh[8] == 0.0f && sh[9] == 0.0f &&
+           sh[10] == 1.0f;
+}
+// orientation of the principal inertia frame: q iq
+__device__ __forceinline__ Q4 inertia_frame(Q4 q, Q4 iq) {
+    if (iq.x == 0.0f && iq.y == 0.0f && iq.z == 0.0f && iq.w == 1.0f) return q;
+    return qmul(q, iq);
+}
+// centre of mass in the world: x + q com
+__device__ __forceinline__ V3 com_world(V3 x, Q4 q, V3 com) {
+    if (com.x == 0.0f && com.y == 0.0f && com.z == 0.0f) return x;
+    return vadd(x, qrot(q, com));
+}
+// body origin from the centre of mass: xc - q com
+__device__ __forceinline__ V3 origin_from_com(V3 xc, Q4 q, V3 com) {
+    if (com.x == 0.0f && com.y == 0.0f && com.z == 0.0f) return xc;
+    return vsub(xc, qrot(q, com));
 }
 
 // Candidates of one shape: emit(k, point, separation, mu, e) with k the static
@@ -145,8 +190,14 @@ template <class B, class F>
 __device__ __forceinline__ void shape_candidates(const B& G, const MgStep& P, const float* sh, Q4 q, V3 x,
                                                  const float* hulls, F&& emit) {
     const int type = (int)sh[0];
-    const Q4 qs = qmul(q, q4(sh[7], sh[8], sh[9], sh[10]));
-    const V3 cs = vadd(x, qrot(q, v3(sh[4], sh[5], sh[6])));
+    // shape pose in the world: a shape at the body origin with the body's
+    // orientation (the usual URDF box / sphere) skips the composition
+    Q4 qs = q;
+    V3 cs = x;
+    if (!shape_pose_identity(sh)) {
+        qs = qmul(q, q4(sh[7], sh[8], sh[9], sh[10]));
+        cs = vadd(x, qrot(q, v3(sh[4], sh[5], sh[6])));
+    }
     const float mu = 0.5f * (sh[11] + P.mu_ground);
     const float e = 0.5f * (sh[12] + P.e_ground);
     if (type == MG_SHAPE_BOX) {
@@ -263,8 +314,8 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
     V3 fsum = v3(0.0f, 0.0f, 0.0f);
 
     for (int st = 0; st < P.substeps; ++st) {
-        const S3 Iw = sym_rdrt(qmat(qmul(q, iq)), invI);
-        const V3 xc = vadd(x, qrot(q, com));
+        const S3 Iw = sym_rdrt(qmat(inertia_frame(q, iq)), invI);
+        const V3 xc = com_world(x, q, com);
 
         // 1. unconstrained velocity
         if (grav_on != 0.0f) v = vmad(v, v3(P.g[0], P.g[1], P.g[2]), h);
@@ -342,9 +393,7 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
             for (int j = 0; j < MAXC; ++j) {
                 if (sl[j].on) {
                     const float s = G.ps(sl[j].s0, dx, dth, sl[j].r);
-                    float tgt = -s * P.inv_sub;
-                    if (s < 0.0f) tgt = fminf(tgt, P.max_depen);
-                    contact_normal<CACHE>(G, sl[j], v, w, invm, Iw, tgt);
+                    contact_normal<CACHE>(G, sl[j], v, w, invm, Iw, pos_target(P, s));
                 }
             }
 #pragma unroll
@@ -359,9 +408,7 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
             for (int j = 0; j < MAXC; ++j) {
                 if (sl[j].on) {
                     const float s = G.ps(sl[j].s0, dx, dth, sl[j].r);
-                    float tgt = s > 0.0f ? -s * P.inv_h : 0.0f;
-                    if (sl[j].e > 0.0f && sl[j].vn0 < -P.bounce_thresh) tgt = fmaxf(tgt, -sl[j].e * sl[j].vn0);
-                    contact_normal<CACHE>(G, sl[j], v, w, invm, Iw, tgt);
+                    contact_normal<CACHE>(G, sl[j], v, w, invm, Iw, vel_target(P, s, sl[j].e, sl[j].vn0));
                 }
             }
 #pragma unroll
@@ -380,9 +427,214 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
         // 4. pose update (centre of mass moves by the integrated delta)
         const V3 xc1 = vadd(xc, dx);
         q = qintegrate(q, dth);
-        x = vsub(xc1, qrot(q, com));
+        x = origin_from_com(xc1, q, com);
     }
 
+    S[0 * nb + b] = x.x; S[1 * nb + b] = x.y; S[2 * nb + b] = x.z;
+    S[3 * nb + b] = q.x; S[4 * nb + b] = q.y; S[5 * nb + b] = q.z; S[6 * nb + b] = q.w;
+    S[7 * nb + b] = v.x; S[8 * nb + b] = v.y; S[9 * nb + b] = v.z;
+    S[10 * nb + b] = w.x; S[11 * nb + b] = w.y; S[12 * nb + b] = w.z;
+    A.cforce[0 * nb + b] = fsum.x * P.inv_dt;
+    A.cforce[1 * nb + b] = fsum.y * P.inv_dt;
+    A.cforce[2 * nb + b] = fsum.z * P.inv_dt;
+}
+
+// ---- single-shape bodies: k_rigid_step1 ------------------------------------
+// Slot of the branch-free solver: an inactive slot holds r = 0, s0 = 0 and zero
+// effective masses (kn = kt1 = kt2 = 0), so every row of it computes
+// ln = max(0 + 0 (tgt - vn), 0) = 0 and applies a zero impulse; its friction
+// limit mu ln is 0. Friction and restitution are per body (one shape).
+struct Slot1 {
+    V3 r;
+    float s0, kn, kt1, kt2, ln, lt1, lt2, vn0;
+    V3 In, I1, I2;       // Iw (r x n), Iw (r x t1), Iw (r x t2)
+};
+
+template <class B>
+__device__ __forceinline__ void row_normal1(const B& G, Slot1& c, V3& v, V3& w, float invm, float tgt) {
+    const float vn = G.vn(v, w, c.r);
+    const float nl = fmaxf(fmaf(c.kn, tgt - vn, c.ln), 0.0f);
+    const float dl = nl - c.ln;
+    c.ln = nl;
+    v = G.fn(v, dl, invm);
+    w = fmad3(w, c.In, dl);
+}
+
+template <class B>
+__device__ __forceinline__ void row_friction1(const B& G, Slot1& c, V3& v, V3& w, float invm, float mu) {
+    const float lim = mu * c.ln;
+    const float n1 = clamp_sym(fmaf(-c.kt1, G.v1(v, w, c.r), c.lt1), lim);
+    const float d1 = n1 - c.lt1;
+    c.lt1 = n1;
+    v = G.f1(v, d1, invm);
+    w = fmad3(w, c.I1, d1);
+    const float n2 = clamp_sym(fmaf(-c.kt2, G.v2(v, w, c.r), c.lt2), lim);
+    const float d2 = n2 - c.lt2;
+    c.lt2 = n2;
+    v = G.f2(v, d2, invm);
+    w = fmad3(w, c.I2, d2);
+}
+
+// T: this body's compact template record (MG_TREC_N floats: MG_TBODY_F_N
+// template floats, then the shape record; shape type < 0 when it has none).
+template <class B>
+__device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const float* T, V3& x, Q4& q, V3& v,
+                                            V3& w, V3& fsum, float invm, V3 invI, Q4 iq, V3 com, V3 fext,
+                                            V3 text, const float* hulls) {
+    const float lin_damp = T[0], ang_damp = T[1], max_lv = T[2], max_av = T[3], grav_on = T[4];
+    const float* sh = T + MG_TBODY_F_N;
+    const bool has_shape = P.has_ground && sh[0] >= 0.0f;
+    const float h = P.h;
+    const float lin_keep = 1.0f - fminf(lin_damp * h, 1.0f);
+    const float ang_keep = 1.0f - fminf(ang_damp * h, 1.0f);
+    const float max_lv2 = max_lv * max_lv;
+    const float max_av2 = max_av * max_av;
+    const float mu = 0.5f * (sh[11] + P.mu_ground);
+    const float e = 0.5f * (sh[12] + P.e_ground);
+
+    q = qnormalize(q);
+    for (int st = 0; st < P.substeps; ++st) {
+        const S3 Iw = sym_rdrt(qmat(inertia_frame(q, iq)), invI);
+        const V3 xc = com_world(x, q, com);
+
+        // 1. unconstrained velocity
+        if (grav_on != 0.0f) v = vmad(v, v3(P.g[0], P.g[1], P.g[2]), h);
+        v = vmad(v, fext, invm * h);
+        w = vmad(w, symmul(Iw, text), h);
+        v = vscale(v, lin_keep);
+        w = vscale(w, ang_keep);
+        {
+            float v2 = vdot(v, v);
+            if (v2 > max_lv2) v = vscale(v, sqrtf(max_lv2 / v2));
+            float w2 = vdot(w, w);
+            if (w2 > max_av2) w = vscale(w, sqrtf(max_av2 / w2));
+        }
+
+        // 2. ground contacts: candidate k of the shape -> slot k
+        Slot1 sl[4];
+        bool on[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            on[j] = false;
+            sl[j].r = v3(0.0f, 0.0f, 0.0f);
+            sl[j].s0 = 0.0f;
+        }
+        if (has_shape)
+            shape_candidates(G, P, sh, q, x, hulls, [&](int k, V3 p, float sep, float, float) {
+                if (sep < P.contact_offset) {
+                    on[k] = true;
+                    sl[k].r = vsub(p, xc);
+                    sl[k].s0 = sep - P.rest_offset;
+                }
+            });
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) any = any || on[j];
+
+        // 3. TGS (skipped by a wave in which no body touches the ground)
+        V3 dx = v3(0.0f, 0.0f, 0.0f), dth = v3(0.0f, 0.0f, 0.0f);
+        if (__any(any)) {
+            // contact constants (inactive slots: r = 0, so In = I1 = I2 = 0, k = 0)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const V3 rn = G.cn(sl[j].r), r1 = G.c1(sl[j].r), r2 = G.c2(sl[j].r);
+                sl[j].In = symmul(Iw, rn);
+                sl[j].I1 = symmul(Iw, r1);
+                sl[j].I2 = symmul(Iw, r2);
+                sl[j].kn = on[j] ? 1.0f / (invm + vdot(rn, sl[j].In)) : 0.0f;
+                sl[j].kt1 = on[j] ? 1.0f / (invm + vdot(r1, sl[j].I1)) : 0.0f;
+                sl[j].kt2 = on[j] ? 1.0f / (invm + vdot(r2, sl[j].I2)) : 0.0f;
+                sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
+                sl[j].vn0 = G.vn(v, w, sl[j].r);
+            }
+            auto pos_iter = [&]() {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    row_normal1(G, sl[j], v, w, invm, pos_target(P, G.ps(sl[j].s0, dx, dth, sl[j].r)));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) row_friction1(G, sl[j], v, w, invm, mu);
+                dx = fmad3(dx, v, P.sub);
+                dth = fmad3(dth, w, P.sub);
+            };
+            // two iterations per trip: the accumulated impulses alternate between
+            // two register sets instead of being copied back every iteration
+            int it = 0;
+            for (; it + 1 < P.npos; it += 2) {
+                pos_iter();
+                pos_iter();
+            }
+            if (it < P.npos) pos_iter();
+            for (int it = 0; it < P.nvel; ++it) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    row_normal1(G, sl[j], v, w, invm, vel_target(P, G.ps(sl[j].s0, dx, dth, sl[j].r), e, sl[j].vn0));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) row_friction1(G, sl[j], v, w, invm, mu);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                fsum = G.addn(fsum, sl[j].ln);
+                fsum = G.add1(fsum, sl[j].lt1);
+                fsum = G.add2(fsum, sl[j].lt2);
+            }
+        } else {
+            // no solver pass: the motion delta is the substep's free flight
+            for (int it = 0; it < P.npos; ++it) {
+                dx = fmad3(dx, v, P.sub);
+                dth = fmad3(dth, w, P.sub);
+            }
+        }
+
+        // 4. pose update (centre of mass moves by the integrated delta)
+        const V3 xc1 = vadd(xc, dx);
+        q = qintegrate(q, dth);
+        x = origin_from_com(xc1, q, com);
+    }
+}
+
+template <bool UPZ, bool LDS_T>
+__global__ void __launch_bounds__(64) k_rigid_step1(MgStep P, MgRigidArgs A) {
+    extern __shared__ float s_trec[];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    const bool live = i < A.nf;
+    const int b = A.free_ids ? A.free_ids[live ? i : A.nf - 1] : (live ? i : A.nf - 1);
+    const int nb = A.nb;
+    float* S = A.state;
+    // this lane's inputs first, so they are in flight with the template staging
+    V3 x = v3(S[0 * nb + b], S[1 * nb + b], S[2 * nb + b]);
+    Q4 q = q4(S[3 * nb + b], S[4 * nb + b], S[5 * nb + b], S[6 * nb + b]);
+    V3 v = v3(S[7 * nb + b], S[8 * nb + b], S[9 * nb + b]);
+    V3 w = v3(S[10 * nb + b], S[11 * nb + b], S[12 * nb + b]);
+    const float* M = A.mass;
+    const float invm = M[0 * nb + b];
+    const V3 invI = v3(M[1 * nb + b], M[2 * nb + b], M[3 * nb + b]);
+    const Q4 iq = q4(M[4 * nb + b], M[5 * nb + b], M[6 * nb + b], M[7 * nb + b]);
+    const V3 com = v3(M[8 * nb + b], M[9 * nb + b], M[10 * nb + b]);
+    const int tb = A.body_tmpl[b];
+    V3 fext = v3(0.0f, 0.0f, 0.0f), text = v3(0.0f, 0.0f, 0.0f);
+    if (A.ext) {
+        fext = v3(A.ext[0 * nb + b], A.ext[1 * nb + b], A.ext[2 * nb + b]);
+        text = v3(A.ext[3 * nb + b], A.ext[4 * nb + b], A.ext[5 * nb + b]);
+    }
+    const float* T;
+    if constexpr (LDS_T) {
+        for (int k = threadIdx.x; k < A.ntb * MG_TREC_N; k += 64) s_trec[k] = A.trec[k];
+        __syncthreads();
+        T = s_trec + tb * MG_TREC_N;
+    } else {
+        T = A.trec + tb * MG_TREC_N;
+    }
+    V3 fsum = v3(0.0f, 0.0f, 0.0f);
+    if constexpr (UPZ) {
+        rigid_body1(BasisZ{}, P, T, x, q, v, w, fsum, invm, invI, iq, com, fext, text, A.hulls);
+    } else {
+        BasisGen G;
+        G.n = v3(P.n[0], P.n[1], P.n[2]);
+        G.t1 = v3(P.t1[0], P.t1[1], P.t1[2]);
+        G.t2 = v3(P.t2[0], P.t2[1], P.t2[2]);
+        rigid_body1(G, P, T, x, q, v, w, fsum, invm, invI, iq, com, fext, text, A.hulls);
+    }
+    if (!live) return;
     S[0 * nb + b] = x.x; S[1 * nb + b] = x.y; S[2 * nb + b] = x.z;
     S[3 * nb + b] = q.x; S[4 * nb + b] = q.y; S[5 * nb + b] = q.z; S[6 * nb + b] = q.w;
     S[7 * nb + b] = v.x; S[8 * nb + b] = v.y; S[9 * nb + b] = v.z;
@@ -434,8 +686,14 @@ hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream
     }
     if (A1.nf > 0) {
         const int blocks = (A1.nf + 63) / 64;
-        if (upz) MG_LAUNCH((k_rigid_step<true, 4, false>), dim3(blocks), dim3(64), 0, s, P, A1);
-        else MG_LAUNCH((k_rigid_step<false, 4, false>), dim3(blocks), dim3(64), 0, s, P, A1);
+        const size_t lds = (size_t)A.ntb * MG_TREC_N * sizeof(float);
+        if (lds <= MG_TREC_LDS_MAX) {
+            if (upz) MG_LAUNCH((k_rigid_step1<true, true>), dim3(blocks), dim3(64), lds, s, P, A1);
+            else MG_LAUNCH((k_rigid_step1<false, true>), dim3(blocks), dim3(64), lds, s, P, A1);
+        } else {
+            if (upz) MG_LAUNCH((k_rigid_step1<true, false>), dim3(blocks), dim3(64), 0, s, P, A1);
+            else MG_LAUNCH((k_rigid_step1<false, false>), dim3(blocks), dim3(64), 0, s, P, A1);
+        }
     }
     if (A2.nf > 0) {
         const int blocks = (A2.nf + 63) / 64;

@@ -89,6 +89,7 @@ struct mg_sim {
     int* d_free_global = nullptr; // [nf] global ids of the free bodies (internal 0..nf-1)
     int* d_perm = nullptr;        // [nb] global body -> internal slot
     float* d_tbf = nullptr;
+    float* d_trec = nullptr;      // [ntb][MG_TREC_N] compact template records (k_rigid_step1)
     int* d_tbi = nullptr;
     float* d_shapes = nullptr;
     float* d_hulls = nullptr;     // convex hull records (MG_SHAPE_CONVEX)
@@ -258,7 +259,7 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
 }
 
 void free_all(mg_sim* s) {
-    void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_tbi, s->d_shapes, s->d_hulls,
+    void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls,
                     s->d_actor_root, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
                     s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
                     s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
@@ -646,6 +647,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(dalloc(&s->d_perm, nb));
     HIP_TRY(dalloc(&s->d_tbf, (size_t)s->ntb * MG_TBODY_F_N));
     HIP_TRY(dalloc(&s->d_tbi, (size_t)s->ntb * MG_TBODY_I_N));
+    HIP_TRY(dalloc(&s->d_trec, (size_t)s->ntb * MG_TREC_N));
     HIP_TRY(dalloc(&s->d_shapes, (size_t)s->ns * MG_SHAPE_STRIDE));
     HIP_TRY(dalloc(&s->d_hulls, (size_t)(m->hulls ? m->num_hull_floats : 0)));
     HIP_TRY(dalloc(&s->d_actor_root, na));
@@ -675,6 +677,21 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(h2d(s->d_perm, perm.data(), (size_t)nb * sizeof(int)));
     HIP_TRY(h2d(s->d_tbf, m->tmpl_body_f, (size_t)s->ntb * MG_TBODY_F_N * sizeof(float)));
     HIP_TRY(h2d(s->d_tbi, m->tmpl_body_i, (size_t)s->ntb * MG_TBODY_I_N * sizeof(int)));
+    {
+        // compact template records of the single-shape kernel: template floats,
+        // then the first shape record (type -1: no shape)
+        std::vector<float> trec((size_t)s->ntb * MG_TREC_N, 0.0f);
+        for (int t = 0; t < s->ntb; ++t) {
+            float* r = &trec[(size_t)t * MG_TREC_N];
+            std::memcpy(r, m->tmpl_body_f + (size_t)t * MG_TBODY_F_N, MG_TBODY_F_N * sizeof(float));
+            const int s0 = m->tmpl_body_i[t * MG_TBODY_I_N + 0], sc = m->tmpl_body_i[t * MG_TBODY_I_N + 1];
+            if (sc > 0)
+                std::memcpy(r + MG_TBODY_F_N, m->shapes + (size_t)s0 * MG_SHAPE_STRIDE, MG_SHAPE_STRIDE * sizeof(float));
+            else
+                r[MG_TBODY_F_N] = -1.0f;
+        }
+        HIP_TRY(h2d(s->d_trec, trec.data(), trec.size() * sizeof(float)));
+    }
     HIP_TRY(h2d(s->d_shapes, m->shapes, (size_t)s->ns * MG_SHAPE_STRIDE * sizeof(float)));
     if (m->hulls) HIP_TRY(h2d(s->d_hulls, m->hulls, (size_t)m->num_hull_floats * sizeof(float)));
     HIP_TRY(h2d(s->d_actor_root, root_int.data(), (size_t)na * sizeof(int)));
@@ -771,6 +788,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.nf = s->nf_rigid; A.nf1 = s->nf1; A.nb = s->nb; A.free_ids = nullptr;   // internal slots 0..nf-1
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
         A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes; A.hulls = s->d_hulls;
+        A.trec = s->d_trec; A.ntb = s->ntb;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
         A.cforce = s->d_cforce;
         HIP_TRY(mg_launch_rigid_step(P, A, st));
