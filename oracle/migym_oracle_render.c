@@ -159,7 +159,7 @@ int oracle_render(const mg_sim_params* p, const float* state, const int32_t* bod
                   const int32_t* seg, const mg_camera* cam, uint8_t* rgba_out, float* depth_out, int32_t* seg_out) {
     rws_t ws[MG_RENDER_MAX_SHAPES];
     int ns = 0, b, k, row, col;
-    v3_t o, f, l, u, upv, leftv, L, gn;
+    v3_t o, f, l, u, upv, leftv, fwdv, L, gn;
     q4_t q;
     float ifx, ify, lx = 0.3f, ly = 0.2f, lz = 1.0f, inv, h0;
     int up_axis = p->up_axis == 0 ? 0 : 1;
@@ -205,14 +205,16 @@ int oracle_render(const mg_sim_params* p, const float* state, const int32_t* bod
     if (up_axis == 1) {
         upv = V(0.0f, 0.0f, 1.0f);
         leftv = V(0.0f, 1.0f, 0.0f);
+        fwdv = V(1.0f, 0.0f, 0.0f);
     } else {
         upv = V(0.0f, 1.0f, 0.0f);
-        leftv = V(0.0f, 0.0f, -1.0f);
+        leftv = V(-1.0f, 0.0f, 0.0f);
+        fwdv = V(0.0f, 0.0f, -1.0f);
         ly = 1.0f; lz = 0.2f;
     }
     inv = 1.0f / sqrtf(lx * lx + ly * ly + lz * lz);
     L = V(lx * inv, ly * inv, lz * inv);
-    f = qrot_(q, V(1.0f, 0.0f, 0.0f));
+    f = qrot_(q, fwdv);
     l = qrot_(q, leftv);
     u = qrot_(q, upv);
     ifx = 1.0f / cam->fx;

@@ -20,8 +20,10 @@ Semantics kept from Isaac Gym:
     no hit; segmentation (H, W) int32.
 Projection (pinned by examples/interop_images/, tests/test_render.py): square
 pixels, fx = fy = (W / 2) / tan(horizontal_fov / 2), principal point at the
-image centre, the camera looking along its local +x with the sim's up axis as
-image up.
+image centre. Camera axes (local): in a z-up sim the camera looks along +x with
++z as image up; in a y-up sim along -z with +y up (pinned by
+examples/graphics_images/*_cam1_*: a camera attached to a ball at offset
+(1, 0, -1) rotated 135 degrees about y sees that ball at the image centre).
 """
 import ctypes
 import math
@@ -43,8 +45,8 @@ def intrinsics(props):
 
 def look_at(pos, target, up_axis):
     """Camera transform at `pos` looking at `target` (gym.set_camera_location):
-    local +x -> the view direction, local up axis -> as close to world up as
-    the view allows (no roll)."""
+    the local view axis (+x z-up, -z y-up) -> the view direction, the local up
+    axis -> as close to world up as the view allows (no roll)."""
     f = np.array([target.x - pos.x, target.y - pos.y, target.z - pos.z], dtype=np.float64)
     f /= max(np.linalg.norm(f), 1e-12)
     up = np.array([0.0, 0.0, 1.0]) if up_axis == T.UP_AXIS_Z else np.array([0.0, 1.0, 0.0])
@@ -56,7 +58,7 @@ def look_at(pos, target, up_axis):
     if up_axis == T.UP_AXIS_Z:
         F0, L0, U0 = np.eye(3)
     else:
-        F0, L0, U0 = np.array([1.0, 0, 0]), np.array([0, 0, -1.0]), np.array([0, 1.0, 0])
+        F0, L0, U0 = np.array([0, 0, -1.0]), np.array([-1.0, 0, 0]), np.array([0, 1.0, 0])
     R = np.outer(f, F0) + np.outer(l, L0) + np.outer(u, U0)
     return T.Transform(T.Vec3(pos.x, pos.y, pos.z), _quat_from_matrix(R))
 

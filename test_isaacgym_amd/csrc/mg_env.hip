@@ -780,11 +780,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         // (b) the full pair test on the survivors, one per lane per round,
         //     contacts placed by a 16-lane prefix sum in pair order.
         int base = 0;
-#ifdef MG_ENV_ABLATE_NP
-        for (int blk = 0; blk < 0; blk += NPB) {
-#else
         for (int blk = 0; __any(blk < npair); blk += NPB) {
-#endif
             int nnear = 0;
 #pragma unroll
             for (int r = 0; r < NPB; r += G) {
@@ -977,11 +973,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 
         // ================= 4. TGS (the lambdas are kept by lane 0 in LDS; every
         // lane of the env computes the same value)
-#ifdef MG_ENV_ABLATE_TGS
-        for (int it = 0; it < 0; ++it) {
-#else
         for (int it = 0; it < P.npos + P.nvel; ++it) {
-#endif
             const bool pos = it < P.npos;
 #pragma unroll
             for (int c = 0; c < MAXCT; ++c) {

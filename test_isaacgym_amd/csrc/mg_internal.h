@@ -165,7 +165,7 @@ struct MgRenderArgs {
     const int*          env_shape_first;   // [nenv + 1]
     int                 has_ground;
     float               gn[3], gpd;        // ground: dot(gn, x) + gpd = 0
-    float               up[3], left[3];    // camera-frame up / left axes (local)
+    float               fwd[3], up[3], left[3];   // camera-frame view / up / left axes (local)
     int                 up_axis;           // 1: checker on (x, y); 0: on (x, z)
     float               light[3];          // unit direction towards the light
 };

@@ -296,7 +296,7 @@ __global__ void __launch_bounds__(256) k_render(MgRenderArgs A) {
             }
         }
         C.o = o;
-        C.f = qrot(q, v3(1.0f, 0.0f, 0.0f));
+        C.f = qrot(q, v3(A.fwd[0], A.fwd[1], A.fwd[2]));
         C.l = qrot(q, v3(A.left[0], A.left[1], A.left[2]));
         C.u = qrot(q, v3(A.up[0], A.up[1], A.up[2]));
         C.cx = K.cx; C.cy = K.cy; C.ifx = K.ifx; C.ify = K.ify;

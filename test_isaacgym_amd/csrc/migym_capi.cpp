@@ -414,9 +414,6 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                 if (k >= 0 && !m->artic_tmpl_i[m->artic_i[(size_t)k * MG_ARTIC_I_N + 2] * MG_ATMPL_I_N + 3])
                     coupled = true;
             }
-#ifdef MG_COUPLE_ARTICULATIONS
-            coupled = coupled || !art.empty();
-#endif
             if (!coupled) continue;
             if (art.size() > 1 || fr.size() > MG_ENV_MAXF || stc.size() > MG_ENV_MAXS)
                 return fail(MG_ERR_UNSUPPORTED,
@@ -1135,16 +1132,20 @@ int32_t mg_render_cameras(mg_sim* s, const mg_camera* cams, int32_t n, void* str
     A.has_ground = p.has_ground;
     for (int k = 0; k < 3; ++k) A.gn[k] = p.ground_normal[k];
     A.gpd = p.ground_distance;
-    // camera frame: forward +x, up = the sim's up axis, left = up x forward;
-    // light from above, a little off the up axis
+    // camera frame (local axes): z-up sims look along +x with +z up (test11's
+    // UAV camera, the controller's rot_coord3); y-up sims look along -z with +y
+    // up (pinned by examples/graphics_images cam1, attached to a ball);
+    // left = up x forward; light from above, a little off the up axis
     A.up_axis = p.up_axis == 0 ? 0 : 1;
     float lx = 0.3f, ly = 0.2f, lz = 1.0f;
     if (A.up_axis == 1) {
+        A.fwd[0] = 1.0f; A.fwd[1] = 0.0f; A.fwd[2] = 0.0f;
         A.up[0] = 0.0f; A.up[1] = 0.0f; A.up[2] = 1.0f;
         A.left[0] = 0.0f; A.left[1] = 1.0f; A.left[2] = 0.0f;
     } else {
+        A.fwd[0] = 0.0f; A.fwd[1] = 0.0f; A.fwd[2] = -1.0f;
         A.up[0] = 0.0f; A.up[1] = 1.0f; A.up[2] = 0.0f;
-        A.left[0] = 0.0f; A.left[1] = 0.0f; A.left[2] = -1.0f;
+        A.left[0] = -1.0f; A.left[1] = 0.0f; A.left[2] = 0.0f;
         ly = 1.0f; lz = 0.2f;
     }
     const float inv = 1.0f / sqrtf(lx * lx + ly * ly + lz * lz);

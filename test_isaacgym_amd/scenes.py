@@ -186,6 +186,76 @@ def interop_scene(gym, num_envs=16, device=0, colors=None):
     return sim, envs, cams
 
 
+def graphics_scene(gym, num_envs=8, device=0, use_gpu_pipeline=True, asset_root=None):
+    """examples/graphics.py:46-180 (y-up defaults, TGS 4/1): per env, eight
+    assets/urdf/ball.urdf balls on a 3x3 grid of pitch 4/3 m, ball 0 at y = 6,
+    the others at y = 0.25, all rotated by Quat(-0.707107, 0, 0, 0.707107),
+    group i, filter 1 (the balls of an env do not collide with each other);
+    camera 0: 360x240 at env-local (1.5, 1, 1.5) looking at the env origin;
+    camera 1: 360x240 attached to ball 0 at offset (1, 0, -1) rotated 135
+    degrees about y, FOLLOW_TRANSFORM. Returns (sim, envs, cams[env] = [c0, c1])."""
+    sp = gymapi.SimParams()
+    sp.physx.solver_type = 1
+    sp.physx.num_position_iterations = 4
+    sp.physx.num_velocity_iterations = 1
+    sp.use_gpu_pipeline = use_gpu_pipeline
+    sim = gym.create_sim(device, device, gymapi.SIM_PHYSX, sp)
+    gym.add_ground(sim, gymapi.PlaneParams())
+    ball = gym.load_asset(sim, asset_root or ASSET_ROOT, "urdf/ball.urdf", gymapi.AssetOptions())
+    if ball is None:
+        raise RuntimeError("failed to load ball.urdf")
+    spacing = 2.0
+    lower = gymapi.Vec3(-spacing, 0.0, -spacing)
+    upper = gymapi.Vec3(spacing, spacing, spacing)
+    nb = 8
+    grid = math.ceil(math.sqrt(nb))
+    d = 2 * spacing / grid
+    envs, cams = [], []
+    for i in range(num_envs):
+        env = gym.create_env(sim, lower, upper, 4)
+        envs.append(env)
+        for j in range(nb):
+            pose = gymapi.Transform()
+            pose.p = gymapi.Vec3(d * (0.5 + j % grid), 6.0 if j == 0 else 0.25, d * (0.5 + j // grid))
+            pose.r = gymapi.Quat(-0.707107, 0.0, 0.0, 0.707107)
+            gym.create_actor(env, ball, pose, "asset_%d" % j, i, 1, 0)
+        cp = gymapi.CameraProperties()
+        cp.width, cp.height = 360, 240
+        cp.enable_tensors = True
+        c0 = gym.create_camera_sensor(env, cp)
+        gym.set_camera_location(c0, env, gymapi.Vec3(1.5, 1, 1.5), gymapi.Vec3(0, 0, 0))
+        c1 = gym.create_camera_sensor(env, cp)
+        body = gym.get_actor_rigid_body_handle(env, gym.get_actor_handle(env, 0), 0)
+        rot = gymapi.Quat.from_axis_angle(gymapi.Vec3(0, 1, 0), math.radians(135.0))
+        gym.attach_camera_to_body(c1, env, body, gymapi.Transform(gymapi.Vec3(1, 0, -1), rot),
+                                  gymapi.FOLLOW_TRANSFORM)
+        cams.append([c0, c1])
+    return sim, envs, cams
+
+
+def graphics_depth_u8(depth):
+    """examples/graphics.py:225-236's depth image transform: -inf -> 0, clamp at
+    -10 m, -255 depth / min(depth + 1e-4), then numpy's float -> uint8 cast
+    (negative values wrap modulo 256 on x86, as in the reference's files)."""
+    d = np.array(depth, dtype=np.float32, copy=True)
+    d[d == -np.inf] = 0
+    d[d < -10] = -10
+    n = -255.0 * (d / np.min(d + 1e-4))
+    return (n.astype(np.int64) % 256).astype(np.uint8)
+
+
+def graphics_depth_ball_mask(u8):
+    """Ball pixels of a graphics.py camera-0 depth image: the ground's depth is
+    constant along an image row (a level camera over a flat ground), so a pixel
+    more than 12 grey levels from its row's median that is not sky (0) is an
+    object in front of the ground. A 3x3 median filter first removes the JPEG
+    ringing of the reference's files along the silhouette."""
+    from scipy.ndimage import median_filter
+    d = median_filter(u8, size=3, mode="nearest").astype(np.int32)
+    med = np.median(d, axis=1)
+    return (np.abs(d - med[:, None]) > 12) & (d > 0)
+
+
 # ------------------------------------------------------------- random actions
 def quat_from_euler_xyz(roll, pitch, yaw):
     """scipy Rotation.from_euler('xyz', [r, p, y]).as_quat() in torch (xyzw)."""

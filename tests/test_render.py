@@ -116,10 +116,13 @@ def test_camera_intrinsics_and_look_at(gym):
     fx, fy, cx, cy = _render.intrinsics(props)
     assert fx == fy == pytest.approx(800.0 / math.tan(math.radians(15.0)))
     assert (cx, cy) == (800.0, 450.0)
-    # y-up: looking down -x, image right = -z (examples/interop_images checker phase)
+    # y-up: the camera's view axis is its local -z (examples/graphics_images cam1);
+    # looking down -x, image right = -z (examples/interop_images checker phase)
     t = _render.look_at(gymapi.Vec3(5, 1, 0), gymapi.Vec3(0, 1, 0), gymapi.UP_AXIS_Y)
-    f = t.r.rotate(gymapi.Vec3(1, 0, 0))
+    f = t.r.rotate(gymapi.Vec3(0, 0, -1))
     up = t.r.rotate(gymapi.Vec3(0, 1, 0))
+    right = t.r.rotate(gymapi.Vec3(1, 0, 0))
+    assert (right.x, right.y, right.z) == pytest.approx((0, 0, -1), abs=1e-6)
     assert (f.x, f.y, f.z) == pytest.approx((-1, 0, 0), abs=1e-6)
     assert (up.x, up.y, up.z) == pytest.approx((0, 1, 0), abs=1e-6)
     # z-up: no roll, local z stays up
