@@ -62,6 +62,24 @@ def _as_tensor_arg(t, name):
     return tt
 
 
+_PHYSX_DEFAULTS = _T.PhysXParams()
+_warned_physx = set()
+
+
+def _warn_unmodelled_physx(params):
+    """PhysX patch-friction parameters the solver does not model
+    (examples/franka_cube_ik_osc.py:124-125 sets both): friction rows are one
+    anchor per contact point, so these have no effect.
+    Said once per parameter and value, on stderr — never dropped silently."""
+    px = params.physx
+    for name in ("friction_offset_threshold", "friction_correlation_distance"):
+        val = float(getattr(px, name))
+        if val != float(getattr(_PHYSX_DEFAULTS, name)) and (name, val) not in _warned_physx:
+            _warned_physx.add((name, val))
+            print("*** migym: physx.%s = %g is not modelled (friction anchors are the contact points "
+                  "themselves; DESIGN.md §3.2)" % (name, val), file=sys.stderr)
+
+
 class Gym:
     def __init__(self):
         self._sims = []
@@ -75,6 +93,7 @@ class Gym:
         if type != _T.SIM_PHYSX:
             print("*** migym: only the PhysX-style rigid solver is available (SIM_FLEX requested)", file=sys.stderr)
             return None
+        _warn_unmodelled_physx(params)
         sim = Sim(compute_device, graphics_device, type, params)
         self._sims.append(sim)
         return sim
@@ -89,6 +108,7 @@ class Gym:
         return sim.params
 
     def set_sim_params(self, sim, params):
+        _warn_unmodelled_physx(params)
         sim.params = params
         if sim.native:
             N.check(N.lib.mg_set_sim_params(sim.native, ctypes.byref(sim.mg_params())), "mg_set_sim_params")

@@ -311,3 +311,36 @@ def test_render_shapes_and_many_bodies_gpu_bitexact(gym):
     for i, env in enumerate(envs):
         _assert_same(sim, st, env, 0, imgs[i], "franka env %d" % i)
         assert np.isfinite(imgs[i][1].cpu().numpy()).mean() > 0.3
+
+
+@pytest.mark.gpu
+def test_render_config5_full_size_sampled_bitexact(gym):
+    """Config 5 at full size (test11_servo_vecenv_camerazoom.py:327-335): 1024
+    envs, one 1600x900 camera per env on the UAV (FOLLOW_TRANSFORM), 12 frames of
+    the bench's S1 step with random teleports and render_all_camera_sensors every
+    frame; 6 sampled cameras are compared bit for bit (color, depth, segmentation)
+    against the restatement, and the images must show the scene (not only sky)."""
+    n, w, h = 1024, 1600, 900
+    sim, envs = scenes.servo_scene(gym, n)
+    imgs = scenes.attach_servo_cameras(gym, sim, envs, w, h, 30.0,
+                                       image_types=(gymapi.IMAGE_COLOR, gymapi.IMAGE_DEPTH, gymapi.IMAGE_SEGMENTATION))
+    gym.prepare_sim(sim)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    acts = scenes.servo_actions(n, 12, DEV, seed=5)
+    gym.refresh_actor_root_state_tensor(sim)
+    for k in range(12):
+        root[:, 3:10] = acts[k]
+        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.simulate(sim)
+        gym.refresh_actor_root_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.render_all_camera_sensors(sim)
+    torch.cuda.synchronize()
+    st = rb.cpu().numpy()
+    lit = []
+    for e in (0, 1, 257, 511, 768, 1023):
+        _assert_same(sim, st, envs[e], 0, [t for t in imgs[e]], "config5 env %d" % e)
+        lit.append(float((imgs[e][0][..., :3].amax(-1) > 0).float().mean()))
+    assert max(lit) > 0.05, lit
+    gym.destroy_sim(sim)

@@ -3,9 +3,10 @@
 # (SQ instruction / wave-cycle counters; HBM write bytes + GPU clock) on it.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 tag=${1:-rpmc}
+files=${2:-tests/test_render.py}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_render.py -m gpu -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 300 python -u -m pytest $files -m gpu -x -q --timeout 300 --timeout-method thread \
   > gpurun_out/pytest_$tag.log 2>&1 || { tail -40 gpurun_out/pytest_$tag.log; exit 1; }
 tail -2 gpurun_out/pytest_$tag.log
 timeout -k 10 200 python tools/kbench_render.py 1024 1600x900 > gpurun_out/kb_$tag.jsonl 2>&1 || { tail gpurun_out/kb_$tag.jsonl; exit 1; }

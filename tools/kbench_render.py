@@ -17,30 +17,34 @@ from test_isaacgym_amd import _native as N  # noqa: E402
 from test_isaacgym_amd import scenes  # noqa: E402
 
 
-def run(n, w, h, reps=10):
+def run(n, w, h, warm=10, reps=20):
+    """The bench's own S5 sequence (bench.py camera_rate): actions
+    servo_actions(n, 16, seed=5), `warm` steps, then `reps` timed renders."""
     gym = gymapi.acquire_gym()
     sim, envs = scenes.servo_scene(gym, n)
     imgs = scenes.attach_servo_cameras(gym, sim, envs, w, h, 30.0)
     gym.prepare_sim(sim)
     N.lib.mg_set_kernel_timing(sim.native, 1)
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
-    acts = scenes.servo_actions(n, 4, "cuda:0", seed=5)
+    acts = scenes.servo_actions(n, 16, "cuda:0", seed=5)
     gym.refresh_actor_root_state_tensor(sim)
     ms = []
-    for k in range(reps + 2):
-        root[:, 3:10] = acts[k % 4]
+    for k in range(warm + reps):
+        root[:, 3:10] = acts[k % 16]
         gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
         gym.simulate(sim)
         gym.refresh_actor_root_state_tensor(sim)
         gym.render_all_camera_sensors(sim)
-        if k >= 2:
+        if k >= warm:
             ms.append(N.lib.mg_last_render_ms(sim.native))
     torch.cuda.synchronize()
     sky = float((imgs[0][0][..., :3].amax(-1) == 0).float().mean())
+    lit = float(np.mean([float((imgs[i][0][..., :3].amax(-1) > 0).float().mean())
+                         for i in range(0, n, max(1, n // 16))]))
     gym.destroy_sim(sim)
     avg = float(np.mean(ms))
     return {"envs": n, "w": w, "h": h, "kernel_ms": avg, "write_GBps": n * w * h * 4 / (avg * 1e-3) / 1e9,
-            "env0_sky_frac": sky}
+            "env0_sky_frac": sky, "sampled_cameras_non_sky_fraction": lit}
 
 
 if __name__ == "__main__":
