@@ -592,8 +592,12 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
     }
 }
 
+// __launch_bounds__(64, 3): at most 168 VGPRs, so three waves share a SIMD in
+// large launches (the Gauss-Seidel chains are latency-bound: more resident
+// waves, not more lanes, fill the SIMD); free of scratch at that budget. The
+// general ground basis needs more registers: two waves.
 template <bool UPZ, bool LDS_T>
-__global__ void __launch_bounds__(64) k_rigid_step1(MgStep P, MgRigidArgs A) {
+__global__ void __launch_bounds__(64, UPZ ? 3 : 2) k_rigid_step1(MgStep P, MgRigidArgs A) {
     extern __shared__ float s_trec[];
     const int i = blockIdx.x * 64 + threadIdx.x;
     const bool live = i < A.nf;
@@ -635,13 +639,18 @@ __global__ void __launch_bounds__(64) k_rigid_step1(MgStep P, MgRigidArgs A) {
         rigid_body1(G, P, T, x, q, v, w, fsum, invm, invI, iq, com, fext, text, A.hulls);
     }
     if (!live) return;
-    S[0 * nb + b] = x.x; S[1 * nb + b] = x.y; S[2 * nb + b] = x.z;
-    S[3 * nb + b] = q.x; S[4 * nb + b] = q.y; S[5 * nb + b] = q.z; S[6 * nb + b] = q.w;
-    S[7 * nb + b] = v.x; S[8 * nb + b] = v.y; S[9 * nb + b] = v.z;
-    S[10 * nb + b] = w.x; S[11 * nb + b] = w.y; S[12 * nb + b] = w.z;
-    A.cforce[0 * nb + b] = fsum.x * P.inv_dt;
-    A.cforce[1 * nb + b] = fsum.y * P.inv_dt;
-    A.cforce[2 * nb + b] = fsum.z * P.inv_dt;
+    // the output addresses are recomputed here (an opaque copy of the slot)
+    // rather than kept live in registers across the frame
+    int bo = b;
+    asm volatile("" : "+v"(bo));
+    float* So = A.state;
+    So[0 * nb + bo] = x.x; So[1 * nb + bo] = x.y; So[2 * nb + bo] = x.z;
+    So[3 * nb + bo] = q.x; So[4 * nb + bo] = q.y; So[5 * nb + bo] = q.z; So[6 * nb + bo] = q.w;
+    So[7 * nb + bo] = v.x; So[8 * nb + bo] = v.y; So[9 * nb + bo] = v.z;
+    So[10 * nb + bo] = w.x; So[11 * nb + bo] = w.y; So[12 * nb + bo] = w.z;
+    A.cforce[0 * nb + bo] = fsum.x * P.inv_dt;
+    A.cforce[1 * nb + bo] = fsum.y * P.inv_dt;
+    A.cforce[2 * nb + bo] = fsum.z * P.inv_dt;
 }
 
 template <bool UPZ, int MAXC, bool MULTI>
