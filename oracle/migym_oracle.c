@@ -488,49 +488,16 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
 
 /* ---- spatial algebra ----------------------------------- */
 typedef struct { v3_t w, v; } sv_t;
-typedef struct { m3_t A, B, C; } si_t;
 
 static sv_t SVc(v3_t w, v3_t v) { sv_t r; r.w = w; r.v = v; return r; }
 static sv_t sv0(void) { return SVc(V(0.0f, 0.0f, 0.0f), V(0.0f, 0.0f, 0.0f)); }
 static sv_t svadd_(sv_t a, sv_t b) { return SVc(add3(a.w, b.w), add3(a.v, b.v)); }
 static sv_t svmul_(sv_t a, float s) { return SVc(mul3(a.w, s), mul3(a.v, s)); }
-static float svdot_(sv_t a, sv_t b) { return dot3(a.w, b.w) + dot3(a.v, b.v); }
 static sv_t crm_(sv_t a, sv_t b) { return SVc(cross3(a.w, b.w), add3(cross3(a.w, b.v), cross3(a.v, b.w))); }
 static sv_t crf_(sv_t a, sv_t f) { return SVc(add3(cross3(a.w, f.w), cross3(a.v, f.v)), cross3(a.w, f.v)); }
 static m3_t M3c(v3_t c0, v3_t c1, v3_t c2) { m3_t m; m.c0 = c0; m.c1 = c1; m.c2 = c2; return m; }
-static m3_t madd_(m3_t a, m3_t b) { return M3c(add3(a.c0, b.c0), add3(a.c1, b.c1), add3(a.c2, b.c2)); }
-static m3_t msub_(m3_t a, m3_t b) { return M3c(sub3(a.c0, b.c0), sub3(a.c1, b.c1), sub3(a.c2, b.c2)); }
-static m3_t mmul_(m3_t a, m3_t b) { return M3c(mv_(a, b.c0), mv_(a, b.c1), mv_(a, b.c2)); }
 static m3_t mt_(m3_t a) { return M3c(V(a.c0.x, a.c1.x, a.c2.x), V(a.c0.y, a.c1.y, a.c2.y), V(a.c0.z, a.c1.z, a.c2.z)); }
-static m3_t mskew_(v3_t r) { return M3c(V(0.0f, r.z, -r.y), V(-r.z, 0.0f, r.x), V(r.y, -r.x, 0.0f)); }
-static m3_t mouter_(v3_t a, v3_t b, float s) { return M3c(mul3(a, b.x * s), mul3(a, b.y * s), mul3(a, b.z * s)); }
-static sv_t simul_(si_t I, sv_t m) { return SVc(add3(mv_(I.A, m.w), mv_(I.B, m.v)), add3(mtv_(I.B, m.w), mv_(I.C, m.v))); }
 static sv_t xmot_(m3_t E, v3_t r, sv_t m) { return SVc(mv_(E, m.w), mv_(E, sub3(m.v, cross3(r, m.w)))); }
-static sv_t xfrc_t_(m3_t E, v3_t r, sv_t f) {
-    v3_t n = mtv_(E, f.w), fo = mtv_(E, f.v);
-    return SVc(add3(n, cross3(r, fo)), fo);
-}
-static si_t xin_t_(m3_t E, v3_t r, si_t I) {
-    m3_t Et = mt_(E);
-    m3_t A = mmul_(mmul_(Et, I.A), E), B = mmul_(mmul_(Et, I.B), E), C = mmul_(mmul_(Et, I.C), E);
-    m3_t rx = mskew_(r);
-    si_t o;
-    o.A = madd_(msub_(A, mmul_(B, rx)), msub_(mmul_(rx, mt_(B)), mmul_(mmul_(rx, C), rx)));
-    o.B = madd_(B, mmul_(rx, C));
-    o.C = C;
-    return o;
-}
-static si_t siadd_(si_t a, si_t b) { si_t o; o.A = madd_(a.A, b.A); o.B = madd_(a.B, b.B); o.C = madd_(a.C, b.C); return o; }
-static si_t sirigid_(float m, v3_t c, m3_t Ic) {
-    si_t o;
-    float cc = dot3(c, c);
-    m3_t ccT = mouter_(c, c, m);
-    m3_t dg = M3c(V(m * cc, 0.0f, 0.0f), V(0.0f, m * cc, 0.0f), V(0.0f, 0.0f, m * cc));
-    o.A = madd_(Ic, msub_(dg, ccT));
-    o.B = mskew_(mul3(c, m));
-    o.C = M3c(V(m, 0.0f, 0.0f), V(0.0f, m, 0.0f), V(0.0f, 0.0f, m));
-    return o;
-}
 static q4_t qaxang_(v3_t a, float th) {
     float s, c, half = 0.5f * th, ah = half < 0.0f ? -half : half;
     sincos_(ah, &s, &c);
@@ -556,26 +523,21 @@ static void joint_(const float* lf, int jt, float qj, q4_t* qrel, v3_t* rr, sv_t
 #include "migym_oracle_env.c"
 #include "migym_oracle_render.c"
 
-/* Templates of at most OR_WORLD_MAXL links take the world-frame ABA (aba_world_,
- * as mg_artic.hip k_artic_world); larger ones the body-frame ABA below
- * (mg_artic.hip k_artic_step). */
-#define OR_WORLD_MAXL 4
-
-/* ---- articulation: Featherstone ABA, implicit drives ---- */
+/* ---- articulation: the world-frame articulated-body
+ * algorithm (aba_world_, with the implicit drives and the effort-limit
+ * re-solve), then the joint integration of an articulation without contacts
+ * and the link states by forward kinematics — as mg_env.hip:k_artic_lanes. */
 static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* state /*[nb][13]*/,
                       float* dof /*[nd][2]*/, const float* tgt /*[nd][3]*/, const float* props /*[nd][12]*/,
-                      float* cforce) {
+                      const float* ext, float* cforce) {
     const int b0 = ai[0], d0 = ai[1], t = ai[2];
     const int* ti = m->artic_tmpl_i + (size_t)t * MG_ATMPL_I_N;
     const int fl = ti[0], L = ti[1], D = ti[2], fixed_base = ti[3];
     const float* LF = m->tmpl_link_f + (size_t)fl * MG_LINK_F_N;
     const int* LI = m->tmpl_link_i + (size_t)fl * MG_LINK_I_N;
     const float h = P->h;
-    float q[OR_MAXL], qd[OR_MAXL], qdd[OR_MAXL], Dl[OR_MAXL], ul[OR_MAXL];
-    m3_t E[OR_MAXL];
-    v3_t r[OR_MAXL];
-    sv_t Sj[OR_MAXL], v[OR_MAXL], c[OR_MAXL], pA[OR_MAXL], U[OR_MAXL], a[OR_MAXL];
-    si_t IA[OR_MAXL];
+    float q[OR_MAXL], qd[OR_MAXL], qdd[OR_MAXL];
+    sv_t v[OR_MAXL];
     q4_t ql[OR_MAXL];
     v3_t xl[OR_MAXL];
     const float* s0 = state + (size_t)b0 * MG_STATE_N;
@@ -583,119 +545,13 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
     const q4_t q0 = qnorm_(Q(s0[3], s0[4], s0[5], s0[6]));
     const float grav_on = m->tmpl_body_f[(size_t)m->body_tmpl[b0] * MG_TBODY_F_N + 4];
     const v3_t gw = grav_on != 0.0f ? V(P->g[0], P->g[1], P->g[2]) : V(0.0f, 0.0f, 0.0f);
-    const v3_t gb = qrot_(Q(-q0.x, -q0.y, -q0.z, q0.w), gw);
     int d, l, st_;
     if (!fixed_base || L > OR_MAXL) return -1;
     for (d = 0; d < D; ++d) { q[d] = dof[(d0 + d) * 2 + 0]; qd[d] = dof[(d0 + d) * 2 + 1]; qdd[d] = 0.0f; }
     for (st_ = 0; st_ < P->substeps; ++st_) {
-      unsigned xmask = 0u, xpos = 0u;
-      float tau0d[OR_MAXL], impd[OR_MAXL];
-      int att;
-      if (L <= OR_WORLD_MAXL) {
-          static aba_ws_t W;
-          float mdiag[OR_MAXL];
-          aba_world_(P, m, LF, LI, L, D, b0, d0, q, qd, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd, 0, NULL);
-      } else
-      for (att = 0; att < 2; ++att) {
-        unsigned nm;
-        for (l = 0; l < L; ++l) {
-            const int p = LI[l * MG_LINK_I_N + 0], jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
-            const float* M = m->body_mass + (size_t)(b0 + l) * MG_MASS_N;
-            if (p < 0) {
-                E[l] = M3c(V(1.0f, 0.0f, 0.0f), V(0.0f, 1.0f, 0.0f), V(0.0f, 0.0f, 1.0f));
-                r[l] = V(0.0f, 0.0f, 0.0f);
-                Sj[l] = sv0(); v[l] = sv0(); c[l] = sv0();
-            } else {
-                q4_t qrel; v3_t rr; sv_t s, vJ;
-                const float qj = dj >= 0 ? q[dj] : 0.0f, qdj = dj >= 0 ? qd[dj] : 0.0f;
-                joint_(LF + l * MG_LINK_F_N, jt, qj, &qrel, &rr, &s);
-                E[l] = mt_(qmat_(qrel));
-                r[l] = rr;
-                Sj[l] = s;
-                vJ = svmul_(s, qdj);
-                v[l] = svadd_(xmot_(E[l], rr, v[p]), vJ);
-                c[l] = crm_(v[l], vJ);
-            }
-            {
-                const float mass = M[11];
-                const v3_t com = V(M[8], M[9], M[10]);
-                const q4_t iq = Q(M[4], M[5], M[6], M[7]);
-                const v3_t Id = V(M[1] > 0.0f ? 1.0f / M[1] : 0.0f, M[2] > 0.0f ? 1.0f / M[2] : 0.0f,
-                                  M[3] > 0.0f ? 1.0f / M[3] : 0.0f);
-                const m3_t Rq = qmat_(iq);
-                const m3_t Ic = mmul_(mmul_(Rq, M3c(V(Id.x, 0.0f, 0.0f), V(0.0f, Id.y, 0.0f), V(0.0f, 0.0f, Id.z))), mt_(Rq));
-                IA[l] = sirigid_(mass, com, Ic);
-                pA[l] = crf_(v[l], simul_(IA[l], v[l]));
-            }
-        }
-        for (l = L - 1; l >= 1; --l) {
-            const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
-            si_t Ia = IA[l];
-            sv_t pa;
-            if (dj >= 0) {
-                const float* pr = props + (size_t)(d0 + dj) * MG_DOFPROP_N;
-                const float* tg = tgt + (size_t)(d0 + dj) * 3;
-                const int mode = (int)pr[0];
-                const float kp = pr[1], kd = pr[2], eff = pr[3], arm = pr[8];
-                float tau = 0.0f, imp = 0.0f, invD;
-                if (mode == MG_DOF_MODE_POS) {
-                    tau = kp * (tg[0] - q[dj] - h * qd[dj]) + kd * (tg[1] - qd[dj]);
-                    imp = h * kd + h * h * kp;
-                } else if (mode == MG_DOF_MODE_VEL) {
-                    tau = kd * (tg[1] - qd[dj]);
-                    imp = h * kd;
-                } else if (mode == MG_DOF_MODE_EFFORT) {
-                    tau = tg[2];
-                }
-                if (eff > 0.0f) {
-                    if ((xmask >> dj) & 1u) {
-                        tau = ((xpos >> dj) & 1u) ? eff : -eff;
-                        imp = 0.0f;
-                    } else if (imp == 0.0f) {
-                        tau = fminf(fmaxf(tau, -eff), eff);
-                    }
-                }
-                tau0d[dj] = tau;
-                impd[dj] = imp;
-                U[l] = simul_(Ia, Sj[l]);
-                Dl[l] = svdot_(Sj[l], U[l]) + arm + imp;
-                ul[l] = tau - svdot_(Sj[l], pA[l]);
-                invD = 1.0f / Dl[l];
-                Ia.A = msub_(Ia.A, mouter_(U[l].w, U[l].w, invD));
-                Ia.B = msub_(Ia.B, mouter_(U[l].w, U[l].v, invD));
-                Ia.C = msub_(Ia.C, mouter_(U[l].v, U[l].v, invD));
-                pa = svadd_(svadd_(pA[l], simul_(Ia, c[l])), svmul_(U[l], ul[l] * invD));
-            } else {
-                pa = svadd_(pA[l], simul_(Ia, c[l]));
-            }
-            if (p > 0 || (p == 0 && !fixed_base)) {
-                IA[p] = siadd_(IA[p], xin_t_(E[l], r[l], Ia));
-                pA[p] = svadd_(pA[p], xfrc_t_(E[l], r[l], pa));
-            }
-        }
-        a[0] = SVc(V(0.0f, 0.0f, 0.0f), mul3(gb, -1.0f));
-        for (l = 1; l < L; ++l) {
-            const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
-            sv_t ap = svadd_(xmot_(E[l], r[l], a[p]), c[l]);
-            if (dj >= 0) {
-                const float acc = (ul[l] - svdot_(U[l], ap)) / Dl[l];
-                qdd[dj] = acc;
-                ap = svadd_(ap, svmul_(Sj[l], acc));
-            }
-            a[l] = ap;
-        }
-        nm = xmask;
-        for (d = 0; d < D; ++d) {
-            const float eff = props[(size_t)(d0 + d) * MG_DOFPROP_N + 3];
-            if (eff > 0.0f && impd[d] != 0.0f) {
-                const float act = tau0d[d] - impd[d] * qdd[d];
-                if (act > eff) { nm |= 1u << d; xpos |= 1u << d; }
-                else if (act < -eff) nm |= 1u << d;
-            }
-        }
-        if (nm == xmask) break;
-        xmask = nm;
-      }
+        float tau0d[OR_MAXL], impd[OR_MAXL], mdiag[OR_MAXL];
+        static aba_ws_t W;
+        aba_world_(P, m, LF, LI, L, D, b0, d0, q, qd, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd, 0, ext);
         for (d = 0; d < D; ++d) {
             const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
             const float maxv = pr[4];
@@ -769,7 +625,7 @@ int oracle_step(const mg_sim_params* p, const mg_model* m, float* state, float* 
     for (k = 0; k < m->num_artics; ++k) {
         const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;
         if (ai[0] < body_begin || ai[0] >= body_end || owned[ai[0]]) continue;
-        if (artic_step(&P, m, ai, state, dof, tgt, props, cforce) != 0) { rc = -1; goto done; }
+        if (artic_step(&P, m, ai, state, dof, tgt, props, ext, cforce) != 0) { rc = -1; goto done; }
     }
     for (b = body_begin; b < body_end; ++b) {
         if (m->body_kind[b] != MG_BODY_FREE || owned[b]) continue;

@@ -298,39 +298,44 @@ MG_HD void spd6_solve(const float* M, const float* b, float* x) {
 // by slots DA..DA+5; the inward pass also folds into link 0 and the root
 // acceleration solves IA_0 a0 = -pA_0 (a0 relative to gravity, as the fixed
 // base's a0 = -g). External wrenches at link COMs (A.ext) enter the bias forces.
+// The articulated-body algorithm is split so that the effort-limit re-solve
+// (a second pass with the flagged drives at constant force) repeats only what
+// the drives change: aba_kin (joint transforms, forward kinematics, motion
+// axes, world inertias, velocities, velocity-product terms) runs once per
+// substep; aba_dyn (drive terms, inward and outward passes) per attempt, after
+// aba_refresh restores the world inertias and bias forces the previous inward
+// pass accumulated into (recomputed: the same values bit for bit).
 template <int MAXL>
-__device__ __forceinline__ void aba_world(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0, Q4 q0,
-                          V3 gw, const LinkC& lk, const DofC& dc, bool is_dof, bool xm, bool xp, int b0) {
-    const float h = P.h;
+__device__ __forceinline__ void aba_vp(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0,
+                                       const LinkC& lk, int b0) {
+    // ---- velocity-product terms (lane l)
+    if (act && ln < LA) {
+        const int dof = A.link_i[ln * MG_LINK_I_N + 2];
+        const float qd = dof >= 0 ? S.u[dof] : 0.0f;
+        const SV v = sv6(S.va[ln]);
+        const SV vJ = svscale(sv6(S.xi[ln]), qd);
+        float Iv[6];
+        for (int i = 0; i < 6; ++i) Iv[i] = dot6(&S.Iw[ln][i * 6], S.va[ln]);
+        put6(S.cc[ln], crm(v, vJ));
+        SV pb = crf(v, sv6(Iv));
+        if (A.ext) {
+            // world force f and torque t at the link COM: the wrench about x0
+            const int b = b0 + ln, nb = A.nb;
+            const V3 f = v3(A.ext[0 * nb + b], A.ext[1 * nb + b], A.ext[2 * nb + b]);
+            const V3 t = v3(A.ext[3 * nb + b], A.ext[4 * nb + b], A.ext[5 * nb + b]);
+            const V3 c = vsub(vadd(S.xl[ln], qrot(S.ql[ln], lk.com)), x0);
+            pb = sv(vsub(pb.w, vadd(t, vcross(c, f))), vsub(pb.v, f));
+        }
+        put6(S.pa[ln], pb);
+    }
+    __syncthreads();
+}
+
+template <int MAXL>
+__device__ __forceinline__ void aba_kin(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0,
+                                        Q4 q0, const LinkC& lk, int b0) {
     const bool fb = A.floating != 0;
     const int DA = A.ndof;
-    // ---- drive terms (lane d): implicit PD force and its h-derivative; a DOF
-    // flagged by the effort-limit test (xm) runs at constant +-effort
-    if (act && is_dof) {
-        const float qv = S.q[ln], uv = S.u[ln];
-        float tau = 0.0f, imp = 0.0f;
-        if (dc.mode == MG_DOF_MODE_POS) {
-            tau = dc.kp * (dc.tpos - qv - h * uv) + dc.kd * (dc.tvel - uv);
-            imp = h * dc.kd + h * h * dc.kp;
-        } else if (dc.mode == MG_DOF_MODE_VEL) {
-            tau = dc.kd * (dc.tvel - uv);
-            imp = h * dc.kd;
-        } else if (dc.mode == MG_DOF_MODE_EFFORT) {
-            tau = dc.force;
-        }
-        if (dc.eff > 0.0f) {
-            if (xm) {
-                tau = xp ? dc.eff : -dc.eff;
-                imp = 0.0f;
-            } else if (imp == 0.0f) {
-                tau = fminf(fmaxf(tau, -dc.eff), dc.eff);
-            }
-        }
-        S.tau0[ln] = tau;
-        S.imp[ln] = imp;
-        S.mdiag[ln] = dc.arm + imp;
-        S.arm[ln] = dc.arm;
-    }
     // ---- joint transforms (lane l)
     if (act && ln < LA && ln > 0) {
         const float* lf = A.link_f + ln * MG_LINK_F_N;
@@ -390,25 +395,48 @@ __device__ __forceinline__ void aba_world(const MgStep& P, const MgEnvArgs& A, E
         }
     }
     __syncthreads();
-    // ---- velocity-product terms (lane l)
-    if (act && ln < LA) {
-        const int dof = A.link_i[ln * MG_LINK_I_N + 2];
-        const float qd = dof >= 0 ? S.u[dof] : 0.0f;
-        const SV v = sv6(S.va[ln]);
-        const SV vJ = svscale(sv6(S.xi[ln]), qd);
-        float Iv[6];
-        for (int i = 0; i < 6; ++i) Iv[i] = dot6(&S.Iw[ln][i * 6], S.va[ln]);
-        put6(S.cc[ln], crm(v, vJ));
-        SV pb = crf(v, sv6(Iv));
-        if (A.ext) {
-            // world force f and torque t at the link COM: the wrench about x0
-            const int b = b0 + ln, nb = A.nb;
-            const V3 f = v3(A.ext[0 * nb + b], A.ext[1 * nb + b], A.ext[2 * nb + b]);
-            const V3 t = v3(A.ext[3 * nb + b], A.ext[4 * nb + b], A.ext[5 * nb + b]);
-            const V3 c = vsub(vadd(S.xl[ln], qrot(S.ql[ln], lk.com)), x0);
-            pb = sv(vsub(pb.w, vadd(t, vcross(c, f))), vsub(pb.v, f));
+    aba_vp<MAXL>(A, S, act, ln, LA, x0, lk, b0);
+}
+
+template <int MAXL>
+__device__ __forceinline__ void aba_refresh(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0,
+                                            const LinkC& lk, int b0) {
+    if (act && ln < LA) world_inertia(lk, S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
+    aba_vp<MAXL>(A, S, act, ln, LA, x0, lk, b0);
+}
+
+template <int MAXL>
+__device__ __forceinline__ void aba_dyn(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0,
+                                        V3 gw, const DofC& dc, bool is_dof, bool xm, bool xp, int b0) {
+    const float h = P.h;
+    const bool fb = A.floating != 0;
+    const int DA = A.ndof;
+    // ---- drive terms (lane d): implicit PD force and its h-derivative; a DOF
+    // flagged by the effort-limit test (xm) runs at constant +-effort
+    if (act && is_dof) {
+        const float qv = S.q[ln], uv = S.u[ln];
+        float tau = 0.0f, imp = 0.0f;
+        if (dc.mode == MG_DOF_MODE_POS) {
+            tau = dc.kp * (dc.tpos - qv - h * uv) + dc.kd * (dc.tvel - uv);
+            imp = h * dc.kd + h * h * dc.kp;
+        } else if (dc.mode == MG_DOF_MODE_VEL) {
+            tau = dc.kd * (dc.tvel - uv);
+            imp = h * dc.kd;
+        } else if (dc.mode == MG_DOF_MODE_EFFORT) {
+            tau = dc.force;
         }
-        put6(S.pa[ln], pb);
+        if (dc.eff > 0.0f) {
+            if (xm) {
+                tau = xp ? dc.eff : -dc.eff;
+                imp = 0.0f;
+            } else if (imp == 0.0f) {
+                tau = fminf(fmaxf(tau, -dc.eff), dc.eff);
+            }
+        }
+        S.tau0[ln] = tau;
+        S.imp[ln] = imp;
+        S.mdiag[ln] = dc.arm + imp;
+        S.arm[ln] = dc.arm;
     }
     __syncthreads();
     // ---- inward pass: articulated inertias and bias forces
@@ -490,6 +518,7 @@ __device__ __forceinline__ void aba_world(const MgStep& P, const MgEnvArgs& A, E
     }
     __syncthreads();
 }
+
 
 // M_eff = joint-space inertia + S.mdiag from world-frame composite inertias
 // (entrywise subtree sums of the link inertias; M_ij = xi_j . IC_i xi_i for j
@@ -722,9 +751,11 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         if (LA > 0) {
             bool xm = false, xp = false;     // this DOF runs at constant +-effort
             bool redo = live && L > 0;
+            aba_kin<MAXL>(P, A, S, redo, ln, LA, x0, q0, lk, b0);
             for (int att = 0; att < 2; ++att) {
                 if (!__any(redo)) break;
-                aba_world<MAXL>(P, A, S, redo, ln, LA, x0, q0, gw, lk, dc, is_dof, xm, xp, b0);
+                if (att > 0) aba_refresh<MAXL>(A, S, redo, ln, LA, x0, lk, b0);
+                aba_dyn<MAXL>(P, A, S, redo, ln, LA, x0, gw, dc, is_dof, xm, xp, b0);
                 // drives whose implicit force exceeds the effort limit
                 bool flip = false;
                 if (redo && is_dof && dc.eff > 0.0f && S.imp[ln] != 0.0f) {
@@ -1164,7 +1195,183 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     PH_MARK(7);
 }
 
+// Uncoupled fixed-base articulations (the S2 gimbal, test12_add_joint.py.py:
+// 69-98): the world-frame articulated-body algorithm of the coupled step
+// (aba_kin / aba_dyn, 16 lanes per articulation, 4 per wavefront, the per-articulation
+// quantities in LDS) followed by the joint integration of an articulation
+// without contacts — q' = q + h clamp(q' + h q'', maxv), joint limits clamped
+// — and the link states by forward kinematics. Restated by
+// oracle/migym_oracle.c:artic_step (aba_world_ + the same integration and
+// outputs).
+template <int MAXL>
+__global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
+    __shared__ EnvLds shm[EPW];
+    const int gi = threadIdx.x / G;
+    const int ln = threadIdx.x % G;
+    const int a = blockIdx.x * EPW + gi;
+    const bool live = a < AA.na;
+    EnvLds& S = shm[gi];
+    MgEnvArgs A{};
+    A.nb = AA.nb; A.nd = AA.nd; A.nl = AA.nl; A.ndof = AA.ndof; A.floating = 0;
+    A.link_f = AA.link_f; A.link_i = AA.link_i;
+    A.state = AA.state; A.mass = AA.mass; A.body_tmpl = AA.body_tmpl; A.tbf = AA.tbf;
+    A.dof_pos = AA.dof_pos; A.dof_vel = AA.dof_vel; A.dof_tpos = AA.dof_tpos; A.dof_tvel = AA.dof_tvel;
+    A.dof_force = AA.dof_force; A.dof_props = AA.dof_props; A.ext = AA.ext; A.cforce = AA.cforce;
+    const int* ai = AA.artic_i + (size_t)(live ? a : 0) * MG_ARTIC_I_N;
+    const int b0 = ai[0], d0 = ai[1];
+    const int nb = A.nb, nd = A.nd;
+    const int LA = A.nl, DA = A.ndof;           // launch-uniform (barriers inside)
+    const int L = live ? LA : 0, D = live ? DA : 0;
+    float* St = A.state;
+    const float* pr = A.dof_props;
+    const float h = P.h;
+    const bool is_dof = ln < D;
+
+    V3 x0 = v3(0.0f, 0.0f, 0.0f), gw = v3(0.0f, 0.0f, 0.0f);
+    Q4 q0 = q4(0.0f, 0.0f, 0.0f, 1.0f);
+    if (live) {
+        x0 = v3(St[0 * nb + b0], St[1 * nb + b0], St[2 * nb + b0]);
+        q0 = qnormalize(q4(St[3 * nb + b0], St[4 * nb + b0], St[5 * nb + b0], St[6 * nb + b0]));
+        if (A.tbf[A.body_tmpl[b0] * MG_TBODY_F_N + 4] != 0.0f) gw = v3(P.g[0], P.g[1], P.g[2]);
+    }
+    float qv = 0.0f, uv = 0.0f;
+    DofC dc = {};
+    if (is_dof) {
+        const int gd = d0 + ln;
+        qv = A.dof_pos[gd];
+        uv = A.dof_vel[gd];
+        dc.mode = (int)pr[0 * nd + gd];
+        dc.kp = pr[1 * nd + gd];
+        dc.kd = pr[2 * nd + gd];
+        dc.eff = pr[3 * nd + gd];
+        dc.maxv = pr[4 * nd + gd];
+        dc.lo = pr[5 * nd + gd];
+        dc.hi = pr[6 * nd + gd];
+        dc.haslim = pr[7 * nd + gd] != 0.0f;
+        dc.arm = pr[8 * nd + gd];
+        dc.tpos = A.dof_tpos[gd];
+        dc.tvel = A.dof_tvel[gd];
+        dc.force = A.dof_force[gd];
+    }
+    LinkC lk = {};
+    if (ln < L) lk = load_link(A.mass, nb, b0 + ln);
+
+    for (int st = 0; st < P.substeps; ++st) {
+        S.q[ln] = qv;
+        S.u[ln] = uv;
+        __syncthreads();
+        bool xm = false, xp = false;     // this DOF runs at constant +-effort
+        bool redo = live;
+        aba_kin<MAXL>(P, A, S, redo, ln, LA, x0, q0, lk, b0);
+        for (int att = 0; att < 2; ++att) {
+            if (!__any(redo)) break;
+            if (att > 0) aba_refresh<MAXL>(A, S, redo, ln, LA, x0, lk, b0);
+            aba_dyn<MAXL>(P, A, S, redo, ln, LA, x0, gw, dc, is_dof, xm, xp, b0);
+            // drives whose implicit force exceeds the effort limit
+            bool flip = false;
+            if (redo && is_dof && dc.eff > 0.0f && S.imp[ln] != 0.0f) {
+                const float actf = S.tau0[ln] - S.imp[ln] * S.qdd[ln];
+                if (actf > dc.eff) { xm = true; xp = true; flip = true; }
+                else if (actf < -dc.eff) { xm = true; flip = true; }
+            }
+            const unsigned long long fb = __ballot(flip);
+            redo = ((fb >> (gi * G)) & 0xFFFFull) != 0ull;
+            __syncthreads();
+        }
+        // integrate the joint (DOF lane)
+        if (is_dof) {
+            float w = uv + h * S.qdd[ln];
+            if (dc.maxv > 0.0f) w = fminf(fmaxf(w, -dc.maxv), dc.maxv);
+            float x = qv + h * w;
+            if (dc.haslim) {
+                if (x < dc.lo) { x = dc.lo; if (w < 0.0f) w = 0.0f; }
+                if (x > dc.hi) { x = dc.hi; if (w > 0.0f) w = 0.0f; }
+            }
+            qv = x;
+            uv = w;
+        }
+        __syncthreads();
+    }
+
+    // outputs: DOF state; link states by forward kinematics at the new (q, qd):
+    // joint transforms per link lane, the kinematic scan on lane 0, world
+    // velocities and stores per link lane
+    if (is_dof) {
+        A.dof_pos[d0 + ln] = qv;
+        A.dof_vel[d0 + ln] = uv;
+    }
+    S.q[ln] = qv;
+    S.u[ln] = uv;
+    __syncthreads();
+    float* vs = &S.va[0][0];          // link velocities (body frame), 6 per link
+    if (ln < L && ln > 0) {
+        const float* lf = A.link_f + ln * MG_LINK_F_N;
+        const int* li = A.link_i + ln * MG_LINK_I_N;
+        const int jt = li[1], dof = li[2];
+        const V3 po = v3(lf[0], lf[1], lf[2]);
+        const Q4 qo = q4(lf[3], lf[4], lf[5], lf[6]);
+        const V3 ax = v3(lf[7], lf[8], lf[9]);
+        const float qj = dof >= 0 ? S.q[dof] : 0.0f;
+        Q4 qrel = qo;
+        V3 rr = po;
+        SV sj = svzero();
+        if (jt == MG_JOINT_REVOLUTE) {
+            qrel = qmul(qo, q_axis_angle(ax, qj));
+            sj = sv(ax, v3(0.0f, 0.0f, 0.0f));
+        } else if (jt == MG_JOINT_PRISMATIC) {
+            rr = vadd(po, qrot(qo, vscale(ax, qj)));
+            sj = sv(v3(0.0f, 0.0f, 0.0f), ax);
+        }
+        S.qr[ln] = qrel;
+        S.rr[ln] = rr;
+        put6(S.xi[ln], sj);
+    }
+    __syncthreads();
+    if (live && ln == 0) {
+        for (int l = 0; l < LA; ++l) {
+            const int p = A.link_i[l * MG_LINK_I_N + 0], dof = A.link_i[l * MG_LINK_I_N + 2];
+            if (p < 0) {
+                S.ql[l] = q0;
+                S.xl[l] = x0;
+                put6(vs + 6 * l, svzero());
+            } else {
+                const Q4 qp = S.ql[p];
+                const Q4 qrel = S.qr[l];
+                const float qdj = dof >= 0 ? S.u[dof] : 0.0f;
+                S.ql[l] = qnormalize(qmul(qp, qrel));
+                S.xl[l] = vadd(S.xl[p], qrot(qp, S.rr[l]));
+                put6(vs + 6 * l, svadd(x_motion(m3t(qmat(qrel)), S.rr[l], sv6(vs + 6 * p)), svscale(sv6(S.xi[l]), qdj)));
+            }
+        }
+    }
+    __syncthreads();
+    if (ln < L) {
+        const int b = b0 + ln;
+        const SV vl = sv6(vs + 6 * ln);
+        const Q4 ql = S.ql[ln];
+        const V3 xl = S.xl[ln];
+        const V3 ww = qrot(ql, vl.w);
+        const V3 vw = qrot(ql, vadd(vl.v, vcross(vl.w, lk.com)));
+        St[0 * nb + b] = xl.x; St[1 * nb + b] = xl.y; St[2 * nb + b] = xl.z;
+        St[3 * nb + b] = ql.x; St[4 * nb + b] = ql.y; St[5 * nb + b] = ql.z; St[6 * nb + b] = ql.w;
+        St[7 * nb + b] = vw.x; St[8 * nb + b] = vw.y; St[9 * nb + b] = vw.z;
+        St[10 * nb + b] = ww.x; St[11 * nb + b] = ww.y; St[12 * nb + b] = ww.z;
+        A.cforce[0 * nb + b] = 0.0f; A.cforce[1 * nb + b] = 0.0f; A.cforce[2 * nb + b] = 0.0f;
+    }
+}
+
 }  // namespace
+
+hipError_t mg_launch_artic_lanes(const MgStep& P, const MgArticArgs& A, hipStream_t s) {
+    if (A.na <= 0) return hipSuccess;
+    if (!A.fixed_base || A.nl > MG_MAX_LINKS || A.ndof > G) return hipErrorNotSupported;
+    const int blocks = (A.na + EPW - 1) / EPW;
+    if (A.nl <= 4 && A.ndof <= 4)
+        MG_LAUNCH((k_artic_lanes<4>), dim3(blocks), dim3(64), 0, s, P, A);
+    else
+        MG_LAUNCH((k_artic_lanes<MG_MAX_LINKS>), dim3(blocks), dim3(64), 0, s, P, A);
+    return hipGetLastError();
+}
 
 hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s) {
     if (A.ne <= 0) return hipSuccess;

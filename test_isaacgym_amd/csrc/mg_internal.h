@@ -198,6 +198,7 @@ hipError_t mg_launch_render(const MgRenderArgs& A, int nblocks, hipStream_t s);
 hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s);
 hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream_t s);
 hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream_t s);
+hipError_t mg_launch_artic_lanes(const MgStep& P, const MgArticArgs& A, hipStream_t s);
 hipError_t mg_launch_gather_rows(const float* soa, int stride, int ncol, const int* ids, int n,
                                  float* aos, hipStream_t s);
 hipError_t mg_launch_scatter_rows(const float* aos, int ncol, const int* ids, const int* sel,
