@@ -482,7 +482,12 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
                                             V3& w, V3& fsum, float invm, V3 invI, Q4 iq, V3 com, V3 fext,
                                             V3 text, const float* hulls) {
     const float lin_damp = T[0], ang_damp = T[1], max_lv = T[2], max_av = T[3], grav_on = T[4];
-    const float* sh = T + MG_TBODY_F_N;
+    // the shape record in registers: read from LDS once (one wait), not per substep
+    float sh[MG_SHAPE_STRIDE];
+#pragma unroll
+    for (int k = 0; k < 13; ++k) sh[k] = T[MG_TBODY_F_N + k];
+#pragma unroll
+    for (int k = 13; k < MG_SHAPE_STRIDE; ++k) sh[k] = 0.0f;
     const bool has_shape = P.has_ground && sh[0] >= 0.0f;
     const float h = P.h;
     const float lin_keep = 1.0f - fminf(lin_damp * h, 1.0f);
