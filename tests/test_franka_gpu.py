@@ -87,10 +87,13 @@ def test_franka_pick_parity_bitexact(gym):
     assert lifted.sum() >= 1      # the window reaches grasp-and-lift contacts
 
 
-def test_franka_pick_lifts_cubes(gym):
-    """256 envs, 600 frames (10 s) of the script's loop: most cubes are grasped
-    and lifted above 0.55 m (the script drops them at 0.6 m, :405)."""
-    n, frames = 256, 600
+@pytest.mark.parametrize("n", [256, 4096])
+def test_franka_pick_lifts_cubes(gym, n):
+    """Config 3 (examples/franka_cube_ik_osc.py --num_envs 4096) at 256 and at
+    the full 4096 envs, 600 frames (10 s) of the script's loop: most cubes are
+    grasped and lifted above 0.55 m (the script drops them at 0.6 m, :405),
+    state stays finite, no cube sinks into the table or the ground."""
+    frames = 600
     sim, info, rb, dof, jac, mm, ctl = _setup(gym, n)
     maxz = torch.zeros(n, device=DEV)
     bi = torch.tensor(info["box_idxs"], device=DEV)
@@ -102,8 +105,13 @@ def test_franka_pick_lifts_cubes(gym):
     assert torch.isfinite(rb).all()
     frac = float((maxz > 0.55).float().mean())
     assert frac >= 0.5, "only %.2f of the cubes were lifted" % frac
-    # nothing sinks through the table or the ground
-    assert float(rb[bi, 2].min()) > 0.0
+    # nothing sinks through the table or the ground: a cube is on the table
+    # (top at 0.4 m, cube half size 0.0225 m), in the gripper, or on the ground
+    z = rb[bi, 2]
+    assert float(z.min()) > 0.0
+    still = rb[bi, 7:10].norm(dim=1) < 0.05
+    sunk = (z > 0.3) & (z < 0.4225 - 0.005) & still
+    assert int(sunk.sum()) == 0, "cubes at rest inside the table: %s" % z[sunk][:8].tolist()
 
 
 def test_franka_jacobian_mass_matrix_float64(gym):
