@@ -407,7 +407,104 @@ def _mesh_vertices(path):
         rec = np.frombuffer(data[84:84 + 50 * n], dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)),
                                                                    ("a", "<u2")]))
         return rec["v"].reshape(-1, 3).astype(np.float64)
+    if ext == ".dae":
+        return _collada_vertices(path)
     return np.zeros((0, 3))
+
+
+def _collada_vertices(path):
+    """Vertex positions of a COLLADA (.dae) file in metres: every <geometry>
+    mesh's POSITION source, placed by the <visual_scene> nodes that instance it
+    (<matrix> / <translate> / <rotate> / <scale>, composed down the node tree;
+    a geometry no node instances is taken as is), times <asset><unit meter>.
+    A Y_UP file is turned to Z_UP (y -> z), as URDF meshes are z-up. Only the
+    vertices matter: the importer reduces a collision mesh to its convex hull."""
+    import xml.etree.ElementTree as ET
+    root = ET.parse(path).getroot()
+
+    def tag(el):
+        return el.tag.rsplit("}", 1)[-1]
+
+    def kids(el, name):
+        return [c for c in el if tag(c) == name]
+
+    def floats(el):
+        return np.array([float(t) for t in (el.text or "").split()], dtype=np.float64)
+
+    unit, up = 1.0, "Z_UP"
+    for a in kids(root, "asset"):
+        for u in kids(a, "unit"):
+            unit = float(u.get("meter", "1"))
+        for ua in kids(a, "up_axis"):
+            up = (ua.text or "Z_UP").strip()
+    geoms = {}
+    for lib in kids(root, "library_geometries"):
+        for g in kids(lib, "geometry"):
+            for mesh in kids(g, "mesh"):
+                srcs = {}
+                for src in kids(mesh, "source"):
+                    for fa in kids(src, "float_array"):
+                        srcs[src.get("id")] = floats(fa)
+                pos = None
+                for vx in kids(mesh, "vertices"):
+                    for inp in kids(vx, "input"):
+                        if inp.get("semantic") == "POSITION":
+                            pos = srcs.get(inp.get("source", "").lstrip("#"))
+                if pos is not None and len(pos) >= 3:
+                    geoms[g.get("id")] = pos[:len(pos) // 3 * 3].reshape(-1, 3)
+
+    def node_matrix(node):
+        M = np.eye(4)
+        for c in node:
+            t = tag(c)
+            if t == "matrix":
+                M = M @ floats(c).reshape(4, 4)
+            elif t == "translate":
+                T4 = np.eye(4)
+                T4[:3, 3] = floats(c)[:3]
+                M = M @ T4
+            elif t == "scale":
+                M = M @ np.diag(list(floats(c)[:3]) + [1.0])
+            elif t == "rotate":
+                ax, ang = floats(c)[:3], math.radians(floats(c)[3])
+                n = np.linalg.norm(ax)
+                if n > 0:
+                    x, y, z = ax / n
+                    cth, sth = math.cos(ang), math.sin(ang)
+                    R = np.array([[cth + x * x * (1 - cth), x * y * (1 - cth) - z * sth, x * z * (1 - cth) + y * sth],
+                                  [y * x * (1 - cth) + z * sth, cth + y * y * (1 - cth), y * z * (1 - cth) - x * sth],
+                                  [z * x * (1 - cth) - y * sth, z * y * (1 - cth) + x * sth, cth + z * z * (1 - cth)]])
+                    R4 = np.eye(4)
+                    R4[:3, :3] = R
+                    M = M @ R4
+        return M
+
+    out, used = [], set()
+
+    def visit(node, M):
+        M = M @ node_matrix(node)
+        for ig in kids(node, "instance_geometry"):
+            gid = ig.get("url", "").lstrip("#")
+            if gid in geoms:
+                v = geoms[gid]
+                out.append(v @ M[:3, :3].T + M[:3, 3])
+                used.add(gid)
+        for c in kids(node, "node"):
+            visit(c, M)
+
+    for lib in kids(root, "library_visual_scenes"):
+        for vs in kids(lib, "visual_scene"):
+            for nd in kids(vs, "node"):
+                visit(nd, np.eye(4))
+    for gid, v in geoms.items():
+        if gid not in used:
+            out.append(v)
+    if not out:
+        return np.zeros((0, 3))
+    v = np.concatenate(out, 0) * unit
+    if up == "Y_UP":
+        v = np.stack([v[:, 0], -v[:, 2], v[:, 1]], 1)
+    return v
 
 
 _HULL_CACHE = {}
