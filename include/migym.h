@@ -218,11 +218,14 @@ int32_t     mg_apply_rigid_body_force(mg_sim* sim, const float* force, const flo
                                       int32_t space, int32_t src_host, void* stream);
 
 /* ---- Jacobian / mass matrix (examples/franka_cube_ik_osc.py:305-316,345-346) */
-/* For the fixed-base articulation template `tmpl` (instances in actor order):
+/* For the articulation template `tmpl` (instances in actor order), fixed base:
  * Jacobian (instances, L-1, 6, D) — link 1..L-1, rows [linear velocity of the
  * link frame origin; angular velocity] in the world frame, one column per DOF;
  * mass matrix (instances, D, D) — joint-space inertia by the composite-rigid-
- * body algorithm, joint armature not included. Both at the current DOF state. */
+ * body algorithm, joint armature not included. Floating base (D + 6 <= 16):
+ * six root columns first (linear velocity of the base-link origin, then
+ * angular velocity, world axes), Jacobian (instances, L, 6, D + 6) over every
+ * link, mass matrix (instances, D + 6, D + 6). At the current state. */
 int32_t     mg_refresh_jacobian(mg_sim* sim, int32_t tmpl, float* dst, int32_t dst_host, void* stream);
 int32_t     mg_refresh_mass_matrix(mg_sim* sim, int32_t tmpl, float* dst, int32_t dst_host, void* stream);
 /* Both in one launch (one forward-kinematics pass): refresh_jacobian_tensors

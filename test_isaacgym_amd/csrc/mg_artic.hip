@@ -87,6 +87,10 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
     }
     __syncthreads();
     // world axes, motion subspaces, inertias (lane l)
+    const bool fb = !A.fixed_base;
+    const int R0 = fb ? 6 : 0;            // root columns (floating base) before the DOFs
+    const int NC = D + R0;                // generalized velocities
+    const int row0 = fb ? 0 : 1;          // first link row of the Jacobian
     if (live && ln < L) {
         const int* li = A.link_i + ln * MG_LINK_I_N;
         const int jt = li[1], dof = li[2];
@@ -99,7 +103,7 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
             else x = sv(v3(0.0f, 0.0f, 0.0f), z);
         }
         put6(S.xi[ln], x);
-        if (mm && ln > 0) world_inertia(load_link(A.mass, nb, b0 + ln), S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
+        if (mm && (ln > 0 || fb)) world_inertia(load_link(A.mass, nb, b0 + ln), S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
     }
     __syncthreads();
     // the link whose joint is DOF ln
@@ -110,27 +114,42 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
             jl = l;
             jrev = A.link_i[l * MG_LINK_I_N + 1] == MG_JOINT_REVOLUTE;
         }
-    if (jac && live && ln < D && jl > 0) {
-        // column ln of every link's 6 x D block: [linear at the link origin; angular]
-        float* J = jac + (size_t)e * (L - 1) * 6 * D;
-        const V3 z = S.zl[jl], xj = S.xl[jl];
-        for (int l = 1; l < L; ++l) {
-            V3 lin = v3(0.0f, 0.0f, 0.0f), ang = v3(0.0f, 0.0f, 0.0f);
-            if ((S.amask[l] >> ln) & 1) {
-                if (jrev) { lin = vcross(z, vsub(S.xl[l], xj)); ang = z; }
-                else lin = z;
+    if (jac && live) {
+        float* J = jac + (size_t)e * (L - row0) * 6 * NC;
+        if (ln < D && jl > 0) {
+            // column R0 + ln of every link's 6 x NC block: [linear at the link origin; angular]
+            const V3 z = S.zl[jl], xj = S.xl[jl];
+            for (int l = row0; l < L; ++l) {
+                V3 lin = v3(0.0f, 0.0f, 0.0f), ang = v3(0.0f, 0.0f, 0.0f);
+                if ((S.amask[l] >> ln) & 1) {
+                    if (jrev) { lin = vcross(z, vsub(S.xl[l], xj)); ang = z; }
+                    else lin = z;
+                }
+                float* Jl = J + (size_t)(l - row0) * 6 * NC + R0 + ln;
+                Jl[0 * NC] = lin.x; Jl[1 * NC] = lin.y; Jl[2 * NC] = lin.z;
+                Jl[3 * NC] = ang.x; Jl[4 * NC] = ang.y; Jl[5 * NC] = ang.z;
             }
-            float* Jl = J + (size_t)(l - 1) * 6 * D + ln;
-            Jl[0 * D] = lin.x; Jl[1 * D] = lin.y; Jl[2 * D] = lin.z;
-            Jl[3 * D] = ang.x; Jl[4 * D] = ang.y; Jl[5 * D] = ang.z;
+        } else if (fb && ln >= D && ln < D + 6) {
+            // root column k: linear velocity of x0 along e_k (k < 3), rotation
+            // about e_(k-3) through x0
+            const int k = ln - D;
+            const V3 ek = v3(k % 3 == 0 ? 1.0f : 0.0f, k % 3 == 1 ? 1.0f : 0.0f, k % 3 == 2 ? 1.0f : 0.0f);
+            for (int l = 0; l < L; ++l) {
+                V3 lin = ek, ang = v3(0.0f, 0.0f, 0.0f);
+                if (k >= 3) { lin = vcross(ek, vsub(S.xl[l], x0)); ang = ek; }
+                float* Jl = J + (size_t)l * 6 * NC + k;
+                Jl[0 * NC] = lin.x; Jl[1 * NC] = lin.y; Jl[2 * NC] = lin.z;
+                Jl[3 * NC] = ang.x; Jl[4 * NC] = ang.y; Jl[5 * NC] = ang.z;
+            }
         }
     }
     if (!mm) return;
     // composite inertias: subtree sums, deepest link first (links are in
-    // topological order: a parent precedes its children)
+    // topological order: a parent precedes its children); a floating base also
+    // folds the tree into link 0
     for (int l = L - 1; l >= 1; --l) {
         const int p = A.link_i[l * MG_LINK_I_N + 0];
-        if (live && p > 0)
+        if (live && (p > 0 || (fb && p == 0)))
             for (int k = ln; k < 36; k += JG) S.Iw[p][k] = S.Iw[p][k] + S.Iw[l][k];
         __syncthreads();
     }
@@ -139,22 +158,44 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
     if (live && ln < D && jl > 0) {
         float F[6];
         for (int r = 0; r < 6; ++r) F[r] = dot6(&S.Iw[jl][r * 6], S.xi[jl]);
-        S.M[ln][ln] = dot6(S.xi[jl], F);
+        const int i = R0 + ln;
+        S.M[i][i] = dot6(S.xi[jl], F);
         int j = A.link_i[jl * MG_LINK_I_N + 0];
         while (j > 0) {
             const int dj = A.link_i[j * MG_LINK_I_N + 2];
             if (dj >= 0) {
                 const float hv = dot6(S.xi[j], F);
-                S.M[ln][dj] = hv;
-                S.M[dj][ln] = hv;
+                S.M[i][R0 + dj] = hv;
+                S.M[R0 + dj][i] = hv;
             }
             j = A.link_i[j * MG_LINK_I_N + 0];
         }
+        if (fb)
+            // DOF - root coupling: the force IC xi (moment about x0, force) paired
+            // with the root's unit motions (linear e_k: force k; angular e_k: moment k)
+            for (int k = 0; k < 3; ++k) {
+                S.M[i][k] = F[3 + k];
+                S.M[k][i] = F[3 + k];
+                S.M[i][3 + k] = F[k];
+                S.M[3 + k][i] = F[k];
+            }
+    }
+    if (live && fb && ln == D) {
+        // root block from the whole-tree composite inertia about x0 ([A B; B^T C],
+        // rows / columns (w, v)) in the root's (linear, angular) order
+        const float* I0 = S.Iw[0];
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                S.M[a][b] = I0[(3 + a) * 6 + 3 + b];
+                S.M[a][3 + b] = I0[(3 + a) * 6 + b];
+                S.M[3 + a][b] = I0[a * 6 + 3 + b];
+                S.M[3 + a][3 + b] = I0[a * 6 + b];
+            }
     }
     __syncthreads();
     if (live) {
-        float* Mo = mm + (size_t)e * D * D;
-        for (int k = ln; k < D * D; k += JG) Mo[k] = S.M[k / D][k % D];
+        float* Mo = mm + (size_t)e * NC * NC;
+        for (int k = ln; k < NC * NC; k += JG) Mo[k] = S.M[k / NC][k % NC];
     }
 }
 
@@ -164,10 +205,14 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
 // (examples/franka_cube_ik_osc.py:305-316,345-346): for a fixed base
 //   J: (instances, L-1, 6, D): link l = 1..L-1, rows [linear xyz of the link
 //      frame origin, angular xyz] in the world frame, column d = DOF d;
-//   M: (instances, D, D): joint-space inertia without joint armature.
+//   M: (instances, D, D): joint-space inertia without joint armature;
+// for a floating base (D + 6 <= 16) the 6 root columns come first — linear
+// velocity of the base-link origin, then angular velocity, world axes:
+//   J: (instances, L, 6, D + 6), every link including the root;
+//   M: (instances, D + 6, D + 6) in the same generalized velocities.
 hipError_t mg_launch_jacobian(const MgArticArgs& A, float* jac, float* mm, hipStream_t s) {
     if (A.na <= 0) return hipSuccess;
-    if (!A.fixed_base || A.nl > MG_MAX_LINKS || A.ndof > JG) return hipErrorNotSupported;
+    if (A.nl > MG_MAX_LINKS || A.ndof + (A.fixed_base ? 0 : 6) > JG) return hipErrorNotSupported;
     hipLaunchKernelGGL(k_artic_jac_mm_g, dim3((A.na + JEPW - 1) / JEPW), dim3(64), 0, s, A, jac, mm);
     return hipGetLastError();
 }

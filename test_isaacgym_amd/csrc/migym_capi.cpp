@@ -971,10 +971,11 @@ static int refresh_jac_mm(mg_sim* s, int32_t tmpl, float* jdst, float* mdst, int
     for (const ArticGroup& x : s->groups)
         if (x.tmpl == tmpl) g = &x;
     if (!g) return fail(MG_ERR_ARG, "no articulation template %d", tmpl);
-    if (!g->fixed_base) return fail(MG_ERR_UNSUPPORTED, "jacobian / mass matrix of floating-base articulations");
+    const int nc = g->ndof + (g->fixed_base ? 0 : 6);
+    if (nc > 16) return fail(MG_ERR_UNSUPPORTED, "jacobian / mass matrix of more than 16 generalized velocities");
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
-    const size_t jper = (size_t)(g->nl - 1) * 6 * g->ndof, mper = (size_t)g->ndof * g->ndof;
+    const size_t jper = (size_t)(g->nl - (g->fixed_base ? 1 : 0)) * 6 * nc, mper = (size_t)nc * nc;
     const size_t jtot = jdst ? jper * g->count : 0, mtot = mdst ? mper * g->count : 0;
     float* jout = jdst;
     float* mout = mdst;

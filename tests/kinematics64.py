@@ -1,4 +1,4 @@
-"""float64 reference kinematics for fixed-base articulations (test helper).
+"""float64 reference kinematics for articulations (test helper).
 
 Independent of the engine's spatial-algebra code: forward kinematics by
 composing joint transforms, geometric Jacobians, and the joint-space mass matrix
@@ -88,5 +88,40 @@ class Articulation:
             Rl = Rs[l] @ qmat(iq)
             Iw = Rl @ Ip @ Rl.T
             J = self.point_jacobian(ps, zs, l, ps[l] + Rs[l] @ com)
+            M += m * J[0:3].T @ J[0:3] + J[3:6].T @ Iw @ J[3:6]
+        return M
+
+
+    # ---- floating base: 6 root columns first — root linear velocity of the
+    # base-link origin x0 (world xyz), then root angular velocity (world xyz) —
+    # then the DOFs (the layout of mg_refresh_jacobian for a floating base)
+    def point_jacobian_fb(self, ps, zs, l, pt):
+        """(6, 6 + D) Jacobian of world point pt fixed to link l."""
+        J = np.zeros((6, 6 + self.D))
+        J[0:3, 0:3] = np.eye(3)
+        r = pt - ps[0]
+        for k in range(3):
+            e = np.eye(3)[k]
+            J[0:3, 3 + k] = np.cross(e, r)
+            J[3:6, 3 + k] = e
+        J[:, 6:] = self.point_jacobian(ps, zs, l, pt)
+        return J
+
+    def jacobian_fb(self, base_pose, q):
+        """(L, 6, 6 + D): every link origin, the root link included."""
+        ps, Rs, zs = self.fk(base_pose, q)
+        return np.stack([self.point_jacobian_fb(ps, zs, l, ps[l]) for l in range(self.L)])
+
+    def mass_matrix_fb(self, base_pose, q, first_body):
+        """(6 + D, 6 + D) inertia in the same generalized velocities (no armature)."""
+        ps, Rs, zs = self.fk(base_pose, q)
+        M = np.zeros((6 + self.D, 6 + self.D))
+        for l in range(self.L):
+            mrow = self.A["body_mass"][first_body + l].astype(np.float64)
+            m, com, iq, invI = mrow[11], mrow[8:11], mrow[4:8], mrow[1:4]
+            Ip = np.diag([1.0 / x if x > 0 else 0.0 for x in invI])
+            Rl = Rs[l] @ qmat(iq)
+            Iw = Rl @ Ip @ Rl.T
+            J = self.point_jacobian_fb(ps, zs, l, ps[l] + Rs[l] @ com)
             M += m * J[0:3].T @ J[0:3] + J[3:6].T @ Iw @ J[3:6]
         return M

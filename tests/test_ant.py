@@ -217,3 +217,49 @@ def test_ant_parity_gpu(gym):
     assert np.array_equal(ncf.cpu().numpy(), cf)
     assert np.all(np.isfinite(got))
     assert np.abs(gd[:, 1]).max() > 0.1                       # the legs moved
+
+
+@pytest.mark.gpu
+def test_floating_base_jacobian_mass_matrix_float64(gym):
+    """acquire_jacobian_tensor / acquire_mass_matrix_tensor of the floating-base
+    ant (examples/apply_forces.py:67's nv_ant.xml): (N, 9, 6, 14) and (N, 14, 14),
+    the 6 root columns (base-origin linear velocity, then angular velocity) before
+    the 8 DOFs, at random root poses and joint angles — against float64 textbook
+    kinematics (tests/kinematics64.py: sum of m Jv^T Jv + Jw^T I Jw over link COM
+    Jacobians), rtol 1e-4."""
+    import kinematics64 as K
+    n = 16
+    sim, info = scenes.ant_scene(gym, n)
+    gym.prepare_sim(sim)
+    jac = gymtorch.wrap_tensor(gym.acquire_jacobian_tensor(sim, "actor"))
+    mm = gymtorch.wrap_tensor(gym.acquire_mass_matrix_tensor(sim, "actor"))
+    assert tuple(jac.shape) == (n, 9, 6, 14) and tuple(mm.shape) == (n, 14, 14)
+    A = sim.model_arrays
+    rng = np.random.RandomState(3)
+    props = A["dof_props"][:8]
+    lo, hi = props[:, 5], props[:, 6]
+    q = (lo + (hi - lo) * rng.uniform(0.1, 0.9, (n, 8))).astype(np.float32)
+    ds = torch.zeros((8 * n, 2), dtype=torch.float32, device="cuda:0")
+    ds[:, 0] = torch.from_numpy(q.reshape(-1)).cuda()
+    gym.set_dof_state_tensor(sim, gymtorch.unwrap_tensor(ds))
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    gym.refresh_actor_root_state_tensor(sim)
+    quat = rng.normal(size=(n, 4))
+    quat /= np.linalg.norm(quat, axis=1, keepdims=True)
+    root[:, 3:7] = torch.from_numpy(quat.astype(np.float32)).cuda()
+    root[:, 0:3] += torch.from_numpy(rng.uniform(-0.5, 0.5, (n, 3)).astype(np.float32)).cuda()
+    gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+    gym.refresh_jacobian_tensors(sim)
+    gym.refresh_mass_matrix_tensors(sim)
+    gym.refresh_actor_root_state_tensor(sim)
+    art = K.Articulation(A, 0)
+    J, M, R = jac.cpu().numpy(), mm.cpu().numpy(), root.cpu().numpy()
+    for e in range(n):
+        fb = int(A["artic_i"][e, 0])
+        base = R[e, 0:7].astype(np.float64)
+        Jr = art.jacobian_fb(base, q[e].astype(np.float64))
+        Mr = art.mass_matrix_fb(base, q[e].astype(np.float64), fb)
+        assert np.allclose(J[e], Jr, rtol=1e-4, atol=1e-5), np.abs(J[e] - Jr).max()
+        assert np.allclose(M[e], Mr, rtol=1e-4, atol=1e-4), np.abs(M[e] - Mr).max()
+        assert np.allclose(M[e], M[e].T, atol=1e-5)
+    gym.destroy_sim(sim)
