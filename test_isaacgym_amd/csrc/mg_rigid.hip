@@ -53,6 +53,7 @@ __device__ __forceinline__ V3 fmad3(V3 v, V3 d, float s) {
     return v3(fmaf(d.x, s, v.x), fmaf(d.y, s, v.y), fmaf(d.z, s, v.z));
 }
 struct BasisGen {
+    static constexpr bool kPacked = false;
     V3 n, t1, t2;
     __device__ __forceinline__ float dn(V3 v) const { return vdot(n, v); }
     __device__ __forceinline__ float d1(V3 v) const { return vdot(t1, v); }
@@ -75,6 +76,7 @@ struct BasisGen {
 };
 // n = (0,0,1), t1 = (0,1,0), t2 = (-1,0,0)
 struct BasisZ {
+    static constexpr bool kPacked = true;   // tgs_z applies (rigid_body1<..., PACK>)
     __device__ __forceinline__ float dn(V3 v) const { return v.z; }
     __device__ __forceinline__ float d1(V3 v) const { return v.y; }
     __device__ __forceinline__ float d2(V3 v) const { return -v.x; }
@@ -444,11 +446,27 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
 // effective masses (kn = kt1 = kt2 = 0), so every row of it computes
 // ln = max(0 + 0 (tgt - vn), 0) = 0 and applies a zero impulse; its friction
 // limit mu ln is 0. Friction and restitution are per body (one shape).
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk2(float a, float b) {
+    f2 r;
+    r.x = a;
+    r.y = b;
+    return r;
+}
+__device__ __forceinline__ f2 bc2(float a) { return pk2(a, a); }
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 struct Slot1 {
     V3 r;
     float s0, kn, kt1, kt2, ln, lt1, lt2, vn0;
-    V3 In, I1, I2;       // Iw (r x n), Iw (r x t1), Iw (r x t2)
+    // Iw (r x n), Iw (r x t1), Iw (r x t2) as register pairs (x, y) + z; InZ
+    // pairs In.z with 1/m (tgs_z's Z = (w.z, v.z) update)
+    f2 InW, InZ, I1W, I2W;
+    float I1z, I2z;
 };
+__device__ __forceinline__ V3 slot_in(const Slot1& c) { return v3(c.InW.x, c.InW.y, c.InZ.x); }
+__device__ __forceinline__ V3 slot_i1(const Slot1& c) { return v3(c.I1W.x, c.I1W.y, c.I1z); }
+__device__ __forceinline__ V3 slot_i2(const Slot1& c) { return v3(c.I2W.x, c.I2W.y, c.I2z); }
 
 template <class B>
 __device__ __forceinline__ void row_normal1(const B& G, Slot1& c, V3& v, V3& w, float invm, float tgt) {
@@ -457,7 +475,7 @@ __device__ __forceinline__ void row_normal1(const B& G, Slot1& c, V3& v, V3& w, 
     const float dl = nl - c.ln;
     c.ln = nl;
     v = G.fn(v, dl, invm);
-    w = fmad3(w, c.In, dl);
+    w = fmad3(w, slot_in(c), dl);
 }
 
 template <class B>
@@ -467,17 +485,109 @@ __device__ __forceinline__ void row_friction1(const B& G, Slot1& c, V3& v, V3& w
     const float d1 = n1 - c.lt1;
     c.lt1 = n1;
     v = G.f1(v, d1, invm);
-    w = fmad3(w, c.I1, d1);
+    w = fmad3(w, slot_i1(c), d1);
     const float n2 = clamp_sym(fmaf(-c.kt2, G.v2(v, w, c.r), c.lt2), lim);
     const float d2 = n2 - c.lt2;
     c.lt2 = n2;
     v = G.f2(v, d2, invm);
-    w = fmad3(w, c.I2, d2);
+    w = fmad3(w, slot_i2(c), d2);
+}
+
+// ---- +Z ground: the solver on packed f32 pairs -------------------------------
+// The same rows as row_normal1 / row_friction1 with BasisZ, but the velocity
+// state lives in register pairs W = (w.x, w.y), Z = (w.z, v.z), V = (v.x, v.y)
+// (and the motion delta in DW = (dth.x, dth.y), DZ = (dth.z, dx.z), DV = (dx.x,
+// dx.y)), so one v_pk_fma_f32 applies two of a row's impulse updates, and the
+// separations of two slots are evaluated by one packed instruction chain. Every
+// component is the same correctly rounded fma / add / mul as the scalar form
+// (a packed op is two independent IEEE ops), so the result is bit-identical to
+// row_normal1 / row_friction1 and to the oracle; only the issue count drops
+// (large launches are VALU-issue bound: DESIGN.md §3.2).
+
+__device__ __forceinline__ void tgs_z(const MgStep& P, Slot1 (&sl)[4], V3& v, V3& w, V3& dx, V3& dth, float invm,
+                                      float mu, float e) {
+    f2 W = pk2(w.x, w.y), Z = pk2(w.z, v.z), V = pk2(v.x, v.y);
+    f2 DW = pk2(dth.x, dth.y), DZ = pk2(dth.z, dx.z), DV = pk2(dx.x, dx.y);
+    f2 S0[2], RY[2], NRX[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        S0[h] = pk2(sl[2 * h].s0, sl[2 * h + 1].s0);
+        RY[h] = pk2(sl[2 * h].r.y, sl[2 * h + 1].r.y);
+        NRX[h] = pk2(-sl[2 * h].r.x, -sl[2 * h + 1].r.x);
+    }
+    // separations of slots (2h, 2h+1): s0 + dx.z + dth.x r.y - dth.y r.x (BasisZ::ps)
+    auto sep = [&](int h) {
+        f2 a = S0[h] + bc2(DZ.y);
+        a = pfma(bc2(DW.x), RY[h], a);
+        return pfma(bc2(DW.y), NRX[h], a);
+    };
+    auto normal = [&](int j, float tgt) {
+        const float nrx = (j & 1) ? NRX[j >> 1].y : NRX[j >> 1].x;
+        const float ry = (j & 1) ? RY[j >> 1].y : RY[j >> 1].x;
+        const float vn = fmaf(W.y, nrx, fmaf(W.x, ry, Z.y));
+        const float nl = fmaxf(fmaf(sl[j].kn, tgt - vn, sl[j].ln), 0.0f);
+        const float dl = nl - sl[j].ln;
+        sl[j].ln = nl;
+        W = pfma(sl[j].InW, bc2(dl), W);
+        Z = pfma(sl[j].InZ, bc2(dl), Z);
+    };
+    auto friction = [&](int j) {
+        const float rx = sl[j].r.x, ry = sl[j].r.y, nrz = -sl[j].r.z;
+        const float lim = mu * sl[j].ln;
+        const float n1 = clamp_sym(fmaf(-sl[j].kt1, fmaf(Z.x, rx, fmaf(W.x, nrz, V.y)), sl[j].lt1), lim);
+        const float d1 = n1 - sl[j].lt1;
+        sl[j].lt1 = n1;
+        V.y = fmaf(d1, invm, V.y);
+        W = pfma(sl[j].I1W, bc2(d1), W);
+        Z.x = fmaf(sl[j].I1z, d1, Z.x);
+        const float n2 = clamp_sym(fmaf(-sl[j].kt2, fmaf(Z.x, ry, fmaf(W.y, nrz, -V.x)), sl[j].lt2), lim);
+        const float d2 = n2 - sl[j].lt2;
+        sl[j].lt2 = n2;
+        V.x = fmaf(-d2, invm, V.x);
+        W = pfma(sl[j].I2W, bc2(d2), W);
+        Z.x = fmaf(sl[j].I2z, d2, Z.x);
+    };
+    const f2 nsub = bc2(-P.inv_sub), psub = bc2(P.sub);
+    auto pos_iter = [&]() {
+        const f2 t0 = sep(0) * nsub, t1 = sep(1) * nsub;   // -s / sub of each slot
+        normal(0, fminf(t0.x, P.max_depen));
+        normal(1, fminf(t0.y, P.max_depen));
+        normal(2, fminf(t1.x, P.max_depen));
+        normal(3, fminf(t1.y, P.max_depen));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) friction(j);
+        DV = pfma(V, psub, DV);
+        DW = pfma(W, psub, DW);
+        DZ = pfma(Z, psub, DZ);
+    };
+    int it = 0;
+    for (; it + 1 < P.npos; it += 2) {
+        pos_iter();
+        pos_iter();
+    }
+    if (it < P.npos) pos_iter();
+    if (P.nvel > 0) {
+        const f2 s01 = sep(0), s23 = sep(1);
+        const float sj[4] = {s01.x, s01.y, s23.x, s23.y};
+        float tg[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tg[j] = vel_target(P, sj[j], e, sl[j].vn0);
+        for (int it = 0; it < P.nvel; ++it) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) normal(j, tg[j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) friction(j);
+        }
+    }
+    v = v3(V.x, V.y, Z.y);
+    w = v3(W.x, W.y, Z.x);
+    dx = v3(DV.x, DV.y, DZ.y);
+    dth = v3(DW.x, DW.y, DZ.x);
 }
 
 // T: this body's compact template record (MG_TREC_N floats: MG_TBODY_F_N
 // template floats, then the shape record; shape type < 0 when it has none).
-template <class B>
+template <bool PACK, class B>
 __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const float* T, V3& x, Q4& q, V3& v,
                                             V3& w, V3& fsum, float invm, V3 invI, Q4 iq, V3 com, V3 fext,
                                             V3 text, const float* hulls) {
@@ -485,10 +595,11 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
     // the shape record in registers: read from LDS once (one wait), not per substep
     float sh[MG_SHAPE_STRIDE];
 #pragma unroll
-    for (int k = 0; k < 13; ++k) sh[k] = T[MG_TBODY_F_N + k];
+    for (int k = 0; k < 14; ++k) sh[k] = T[MG_TBODY_F_N + k];
 #pragma unroll
-    for (int k = 13; k < MG_SHAPE_STRIDE; ++k) sh[k] = 0.0f;
+    for (int k = 14; k < MG_SHAPE_STRIDE; ++k) sh[k] = 0.0f;
     const bool has_shape = P.has_ground && sh[0] >= 0.0f;
+    const float rho = sh[13];   // bounding radius about the body origin (< 0: none)
     const float h = P.h;
     const float lin_keep = 1.0f - fminf(lin_damp * h, 1.0f);
     const float ang_keep = 1.0f - fminf(ang_damp * h, 1.0f);
@@ -524,7 +635,12 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
             sl[j].r = v3(0.0f, 0.0f, 0.0f);
             sl[j].s0 = 0.0f;
         }
-        if (has_shape)
+        // a body clearing the plane by more than its bounding radius (plus a
+        // rounding margin far above the candidates' own error) has no candidate
+        // within contact_offset: a wave of only such bodies skips the search
+        const float clear = G.dn(x) + P.pd;
+        const bool far = rho >= 0.0f && clear - rho > P.contact_offset + 1e-3f * (1.0f + fabsf(clear) + rho);
+        if (__any(has_shape && !far) && has_shape)
             shape_candidates(G, P, sh, q, x, hulls, [&](int k, V3 p, float sep, float, float) {
                 if (sep < P.contact_offset) {
                     on[k] = true;
@@ -543,38 +659,47 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const V3 rn = G.cn(sl[j].r), r1 = G.c1(sl[j].r), r2 = G.c2(sl[j].r);
-                sl[j].In = symmul(Iw, rn);
-                sl[j].I1 = symmul(Iw, r1);
-                sl[j].I2 = symmul(Iw, r2);
-                sl[j].kn = on[j] ? 1.0f / (invm + vdot(rn, sl[j].In)) : 0.0f;
-                sl[j].kt1 = on[j] ? 1.0f / (invm + vdot(r1, sl[j].I1)) : 0.0f;
-                sl[j].kt2 = on[j] ? 1.0f / (invm + vdot(r2, sl[j].I2)) : 0.0f;
+                const V3 In = symmul(Iw, rn), I1 = symmul(Iw, r1), I2 = symmul(Iw, r2);
+                sl[j].InW = pk2(In.x, In.y);
+                sl[j].InZ = pk2(In.z, invm);
+                sl[j].I1W = pk2(I1.x, I1.y);
+                sl[j].I2W = pk2(I2.x, I2.y);
+                sl[j].I1z = I1.z;
+                sl[j].I2z = I2.z;
+                sl[j].kn = on[j] ? 1.0f / (invm + vdot(rn, In)) : 0.0f;
+                sl[j].kt1 = on[j] ? 1.0f / (invm + vdot(r1, I1)) : 0.0f;
+                sl[j].kt2 = on[j] ? 1.0f / (invm + vdot(r2, I2)) : 0.0f;
                 sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
                 sl[j].vn0 = G.vn(v, w, sl[j].r);
             }
-            auto pos_iter = [&]() {
+            if constexpr (B::kPacked && PACK) {
+                tgs_z(P, sl, v, w, dx, dth, invm, mu, e);
+            } else {
+                auto pos_iter = [&]() {
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    row_normal1(G, sl[j], v, w, invm, pos_target(P, G.ps(sl[j].s0, dx, dth, sl[j].r)));
+                    for (int j = 0; j < 4; ++j)
+                        row_normal1(G, sl[j], v, w, invm, pos_target(P, G.ps(sl[j].s0, dx, dth, sl[j].r)));
 #pragma unroll
-                for (int j = 0; j < 4; ++j) row_friction1(G, sl[j], v, w, invm, mu);
-                dx = fmad3(dx, v, P.sub);
-                dth = fmad3(dth, w, P.sub);
-            };
-            // two iterations per trip: the accumulated impulses alternate between
-            // two register sets instead of being copied back every iteration
-            int it = 0;
-            for (; it + 1 < P.npos; it += 2) {
-                pos_iter();
-                pos_iter();
-            }
-            if (it < P.npos) pos_iter();
-            for (int it = 0; it < P.nvel; ++it) {
+                    for (int j = 0; j < 4; ++j) row_friction1(G, sl[j], v, w, invm, mu);
+                    dx = fmad3(dx, v, P.sub);
+                    dth = fmad3(dth, w, P.sub);
+                };
+                // two iterations per trip: the accumulated impulses alternate between
+                // two register sets instead of being copied back every iteration
+                int it = 0;
+                for (; it + 1 < P.npos; it += 2) {
+                    pos_iter();
+                    pos_iter();
+                }
+                if (it < P.npos) pos_iter();
+                for (int it = 0; it < P.nvel; ++it) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    row_normal1(G, sl[j], v, w, invm, vel_target(P, G.ps(sl[j].s0, dx, dth, sl[j].r), e, sl[j].vn0));
+                    for (int j = 0; j < 4; ++j)
+                        row_normal1(G, sl[j], v, w, invm,
+                                    vel_target(P, G.ps(sl[j].s0, dx, dth, sl[j].r), e, sl[j].vn0));
 #pragma unroll
-                for (int j = 0; j < 4; ++j) row_friction1(G, sl[j], v, w, invm, mu);
+                    for (int j = 0; j < 4; ++j) row_friction1(G, sl[j], v, w, invm, mu);
+                }
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -601,10 +726,10 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
 // large launches (the Gauss-Seidel chains are latency-bound: more resident
 // waves, not more lanes, fill the SIMD); free of scratch at that budget. The
 // general ground basis needs more registers: two waves.
-template <bool UPZ, bool LDS_T>
+template <bool UPZ, bool LDS_T, bool WIDE>
 __global__ void __launch_bounds__(64, UPZ ? 3 : 2) k_rigid_step1(MgStep P, MgRigidArgs A) {
     extern __shared__ float s_trec[];
-    const int i = blockIdx.x * 64 + threadIdx.x;
+    const int i = (WIDE ? gridDim.x - 1 - blockIdx.x : blockIdx.x) * 64 + threadIdx.x;
     const bool live = i < A.nf;
     const int b = A.free_ids ? A.free_ids[live ? i : A.nf - 1] : (live ? i : A.nf - 1);
     const int nb = A.nb;
@@ -635,13 +760,13 @@ __global__ void __launch_bounds__(64, UPZ ? 3 : 2) k_rigid_step1(MgStep P, MgRig
     }
     V3 fsum = v3(0.0f, 0.0f, 0.0f);
     if constexpr (UPZ) {
-        rigid_body1(BasisZ{}, P, T, x, q, v, w, fsum, invm, invI, iq, com, fext, text, A.hulls);
+        rigid_body1<!WIDE>(BasisZ{}, P, T, x, q, v, w, fsum, invm, invI, iq, com, fext, text, A.hulls);
     } else {
         BasisGen G;
         G.n = v3(P.n[0], P.n[1], P.n[2]);
         G.t1 = v3(P.t1[0], P.t1[1], P.t1[2]);
         G.t2 = v3(P.t2[0], P.t2[1], P.t2[2]);
-        rigid_body1(G, P, T, x, q, v, w, fsum, invm, invI, iq, com, fext, text, A.hulls);
+        rigid_body1<!WIDE>(G, P, T, x, q, v, w, fsum, invm, invI, iq, com, fext, text, A.hulls);
     }
     if (!live) return;
     // the output addresses are recomputed here (an opaque copy of the slot)
@@ -681,6 +806,18 @@ bool mg_step_is_upz(const MgStep& P) {
            P.t1[2] == 0.0f && P.t2[0] == -1.0f && P.t2[1] == 0.0f && P.t2[2] == 0.0f;
 }
 
+static int mg_cu_count() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cus[dev] <= 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
 // A.free_ids lists the single-shape bodies first (A.nf1 of them), then the
 // multi-shape ones; each group is its own launch.
 hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream_t s) {
@@ -700,14 +837,26 @@ hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream
     }
     if (A1.nf > 0) {
         const int blocks = (A1.nf + 63) / 64;
+        // wide: more waves than one resident round (4 SIMDs x 3 or 2 waves per
+        // CU). Such a launch is issue-bound, not latency-bound: it dispatches
+        // longest-first (back to front: the free-body order, migym_capi.cpp) and
+        // solves with the scalar rows (tgs_z's packed pairs save latency, not
+        // issue slots: tools/gpu_ab_var.sh).
+        const bool wide = blocks > mg_cu_count() * 4 * (upz ? 3 : 2);
         const size_t lds = (size_t)A.ntb * MG_TREC_N * sizeof(float);
+#define MG_K1(U, L) \
+    do { \
+        if (wide) MG_LAUNCH((k_rigid_step1<U, L, true>), dim3(blocks), dim3(64), L ? lds : 0, s, P, A1); \
+        else MG_LAUNCH((k_rigid_step1<U, L, false>), dim3(blocks), dim3(64), L ? lds : 0, s, P, A1); \
+    } while (0)
         if (lds <= MG_TREC_LDS_MAX) {
-            if (upz) MG_LAUNCH((k_rigid_step1<true, true>), dim3(blocks), dim3(64), lds, s, P, A1);
-            else MG_LAUNCH((k_rigid_step1<false, true>), dim3(blocks), dim3(64), lds, s, P, A1);
+            if (upz) MG_K1(true, true);
+            else MG_K1(false, true);
         } else {
-            if (upz) MG_LAUNCH((k_rigid_step1<true, false>), dim3(blocks), dim3(64), 0, s, P, A1);
-            else MG_LAUNCH((k_rigid_step1<false, false>), dim3(blocks), dim3(64), 0, s, P, A1);
+            if (upz) MG_K1(true, false);
+            else MG_K1(false, false);
         }
+#undef MG_K1
     }
     if (A2.nf > 0) {
         const int blocks = (A2.nf + 63) / 64;

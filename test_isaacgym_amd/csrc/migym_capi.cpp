@@ -528,16 +528,43 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
 
     // free bodies ordered by template body (stable): bodies of one kind share
     // waves, so e.g. the servo scene's airborne UAVs and grounded vehicles do
-    // not interleave lane by lane (results do not depend on the order). Free
-    // bodies of coupled envs come last (the per-env kernel reads them).
+    // not interleave lane by lane (results do not depend on the order).
+    // Templates whose instances start farthest from the ground plane come
+    // first: a launch larger than one resident round dispatches the array back
+    // to front (mg_launch_rigid_step), i.e. the likely-in-contact (long) waves
+    // first and the airborne (short) ones last, filling the last round's tail.
+    // Free bodies of coupled envs come last (the per-env kernel reads them).
     std::vector<int> free_ids, free_cpl;
     for (int b = 0; b < nb; ++b)
         if (m->body_kind[b] == MG_BODY_FREE) (coupled_body[b] ? free_cpl : free_ids).push_back(b);
     auto nshapes = [m](int b) { return m->tmpl_body_i[m->body_tmpl[b] * MG_TBODY_I_N + 1]; };
+    std::vector<double> clear_sum(m->num_tmpl_bodies, 0.0);
+    std::vector<int> clear_n(m->num_tmpl_bodies, 0);
+    {
+        const mg_sim_params& p = s->params;
+        float gn[3] = {0.0f, 0.0f, 0.0f};
+        float gd = 0.0f;
+        if (p.has_ground) {
+            for (int k = 0; k < 3; ++k) gn[k] = p.ground_normal[k];
+            gd = p.ground_distance;
+        } else {
+            gn[p.up_axis == 0 ? 1 : 2] = 1.0f;
+        }
+        for (int b : free_ids) {
+            const float* x = m->body_state0 + (size_t)b * MG_STATE_N;
+            clear_sum[m->body_tmpl[b]] += (double)gn[0] * x[0] + (double)gn[1] * x[1] + (double)gn[2] * x[2] + gd;
+            clear_n[m->body_tmpl[b]] += 1;
+        }
+    }
+    auto clearance = [&](int t) { return clear_n[t] ? clear_sum[t] / clear_n[t] : 0.0; };
     std::stable_sort(free_ids.begin(), free_ids.end(), [&](int a, int b) {
         const bool ma = nshapes(a) > 1, mb = nshapes(b) > 1;   // single-shape bodies first
         if (ma != mb) return !ma;
-        return m->body_tmpl[a] < m->body_tmpl[b];
+        const int ta = m->body_tmpl[a], tb = m->body_tmpl[b];
+        if (ta == tb) return false;
+        const double ca = clearance(ta), cb = clearance(tb);
+        if (ca != cb) return ca > cb;
+        return ta < tb;
     });
     s->nf1 = 0;
     for (int b : free_ids) s->nf1 += nshapes(b) <= 1 ? 1 : 0;
@@ -682,10 +709,25 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
             float* r = &trec[(size_t)t * MG_TREC_N];
             std::memcpy(r, m->tmpl_body_f + (size_t)t * MG_TBODY_F_N, MG_TBODY_F_N * sizeof(float));
             const int s0 = m->tmpl_body_i[t * MG_TBODY_I_N + 0], sc = m->tmpl_body_i[t * MG_TBODY_I_N + 1];
-            if (sc > 0)
-                std::memcpy(r + MG_TBODY_F_N, m->shapes + (size_t)s0 * MG_SHAPE_STRIDE, MG_SHAPE_STRIDE * sizeof(float));
-            else
+            if (sc > 0) {
+                const float* sr = m->shapes + (size_t)s0 * MG_SHAPE_STRIDE;
+                std::memcpy(r + MG_TBODY_F_N, sr, MG_SHAPE_STRIDE * sizeof(float));
+                // pad[0] of the copy: bounding radius of the shape about the body
+                // origin (k_rigid_step1 skips the candidates of a wave whose bodies
+                // all clear the ground by more than it); -1: unknown, never skipped
+                double ext = -1.0;
+                switch ((int)sr[0]) {
+                    case MG_SHAPE_SPHERE: ext = sr[1]; break;
+                    case MG_SHAPE_BOX: ext = std::sqrt((double)sr[1] * sr[1] + (double)sr[2] * sr[2] + (double)sr[3] * sr[3]); break;
+                    case MG_SHAPE_CAPSULE: ext = (double)sr[1] + sr[2]; break;
+                    case MG_SHAPE_CONVEX: ext = sr[1]; break;
+                    default: break;
+                }
+                const double po = std::sqrt((double)sr[4] * sr[4] + (double)sr[5] * sr[5] + (double)sr[6] * sr[6]);
+                r[MG_TBODY_F_N + 13] = (ext >= 0.0 && std::isfinite(ext + po)) ? (float)((ext + po) * (1.0 + 1e-6)) : -1.0f;
+            } else {
                 r[MG_TBODY_F_N] = -1.0f;
+            }
         }
         HIP_TRY(h2d(s->d_trec, trec.data(), trec.size() * sizeof(float)));
     }

@@ -66,6 +66,32 @@ def test_servo_single_step_parity(gym):
     assert exact, "within tolerance but not bit-exact (max |diff| %g)" % worst
 
 
+def test_servo_large_launch_step_parity(gym):
+    """131072 envs = 262144 single-shape bodies = 4096 waves, more than one
+    resident round of k_rigid_step1, so the launch dispatches back to front
+    (mg_launch_rigid_step): still bit for bit the oracle's step."""
+    n, steps = 131072, 2
+    sim, _ = scenes.servo_scene(gym, n)
+    gym.prepare_sim(sim)
+    root, rb, _, ncf = _tensors(gym, sim)
+    acts = scenes.servo_actions(n, steps, DEV, seed=3)
+    p, m = sim.mg_params(), sim.mg_model()
+    gym.refresh_actor_root_state_tensor(sim)
+    for k in range(steps):
+        root[:, 3:10] = acts[k]
+        assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.refresh_rigid_body_state_tensor(sim)
+        inp = rb.cpu().numpy().copy()
+        gym.simulate(sim)
+        gym.fetch_results(sim, True)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_net_contact_force_tensor(sim)
+        got = rb.cpu().numpy()
+        cf = oracle.step(p, m, inp, np.zeros((0, 2), np.float32))
+        assert np.array_equal(got, inp), "step %d: max |diff| %g" % (k, np.abs(got - inp).max())
+        assert np.array_equal(ncf.cpu().numpy(), cf)
+
+
 def test_servo_trajectory_bitexact(gym):
     """A 120-frame rollout with a random root teleport every frame, device vs
     oracle from the same initial state: no re-synchronisation."""
