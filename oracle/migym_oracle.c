@@ -172,9 +172,6 @@ static step_t make_step_(const mg_sim_params* p) {
  * written out explicitly (as the device's BasisZ specialisation). */
 typedef struct { int upz; v3_t n, t1, t2; } basis_t;
 static float b_dn(const basis_t* B, v3_t v) { return B->upz ? v.z : dot3(B->n, v); }
-static v3_t b_cn(const basis_t* B, v3_t r) { return B->upz ? V(r.y, -r.x, 0.0f) : cross3(r, B->n); }
-static v3_t b_c1(const basis_t* B, v3_t r) { return B->upz ? V(-r.z, 0.0f, r.x) : cross3(r, B->t1); }
-static v3_t b_c2(const basis_t* B, v3_t r) { return B->upz ? V(0.0f, -r.z, r.y) : cross3(r, B->t2); }
 static v3_t b_addn(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x, v.y, v.z + s) : mad3(v, B->n, s); }
 static v3_t b_add1(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x, v.y + s, v.z) : mad3(v, B->t1, s); }
 static v3_t b_add2(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x - s, v.y, v.z) : mad3(v, B->t2, s); }
@@ -204,6 +201,33 @@ static v3_t b_f1(const basis_t* B, v3_t v, float dl, float invm) {
 static v3_t b_f2(const basis_t* B, v3_t v, float dl, float invm) {
     return B->upz ? V(fmaf(-dl, invm, v.x), v.y, v.z) : fmad3_(v, B->t2, dl * invm);
 }
+/* Iw (r x d) and (r x d) . Iw (r x d) per row direction; the +Z basis drops the
+ * zero component of r x d (mg_rigid.hip BasisZ iwn / iw1 / iw2 / kn / k1 / k2,
+ * symmul's term order otherwise) */
+static v3_t b_iwn(const basis_t* B, const s3_t* I, v3_t r) {
+    if (!B->upz) return symmul_(*I, cross3(r, B->n));
+    {
+        const float a = r.y, b = -r.x;
+        return V(I->xx * a + I->xy * b, I->xy * a + I->yy * b, I->xz * a + I->yz * b);
+    }
+}
+static v3_t b_iw1(const basis_t* B, const s3_t* I, v3_t r) {
+    if (!B->upz) return symmul_(*I, cross3(r, B->t1));
+    {
+        const float a = -r.z, c = r.x;
+        return V(I->xx * a + I->xz * c, I->xy * a + I->yz * c, I->xz * a + I->zz * c);
+    }
+}
+static v3_t b_iw2(const basis_t* B, const s3_t* I, v3_t r) {
+    if (!B->upz) return symmul_(*I, cross3(r, B->t2));
+    {
+        const float b = -r.z, c = r.y;
+        return V(I->xy * b + I->xz * c, I->yy * b + I->yz * c, I->yz * b + I->zz * c);
+    }
+}
+static float b_kn(const basis_t* B, v3_t r, v3_t In) { return B->upz ? r.y * In.x + -r.x * In.y : dot3(cross3(r, B->n), In); }
+static float b_k1(const basis_t* B, v3_t r, v3_t I1) { return B->upz ? -r.z * I1.x + r.x * I1.z : dot3(cross3(r, B->t1), I1); }
+static float b_k2(const basis_t* B, v3_t r, v3_t I2) { return B->upz ? -r.z * I2.y + r.y * I2.z : dot3(cross3(r, B->t2), I2); }
 
 typedef struct {
     v3_t r; float s0, mu, e, kn, kt1, kt2, ln, lt1, lt2, vn0; int on;
@@ -223,33 +247,30 @@ static float vel_target_(const step_t* P, float s, float e, float vn0) {
 }
 
 static void contact_normal(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw, float tgt) {
-    v3_t rn = b_cn(B, c->r);
     float vn = b_vn(B, *v, *w, c->r);
     float nl = fmaxf(fmaf(c->kn, tgt - vn, c->ln), 0.0f);
     float dl = nl - c->ln;
     c->ln = nl;
     *v = b_fn(B, *v, dl, invm);
-    *w = fmad3_(*w, symmul_(*Iw, rn), dl);
+    *w = fmad3_(*w, b_iwn(B, Iw, c->r), dl);
 }
 
 /* PhysX-style pyramid friction: tangent rows one after the other, each
  * accumulated impulse clamped to [-mu ln, mu ln] */
 static void contact_friction(const basis_t* B, slot_t* c, v3_t* v, v3_t* w, float invm, const s3_t* Iw) {
     const float lim = c->mu * c->ln;
-    v3_t r1 = b_c1(B, c->r), r2;
     float vt1 = b_v1(B, *v, *w, c->r), vt2, n1, n2, d1, d2;
     n1 = clamp_sym_(fmaf(-c->kt1, vt1, c->lt1), lim);
     d1 = n1 - c->lt1;
     c->lt1 = n1;
     *v = b_f1(B, *v, d1, invm);
-    *w = fmad3_(*w, symmul_(*Iw, r1), d1);
-    r2 = b_c2(B, c->r);
+    *w = fmad3_(*w, b_iw1(B, Iw, c->r), d1);
     vt2 = b_v2(B, *v, *w, c->r);
     n2 = clamp_sym_(fmaf(-c->kt2, vt2, c->lt2), lim);
     d2 = n2 - c->lt2;
     c->lt2 = n2;
     *v = b_f2(B, *v, d2, invm);
-    *w = fmad3_(*w, symmul_(*Iw, r2), d2);
+    *w = fmad3_(*w, b_iw2(B, Iw, c->r), d2);
 }
 
 /* Identity skips (mg_rigid.hip shape_pose_identity / inertia_frame / com_world
@@ -376,8 +397,10 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
         int j, it;
         v3_t dx = V(0.0f, 0.0f, 0.0f), dth = V(0.0f, 0.0f, 0.0f);
         if (tf[4] != 0.0f) v = mad3(v, V(P->g[0], P->g[1], P->g[2]), h);
-        v = mad3(v, fext, invm * h);
-        w = mad3(w, symmul_(Iw, text), h);
+        if (ext) {   /* an applied wrench this frame (the device: A.ext non-null) */
+            v = mad3(v, fext, invm * h);
+            w = mad3(w, symmul_(Iw, text), h);
+        }
         v = mul3(v, lin_keep);
         w = mul3(w, ang_keep);
         {
@@ -426,10 +449,10 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                     if (!act) { sl[j].r = V(0.0f, 0.0f, 0.0f); sl[j].s0 = 0.0f; }
                     sl[j].mu = mu; sl[j].e = e;
                     {
-                        const v3_t rn = b_cn(&B, sl[j].r), r1 = b_c1(&B, sl[j].r), r2 = b_c2(&B, sl[j].r);
-                        sl[j].kn = act ? 1.0f / (invm + dot3(rn, symmul_(Iw, rn))) : 0.0f;
-                        sl[j].kt1 = act ? 1.0f / (invm + dot3(r1, symmul_(Iw, r1))) : 0.0f;
-                        sl[j].kt2 = act ? 1.0f / (invm + dot3(r2, symmul_(Iw, r2))) : 0.0f;
+                        const v3_t r = sl[j].r;
+                        sl[j].kn = act ? 1.0f / (invm + b_kn(&B, r, b_iwn(&B, &Iw, r))) : 0.0f;
+                        sl[j].kt1 = act ? 1.0f / (invm + b_k1(&B, r, b_iw1(&B, &Iw, r))) : 0.0f;
+                        sl[j].kt2 = act ? 1.0f / (invm + b_k2(&B, r, b_iw2(&B, &Iw, r))) : 0.0f;
                     }
                     sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
                     sl[j].vn0 = b_vn(&B, v, w, sl[j].r);
@@ -440,10 +463,10 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
         for (j = 0; j < OR_MAXC; ++j) {
             if (!sl[j].on || nsh <= 1) continue;
             {
-                const v3_t rn = b_cn(&B, sl[j].r), r1 = b_c1(&B, sl[j].r), r2 = b_c2(&B, sl[j].r);
-                sl[j].kn = 1.0f / (invm + dot3(rn, symmul_(Iw, rn)));
-                sl[j].kt1 = 1.0f / (invm + dot3(r1, symmul_(Iw, r1)));
-                sl[j].kt2 = 1.0f / (invm + dot3(r2, symmul_(Iw, r2)));
+                const v3_t r = sl[j].r;
+                sl[j].kn = 1.0f / (invm + b_kn(&B, r, b_iwn(&B, &Iw, r)));
+                sl[j].kt1 = 1.0f / (invm + b_k1(&B, r, b_iw1(&B, &Iw, r)));
+                sl[j].kt2 = 1.0f / (invm + b_k2(&B, r, b_iw2(&B, &Iw, r)));
                 sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
                 sl[j].vn0 = b_vn(&B, v, w, sl[j].r);
             }

@@ -73,6 +73,13 @@ struct BasisGen {
     __device__ __forceinline__ V3 fn(V3 v, float dl, float invm) const { return fmad3(v, n, dl * invm); }
     __device__ __forceinline__ V3 f1(V3 v, float dl, float invm) const { return fmad3(v, t1, dl * invm); }
     __device__ __forceinline__ V3 f2(V3 v, float dl, float invm) const { return fmad3(v, t2, dl * invm); }
+    // Iw (r x d) and (r x d) . Iw (r x d) of the three row directions
+    __device__ __forceinline__ V3 iwn(const S3& I, V3 r) const { return symmul(I, cn(r)); }
+    __device__ __forceinline__ V3 iw1(const S3& I, V3 r) const { return symmul(I, c1(r)); }
+    __device__ __forceinline__ V3 iw2(const S3& I, V3 r) const { return symmul(I, c2(r)); }
+    __device__ __forceinline__ float kn(V3 r, V3 In) const { return vdot(cn(r), In); }
+    __device__ __forceinline__ float k1(V3 r, V3 I1) const { return vdot(c1(r), I1); }
+    __device__ __forceinline__ float k2(V3 r, V3 I2) const { return vdot(c2(r), I2); }
 };
 // n = (0,0,1), t1 = (0,1,0), t2 = (-1,0,0)
 struct BasisZ {
@@ -96,6 +103,22 @@ struct BasisZ {
     __device__ __forceinline__ V3 fn(V3 v, float dl, float invm) const { return v3(v.x, v.y, fmaf(dl, invm, v.z)); }
     __device__ __forceinline__ V3 f1(V3 v, float dl, float invm) const { return v3(v.x, fmaf(dl, invm, v.y), v.z); }
     __device__ __forceinline__ V3 f2(V3 v, float dl, float invm) const { return v3(fmaf(-dl, invm, v.x), v.y, v.z); }
+    // symmul / vdot with the zero component of r x d dropped (symmul's term order)
+    __device__ __forceinline__ V3 iwn(const S3& I, V3 r) const {
+        const float a = r.y, b = -r.x;   // r x n = (a, b, 0)
+        return v3(I.xx * a + I.xy * b, I.xy * a + I.yy * b, I.xz * a + I.yz * b);
+    }
+    __device__ __forceinline__ V3 iw1(const S3& I, V3 r) const {
+        const float a = -r.z, c = r.x;   // r x t1 = (a, 0, c)
+        return v3(I.xx * a + I.xz * c, I.xy * a + I.yz * c, I.xz * a + I.zz * c);
+    }
+    __device__ __forceinline__ V3 iw2(const S3& I, V3 r) const {
+        const float b = -r.z, c = r.y;   // r x t2 = (0, b, c)
+        return v3(I.xy * b + I.xz * c, I.yy * b + I.yz * c, I.yz * b + I.zz * c);
+    }
+    __device__ __forceinline__ float kn(V3 r, V3 In) const { return r.y * In.x + -r.x * In.y; }
+    __device__ __forceinline__ float k1(V3 r, V3 I1) const { return -r.z * I1.x + r.x * I1.z; }
+    __device__ __forceinline__ float k2(V3 r, V3 I2) const { return -r.z * I2.y + r.y * I2.z; }
 };
 
 // clamp x to [-lim, lim] (lim >= 0): the median of three, one instruction
@@ -126,7 +149,7 @@ __device__ __forceinline__ void contact_normal(const B& G, Slot& c, V3& v, V3& w
     const float dl = nl - c.ln;
     c.ln = nl;
     v = G.fn(v, dl, invm);
-    w = fmad3(w, CACHE ? c.In : symmul(Iw, G.cn(c.r)), dl);
+    w = fmad3(w, CACHE ? c.In : G.iwn(Iw, c.r), dl);
 }
 
 // Coulomb friction, PhysX-style pyramid: the two tangent rows are solved one
@@ -141,13 +164,13 @@ __device__ __forceinline__ void contact_friction(const B& G, Slot& c, V3& v, V3&
     const float d1 = n1 - c.lt1;
     c.lt1 = n1;
     v = G.f1(v, d1, invm);
-    w = fmad3(w, CACHE ? c.I1 : symmul(Iw, G.c1(c.r)), d1);
+    w = fmad3(w, CACHE ? c.I1 : G.iw1(Iw, c.r), d1);
     const float vt2 = G.v2(v, w, c.r);
     const float n2 = clamp_sym(fmaf(-c.kt2, vt2, c.lt2), lim);
     const float d2 = n2 - c.lt2;
     c.lt2 = n2;
     v = G.f2(v, d2, invm);
-    w = fmad3(w, CACHE ? c.I2 : symmul(Iw, G.c2(c.r)), d2);
+    w = fmad3(w, CACHE ? c.I2 : G.iw2(Iw, c.r), d2);
 }
 
 // Row targets. Position iterations: v_n >= -s / sub, capped at the maximum
@@ -321,8 +344,10 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
 
         // 1. unconstrained velocity
         if (grav_on != 0.0f) v = vmad(v, v3(P.g[0], P.g[1], P.g[2]), h);
-        v = vmad(v, fext, invm * h);
-        w = vmad(w, symmul(Iw, text), h);
+        if (A.ext) {   // applied wrench this frame (uniform; none: no update, as the oracle)
+            v = vmad(v, fext, invm * h);
+            w = vmad(w, symmul(Iw, text), h);
+        }
         v = vscale(v, lin_keep);
         w = vscale(w, ang_keep);
         {
@@ -375,14 +400,11 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
 #pragma unroll
         for (int j = 0; j < MAXC; ++j) {
             if (sl[j].on) {
-                const V3 rn = G.cn(sl[j].r);
-                const V3 r1 = G.c1(sl[j].r);
-                const V3 r2 = G.c2(sl[j].r);
-                const V3 In = symmul(Iw, rn), I1 = symmul(Iw, r1), I2 = symmul(Iw, r2);
+                const V3 In = G.iwn(Iw, sl[j].r), I1 = G.iw1(Iw, sl[j].r), I2 = G.iw2(Iw, sl[j].r);
                 if (CACHE) { sl[j].In = In; sl[j].I1 = I1; sl[j].I2 = I2; }
-                sl[j].kn = 1.0f / (invm + vdot(rn, In));
-                sl[j].kt1 = 1.0f / (invm + vdot(r1, I1));
-                sl[j].kt2 = 1.0f / (invm + vdot(r2, I2));
+                sl[j].kn = 1.0f / (invm + G.kn(sl[j].r, In));
+                sl[j].kt1 = 1.0f / (invm + G.k1(sl[j].r, I1));
+                sl[j].kt2 = 1.0f / (invm + G.k2(sl[j].r, I2));
                 sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
                 sl[j].vn0 = G.vn(v, w, sl[j].r);
             }
@@ -589,8 +611,8 @@ __device__ __forceinline__ void tgs_z(const MgStep& P, Slot1 (&sl)[4], V3& v, V3
 // template floats, then the shape record; shape type < 0 when it has none).
 template <bool PACK, class B>
 __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const float* T, V3& x, Q4& q, V3& v,
-                                            V3& w, V3& fsum, float invm, V3 invI, Q4 iq, V3 com, V3 fext,
-                                            V3 text, const float* hulls) {
+                                            V3& w, V3& fsum, float invm, V3 invI, Q4 iq, V3 com, bool has_ext,
+                                            V3 fext, V3 text, const float* hulls) {
     const float lin_damp = T[0], ang_damp = T[1], max_lv = T[2], max_av = T[3], grav_on = T[4];
     // the shape record in registers: read from LDS once (one wait), not per substep
     float sh[MG_SHAPE_STRIDE];
@@ -615,8 +637,10 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
 
         // 1. unconstrained velocity
         if (grav_on != 0.0f) v = vmad(v, v3(P.g[0], P.g[1], P.g[2]), h);
-        v = vmad(v, fext, invm * h);
-        w = vmad(w, symmul(Iw, text), h);
+        if (has_ext) {   // applied wrench this frame (uniform; none: no update, as the oracle)
+            v = vmad(v, fext, invm * h);
+            w = vmad(w, symmul(Iw, text), h);
+        }
         v = vscale(v, lin_keep);
         w = vscale(w, ang_keep);
         {
@@ -658,17 +682,16 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
             // contact constants (inactive slots: r = 0, so In = I1 = I2 = 0, k = 0)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const V3 rn = G.cn(sl[j].r), r1 = G.c1(sl[j].r), r2 = G.c2(sl[j].r);
-                const V3 In = symmul(Iw, rn), I1 = symmul(Iw, r1), I2 = symmul(Iw, r2);
+                const V3 In = G.iwn(Iw, sl[j].r), I1 = G.iw1(Iw, sl[j].r), I2 = G.iw2(Iw, sl[j].r);
                 sl[j].InW = pk2(In.x, In.y);
                 sl[j].InZ = pk2(In.z, invm);
                 sl[j].I1W = pk2(I1.x, I1.y);
                 sl[j].I2W = pk2(I2.x, I2.y);
                 sl[j].I1z = I1.z;
                 sl[j].I2z = I2.z;
-                sl[j].kn = on[j] ? 1.0f / (invm + vdot(rn, In)) : 0.0f;
-                sl[j].kt1 = on[j] ? 1.0f / (invm + vdot(r1, I1)) : 0.0f;
-                sl[j].kt2 = on[j] ? 1.0f / (invm + vdot(r2, I2)) : 0.0f;
+                sl[j].kn = on[j] ? 1.0f / (invm + G.kn(sl[j].r, In)) : 0.0f;
+                sl[j].kt1 = on[j] ? 1.0f / (invm + G.k1(sl[j].r, I1)) : 0.0f;
+                sl[j].kt2 = on[j] ? 1.0f / (invm + G.k2(sl[j].r, I2)) : 0.0f;
                 sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
                 sl[j].vn0 = G.vn(v, w, sl[j].r);
             }
@@ -760,13 +783,13 @@ __global__ void __launch_bounds__(64, UPZ ? 3 : 2) k_rigid_step1(MgStep P, MgRig
     }
     V3 fsum = v3(0.0f, 0.0f, 0.0f);
     if constexpr (UPZ) {
-        rigid_body1<!WIDE>(BasisZ{}, P, T, x, q, v, w, fsum, invm, invI, iq, com, fext, text, A.hulls);
+        rigid_body1<!WIDE>(BasisZ{}, P, T, x, q, v, w, fsum, invm, invI, iq, com, A.ext != nullptr, fext, text, A.hulls);
     } else {
         BasisGen G;
         G.n = v3(P.n[0], P.n[1], P.n[2]);
         G.t1 = v3(P.t1[0], P.t1[1], P.t1[2]);
         G.t2 = v3(P.t2[0], P.t2[1], P.t2[2]);
-        rigid_body1<!WIDE>(G, P, T, x, q, v, w, fsum, invm, invI, iq, com, fext, text, A.hulls);
+        rigid_body1<!WIDE>(G, P, T, x, q, v, w, fsum, invm, invI, iq, com, A.ext != nullptr, fext, text, A.hulls);
     }
     if (!live) return;
     // the output addresses are recomputed here (an opaque copy of the slot)
