@@ -191,7 +191,14 @@ int32_t     mg_refresh_net_contact_force(mg_sim* sim, float* dst, int32_t dst_ho
  * gym.set_actor_root_state_tensor (test10_servo_vecenv.py:456) and the
  * _indexed variant: `src` is (num_actors, 13); when `idx` is non-NULL only the
  * n_idx actor rows it lists are applied (idx is int32, host or device like src).
- * src is consumed in stream order, so the caller may reuse it right away. */
+ * src is consumed in stream order, so the caller may reuse it right away —
+ * except for the fused root set (mg_set_fusion, MG_FUSE_ROOT_SET, on by
+ * default): a device-resident, non-indexed set on a sim whose actor roots are
+ * all single-shape free bodies is read by the next mg_simulate's free-body
+ * kernel (the scatter fused into the step), or by the scatter that any earlier
+ * call reading the state issues first (refresh_*, set_rigid_body_state, an
+ * indexed or host set, the render snapshot). The caller keeps such a src alive
+ * and unmodified until then (the gymapi layer holds the tensor). */
 int32_t     mg_set_actor_root_state(mg_sim* sim, const float* src, int32_t src_host,
                                     const int32_t* idx, int32_t n_idx, void* stream);
 /* gym.set_rigid_body_state_tensor (test/test05_isaacgym_vel_batch.py:367-385):
@@ -273,6 +280,22 @@ int32_t     mg_snapshot_render_state(mg_sim* sim, void* stream);
 int32_t     mg_render_cameras(mg_sim* sim, const mg_camera* cams, int32_t n, void* stream);
 /* Duration in ms of the last mg_render_cameras launch (HIP events), -1 if none. */
 float       mg_last_render_ms(mg_sim* sim);
+
+/* ---- step fusion ------------------------------------------------------------
+ * MG_FUSE_ROOT_SET: the deferred root-state set described above.
+ * MG_FUSE_REFRESH: with targets bound by mg_bind_refresh_targets (the persistent
+ * tensors acquire_actor_root_state_tensor / acquire_rigid_body_state_tensor hand
+ * out), a root refresh into the bound root tensor also writes the bound
+ * rigid-body tensor (one gather launch for test10_servo_vecenv.py:394-395), and
+ * a rigid-body refresh into it is then served without a launch while no
+ * simulate or set has changed the state. The bound rigid-body tensor is thus
+ * refreshed no later than requested (possibly at the root refresh).
+ * mg_set_fusion returns the previous flags; both are on by default. The bound
+ * pointers must stay valid for the sim's lifetime (NULL unbinds). */
+#define MG_FUSE_ROOT_SET  1
+#define MG_FUSE_REFRESH   2
+int32_t     mg_set_fusion(mg_sim* sim, int32_t flags);
+int32_t     mg_bind_refresh_targets(mg_sim* sim, float* root_dst, float* rigid_body_dst);
 
 /* ---- introspection for tests and the bench ------------------------------- */
 /* Kernel timing is opt-in (default off): while on, every eager simulate() and

@@ -127,6 +127,8 @@ def _load():
         "mg_refresh_mass_matrix": (i32, [vp, i32, vp, i32, vp]),
         "mg_refresh_jacobian_mass_matrix": (i32, [vp, i32, vp, vp, i32, vp]),
         "mg_set_kernel_timing": (i32, [vp, i32]),
+        "mg_set_fusion": (i32, [vp, i32]),
+        "mg_bind_refresh_targets": (i32, [vp, vp, vp]),
         "mg_last_step_ms": (ctypes.c_float, [vp]),
         "mg_step_time_stats": (i32, [vp, i32, vp, vp, vp]),
         "mg_num_free_bodies": (i32, [vp]),
@@ -155,7 +157,7 @@ EXPORTED_SYMBOLS = (
     "mg_refresh_net_contact_force", "mg_set_actor_root_state", "mg_set_rigid_body_state",
     "mg_set_dof_state", "mg_set_dof_position_target", "mg_set_dof_velocity_target",
     "mg_set_dof_actuation_force", "mg_set_dof_props", "mg_apply_rigid_body_force",
-    "mg_refresh_jacobian", "mg_refresh_mass_matrix", "mg_set_kernel_timing", "mg_last_step_ms", "mg_step_time_stats", "mg_num_free_bodies",
+    "mg_refresh_jacobian", "mg_refresh_mass_matrix", "mg_set_kernel_timing", "mg_set_fusion", "mg_bind_refresh_targets", "mg_last_step_ms", "mg_step_time_stats", "mg_num_free_bodies",
     "mg_num_articulations",
     "mg_num_coupled_envs", "mg_refresh_jacobian_mass_matrix",
     "mg_set_render_bodies", "mg_snapshot_render_state", "mg_render_cameras", "mg_last_render_ms",

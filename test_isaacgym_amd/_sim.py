@@ -143,6 +143,7 @@ class Sim:
         # state epoch: bumped by simulate and every state setter; the mass matrix
         # computed alongside the Jacobian is reused while the epoch is unchanged
         self.epoch = 0
+        self.held_src = None   # a fused root-state set's tensor, until the next simulate
         self.mm_cache = {}
         self._renderer = None
         self.cam_version = 0       # bumped by every camera change (render tables are rebuilt)
@@ -400,6 +401,12 @@ class Sim:
                 raise N.MigymError("mg_create_sim: " + N.last_error())
             self.native = handle
             N.check(N.lib.mg_upload_model(handle, ctypes.byref(self.mg_model())), "mg_upload_model")
+            # the persistent root / rigid-body tensors: a root refresh serves both
+            # (mg_bind_refresh_targets, MG_FUSE_REFRESH)
+            root, rb = self.tensors["root"], self.tensors["rb"]
+            if root.is_cuda and rb.is_cuda and root.numel() and rb.numel():
+                N.check(N.lib.mg_bind_refresh_targets(handle, root.data_ptr(), rb.data_ptr()),
+                        "mg_bind_refresh_targets")
             # actor DOF targets / props set before prepare
             self._push_dof_targets_all()
         self.finalized = True

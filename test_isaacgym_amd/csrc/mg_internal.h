@@ -55,6 +55,8 @@ struct MgRigidArgs {
     float*       cforce;      // [3][nb] net contact force out
     const float* trec;        // [ntb][MG_TREC_N] compact template records
     int          ntb;         // template bodies
+    const float* root_src;    // fused root-state set: [na][13] rows, or null
+    const int*   root_row;    // [nb] internal slot -> actor row of root_src (-1: none)
 };
 
 // Articulation step arguments (lane = articulation instance).
@@ -201,6 +203,8 @@ hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream
 hipError_t mg_launch_artic_lanes(const MgStep& P, const MgArticArgs& A, hipStream_t s);
 hipError_t mg_launch_gather_rows(const float* soa, int stride, int ncol, const int* ids, int n,
                                  float* aos, hipStream_t s);
+hipError_t mg_launch_gather_rows2(const float* soa, int stride, int ncol, const int* ids_a, int na, float* aos_a,
+                                  const int* ids_b, int nb, float* aos_b, hipStream_t s);
 hipError_t mg_launch_scatter_rows(const float* aos, int ncol, const int* ids, const int* sel,
                                   int n, int nrows, float* soa, int stride, hipStream_t s);
 hipError_t mg_launch_scatter_dofs(const float* aos, int ncol, const int* actor_dof, const int* sel,

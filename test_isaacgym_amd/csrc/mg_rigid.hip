@@ -756,12 +756,22 @@ __global__ void __launch_bounds__(64, UPZ ? 3 : 2) k_rigid_step1(MgStep P, MgRig
     const bool live = i < A.nf;
     const int b = A.free_ids ? A.free_ids[live ? i : A.nf - 1] : (live ? i : A.nf - 1);
     const int nb = A.nb;
-    float* S = A.state;
-    // this lane's inputs first, so they are in flight with the template staging
-    V3 x = v3(S[0 * nb + b], S[1 * nb + b], S[2 * nb + b]);
-    Q4 q = q4(S[3 * nb + b], S[4 * nb + b], S[5 * nb + b], S[6 * nb + b]);
-    V3 v = v3(S[7 * nb + b], S[8 * nb + b], S[9 * nb + b]);
-    V3 w = v3(S[10 * nb + b], S[11 * nb + b], S[12 * nb + b]);
+    // this lane's inputs first, so they are in flight with the template staging;
+    // a fused root-state set (migym_capi.cpp) supplies them from the actor's row
+    // of the user tensor instead (the scatter that would have written them)
+    const float* Si = A.state + b;
+    int si = nb;
+    if (A.root_src) {
+        const int rr = A.root_row[b];
+        if (rr >= 0) {
+            Si = A.root_src + (size_t)rr * MG_STATE_N;
+            si = 1;
+        }
+    }
+    V3 x = v3(Si[0 * si], Si[1 * si], Si[2 * si]);
+    Q4 q = q4(Si[3 * si], Si[4 * si], Si[5 * si], Si[6 * si]);
+    V3 v = v3(Si[7 * si], Si[8 * si], Si[9 * si]);
+    V3 w = v3(Si[10 * si], Si[11 * si], Si[12 * si]);
     const float* M = A.mass;
     const float invm = M[0 * nb + b];
     const V3 invI = v3(M[1 * nb + b], M[2 * nb + b], M[3 * nb + b]);
@@ -847,6 +857,7 @@ hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream
     if (A.nf <= 0) return hipSuccess;
     const bool upz = mg_step_is_upz(P);
     MgRigidArgs A1 = A, A2 = A;
+    A2.root_src = nullptr;   // fused root sets only with single-shape bodies (migym_capi.cpp)
     A1.nf = A.nf1;
     A2.nf = A.nf - A.nf1;
     if (A.free_ids) {

@@ -94,6 +94,20 @@ struct mg_sim {
     float* d_shapes = nullptr;
     float* d_hulls = nullptr;     // convex hull records (MG_SHAPE_CONVEX)
     int* d_actor_root = nullptr;  // [na] internal slot of each actor's root body
+    // Step fusion (mg_set_fusion): a device-resident, non-indexed root-state set
+    // of a sim whose actor roots are all single-shape free bodies is read by the
+    // next simulate's free-body kernel (d_root_row: internal slot -> actor row,
+    // -1 for non-roots) instead of a scatter launch; any earlier reader of the
+    // state flushes it as the scatter. A root refresh into the bound root tensor
+    // also gathers the bound rigid-body tensor (one launch), and the rigid-body
+    // refresh that follows is served by it while the state is unchanged.
+    int* d_root_row = nullptr;
+    bool roots_free = false;
+    int fusion = MG_FUSE_ROOT_SET | MG_FUSE_REFRESH;
+    const float* pend_root = nullptr;
+    float* bind_root = nullptr;
+    float* bind_rb = nullptr;
+    long long state_gen = 0, rb_gen = -1;
     int* d_actor_dof = nullptr;   // [na+1]
     float* d_cforce = nullptr;    // [3][nb]
     float* d_ext = nullptr;       // [6][nb]
@@ -239,6 +253,16 @@ int stage_src(mg_sim* s, const float* src, int src_host, size_t nfloat, const in
     return MG_OK;
 }
 
+// apply a deferred root-state set as the ordinary scatter (a reader of the
+// state comes before the next simulate)
+int flush_root(mg_sim* s, hipStream_t st) {
+    if (!s->pend_root) return MG_OK;
+    const float* src = s->pend_root;
+    s->pend_root = nullptr;
+    HIP_TRY(mg_launch_scatter_rows(src, MG_STATE_N, s->d_actor_root, nullptr, s->na, s->na, s->d_state, s->nb, st));
+    return MG_OK;
+}
+
 int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* dst0, float* dst1,
                     const int* idx, int n_idx, hipStream_t st) {
     if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
@@ -260,7 +284,7 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
 
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls,
-                    s->d_actor_root, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
+                    s->d_actor_root, s->d_root_row, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
                     s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
                     s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
@@ -734,6 +758,21 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(h2d(s->d_shapes, m->shapes, (size_t)s->ns * MG_SHAPE_STRIDE * sizeof(float)));
     if (m->hulls) HIP_TRY(h2d(s->d_hulls, m->hulls, (size_t)m->num_hull_floats * sizeof(float)));
     HIP_TRY(h2d(s->d_actor_root, root_int.data(), (size_t)na * sizeof(int)));
+    {
+        // fusable root sets: every actor root is a single-shape free body of the
+        // free-body kernel (internal slots 0..nf1-1), and that kernel steps all
+        // free bodies (no multi-shape ones, no articulations, no coupled envs)
+        std::vector<int> row(nb, -1);
+        bool ok = s->nf1 == s->nf_rigid && s->nf_rigid == s->nf && s->nartic == 0 && s->n_coupled == 0 && na > 0;
+        for (int a = 0; a < na && ok; ++a) {
+            const int slot = root_int[a];
+            ok = slot >= 0 && slot < s->nf1 && row[slot] < 0;
+            if (ok) row[slot] = a;
+        }
+        s->roots_free = ok;
+        HIP_TRY(dalloc(&s->d_root_row, (size_t)std::max(nb, 1)));
+        HIP_TRY(h2d(s->d_root_row, row.data(), (size_t)nb * sizeof(int)));
+    }
     HIP_TRY(h2d(s->d_actor_dof, m->actor_dof, (size_t)(na + 1) * sizeof(int)));
     HIP_TRY(hipMemset(s->d_cforce, 0, (size_t)nb * 3 * sizeof(float)));
     HIP_TRY(hipMemset(s->d_ext, 0, (size_t)nb * 6 * sizeof(float)));
@@ -830,8 +869,15 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.trec = s->d_trec; A.ntb = s->ntb;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
         A.cforce = s->d_cforce;
+        if (s->pend_root) {   // the deferred root set, read by the step kernel
+            A.root_src = s->pend_root;
+            A.root_row = s->d_root_row;
+            s->pend_root = nullptr;
+        }
         HIP_TRY(mg_launch_rigid_step(P, A, st));
     }
+    if (int rc_ = flush_root(s, st)) return rc_;   // a root set with no free-body launch
+    s->state_gen++;
     if (s->ext_pending) {
         HIP_TRY(hipMemsetAsync(s->d_ext, 0, (size_t)s->nb * 6 * sizeof(float), st));
         s->ext_pending = false;
@@ -856,6 +902,21 @@ int32_t mg_fetch_results(mg_sim* s, int32_t wait) {
         if (s->timed_step) HIP_TRY(hipEventSynchronize(s->ev_end));
         else HIP_TRY(hipStreamSynchronize(s->last_stream));
     }
+    return MG_OK;
+}
+
+int32_t mg_set_fusion(mg_sim* s, int32_t flags) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    const int32_t prev = s->fusion;
+    s->fusion = flags & (MG_FUSE_ROOT_SET | MG_FUSE_REFRESH);
+    return prev;
+}
+
+int32_t mg_bind_refresh_targets(mg_sim* s, float* root_dst, float* rigid_body_dst) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    s->bind_root = root_dst;
+    s->bind_rb = rigid_body_dst;
+    s->rb_gen = -1;
     return MG_OK;
 }
 
@@ -907,11 +968,31 @@ int32_t mg_num_coupled_envs(mg_sim* s) { return s ? s->n_coupled : 0; }
 
 int32_t mg_refresh_actor_root_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
-    return refresh_rows(s, s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, dst, dst_host, (hipStream_t)stream);
+    if (!s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(s->device));
+    if (int rc_ = flush_root(s, st)) return rc_;
+    if (!dst_host && dst && dst == s->bind_root && s->bind_rb && (s->fusion & MG_FUSE_REFRESH) &&
+        s->rb_gen != s->state_gen && s->na > 0) {
+        // the bound root and rigid-body tensors in one launch
+        HIP_TRY(mg_launch_gather_rows2(s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, dst, s->d_perm, s->nb,
+                                       s->bind_rb, st));
+        s->rb_gen = s->state_gen;
+        return MG_OK;
+    }
+    return refresh_rows(s, s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, dst, dst_host, st);
 }
 int32_t mg_refresh_rigid_body_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
-    return refresh_rows(s, s->d_state, s->nb, MG_STATE_N, s->d_perm, s->nb, dst, dst_host, (hipStream_t)stream);
+    if (!s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(s->device));
+    if (int rc_ = flush_root(s, st)) return rc_;
+    const bool bound = !dst_host && dst && dst == s->bind_rb;
+    if (bound && (s->fusion & MG_FUSE_REFRESH) && s->rb_gen == s->state_gen) return MG_OK;   // served
+    const int rc = refresh_rows(s, s->d_state, s->nb, MG_STATE_N, s->d_perm, s->nb, dst, dst_host, st);
+    if (rc == MG_OK && bound) s->rb_gen = s->state_gen;
+    return rc;
 }
 int32_t mg_refresh_dof_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
@@ -931,6 +1012,12 @@ int32_t mg_set_actor_root_state(mg_sim* s, const float* src, int32_t src_host, c
     hipStream_t st = (hipStream_t)stream;
     const float* dsrc;
     const int* didx;
+    s->state_gen++;
+    if (!src_host && !idx && s->roots_free && (s->fusion & MG_FUSE_ROOT_SET)) {
+        s->pend_root = src;   // read by the next simulate (a later full set replaces it)
+        return MG_OK;
+    }
+    if (int rc_ = flush_root(s, st)) return rc_;
     int rc = stage_src(s, src, src_host, (size_t)s->na * MG_STATE_N, idx, n_idx, st, &dsrc, &didx);
     if (rc) return rc;
     HIP_TRY(mg_launch_scatter_rows(dsrc, MG_STATE_N, s->d_actor_root, didx, idx ? n_idx : s->na, s->na,
@@ -945,6 +1032,8 @@ int32_t mg_set_rigid_body_state(mg_sim* s, const float* src, int32_t src_host, v
     hipStream_t st = (hipStream_t)stream;
     const float* dsrc;
     const int* didx;
+    if (int rc_ = flush_root(s, st)) return rc_;
+    s->state_gen++;
     int rc = stage_src(s, src, src_host, (size_t)s->nb * MG_STATE_N, nullptr, 0, st, &dsrc, &didx);
     if (rc) return rc;
     // free bodies only: rows are selected through the free-body list
@@ -1105,6 +1194,7 @@ int32_t mg_snapshot_render_state(mg_sim* s, void* stream) {
     if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
     HIP_TRY(hipSetDevice(s->device));
     if (!s->d_rstate) HIP_TRY(dalloc(&s->d_rstate, (size_t)s->nb * MG_STATE_N));
+    if (int rc_ = flush_root(s, (hipStream_t)stream)) return rc_;
     HIP_TRY(hipMemcpyAsync(s->d_rstate, s->d_state, (size_t)s->nb * MG_STATE_N * sizeof(float),
                            hipMemcpyDeviceToDevice, (hipStream_t)stream));
     s->rstate_valid = true;

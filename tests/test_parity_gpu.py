@@ -92,6 +92,48 @@ def test_servo_large_launch_step_parity(gym):
         assert np.array_equal(ncf.cpu().numpy(), cf)
 
 
+def test_fused_step_matches_unfused(gym):
+    """Step fusion (mg_set_fusion): the root-state set read by the step kernel
+    and the paired root + rigid-body refresh give the same tensors, bit for bit,
+    as the scatter / two-gather sequence; a reader between set and simulate
+    sees the set rows (the deferred set is flushed first)."""
+    from test_isaacgym_amd import _native as N
+    n, steps = 512, 24
+    sims = []
+    for fused in (True, False):
+        sim, _ = scenes.servo_scene(gym, n)
+        gym.prepare_sim(sim)
+        if not fused:
+            N.lib.mg_set_fusion(sim.native, 0)
+        sims.append((sim, _tensors(gym, sim)))
+    acts = scenes.servo_actions(n, steps, DEV, seed=4)
+    for sim, (root, _, _, _) in sims:
+        gym.refresh_actor_root_state_tensor(sim)
+    for k in range(steps):
+        for sim, (root, rb, _, _) in sims:
+            root[:, 3:10] = acts[k]
+            assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+            gym.simulate(sim)
+            gym.fetch_results(sim, True)
+            gym.refresh_actor_root_state_tensor(sim)
+            gym.refresh_rigid_body_state_tensor(sim)
+        (ra, rba, _, _), (rb_, rbb, _, _) = sims[0][1], sims[1][1]
+        assert torch.equal(ra, rb_), "step %d: root state differs" % k
+        assert torch.equal(rba, rbb), "step %d: rigid-body state differs" % k
+    # set, then read before simulate: the reader sees the set rows
+    sim, (root, rb, _, _) = sims[0]
+    want = root.clone()
+    want[:, 0:3] += 1.0
+    root.copy_(want)
+    assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+    gym.refresh_rigid_body_state_tensor(sim)
+    roots = torch.as_tensor(sim.model_arrays["actor_root_body"], device=DEV, dtype=torch.long)
+    assert torch.equal(rb[roots], want)
+    root.zero_()
+    gym.refresh_actor_root_state_tensor(sim)
+    assert torch.equal(root, want)
+
+
 def test_servo_trajectory_bitexact(gym):
     """A 120-frame rollout with a random root teleport every frame, device vs
     oracle from the same initial state: no re-synchronisation."""
