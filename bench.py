@@ -75,6 +75,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-franka", action="store_true", help="skip the secondary S3 Franka cube-pick measurement")
     ap.add_argument("--no-cameras", action="store_true", help="skip the secondary S5 camera-render measurement")
     ap.add_argument("--no-large-n", action="store_true", help="skip the 262,144-env S1 kernel leg")
+    ap.add_argument("--pmc-calibrate", action="store_true",
+                    help="before the warm-up, 4 indexed root-state sets of every actor (k_scatter_rows: the "
+                         "known-volume kernel profiles/collect_pmc.py calibrates FETCH_SIZE on)")
     ap.add_argument("--large-n", type=int, default=LARGE_N)
     ap.add_argument("--camera-envs", type=int, default=1024)
     ap.add_argument("--eager", action="store_true",
@@ -586,6 +589,12 @@ def main():
             sharding.all_gather_rows(root)      # RCCL over xGMI: (world * 2n, 13) observation
 
     gym.refresh_actor_root_state_tensor(sim)
+    if args.pmc_calibrate:
+        every = torch.arange(root.shape[0], dtype=torch.int32, device=dev)
+        for _ in range(4):
+            gym.set_actor_root_state_tensor_indexed(sim, gymtorch.unwrap_tensor(root), gymtorch.unwrap_tensor(every),
+                                                    root.shape[0])
+            gym.refresh_actor_root_state_tensor(sim)
     k = 0
     for _ in range(args.warmup):
         step(k)

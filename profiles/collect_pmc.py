@@ -6,8 +6,9 @@ Units and gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE / WRITE_SIZE
 are KiB; FETCH_SIZE under-reads wide coalesced loads by exactly 2x and other
 widths are uncalibrated, so the read factor is calibrated here on a kernel of
 the same run with a known read volume and the same access width (dword loads):
-k_scatter_rows of set_actor_root_state reads the (2N, 13) f32 root tensor once
-(fully coalesced) plus its int32 root-body index per row.
+k_scatter_rows of bench.py --pmc-calibrate's indexed set_actor_root_state of
+every actor reads the (2N, 13) f32 root tensor once (fully coalesced) plus the
+int32 selection and root-body index per row.
 
 usage: python profiles/collect_pmc.py FETCH.csv WRITE.csv ENVS OUT.json
 """
@@ -35,7 +36,9 @@ def main():
     f, nf = per_kernel(fetch_csv, "FETCH_SIZE")
     w, _ = per_kernel(write_csv, "WRITE_SIZE")
     actors = 2 * envs
-    known_read = actors * 13 * 4 + actors * 4
+    # bench.py --pmc-calibrate: indexed sets of every actor (the fused step reads a
+    # full set itself): the (2N, 13) rows, the int32 selection and root-body index
+    known_read = actors * 13 * 4 + 2 * actors * 4
     factor = known_read / (f["k_scatter_rows"] * 1024.0)
     rigid_read = f["k_rigid_step"] * 1024.0 * factor
     rigid_write = w["k_rigid_step"] * 1024.0

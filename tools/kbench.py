@@ -1,6 +1,7 @@
 """Kernel microbenchmark: average k_rigid_step duration (HIP events around each
 launch) for the servo scene at several env counts, for the library selected
-by MIGYM_LIB (default: the in-tree build). Prints one JSON line per size."""
+by MIGYM_LIB (default: the in-tree build). KB_FUSION sets mg_set_fusion's flags
+(default: the library's, both fusions on). Prints one JSON line per size."""
 import ctypes
 import json
 import os
@@ -19,6 +20,9 @@ def run(n, steps=200, warm=20):
     sim, _ = scenes.servo_scene(gym, n)
     gym.prepare_sim(sim)
     N.lib.mg_set_kernel_timing(sim.native, 1)
+    fusion = os.environ.get("KB_FUSION")
+    if fusion is not None:
+        N.lib.mg_set_fusion(sim.native, int(fusion))
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     acts = scenes.servo_actions(n, 32, "cuda:0", seed=0)
     gym.refresh_actor_root_state_tensor(sim)
@@ -32,7 +36,7 @@ def run(n, steps=200, warm=20):
     used = N.lib.mg_step_time_stats(sim.native, steps, ctypes.byref(avg), ctypes.byref(lo), None)
     gym.destroy_sim(sim)
     return {"lib": os.path.basename(N.LIB_PATH), "envs": n, "kernel_us_avg": 1e3 * avg.value,
-            "kernel_us_min": 1e3 * lo.value, "launches": used}
+            "kernel_us_min": 1e3 * lo.value, "launches": used, "fusion": os.environ.get("KB_FUSION", "default")}
 
 
 if __name__ == "__main__":
