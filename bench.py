@@ -489,10 +489,22 @@ def large_n_rate(n, steps, dev, use_graph=True):
             step(base + k)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    # the same kernel without the fused root-state read (mg_set_fusion 0: the set
+    # is a scatter launch and the step reads the SoA state): at this size the
+    # fused read costs the kernel the user rows' other-template halves (test10's
+    # actor rows alternate UAV / vehicle, whose waves run apart: DESIGN.md §3.2)
+    from test_isaacgym_amd import _native as N
+    prev = N.lib.mg_set_fusion(sim.native, 0)
+    ukms, ukmin, uused = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
+                                      lambda: [step(k) for k in range(KERNEL_TIMED_LAUNCHES)])
+    N.lib.mg_set_fusion(sim.native, prev)
     gym.destroy_sim(sim)
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps, "steps": steps,
             "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graphs is not None else "eager",
-            "roofline": rigid_roofline(n, kms, kmin, used, "%d eager steps after a 10-step warm-up" % used)}
+            "roofline": rigid_roofline(n, kms, kmin, used, "%d eager steps after a 10-step warm-up" % used),
+            "roofline_unfused": rigid_roofline(n, ukms, ukmin, uused,
+                                               "%d eager steps with mg_set_fusion(0) (scatter launch, then the "
+                                               "step kernel on the SoA state)" % uused)}
 
 
 # --------------------------------------------------------------------------- dry run (no GPU)
