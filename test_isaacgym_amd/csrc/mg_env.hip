@@ -615,9 +615,26 @@ __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool a
     }
 }
 
+// The template's link constants (joint frames, axes, parents, DOF indices) in
+// LDS for the whole kernel: the serial loops of the kinematic scan and the
+// inward / outward passes read them per link, and from HBM / L2 every such read
+// was a dependent round trip on the critical path (S2: ~4 us of a 24.9 us step).
+template <int MAXL>
+__device__ __forceinline__ void stage_links(MgEnvArgs& A) {
+    __shared__ float s_lf[MAXL * MG_LINK_F_N];
+    __shared__ int s_li[MAXL * MG_LINK_I_N];
+    const int nl = A.nl < MAXL ? A.nl : MAXL;
+    for (int k = threadIdx.x; k < nl * MG_LINK_F_N; k += 64) s_lf[k] = A.link_f[k];
+    for (int k = threadIdx.x; k < nl * MG_LINK_I_N; k += 64) s_li[k] = A.link_i[k];
+    __syncthreads();
+    A.link_f = s_lf;
+    A.link_i = s_li;
+}
+
 template <int MAXL>
 __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     __shared__ EnvLds shm[EPW];
+    stage_links<MAXL>(A);
     const int gi = threadIdx.x / G;
     const int ln = threadIdx.x % G;
     const int e = blockIdx.x * EPW + gi;
@@ -1214,6 +1231,7 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
     MgEnvArgs A{};
     A.nb = AA.nb; A.nd = AA.nd; A.nl = AA.nl; A.ndof = AA.ndof; A.floating = 0;
     A.link_f = AA.link_f; A.link_i = AA.link_i;
+    stage_links<MAXL>(A);
     A.state = AA.state; A.mass = AA.mass; A.body_tmpl = AA.body_tmpl; A.tbf = AA.tbf;
     A.dof_pos = AA.dof_pos; A.dof_vel = AA.dof_vel; A.dof_tpos = AA.dof_tpos; A.dof_tvel = AA.dof_tvel;
     A.dof_force = AA.dof_force; A.dof_props = AA.dof_props; A.ext = AA.ext; A.cforce = AA.cforce;
