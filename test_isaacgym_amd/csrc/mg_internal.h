@@ -67,6 +67,7 @@ struct MgArticArgs {
     int          tmpl;        // template id handled by this launch
     int          nl, ndof;    // links / dofs of the template
     int          fixed_base;
+    int          chain;       // fixed base, link l's parent l - 1 and DOF l - 1 (k_artic_chain)
     const float* link_f;      // [nl][16] template link constants
     const int*   link_i;      // [nl][4]
     float*       state;       // [13][nb]  link states (root = primary, others FK output)

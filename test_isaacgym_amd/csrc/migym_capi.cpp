@@ -56,6 +56,7 @@ std::vector<T> to_soa(const T* aos, int n, int ncol) {
 }
 
 struct ArticGroup {
+    int chain;                     // serial chain with one DOF per moving link (MgArticArgs.chain)
     int tmpl, first_link, nl, ndof, fixed_base;
     int offset, count;             // into the template-sorted instance list (all instances)
     int step_offset, step_count;   // into the list stepped by k_artic_step (uncoupled envs)
@@ -621,6 +622,11 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                 return fail(MG_ERR_ARG, "articulation template %d: links not in topological order", t);
             if (li[2] >= g.ndof) return fail(MG_ERR_ARG, "articulation template %d: bad dof index", t);
         }
+        g.chain = g.fixed_base && g.ndof == g.nl - 1;
+        for (int l = 1; l < g.nl && g.chain; ++l) {
+            const int* li = m->tmpl_link_i + (size_t)(g.first_link + l) * MG_LINK_I_N;
+            g.chain = li[0] == l - 1 && li[2] == l - 1 && (li[1] == MG_JOINT_REVOLUTE || li[1] == MG_JOINT_PRISMATIC);
+        }
         g.offset = (int)artic_sorted.size() / MG_ARTIC_I_N;
         g.count = 0;
         g.step_offset = (int)artic_step.size() / MG_ARTIC_I_N;
@@ -829,7 +835,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         MgArticArgs A{};
         A.na = g.step_count; A.nb = s->nb; A.nd = s->nd;
         A.artic_i = s->d_artic_step + (size_t)g.step_offset * MG_ARTIC_I_N;
-        A.tmpl = g.tmpl; A.nl = g.nl; A.ndof = g.ndof; A.fixed_base = g.fixed_base;
+        A.tmpl = g.tmpl; A.nl = g.nl; A.ndof = g.ndof; A.fixed_base = g.fixed_base; A.chain = g.chain;
         A.link_f = s->d_link_f + (size_t)g.first_link * MG_LINK_F_N;
         A.link_i = s->d_link_i + (size_t)g.first_link * MG_LINK_I_N;
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl; A.tbf = s->d_tbf;

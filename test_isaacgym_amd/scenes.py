@@ -86,7 +86,7 @@ def servo_scene(gym, num_envs, use_gpu_pipeline=True, device=0, uav_height=102.0
 
 
 def gimbal_scene(gym, num_envs, use_gpu_pipeline=True, device=0, stiffness=50.0, damping=5.0,
-                 asset_root=None, asset_file="servo/gimbal.urdf", drive_mode=None):
+                 asset_root=None, asset_file="servo/gimbal.urdf", drive_mode=None, link_mass_scale=None):
     sp = gymapi.SimParams()
     sp.substeps = 2
     sp.dt = 1.0 / 60.0
@@ -122,6 +122,11 @@ def gimbal_scene(gym, num_envs, use_gpu_pipeline=True, device=0, stiffness=50.0,
         props["stiffness"][:] = stiffness
         props["damping"][:] = damping
         gym.set_actor_dof_properties(env, h, props)
+        if link_mass_scale is not None:   # heavier links (inertia scaled with the mass)
+            bp = gym.get_actor_rigid_body_properties(env, h)
+            for b in bp:
+                b.mass = b.mass * link_mass_scale
+            gym.set_actor_rigid_body_properties(env, h, bp, True)
     return sim, envs
 
 

@@ -275,6 +275,34 @@ def test_gimbal_parity(gym):
     assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
 
 
+def test_gimbal_effort_limit_parity(gym):
+    """Stiff, lightly damped PD drives (kp 2000, kd 0.5) on 10 kg links against the URDF's 10 N m effort limit:
+    the implicit drive force exceeds the limit, so the articulated-body pass is
+    re-solved with those drives at constant +-effort — bit for
+    bit the oracle's re-solve."""
+    n, steps = 128, 40
+    sim, _ = scenes.gimbal_scene(gym, n, stiffness=2000.0, damping=0.5, link_mass_scale=1000.0)
+    gym.prepare_sim(sim)
+    _, rb, dof, _ = _tensors(gym, sim)
+    tg = scenes.gimbal_targets(n, steps, DEV, seed=5)
+    tg_h = tg.cpu().numpy()
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    ds = sim.model_arrays["dof_state0"].copy()
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+    for k in range(steps):
+        assert gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[k].contiguous()))
+        gym.simulate(sim)
+        tgt[:, 0] = tg_h[k]
+        oracle.step(p, m, st, ds, tgt=tgt)
+    gym.refresh_dof_state_tensor(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    got_d, got = dof.cpu().numpy(), rb.cpu().numpy()
+    assert np.all(np.isfinite(got_d))
+    assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+
+
 def test_gimbal_velocity_drive_parity(gym):
     """DOF_MODE_VEL (examples/dof_controls.py:89-150: velocity targets, the
     stiffness is ignored, damping drives the joint speed): random velocity
