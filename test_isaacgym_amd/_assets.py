@@ -530,6 +530,36 @@ def mesh_shape(verts, p, q, source):
     return Shape(CONVEX, (brad,), np.asarray(p) + _qmat(q) @ hull.box_centre, q, source, hull)
 
 
+_DECOMP_CACHE = {}
+
+
+def _decomposed_shapes(path, scale, p, q, params, base):
+    """AssetOptions.vhacd_enabled: the mesh as several convex hulls
+    (_decomp.decompose with the VhacdParams' hull budget, voxel resolution,
+    concavity and minimum piece volume), or [] when the file has no triangles
+    (the caller then takes the single hull)."""
+    from . import _decomp
+    key = (os.path.abspath(path), os.path.getmtime(path), tuple(np.asarray(scale, float)),
+           int(params.max_convex_hulls), int(params.resolution), float(params.concavity),
+           float(params.min_volume_per_ch))
+    pts = _DECOMP_CACHE.get(key)
+    if pts is None:
+        tm = _decomp.mesh_triangles(path)
+        if tm is None or len(tm[1]) == 0:
+            return []
+        v, f = tm
+        pts = _decomp.decompose(v * scale, f, max_convex_hulls=int(params.max_convex_hulls),
+                                resolution=int(params.resolution), concavity=float(params.concavity),
+                                min_volume_per_ch=float(params.min_volume_per_ch))
+        _DECOMP_CACHE[key] = pts
+    out = []
+    for k, pc in enumerate(pts):
+        sh = mesh_shape(pc, p, q, "vhacd:%s#%d" % (base, k)) if len(pc) >= 4 else None
+        if sh is not None:
+            out.append(sh)
+    return out
+
+
 def _resolve(filename, urdf_dir, asset_root):
     if filename.startswith("package://"):
         rest = filename[len("package://"):]
@@ -593,6 +623,11 @@ def _geometry_shapes(col, urdf_dir, asset_root, options, warnings):
             path = _resolve(fn, urdf_dir, asset_root)
             base = os.path.basename(fn)
             if os.path.exists(path):
+                if getattr(options, "vhacd_enabled", False):
+                    pieces = _decomposed_shapes(path, np.array(scale), p, q, options.vhacd_params, base)
+                    if pieces:
+                        out.extend(pieces)
+                        continue
                 vs = _mesh_vertices(path) * np.array(scale)
                 sh = mesh_shape(vs, p, q, "mesh-hull:" + base) if len(vs) >= 4 else None
                 if sh is not None:

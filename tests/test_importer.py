@@ -75,3 +75,57 @@ def test_reference_anymal_dae_meshes():
         o_zup = np.stack([o[:, 0], -o[:, 2], o[:, 1]], 1)
         assert len(v) > 1000
         assert np.allclose(v.min(0), o_zup.min(0), atol=1.5) and np.allclose(v.max(0), o_zup.max(0), atol=1.5)
+
+
+def _u_obj(path, depth=1.0):
+    """A U-shaped prism (two posts on a bar, 3 x 3 x depth, volume 7 depth) as a
+    closed OBJ triangle mesh."""
+    poly = [(0, 0), (3, 0), (3, 3), (2, 3), (2, 1), (1, 1), (1, 3), (0, 3)]
+    n = len(poly)
+    lines = ["v %g %g %g" % (x - 1.5, y - 1.5, z - 0.5 * depth) for z in (0.0, depth) for (x, y) in poly]
+    for i in range(n):
+        j = (i + 1) % n
+        lines += ["f %d %d %d" % (i + 1, j + 1, n + j + 1), "f %d %d %d" % (i + 1, n + j + 1, n + i + 1)]
+    for t in [[0, 1, 4], [0, 4, 5], [1, 2, 3], [1, 3, 4], [0, 5, 6], [0, 6, 7]]:
+        lines.append("f %d %d %d" % (t[2] + 1, t[1] + 1, t[0] + 1))
+        lines.append("f %d %d %d" % (n + t[0] + 1, n + t[1] + 1, n + t[2] + 1))
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def _u_urdf(d, scale=0.1):
+    _u_obj(os.path.join(d, "u.obj"))
+    with open(os.path.join(d, "u.urdf"), "w") as f:
+        f.write(textwrap.dedent("""\
+            <robot name="u"><link name="u">
+              <inertial><mass value="1"/><inertia ixx="0.01" iyy="0.01" izz="0.01" ixy="0" ixz="0" iyz="0"/></inertial>
+              <collision><geometry><mesh filename="u.obj" scale="%g %g %g"/></geometry></collision>
+            </link></robot>""" % (scale, scale, scale)))
+    return "u.urdf"
+
+
+def test_convex_decomposition_of_a_concave_mesh(gym, tmp_path):
+    """AssetOptions.vhacd_enabled (examples/convex_decomposition.py's option): a
+    U-shaped mesh becomes several convex hulls that keep its gap empty and
+    whose volumes sum to the solid's (the single hull fills the gap)."""
+    from scipy.spatial import ConvexHull
+    d = str(tmp_path)
+    f = _u_urdf(d)
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, gymapi.SimParams())
+    one = gym.load_asset(sim, d, f, gymapi.AssetOptions())
+    opts = gymapi.AssetOptions()
+    opts.vhacd_enabled = True
+    opts.vhacd_params.max_convex_hulls = 8
+    dec = gym.load_asset(sim, d, f, opts)
+    s1, sd = one.bodies[0].shapes, dec.bodies[0].shapes
+    assert len(s1) == 1 and 2 <= len(sd) <= 8
+    assert all(s.type == _assets.CONVEX for s in sd)
+    vol = 0.0
+    gap = np.array([0.0, 0.05, 0.0])           # the middle of the U's gap (scale 0.1)
+    for s in sd:
+        v = s.hull.verts @ _assets._qmat(s.q).T + s.p
+        h = ConvexHull(v)
+        vol += h.volume
+        assert np.any(h.equations @ np.append(gap, 1.0) > 1e-9), "a piece covers the gap"
+    assert abs(vol - 7e-3) < 0.15 * 7e-3, vol
+    assert ConvexHull(s1[0].hull.verts).volume > 8.5e-3        # the single hull: 9e-3, gap included

@@ -247,6 +247,43 @@ def test_hull_drops_parity(gym, tmp_path):
     assert np.all(np.abs(got[:, 7:10]) < 0.05)
 
 
+def test_decomposed_mesh_drops_parity(gym, tmp_path):
+    """A concave mesh split into convex hulls (AssetOptions.vhacd_enabled: a U
+    of 3 pieces, a multi-shape body) dropped onto the ground at random poses:
+    the free-body kernel's shift-register slots over several hulls, bit for bit
+    the oracle, and at rest."""
+    import test_importer
+    f = test_importer._u_urdf(str(tmp_path), scale=0.1)
+    sp = scenes.servo_sim_params(True)
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim, plane)
+    opts = gymapi.AssetOptions()
+    opts.vhacd_enabled = True
+    opts.vhacd_params.max_convex_hulls = 4
+    asset = gym.load_asset(sim, str(tmp_path), f, opts)
+    assert len(asset.bodies[0].shapes) >= 2
+    rng = np.random.RandomState(7)
+    for i in range(32):
+        env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 8)
+        q = gymapi.Quat(*rng.randn(4)).normalize()
+        gym.create_actor(env, asset, gymapi.Transform(gymapi.Vec3(0, 0, 0.4 + 0.3 * rng.rand()), q), "u", i, 0)
+    gym.prepare_sim(sim)
+    _, rb, _, ncf = _tensors(gym, sim)
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    for _ in range(150):
+        gym.simulate(sim)
+        cf = oracle.step(p, m, st, np.zeros((0, 2), np.float32))
+    gym.refresh_rigid_body_state_tensor(sim)
+    gym.refresh_net_contact_force_tensor(sim)
+    got = rb.cpu().numpy()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+    assert np.array_equal(ncf.cpu().numpy(), cf)
+    assert np.all(got[:, 2] > 0.0) and np.all(got[:, 2] < 0.4)
+
+
 def test_gimbal_parity(gym):
     """S2: the 3-DOF camera gimbal under random PD position targets."""
     n, steps = 256, 60
