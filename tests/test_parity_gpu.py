@@ -340,6 +340,66 @@ def test_gimbal_effort_limit_parity(gym):
     assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
 
 
+def _tree_urdf(d):
+    """A fixed base with two revolute branches of two links each (not a serial
+    chain: the lane-parallel articulation kernel), 5 kg links, 20 N m limits."""
+    link = ('<link name="%s"><inertial><origin xyz="0.2 0 0"/><mass value="5"/>'
+            '<inertia ixx="0.02" iyy="0.08" izz="0.08" ixy="0" ixz="0" iyz="0"/></inertial>'
+            '<collision><origin xyz="0.2 0 0"/><geometry><box size="0.4 0.05 0.05"/></geometry></collision></link>')
+    joint = ('<joint name="%s" type="revolute"><parent link="%s"/><child link="%s"/>'
+             '<origin xyz="%s" rpy="0 0 0"/><axis xyz="%s"/><limit lower="-2" upper="2" effort="20" velocity="50"/></joint>')
+    body = ['<link name="base"><inertial><mass value="1"/><inertia ixx="0.01" iyy="0.01" izz="0.01" ixy="0" ixz="0" iyz="0"/>'
+            '</inertial></link>']
+    body += [link % n for n in ("a1", "a2", "b1", "b2")]
+    body += [joint % ("ja1", "base", "a1", "0 0 0", "0 0 1"), joint % ("ja2", "a1", "a2", "0.4 0 0", "0 1 0"),
+             joint % ("jb1", "base", "b1", "0 0 0.1", "0 0 1"), joint % ("jb2", "b1", "b2", "0.4 0 0", "1 0 0")]
+    with open(os.path.join(d, "tree.urdf"), "w") as f:
+        f.write('<robot name="tree">' + "".join(body) + "</robot>")
+    return "tree.urdf"
+
+
+def test_tree_effort_limit_parity(gym, tmp_path):
+    """A branched articulation (k_artic_lanes, not the chain kernel) with stiff
+    drives on heavy links: the effort-limit re-solve of the lane-parallel
+    articulated-body pass, bit for bit the oracle."""
+    sp = gymapi.SimParams()
+    sp.dt, sp.substeps = 1.0 / 60.0, 2
+    sp.gravity = gymapi.Vec3(0.0, 0.0, -9.8)
+    sp.physx.solver_type = 1
+    sp.use_gpu_pipeline = True
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    asset = gym.load_asset(sim, str(tmp_path), _tree_urdf(str(tmp_path)), opts)
+    n, steps = 64, 40
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 8)
+        h = gym.create_actor(env, asset, gymapi.Transform(gymapi.Vec3(0, 0, 1)), "tree", i, 1)
+        props = gym.get_actor_dof_properties(env, h)
+        props["driveMode"][:] = gymapi.DOF_MODE_POS
+        props["stiffness"][:] = 3000.0
+        props["damping"][:] = 1.0
+        gym.set_actor_dof_properties(env, h, props)
+    gym.prepare_sim(sim)
+    _, rb, dof, _ = _tensors(gym, sim)
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    ds = sim.model_arrays["dof_state0"].copy()
+    rng = np.random.RandomState(11)
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+    for k in range(steps):
+        tgt[:, 0] = rng.uniform(-1.5, 1.5, size=ds.shape[0]).astype(np.float32)
+        assert gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(torch.from_numpy(tgt[:, 0].copy()).to(DEV)))
+        gym.simulate(sim)
+        oracle.step(p, m, st, ds, tgt=tgt)
+    gym.refresh_dof_state_tensor(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    got_d, got = dof.cpu().numpy(), rb.cpu().numpy()
+    assert np.all(np.isfinite(got_d))
+    assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+
+
 def test_gimbal_velocity_drive_parity(gym):
     """DOF_MODE_VEL (examples/dof_controls.py:89-150: velocity targets, the
     stiffness is ignored, damping drives the joint speed): random velocity
