@@ -137,6 +137,15 @@ def kernel_stats(sim, n_launches, run):
     return avg.value, lo.value, int(used)
 
 
+def fuse_in_capture(sim):
+    """MG_FUSE_IN_CAPTURE on this sim: every captured step of this leg is set ->
+    simulate -> refresh, so each captured set is consumed by the captured
+    simulate after it (include/migym.h; the S3 leg's frames end with the DOF
+    setters and keep the default)."""
+    from test_isaacgym_amd import _native as N
+    N.lib.mg_set_fusion(sim.native, 1 | 2 | 4 | 8)
+
+
 def load_pmc(name):
     """Committed rocprofv3 PMC summary (profiles/<round>_pmc_<name>.json, newest
     round first, written by profiles/collect_pmc.py): (dict, file) or (None, None)."""
@@ -227,6 +236,7 @@ def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     gym = gymapi.acquire_gym()
     sim, _ = scenes.gimbal_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
     gym.prepare_sim(sim)
+    fuse_in_capture(sim)
     gym.acquire_dof_state_tensor(sim)
     gym.acquire_rigid_body_state_tensor(sim)
     tg = scenes.gimbal_targets(n, 64, dev, seed=0)
@@ -372,6 +382,7 @@ def camera_rate(n, steps, warmup, dev, use_graph=True, width=1600, height=900):
     sim, envs = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
     imgs = scenes.attach_servo_cameras(gym, sim, envs, width, height, 30.0)
     gym.prepare_sim(sim)
+    fuse_in_capture(sim)
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     gym.acquire_rigid_body_state_tensor(sim)
     acts = scenes.servo_actions(n, 16, dev, seed=5)
@@ -449,6 +460,7 @@ def large_n_rate(n, steps, dev, use_graph=True):
     gym = gymapi.acquire_gym()
     sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
     gym.prepare_sim(sim)
+    fuse_in_capture(sim)
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     gym.acquire_rigid_body_state_tensor(sim)
     gym.acquire_dof_state_tensor(sim)
@@ -583,6 +595,7 @@ def main():
     sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=dev_index, env_offset=rank * n,
                                 grid_envs=world * n)
     gym.prepare_sim(sim)
+    fuse_in_capture(sim)
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     gym.acquire_rigid_body_state_tensor(sim)
     gym.acquire_dof_state_tensor(sim)

@@ -283,6 +283,11 @@ float       mg_last_render_ms(mg_sim* sim);
 
 /* ---- step fusion ------------------------------------------------------------
  * MG_FUSE_ROOT_SET: the deferred root-state set described above.
+ * MG_FUSE_DOF_TARGETS: a device-resident, non-indexed mg_set_dof_position_target /
+ * _velocity_target / _actuation_force is read by the next mg_simulate's
+ * articulation kernels (which write it through to the sim's own targets) instead
+ * of a copy launch; the caller keeps src alive and unmodified until then (an
+ * indexed or host set of the same column applies it first).
  * MG_FUSE_REFRESH: with targets bound by mg_bind_refresh_targets (the persistent
  * tensors acquire_actor_root_state_tensor / acquire_rigid_body_state_tensor hand
  * out), a root refresh into the bound root tensor also writes the bound
@@ -290,10 +295,18 @@ float       mg_last_render_ms(mg_sim* sim);
  * a rigid-body refresh into it is then served without a launch while no
  * simulate or set has changed the state. The bound rigid-body tensor is thus
  * refreshed no later than requested (possibly at the root refresh).
- * mg_set_fusion returns the previous flags; both are on by default. The bound
+ * mg_set_fusion returns the previous flags; all but MG_FUSE_IN_CAPTURE are on by
+ * default. The bound
  * pointers must stay valid for the sim's lifetime (NULL unbinds). */
 #define MG_FUSE_ROOT_SET  1
 #define MG_FUSE_REFRESH   2
+#define MG_FUSE_DOF_TARGETS 4
+/* MG_FUSE_IN_CAPTURE (opt-in): the fusions above also inside a stream capture
+ * (hipGraph). Without it a captured set is an ordinary launch and a captured
+ * rigid-body refresh is never skipped, so any captured region replays right; with
+ * it the caller guarantees every captured set is consumed by a simulate in the
+ * same capture (e.g. set -> simulate -> refresh per captured step, as bench.py). */
+#define MG_FUSE_IN_CAPTURE  8
 int32_t     mg_set_fusion(mg_sim* sim, int32_t flags);
 int32_t     mg_bind_refresh_targets(mg_sim* sim, float* root_dst, float* rigid_body_dst);
 

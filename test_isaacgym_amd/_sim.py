@@ -143,7 +143,7 @@ class Sim:
         # state epoch: bumped by simulate and every state setter; the mass matrix
         # computed alongside the Jacobian is reused while the epoch is unchanged
         self.epoch = 0
-        self.held_src = None   # a fused root-state set's tensor, until the next simulate
+        self.held_src = []     # fused sets' tensors (root state, DOF targets), until the next simulate
         self.mm_cache = {}
         self._renderer = None
         self.cam_version = 0       # bumped by every camera change (render tables are rebuilt)

@@ -745,6 +745,9 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         dc.tpos = A.dof_tpos[gd];
         dc.tvel = A.dof_tvel[gd];
         dc.force = A.dof_force[gd];
+        if (A.tpos_w) A.tpos_w[gd] = dc.tpos;
+        if (A.tvel_w) A.tvel_w[gd] = dc.tvel;
+        if (A.force_w) A.force_w[gd] = dc.force;
     } else if (is_root) {
         // root slots: w and the velocity of the base origin v_O = v_com - w x (R c)
         const V3 w = v3(St[10 * nb + b0], St[11 * nb + b0], St[12 * nb + b0]);
@@ -1244,6 +1247,7 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
     A.state = AA.state; A.mass = AA.mass; A.body_tmpl = AA.body_tmpl; A.tbf = AA.tbf;
     A.dof_pos = AA.dof_pos; A.dof_vel = AA.dof_vel; A.dof_tpos = AA.dof_tpos; A.dof_tvel = AA.dof_tvel;
     A.dof_force = AA.dof_force; A.dof_props = AA.dof_props; A.ext = AA.ext; A.cforce = AA.cforce;
+    A.tpos_w = live ? AA.tpos_w : nullptr; A.tvel_w = live ? AA.tvel_w : nullptr; A.force_w = live ? AA.force_w : nullptr;
     const int* ai = AA.artic_i + (size_t)(live ? a : 0) * MG_ARTIC_I_N;
     const int b0 = ai[0], d0 = ai[1];
     const int nb = A.nb, nd = A.nd;
@@ -1279,6 +1283,9 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
         dc.tpos = A.dof_tpos[gd];
         dc.tvel = A.dof_tvel[gd];
         dc.force = A.dof_force[gd];
+        if (A.tpos_w) A.tpos_w[gd] = dc.tpos;
+        if (A.tvel_w) A.tvel_w[gd] = dc.tvel;
+        if (A.force_w) A.force_w[gd] = dc.force;
     }
     LinkC lk = {};
     if (ln < L) lk = load_link(A.mass, nb, b0 + ln);
@@ -1450,6 +1457,11 @@ __global__ void __launch_bounds__(64, 1) k_artic_chain(MgStep P, MgArticArgs AA)
         dc[d].tpos = AA.dof_tpos[gd];
         dc[d].tvel = AA.dof_tvel[gd];
         dc[d].force = AA.dof_force[gd];
+        if (live) {   // fused target sets: write through (the only lane of this DOF)
+            if (AA.tpos_w) AA.tpos_w[gd] = dc[d].tpos;
+            if (AA.tvel_w) AA.tvel_w[gd] = dc[d].tvel;
+            if (AA.force_w) AA.force_w[gd] = dc[d].force;
+        }
     }
     LinkC lk[NL];
 #pragma unroll

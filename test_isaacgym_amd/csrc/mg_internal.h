@@ -79,6 +79,12 @@ struct MgArticArgs {
     const float* dof_tpos;    // [nd]
     const float* dof_tvel;    // [nd]
     const float* dof_force;   // [nd]
+    // fused DOF target sets (migym_capi.cpp): dof_* then point at the user's
+    // tensors and each lane writes the value it read through to the sim's own
+    // column (null: not fused)
+    float*       tpos_w;
+    float*       tvel_w;
+    float*       force_w;
     const float* dof_props;   // [12][nd]
     const float* ext;         // [6][nb] or null
     float*       cforce;      // [3][nb]
@@ -127,6 +133,9 @@ struct MgEnvArgs {
     const float* dof_tpos;
     const float* dof_tvel;
     const float* dof_force;
+    float*       tpos_w;      // fused DOF target sets: write-through (MgArticArgs)
+    float*       tvel_w;
+    float*       force_w;
     const float* dof_props;
     const float* ext;
     float*       cforce;

@@ -104,8 +104,13 @@ struct mg_sim {
     // refresh that follows is served by it while the state is unchanged.
     int* d_root_row = nullptr;
     bool roots_free = false;
-    int fusion = MG_FUSE_ROOT_SET | MG_FUSE_REFRESH;
+    int fusion = MG_FUSE_ROOT_SET | MG_FUSE_REFRESH | MG_FUSE_DOF_TARGETS;   // MG_FUSE_IN_CAPTURE: opt-in
     const float* pend_root = nullptr;
+    const float* pend_tgt[3] = {nullptr, nullptr, nullptr};   // fused DOF target sets (pos, vel, force)
+    // stream-capture id (0: eager) at which each deferred set / the paired
+    // refresh happened: fused work is only combined within one capture (or
+    // eagerly), so a graph never relies on work it did not record
+    unsigned long long pend_root_cap = 0, pend_tgt_cap[3] = {0, 0, 0}, rb_cap = 0;
     float* bind_root = nullptr;
     float* bind_rb = nullptr;
     long long state_gen = 0, rb_gen = -1;
@@ -254,6 +259,18 @@ int stage_src(mg_sim* s, const float* src, int src_host, size_t nfloat, const in
     return MG_OK;
 }
 
+// id of the stream capture in progress on st + 1, or 0 when st is not capturing
+unsigned long long capture_id(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    if (hipStreamGetCaptureInfo(st, &cs, &id) != hipSuccess || cs != hipStreamCaptureStatusActive) return 0;
+    return id + 1;
+}
+// may this call defer / combine work? always eagerly; inside a stream capture
+// only when the caller opted in (MG_FUSE_IN_CAPTURE): a deferred set left at
+// the end of a captured region would never be applied by its replays
+bool fuse_here(const mg_sim* s, unsigned long long cid) { return cid == 0 || (s->fusion & MG_FUSE_IN_CAPTURE); }
+
 // apply a deferred root-state set as the ordinary scatter (a reader of the
 // state comes before the next simulate)
 int flush_root(mg_sim* s, hipStream_t st) {
@@ -261,6 +278,16 @@ int flush_root(mg_sim* s, hipStream_t st) {
     const float* src = s->pend_root;
     s->pend_root = nullptr;
     HIP_TRY(mg_launch_scatter_rows(src, MG_STATE_N, s->d_actor_root, nullptr, s->na, s->na, s->d_state, s->nb, st));
+    return MG_OK;
+}
+
+// apply a deferred DOF target column (0 pos, 1 vel, 2 force) as a copy
+int flush_tgt(mg_sim* s, int k, hipStream_t st) {
+    if (!s->pend_tgt[k]) return MG_OK;
+    const float* src = s->pend_tgt[k];
+    s->pend_tgt[k] = nullptr;
+    HIP_TRY(hipMemcpyAsync(s->d_dof_tgt + (size_t)k * s->nd, src, (size_t)s->nd * sizeof(float),
+                           hipMemcpyDeviceToDevice, st));
     return MG_OK;
 }
 
@@ -803,11 +830,34 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     return MG_OK;
 }
 
+// the pending DOF target columns as the kernels' inputs, with write-through
+static void fused_targets(mg_sim* s, const float*& tp, const float*& tv, const float*& tf, float*& wp, float*& wv,
+                          float*& wf) {
+    const float** in[3] = {&tp, &tv, &tf};
+    float** out[3] = {&wp, &wv, &wf};
+    for (int k = 0; k < 3; ++k) {
+        *out[k] = nullptr;
+        if (s->pend_tgt[k]) {
+            *in[k] = s->pend_tgt[k];
+            *out[k] = s->d_dof_tgt + (size_t)k * s->nd;
+        }
+    }
+}
+
 int32_t mg_simulate(mg_sim* s, void* stream) {
     if (!s || !s->uploaded) return fail(MG_ERR_STATE, "simulate before the model was uploaded");
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
     const MgStep P = make_step(s->params);
+    {   // deferred sets of another capture (or of the eager stream while capturing):
+        // applied here as ordinary launches, not read by this step's kernels
+        const unsigned long long cid = capture_id(st);
+        if (s->pend_root && s->pend_root_cap != cid)
+            if (int rc_ = flush_root(s, st)) return rc_;
+        for (int k = 0; k < 3; ++k)
+            if (s->pend_tgt[k] && s->pend_tgt_cap[k] != cid)
+                if (int rc_ = flush_tgt(s, k, st)) return rc_;
+    }
     // Under HIP stream capture (a hipGraph of the tensor-API step) the launches
     // are recorded as graph nodes; the timing events are left out (they would
     // become fixed nodes of the graph) and fetch_results does not block.
@@ -841,6 +891,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl; A.tbf = s->d_tbf;
         A.dof_pos = s->d_dof; A.dof_vel = s->d_dof + s->nd;
         A.dof_tpos = s->d_dof_tgt; A.dof_tvel = s->d_dof_tgt + s->nd; A.dof_force = s->d_dof_tgt + 2 * (size_t)s->nd;
+        fused_targets(s, A.dof_tpos, A.dof_tvel, A.dof_force, A.tpos_w, A.tvel_w, A.force_w);
         A.dof_props = s->d_dof_props;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
         A.cforce = s->d_cforce;
@@ -861,6 +912,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes; A.hulls = s->d_hulls;
         A.dof_pos = s->d_dof; A.dof_vel = s->d_dof + s->nd;
         A.dof_tpos = s->d_dof_tgt; A.dof_tvel = s->d_dof_tgt + s->nd; A.dof_force = s->d_dof_tgt + 2 * (size_t)s->nd;
+        fused_targets(s, A.dof_tpos, A.dof_tvel, A.dof_force, A.tpos_w, A.tvel_w, A.force_w);
         A.dof_props = s->d_dof_props;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
         A.cforce = s->d_cforce;
@@ -883,6 +935,10 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         HIP_TRY(mg_launch_rigid_step(P, A, st));
     }
     if (int rc_ = flush_root(s, st)) return rc_;   // a root set with no free-body launch
+    if (s->groups.empty() && s->env_groups.empty())
+        for (int k = 0; k < 3; ++k)
+            if (int rc_ = flush_tgt(s, k, st)) return rc_;
+    for (int k = 0; k < 3; ++k) s->pend_tgt[k] = nullptr;   // read (and written through) by the step
     s->state_gen++;
     if (s->ext_pending) {
         HIP_TRY(hipMemsetAsync(s->d_ext, 0, (size_t)s->nb * 6 * sizeof(float), st));
@@ -914,7 +970,7 @@ int32_t mg_fetch_results(mg_sim* s, int32_t wait) {
 int32_t mg_set_fusion(mg_sim* s, int32_t flags) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
     const int32_t prev = s->fusion;
-    s->fusion = flags & (MG_FUSE_ROOT_SET | MG_FUSE_REFRESH);
+    s->fusion = flags & (MG_FUSE_ROOT_SET | MG_FUSE_REFRESH | MG_FUSE_DOF_TARGETS | MG_FUSE_IN_CAPTURE);
     return prev;
 }
 
@@ -978,12 +1034,14 @@ int32_t mg_refresh_actor_root_state(mg_sim* s, float* dst, int32_t dst_host, voi
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(s->device));
     if (int rc_ = flush_root(s, st)) return rc_;
+    const unsigned long long cid = capture_id(st);
     if (!dst_host && dst && dst == s->bind_root && s->bind_rb && (s->fusion & MG_FUSE_REFRESH) &&
-        s->rb_gen != s->state_gen && s->na > 0) {
+        fuse_here(s, cid) && s->na > 0) {
         // the bound root and rigid-body tensors in one launch
         HIP_TRY(mg_launch_gather_rows2(s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, dst, s->d_perm, s->nb,
                                        s->bind_rb, st));
         s->rb_gen = s->state_gen;
+        s->rb_cap = cid;
         return MG_OK;
     }
     return refresh_rows(s, s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, dst, dst_host, st);
@@ -995,9 +1053,13 @@ int32_t mg_refresh_rigid_body_state(mg_sim* s, float* dst, int32_t dst_host, voi
     HIP_TRY(hipSetDevice(s->device));
     if (int rc_ = flush_root(s, st)) return rc_;
     const bool bound = !dst_host && dst && dst == s->bind_rb;
-    if (bound && (s->fusion & MG_FUSE_REFRESH) && s->rb_gen == s->state_gen) return MG_OK;   // served
+    if (bound && (s->fusion & MG_FUSE_REFRESH) && s->rb_gen == s->state_gen && s->rb_cap == capture_id(st))
+        return MG_OK;   // served by the paired gather of the same capture (or eagerly)
     const int rc = refresh_rows(s, s->d_state, s->nb, MG_STATE_N, s->d_perm, s->nb, dst, dst_host, st);
-    if (rc == MG_OK && bound) s->rb_gen = s->state_gen;
+    if (rc == MG_OK && bound) {
+        s->rb_gen = s->state_gen;
+        s->rb_cap = capture_id(st);
+    }
     return rc;
 }
 int32_t mg_refresh_dof_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
@@ -1019,8 +1081,12 @@ int32_t mg_set_actor_root_state(mg_sim* s, const float* src, int32_t src_host, c
     const float* dsrc;
     const int* didx;
     s->state_gen++;
-    if (!src_host && !idx && s->roots_free && (s->fusion & MG_FUSE_ROOT_SET)) {
+    const unsigned long long cid = capture_id(st);
+    if (!src_host && !idx && s->roots_free && (s->fusion & MG_FUSE_ROOT_SET) && fuse_here(s, cid)) {
+        if (s->pend_root && s->pend_root_cap != cid)
+            if (int rc_ = flush_root(s, st)) return rc_;
         s->pend_root = src;   // read by the next simulate (a later full set replaces it)
+        s->pend_root_cap = cid;
         return MG_OK;
     }
     if (int rc_ = flush_root(s, st)) return rc_;
@@ -1053,21 +1119,37 @@ int32_t mg_set_dof_state(mg_sim* s, const float* src, int32_t src_host, const in
     if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
     return set_dof_columns(s, src, src_host, 2, s->d_dof, s->d_dof + s->nd, idx, n_idx, (hipStream_t)stream);
 }
+// column k of the DOF targets; a device-resident full set is read by the next
+// simulate's articulation kernels (MG_FUSE_DOF_TARGETS), else a scatter / copy
+static int32_t set_dof_target(mg_sim* s, int k, const float* src, int32_t src_host, const int32_t* idx,
+                              int32_t n_idx, void* stream) {
+    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (s->nd == 0) return MG_OK;
+    if (!src) return fail(MG_ERR_ARG, "null source tensor");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(s->device));
+    const unsigned long long cid = capture_id(st);
+    if (!src_host && !idx && (s->fusion & MG_FUSE_DOF_TARGETS) && fuse_here(s, cid)) {
+        if (s->pend_tgt[k] && s->pend_tgt_cap[k] != cid)
+            if (int rc_ = flush_tgt(s, k, st)) return rc_;
+        s->pend_tgt[k] = src;
+        s->pend_tgt_cap[k] = cid;
+        return MG_OK;
+    }
+    if (int rc_ = flush_tgt(s, k, st)) return rc_;
+    return set_dof_columns(s, src, src_host, 1, s->d_dof_tgt + (size_t)k * s->nd, nullptr, idx, n_idx, st);
+}
 int32_t mg_set_dof_position_target(mg_sim* s, const float* src, int32_t src_host, const int32_t* idx,
                                    int32_t n_idx, void* stream) {
-    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
-    return set_dof_columns(s, src, src_host, 1, s->d_dof_tgt, nullptr, idx, n_idx, (hipStream_t)stream);
+    return set_dof_target(s, 0, src, src_host, idx, n_idx, stream);
 }
 int32_t mg_set_dof_velocity_target(mg_sim* s, const float* src, int32_t src_host, const int32_t* idx,
                                    int32_t n_idx, void* stream) {
-    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
-    return set_dof_columns(s, src, src_host, 1, s->d_dof_tgt + s->nd, nullptr, idx, n_idx, (hipStream_t)stream);
+    return set_dof_target(s, 1, src, src_host, idx, n_idx, stream);
 }
 int32_t mg_set_dof_actuation_force(mg_sim* s, const float* src, int32_t src_host, const int32_t* idx,
                                    int32_t n_idx, void* stream) {
-    if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
-    return set_dof_columns(s, src, src_host, 1, s->d_dof_tgt + 2 * (size_t)s->nd, nullptr, idx, n_idx,
-                           (hipStream_t)stream);
+    return set_dof_target(s, 2, src, src_host, idx, n_idx, stream);
 }
 
 int32_t mg_set_dof_props(mg_sim* s, const float* props_host) {

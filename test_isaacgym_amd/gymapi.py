@@ -127,7 +127,7 @@ class Gym:
         """One frame (test10_servo_vecenv.py:380): the fused HIP step kernels."""
         h = sim.require_native("gym.simulate")
         N.check(N.lib.mg_simulate(h, sim.stream()), "mg_simulate")
-        sim.held_src = None
+        sim.held_src = []
         sim.epoch += 1
         sim.frame += 1
         sim.time += sim.params.dt
@@ -797,9 +797,9 @@ class Gym:
             rc = fn(sim.require_native(what), t.data_ptr(), host, it.data_ptr(), n, sim.stream())
         else:
             rc = fn(sim.require_native(what), t.data_ptr(), host, None, 0, sim.stream())
-            # a fused root set (MG_FUSE_ROOT_SET) is read by the next simulate:
-            # keep its tensor alive until then
-            sim.held_src = t
+            # a fused set (MG_FUSE_ROOT_SET / MG_FUSE_DOF_TARGETS) is read by the
+            # next simulate: keep its tensor alive until then
+            sim.held_src.append(t)
         if rc != N.MG_OK:
             print("*** migym: %s: %s" % (what, N.last_error()), file=sys.stderr)
             return False

@@ -620,11 +620,14 @@ def test_hipgraph_replay_matches_eager(gym):
     records its kernels into the capture and leaves out its timing events) and
     replayed 50 times gives the same states, bit for bit, as 50 eager steps; so
     does a graph of 5 consecutive steps replayed 10 times (bench.py's chunks)."""
+    from test_isaacgym_amd import _native as N
     n, steps = 256, 50
     outs = []
-    for mode in ("eager", "graph", "graph5"):
+    for mode in ("eager", "graph", "graph5", "graph5_fused"):
         sim, _ = scenes.servo_scene(gym, n)
         gym.prepare_sim(sim)
+        if mode == "graph5_fused":   # MG_FUSE_IN_CAPTURE: the fused set / refresh inside the graph
+            N.lib.mg_set_fusion(sim.native, 1 | 2 | 4 | 8)
         root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
         rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
         acts = scenes.servo_actions(n, 8, DEV, seed=5)
@@ -645,7 +648,7 @@ def test_hipgraph_replay_matches_eager(gym):
             for _ in range(steps):
                 step()
         else:
-            per = 5 if mode == "graph5" else 1
+            per = 5 if mode.startswith("graph5") else 1
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 for _ in range(per):
@@ -659,3 +662,4 @@ def test_hipgraph_replay_matches_eager(gym):
     assert np.all(np.isfinite(outs[0]))
     assert np.array_equal(outs[0], outs[1]), "max |diff| %g" % np.abs(outs[0] - outs[1]).max()
     assert np.array_equal(outs[0], outs[2]), "max |diff| %g" % np.abs(outs[0] - outs[2]).max()
+    assert np.array_equal(outs[0], outs[3]), "max |diff| %g" % np.abs(outs[0] - outs[3]).max()
