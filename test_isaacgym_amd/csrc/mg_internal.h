@@ -35,7 +35,11 @@ struct MgStep {
 // Compact per-template record of the single-shape free-body kernel (built at
 // upload): the MG_TBODY_F_N template floats, then the template's first shape
 // record (type -1 when it has none). Staged in LDS when the table fits.
-#define MG_TREC_N        (MG_TBODY_F_N + MG_SHAPE_STRIDE)
+// compact template record of k_rigid_step1: the template body floats (pad[0] =
+// 1: all its free bodies share one mass row), the first shape record (pad[0] =
+// bounding radius), then that shared mass row (MG_MASS_N floats)
+#define MG_TREC_N        (MG_TBODY_F_N + MG_SHAPE_STRIDE + MG_MASS_N)
+#define MG_TREC_MASS     (MG_TBODY_F_N + MG_SHAPE_STRIDE)
 #define MG_TREC_LDS_MAX  (48 * 1024)
 
 // Kernel argument block of the free-body step (SoA arrays, stride = nb).

@@ -772,11 +772,6 @@ __global__ void __launch_bounds__(64, UPZ ? 3 : 2) k_rigid_step1(MgStep P, MgRig
     Q4 q = q4(Si[3 * si], Si[4 * si], Si[5 * si], Si[6 * si]);
     V3 v = v3(Si[7 * si], Si[8 * si], Si[9 * si]);
     V3 w = v3(Si[10 * si], Si[11 * si], Si[12 * si]);
-    const float* M = A.mass;
-    const float invm = M[0 * nb + b];
-    const V3 invI = v3(M[1 * nb + b], M[2 * nb + b], M[3 * nb + b]);
-    const Q4 iq = q4(M[4 * nb + b], M[5 * nb + b], M[6 * nb + b], M[7 * nb + b]);
-    const V3 com = v3(M[8 * nb + b], M[9 * nb + b], M[10 * nb + b]);
     const int tb = A.body_tmpl[b];
     V3 fext = v3(0.0f, 0.0f, 0.0f), text = v3(0.0f, 0.0f, 0.0f);
     if (A.ext) {
@@ -791,6 +786,20 @@ __global__ void __launch_bounds__(64, UPZ ? 3 : 2) k_rigid_step1(MgStep P, MgRig
     } else {
         T = A.trec + tb * MG_TREC_N;
     }
+    // mass row: the template's own when all its bodies share it (the servo scene:
+    // no per-body loads), else the body's SoA row (migym_capi.cpp upload)
+    float mr[11];
+    if (T[5] != 0.0f) {
+#pragma unroll
+        for (int k = 0; k < 11; ++k) mr[k] = T[MG_TREC_MASS + k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 11; ++k) mr[k] = A.mass[k * nb + b];
+    }
+    const float invm = mr[0];
+    const V3 invI = v3(mr[1], mr[2], mr[3]);
+    const Q4 iq = q4(mr[4], mr[5], mr[6], mr[7]);
+    const V3 com = v3(mr[8], mr[9], mr[10]);
     V3 fsum = v3(0.0f, 0.0f, 0.0f);
     if constexpr (UPZ) {
         rigid_body1<!WIDE>(BasisZ{}, P, T, x, q, v, w, fsum, invm, invI, iq, com, A.ext != nullptr, fext, text, A.hulls);

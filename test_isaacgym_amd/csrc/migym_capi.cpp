@@ -786,6 +786,22 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                 r[MG_TBODY_F_N] = -1.0f;
             }
         }
+        // one mass row per template when all its free bodies share it (the kernel
+        // then reads it from the record instead of 44 B per body)
+        std::vector<int> seen(s->ntb, 0), uniform(s->ntb, 1);
+        for (int b = 0; b < nb; ++b) {
+            if (m->body_kind[b] != MG_BODY_FREE) continue;
+            const int t = m->body_tmpl[b];
+            const float* mr = m->body_mass + (size_t)b * MG_MASS_N;
+            float* r = &trec[(size_t)t * MG_TREC_N];
+            if (!seen[t]) {
+                std::memcpy(r + MG_TREC_MASS, mr, MG_MASS_N * sizeof(float));
+                seen[t] = 1;
+            } else if (std::memcmp(r + MG_TREC_MASS, mr, MG_MASS_N * sizeof(float)) != 0) {
+                uniform[t] = 0;
+            }
+        }
+        for (int t = 0; t < s->ntb; ++t) trec[(size_t)t * MG_TREC_N + 5] = seen[t] && uniform[t] ? 1.0f : 0.0f;
         HIP_TRY(h2d(s->d_trec, trec.data(), trec.size() * sizeof(float)));
     }
     HIP_TRY(h2d(s->d_shapes, m->shapes, (size_t)s->ns * MG_SHAPE_STRIDE * sizeof(float)));
