@@ -217,8 +217,8 @@ hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream
 hipError_t mg_launch_artic_lanes(const MgStep& P, const MgArticArgs& A, hipStream_t s);
 hipError_t mg_launch_gather_rows(const float* soa, int stride, int ncol, const int* ids, int n,
                                  float* aos, hipStream_t s);
-hipError_t mg_launch_gather_rows2(const float* soa, int stride, int ncol, const int* ids_a, int na, float* aos_a,
-                                  const int* ids_b, int nb, float* aos_b, hipStream_t s);
+hipError_t mg_launch_gather_rb_root(const float* soa, int stride, int ncol, const int* perm, int nb, float* rb,
+                                    const int* body_actor, float* root, hipStream_t s);
 hipError_t mg_launch_scatter_rows(const float* aos, int ncol, const int* ids, const int* sel,
                                   int n, int nrows, float* soa, int stride, hipStream_t s);
 hipError_t mg_launch_scatter_dofs(const float* aos, int ncol, const int* actor_dof, const int* sel,

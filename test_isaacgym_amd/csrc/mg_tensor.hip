@@ -22,25 +22,20 @@ __global__ void k_gather_rows(const float* __restrict__ soa, int stride, int nco
     aos[t] = soa[(size_t)f * stride + r];
 }
 
-// two gathers of the same SoA in one launch: rows t < na*ncol go to aos_a
-// through ids_a, the rest to aos_b through ids_b (the fused root + rigid-body
-// refresh, migym_capi.cpp)
-__global__ void k_gather_rows2(const float* __restrict__ soa, int stride, int ncol, const int* __restrict__ ids_a,
-                               int na, float* __restrict__ aos_a, const int* __restrict__ ids_b, int nb,
-                               float* __restrict__ aos_b) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int ta = na * ncol;
-    const int* ids = ids_a;
-    float* aos = aos_a;
-    if (t >= ta) {
-        t -= ta;
-        if (t >= nb * ncol) return;
-        ids = ids_b;
-        aos = aos_b;
-    }
-    const int i = t / ncol;
-    const int f = t - i * ncol;
-    aos[t] = soa[(size_t)f * stride + ids[i]];
+// the rigid-body and actor-root tensors in one launch (the paired refresh,
+// migym_capi.cpp): thread (body g, field f) reads the SoA state once and writes
+// rb[g][f], and root[a][f] when g is actor a's root body (body_actor[g] = a)
+__global__ void k_gather_rb_root(const float* __restrict__ soa, int stride, int ncol, const int* __restrict__ perm,
+                                 int nb, float* __restrict__ rb, const int* __restrict__ body_actor,
+                                 float* __restrict__ root) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nb * ncol) return;
+    const int g = t / ncol;
+    const int f = t - g * ncol;
+    const float v = soa[(size_t)f * stride + perm[g]];
+    rb[t] = v;
+    const int a = body_actor[g];
+    if (a >= 0) root[(size_t)a * ncol + f] = v;
 }
 
 // for k < n: i = sel ? sel[k] : k;  soa[f][ids ? ids[i] : i] = aos[i][f]
@@ -96,12 +91,12 @@ hipError_t mg_launch_gather_rows(const float* soa, int stride, int ncol, const i
     return hipGetLastError();
 }
 
-hipError_t mg_launch_gather_rows2(const float* soa, int stride, int ncol, const int* ids_a, int na, float* aos_a,
-                                  const int* ids_b, int nb, float* aos_b, hipStream_t s) {
-    if (na < 0 || nb < 0 || ncol <= 0 || ((long)na + nb) * ncol >= (1L << 31)) return hipErrorInvalidValue;
-    if (na + nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gather_rows2, dim3(nblocks(((long)na + nb) * ncol, 256)), dim3(256), 0, s, soa, stride, ncol,
-                       ids_a, na, aos_a, ids_b, nb, aos_b);
+hipError_t mg_launch_gather_rb_root(const float* soa, int stride, int ncol, const int* perm, int nb, float* rb,
+                                    const int* body_actor, float* root, hipStream_t s) {
+    if (nb <= 0) return hipSuccess;
+    if (ncol <= 0 || (long)nb * ncol >= (1L << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_gather_rb_root, dim3(nblocks((long)nb * ncol, 256)), dim3(256), 0, s, soa, stride, ncol, perm,
+                       nb, rb, body_actor, root);
     return hipGetLastError();
 }
 

@@ -95,6 +95,7 @@ struct mg_sim {
     float* d_shapes = nullptr;
     float* d_hulls = nullptr;     // convex hull records (MG_SHAPE_CONVEX)
     int* d_actor_root = nullptr;  // [na] internal slot of each actor's root body
+    int* d_body_actor = nullptr;  // [nb] global body -> the actor it is the root of, or -1
     // Step fusion (mg_set_fusion): a device-resident, non-indexed root-state set
     // of a sim whose actor roots are all single-shape free bodies is read by the
     // next simulate's free-body kernel (d_root_row: internal slot -> actor row,
@@ -312,7 +313,7 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
 
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls,
-                    s->d_actor_root, s->d_root_row, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
+                    s->d_actor_root, s->d_root_row, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
                     s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
                     s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
@@ -808,6 +809,12 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     if (m->hulls) HIP_TRY(h2d(s->d_hulls, m->hulls, (size_t)m->num_hull_floats * sizeof(float)));
     HIP_TRY(h2d(s->d_actor_root, root_int.data(), (size_t)na * sizeof(int)));
     {
+        std::vector<int> body_actor(nb, -1);
+        for (int a = 0; a < na; ++a) body_actor[m->actor_root_body[a]] = a;
+        HIP_TRY(dalloc(&s->d_body_actor, (size_t)std::max(nb, 1)));
+        HIP_TRY(h2d(s->d_body_actor, body_actor.data(), (size_t)nb * sizeof(int)));
+    }
+    {
         // fusable root sets: every actor root is a single-shape free body of the
         // free-body kernel (internal slots 0..nf1-1), and that kernel steps all
         // free bodies (no multi-shape ones, no articulations, no coupled envs)
@@ -1054,8 +1061,8 @@ int32_t mg_refresh_actor_root_state(mg_sim* s, float* dst, int32_t dst_host, voi
     if (!dst_host && dst && dst == s->bind_root && s->bind_rb && (s->fusion & MG_FUSE_REFRESH) &&
         fuse_here(s, cid) && s->na > 0) {
         // the bound root and rigid-body tensors in one launch
-        HIP_TRY(mg_launch_gather_rows2(s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, dst, s->d_perm, s->nb,
-                                       s->bind_rb, st));
+        HIP_TRY(mg_launch_gather_rb_root(s->d_state, s->nb, MG_STATE_N, s->d_perm, s->nb, s->bind_rb, s->d_body_actor,
+                                         dst, st));
         s->rb_gen = s->state_gen;
         s->rb_cap = cid;
         return MG_OK;
