@@ -592,8 +592,9 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
     for (d = 0; d < D; ++d) { dof[(d0 + d) * 2 + 0] = q[d]; dof[(d0 + d) * 2 + 1] = qd[d]; }
     for (l = 0; l < L; ++l) {
         const int p = LI[l * MG_LINK_I_N + 0], jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
-        const float* M = m->body_mass + (size_t)(b0 + l) * MG_MASS_N;
-        float* so = state + (size_t)(b0 + l) * MG_STATE_N;
+        const int bl = LI[l * MG_LINK_I_N + 3];          /* -1: virtual link of a ball joint */
+        const float* M = link_mass_(m, LI, b0, l);
+        float* so = bl >= 0 ? state + (size_t)(b0 + bl) * MG_STATE_N : NULL;
         v3_t ww, vw, com = V(M[8], M[9], M[10]);
         if (p < 0) {
             ql[l] = q0; xl[l] = x0; v[l] = sv0();
@@ -605,15 +606,16 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
             xl[l] = add3(xl[p], qrot_(ql[p], rr));
             v[l] = svadd_(xmot_(mt_(qmat_(qrel)), rr, v[p]), svmul_(s, qdj));
         }
+        if (!so) continue;
         ww = qrot_(ql[l], v[l].w);
         vw = qrot_(ql[l], add3(v[l].v, cross3(v[l].w, com)));
         so[0] = xl[l].x; so[1] = xl[l].y; so[2] = xl[l].z;
         so[3] = ql[l].x; so[4] = ql[l].y; so[5] = ql[l].z; so[6] = ql[l].w;
         so[7] = vw.x; so[8] = vw.y; so[9] = vw.z;
         so[10] = ww.x; so[11] = ww.y; so[12] = ww.z;
-        cforce[(size_t)(b0 + l) * 3 + 0] = 0.0f;
-        cforce[(size_t)(b0 + l) * 3 + 1] = 0.0f;
-        cforce[(size_t)(b0 + l) * 3 + 2] = 0.0f;
+        cforce[(size_t)(b0 + bl) * 3 + 0] = 0.0f;
+        cforce[(size_t)(b0 + bl) * 3 + 1] = 0.0f;
+        cforce[(size_t)(b0 + bl) * 3 + 2] = 0.0f;
     }
     return 0;
 }

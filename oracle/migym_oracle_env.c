@@ -541,6 +541,14 @@ static float dot6_(const float* a, const float* b) {   /* fused chain, as mg_wor
 static sv_t sv6_(const float* a) { return SVc(V(a[0], a[1], a[2]), V(a[3], a[4], a[5])); }
 static void put6_(float* a, sv_t s) { a[0] = s.w.x; a[1] = s.w.y; a[2] = s.w.z; a[3] = s.v.x; a[4] = s.v.y; a[5] = s.v.z; }
 
+/* link l's mass row; a virtual link (ball joint: tmpl_link_i body -1) has none —
+ * zero mass and inertia, identity principal frame (mg_env.hip k_artic_lanes) */
+static const float* link_mass_(const mg_model* m, const int* LI, int b0, int l) {
+    static const float zero[MG_MASS_N] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    const int bl = LI[l * MG_LINK_I_N + 3];
+    return bl < 0 ? zero : m->body_mass + (size_t)(b0 + bl) * MG_MASS_N;
+}
+
 /* world-frame spatial inertia about O (mg_env.hip world_inertia) */
 static void world_inertia_(const float* M, q4_t ql, v3_t xl, v3_t O, float* I) {
     const float m = M[11];
@@ -657,7 +665,7 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
                     else x = SVc(V(0.0f, 0.0f, 0.0f), zl[l]);
                 }
                 put6_(xi[l], x);
-                world_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N, ql[l], xl[l], x0, Iw[l]);
+                world_inertia_(link_mass_(m, LI, b0, l), ql[l], xl[l], x0, Iw[l]);
             }
             for (i = 0; i < 6; ++i) va[0][i] = fb ? u[D + i] : 0.0f;
             for (l = 1; l < L; ++l) {
@@ -675,9 +683,9 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
                 put6_(ccv[l], crm_(v, vJ));
                 {
                     sv_t pb = crf_(v, sv6_(Iv));
-                    if (ext) {
-                        const float* x = ext + (size_t)(b0 + l) * 6;
-                        const float* M = m->body_mass + (size_t)(b0 + l) * MG_MASS_N;
+                    if (ext && LI[l * MG_LINK_I_N + 3] >= 0) {
+                        const float* x = ext + (size_t)(b0 + LI[l * MG_LINK_I_N + 3]) * 6;
+                        const float* M = link_mass_(m, LI, b0, l);
                         const v3_t f = V(x[0], x[1], x[2]), t = V(x[3], x[4], x[5]);
                         const v3_t c = sub3(add3(xl[l], qrot_(ql[l], V(M[8], M[9], M[10]))), x0);
                         pb = SVc(sub3(pb.w, add3(t, cross3(c, f))), sub3(pb.v, f));
@@ -991,7 +999,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         }
         /* ---- 3. rows */
         if (link_rows) {
-            for (l = 0; l < L; ++l) world_inertia_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N, ql[l], xl[l], x0, Iw[l]);
+            for (l = 0; l < L; ++l) world_inertia_(link_mass_(m, LI, b0, l), ql[l], xl[l], x0, Iw[l]);
             for (l = L - 1; l >= 1; --l) {
                 const int p = LI[l * MG_LINK_I_N + 0];
                 if (p > 0 || (fb && p == 0))
@@ -1286,6 +1294,12 @@ static int classify_envs_(const mg_model* m, oenv_t* envs, char* owned) {
                 if (ai[0] == r0) { ev->art_body = r0; ev->art_dof = ai[1]; ev->art_tmpl = ai[2]; }
             }
             if (ev->art_body < 0) { n = -1; break; }
+            {   /* ball joints (virtual links) step in the articulation kernel only */
+                const int* ti = m->artic_tmpl_i + (size_t)ev->art_tmpl * MG_ATMPL_I_N;
+                for (i = 0; i < ti[1]; ++i)
+                    if (m->tmpl_link_i[(size_t)(ti[0] + i) * MG_LINK_I_N + 3] != i) n = -1;
+                if (n < 0) break;
+            }
             owned[r0] = 1;
         }
         ev->nf = nf;

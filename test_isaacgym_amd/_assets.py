@@ -250,7 +250,15 @@ class Joint:
 
     @property
     def has_dof(self):
-        return self.type in (T.JOINT_REVOLUTE, T.JOINT_PRISMATIC)
+        return self.ndof > 0
+
+    @property
+    def ndof(self):
+        """DOFs of the joint: 1 revolute / prismatic, 3 spherical (rotations about the
+        joint frame's x, y, z axes), 0 otherwise."""
+        if self.type in (T.JOINT_REVOLUTE, T.JOINT_PRISMATIC):
+            return 1
+        return 3 if self.type == T.JOINT_BALL else 0
 
 
 class MassProps:
@@ -288,22 +296,34 @@ class Asset:
     # ---- derived structure
     @property
     def dof_joints(self):
-        return [j for j in self.joints if j.has_dof]
+        """The joint of every DOF, in DOF order (a spherical joint three times)."""
+        return [j for j in self.joints for _ in range(j.ndof)]
+
+    @property
+    def dof_names(self):
+        """DOF names: the joint's name; a spherical joint's three DOFs get
+        `<joint>_0/_1/_2` (x, y, z of its frame; naming unpinned by the reference)."""
+        out = []
+        for j in self.joints:
+            if j.ndof == 1:
+                out.append(j.name)
+            else:
+                out.extend("%s_%d" % (j.name, k) for k in range(j.ndof))
+        return out
 
     @property
     def num_dofs(self):
-        return len(self.dof_joints)
+        return sum(j.ndof for j in self.joints)
 
     def dof_of_body(self, b):
-        """local DOF index driven by body b's joint, or -1."""
+        """first local DOF driven by body b's joint, or -1."""
         if b == 0:
             return -1
         d = 0
         for k, j in enumerate(self.joints):
             if k + 1 == b:
                 return d if j.has_dof else -1
-            if j.has_dof:
-                d += 1
+            d += j.ndof
         return -1
 
     @property
@@ -643,7 +663,8 @@ def _geometry_shapes(col, urdf_dir, asset_root, options, warnings):
 
 
 _URDF_JOINT = {"revolute": T.JOINT_REVOLUTE, "continuous": T.JOINT_REVOLUTE, "prismatic": T.JOINT_PRISMATIC,
-               "fixed": T.JOINT_FIXED, "floating": T.JOINT_FLOATING, "planar": T.JOINT_PLANAR}
+               "fixed": T.JOINT_FIXED, "floating": T.JOINT_FLOATING, "planar": T.JOINT_PLANAR,
+               "spherical": T.JOINT_BALL}
 
 
 def load_urdf(asset_root, filename, options):

@@ -223,6 +223,14 @@ class Sim:
             if j.type == T.JOINT_REVOLUTE:
                 s, c = np.sin(0.5 * qj), np.cos(0.5 * qj)
                 qrel = _qmul(j.q, np.array([j.axis[0] * s, j.axis[1] * s, j.axis[2] * s, c]))
+            elif j.type == T.JOINT_BALL:
+                # rotations about the joint frame's x, y, z in turn (the three
+                # packed links of build_model)
+                for k in range(3):
+                    th = float(a.dof_state[d + k, 0])
+                    e = np.zeros(4)
+                    e[k], e[3] = np.sin(0.5 * th), np.cos(0.5 * th)
+                    qrel = _qmul(qrel, e)
             elif j.type == T.JOINT_PRISMATIC:
                 rr = j.p + _qmat(j.q) @ (j.axis * qj)
             pp, pq = ps[j.parent], qs[j.parent]
@@ -326,19 +334,40 @@ class Sim:
                 if id(asset) not in atmpl_key:
                     atmpl_key[id(asset)] = len(atmpl)
                     atmpl.append([len(lf), len(asset.bodies), asset.num_dofs, 1 if opts.fix_base_link else 0])
+                    nl0 = len(lf)
+                    link_of = []          # body -> its kernel link (local)
                     for b in range(len(asset.bodies)):
-                        f = np.zeros(N.MG_LINK_F_N, dtype=np.float32)
-                        ii = [-1, 0, -1, 0]
-                        if b > 0:
-                            j = asset.joints[b - 1]
+                        if b == 0:
+                            lf.append(np.zeros(N.MG_LINK_F_N, dtype=np.float32))
+                            li.append([-1, 0, -1, 0])
+                            link_of.append(0)
+                            continue
+                        j = asset.joints[b - 1]
+                        d = asset.dof_of_body(b)
+                        parent = link_of[j.parent]
+                        if j.type == T.JOINT_BALL:
+                            # three revolute links about the joint frame's x, y, z:
+                            # two virtual (body -1), then the child body
+                            for k in range(3):
+                                f = np.zeros(N.MG_LINK_F_N, dtype=np.float32)
+                                f[3:7] = (0, 0, 0, 1)
+                                if k == 0:
+                                    f[0:3] = j.p
+                                    f[3:7] = j.q
+                                f[7 + k] = 1.0
+                                lf.append(f)
+                                li.append([parent, T.JOINT_REVOLUTE, d + k, b if k == 2 else -1])
+                                parent = len(lf) - 1 - nl0
+                        else:
+                            f = np.zeros(N.MG_LINK_F_N, dtype=np.float32)
                             f[0:3] = j.p
                             f[3:7] = j.q
                             f[7:10] = j.axis
-                            ii = [j.parent, j.type if j.type in (T.JOINT_FIXED, T.JOINT_REVOLUTE,
-                                                                 T.JOINT_PRISMATIC) else T.JOINT_FIXED,
-                                  asset.dof_of_body(b), 0]
-                        lf.append(f)
-                        li.append(ii)
+                            li.append([parent, j.type if j.type in (T.JOINT_FIXED, T.JOINT_REVOLUTE,
+                                                                    T.JOINT_PRISMATIC) else T.JOINT_FIXED, d, b])
+                            lf.append(f)
+                        link_of.append(len(lf) - 1 - nl0)
+                    atmpl[-1][1] = len(lf) - nl0
                 artic.append([a.global_body, a.global_dof, atmpl_key[id(asset)], 0])
         self.model_arrays = dict(
             body_state0=st, body_mass=mass, body_kind=kind, body_tmpl=btmpl,

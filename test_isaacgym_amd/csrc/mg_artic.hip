@@ -103,7 +103,14 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
             else x = sv(v3(0.0f, 0.0f, 0.0f), z);
         }
         put6(S.xi[ln], x);
-        if (mm && (ln > 0 || fb)) world_inertia(load_link(A.mass, nb, b0 + ln), S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
+        // a virtual link (ball joint, body -1) has no mass
+        if (mm && (ln > 0 || fb)) {
+            if (li[3] >= 0) {
+                world_inertia(load_link(A.mass, nb, b0 + li[3]), S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
+            } else {
+                for (int k = 0; k < 36; ++k) S.Iw[ln][k] = 0.0f;
+            }
+        }
     }
     __syncthreads();
     // the link whose joint is DOF ln
@@ -115,17 +122,20 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
             jrev = A.link_i[l * MG_LINK_I_N + 1] == MG_JOINT_REVOLUTE;
         }
     if (jac && live) {
-        float* J = jac + (size_t)e * (L - row0) * 6 * NC;
+        // rows: the template's bodies (virtual links of ball joints have none)
+        float* J = jac + (size_t)e * (A.nbl - row0) * 6 * NC;
         if (ln < D && jl > 0) {
             // column R0 + ln of every link's 6 x NC block: [linear at the link origin; angular]
             const V3 z = S.zl[jl], xj = S.xl[jl];
             for (int l = row0; l < L; ++l) {
+                const int bl = A.link_i[l * MG_LINK_I_N + 3];
+                if (bl < 0) continue;
                 V3 lin = v3(0.0f, 0.0f, 0.0f), ang = v3(0.0f, 0.0f, 0.0f);
                 if ((S.amask[l] >> ln) & 1) {
                     if (jrev) { lin = vcross(z, vsub(S.xl[l], xj)); ang = z; }
                     else lin = z;
                 }
-                float* Jl = J + (size_t)(l - row0) * 6 * NC + R0 + ln;
+                float* Jl = J + (size_t)(bl - row0) * 6 * NC + R0 + ln;
                 Jl[0 * NC] = lin.x; Jl[1 * NC] = lin.y; Jl[2 * NC] = lin.z;
                 Jl[3 * NC] = ang.x; Jl[4 * NC] = ang.y; Jl[5 * NC] = ang.z;
             }
@@ -135,9 +145,11 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
             const int k = ln - D;
             const V3 ek = v3(k % 3 == 0 ? 1.0f : 0.0f, k % 3 == 1 ? 1.0f : 0.0f, k % 3 == 2 ? 1.0f : 0.0f);
             for (int l = 0; l < L; ++l) {
+                const int bl = A.link_i[l * MG_LINK_I_N + 3];
+                if (bl < 0) continue;
                 V3 lin = ek, ang = v3(0.0f, 0.0f, 0.0f);
                 if (k >= 3) { lin = vcross(ek, vsub(S.xl[l], x0)); ang = ek; }
-                float* Jl = J + (size_t)l * 6 * NC + k;
+                float* Jl = J + (size_t)bl * 6 * NC + k;
                 Jl[0 * NC] = lin.x; Jl[1 * NC] = lin.y; Jl[2 * NC] = lin.z;
                 Jl[3 * NC] = ang.x; Jl[4 * NC] = ang.y; Jl[5 * NC] = ang.z;
             }
@@ -203,7 +215,8 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
 
 // refresh_jacobian_tensors / refresh_mass_matrix_tensors
 // (examples/franka_cube_ik_osc.py:305-316,345-346): for a fixed base
-//   J: (instances, L-1, 6, D): link l = 1..L-1, rows [linear xyz of the link
+//   J: (instances, B-1, 6, D): body l = 1..B-1 (B bodies: the template's links
+//      minus the virtual links of ball joints), rows [linear xyz of the link
 //      frame origin, angular xyz] in the world frame, column d = DOF d;
 //   M: (instances, D, D): joint-space inertia without joint armature;
 // for a floating base (D + 6 <= 16) the 6 root columns come first — linear

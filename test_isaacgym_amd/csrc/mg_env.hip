@@ -319,9 +319,10 @@ __device__ __forceinline__ void aba_vp(const MgEnvArgs& A, EnvLds& S, bool act, 
         for (int i = 0; i < 6; ++i) Iv[i] = dot6(&S.Iw[ln][i * 6], S.va[ln]);
         put6(S.cc[ln], crm(v, vJ));
         SV pb = crf(v, sv6(Iv));
-        if (A.ext) {
+        const int bl = A.link_i[ln * MG_LINK_I_N + 3];      // -1: virtual link
+        if (A.ext && bl >= 0) {
             // world force f and torque t at the link COM: the wrench about x0
-            const int b = b0 + ln, nb = A.nb;
+            const int b = b0 + bl, nb = A.nb;
             const V3 f = v3(A.ext[0 * nb + b], A.ext[1 * nb + b], A.ext[2 * nb + b]);
             const V3 t = v3(A.ext[3 * nb + b], A.ext[4 * nb + b], A.ext[5 * nb + b]);
             const V3 c = vsub(vadd(S.xl[ln], qrot(S.ql[ln], lk.com)), x0);
@@ -1287,8 +1288,11 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
         if (A.tvel_w) A.tvel_w[gd] = dc.tvel;
         if (A.force_w) A.force_w[gd] = dc.force;
     }
+    // link ln's body (-1: a virtual link of a ball joint: no mass, no state row)
+    const int bl = ln < LA ? A.link_i[ln * MG_LINK_I_N + 3] : -1;
     LinkC lk = {};
-    if (ln < L) lk = load_link(A.mass, nb, b0 + ln);
+    lk.iq = q4(0.0f, 0.0f, 0.0f, 1.0f);
+    if (ln < L && bl >= 0) lk = load_link(A.mass, nb, b0 + bl);
 
     for (int st = 0; st < P.substeps; ++st) {
         S.q[ln] = qv;
@@ -1379,8 +1383,8 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
         }
     }
     __syncthreads();
-    if (ln < L) {
-        const int b = b0 + ln;
+    if (ln < L && bl >= 0) {
+        const int b = b0 + bl;
         const SV vl = sv6(vs + 6 * ln);
         const Q4 ql = S.ql[ln];
         const V3 xl = S.xl[ln];

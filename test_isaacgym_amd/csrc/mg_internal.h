@@ -70,6 +70,7 @@ struct MgArticArgs {
     const int*   artic_i;     // [na][4] first_body, first_dof, tmpl, pad
     int          tmpl;        // template id handled by this launch
     int          nl, ndof;    // links / dofs of the template
+    int          nbl;         // bodies of the template (nl minus virtual links; Jacobian rows)
     int          fixed_base;
     int          chain;       // fixed base, link l's parent l - 1 and DOF l - 1 (k_artic_chain)
     const float* link_f;      // [nl][16] template link constants

@@ -58,6 +58,7 @@ std::vector<T> to_soa(const T* aos, int n, int ncol) {
 struct ArticGroup {
     int chain;                     // serial chain with one DOF per moving link (MgArticArgs.chain)
     int tmpl, first_link, nl, ndof, fixed_base;
+    int nbody;                     // bodies per instance (nl minus the virtual links of ball joints)
     int offset, count;             // into the template-sorted instance list (all instances)
     int step_offset, step_count;   // into the list stepped by k_artic_step (uncoupled envs)
 };
@@ -481,6 +482,13 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                 art_nl = m->artic_tmpl_i[t * MG_ATMPL_I_N + 1];
                 art_nd = m->artic_tmpl_i[t * MG_ATMPL_I_N + 2];
                 art_fb = m->artic_tmpl_i[t * MG_ATMPL_I_N + 3] ? 0 : 1;
+                const int fl = m->artic_tmpl_i[t * MG_ATMPL_I_N + 0];
+                if (fl < 0 || art_nl < 1 || fl + art_nl > m->num_tmpl_links)
+                    return fail(MG_ERR_ARG, "env %d: bad articulation template %d", e, t);
+                for (int l = 0; l < art_nl; ++l)
+                    if (m->tmpl_link_i[(size_t)(fl + l) * MG_LINK_I_N + 3] != l)
+                        return fail(MG_ERR_UNSUPPORTED, "env %d: ball joints (virtual links) in the coupled per-env "
+                                    "step (contacts between actors, or a floating base)", e);
             }
             if (art_nd + 6 * art_fb + 6 * (int)fr.size() > MG_ENV_G)
                 return fail(MG_ERR_UNSUPPORTED, "env %d: %d DOFs%s + %zu free bodies exceed the %d velocity slots of "
@@ -644,13 +652,22 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         if (g.nl < 1 || g.nl > MG_MAX_LINKS || g.ndof > g.nl || g.ndof > MG_MAX_DOFS || g.first_link < 0 ||
             g.first_link + g.nl > s->ntl)
             return fail(MG_ERR_UNSUPPORTED, "articulation template %d: %d links / %d dofs unsupported", t, g.nl, g.ndof);
+        g.nbody = 0;
         for (int l = 0; l < g.nl; ++l) {
             const int* li = m->tmpl_link_i + (size_t)(g.first_link + l) * MG_LINK_I_N;
             if (li[0] >= l || (l > 0 && li[0] < 0) || (l == 0 && li[0] != -1))
                 return fail(MG_ERR_ARG, "articulation template %d: links not in topological order", t);
             if (li[2] >= g.ndof) return fail(MG_ERR_ARG, "articulation template %d: bad dof index", t);
+            // real links carry bodies 0, 1, 2, ... in link order; virtual links
+            // (the first two of a ball joint) are revolute with a DOF and no body
+            if (li[3] >= 0) {
+                if (li[3] != g.nbody) return fail(MG_ERR_ARG, "articulation template %d: link bodies out of order", t);
+                g.nbody++;
+            } else if (l == 0 || li[1] != MG_JOINT_REVOLUTE || li[2] < 0) {
+                return fail(MG_ERR_ARG, "articulation template %d: bad virtual link %d", t, l);
+            }
         }
-        g.chain = g.fixed_base && g.ndof == g.nl - 1;
+        g.chain = g.fixed_base && g.ndof == g.nl - 1 && g.nbody == g.nl;
         for (int l = 1; l < g.nl && g.chain; ++l) {
             const int* li = m->tmpl_link_i + (size_t)(g.first_link + l) * MG_LINK_I_N;
             g.chain = li[0] == l - 1 && li[2] == l - 1 && (li[1] == MG_JOINT_REVOLUTE || li[1] == MG_JOINT_PRISMATIC);
@@ -662,14 +679,17 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         for (int k = 0; k < m->num_artics; ++k) {
             const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;
             if (ai[2] != t) continue;
-            if (ai[0] < 0 || ai[0] + g.nl > nb || ai[1] < 0 || ai[1] + g.ndof > nd)
+            if (ai[0] < 0 || ai[0] + g.nbody > nb || ai[1] < 0 || ai[1] + g.ndof > nd)
                 return fail(MG_ERR_ARG, "articulation %d out of range", k);
             for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_sorted.push_back(ai[j]);
             if (!coupled_body[ai[0]]) {
                 for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_step.push_back(ai[j]);
                 g.step_count++;
             }
-            for (int l = 0; l < g.nl; ++l) {
+            if (coupled_body[ai[0]] && g.nbody != g.nl)
+                return fail(MG_ERR_UNSUPPORTED, "articulation %d: ball joints in the coupled per-env step (an env "
+                            "with contacts between actors, or a floating base)", k);
+            for (int l = 0; l < g.nbody; ++l) {
                 if (placed[ai[0] + l]) return fail(MG_ERR_ARG, "articulation %d overlaps another body", k);
                 placed[ai[0] + l] = 1;
                 order.push_back(ai[0] + l);
@@ -908,7 +928,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         MgArticArgs A{};
         A.na = g.step_count; A.nb = s->nb; A.nd = s->nd;
         A.artic_i = s->d_artic_step + (size_t)g.step_offset * MG_ARTIC_I_N;
-        A.tmpl = g.tmpl; A.nl = g.nl; A.ndof = g.ndof; A.fixed_base = g.fixed_base; A.chain = g.chain;
+        A.tmpl = g.tmpl; A.nl = g.nl; A.ndof = g.ndof; A.fixed_base = g.fixed_base; A.chain = g.chain; A.nbl = g.nbody;
         A.link_f = s->d_link_f + (size_t)g.first_link * MG_LINK_F_N;
         A.link_i = s->d_link_i + (size_t)g.first_link * MG_LINK_I_N;
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl; A.tbf = s->d_tbf;
@@ -1217,7 +1237,7 @@ static int refresh_jac_mm(mg_sim* s, int32_t tmpl, float* jdst, float* mdst, int
     if (nc > 16) return fail(MG_ERR_UNSUPPORTED, "jacobian / mass matrix of more than 16 generalized velocities");
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
-    const size_t jper = (size_t)(g->nl - (g->fixed_base ? 1 : 0)) * 6 * nc, mper = (size_t)nc * nc;
+    const size_t jper = (size_t)(g->nbody - (g->fixed_base ? 1 : 0)) * 6 * nc, mper = (size_t)nc * nc;
     const size_t jtot = jdst ? jper * g->count : 0, mtot = mdst ? mper * g->count : 0;
     float* jout = jdst;
     float* mout = mdst;
@@ -1230,7 +1250,7 @@ static int refresh_jac_mm(mg_sim* s, int32_t tmpl, float* jdst, float* mdst, int
     MgArticArgs A{};
     A.na = g->count; A.nb = s->nb; A.nd = s->nd;
     A.artic_i = s->d_artic + (size_t)g->offset * MG_ARTIC_I_N;
-    A.tmpl = g->tmpl; A.nl = g->nl; A.ndof = g->ndof; A.fixed_base = g->fixed_base;
+    A.tmpl = g->tmpl; A.nl = g->nl; A.ndof = g->ndof; A.fixed_base = g->fixed_base; A.nbl = g->nbody;
     A.link_f = s->d_link_f + (size_t)g->first_link * MG_LINK_F_N;
     A.link_i = s->d_link_i + (size_t)g->first_link * MG_LINK_I_N;
     A.state = s->d_state; A.mass = s->d_mass;

@@ -235,20 +235,20 @@ class Gym:
         return asset.num_dofs
 
     def get_asset_dof_name(self, asset, i):
-        return asset.dof_joints[i].name
+        return asset.dof_names[i]
 
     def get_asset_dof_names(self, asset):
-        return [j.name for j in asset.dof_joints]
+        return asset.dof_names
 
     def get_asset_dof_dict(self, asset):
-        return {j.name: i for i, j in enumerate(asset.dof_joints)}
+        return {n: i for i, n in enumerate(asset.dof_names)}
 
     def find_asset_dof_index(self, asset, name):
         return self.get_asset_dof_dict(asset).get(name, _T.INVALID_HANDLE)
 
     def get_asset_dof_type(self, asset, i):
         j = asset.dof_joints[i]
-        return _T.DOF_ROTATION if j.type == _T.JOINT_REVOLUTE else _T.DOF_TRANSLATION
+        return _T.DOF_ROTATION if j.type in (_T.JOINT_REVOLUTE, _T.JOINT_BALL) else _T.DOF_TRANSLATION
 
     def get_asset_dof_properties(self, asset):
         return asset.dof_props.copy()
@@ -385,10 +385,10 @@ class Gym:
         return self._actor(env, handle).num_dofs
 
     def get_actor_dof_names(self, env, handle):
-        return [j.name for j in self._actor(env, handle).asset.dof_joints]
+        return self._actor(env, handle).asset.dof_names
 
     def get_actor_dof_dict(self, env, handle):
-        return {j.name: i for i, j in enumerate(self._actor(env, handle).asset.dof_joints)}
+        return {n: i for i, n in enumerate(self._actor(env, handle).asset.dof_names)}
 
     def get_actor_dof_handle(self, env, handle, index):
         a = self._actor(env, handle)

@@ -72,17 +72,22 @@ class Articulation:
             j = int(self.li[j, 0])
         return J
 
+    def bodies(self):
+        """(link, local body) of the real links (a ball joint's two virtual
+        links have body -1: no Jacobian row, no mass)."""
+        return [(l, int(self.li[l, 3])) for l in range(self.L) if int(self.li[l, 3]) >= 0]
+
     def jacobian(self, base_pose, q):
-        """(L-1, 6, D): link origins, as mg_refresh_jacobian."""
+        """(B-1, 6, D): body origins, as mg_refresh_jacobian."""
         ps, Rs, zs = self.fk(base_pose, q)
-        return np.stack([self.point_jacobian(ps, zs, l, ps[l]) for l in range(1, self.L)])
+        return np.stack([self.point_jacobian(ps, zs, l, ps[l]) for l, _ in self.bodies()[1:]])
 
     def mass_matrix(self, base_pose, q, first_body):
         """(D, D) joint-space inertia (no armature)."""
         ps, Rs, zs = self.fk(base_pose, q)
         M = np.zeros((self.D, self.D))
-        for l in range(1, self.L):
-            mrow = self.A["body_mass"][first_body + l].astype(np.float64)
+        for l, b in self.bodies()[1:]:
+            mrow = self.A["body_mass"][first_body + b].astype(np.float64)
             m, com, iq, invI = mrow[11], mrow[8:11], mrow[4:8], mrow[1:4]
             Ip = np.diag([1.0 / x if x > 0 else 0.0 for x in invI])
             Rl = Rs[l] @ qmat(iq)
@@ -110,14 +115,14 @@ class Articulation:
     def jacobian_fb(self, base_pose, q):
         """(L, 6, 6 + D): every link origin, the root link included."""
         ps, Rs, zs = self.fk(base_pose, q)
-        return np.stack([self.point_jacobian_fb(ps, zs, l, ps[l]) for l in range(self.L)])
+        return np.stack([self.point_jacobian_fb(ps, zs, l, ps[l]) for l, _ in self.bodies()])
 
     def mass_matrix_fb(self, base_pose, q, first_body):
         """(6 + D, 6 + D) inertia in the same generalized velocities (no armature)."""
         ps, Rs, zs = self.fk(base_pose, q)
         M = np.zeros((6 + self.D, 6 + self.D))
-        for l in range(self.L):
-            mrow = self.A["body_mass"][first_body + l].astype(np.float64)
+        for l, b in self.bodies():
+            mrow = self.A["body_mass"][first_body + b].astype(np.float64)
             m, com, iq, invI = mrow[11], mrow[8:11], mrow[4:8], mrow[1:4]
             Ip = np.diag([1.0 / x if x > 0 else 0.0 for x in invI])
             Rl = Rs[l] @ qmat(iq)

@@ -110,3 +110,25 @@ def test_test11_camerazoom_setup(monkeypatch):
     cam = envs[1].cameras[29]
     assert cam.props.horizontal_fov == 30 and cam.props.width == 1600 and cam.body == 0
     assert (cam.local.p.x, cam.local.p.y, cam.local.p.z) == (5, 0, 0)
+
+
+@pytest.mark.skipif(has_gpu(), reason="CPU-container variant")
+def test_test13_spherical_joint_setup(monkeypatch):
+    """test13_camera_spherical_joint.py: 3 prismatic + 1 spherical joint, the DOF
+    state viewed as (num_envs, 6, 1) (:266-269); the spherical joint is 3 rotation
+    DOFs packed as three kernel links (two virtual)."""
+    from test_isaacgym_amd import gymapi as G
+    ns, err = _exec_script(os.path.join(REFERENCE, "test13_camera_spherical_joint.py"), REFERENCE, monkeypatch)
+    assert err is not None
+    gym, asset, sim = ns["gym"], ns["asset"], ns["sim"]
+    assert gym.get_asset_rigid_body_count(asset) == 5
+    assert gym.get_asset_dof_count(asset) == 6
+    assert [gym.get_asset_dof_type(asset, i) for i in range(6)] == [G.DOF_TRANSLATION] * 3 + [G.DOF_ROTATION] * 3
+    assert gym.get_asset_joint_type(asset, 3) == G.JOINT_BALL
+    assert tuple(ns["dof_pos"].shape) == (ns["num_envs"], 6, 1)
+    A = sim.model_arrays
+    li = A["tmpl_link_i"]
+    assert li[:, 3].tolist() == [0, 1, 2, 3, -1, -1, 4]          # bodies; two virtual links
+    assert li[4:, 2].tolist() == [3, 4, 5] and li[4:, 0].tolist() == [3, 4, 5]
+    assert A["artic_tmpl_i"][0, 1] == 7 and A["artic_tmpl_i"][0, 2] == 6
+    assert gym.get_sim_rigid_body_count(sim) == 5 * ns["num_envs"]
