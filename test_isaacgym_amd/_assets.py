@@ -981,9 +981,9 @@ def load_mjcf(asset_root, filename, options):
             if hinge:
                 ja = defaults.attrs(hinge[0], hinge[0].get("class", cls))
                 typ = ja.get("type", "hinge")
-                if typ not in ("hinge", "slide"):
+                if typ not in ("hinge", "slide", "ball"):
                     raise ValueError("MJCF %s: joint type %s unsupported" % (path, typ))
-                j.type = T.JOINT_REVOLUTE if typ == "hinge" else T.JOINT_PRISMATIC
+                j.type = {"hinge": T.JOINT_REVOLUTE, "slide": T.JOINT_PRISMATIC, "ball": T.JOINT_BALL}[typ]
                 ax = np.array(_mj_floats(ja.get("axis"), (0, 0, 1)), dtype=np.float64)
                 j.axis = ax / np.linalg.norm(ax)
                 anchor = np.array(_mj_floats(ja.get("pos"), (0, 0, 0)), dtype=np.float64)
@@ -992,7 +992,7 @@ def load_mjcf(asset_root, filename, options):
                     j.p = bp + _qmat(bq) @ anchor
                 rng = _mj_floats(ja.get("range"))
                 limited = ja.get("limited", "auto")
-                if rng is not None and limited in ("true", "auto"):
+                if rng is not None and limited in ("true", "auto") and typ != "ball":   # a cone limit: not modelled
                     s = k_ang if typ == "hinge" else 1.0
                     j.has_limits, j.lower, j.upper = True, rng[0] * s, rng[1] * s
                 j.damping = float(ja.get("damping", 0.0))

@@ -122,6 +122,27 @@ def test_layout_and_names(gym, tmp_path):
     assert A["tmpl_link_f"][4:7, 7:10].tolist() == np.eye(3).tolist()
 
 
+def test_mjcf_ball_joint(gym, tmp_path):
+    """MJCF <joint type="ball"> (assets/mjcf/spherical_joint.xml is test13's
+    commented-out alternative, :39): three rotation DOFs, the same packing."""
+    xml = ('<mujoco><worldbody><body name="base" pos="0 0 1"><geom type="box" size="0.1 0.1 0.1"/>'
+           '<body name="bob" pos="0 0 -0.2"><joint name="sph" type="ball" range="0 90"/>'
+           '<geom type="sphere" size="0.05" pos="0 0 -0.3"/></body></body></worldbody></mujoco>')
+    with open(os.path.join(str(tmp_path), "b.xml"), "w") as f:
+        f.write(xml)
+    sim = _sim(gym)
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    asset = gym.load_asset(sim, str(tmp_path), "b.xml", opts)
+    assert gym.get_asset_dof_count(asset) == 3
+    assert gym.get_asset_dof_names(asset) == ["sph_0", "sph_1", "sph_2"]
+    assert not gym.get_asset_dof_properties(asset)["hasLimits"].any()
+    env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 2), 1)
+    gym.create_actor(env, asset, gymapi.Transform(), "b", 0, 1)
+    A = sim.build_model()
+    assert A["tmpl_link_i"][:, 3].tolist() == [0, -1, -1, 1]
+
+
 def test_rest_without_gravity_is_static(gym, tmp_path):
     """test13's setting (gravity 0, no drives): nothing moves, bit for bit."""
     sim, _ = _scene(gym, str(tmp_path), 2, _urdf(str(tmp_path), "b.urdf", bob_com=(0, 0, 0)), gravity=0.0)
