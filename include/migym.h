@@ -50,9 +50,9 @@ extern "C" {
 #define MG_SHAPE_CONVEX   3   /* convex hull of a mesh: size[0] = bounding radius about the shape
                                  origin, size[1] = offset of its record in mg_model.hulls */
 
-/* convex hull record (floats, shape-local frame): nv, nf, 0, 0, then nv vertices
+/* convex hull record (floats, shape-local frame): nv, nf, ne, 0, then nv vertices
  * (x, y, z), then nf face planes (n.x, n.y, n.z, d) with unit outward n and
- * n . x <= d inside */
+ * n . x <= d inside, then ne edges (vertex index pairs; ne <= 3 MG_HULL_MAX_VERTS) */
 #define MG_HULL_HEADER     4
 #define MG_HULL_MAX_VERTS 32
 #define MG_HULL_MAX_FACES 64
@@ -95,7 +95,7 @@ extern "C" {
  * floating base (the root link moves freely, e.g. the MJCF ant of
  * examples/apply_forces.py:67); such an articulation steps in the coupled per-env
  * kernel (needs actor_coll) with num_dofs + 6 (+ 6 per free body of its env) <= 16
- * velocity slots; its Jacobian / mass-matrix tensors are not supported. */
+ * velocity slots; its Jacobian / mass-matrix tensors put the 6 root columns first. */
 #define MG_ATMPL_I_N       4
 #define MG_ACOLL_N         4  /* env, collision group, collision filter, pad */
 #define MG_RENDER_MAX_SHAPES 64 /* shapes one camera's env may hold */

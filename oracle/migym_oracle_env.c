@@ -276,6 +276,79 @@ static void deep4_emit_(const pair_t* D, pair_t* o) {
     int k;
     for (k = 0; k < D->n; ++k) ppush_(o, D->p[k], D->nrm[k], D->sep[k]);
 }
+/* edges (mg_collide.h cvx_edge_ids): a box's 12, a hull's index pairs after its planes */
+static int cvx_ne_(const cshape_t* S) { return S->type == MG_SHAPE_BOX ? 12 : (int)S->hv[2]; }
+static void cvx_edge_ids_(const cshape_t* S, int e, int* ia, int* ib) {
+    if (S->type == MG_SHAPE_BOX) {
+        const int k = e >> 2, r = e & 3;
+        const int k1 = k == 2 ? 0 : k + 1, k2 = k == 0 ? 2 : k - 1;
+        *ia = ((r & 1) << k1) | (((r >> 1) & 1) << k2);
+        *ib = *ia | (1 << k);
+    } else {
+        const float* E = S->hv + MG_HULL_HEADER + 3 * (int)S->hv[0] + 4 * (int)S->hv[1] + 2 * e;
+        *ia = (int)E[0];
+        *ib = (int)E[1];
+    }
+}
+static v3_t cvx_vertex_l_(const cshape_t* S, int i) {
+    if (S->type == MG_SHAPE_BOX)
+        return V((i & 1) ? S->h.x : -S->h.x, (i & 2) ? S->h.y : -S->h.y, (i & 4) ? S->h.z : -S->h.z);
+    return V(S->hv[MG_HULL_HEADER + 3 * i], S->hv[MG_HULL_HEADER + 3 * i + 1], S->hv[MG_HULL_HEADER + 3 * i + 2]);
+}
+static float cvx_radius_(const cshape_t* S) { return S->type == MG_SHAPE_BOX ? sqrtf(dot3(S->h, S->h)) : S->h.x; }
+/* edge crossings, X's edges by Y's planes in Y's frame (mg_collide.h
+ * cvx_edges_vs): sphere gate, per-edge distance prefilter, Cyrus-Beck clip
+ * against the planes pushed out by the margin, one candidate at the chord's
+ * midpoint */
+static void cvx_edges_vs_(const cshape_t* X, const cshape_t* Y, float margin, int onY, pair_t* D) {
+    const v3_t t = mtv_(Y->R, sub3(X->c, Y->c));
+    const float rx = cvx_radius_(X) + margin, ry = cvx_radius_(Y) + margin;
+    m3_t M;
+    int e, f, ne, nf;
+    if (Y->type == MG_SHAPE_BOX) {
+        const v3_t dq = V(t.x - fminf(fmaxf(t.x, -Y->h.x), Y->h.x), t.y - fminf(fmaxf(t.y, -Y->h.y), Y->h.y),
+                          t.z - fminf(fmaxf(t.z, -Y->h.z), Y->h.z));
+        if (dot3(dq, dq) > rx * rx) return;
+    } else if (dot3(t, t) > (rx + ry) * (rx + ry)) {
+        return;
+    }
+    M.c0 = mtv_(Y->R, X->R.c0);
+    M.c1 = mtv_(Y->R, X->R.c1);
+    M.c2 = mtv_(Y->R, X->R.c2);
+    ne = cvx_ne_(X);
+    nf = cvx_nf_(Y);
+    for (e = 0; e < ne; ++e) {
+        int ia, ib;
+        v3_t al, ab, dc, p;
+        float t0 = 0.0f, t1 = 1.0f, tm, sv, tc;
+        cvx_edge_ids_(X, e, &ia, &ib);
+        al = add3(t, mv_(M, cvx_vertex_l_(X, ia)));
+        ab = sub3(add3(t, mv_(M, cvx_vertex_l_(X, ib))), al);
+        tc = fminf(fmaxf(-dot3(al, ab) / dot3(ab, ab), 0.0f), 1.0f);
+        dc = add3(al, mul3(ab, tc));
+        if (dot3(dc, dc) > ry * ry) continue;
+        for (f = 0; f < nf; ++f) {
+            v3_t nl;
+            float dl, sa, sb;
+            cvx_plane_l_(Y, f, &nl, &dl);
+            sa = (dot3(nl, al) - dl) - margin;
+            sb = (dot3(nl, add3(al, ab)) - dl) - margin;
+            if (sa >= 0.0f && sb >= 0.0f) { t0 = 1.0f; t1 = 0.0f; }
+            else if (sa >= 0.0f) t0 = fmaxf(t0, sa / (sa - sb));
+            else if (sb >= 0.0f) t1 = fminf(t1, sa / (sa - sb));
+            if (!(t0 < t1)) break;
+        }
+        if (!(t0 < t1)) continue;
+        tm = 0.5f * (t0 + t1);
+        p = add3(Y->c, mv_(Y->R, add3(al, mul3(ab, tm))));
+        sv = cvx_sd_(Y, p, &f);
+        if (sv < margin) {
+            const v3_t n = cvx_normal_(Y, f);
+            if (onY) deep4_add_(D, sv, sub3(p, mul3(n, sv)), mul3(n, -1.0f));
+            else deep4_add_(D, sv, p, n);
+        }
+    }
+}
 static void convex_convex_(const cshape_t* A, const cshape_t* B, float margin, pair_t* o) {
     pair_t D;
     int i, f;
@@ -293,6 +366,10 @@ static void convex_convex_(const cshape_t* A, const cshape_t* B, float margin, p
             const v3_t nA = cvx_normal_(A, f);
             deep4_add_(&D, sd, sub3(v, mul3(nA, sd)), mul3(nA, -1.0f));
         }
+    }
+    if (D.n == 0) {      /* no vertex candidate: edge crossings, the same two ways */
+        cvx_edges_vs_(A, B, margin, 0, &D);
+        cvx_edges_vs_(B, A, margin, 1, &D);
     }
     deep4_emit_(&D, o);
 }

@@ -104,18 +104,27 @@ class Hull:
     (unit outward n, d) with n . x <= d inside, and unit-density mass
     properties (volume, centroid, inertia about the centroid)."""
 
-    def __init__(self, verts, planes, volume, com, inertia):
+    def __init__(self, verts, planes, volume, com, inertia, edge_list=None):
         self.verts = verts
         self.planes = planes
         self.volume = volume
         self.com = com
         self.inertia = inertia
+        self.edge_list = edge_list
+
+    def edges(self):
+        """(ne, 2) vertex index pairs of the hull's edges: the triangulation's edges
+        whose two triangles lie on different merged face planes (diagonals inside a
+        merged face dropped); ascending (i, j)."""
+        return self.edge_list if self.edge_list is not None else np.zeros((0, 2), np.int64)
 
     def record(self):
-        """The MG_HULL record (include/migym.h) as float32."""
-        head = np.array([len(self.verts), len(self.planes), 0, 0], dtype=np.float32)
+        """The MG_HULL record (include/migym.h) as float32: header (nv, nf, ne, 0),
+        vertices, face planes, edges."""
+        E = self.edges()
+        head = np.array([len(self.verts), len(self.planes), len(E), 0], dtype=np.float32)
         return np.concatenate([head, self.verts.astype(np.float32).reshape(-1),
-                               self.planes.astype(np.float32).reshape(-1)])
+                               self.planes.astype(np.float32).reshape(-1), E.astype(np.float32).reshape(-1)])
 
 
 def _farthest_points(pts, k):
@@ -145,11 +154,13 @@ def make_hull(verts, max_verts=HULL_MAX_VERTS):
         h = ConvexHull(cand)
         hv = cand[np.sort(h.vertices)]
         h = ConvexHull(hv)
-        planes = []
+        planes, tri_plane = [], []
         for eq in h.equations:                     # n . x + e <= 0 inside
             n, d = eq[:3], -eq[3]
-            if not any(abs(np.dot(n, q[:3]) - 1.0) < 1e-6 and abs(d - q[3]) < 1e-6 for q in planes):
+            match = [k for k, q in enumerate(planes) if abs(np.dot(n, q[:3]) - 1.0) < 1e-6 and abs(d - q[3]) < 1e-6]
+            if not match:
                 planes.append(np.array([n[0], n[1], n[2], d]))
+            tri_plane.append(match[0] if match else len(planes) - 1)
         if len(planes) <= HULL_MAX_FACES or nv <= 8:
             break
         nv -= 2
@@ -165,7 +176,12 @@ def make_hull(verts, max_verts=HULL_MAX_VERTS):
     r = mom1 / vol
     I_o = np.trace(C) * np.eye(3) - C
     I_c = I_o - vol * (np.dot(r, r) * np.eye(3) - np.outer(r, r))
-    return Hull(hv, np.array(planes), vol, r + o, I_c)
+    inc = {}                                       # triangulation edge -> merged planes of its triangles
+    for t, tri in enumerate(h.simplices):
+        for u, v in ((tri[0], tri[1]), (tri[1], tri[2]), (tri[2], tri[0])):
+            inc.setdefault((min(u, v), max(u, v)), set()).add(tri_plane[t])
+    edges = np.array(sorted(e for e, ps in inc.items() if len(ps) > 1), dtype=np.int64).reshape(-1, 2)
+    return Hull(hv, np.array(planes), vol, r + o, I_c, edges)
 
 
 class Shape:
@@ -543,7 +559,7 @@ def mesh_shape(verts, p, q, source):
         c = 0.5 * (hull.verts.min(0) + hull.verts.max(0))
         hull = Hull(hull.verts - c, np.concatenate([hull.planes[:, :3], hull.planes[:, 3:] -
                                                     hull.planes[:, :3] @ c[:, None]], 1),
-                    hull.volume, hull.com - c, hull.inertia)
+                    hull.volume, hull.com - c, hull.inertia, hull.edge_list)
         hull.box_centre = c
         _HULL_CACHE[key] = hull
     brad = float(np.sqrt((hull.verts ** 2).sum(1).max()))

@@ -10,8 +10,9 @@
 // ways — every vertex of one shape within the margin of the other, by the
 // other's face planes (signed distance = the largest plane distance, the face
 // attaining it gives the normal) — the 4 deepest kept; against spheres /
-// capsule caps: the centre's plane distance. Edge-edge crossings without a
-// vertex inside are not detected (documented approximation).
+// capsule caps: the centre's plane distance. When no vertex is within the
+// margin, edge crossings: each edge clipped against the other shape's planes,
+// one candidate at the chord's midpoint (cvx_edges_vs).
 // Box–box is SAT over the 15 axes (face axes preferred unless an edge axis
 // separates by more than 1e-3 m), then Sutherland–Hodgman clipping of the
 // incident face against the reference face (at most 8 points, the 4 deepest
@@ -421,14 +422,97 @@ MG_HD void cvx_vertices_vs(const CShape& X, const CShape& Y, float margin, bool 
     }
 }
 
+// edges: a box's 12 (axis k = e / 4, the other two axes' signs from e % 4); a
+// hull's from its record (MG_HULL_HEADER + 3 nv + 4 nf: vertex index pairs,
+// hv[2] of them, the importer's Hull.record). Local vertex indices.
+MG_HD int cvx_ne(const CShape& S) { return S.type == MG_SHAPE_BOX ? 12 : (int)S.hv[2]; }
+MG_HD void cvx_edge_ids(const CShape& S, int e, int& ia, int& ib) {
+    if (S.type == MG_SHAPE_BOX) {
+        const int k = e >> 2, r = e & 3;
+        const int k1 = k == 2 ? 0 : k + 1, k2 = k == 0 ? 2 : k - 1;
+        ia = ((r & 1) << k1) | (((r >> 1) & 1) << k2);
+        ib = ia | (1 << k);
+    } else {
+        const float* E = S.hv + MG_HULL_HEADER + 3 * (int)S.hv[0] + 4 * (int)S.hv[1] + 2 * e;
+        ia = (int)E[0];
+        ib = (int)E[1];
+    }
+}
+MG_HD V3 cvx_vertex_l(const CShape& S, int i) {      // shape-local vertex i
+    if (S.type == MG_SHAPE_BOX)
+        return v3((i & 1) ? S.h.x : -S.h.x, (i & 2) ? S.h.y : -S.h.y, (i & 4) ? S.h.z : -S.h.z);
+    const float* v = S.hv + MG_HULL_HEADER + 3 * i;
+    return v3(v[0], v[1], v[2]);
+}
+MG_HD float cvx_radius(const CShape& S) { return S.type == MG_SHAPE_BOX ? sqrtf(vdot(S.h, S.h)) : S.h.x; }
+
+// edge crossings (run when no vertex of either shape is within the margin of
+// the other), in Y's frame: nothing unless X's bounding sphere reaches Y's box
+// (or Y's bounding sphere); an edge farther from Y's centre than Y's bounding
+// radius + margin is skipped; the rest are clipped against Y's face planes
+// pushed out by the margin (Cyrus-Beck), and a non-empty chord [t0, t1] gives
+// one candidate at its midpoint, by Y's planes like a vertex (cvx_sd:
+// separation and face normal; onY: the point on Y's face)
+MG_HD void cvx_edges_vs(const CShape& X, const CShape& Y, float margin, bool onY, Deep4& D) {
+    const V3 t = mtmul(Y.R, vsub(X.c, Y.c));               // X's centre in Y's frame
+    const float rx = cvx_radius(X) + margin, ry = cvx_radius(Y) + margin;
+    if (Y.type == MG_SHAPE_BOX) {
+        const V3 dq = v3(t.x - fminf(fmaxf(t.x, -Y.h.x), Y.h.x), t.y - fminf(fmaxf(t.y, -Y.h.y), Y.h.y),
+                         t.z - fminf(fmaxf(t.z, -Y.h.z), Y.h.z));
+        if (vdot(dq, dq) > rx * rx) return;
+    } else if (vdot(t, t) > (rx + ry) * (rx + ry)) {
+        return;
+    }
+    M3 M;                                                   // X's axes in Y's frame
+    M.c0 = mtmul(Y.R, X.R.c0);
+    M.c1 = mtmul(Y.R, X.R.c1);
+    M.c2 = mtmul(Y.R, X.R.c2);
+    const int ne = cvx_ne(X), nf = cvx_nf(Y);
+    for (int e = 0; e < ne; ++e) {
+        int ia, ib;
+        cvx_edge_ids(X, e, ia, ib);
+        const V3 al = vadd(t, mmul(M, cvx_vertex_l(X, ia)));
+        const V3 ab = vsub(vadd(t, mmul(M, cvx_vertex_l(X, ib))), al);
+        const float tc = fminf(fmaxf(-vdot(al, ab) / vdot(ab, ab), 0.0f), 1.0f);
+        const V3 dc = vadd(al, vscale(ab, tc));
+        if (vdot(dc, dc) > ry * ry) continue;
+        float t0 = 0.0f, t1 = 1.0f;
+        for (int f = 0; f < nf; ++f) {
+            V3 nl;
+            float dl;
+            cvx_plane_l(Y, f, nl, dl);
+            const float sa = (vdot(nl, al) - dl) - margin, sb = (vdot(nl, vadd(al, ab)) - dl) - margin;
+            if (sa >= 0.0f && sb >= 0.0f) { t0 = 1.0f; t1 = 0.0f; }
+            else if (sa >= 0.0f) t0 = fmaxf(t0, sa / (sa - sb));
+            else if (sb >= 0.0f) t1 = fminf(t1, sa / (sa - sb));
+            if (!(t0 < t1)) break;
+        }
+        if (!(t0 < t1)) continue;
+        const float tm = 0.5f * (t0 + t1);
+        const V3 p = vadd(Y.c, mmul(Y.R, vadd(al, vscale(ab, tm))));
+        int f;
+        const float sv = cvx_sd(Y, p, f, 0.0f, margin);
+        if (sv < margin) {
+            const V3 n = cvx_normal(Y, f);
+            if (onY) deep4_add(D, sv, vsub(p, vscale(n, sv)), vscale(n, -1.0f));
+            else deep4_add(D, sv, p, n);
+        }
+    }
+}
+
 // convex A vs convex B (box or hull), vertex penetration both ways: A's vertices
 // by B's planes (normal = B's face normal), then B's vertices by A's planes
-// (point on A's face, normal = -A's)
+// (point on A's face, normal = -A's); with no vertex candidate, edge crossings
+// the same two ways
 MG_HD void convex_convex(const CShape& A, const CShape& B, float margin, PairOut& o) {
     Deep4 D;
     D.n = 0;
     cvx_vertices_vs(A, B, margin, false, D);
     cvx_vertices_vs(B, A, margin, true, D);
+    if (D.n == 0) {
+        cvx_edges_vs(A, B, margin, false, D);
+        cvx_edges_vs(B, A, margin, true, D);
+    }
     deep4_emit(D, o);
 }
 

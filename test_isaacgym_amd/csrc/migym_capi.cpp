@@ -404,10 +404,14 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         if (t != MG_SHAPE_CONVEX) continue;
         const long off = (long)sh[2], nh = m->hulls ? m->num_hull_floats : 0;
         if (off < 0 || off + MG_HULL_HEADER > nh) return fail(MG_ERR_ARG, "shape %d: hull offset %ld out of range", k, off);
-        const int nv = (int)m->hulls[off], nfc = (int)m->hulls[off + 1];
-        if (nv < 4 || nv > MG_HULL_MAX_VERTS || nfc < 4 || nfc > MG_HULL_MAX_FACES ||
-            off + MG_HULL_HEADER + 3L * nv + 4L * nfc > nh)
-            return fail(MG_ERR_ARG, "shape %d: bad hull record (%d vertices, %d faces)", k, nv, nfc);
+        const int nv = (int)m->hulls[off], nfc = (int)m->hulls[off + 1], ned = (int)m->hulls[off + 2];
+        if (nv < 4 || nv > MG_HULL_MAX_VERTS || nfc < 4 || nfc > MG_HULL_MAX_FACES || ned < 0 ||
+            ned > 3 * MG_HULL_MAX_VERTS || off + MG_HULL_HEADER + 3L * nv + 4L * nfc + 2L * ned > nh)
+            return fail(MG_ERR_ARG, "shape %d: bad hull record (%d vertices, %d faces, %d edges)", k, nv, nfc, ned);
+        for (int e = 0; e < 2 * ned; ++e) {
+            const float vi = m->hulls[off + MG_HULL_HEADER + 3L * nv + 4L * nfc + e];
+            if (!(vi >= 0.0f && vi < (float)nv)) return fail(MG_ERR_ARG, "shape %d: hull edge vertex out of range", k);
+        }
     }
     for (int a = 0; a < na; ++a) {
         if (m->actor_root_body[a] < 0 || m->actor_root_body[a] >= nb) return fail(MG_ERR_ARG, "actor %d: bad root", a);

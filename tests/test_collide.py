@@ -189,6 +189,47 @@ def test_hull_of_box_matches_box_box_face_contact():
         assert np.allclose(rh[np.argmin(rh[:, 6]), 3:6], [0, 0, 1], atol=1e-5)
 
 
+def test_hull_edges():
+    """Hull records carry their edges (vertex pairs on two common merged faces):
+    a box 12, an octahedron 12, a random 32-vertex hull V + F - 2 by Euler for its
+    triangulated faces (merged faces only remove diagonals)."""
+    from test_isaacgym_amd import _assets
+    assert len(_hull_of_box((0.1, 0.2, 0.3)).edges()) == 12
+    octa = _assets.make_hull(np.array([[0.1, 0, 0], [-0.1, 0, 0], [0, 0.1, 0], [0, -0.1, 0], [0, 0, 0.1], [0, 0, -0.1]]))
+    assert len(octa.edges()) == 12
+    rng = np.random.RandomState(0)
+    h = _assets.make_hull(rng.normal(size=(200, 3)))
+    E = h.edges()
+    assert len(E) == len(h.verts) + len(h.planes) - 2
+    rec = h.record()
+    assert rec[2] == len(E) and len(rec) == 4 + 3 * len(h.verts) + 4 * len(h.planes) + 2 * len(E)
+
+
+def test_hull_edge_edge_crossing():
+    """Two cube hulls turned 45 degrees about x and about y, their edges crossing
+    1 mm deep with no vertex of either inside the other: found by the edge
+    fallback (Cyrus-Beck chords), one candidate each way, separation the chord
+    midpoint's depth below the other cube's face (-1 mm / sqrt 2), the normal
+    pushing them apart; and nothing 1 mm apart with a 0.5 mm margin."""
+    h = 0.05
+    rec = _hull_of_box((h, h, h)).record()
+    r2 = h * math.sqrt(2)
+    for depth, margin, n_expect in ((0.001, 0.01, 2), (-0.001, 0.0005, 0)):
+        A = _shape(CONVEX, (0, 0, 0), _quat((1, 0, 0), math.pi / 4), (h * math.sqrt(3), 0, 0))
+        B = _shape(CONVEX, (0, 0, 2 * r2 - depth), _quat((0, 1, 0), math.pi / 4), (h * math.sqrt(3), 0, 0))
+        out = oracle.collide(A, B, margin, hull_a=rec, hull_b=rec)
+        assert len(out) == n_expect
+        for row in out:
+            assert abs(row[6] + depth / math.sqrt(2)) < 2e-5
+            assert row[5] < -0.7                         # normal b -> a points down
+        # the box-box SAT path agrees on the crossing (one contact, depth 1 mm along z)
+        if n_expect:
+            Ab = _shape(BOX, A[1:4], A[4:8], (h, h, h))
+            Bb = _shape(BOX, B[1:4], B[4:8], (h, h, h))
+            ob = oracle.collide(Ab, Bb, margin)
+            assert len(ob) == 1 and abs(ob[0, 6] + depth) < 2e-5
+
+
 def test_hull_against_ground_and_sphere():
     from test_isaacgym_amd import _assets
     # octahedron, radius 0.1, one vertex 2 mm into a box below; a sphere resting on a face
