@@ -300,7 +300,11 @@ static float cvx_radius_(const cshape_t* S) { return S->type == MG_SHAPE_BOX ? s
  * cvx_edges_vs): sphere gate, per-edge distance prefilter, Cyrus-Beck clip
  * against the planes pushed out by the margin, one candidate at the chord's
  * midpoint */
-static void cvx_edges_vs_(const cshape_t* X, const cshape_t* Y, float margin, int onY, pair_t* D) {
+static void aabb_add_(v3_t* lo, v3_t* hi, v3_t v) {
+    *lo = V(fminf(lo->x, v.x), fminf(lo->y, v.y), fminf(lo->z, v.z));
+    *hi = V(fmaxf(hi->x, v.x), fmaxf(hi->y, v.y), fmaxf(hi->z, v.z));
+}
+static void cvx_edges_vs_(const cshape_t* X, const cshape_t* Y, float margin, int onY, pair_t* D, v3_t lo, v3_t hi) {
     const v3_t t = mtv_(Y->R, sub3(X->c, Y->c));
     const float rx = cvx_radius_(X) + margin, ry = cvx_radius_(Y) + margin;
     m3_t M;
@@ -315,6 +319,11 @@ static void cvx_edges_vs_(const cshape_t* X, const cshape_t* Y, float margin, in
     M.c0 = mtv_(Y->R, X->R.c0);
     M.c1 = mtv_(Y->R, X->R.c1);
     M.c2 = mtv_(Y->R, X->R.c2);
+    if (Y->type == MG_SHAPE_BOX) {   /* Y's face axes separate X (vertex-pass bounds): no crossing */
+        if (lo.x > Y->h.x + margin || hi.x < -Y->h.x - margin || lo.y > Y->h.y + margin || hi.y < -Y->h.y - margin ||
+            lo.z > Y->h.z + margin || hi.z < -Y->h.z - margin)
+            return;
+    }
     ne = cvx_ne_(X);
     nf = cvx_nf_(Y);
     for (e = 0; e < ne; ++e) {
@@ -353,23 +362,26 @@ static void convex_convex_(const cshape_t* A, const cshape_t* B, float margin, p
     pair_t D;
     int i, f;
     const int na = cvx_nv_(A), nb = cvx_nv_(B);
+    v3_t loA = V(1e30f, 1e30f, 1e30f), hiA = V(-1e30f, -1e30f, -1e30f), loB = loA, hiB = hiA;
     D.n = 0;
     for (i = 0; i < na; ++i) {
         const v3_t v = cvx_vertex_(A, i);
         const float sd = cvx_sd_(B, v, &f);
+        aabb_add_(&loA, &hiA, mtv_(B->R, sub3(v, B->c)));
         if (sd < margin) deep4_add_(&D, sd, v, cvx_normal_(B, f));
     }
     for (i = 0; i < nb; ++i) {
         const v3_t v = cvx_vertex_(B, i);
         const float sd = cvx_sd_(A, v, &f);
+        aabb_add_(&loB, &hiB, mtv_(A->R, sub3(v, A->c)));
         if (sd < margin) {
             const v3_t nA = cvx_normal_(A, f);
             deep4_add_(&D, sd, sub3(v, mul3(nA, sd)), mul3(nA, -1.0f));
         }
     }
-    if (D.n == 0) {      /* no vertex candidate: edge crossings, the same two ways */
-        cvx_edges_vs_(A, B, margin, 0, &D);
-        cvx_edges_vs_(B, A, margin, 1, &D);
+    if (D.n == 0) {      /* no vertex candidate: edge crossings, one direction (mg_collide.h) */
+        if (A->type == MG_SHAPE_BOX && B->type != MG_SHAPE_BOX) cvx_edges_vs_(B, A, margin, 1, &D, loB, hiB);
+        else cvx_edges_vs_(A, B, margin, 0, &D, loA, hiA);
     }
     deep4_emit_(&D, o);
 }

@@ -390,8 +390,16 @@ MG_HD V3 hull_vl(const float* V, int n, int i) {
 // D: a vertex v within the margin (cvx_sd: the largest plane distance s, first
 // face f on ties) gives (s, v, n_f) when the point is taken on X (onY false), or
 // (s, v - n_f s, -n_f) on Y's face. A hull X streams its vertices 4 ahead.
-MG_HD void cvx_vertices_vs(const CShape& X, const CShape& Y, float margin, bool onY, Deep4& D) {
+// Also the bounds (lo, hi) of X's vertices in Y's frame (the face-axis test of
+// the edge pass).
+MG_HD void aabb_add(V3& lo, V3& hi, V3 v) {
+    lo = v3(fminf(lo.x, v.x), fminf(lo.y, v.y), fminf(lo.z, v.z));
+    hi = v3(fmaxf(hi.x, v.x), fmaxf(hi.y, v.y), fmaxf(hi.z, v.z));
+}
+MG_HD void cvx_vertices_vs(const CShape& X, const CShape& Y, float margin, bool onY, Deep4& D, V3& lo, V3& hi) {
     const int nx = cvx_nv(X);
+    lo = v3(1e30f, 1e30f, 1e30f);
+    hi = v3(-1e30f, -1e30f, -1e30f);
     if (X.type == MG_SHAPE_CONVEX) {
         const float* V = X.hv + MG_HULL_HEADER;
         V3 r0 = hull_vl(V, nx, 0), r1 = hull_vl(V, nx, 1), r2 = hull_vl(V, nx, 2), r3 = hull_vl(V, nx, 3);
@@ -400,6 +408,7 @@ MG_HD void cvx_vertices_vs(const CShape& X, const CShape& Y, float margin, bool 
             r0 = r1; r1 = r2; r2 = r3;
             r3 = hull_vl(V, nx, i + 4);
             const V3 v = vadd(X.c, mmul(X.R, l));            // cvx_vertex(X, i)
+            aabb_add(lo, hi, mtmul(Y.R, vsub(v, Y.c)));
             int f;
             const float sv = cvx_sd(Y, v, f, 0.0f, margin);
             if (sv < margin) {
@@ -412,6 +421,7 @@ MG_HD void cvx_vertices_vs(const CShape& X, const CShape& Y, float margin, bool 
     }
     for (int i = 0; i < nx; ++i) {
         const V3 v = cvx_vertex(X, i);
+        aabb_add(lo, hi, mtmul(Y.R, vsub(v, Y.c)));
         int f;
         const float sv = cvx_sd(Y, v, f, 0.0f, margin);
         if (sv < margin) {
@@ -453,7 +463,7 @@ MG_HD float cvx_radius(const CShape& S) { return S.type == MG_SHAPE_BOX ? sqrtf(
 // pushed out by the margin (Cyrus-Beck), and a non-empty chord [t0, t1] gives
 // one candidate at its midpoint, by Y's planes like a vertex (cvx_sd:
 // separation and face normal; onY: the point on Y's face)
-MG_HD void cvx_edges_vs(const CShape& X, const CShape& Y, float margin, bool onY, Deep4& D) {
+MG_HD void cvx_edges_vs(const CShape& X, const CShape& Y, float margin, bool onY, Deep4& D, V3 lo, V3 hi) {
     const V3 t = mtmul(Y.R, vsub(X.c, Y.c));               // X's centre in Y's frame
     const float rx = cvx_radius(X) + margin, ry = cvx_radius(Y) + margin;
     if (Y.type == MG_SHAPE_BOX) {
@@ -467,12 +477,29 @@ MG_HD void cvx_edges_vs(const CShape& X, const CShape& Y, float margin, bool onY
     M.c0 = mtmul(Y.R, X.R.c0);
     M.c1 = mtmul(Y.R, X.R.c1);
     M.c2 = mtmul(Y.R, X.R.c2);
+    if (Y.type == MG_SHAPE_BOX) {
+        // Y's face axes separate X (X's vertex bounds from the vertex pass beyond
+        // one face plus the margin): no crossing (a link hull just above a table)
+        if (lo.x > Y.h.x + margin || hi.x < -Y.h.x - margin || lo.y > Y.h.y + margin || hi.y < -Y.h.y - margin ||
+            lo.z > Y.h.z + margin || hi.z < -Y.h.z - margin)
+            return;
+    }
     const int ne = cvx_ne(X), nf = cvx_nf(Y);
+    if (ne <= 0) return;
+    // a hull's edge ids and endpoints are streamed ahead (ids two edges, the
+    // endpoints one edge): the loads of the next edge are in flight while this
+    // one is tested (at one wave per SIMD nothing else hides their latency)
+    int ia1, ib1, ia2, ib2;
+    cvx_edge_ids(X, 0, ia1, ib1);
+    V3 la1 = cvx_vertex_l(X, ia1), lb1 = cvx_vertex_l(X, ib1);
+    cvx_edge_ids(X, ne > 1 ? 1 : 0, ia2, ib2);
     for (int e = 0; e < ne; ++e) {
-        int ia, ib;
-        cvx_edge_ids(X, e, ia, ib);
-        const V3 al = vadd(t, mmul(M, cvx_vertex_l(X, ia)));
-        const V3 ab = vsub(vadd(t, mmul(M, cvx_vertex_l(X, ib))), al);
+        const V3 la = la1, lb = lb1;
+        la1 = cvx_vertex_l(X, ia2);
+        lb1 = cvx_vertex_l(X, ib2);
+        cvx_edge_ids(X, e + 2 < ne ? e + 2 : ne - 1, ia2, ib2);
+        const V3 al = vadd(t, mmul(M, la));
+        const V3 ab = vsub(vadd(t, mmul(M, lb)), al);
         const float tc = fminf(fmaxf(-vdot(al, ab) / vdot(ab, ab), 0.0f), 1.0f);
         const V3 dc = vadd(al, vscale(ab, tc));
         if (vdot(dc, dc) > ry * ry) continue;
@@ -503,15 +530,18 @@ MG_HD void cvx_edges_vs(const CShape& X, const CShape& Y, float margin, bool onY
 // convex A vs convex B (box or hull), vertex penetration both ways: A's vertices
 // by B's planes (normal = B's face normal), then B's vertices by A's planes
 // (point on A's face, normal = -A's); with no vertex candidate, edge crossings
-// the same two ways
 MG_HD void convex_convex(const CShape& A, const CShape& B, float margin, PairOut& o) {
     Deep4 D;
     D.n = 0;
-    cvx_vertices_vs(A, B, margin, false, D);
-    cvx_vertices_vs(B, A, margin, true, D);
+    V3 loA, hiA, loB, hiB;              // A's vertices in B's frame, B's in A's
+    cvx_vertices_vs(A, B, margin, false, D, loA, hiA);
+    cvx_vertices_vs(B, A, margin, true, D, loB, hiB);
     if (D.n == 0) {
-        cvx_edges_vs(A, B, margin, false, D);
-        cvx_edges_vs(B, A, margin, true, D);
+        // an edge crossing puts an edge of each shape through the other: one
+        // direction finds it — the edges of the shape that is not a box, clipped
+        // by the box's 6 planes behind its face-axis test (two hulls: A's edges)
+        if (A.type == MG_SHAPE_BOX && B.type != MG_SHAPE_BOX) cvx_edges_vs(B, A, margin, true, D, loB, hiB);
+        else cvx_edges_vs(A, B, margin, false, D, loA, hiA);
     }
     deep4_emit(D, o);
 }

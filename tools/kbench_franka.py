@@ -7,6 +7,8 @@ import json
 import os
 import sys
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
@@ -42,6 +44,12 @@ def run(n, warm=150, steps=100):
             torch.cuda.synchronize()
             N.lib.mg_debug_env_phase_reset()
     torch.cuda.synchronize()
+    if os.environ.get("KB_DUMP"):
+        # the grasp-phase state and targets, for replaying one step on the host restatement
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_dof_state_tensor(sim)
+        np.savez(os.environ["KB_DUMP"], rb=rb.cpu().numpy(), dof=dof.cpu().numpy(), pa=pa.cpu().numpy(),
+                 ea=ea.cpu().numpy())
     phases = None
     if hasattr(N.lib, "mg_debug_env_phase"):
         buf = (ctypes.c_ulonglong * 12)()
