@@ -379,10 +379,8 @@ static void convex_convex_(const cshape_t* A, const cshape_t* B, float margin, p
             deep4_add_(&D, sd, sub3(v, mul3(nA, sd)), mul3(nA, -1.0f));
         }
     }
-    if (D.n == 0) {      /* no vertex candidate: edge crossings, one direction (mg_collide.h) */
-        if (A->type == MG_SHAPE_BOX && B->type != MG_SHAPE_BOX) cvx_edges_vs_(B, A, margin, 1, &D, loB, hiB);
-        else cvx_edges_vs_(A, B, margin, 0, &D, loA, hiA);
-    }
+    if (D.n == 0 && A->type == MG_SHAPE_CONVEX && B->type == MG_SHAPE_CONVEX)   /* two hulls: A's edges (mg_collide.h) */
+        cvx_edges_vs_(A, B, margin, 0, &D, loA, hiA);
     deep4_emit_(&D, o);
 }
 static void sph_cvx_(v3_t s, float r, const cshape_t* B, float margin, pair_t* o) {

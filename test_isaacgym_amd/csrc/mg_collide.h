@@ -10,9 +10,9 @@
 // ways — every vertex of one shape within the margin of the other, by the
 // other's face planes (signed distance = the largest plane distance, the face
 // attaining it gives the normal) — the 4 deepest kept; against spheres /
-// capsule caps: the centre's plane distance. When no vertex is within the
-// margin, edge crossings: each edge clipped against the other shape's planes,
-// one candidate at the chord's midpoint (cvx_edges_vs).
+// capsule caps: the centre's plane distance. Two hulls with no vertex within
+// the margin: edge crossings, A's edges clipped against B's planes, one
+// candidate at the chord's midpoint (cvx_edges_vs).
 // Box–box is SAT over the 15 axes (face axes preferred unless an edge axis
 // separates by more than 1e-3 m), then Sutherland–Hodgman clipping of the
 // incident face against the reference face (at most 8 points, the 4 deepest
@@ -536,12 +536,12 @@ MG_HD void convex_convex(const CShape& A, const CShape& B, float margin, PairOut
     V3 loA, hiA, loB, hiB;              // A's vertices in B's frame, B's in A's
     cvx_vertices_vs(A, B, margin, false, D, loA, hiA);
     cvx_vertices_vs(B, A, margin, true, D, loB, hiB);
-    if (D.n == 0) {
-        // an edge crossing puts an edge of each shape through the other: one
-        // direction finds it — the edges of the shape that is not a box, clipped
-        // by the box's 6 planes behind its face-axis test (two hulls: A's edges)
-        if (A.type == MG_SHAPE_BOX && B.type != MG_SHAPE_BOX) cvx_edges_vs(B, A, margin, true, D, loB, hiB);
-        else cvx_edges_vs(A, B, margin, false, D, loA, hiA);
+    if (D.n == 0 && A.type == MG_SHAPE_CONVEX && B.type == MG_SHAPE_CONVEX) {
+        // two hulls: an edge crossing puts an edge of each through the other, so
+        // A's edges find it. Not against a box: the face normal at a box's edge
+        // can point along the wrong face (a finger grazing a cube's top edge
+        // pressed it into the table in the 4096-env Franka test)
+        cvx_edges_vs(A, B, margin, false, D, loA, hiA);
     }
     deep4_emit(D, o);
 }

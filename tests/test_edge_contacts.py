@@ -1,4 +1,4 @@
-"""Edge crossings between convex hulls in the coupled per-env step
+"""Edge crossings between two convex hulls in the coupled per-env step
 (mg_collide.h cvx_edges_vs; oracle/migym_oracle_env.c cvx_edges_vs_).
 
 Scene: a fixed cube hull turned 45 degrees about y (a ridge along y) and a free
