@@ -53,7 +53,7 @@ SIM_BYTES_PER_ENV = 376          # simulate share of the 688 
 STEP_BYTES_PER_ENV = 688         # whole tensor-API step
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 KERNEL_TIMED_LAUNCHES = 128      # eager launches with dispatch timestamps (ring holds 256)
-GRAPH_CHUNK = 8                  # tensor-API steps captured per hipGraph (amortizes the graph launch)
+GRAPH_CHUNK_MAX = 64             # tensor-API steps captured per hipGraph at most (amortizes the graph launch)
 
 
 def parse_args(argv=None):
@@ -95,10 +95,17 @@ def _launcher():
 
 
 # --------------------------------------------------------------------------- helpers
-def graph_chunk(steps, slots):
-    """Steps per captured graph: GRAPH_CHUNK when it divides both the timed step
-    count and the action-slot cycle, else the largest common divisor."""
-    return math.gcd(math.gcd(steps, slots), GRAPH_CHUNK)
+def graph_chunk(steps, cap=GRAPH_CHUNK_MAX):
+    """Steps per captured graph: the largest divisor of the timed step count
+    that is <= cap, so a timed region of `steps` replays steps / chunk graphs
+    (one graph for --steps <= 64: the driver's 20-step region is one launch)."""
+    return max(d for d in range(1, min(steps, cap) + 1) if steps % d == 0)
+
+
+def bank_slots(chunk, at_least=64):
+    """Action-bank size: a multiple of the graph chunk (each captured graph
+    covers `chunk` consecutive slots), at least `at_least` slots."""
+    return chunk * -(-at_least // chunk)
 
 
 def capture_chunks(step, slots, chunk):
@@ -137,13 +144,20 @@ def kernel_stats(sim, n_launches, run):
     return avg.value, lo.value, int(used)
 
 
+STEP_FUSION_NOTE = ("opt-in step fusion (gym.set_step_fusion(sim, STEP_FUSION_ALL)): every step writes the "
+                    "action into the source before its set and never touches it again before simulate, so "
+                    "the deferred read equals Isaac Gym's copy-at-set (checked by version counters); off by "
+                    "default in the library")
+
+
 def fuse_in_capture(sim):
-    """MG_FUSE_IN_CAPTURE on this sim: every captured step of this leg is set ->
-    simulate -> refresh, so each captured set is consumed by the captured
-    simulate after it (include/migym.h; the S3 leg's frames end with the DOF
-    setters and keep the default)."""
-    from test_isaacgym_amd import _native as N
-    N.lib.mg_set_fusion(sim.native, 1 | 2 | 4 | 8)
+    """Opt in to step fusion, inside captures too (STEP_FUSION_ALL): every
+    (captured) step of this leg is set -> simulate -> refresh, so each set is
+    consumed by the simulate after it and its source is not written in between
+    (include/migym.h; the S3 leg's frames end with the DOF setters and keep the
+    default, no fusion)."""
+    from isaacgym import gymapi
+    gymapi.acquire_gym().set_step_fusion(sim, gymapi.STEP_FUSION_ALL)
 
 
 def load_pmc(name):
@@ -174,55 +188,112 @@ def rigid_roofline(n, kern_ms, kmin, launches, segment):
 
 
 # --------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(seconds=10.0, threads=None):
-    """The oracle (C restatement) on the same 4096-env scene, on `threads` host
-    cores: each step splits the bodies into contiguous ranges, one per thread
-    (oracle.step's body_range; ctypes releases the GIL, envs are independent),
-    plus a single-thread figure on the same sample for reference."""
-    import concurrent.futures as cf
+def cpu_threads():
+    """(all host cores as os.cpu_count() reports them, the CPUs this process may
+    run on, the cgroup CPU quota in CPUs or None)."""
+    ncpu = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = ncpu
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return ncpu, aff, quota
+
+
+def _cpu_scene(leg, n):
+    """The bench legs' scenes on the host (no GPU pipeline): (sim, per-step
+    hook(state, k), tgt). S1 teleports every root each step like the GPU leg;
+    S2 draws new PD targets each step; S3 holds the Franka at its default DOF
+    targets (the OSC controller is not part of the oracle)."""
     import numpy as np
-    import oracle
     from isaacgym import gymapi
     from test_isaacgym_amd import scenes
     gym = gymapi.acquire_gym()
-    sim, _ = scenes.servo_scene(gym, ENVS_PER_GPU, use_gpu_pipeline=False)
+    if leg == "s1":
+        sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=False)
+        sim.build_model()
+        roots = sim.model_arrays["actor_root_body"]
+        acts = scenes.servo_actions(n, 16, "cpu", seed=0).numpy()
+
+        def hook(st, tgt, k):
+            st[roots, 3:10] = acts[k % len(acts)]
+        return sim, hook, None
+    if leg == "s2":
+        sim, _ = scenes.gimbal_scene(gym, n, use_gpu_pipeline=False)
+        sim.build_model()
+        tg = scenes.gimbal_targets(n, 16, "cpu", seed=0).numpy()
+        tgt = np.zeros((3 * n, 3), np.float32)
+
+        def hook(st, tgt, k):
+            tgt[:, 0] = tg[k % len(tg)]
+        return sim, hook, tgt
+    sim, info = scenes.franka_scene(gym, n, use_gpu_pipeline=False)
     sim.build_model()
+    nd = sim.model_arrays["dof_state0"].shape[0]
+    tgt = np.zeros((nd, 3), np.float32)
+    tgt[:, 0] = np.tile(np.asarray(info["default_dof_pos"], np.float32), nd // 9)
+    return sim, (lambda st, tgt, k: None), tgt
+
+
+def cpu_leg(leg, n, seconds, thread_counts):
+    """env-steps/s of oracle.step_threads (the C restatement on OpenMP host
+    threads) on the leg's n-env scene, per thread count, each for ~seconds."""
+    import numpy as np
+    import oracle
+    sim, hook, tgt = _cpu_scene(leg, n)
     p, m = sim.mg_params(), sim.mg_model()
     st = sim.model_arrays["body_state0"].copy()
-    nb = st.shape[0]
-    roots = sim.model_arrays["actor_root_body"]
-    acts = scenes.servo_actions(ENVS_PER_GPU, 16, "cpu", seed=0).numpy()
-    dof = np.zeros((0, 2), np.float32)
-    cforce = np.zeros((nb, 3), np.float32)
-    ncpu = os.cpu_count() or 1
-    # 16 = the GPU box's CPU share per GPU (os.cpu_count() there shows the whole machine)
-    threads = threads or max(1, min(16, ncpu))
+    dof = sim.model_arrays["dof_state0"].copy()
+    if tgt is None:
+        tgt = np.zeros((max(dof.shape[0], 1), 3), np.float32)
+    cforce = np.zeros((st.shape[0], 3), np.float32)
+    out = {}
+    for nt, secs in thread_counts:
+        steps, t0 = 0, time.perf_counter()
+        while True:
+            hook(st, tgt, steps)
+            oracle.step_threads(p, m, st, dof, nt, tgt=tgt, cforce=cforce)
+            steps += 1
+            el = time.perf_counter() - t0
+            if (el >= secs and steps >= 3) or steps >= 100000:
+                break
+        out[nt] = (n * steps / el, steps, el)
+    return out
 
-    def run(nthr, budget):
-        cuts = [nb * k // nthr for k in range(nthr + 1)]
-        cuts = [c - (c % 2) for c in cuts]              # an env's two bodies stay in one range
-        cuts[-1] = nb
-        steps = 0
-        with cf.ThreadPoolExecutor(nthr) as pool:
-            t0 = time.perf_counter()
-            while True:
-                st[roots, 3:10] = acts[steps % len(acts)]
-                list(pool.map(lambda k: oracle.step(p, m, st, dof, cforce=cforce,
-                                                    body_range=(cuts[k], cuts[k + 1])), range(nthr)))
-                steps += 1
-                el = time.perf_counter() - t0
-                if el >= budget and steps >= 5:
-                    return steps, el
 
-    s1, e1 = run(1, seconds * 0.3)
-    sn, en = run(threads, seconds * 0.7) if threads > 1 else (s1, e1)
-    return {"value": ENVS_PER_GPU * sn / en, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "host_cpu_count": ncpu,
-            "single_thread_value": ENVS_PER_GPU * s1 / e1,
-            "sample": "%d simulate() steps of the 4096-env servo scene with random root teleports, "
-                      "oracle/migym_oracle.c (CPU restatement, not Isaac Gym) on %d host threads "
-                      "(os.cpu_count() = %d), bodies split into contiguous ranges (%.1f s); "
-                      "single thread: %d steps (%.1f s)" % (sn, threads, ncpu, en, s1, e1)}
+def cpu_baseline(seconds=10.0):
+    """SURVEY.md §8d "CPU beside it" / BASELINE.md §3: the oracle (C restatement,
+    "port") on every host core os.cpu_count() reports (OpenMP, num_threads set
+    explicitly), on the three bench scenes at 4096 envs: S1 (the headline), S2,
+    S3. Also 16 threads (the GPU box's CPU share per GPU) and 1 thread for S1."""
+    ncpu, aff, quota = cpu_threads()
+    n = ENVS_PER_GPU
+    s1 = cpu_leg("s1", n, seconds, [(ncpu, seconds * 0.4), (16, seconds * 0.2), (1, seconds * 0.2)])
+    s2 = cpu_leg("s2", n, seconds, [(ncpu, seconds * 0.3), (16, seconds * 0.15)])
+    s3 = cpu_leg("s3", n, seconds, [(ncpu, seconds * 0.5), (16, seconds * 0.3)])
+
+    def leg(r, what):
+        v, steps, el = r[ncpu]
+        return {"value": v, "unit": "env-steps/s", "cores": ncpu, "steps": steps, "seconds": el,
+                "value_16_threads": r[16][0], "sample": what}
+    out = leg(s1, "%d simulate() steps of the 4096-env servo scene with random root teleports (S1)" % s1[ncpu][1])
+    out.update({"kind": "port", "host_cpu_count": ncpu, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                "single_thread_value": s1[1][0],
+                "note": "oracle/migym_oracle.c (CPU restatement, not Isaac Gym: the reference engine is a closed "
+                        "binary absent here) via oracle_step_mt, OpenMP with num_threads = os.cpu_count(); "
+                        "the box's cgroup quota (cgroup_cpu_quota CPUs) caps what those threads get",
+                "s2": leg(s2, "%d simulate() steps of 4096 3-DOF gimbals under random PD targets (S2)" % s2[ncpu][1]),
+                "s3": leg(s3, "%d simulate() steps of 4096 Franka cube-pick envs holding their default DOF "
+                              "targets (S3 physics only; the OSC controller is not in the oracle)" % s3[ncpu][1])})
+    out["sample"] = out["sample"] + "; S2 and S3 under s2 / s3"
+    return out
 
 
 # --------------------------------------------------------------------------- secondary legs (N = 1)
@@ -239,10 +310,11 @@ def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     fuse_in_capture(sim)
     gym.acquire_dof_state_tensor(sim)
     gym.acquire_rigid_body_state_tensor(sim)
-    tg = scenes.gimbal_targets(n, 64, dev, seed=0)
+    chunk = graph_chunk(steps)
+    tg = scenes.gimbal_targets(n, bank_slots(chunk), dev, seed=0)
 
     def step(k):
-        gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[k % 64]))
+        gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[k % tg.shape[0]]))
         gym.simulate(sim)
         gym.refresh_dof_state_tensor(sim)
         gym.refresh_rigid_body_state_tensor(sim)
@@ -252,7 +324,6 @@ def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     kms, kmin, used = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
                                    lambda: [step(warmup + k) for k in range(KERNEL_TIMED_LAUNCHES)])
     graphs = None
-    chunk = graph_chunk(steps, tg.shape[0])
     base = -(-(warmup + KERNEL_TIMED_LAUNCHES + chunk) // chunk) * chunk
     if use_graph:
         try:
@@ -328,7 +399,7 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
     torch.cuda.synchronize(dev)
     eager_ms = 1e3 * (time.perf_counter() - t_e) / 10
     graph = None
-    chunk = math.gcd(steps, GRAPH_CHUNK)
+    chunk = graph_chunk(steps, 8)
     if use_graph:
         try:
             side = torch.cuda.Stream(dev)
@@ -481,6 +552,7 @@ def large_n_rate(n, steps, dev, use_graph=True):
     kms, kmin, used = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
                                    lambda: [step(10 + k) for k in range(KERNEL_TIMED_LAUNCHES)])
     chunk = graph_chunk(steps, acts.shape[0])
+    assert acts.shape[0] % chunk == 0
     graphs = None
     base = -(-(10 + KERNEL_TIMED_LAUNCHES) // chunk) * chunk
     if use_graph:
@@ -505,17 +577,16 @@ def large_n_rate(n, steps, dev, use_graph=True):
     # is a scatter launch and the step reads the SoA state): at this size the
     # fused read costs the kernel the user rows' other-template halves (test10's
     # actor rows alternate UAV / vehicle, whose waves run apart: DESIGN.md §3.2)
-    from test_isaacgym_amd import _native as N
-    prev = N.lib.mg_set_fusion(sim.native, 0)
+    prev = gym.set_step_fusion(sim, 0)
     ukms, ukmin, uused = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
                                       lambda: [step(k) for k in range(KERNEL_TIMED_LAUNCHES)])
-    N.lib.mg_set_fusion(sim.native, prev)
+    gym.set_step_fusion(sim, prev)
     gym.destroy_sim(sim)
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps, "steps": steps,
             "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graphs is not None else "eager",
             "roofline": rigid_roofline(n, kms, kmin, used, "%d eager steps after a 10-step warm-up" % used),
             "roofline_unfused": rigid_roofline(n, ukms, ukmin, uused,
-                                               "%d eager steps with mg_set_fusion(0) (scatter launch, then the "
+                                               "%d eager steps with step fusion off (scatter launch, then the "
                                                "step kernel on the SoA state)" % uused)}
 
 
@@ -599,7 +670,8 @@ def main():
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     gym.acquire_rigid_body_state_tensor(sim)
     gym.acquire_dof_state_tensor(sim)
-    acts = scenes.servo_actions(n, 64, dev, seed=rank)
+    chunk = graph_chunk(args.steps)
+    acts = scenes.servo_actions(n, bank_slots(chunk), dev, seed=rank)
     gathered = args.allgather and world > 1
 
     def step(k, gather=gathered):
@@ -643,7 +715,6 @@ def main():
     # acts[j]), sharing one memory pool; the replayed sequence is exactly the eager
     # loop's, and one graph launch is paid per `chunk` steps instead of per step
     graphs = None
-    chunk = graph_chunk(args.steps, acts.shape[0])
     if not args.eager and not gathered:
         try:
             side = torch.cuda.Stream(dev)
@@ -741,13 +812,17 @@ def main():
                     backend if world > 1 else "single rank",
                     ", all-gather of root state in the loop" if gathered else ", no collectives in the loop"),
                 "timed_loop": ("hipGraph replay: %d captured tensor-API steps per graph (every step's full "
-                               "kernel sequence, action slot by slot)" % chunk) if graphs is not None
+                               "kernel sequence, action slot by slot), %d graph launches per timed region"
+                               % (chunk, args.steps // chunk)) if graphs is not None
                               else "eager Python loop",
+                "graph_chunk": chunk if graphs is not None else None,
+                "action_slots": int(acts.shape[0]),
                 "repeats": reps,
                 "ms_per_step_runs": [1e3 * e / args.steps for e in el_max],
                 "ms_per_step_per_rank": [[1e3 * e / args.steps for e in row] for row in per_rank],
                 "eager_ms_per_step": eager_ms,
                 "eager_note": "eager Python loop with kernel timing off (timing is opt-in: mg_set_kernel_timing)",
+                "step_fusion": STEP_FUSION_NOTE,
             },
             "roofline": dict(rigid_roofline(n, kern_ms, kmin, used,
                                             "a %d-step eager segment after the warm-up" % KERNEL_TIMED_LAUNCHES),

@@ -199,9 +199,10 @@ int32_t     mg_refresh_net_contact_force(mg_sim* sim, float* dst, int32_t dst_ho
  * gym.set_actor_root_state_tensor (test10_servo_vecenv.py:456) and the
  * _indexed variant: `src` is (num_actors, 13); when `idx` is non-NULL only the
  * n_idx actor rows it lists are applied (idx is int32, host or device like src).
- * src is consumed in stream order, so the caller may reuse it right away —
- * except for the fused root set (mg_set_fusion, MG_FUSE_ROOT_SET, on by
- * default): a device-resident, non-indexed set on a sim whose actor roots are
+ * src is consumed in stream order, so the caller may reuse it right away
+ * (Isaac Gym's copy-at-set contract, SURVEY.md §8b Ownership) — except for the
+ * fused root set (mg_set_fusion, MG_FUSE_ROOT_SET, opt-in, off by default): a
+ * device-resident, non-indexed set on a sim whose actor roots are
  * all single-shape free bodies is read by the next mg_simulate's free-body
  * kernel (the scatter fused into the step), or by the scatter that any earlier
  * call reading the state issues first (refresh_*, set_rigid_body_state, an
@@ -303,8 +304,11 @@ float       mg_last_render_ms(mg_sim* sim);
  * a rigid-body refresh into it is then served without a launch while no
  * simulate or set has changed the state. The bound rigid-body tensor is thus
  * refreshed no later than requested (possibly at the root refresh).
- * mg_set_fusion returns the previous flags; all but MG_FUSE_IN_CAPTURE are on by
- * default. The bound
+ * mg_set_fusion returns the previous flags. Every fusion is OFF by default:
+ * with it on, a set source is read after the set call and a rigid-body tensor
+ * may be refreshed early, which departs from Isaac Gym's tensor contract; the
+ * gymapi layer (gym.set_step_fusion) checks the sources' torch version counters
+ * and raises rather than read a source written after its set. The bound
  * pointers must stay valid for the sim's lifetime (NULL unbinds). */
 #define MG_FUSE_ROOT_SET  1
 #define MG_FUSE_REFRESH   2

@@ -26,6 +26,8 @@ def _load():
     vp = ctypes.c_void_p
     lib.oracle_step.restype = ctypes.c_int
     lib.oracle_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
+    lib.oracle_step_mt.restype = ctypes.c_int
+    lib.oracle_step_mt.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
     return lib
 
 
@@ -68,6 +70,26 @@ def step(sim_params, model, state, dof, tgt=None, props=None, ext=None, cforce=N
                            _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), int(b0), int(b1))
     if rc != 0:
         raise RuntimeError("oracle_step: unsupported model")
+    return cforce
+
+
+def step_threads(sim_params, model, state, dof, nthreads, tgt=None, props=None, ext=None, cforce=None):
+    """step() on `nthreads` host threads (oracle_step_mt, OpenMP): the same
+    result; the CPU baseline of bench.py."""
+    nb, nd = state.shape[0], dof.shape[0]
+    assert state.dtype == np.float32 and state.flags.c_contiguous and state.shape[1] == 13
+    assert dof.dtype == np.float32 and dof.flags.c_contiguous
+    if tgt is None:
+        tgt = np.zeros((max(nd, 1), 3), dtype=np.float32)
+    if cforce is None:
+        cforce = np.zeros((nb, 3), dtype=np.float32)
+    tgt_c = np.ascontiguousarray(tgt, dtype=np.float32)
+    props_c = None if props is None else np.ascontiguousarray(props, dtype=np.float32)
+    ext_c = None if ext is None else np.ascontiguousarray(ext, dtype=np.float32)
+    rc = lib().oracle_step_mt(ctypes.addressof(sim_params), ctypes.addressof(model), _ptr(state), _ptr(dof),
+                              _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), int(nthreads))
+    if rc != 0:
+        raise RuntimeError("oracle_step_mt: unsupported model")
     return cforce
 
 

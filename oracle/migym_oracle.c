@@ -573,7 +573,7 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
     for (d = 0; d < D; ++d) { q[d] = dof[(d0 + d) * 2 + 0]; qd[d] = dof[(d0 + d) * 2 + 1]; qdd[d] = 0.0f; }
     for (st_ = 0; st_ < P->substeps; ++st_) {
         float tau0d[OR_MAXL], impd[OR_MAXL], mdiag[OR_MAXL];
-        static aba_ws_t W;
+        static __thread aba_ws_t W;   /* per thread: oracle_step_mt */
         aba_world_(P, m, LF, LI, L, D, b0, d0, q, qd, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd, 0, ext);
         for (d = 0; d < D; ++d) {
             const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
@@ -656,6 +656,52 @@ int oracle_step(const mg_sim_params* p, const mg_model* m, float* state, float* 
         if (m->body_kind[b] != MG_BODY_FREE || owned[b]) continue;
         rigid_body_step(&P, m, b, state + (size_t)b * MG_STATE_N, ext ? ext + (size_t)b * 6 : NULL,
                         cforce + (size_t)b * 3);
+    }
+done:
+    free(envs);
+    free(owned);
+    return rc;
+}
+
+/* The same step on `nthreads` host threads (OpenMP, explicit num_threads: the
+ * CPU baseline of bench.py, SURVEY.md §8d "CPU beside it"). Envs, articulations
+ * and free bodies are independent, so each of the three loops is split across
+ * the threads after one classification; results equal oracle_step's. */
+int oracle_step_mt(const mg_sim_params* p, const mg_model* m, float* state, float* dof, const float* tgt,
+                   const float* props, const float* ext, float* cforce, int nthreads) {
+    step_t P = make_step_(p);
+    int ne, rc = 0;
+    oenv_t* envs = NULL;
+    char* owned = NULL;
+    if (!props) props = m->dof_props;
+    if (nthreads < 1) nthreads = 1;
+    envs = (oenv_t*)calloc((size_t)(m->num_envs > 0 ? m->num_envs : 1), sizeof(oenv_t));
+    owned = (char*)calloc((size_t)(m->num_bodies > 0 ? m->num_bodies : 1), 1);
+    if (!envs || !owned) { rc = -1; goto done; }
+    ne = classify_envs_(m, envs, owned);
+    if (ne < 0) { rc = -1; goto done; }
+    {
+        int bad = 0;
+#pragma omp parallel num_threads(nthreads) reduction(| : bad)
+        {
+            int k, b;
+#pragma omp for schedule(dynamic, 16)
+            for (k = 0; k < ne; ++k)
+                if (env_step_(&P, m, &envs[k], state, dof, tgt, props, ext, cforce) != 0) bad = 1;
+#pragma omp for schedule(static)
+            for (k = 0; k < m->num_artics; ++k) {
+                const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;
+                if (owned[ai[0]]) continue;
+                if (artic_step(&P, m, ai, state, dof, tgt, props, ext, cforce) != 0) bad = 1;
+            }
+#pragma omp for schedule(static)
+            for (b = 0; b < m->num_bodies; ++b) {
+                if (m->body_kind[b] != MG_BODY_FREE || owned[b]) continue;
+                rigid_body_step(&P, m, b, state + (size_t)b * MG_STATE_N, ext ? ext + (size_t)b * 6 : NULL,
+                                cforce + (size_t)b * 3);
+            }
+        }
+        if (bad) rc = -1;
     }
 done:
     free(envs);

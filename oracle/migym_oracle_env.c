@@ -349,6 +349,42 @@ static void cvx_edges_vs_(const cshape_t* X, const cshape_t* Y, float margin, in
         }
         if (!(t0 < t1)) continue;
         tm = 0.5f * (t0 + t1);
+        if (Y->type == MG_SHAPE_BOX) {   /* near a box edge: edge-edge normal (mg_collide.h) */
+            const v3_t mm = add3(al, mul3(ab, tm));
+            const float ex = fabsf(mm.x) - Y->h.x, ey = fabsf(mm.y) - Y->h.y, ez = fabsf(mm.z) - Y->h.z;
+            int k = 0;
+            float ek = ex, e1, e2;
+            if (ey < ek) { k = 1; ek = ey; }
+            if (ez < ek) k = 2;
+            e1 = k == 0 ? ey : ex;
+            e2 = k == 2 ? ey : ez;
+            if (e1 > -margin && e2 > -margin) {
+                const v3_t dk = V(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
+                const v3_t p0 = V(k == 0 ? 0.0f : (mm.x < 0.0f ? -Y->h.x : Y->h.x),
+                                  k == 1 ? 0.0f : (mm.y < 0.0f ? -Y->h.y : Y->h.y),
+                                  k == 2 ? 0.0f : (mm.z < 0.0f ? -Y->h.z : Y->h.z));
+                const v3_t nn = cross3(ab, dk);
+                const float l2 = dot3(nn, nn);
+                if (l2 > 1e-12f * dot3(ab, ab)) {
+                    v3_t n = mul3(nn, 1.0f / sqrtf(l2));
+                    v3_t r;
+                    float svv;
+                    if (dot3(n, p0) < 0.0f) n = mul3(n, -1.0f);
+                    r = sub3(al, p0);
+                    svv = dot3(n, r);
+                    if (svv < margin) {
+                        const float bq = dot3(ab, dk), aq = dot3(ab, ab);
+                        const float den = aq - bq * bq;
+                        const float ts = fminf(fmaxf((bq * dot3(dk, r) - dot3(ab, r)) / den, 0.0f), 1.0f);
+                        const v3_t pp = add3(Y->c, mv_(Y->R, add3(al, mul3(ab, ts))));
+                        const v3_t nw = mv_(Y->R, n);
+                        if (onY) deep4_add_(D, svv, sub3(pp, mul3(nw, svv)), mul3(nw, -1.0f));
+                        else deep4_add_(D, svv, pp, nw);
+                    }
+                    continue;
+                }
+            }
+        }
         p = add3(Y->c, mv_(Y->R, add3(al, mul3(ab, tm))));
         sv = cvx_sd_(Y, p, &f);
         if (sv < margin) {
@@ -379,8 +415,14 @@ static void convex_convex_(const cshape_t* A, const cshape_t* B, float margin, p
             deep4_add_(&D, sd, sub3(v, mul3(nA, sd)), mul3(nA, -1.0f));
         }
     }
-    if (D.n == 0 && A->type == MG_SHAPE_CONVEX && B->type == MG_SHAPE_CONVEX)   /* two hulls: A's edges (mg_collide.h) */
-        cvx_edges_vs_(A, B, margin, 0, &D, loA, hiA);
+    if (D.n == 0) {      /* no vertex candidate: edge crossings (mg_collide.h convex_convex) */
+        if (A->type == MG_SHAPE_BOX && B->type != MG_SHAPE_BOX) {
+            cvx_edges_vs_(B, A, margin, 1, &D, loB, hiB);
+        } else {
+            cvx_edges_vs_(A, B, margin, 0, &D, loA, hiA);
+            if (D.n == 0 && B->type != MG_SHAPE_BOX) cvx_edges_vs_(B, A, margin, 1, &D, loB, hiB);
+        }
+    }
     deep4_emit_(&D, o);
 }
 static void sph_cvx_(v3_t s, float r, const cshape_t* B, float margin, pair_t* o) {
@@ -894,21 +936,21 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     const int* LI = ti ? m->tmpl_link_i + (size_t)ti[0] * MG_LINK_I_N : NULL;
     const float h = P->h;
     const v3_t gvec = V(P->g[0], P->g[1], P->g[2]);
-    static epair_t pairs[OE_MAXPAIRS];
+    static __thread epair_t pairs[OE_MAXPAIRS];   /* per thread: oracle_step_mt */
     int npair;
     v3_t x0 = V(0.0f, 0.0f, 0.0f), gw = V(0.0f, 0.0f, 0.0f);
     q4_t q0 = Q(0.0f, 0.0f, 0.0f, 1.0f);
     /* slots */
     float q[OE_G], u[OE_G], dp[OE_G], qdd[OE_G], mdiag[OE_G], tau0d[OE_G], impd[OE_G];
     /* links */
-    static aba_ws_t W;
+    static __thread aba_ws_t W;   /* per thread: oracle_step_mt */
     v3_t* xl = W.xl; v3_t* zl = W.zl; q4_t* ql = W.ql;
     v3_t lsum[OR_MAXL];
     sv_t vl[OR_MAXL];
     float (*Iw)[36] = W.Iw;
     float (*xi)[6] = W.xi;
     int amask[OR_MAXL], dlink[OE_G], drev[OE_G];
-    static float Lc[OE_G][OE_G], Mi[OE_G][OE_G];
+    static __thread float Lc[OE_G][OE_G], Mi[OE_G][OE_G];
     float invd[OE_G];
     /* free bodies */
     v3_t fx[OE_MAXF], fxc[OE_MAXF], fcom[OE_MAXF], finvI[OE_MAXF], fext[OE_MAXF], text[OE_MAXF], fsum[OE_MAXF];
@@ -919,7 +961,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     int ca[OE_MAXCT], cb[OE_MAXCT];
     v3_t cp[OE_MAXCT], cd[OE_MAXCT][3];
     float cs0[OE_MAXCT], cmu[OE_MAXCT], ce[OE_MAXCT], cvn0[OE_MAXCT], ck[OE_MAXCT][3], clam[OE_MAXCT][3];
-    static float Jr[OE_MAXCT * 3][OE_G], Wr[OE_MAXCT * 3][OE_G];
+    static __thread float Jr[OE_MAXCT * 3][OE_G], Wr[OE_MAXCT * 3][OE_G];
     int d, l, k, c, i, j, st_, it;
     if (L > OR_MAXL || NS + 6 * nfr > OE_G || nfr > OE_MAXF) return -1;
     npair = env_pairs_(m, ev, P->ground, L, fb, pairs, OE_MAXPAIRS);

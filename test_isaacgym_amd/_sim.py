@@ -131,6 +131,8 @@ class Sim:
         self.env_offset = 0        # global index of this sim's first env (sharding.shard_sim)
         self.envs = []
         self.assets = []
+        self.num_actors = self.num_bodies = self.num_dofs = 0
+        self._idx_dirty = False    # global actor / body / DOF indices need a recompute
         self.finalized = False
         self.native = None
         self.frame = 0
@@ -143,7 +145,10 @@ class Sim:
         # state epoch: bumped by simulate and every state setter; the mass matrix
         # computed alongside the Jacobian is reused while the epoch is unchanged
         self.epoch = 0
-        self.held_src = []     # fused sets' tensors (root state, DOF targets), until the next simulate
+        self.held_src = []     # fused sets: (tensor, torch version at the set, setter), until the next simulate
+        # step fusion (gym.set_step_fusion; opt-in, MIGYM_STEP_FUSION sets the default)
+        self.fusion = int(os.environ.get("MIGYM_STEP_FUSION", "0") or 0) & 15
+        self.rb_paired_version = None   # rb tensor version after a fused root refresh filled it
         self.mm_cache = {}
         self._renderer = None
         self.cam_version = 0       # bumped by every camera change (render tables are rebuilt)
@@ -188,7 +193,23 @@ class Sim:
             for a in e.actors:
                 yield a
 
+    def note_actor_added(self, env, a):
+        """Global indices of an actor appended to the last env follow from the
+        running totals (the usual build order: O(1) per actor, so per-env index
+        queries while building, examples/franka_cube_ik_osc.py:255, stay linear);
+        an actor added to an earlier env shifts later ones: full recompute."""
+        if not self._idx_dirty and env is self.envs[-1]:
+            a.global_index, a.global_body, a.global_dof = self.num_actors, self.num_bodies, self.num_dofs
+            self.num_actors += 1
+            self.num_bodies += a.num_bodies
+            self.num_dofs += a.num_dofs
+        else:
+            self._idx_dirty = True
+
     def _assign_indices(self):
+        if not self._idx_dirty:
+            return
+        self._idx_dirty = False
         ai = bi = di = 0
         for e in self.envs:
             for a in e.actors:
@@ -436,6 +457,7 @@ class Sim:
             if root.is_cuda and rb.is_cuda and root.numel() and rb.numel():
                 N.check(N.lib.mg_bind_refresh_targets(handle, root.data_ptr(), rb.data_ptr()),
                         "mg_bind_refresh_targets")
+            N.lib.mg_set_fusion(handle, self.fusion)
             # actor DOF targets / props set before prepare
             self._push_dof_targets_all()
         self.finalized = True

@@ -10,9 +10,10 @@
 // ways — every vertex of one shape within the margin of the other, by the
 // other's face planes (signed distance = the largest plane distance, the face
 // attaining it gives the normal) — the 4 deepest kept; against spheres /
-// capsule caps: the centre's plane distance. Two hulls with no vertex within
-// the margin: edge crossings, A's edges clipped against B's planes, one
-// candidate at the chord's midpoint (cvx_edges_vs).
+// capsule caps: the centre's plane distance. With no vertex within the margin:
+// edge crossings, the non-box shape's edges clipped against the other's planes,
+// one candidate per chord — the edge-edge contact near a box edge, else the
+// chord's midpoint by the planes (cvx_edges_vs).
 // Box–box is SAT over the 15 axes (face axes preferred unless an edge axis
 // separates by more than 1e-3 m), then Sutherland–Hodgman clipping of the
 // incident face against the reference face (at most 8 points, the 4 deepest
@@ -516,6 +517,44 @@ MG_HD void cvx_edges_vs(const CShape& X, const CShape& Y, float margin, bool onY
         }
         if (!(t0 < t1)) continue;
         const float tm = 0.5f * (t0 + t1);
+        if (Y.type == MG_SHAPE_BOX) {
+            // the chord's midpoint m near a box edge (its two other coordinates
+            // within the margin of their faces, along the axis k it is deepest
+            // inside): an edge-edge contact — normal along the cross product of
+            // the two edges, pointing out of the box, separation the distance of
+            // the two lines along it, the point the closest one on X's edge
+            const V3 m = vadd(al, vscale(ab, tm));
+            const float ex = fabsf(m.x) - Y.h.x, ey = fabsf(m.y) - Y.h.y, ez = fabsf(m.z) - Y.h.z;
+            int k = 0;
+            float ek = ex;
+            if (ey < ek) { k = 1; ek = ey; }
+            if (ez < ek) k = 2;
+            const float e1 = k == 0 ? ey : ex, e2 = k == 2 ? ey : ez;
+            if (e1 > -margin && e2 > -margin) {
+                const V3 dk = v3(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
+                const V3 p0 = v3(k == 0 ? 0.0f : (m.x < 0.0f ? -Y.h.x : Y.h.x),
+                                 k == 1 ? 0.0f : (m.y < 0.0f ? -Y.h.y : Y.h.y),
+                                 k == 2 ? 0.0f : (m.z < 0.0f ? -Y.h.z : Y.h.z));
+                const V3 nn = vcross(ab, dk);
+                const float l2 = vdot(nn, nn);
+                if (l2 > 1e-12f * vdot(ab, ab)) {
+                    V3 n = vscale(nn, 1.0f / sqrtf(l2));
+                    if (vdot(n, p0) < 0.0f) n = vscale(n, -1.0f);
+                    const V3 r = vsub(al, p0);
+                    const float sv = vdot(n, r);
+                    if (sv < margin) {
+                        const float bq = vdot(ab, dk), aq = vdot(ab, ab);
+                        const float den = aq - bq * bq;
+                        const float ts = fminf(fmaxf((bq * vdot(dk, r) - vdot(ab, r)) / den, 0.0f), 1.0f);
+                        const V3 p = vadd(Y.c, mmul(Y.R, vadd(al, vscale(ab, ts))));
+                        const V3 nw = mmul(Y.R, n);
+                        if (onY) deep4_add(D, sv, vsub(p, vscale(nw, sv)), vscale(nw, -1.0f));
+                        else deep4_add(D, sv, p, nw);
+                    }
+                    continue;
+                }
+            }
+        }
         const V3 p = vadd(Y.c, mmul(Y.R, vadd(al, vscale(ab, tm))));
         int f;
         const float sv = cvx_sd(Y, p, f, 0.0f, margin);
@@ -536,12 +575,18 @@ MG_HD void convex_convex(const CShape& A, const CShape& B, float margin, PairOut
     V3 loA, hiA, loB, hiB;              // A's vertices in B's frame, B's in A's
     cvx_vertices_vs(A, B, margin, false, D, loA, hiA);
     cvx_vertices_vs(B, A, margin, true, D, loB, hiB);
-    if (D.n == 0 && A.type == MG_SHAPE_CONVEX && B.type == MG_SHAPE_CONVEX) {
-        // two hulls: an edge crossing puts an edge of each through the other, so
-        // A's edges find it. Not against a box: the face normal at a box's edge
-        // can point along the wrong face (a finger grazing a cube's top edge
-        // pressed it into the table in the 4096-env Franka test)
-        cvx_edges_vs(A, B, margin, false, D, loA, hiA);
+    if (D.n == 0) {
+        // edge crossings: the edges of the shape that is not a box, clipped by
+        // the box's 6 planes behind its face-axis test; two hulls: A's edges by
+        // B's planes, and when they find nothing B's by A's (a thin hull through
+        // the middle of a larger one's face crosses only B's edges: the result
+        // must not depend on the pair order)
+        if (A.type == MG_SHAPE_BOX && B.type != MG_SHAPE_BOX) {
+            cvx_edges_vs(B, A, margin, true, D, loB, hiB);
+        } else {
+            cvx_edges_vs(A, B, margin, false, D, loA, hiA);
+            if (D.n == 0 && B.type != MG_SHAPE_BOX) cvx_edges_vs(B, A, margin, true, D, loB, hiB);
+        }
     }
     deep4_emit(D, o);
 }

@@ -106,7 +106,7 @@ struct mg_sim {
     // refresh that follows is served by it while the state is unchanged.
     int* d_root_row = nullptr;
     bool roots_free = false;
-    int fusion = MG_FUSE_ROOT_SET | MG_FUSE_REFRESH | MG_FUSE_DOF_TARGETS;   // MG_FUSE_IN_CAPTURE: opt-in
+    int fusion = 0;   // opt-in (mg_set_fusion): Isaac Gym copies at set time and refreshes exactly what is asked
     const float* pend_root = nullptr;
     const float* pend_tgt[3] = {nullptr, nullptr, nullptr};   // fused DOF target sets (pos, vel, force)
     // stream-capture id (0: eager) at which each deferred set / the paired

@@ -62,6 +62,31 @@ def _as_tensor_arg(t, name):
     return tt
 
 
+# step fusion flags (gym.set_step_fusion; include/migym.h MG_FUSE_*)
+STEP_FUSION_ROOT_SET = 1
+STEP_FUSION_REFRESH = 2
+STEP_FUSION_DOF_TARGETS = 4
+STEP_FUSION_IN_CAPTURE = 8
+STEP_FUSION_ALL = 15
+
+
+def _check_held(sim, what):
+    """Copy-at-set guard for opt-in step fusion: a fused set's source is read at
+    the next simulate (or the flush before `what`), so it must still hold what it
+    held at the set call. Isaac Gym reads it during set_*_tensor
+    (SURVEY.md §8b Ownership); rather than read newer data silently, raise."""
+    if not sim.fusion:
+        return
+    for t, ver, setter in sim.held_src:
+        if t._version != ver:
+            sim.held_src = []
+            raise N.MigymError(
+                "%s: the tensor passed to %s was modified before the simulate that reads it; with step "
+                "fusion on (gym.set_step_fusion) a full device set is read at the next simulate, not at the "
+                "set call — write the source before the set, or turn fusion off (Isaac Gym copies at set "
+                "time)" % (what, setter))
+
+
 _PHYSX_DEFAULTS = _T.PhysXParams()
 _warned_physx = set()
 
@@ -126,11 +151,32 @@ class Gym:
     def simulate(self, sim):
         """One frame (test10_servo_vecenv.py:380): the fused HIP step kernels."""
         h = sim.require_native("gym.simulate")
+        _check_held(sim, "simulate")
         N.check(N.lib.mg_simulate(h, sim.stream()), "mg_simulate")
         sim.held_src = []
         sim.epoch += 1
         sim.frame += 1
         sim.time += sim.params.dt
+
+    def set_step_fusion(self, sim, flags):
+        """migym extension (not in Isaac Gym): opt in to step fusion
+        (include/migym.h mg_set_fusion; STEP_FUSION_* flags, 0 = off, the
+        default). With it, a full device-resident set_actor_root_state_tensor /
+        set_dof_*_target_tensor / set_dof_actuation_force_tensor is read by the
+        next simulate instead of at the set call, and a root-state refresh also
+        refreshes the rigid-body tensor. Isaac Gym copies the source at the set
+        call (SURVEY.md §8b Ownership), so a source written between its set and
+        the simulate that consumes it raises MigymError instead of being read
+        (torch version counters); the environment variable MIGYM_STEP_FUSION sets
+        the default for new sims. Returns the previous flags."""
+        prev = sim.fusion
+        sim.fusion = int(flags) & STEP_FUSION_ALL
+        if sim.native:
+            N.lib.mg_set_fusion(sim.native, sim.fusion)
+        return prev
+
+    def get_step_fusion(self, sim):
+        return sim.fusion
 
     def fetch_results(self, sim, wait=True):
         if sim.native:
@@ -297,6 +343,7 @@ class Gym:
         env.actors.append(a)
         env.num_bodies += a.num_bodies
         env.num_dofs += a.num_dofs
+        env.sim.note_actor_added(env, a)
         return a.handle
 
     def _actor(self, env, handle):
@@ -494,6 +541,7 @@ class Gym:
     def _host_state(self, sim):
         """Current (body_state[nb,13], dof_state[nd,2]) on the host."""
         sim.finalize()
+        _check_held(sim, "a host state read")
         if sim.native is None:
             A = sim.model_arrays
             return A["body_state0"].copy(), A["dof_state0"].copy()
@@ -745,7 +793,17 @@ class Gym:
         if t.numel() == 0:
             return True
         h = sim.require_native(what)
+        _check_held(sim, what)
+        if key == "rb" and sim.rb_paired_version is not None and t._version != sim.rb_paired_version:
+            # the user wrote the rigid-body tensor after the paired root refresh
+            # filled it: re-gather it (rebinding clears the served-by-root mark)
+            N.check(N.lib.mg_bind_refresh_targets(h, sim.tensors["root"].data_ptr(), t.data_ptr()),
+                    "mg_bind_refresh_targets")
         N.check(fn(h, t.data_ptr(), 1 if t.device.type == "cpu" else 0, sim.stream()), what)
+        if key == "root" and sim.fusion & STEP_FUSION_REFRESH:
+            sim.rb_paired_version = sim.tensors["rb"]._version
+        elif key == "rb":
+            sim.rb_paired_version = None
         return True
 
     def refresh_actor_root_state_tensor(self, sim):
@@ -765,6 +823,7 @@ class Gym:
         sim.finalize()
         sim.epoch += 1
         t = _as_tensor_arg(tensor, what)
+        _check_held(sim, what)
         if t.dtype != torch.float32 or t.numel() != nrows * ncols:
             print("*** migym: %s: expected a float32 tensor of %d x %d" % (what, nrows, ncols), file=sys.stderr)
             return False
@@ -797,9 +856,10 @@ class Gym:
             rc = fn(sim.require_native(what), t.data_ptr(), host, it.data_ptr(), n, sim.stream())
         else:
             rc = fn(sim.require_native(what), t.data_ptr(), host, None, 0, sim.stream())
-            # a fused set (MG_FUSE_ROOT_SET / MG_FUSE_DOF_TARGETS) is read by the
-            # next simulate: keep its tensor alive until then
-            sim.held_src.append(t)
+            # a fused set (opt-in: STEP_FUSION_ROOT_SET / _DOF_TARGETS) is read by
+            # the next simulate: keep its tensor alive until then and remember its
+            # version, so a write to it before that read raises (_check_held)
+            sim.held_src.append((t, t._version, what))
         if rc != N.MG_OK:
             print("*** migym: %s: %s" % (what, N.last_error()), file=sys.stderr)
             return False
@@ -817,6 +877,7 @@ class Gym:
     def set_rigid_body_state_tensor(self, sim, tensor):
         sim.finalize()
         t = _as_tensor_arg(tensor, "set_rigid_body_state_tensor")
+        _check_held(sim, "set_rigid_body_state_tensor")
         if t.numel() != sim.num_bodies * 13:
             return False
         h = sim.require_native("set_rigid_body_state_tensor")
@@ -1079,6 +1140,7 @@ class Gym:
     def render_all_camera_sensors(self, sim):
         """test11_servo_vecenv_camerazoom.py:388: freezes the poses the cameras
         see and renders every camera that has a GPU image tensor (one launch)."""
+        _check_held(sim, "render_all_camera_sensors")
         return sim.renderer.render_all()
 
     def start_access_image_tensors(self, sim):

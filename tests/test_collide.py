@@ -25,6 +25,13 @@ def _quat(axis, ang):
     return np.array([axis[0] * s, axis[1] * s, axis[2] * s, math.cos(0.5 * ang)])
 
 
+def _qmul(a, b):
+    ax, ay, az, aw = a
+    bx, by, bz, bw = b
+    return (aw * bx + ax * bw + ay * bz - az * by, aw * by - ax * bz + ay * bw + az * bx,
+            aw * bz + ax * by - ay * bx + az * bw, aw * bw - ax * bx - ay * by - az * bz)
+
+
 def _rot(q):
     x, y, z, w = q
     return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
@@ -228,6 +235,48 @@ def test_hull_edge_edge_crossing():
             Bb = _shape(BOX, B[1:4], B[4:8], (h, h, h))
             ob = oracle.collide(Ab, Bb, margin)
             assert len(ob) == 1 and abs(ob[0, 6] + depth) < 2e-5
+
+
+def test_hull_box_edge_edge_matches_sat():
+    """A cube hull crossing a box edge to edge (no vertex inside): the box-edge
+    branch of the edge pass gives the edge-edge normal and line distance, the
+    same contact as box-box SAT (random crossing angles and depths)."""
+    h = 0.05
+    rec = _hull_of_box((h, h, h)).record()
+    r2 = h * math.sqrt(2)
+    rng = np.random.RandomState(2)
+    for _ in range(20):
+        depth = rng.uniform(0.0002, 0.002)
+        yaw = rng.uniform(-0.5, 0.5)
+        qa = _quat((1, 0, 0), math.pi / 4)
+        qb = _qmul(_quat((0, 0, 1), yaw), _quat((0, 1, 0), math.pi / 4))
+        for hull_on_a in (True, False):
+            A = _shape(CONVEX if hull_on_a else BOX, (0, 0, 0), qa, (h * math.sqrt(3), 0, 0) if hull_on_a else (h, h, h))
+            B = _shape(BOX if hull_on_a else CONVEX, (0, 0, 2 * r2 - depth), qb,
+                       (h, h, h) if hull_on_a else (h * math.sqrt(3), 0, 0))
+            out = oracle.collide(A, B, 0.01, hull_a=rec if hull_on_a else None, hull_b=None if hull_on_a else rec)
+            ref = oracle.collide(_shape(BOX, A[1:4], A[4:8], (h, h, h)), _shape(BOX, B[1:4], B[4:8], (h, h, h)), 0.01)
+            assert len(out) == 1 and len(ref) == 1
+            assert abs(out[0, 6] - ref[0, 6]) < 2e-5
+            assert np.allclose(out[0, 3:6], ref[0, 3:6], atol=1e-4)
+
+
+def test_hull_edge_crossing_independent_of_pair_order():
+    """A thin rod hull pushed through the middle of a cube hull's faces, no vertex
+    of either inside the other: only the rod's edges cross the cube, the cube's
+    edges miss the rod. Both pair orders find the crossing (A's edges first, then
+    B's when A's find nothing), with the same separation and opposite normals."""
+    rod = _hull_of_box((0.002, 0.002, 0.15)).record()
+    cube = _hull_of_box((0.1, 0.1, 0.1)).record()
+    q = _quat((0, 0, 1), 0.3)
+    R = _shape(CONVEX, (0.01, -0.02, 0.0), q, (math.sqrt(2 * 0.002 ** 2 + 0.15 ** 2), 0, 0))
+    C = _shape(CONVEX, (0, 0, 0), (0, 0, 0, 1), (0.1 * math.sqrt(3), 0, 0))
+    rc = oracle.collide(R, C, 0.01, hull_a=rod, hull_b=cube)
+    cr = oracle.collide(C, R, 0.01, hull_a=cube, hull_b=rod)
+    assert len(rc) >= 1 and len(cr) == len(rc)
+    assert np.allclose(np.sort(rc[:, 6]), np.sort(cr[:, 6]), atol=1e-6)
+    assert rc[:, 6].max() < -0.05                       # deep inside the cube
+    assert np.allclose(rc[np.argmin(rc[:, 6]), 3:6], -cr[np.argmin(cr[:, 6]), 3:6], atol=1e-6)
 
 
 def test_hull_against_ground_and_sphere():

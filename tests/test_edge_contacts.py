@@ -7,6 +7,9 @@ it: the first contact is an edge crossing with no vertex of either cube within
 the contact offset of the other, the case the vertex tests alone miss (the cube
 fell through the ridge before). It lands on the ridge and balances there until
 rounding tips it off (an unstable equilibrium), as a physical cube would.
+The same with one of the two cubes a box primitive (gym.create_box): a hull
+edge crossing a box edge, where the edge pass gives the edge-edge normal (the
+cross product of the two edges) instead of a box face's.
 CPU: the oracle's behaviour; GPU: k_env_step bit for bit the oracle, 64 envs
 with small random offsets.
 """
@@ -36,7 +39,10 @@ def _cube_urdf(d):
     return "cube.urdf"
 
 
-def _scene(gym, d, n, gpu, seed=0):
+KINDS = ("hull_hull", "box_wedge", "box_cube")
+
+
+def _scene(gym, d, n, gpu, seed=0, kind="hull_hull"):
     sp = gymapi.SimParams()
     sp.up_axis = gymapi.UP_AXIS_Z
     sp.gravity = gymapi.Vec3(0, 0, -9.8)
@@ -51,9 +57,15 @@ def _scene(gym, d, n, gpu, seed=0):
     f = _cube_urdf(d)
     fixed = gymapi.AssetOptions()
     fixed.fix_base_link = True
-    wedge = gym.load_asset(sim, d, f, fixed)
-    cube = gym.load_asset(sim, d, f, gymapi.AssetOptions())
-    assert cube.bodies[0].shapes[0].type == 3                  # a hull, not a box
+    if kind == "box_wedge":
+        wedge = gym.create_box(sim, 2 * H, 2 * H, 2 * H, fixed)
+    else:
+        wedge = gym.load_asset(sim, d, f, fixed)
+    if kind == "box_cube":
+        cube = gym.create_box(sim, 2 * H, 2 * H, 2 * H, gymapi.AssetOptions())
+    else:
+        cube = gym.load_asset(sim, d, f, gymapi.AssetOptions())
+        assert cube.bodies[0].shapes[0].type == 3              # a hull, not a box
     qy = gymapi.Quat.from_axis_angle(gymapi.Vec3(0, 1, 0), math.pi / 4)
     qx = gymapi.Quat.from_axis_angle(gymapi.Vec3(1, 0, 0), math.pi / 4)
     rng = np.random.RandomState(seed)
@@ -65,8 +77,9 @@ def _scene(gym, d, n, gpu, seed=0):
     return sim
 
 
-def test_cube_lands_on_ridge_edge_crossing(gym, tmp_path):
-    sim = _scene(gym, str(tmp_path), 1, False)
+@pytest.mark.parametrize("kind", KINDS)
+def test_cube_lands_on_ridge_edge_crossing(gym, tmp_path, kind):
+    sim = _scene(gym, str(tmp_path), 1, False, kind=kind)
     A = sim.build_model()
     p, m = sim.mg_params(), sim.mg_model()
     st = A["body_state0"].copy()
@@ -80,9 +93,10 @@ def test_cube_lands_on_ridge_edge_crossing(gym, tmp_path):
 
 
 @pytest.mark.gpu
-def test_edge_crossing_parity_gpu(gym, tmp_path):
+@pytest.mark.parametrize("kind", KINDS)
+def test_edge_crossing_parity_gpu(gym, tmp_path, kind):
     n, steps = 64, 45
-    sim = _scene(gym, str(tmp_path), n, True, seed=4)
+    sim = _scene(gym, str(tmp_path), n, True, seed=4, kind=kind)
     gym.prepare_sim(sim)
     rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
     ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))

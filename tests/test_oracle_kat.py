@@ -186,3 +186,30 @@ def test_joint_limit_clamp(gym):
         oracle.step(p, m, st, ds, tgt=tgt)
     assert ds[0, 0] == pytest.approx(0.5, abs=1e-6)
     assert ds[0, 1] == 0.0
+
+
+def test_step_threads_equals_step():
+    """oracle.step_threads (OpenMP, bench.py's CPU baseline) gives oracle.step's
+    result bit for bit on the S1, S2 and S3 scenes."""
+    import bench
+    import oracle as O
+    for leg, n in (("s1", 64), ("s2", 32), ("s3", 8)):
+        sim, hook, tgt = bench._cpu_scene(leg, n)
+        p, m = sim.mg_params(), sim.mg_model()
+        st0 = sim.model_arrays["body_state0"].copy()
+        d0 = sim.model_arrays["dof_state0"].copy()
+        if tgt is None:
+            tgt = np.zeros((max(d0.shape[0], 1), 3), np.float32)
+        outs = []
+        for nt in (0, 4):
+            st, dof = st0.copy(), d0.copy()
+            for k in range(5):
+                hook(st, tgt, k)
+                if nt:
+                    O.step_threads(p, m, st, dof, nt, tgt=tgt)
+                else:
+                    O.step(p, m, st, dof, tgt=tgt)
+            outs.append((st, dof))
+        assert np.array_equal(outs[0][0], outs[1][0]), leg
+        assert np.array_equal(outs[0][1], outs[1][1]), leg
+        assert not np.array_equal(outs[0][0], st0), leg

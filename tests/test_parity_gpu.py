@@ -103,8 +103,8 @@ def test_fused_step_matches_unfused(gym):
     for fused in (True, False):
         sim, _ = scenes.servo_scene(gym, n)
         gym.prepare_sim(sim)
-        if not fused:
-            N.lib.mg_set_fusion(sim.native, 0)
+        if fused:
+            gym.set_step_fusion(sim, gymapi.STEP_FUSION_ALL)
         sims.append((sim, _tensors(gym, sim)))
     acts = scenes.servo_actions(n, steps, DEV, seed=4)
     for sim, (root, _, _, _) in sims:
@@ -132,6 +132,82 @@ def test_fused_step_matches_unfused(gym):
     root.zero_()
     gym.refresh_actor_root_state_tensor(sim)
     assert torch.equal(root, want)
+
+
+def test_step_fusion_copy_at_set_contract(gym):
+    """Isaac Gym reads a set_*_tensor source during the set call (SURVEY.md §8b
+    Ownership). With step fusion off (the default) a source written after its
+    set and before simulate does not reach the step: the result equals a sim
+    given an untouched copy, bit for bit. With fusion on (opt-in) that write
+    raises MigymError instead of being read. Same for DOF position targets. A
+    rigid-body tensor edited by the user survives a root refresh (fusion off),
+    and with fusion on a later rigid-body refresh re-gathers the edited tensor."""
+    from test_isaacgym_amd import _native as N
+    n = 64
+    acts = scenes.servo_actions(n, 2, DEV, seed=9)
+    outs = []
+    for mode in ("copy", "write_after_set"):
+        sim, _ = scenes.servo_scene(gym, n)
+        gym.prepare_sim(sim)
+        root, rb, _, _ = _tensors(gym, sim)
+        gym.refresh_actor_root_state_tensor(sim)
+        root[:, 3:10] = acts[0]
+        src = root.clone()
+        assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(src))
+        if mode == "write_after_set":
+            src[:, 3:10] = acts[1]          # too late: the set already took its copy
+        gym.simulate(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        outs.append(rb.clone())
+        # user edits to the rigid-body tensor survive a root refresh (no fusion)
+        rb[:, 0] = -7.0
+        gym.refresh_actor_root_state_tensor(sim)
+        assert torch.all(rb[:, 0] == -7.0)
+        gym.destroy_sim(sim)
+    assert torch.equal(outs[0], outs[1])
+    # fusion on: the same write raises at simulate; an edited rb tensor is re-gathered
+    sim, _ = scenes.servo_scene(gym, n)
+    gym.prepare_sim(sim)
+    gym.set_step_fusion(sim, gymapi.STEP_FUSION_ALL)
+    root, rb, _, _ = _tensors(gym, sim)
+    gym.refresh_actor_root_state_tensor(sim)
+    src = root.clone()
+    src[:, 3:10] = acts[0]
+    assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(src))
+    src[:, 3:10] = acts[1]
+    with pytest.raises(N.MigymError):
+        gym.simulate(sim)
+    assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(src))
+    gym.simulate(sim)
+    gym.refresh_actor_root_state_tensor(sim)       # fused: fills rb as well
+    want = rb.clone()
+    rb[:, 0] = -7.0
+    gym.refresh_rigid_body_state_tensor(sim)
+    assert torch.equal(rb, want)
+    gym.destroy_sim(sim)
+    # DOF position targets
+    tg = scenes.gimbal_targets(16, 2, DEV, seed=3)
+    douts = []
+    for fusion in (0, gymapi.STEP_FUSION_ALL):
+        for write_after in (False, True):
+            sim, _ = scenes.gimbal_scene(gym, 16)
+            gym.prepare_sim(sim)
+            gym.set_step_fusion(sim, fusion)
+            dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+            t = tg[0].clone()
+            assert gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(t))
+            if write_after:
+                t.copy_(tg[1])
+            if fusion and write_after:
+                with pytest.raises(N.MigymError):
+                    gym.simulate(sim)
+            else:
+                gym.simulate(sim)
+                gym.refresh_dof_state_tensor(sim)
+                douts.append(dof.clone())
+            gym.destroy_sim(sim)
+    assert len(douts) == 3
+    assert torch.equal(douts[0], douts[1]) and torch.equal(douts[0], douts[2])
 
 
 def test_servo_trajectory_bitexact(gym):
@@ -627,7 +703,7 @@ def test_hipgraph_replay_matches_eager(gym):
         sim, _ = scenes.servo_scene(gym, n)
         gym.prepare_sim(sim)
         if mode == "graph5_fused":   # MG_FUSE_IN_CAPTURE: the fused set / refresh inside the graph
-            N.lib.mg_set_fusion(sim.native, 1 | 2 | 4 | 8)
+            gym.set_step_fusion(sim, gymapi.STEP_FUSION_ALL)
         root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
         rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
         acts = scenes.servo_actions(n, 8, DEV, seed=5)
