@@ -51,6 +51,8 @@ ENVS_PER_GPU = 4096
 LARGE_N = 262144
 SIM_BYTES_PER_ENV = 376          # simulate share of the 688 B/env-step
 STEP_BYTES_PER_ENV = 688         # whole tensor-API step
+S2_BYTES_PER_ENV = 532           # SURVEY.md §8d S2 (servo-arm gimbal)
+S2_LARGE_N = 262144
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 KERNEL_TIMED_LAUNCHES = 128      # eager launches with dispatch timestamps (ring holds 256)
 GRAPH_CHUNK_MAX = 64             # tensor-API steps captured per hipGraph at most (amortizes the graph launch)
@@ -175,7 +177,7 @@ def rigid_roofline(n, kern_ms, kmin, launches, segment):
     bytes_launch = SIM_BYTES_PER_ENV * n
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms else None
     pmc, pmc_file = load_pmc("rigid_%d" % n)
-    return {"bound": "hbm", "kernel": "k_rigid_step",
+    return {"bound": "hbm", "kernel": "k_rigid_step1",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
@@ -270,28 +272,38 @@ def cpu_leg(leg, n, seconds, thread_counts):
 
 def cpu_baseline(seconds=10.0):
     """SURVEY.md §8d "CPU beside it" / BASELINE.md §3: the oracle (C restatement,
-    "port") on every host core os.cpu_count() reports (OpenMP, num_threads set
-    explicitly), on the three bench scenes at 4096 envs: S1 (the headline), S2,
-    S3. Also 16 threads (the GPU box's CPU share per GPU) and 1 thread for S1."""
+    "port") on the host's cores (OpenMP, num_threads set explicitly), on the
+    three bench scenes at 4096 envs: S1 (the headline), S2, S3.
+
+    `cores` is the CPUs this process can actually use: os.cpu_count() bounded by
+    the affinity mask and the cgroup CPU quota (the GPU box reports 256 CPUs but
+    grants a quota of 16; 256 OpenMP threads under that quota are throttled to a
+    few steps per second, so that figure is reported beside it, not as the
+    baseline). Also 1 thread for S1."""
     ncpu, aff, quota = cpu_threads()
+    usable = max(1, min(ncpu, aff, int(quota) if quota else ncpu))
     n = ENVS_PER_GPU
-    s1 = cpu_leg("s1", n, seconds, [(ncpu, seconds * 0.4), (16, seconds * 0.2), (1, seconds * 0.2)])
-    s2 = cpu_leg("s2", n, seconds, [(ncpu, seconds * 0.3), (16, seconds * 0.15)])
-    s3 = cpu_leg("s3", n, seconds, [(ncpu, seconds * 0.5), (16, seconds * 0.3)])
+    extra = [(ncpu, seconds * 0.1)] if ncpu != usable else []
+    s1 = cpu_leg("s1", n, seconds, [(usable, seconds * 0.4), (1, seconds * 0.2)] + extra)
+    s2 = cpu_leg("s2", n, seconds, [(usable, seconds * 0.3)] + extra)
+    s3 = cpu_leg("s3", n, seconds, [(usable, seconds * 0.5)] + extra)
 
     def leg(r, what):
-        v, steps, el = r[ncpu]
-        return {"value": v, "unit": "env-steps/s", "cores": ncpu, "steps": steps, "seconds": el,
-                "value_16_threads": r[16][0], "sample": what}
-    out = leg(s1, "%d simulate() steps of the 4096-env servo scene with random root teleports (S1)" % s1[ncpu][1])
+        v, steps, el = r[usable]
+        d = {"value": v, "unit": "env-steps/s", "cores": usable, "steps": steps, "seconds": el, "sample": what}
+        if ncpu in r and ncpu != usable:
+            d["value_all_host_threads"] = r[ncpu][0]
+        return d
+    out = leg(s1, "%d simulate() steps of the 4096-env servo scene with random root teleports (S1)" % s1[usable][1])
     out.update({"kind": "port", "host_cpu_count": ncpu, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
                 "single_thread_value": s1[1][0],
                 "note": "oracle/migym_oracle.c (CPU restatement, not Isaac Gym: the reference engine is a closed "
-                        "binary absent here) via oracle_step_mt, OpenMP with num_threads = os.cpu_count(); "
-                        "the box's cgroup quota (cgroup_cpu_quota CPUs) caps what those threads get",
-                "s2": leg(s2, "%d simulate() steps of 4096 3-DOF gimbals under random PD targets (S2)" % s2[ncpu][1]),
+                        "binary absent here) via oracle_step_mt, OpenMP with num_threads = cores = os.cpu_count() "
+                        "bounded by the affinity mask and the cgroup CPU quota; value_all_host_threads = the same "
+                        "with os.cpu_count() threads, throttled by that quota",
+                "s2": leg(s2, "%d simulate() steps of 4096 3-DOF gimbals under random PD targets (S2)" % s2[usable][1]),
                 "s3": leg(s3, "%d simulate() steps of 4096 Franka cube-pick envs holding their default DOF "
-                              "targets (S3 physics only; the OSC controller is not in the oracle)" % s3[ncpu][1])})
+                              "targets (S3 physics only; the OSC controller is not in the oracle)" % s3[usable][1])})
     out["sample"] = out["sample"] + "; S2 and S3 under s2 / s3"
     return out
 
@@ -343,12 +355,20 @@ def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     gym.destroy_sim(sim)
-    ach = 532 * n / (kms * 1e-3) / 1e9 if kms else None
+    ach = S2_BYTES_PER_ENV * n / (kms * 1e-3) / 1e9 if kms else None
+    pmc, pmc_file = load_pmc("gimbal_%d" % n)
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
             "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graphs is not None else "eager Python loop",
-            "kernel": "S2 articulation step", "kernel_ms_avg": kms, "kernel_ms_min": kmin,
-            "kernel_launches_timed": used, "algorithmic_bytes_per_env": 532,
-            "kernel_achieved_GBs": ach}
+            "kernel": "S2 articulation step (k_artic_chain<4>)", "kernel_ms_avg": kms, "kernel_ms_min": kmin,
+            "kernel_launches_timed": used, "algorithmic_bytes_per_env": S2_BYTES_PER_ENV,
+            "kernel_achieved_GBs": ach,
+            "roofline": {"bound": "hbm", "kernel": "k_artic_chain<4>", "achieved": ach, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": (ach / HBM_PEAK_GBS) if ach else None,
+                         "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None, "traffic_source": pmc_file,
+                         "algorithmic_bytes_per_launch": S2_BYTES_PER_ENV * n,
+                         "note": "SURVEY.md §8d S2: 532 B per env-step (DOF state in/out, targets, drive params, "
+                                 "link mass properties, target set, DOF + rigid-body refresh) priced on the "
+                                 "simulate kernel's own dispatch-timestamp duration"}}
 
 
 def franka_rate(n, steps, warmup, dev, use_graph=True):
@@ -836,6 +856,8 @@ def main():
             out["large_n"] = large_n_rate(args.large_n, 64, dev, not args.eager)
         if not args.no_gimbal:
             out["s2_servo_arm"] = gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
+            if not args.no_large_n:
+                out["s2_servo_arm"]["large_n"] = gimbal_rate(S2_LARGE_N, 64, 10, dev, not args.eager)
         if not args.no_franka:
             out["s3_franka"] = franka_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
         if not args.no_cameras:

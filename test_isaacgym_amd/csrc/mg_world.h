@@ -1,5 +1,5 @@
 // mg_world.h — world-frame spatial quantities shared by the articulated-body
-// kernels (mg_env.hip aba_world, mg_artic.hip k_artic_world): 6-vectors as
+// kernels (mg_env.hip k_env_step / k_artic_lanes / k_artic_chain, mg_artic.hip k_artic_jac_mm): 6-vectors as
 // float[6] (angular, linear), link mass constants, and the world-frame spatial
 // inertia of a link about a point. Restated in oracle/migym_oracle_env.c.
 #pragma once

@@ -60,7 +60,7 @@ struct ArticGroup {
     int tmpl, first_link, nl, ndof, fixed_base;
     int nbody;                     // bodies per instance (nl minus the virtual links of ball joints)
     int offset, count;             // into the template-sorted instance list (all instances)
-    int step_offset, step_count;   // into the list stepped by k_artic_step (uncoupled envs)
+    int step_offset, step_count;   // into the list stepped by k_artic_chain / k_artic_lanes (uncoupled envs)
 };
 
 // coupled envs (mg_env.hip) of one articulation template (tmpl -1: none)
@@ -128,7 +128,7 @@ struct mg_sim {
     float* d_link_f = nullptr;
     int* d_link_i = nullptr;
     std::vector<ArticGroup> groups;
-    int* d_artic_step = nullptr;  // [..][4] instances stepped by k_artic_step
+    int* d_artic_step = nullptr;  // [..][4] instances stepped by k_artic_chain / k_artic_lanes
     int* d_env = nullptr;         // [n_coupled][MG_ENV_I_N] coupled envs, by group
     int* d_pairs = nullptr;       // [..][4] candidate shape pairs of the coupled envs
     int n_coupled = 0;

@@ -70,14 +70,25 @@ STEP_FUSION_IN_CAPTURE = 8
 STEP_FUSION_ALL = 15
 
 
-def _check_held(sim, what):
-    """Copy-at-set guard for opt-in step fusion: a fused set's source is read at
-    the next simulate (or the flush before `what`), so it must still hold what it
-    held at the set call. Isaac Gym reads it during set_*_tensor
-    (SURVEY.md §8b Ownership); rather than read newer data silently, raise."""
-    if not sim.fusion:
+_FUSED_KIND = {"mg_set_actor_root_state": "root", "mg_set_dof_position_target": "tgt0",
+               "mg_set_dof_velocity_target": "tgt1", "mg_set_dof_actuation_force": "tgt2"}
+
+
+def _check_held(sim, what, kinds=None):
+    """Copy-at-set guard for opt-in step fusion. A fused set's source is read by
+    the call that consumes the pending set — the next simulate, or for a root set
+    any earlier reader of the state (the library flushes it as a scatter) — so it
+    must still hold what it held at the set call: Isaac Gym reads it during
+    set_*_tensor (SURVEY.md §8b Ownership). Rather than read newer data silently,
+    raise. `kinds`: the pending sets this call consumes (None: all); consumed
+    entries are dropped."""
+    if not sim.held_src:
         return
-    for t, ver, setter in sim.held_src:
+    keep = []
+    for t, ver, setter, kind in sim.held_src:
+        if kinds is not None and kind not in kinds:
+            keep.append((t, ver, setter, kind))
+            continue
         if t._version != ver:
             sim.held_src = []
             raise N.MigymError(
@@ -85,6 +96,7 @@ def _check_held(sim, what):
                 "fusion on (gym.set_step_fusion) a full device set is read at the next simulate, not at the "
                 "set call — write the source before the set, or turn fusion off (Isaac Gym copies at set "
                 "time)" % (what, setter))
+    sim.held_src = keep
 
 
 _PHYSX_DEFAULTS = _T.PhysXParams()
@@ -541,7 +553,7 @@ class Gym:
     def _host_state(self, sim):
         """Current (body_state[nb,13], dof_state[nd,2]) on the host."""
         sim.finalize()
-        _check_held(sim, "a host state read")
+        _check_held(sim, "a host state read", ("root",))
         if sim.native is None:
             A = sim.model_arrays
             return A["body_state0"].copy(), A["dof_state0"].copy()
@@ -793,7 +805,8 @@ class Gym:
         if t.numel() == 0:
             return True
         h = sim.require_native(what)
-        _check_held(sim, what)
+        if key in ("root", "rb"):
+            _check_held(sim, what, ("root",))      # flushes a pending root set
         if key == "rb" and sim.rb_paired_version is not None and t._version != sim.rb_paired_version:
             # the user wrote the rigid-body tensor after the paired root refresh
             # filled it: re-gather it (rebinding clears the served-by-root mark)
@@ -823,7 +836,9 @@ class Gym:
         sim.finalize()
         sim.epoch += 1
         t = _as_tensor_arg(tensor, what)
-        _check_held(sim, what)
+        kind = _FUSED_KIND.get(getattr(fn, "__name__", ""))
+        if kind is not None:
+            _check_held(sim, what, (kind,))        # a set of the same kind applies / replaces the pending one
         if t.dtype != torch.float32 or t.numel() != nrows * ncols:
             print("*** migym: %s: expected a float32 tensor of %d x %d" % (what, nrows, ncols), file=sys.stderr)
             return False
@@ -859,7 +874,8 @@ class Gym:
             # a fused set (opt-in: STEP_FUSION_ROOT_SET / _DOF_TARGETS) is read by
             # the next simulate: keep its tensor alive until then and remember its
             # version, so a write to it before that read raises (_check_held)
-            sim.held_src.append((t, t._version, what))
+            if kind is not None and sim.fusion:
+                sim.held_src.append((t, t._version, what, kind))
         if rc != N.MG_OK:
             print("*** migym: %s: %s" % (what, N.last_error()), file=sys.stderr)
             return False
@@ -877,7 +893,7 @@ class Gym:
     def set_rigid_body_state_tensor(self, sim, tensor):
         sim.finalize()
         t = _as_tensor_arg(tensor, "set_rigid_body_state_tensor")
-        _check_held(sim, "set_rigid_body_state_tensor")
+        _check_held(sim, "set_rigid_body_state_tensor", ("root",))
         if t.numel() != sim.num_bodies * 13:
             return False
         h = sim.require_native("set_rigid_body_state_tensor")
@@ -1140,7 +1156,7 @@ class Gym:
     def render_all_camera_sensors(self, sim):
         """test11_servo_vecenv_camerazoom.py:388: freezes the poses the cameras
         see and renders every camera that has a GPU image tensor (one launch)."""
-        _check_held(sim, "render_all_camera_sensors")
+        _check_held(sim, "render_all_camera_sensors", ("root",))
         return sim.renderer.render_all()
 
     def start_access_image_tensors(self, sim):

@@ -1,7 +1,9 @@
 """Kernel microbenchmark of the coupled per-env step (k_env_step): the S3
 Franka cube-pick loop (OSC controller) at n envs; warm frames bring the arms to
 the cubes (grasp contacts), then the average simulate() kernel time over the
-timed frames (HIP events). Library from MIGYM_LIB (default in-tree)."""
+timed frames (HIP events), then the loop continues to KB_FRAMES (default 600)
+frames for the fraction of cubes lifted above 0.55 m and the cubes at rest
+inside the table. Library from MIGYM_LIB (default in-tree)."""
 import ctypes
 import json
 import os
@@ -30,7 +32,11 @@ def run(n, warm=150, steps=100):
     h = info["hand_index"]
     bi = torch.tensor(info["box_idxs"], device="cuda:0")
     hi = torch.tensor(info["hand_idxs"], device="cuda:0")
-    for k in range(warm + steps):
+    total = max(warm + steps, int(os.environ.get("KB_FRAMES", "600")))
+    maxz = torch.zeros(n, device="cuda:0")
+    avg, lo = ctypes.c_float(), ctypes.c_float()
+    used = 0
+    for k in range(total):
         gym.simulate(sim)
         gym.refresh_rigid_body_state_tensor(sim)
         gym.refresh_dof_state_tensor(sim)
@@ -40,6 +46,17 @@ def run(n, warm=150, steps=100):
                           mm[:, :7, :7], bi, hi)
         gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(pa))
         gym.set_dof_actuation_force_tensor(sim, gymtorch.unwrap_tensor(ea))
+        maxz = torch.maximum(maxz, rb[bi, 2])
+        if k == warm + steps - 1:      # the timed window: frames [warm, warm + steps)
+            used = N.lib.mg_step_time_stats(sim.native, steps, ctypes.byref(avg), ctypes.byref(lo), None)
+            phases = None
+            if hasattr(N.lib, "mg_debug_env_phase"):
+                buf = (ctypes.c_ulonglong * 12)()
+                N.lib.mg_debug_env_phase(buf)
+                waves = (n + 3) // 4
+                names = ["unconstrained", "narrowphase_rest", "crba_minv", "rows", "tgs", "integrate", "setup",
+                         "outputs", "np_screen", "np_collide", "pairs_tested", "pairs_with_hull"]
+                phases = {nm: buf[i] / waves / steps for i, nm in enumerate(names)}   # cycles per wave per frame
         if k == warm - 1 and hasattr(N.lib, "mg_debug_env_phase_reset"):
             torch.cuda.synchronize()
             N.lib.mg_debug_env_phase_reset()
@@ -50,19 +67,13 @@ def run(n, warm=150, steps=100):
         gym.refresh_dof_state_tensor(sim)
         np.savez(os.environ["KB_DUMP"], rb=rb.cpu().numpy(), dof=dof.cpu().numpy(), pa=pa.cpu().numpy(),
                  ea=ea.cpu().numpy())
-    phases = None
-    if hasattr(N.lib, "mg_debug_env_phase"):
-        buf = (ctypes.c_ulonglong * 12)()
-        N.lib.mg_debug_env_phase(buf)
-        waves = (n + 3) // 4
-        names = ["unconstrained", "narrowphase_rest", "crba_minv", "rows", "tgs", "integrate", "setup", "outputs",
-                 "np_screen", "np_collide", "pairs_tested", "pairs_with_hull"]
-        phases = {nm: buf[i] / waves / steps for i, nm in enumerate(names)}   # cycles per wave per frame
-    avg, lo = ctypes.c_float(), ctypes.c_float()
-    used = N.lib.mg_step_time_stats(sim.native, steps, ctypes.byref(avg), ctypes.byref(lo), None)
+    lifted = float((maxz > 0.55).float().mean())
+    bz = rb[bi, 2]
+    sunk = int(((bz > 0.3) & (bz < 0.4225 - 0.005) & (rb[bi, 7:10].norm(dim=1) < 0.05)).sum())
     gym.destroy_sim(sim)
     return {"lib": os.path.basename(N.LIB_PATH), "envs": n, "kernel_us_avg": 1e3 * avg.value,
-            "kernel_us_min": 1e3 * lo.value, "launches": used, "phase_cycles_per_wave": phases}
+            "kernel_us_min": 1e3 * lo.value, "launches": used, "window": [warm, warm + steps],
+            "frames": total, "cubes_lifted_frac": lifted, "cubes_sunk": sunk, "phase_cycles_per_wave": phases}
 
 
 if __name__ == "__main__":
