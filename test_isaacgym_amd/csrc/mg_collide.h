@@ -463,19 +463,24 @@ MG_HD float cvx_radius(const CShape& S) { return S.type == MG_SHAPE_BOX ? sqrtf(
 // radius + margin is skipped; the rest are clipped against Y's face planes
 // pushed out by the margin (Cyrus-Beck), and a non-empty chord [t0, t1] gives
 // one candidate at its midpoint, by Y's planes like a vertex (cvx_sd:
-// separation and face normal; onY: the point on Y's face)
-MG_HD void cvx_edges_vs(const CShape& X, const CShape& Y, float margin, bool onY, Deep4& D, V3 lo, V3 hi) {
-    const V3 t = mtmul(Y.R, vsub(X.c, Y.c));               // X's centre in Y's frame
-    const float rx = cvx_radius(X) + margin, ry = cvx_radius(Y) + margin;
+// separation and face normal; onY: the point on Y's face).
+// cvx_edges_gate: the gates shared by every edge; t = X's centre and M = X's
+// axes in Y's frame, ry = Y's bounding radius + margin. cvx_edge_one: one edge
+// (X-local endpoints la, lb) -> at most one candidate. The sequential pass
+// (cvx_edges_vs) and mg_env.hip's 16-lane pass (edges spread over the lanes)
+// run the same two functions.
+MG_HD bool cvx_edges_gate(const CShape& X, const CShape& Y, float margin, V3 lo, V3 hi, V3& t, M3& M, float& ry) {
+    t = mtmul(Y.R, vsub(X.c, Y.c));                         // X's centre in Y's frame
+    const float rx = cvx_radius(X) + margin;
+    ry = cvx_radius(Y) + margin;
     if (Y.type == MG_SHAPE_BOX) {
         const V3 dq = v3(t.x - fminf(fmaxf(t.x, -Y.h.x), Y.h.x), t.y - fminf(fmaxf(t.y, -Y.h.y), Y.h.y),
                          t.z - fminf(fmaxf(t.z, -Y.h.z), Y.h.z));
-        if (vdot(dq, dq) > rx * rx) return;
+        if (vdot(dq, dq) > rx * rx) return false;
     } else if (vdot(t, t) > (rx + ry) * (rx + ry)) {
-        return;
+        return false;
     }
-    M3 M;                                                   // X's axes in Y's frame
-    M.c0 = mtmul(Y.R, X.R.c0);
+    M.c0 = mtmul(Y.R, X.R.c0);                              // X's axes in Y's frame
     M.c1 = mtmul(Y.R, X.R.c1);
     M.c2 = mtmul(Y.R, X.R.c2);
     if (Y.type == MG_SHAPE_BOX) {
@@ -483,13 +488,87 @@ MG_HD void cvx_edges_vs(const CShape& X, const CShape& Y, float margin, bool onY
         // one face plus the margin): no crossing (a link hull just above a table)
         if (lo.x > Y.h.x + margin || hi.x < -Y.h.x - margin || lo.y > Y.h.y + margin || hi.y < -Y.h.y - margin ||
             lo.z > Y.h.z + margin || hi.z < -Y.h.z - margin)
-            return;
+            return false;
     }
-    const int ne = cvx_ne(X), nf = cvx_nf(Y);
-    if (ne <= 0) return;
+    return cvx_ne(X) > 0;
+}
+MG_HD void cvx_edge_one(const CShape& Y, float margin, bool onY, V3 t, const M3& M, float ry, V3 la, V3 lb,
+                        Deep4& D) {
+    const int nf = cvx_nf(Y);
+    const V3 al = vadd(t, mmul(M, la));
+    const V3 ab = vsub(vadd(t, mmul(M, lb)), al);
+    const float tc = fminf(fmaxf(-vdot(al, ab) / vdot(ab, ab), 0.0f), 1.0f);
+    const V3 dc = vadd(al, vscale(ab, tc));
+    if (vdot(dc, dc) > ry * ry) return;
+    float t0 = 0.0f, t1 = 1.0f;
+    for (int f = 0; f < nf; ++f) {
+        V3 nl;
+        float dl;
+        cvx_plane_l(Y, f, nl, dl);
+        const float sa = (vdot(nl, al) - dl) - margin, sb = (vdot(nl, vadd(al, ab)) - dl) - margin;
+        if (sa >= 0.0f && sb >= 0.0f) { t0 = 1.0f; t1 = 0.0f; }
+        else if (sa >= 0.0f) t0 = fmaxf(t0, sa / (sa - sb));
+        else if (sb >= 0.0f) t1 = fminf(t1, sa / (sa - sb));
+        if (!(t0 < t1)) break;
+    }
+    if (!(t0 < t1)) return;
+    const float tm = 0.5f * (t0 + t1);
+    if (Y.type == MG_SHAPE_BOX) {
+        // the chord's midpoint m near a box edge (its two other coordinates
+        // within the margin of their faces, along the axis k it is deepest
+        // inside): an edge-edge contact — normal along the cross product of
+        // the two edges, pointing out of the box, separation the distance of
+        // the two lines along it, the point the closest one on X's edge
+        const V3 m = vadd(al, vscale(ab, tm));
+        const float ex = fabsf(m.x) - Y.h.x, ey = fabsf(m.y) - Y.h.y, ez = fabsf(m.z) - Y.h.z;
+        int k = 0;
+        float ek = ex;
+        if (ey < ek) { k = 1; ek = ey; }
+        if (ez < ek) k = 2;
+        const float e1 = k == 0 ? ey : ex, e2 = k == 2 ? ey : ez;
+        if (e1 > -margin && e2 > -margin) {
+            const V3 dk = v3(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
+            const V3 p0 = v3(k == 0 ? 0.0f : (m.x < 0.0f ? -Y.h.x : Y.h.x),
+                             k == 1 ? 0.0f : (m.y < 0.0f ? -Y.h.y : Y.h.y),
+                             k == 2 ? 0.0f : (m.z < 0.0f ? -Y.h.z : Y.h.z));
+            const V3 nn = vcross(ab, dk);
+            const float l2 = vdot(nn, nn);
+            if (l2 > 1e-12f * vdot(ab, ab)) {
+                V3 n = vscale(nn, 1.0f / sqrtf(l2));
+                if (vdot(n, p0) < 0.0f) n = vscale(n, -1.0f);
+                const V3 r = vsub(al, p0);
+                const float sv = vdot(n, r);
+                if (sv < margin) {
+                    const float bq = vdot(ab, dk), aq = vdot(ab, ab);
+                    const float den = aq - bq * bq;
+                    const float ts = fminf(fmaxf((bq * vdot(dk, r) - vdot(ab, r)) / den, 0.0f), 1.0f);
+                    const V3 p = vadd(Y.c, mmul(Y.R, vadd(al, vscale(ab, ts))));
+                    const V3 nw = mmul(Y.R, n);
+                    if (onY) deep4_add(D, sv, vsub(p, vscale(nw, sv)), vscale(nw, -1.0f));
+                    else deep4_add(D, sv, p, nw);
+                }
+                return;
+            }
+        }
+    }
+    const V3 p = vadd(Y.c, mmul(Y.R, vadd(al, vscale(ab, tm))));
+    int f;
+    const float sv = cvx_sd(Y, p, f, 0.0f, margin);
+    if (sv < margin) {
+        const V3 n = cvx_normal(Y, f);
+        if (onY) deep4_add(D, sv, vsub(p, vscale(n, sv)), vscale(n, -1.0f));
+        else deep4_add(D, sv, p, n);
+    }
+}
+MG_HD void cvx_edges_vs(const CShape& X, const CShape& Y, float margin, bool onY, Deep4& D, V3 lo, V3 hi) {
+    V3 t;
+    M3 M;
+    float ry;
+    if (!cvx_edges_gate(X, Y, margin, lo, hi, t, M, ry)) return;
+    const int ne = cvx_ne(X);
     // a hull's edge ids and endpoints are streamed ahead (ids two edges, the
     // endpoints one edge): the loads of the next edge are in flight while this
-    // one is tested (at one wave per SIMD nothing else hides their latency)
+    // one is tested
     int ia1, ib1, ia2, ib2;
     cvx_edge_ids(X, 0, ia1, ib1);
     V3 la1 = cvx_vertex_l(X, ia1), lb1 = cvx_vertex_l(X, ib1);
@@ -499,70 +578,22 @@ MG_HD void cvx_edges_vs(const CShape& X, const CShape& Y, float margin, bool onY
         la1 = cvx_vertex_l(X, ia2);
         lb1 = cvx_vertex_l(X, ib2);
         cvx_edge_ids(X, e + 2 < ne ? e + 2 : ne - 1, ia2, ib2);
-        const V3 al = vadd(t, mmul(M, la));
-        const V3 ab = vsub(vadd(t, mmul(M, lb)), al);
-        const float tc = fminf(fmaxf(-vdot(al, ab) / vdot(ab, ab), 0.0f), 1.0f);
-        const V3 dc = vadd(al, vscale(ab, tc));
-        if (vdot(dc, dc) > ry * ry) continue;
-        float t0 = 0.0f, t1 = 1.0f;
-        for (int f = 0; f < nf; ++f) {
-            V3 nl;
-            float dl;
-            cvx_plane_l(Y, f, nl, dl);
-            const float sa = (vdot(nl, al) - dl) - margin, sb = (vdot(nl, vadd(al, ab)) - dl) - margin;
-            if (sa >= 0.0f && sb >= 0.0f) { t0 = 1.0f; t1 = 0.0f; }
-            else if (sa >= 0.0f) t0 = fmaxf(t0, sa / (sa - sb));
-            else if (sb >= 0.0f) t1 = fminf(t1, sa / (sa - sb));
-            if (!(t0 < t1)) break;
-        }
-        if (!(t0 < t1)) continue;
-        const float tm = 0.5f * (t0 + t1);
-        if (Y.type == MG_SHAPE_BOX) {
-            // the chord's midpoint m near a box edge (its two other coordinates
-            // within the margin of their faces, along the axis k it is deepest
-            // inside): an edge-edge contact — normal along the cross product of
-            // the two edges, pointing out of the box, separation the distance of
-            // the two lines along it, the point the closest one on X's edge
-            const V3 m = vadd(al, vscale(ab, tm));
-            const float ex = fabsf(m.x) - Y.h.x, ey = fabsf(m.y) - Y.h.y, ez = fabsf(m.z) - Y.h.z;
-            int k = 0;
-            float ek = ex;
-            if (ey < ek) { k = 1; ek = ey; }
-            if (ez < ek) k = 2;
-            const float e1 = k == 0 ? ey : ex, e2 = k == 2 ? ey : ez;
-            if (e1 > -margin && e2 > -margin) {
-                const V3 dk = v3(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
-                const V3 p0 = v3(k == 0 ? 0.0f : (m.x < 0.0f ? -Y.h.x : Y.h.x),
-                                 k == 1 ? 0.0f : (m.y < 0.0f ? -Y.h.y : Y.h.y),
-                                 k == 2 ? 0.0f : (m.z < 0.0f ? -Y.h.z : Y.h.z));
-                const V3 nn = vcross(ab, dk);
-                const float l2 = vdot(nn, nn);
-                if (l2 > 1e-12f * vdot(ab, ab)) {
-                    V3 n = vscale(nn, 1.0f / sqrtf(l2));
-                    if (vdot(n, p0) < 0.0f) n = vscale(n, -1.0f);
-                    const V3 r = vsub(al, p0);
-                    const float sv = vdot(n, r);
-                    if (sv < margin) {
-                        const float bq = vdot(ab, dk), aq = vdot(ab, ab);
-                        const float den = aq - bq * bq;
-                        const float ts = fminf(fmaxf((bq * vdot(dk, r) - vdot(ab, r)) / den, 0.0f), 1.0f);
-                        const V3 p = vadd(Y.c, mmul(Y.R, vadd(al, vscale(ab, ts))));
-                        const V3 nw = mmul(Y.R, n);
-                        if (onY) deep4_add(D, sv, vsub(p, vscale(nw, sv)), vscale(nw, -1.0f));
-                        else deep4_add(D, sv, p, nw);
-                    }
-                    continue;
-                }
-            }
-        }
-        const V3 p = vadd(Y.c, mmul(Y.R, vadd(al, vscale(ab, tm))));
-        int f;
-        const float sv = cvx_sd(Y, p, f, 0.0f, margin);
-        if (sv < margin) {
-            const V3 n = cvx_normal(Y, f);
-            if (onY) deep4_add(D, sv, vsub(p, vscale(n, sv)), vscale(n, -1.0f));
-            else deep4_add(D, sv, p, n);
-        }
+        cvx_edge_one(Y, margin, onY, t, M, ry, la, lb, D);
+    }
+}
+
+// vertex i of X against Y's planes: the candidate cvx_vertices_vs makes of it
+// (and v, X's vertex in the world)
+MG_HD void cvx_vertex_one(const CShape& X, const CShape& Y, float margin, bool onY, int i, Deep4& D, V3& lo,
+                          V3& hi) {
+    const V3 v = cvx_vertex(X, i);
+    aabb_add(lo, hi, mtmul(Y.R, vsub(v, Y.c)));
+    int f;
+    const float sv = cvx_sd(Y, v, f, 0.0f, margin);
+    if (sv < margin) {
+        const V3 n = cvx_normal(Y, f);
+        if (onY) deep4_add(D, sv, vsub(v, vscale(n, sv)), vscale(n, -1.0f));
+        else deep4_add(D, sv, v, n);
     }
 }
 

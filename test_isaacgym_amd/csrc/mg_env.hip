@@ -31,22 +31,25 @@
 
 #ifdef MG_ENV_PHASE_TIMING
 // profiling build only: per-phase shader-clock cycles summed over waves
-__device__ unsigned long long g_env_phase[12];
+__device__ unsigned long long g_env_phase[16];
 #define PH_T0() unsigned long long ph_t = clock64()
 #define PH_MARK(k) do { const unsigned long long t_ = clock64(); \
     if (threadIdx.x == 0) atomicAdd(&g_env_phase[k], t_ - ph_t); ph_t = t_; } while (0)
 #define PH_COUNT(k, v) atomicAdd(&g_env_phase[k], (unsigned long long)(v))
+#define PH_SUB(k) do { const unsigned long long t_ = clock64(); \
+    if (threadIdx.x == 0) atomicAdd(&g_env_phase[k], t_ - ph_sub); ph_sub = t_; } while (0)
 extern "C" int mg_debug_env_phase(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_env_phase), sizeof(g_env_phase)) == hipSuccess ? 0 : -1;
 }
 extern "C" int mg_debug_env_phase_reset(void) {
-    unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_env_phase), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #else
 #define PH_T0() do { } while (0)
 #define PH_MARK(k) do { } while (0)
 #define PH_COUNT(k, v) do { } while (0)
+#define PH_SUB(k) do { } while (0)
 #endif
 
 namespace {
@@ -121,6 +124,204 @@ __device__ __forceinline__ float bcast16(float v, int k) {
     case 12: return dpp<0x15C>(v); case 13: return dpp<0x15D>(v);
     case 14: return dpp<0x15E>(v); default: return dpp<0x15F>(v);
     }
+}
+
+// ---- cooperative convex-convex narrow phase ---------------------------------
+// A pair of convex shapes (box or hull, at least one hull) on all 16 lanes of
+// an env group: the same result, in every lane, as convex_convex (mg_collide.h)
+// on one lane. Vertex i of A is tested on lane i % 16 (candidate order i),
+// vertex i of B likewise (order 64 + i), edges the same way (order e). Every
+// per-vertex / per-edge result is computed by the sequential code's own
+// functions (cvx_vertex_one, cvx_edge_one); each lane keeps its candidates in
+// order, and the group merges the 4 smallest (separation, order) keys — the
+// set and the order deep4_add's in-order insertion keeps (ties go to the
+// earlier candidate). So no oracle change: oracle/migym_oracle_env.c's
+// sequential convex_convex_ is the definition.
+struct CandQ {
+    int n;
+    float s[MG_PAIR_MAXC];
+    int id[MG_PAIR_MAXC];
+    V3 p[MG_PAIR_MAXC], nrm[MG_PAIR_MAXC];
+};
+__device__ __forceinline__ void candq_add(CandQ& Q, float s, int id, V3 p, V3 n) {
+    // ids arrive in increasing order per lane: deep4_add's rule
+    if (Q.n == MG_PAIR_MAXC && !(s < Q.s[MG_PAIR_MAXC - 1])) return;
+    int at = 0;
+#pragma unroll
+    for (int k = 0; k < MG_PAIR_MAXC; ++k)
+        if (k < Q.n && Q.s[k] <= s) at = k + 1;
+#pragma unroll
+    for (int k = MG_PAIR_MAXC - 1; k > 0; --k)
+        if (k > at) { Q.s[k] = Q.s[k - 1]; Q.id[k] = Q.id[k - 1]; Q.p[k] = Q.p[k - 1]; Q.nrm[k] = Q.nrm[k - 1]; }
+#pragma unroll
+    for (int k = 0; k < MG_PAIR_MAXC; ++k)
+        if (k == at) { Q.s[k] = s; Q.id[k] = id; Q.p[k] = p; Q.nrm[k] = n; }
+    if (Q.n < MG_PAIR_MAXC) Q.n = Q.n + 1;
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ __forceinline__ void minkey_step(float& s, int& id) {
+    const float s2 = dpp<CTRL>(s);
+    const int i2 = dppi<CTRL>(id);
+    if (s2 < s || (s2 == s && i2 < id)) { s = s2; id = i2; }
+}
+// the smallest (s, id) of the 16-lane row, in every lane of the row
+__device__ __forceinline__ void grp_minkey(float& s, int& id) {
+    minkey_step<0x128>(s, id);   // row_ror:8
+    minkey_step<0x124>(s, id);   // row_ror:4
+    minkey_step<0x4E>(s, id);    // quad_perm [2,3,0,1]
+    minkey_step<0xB1>(s, id);    // quad_perm [1,0,3,2]
+}
+template <int CTRL>
+__device__ __forceinline__ void bounds_step(V3& lo, V3& hi) {
+    lo = v3(fminf(lo.x, dpp<CTRL>(lo.x)), fminf(lo.y, dpp<CTRL>(lo.y)), fminf(lo.z, dpp<CTRL>(lo.z)));
+    hi = v3(fmaxf(hi.x, dpp<CTRL>(hi.x)), fmaxf(hi.y, dpp<CTRL>(hi.y)), fmaxf(hi.z, dpp<CTRL>(hi.z)));
+}
+// vertex bounds over the row (min / max are exact: order-free)
+__device__ __forceinline__ void grp_bounds(V3& lo, V3& hi) {
+    bounds_step<0x128>(lo, hi);
+    bounds_step<0x124>(lo, hi);
+    bounds_step<0x4E>(lo, hi);
+    bounds_step<0xB1>(lo, hi);
+}
+__device__ __forceinline__ unsigned grp_ballot(bool b, int gi) {
+    return (unsigned)((__ballot(b) >> (gi * G)) & 0xFFFFull);
+}
+// X's edges against Y on the group, into each lane's queue (order = edge index).
+// A lane's edges (e = ln + 16 k, at most 3 MG_HULL_MAX_VERTS / 16 = 6) in two
+// batches of 3: all the batch's edge ids, then all its endpoints are loaded
+// before any is tested (two dependent round trips per batch, not two per edge)
+constexpr int CE_PER_LANE = (3 * MG_HULL_MAX_VERTS + G - 1) / G;
+__device__ __forceinline__ void coop_edges(const CShape& X, const CShape& Y, float margin, bool onY, V3 lo, V3 hi,
+                                           int ln, CandQ& Q) {
+    V3 t;
+    M3 M;
+    float ry;
+    if (!cvx_edges_gate(X, Y, margin, lo, hi, t, M, ry)) return;
+    const int ne = cvx_ne(X);
+#pragma unroll
+    for (int k0 = 0; k0 < CE_PER_LANE; k0 += 3) {
+        if (ln + G * k0 >= ne) break;
+        int ia[3], ib[3];
+        V3 la[3], lb[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int e = ln + G * (k0 + k);
+            cvx_edge_ids(X, e < ne ? e : ne - 1, ia[k], ib[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            la[k] = cvx_vertex_l(X, ia[k]);
+            lb[k] = cvx_vertex_l(X, ib[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int e = ln + G * (k0 + k);
+            if (e < ne) {
+                Deep4 T;
+                T.n = 0;
+                cvx_edge_one(Y, margin, onY, t, M, ry, la[k], lb[k], T);
+                if (T.n) candq_add(Q, T.s[0], e, T.p[0], T.nrm[0]);
+            }
+        }
+    }
+}
+// X's vertices (i = ln + 16 k, at most 2 per lane) against Y's planes, into the
+// lane's queue (order idbase + i); both vertices loaded before either is tested
+__device__ __forceinline__ void coop_vertices(const CShape& X, const CShape& Y, float margin, bool onY, int idbase,
+                                              int ln, CandQ& Q, V3& lo, V3& hi) {
+    const int nv = cvx_nv(X);
+    V3 vw[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int i = ln + G * k;
+        vw[k] = cvx_vertex(X, i < nv ? i : nv - 1);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int i = ln + G * k;
+        if (i < nv) {
+            const V3 v = vw[k];
+            aabb_add(lo, hi, mtmul(Y.R, vsub(v, Y.c)));
+            int f;
+            const float sv = cvx_sd(Y, v, f, 0.0f, margin);     // cvx_vertex_one's candidate
+            if (sv < margin) {
+                const V3 n = cvx_normal(Y, f);
+                if (onY) candq_add(Q, sv, idbase + i, vsub(v, vscale(n, sv)), vscale(n, -1.0f));
+                else candq_add(Q, sv, idbase + i, v, n);
+            }
+        }
+    }
+}
+// every lane of the group calls it with the same pair (group-uniform control)
+__device__ void coop_convex_convex(const CShape& A, const CShape& B, float margin, int ln, int gi, PairOut& o) {
+#ifdef MG_ENV_PHASE_TIMING
+    unsigned long long ph_sub = clock64();
+#endif
+    CandQ Q;
+    Q.n = 0;
+    V3 loA = v3(1e30f, 1e30f, 1e30f), hiA = v3(-1e30f, -1e30f, -1e30f), loB = loA, hiB = hiA;
+    coop_vertices(A, B, margin, false, 0, ln, Q, loA, hiA);     // A's vertices by B's planes
+    coop_vertices(B, A, margin, true, 64, ln, Q, loB, hiB);     // B's vertices by A's planes
+    PH_SUB(12);
+    if (grp_ballot(Q.n > 0, gi) == 0u) {
+        // no vertex candidate: edge crossings (convex_convex's order of passes)
+        grp_bounds(loA, hiA);
+        grp_bounds(loB, hiB);
+        if (A.type == MG_SHAPE_BOX && B.type != MG_SHAPE_BOX) {
+            coop_edges(B, A, margin, true, loB, hiB, ln, Q);
+        } else {
+            coop_edges(A, B, margin, false, loA, hiA, ln, Q);
+            if (B.type != MG_SHAPE_BOX && grp_ballot(Q.n > 0, gi) == 0u) coop_edges(B, A, margin, true, loB, hiB, ln, Q);
+        }
+        PH_COUNT(15, 1);
+    }
+    PH_SUB(13);
+    // merge: the group's smallest (s, order) keys, ascending
+    o.n = 0;
+#pragma unroll
+    for (int r = 0; r < MG_PAIR_MAXC; ++r) {
+        if (grp_ballot(Q.n > 0, gi) == 0u) break;     // group-uniform: nothing left
+        float s = Q.n > 0 ? Q.s[0] : 3.0e38f;
+        int id = Q.n > 0 ? Q.id[0] : 0x7fffffff;
+        grp_minkey(s, id);
+        const unsigned m = grp_ballot(Q.n > 0 && Q.id[0] == id, gi);
+        const int owner = m ? __ffs(m) - 1 : 0;
+        const V3 p = v3(__shfl(Q.p[0].x, owner, G), __shfl(Q.p[0].y, owner, G), __shfl(Q.p[0].z, owner, G));
+        const V3 n = v3(__shfl(Q.nrm[0].x, owner, G), __shfl(Q.nrm[0].y, owner, G), __shfl(Q.nrm[0].z, owner, G));
+        if (m != 0u && ln == owner) {           // pop the head
+#pragma unroll
+            for (int k = 0; k + 1 < MG_PAIR_MAXC; ++k) {
+                Q.s[k] = Q.s[k + 1]; Q.id[k] = Q.id[k + 1]; Q.p[k] = Q.p[k + 1]; Q.nrm[k] = Q.nrm[k + 1];
+            }
+            Q.n = Q.n - 1;
+        }
+        if (m != 0u) pair_push(o, p, n, s);
+    }
+    PH_SUB(14);
+}
+// lane k's placed shape, to every lane of the group (ds_bpermute: no global
+// round trips for the pair record, the shape rows and the poses)
+__device__ __forceinline__ V3 shfl3(V3 v, int k) { return v3(__shfl(v.x, k, G), __shfl(v.y, k, G), __shfl(v.z, k, G)); }
+__device__ __forceinline__ CShape shfl_shape(const CShape& c, int k) {
+    CShape r;
+    r.type = __shfl(c.type, k, G);
+    r.c = shfl3(c.c, k);
+    r.R.c0 = shfl3(c.R.c0, k);
+    r.R.c1 = shfl3(c.R.c1, k);
+    r.R.c2 = shfl3(c.R.c2, k);
+    r.h = shfl3(c.h, k);
+    const unsigned long long hp = (unsigned long long)(uintptr_t)c.hv;
+    const unsigned lo = __shfl((unsigned)(hp & 0xFFFFFFFFull), k, G), hi = __shfl((unsigned)(hp >> 32), k, G);
+    r.hv = (const float*)(uintptr_t)(((unsigned long long)hi << 32) | lo);
+    return r;
+}
+// the pairs convex_convex handles (collide's dispatch): box / hull against box /
+// hull, at least one hull (box-box is SAT)
+__device__ __forceinline__ bool cvx_pair(int ta, int tb) {
+    const bool pa = ta == MG_SHAPE_BOX || ta == MG_SHAPE_CONVEX, pb = tb == MG_SHAPE_BOX || tb == MG_SHAPE_CONVEX;
+    return pa && pb && (ta == MG_SHAPE_CONVEX || tb == MG_SHAPE_CONVEX);
 }
 
 // substep-invariant per-lane constants: lane d < D holds DOF d's drive
@@ -868,6 +1069,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 o.n = 0;
                 float mu = 0.0f, rest = 0.0f;
                 int pa = 0, pb = -1;
+                bool coop = false;
+                CShape cA = {}, cB = {};
                 if (rb + ln < nnear) {
                     PH_COUNT(10, 1);
                     const int* pp = A.pairs + (size_t)(pair0 + S.npl[rb + ln]) * 4;
@@ -876,23 +1079,38 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     pb = pp[2];
                     const int sb = pp[3];
                     const float* sha = A.shapes + sa * MG_SHAPE_STRIDE;
-                    V3 xa;
-                    Q4 qa;
-                    pair_pose(S, pa, xa, qa);
-                    const CShape ca = place_shape(sha, xa, qa, A.hulls);
                     if (pb < 0) {
-                        ground_pair(P, ca, o);
+                        V3 xa;
+                        Q4 qa;
+                        pair_pose(S, pa, xa, qa);
+                        ground_pair(P, place_shape(sha, xa, qa, A.hulls), o);
                         mu = 0.5f * (sha[11] + P.mu_ground);
                         rest = 0.5f * (sha[12] + P.e_ground);
                     } else {
                         const float* shb = A.shapes + sb * MG_SHAPE_STRIDE;
-                        V3 xb;
-                        Q4 qb;
+                        coop = cvx_pair((int)sha[0], (int)shb[0]);
+                        V3 xa, xb;
+                        Q4 qa, qb;
+                        pair_pose(S, pa, xa, qa);
                         pair_pose(S, pb, xb, qb);
-                        collide(ca, place_shape(shb, xb, qb, A.hulls), P.contact_offset, o);
+                        cA = place_shape(sha, xa, qa, A.hulls);
+                        cB = place_shape(shb, xb, qb, A.hulls);
+                        if (!coop) collide(cA, cB, P.contact_offset, o);
                         PH_COUNT(11, ((int)sha[0] == MG_SHAPE_CONVEX || (int)shb[0] == MG_SHAPE_CONVEX) ? 1 : 0);
                         mu = 0.5f * (sha[11] + shb[11]);
                         rest = 0.5f * (sha[12] + shb[12]);
+                    }
+                }
+                // this round's convex pairs, one at a time on the whole group (in
+                // lane order; the result goes to the pair's own lane)
+                unsigned cm = grp_ballot(coop, gi);
+                while (__any(cm != 0u)) {
+                    if (cm != 0u) {                       // group-uniform
+                        const int k = __ffs(cm) - 1;
+                        cm &= cm - 1u;
+                        PairOut t;
+                        coop_convex_convex(shfl_shape(cA, k), shfl_shape(cB, k), P.contact_offset, ln, gi, t);
+                        if (ln == k) o = t;
                     }
                 }
                 // exclusive prefix sum of the counts over the 16 lanes

@@ -51,11 +51,12 @@ def run(n, warm=150, steps=100):
             used = N.lib.mg_step_time_stats(sim.native, steps, ctypes.byref(avg), ctypes.byref(lo), None)
             phases = None
             if hasattr(N.lib, "mg_debug_env_phase"):
-                buf = (ctypes.c_ulonglong * 12)()
+                buf = (ctypes.c_ulonglong * 16)()
                 N.lib.mg_debug_env_phase(buf)
                 waves = (n + 3) // 4
                 names = ["unconstrained", "narrowphase_rest", "crba_minv", "rows", "tgs", "integrate", "setup",
-                         "outputs", "np_screen", "np_collide", "pairs_tested", "pairs_with_hull"]
+                         "outputs", "np_screen", "np_collide", "pairs_tested", "pairs_with_hull",
+                         "coop_vertices", "coop_edges", "coop_merge", "coop_edge_passes"]
                 phases = {nm: buf[i] / waves / steps for i, nm in enumerate(names)}   # cycles per wave per frame
         if k == warm - 1 and hasattr(N.lib, "mg_debug_env_phase_reset"):
             torch.cuda.synchronize()
