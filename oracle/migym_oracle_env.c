@@ -609,6 +609,8 @@ typedef struct { int a, sa, b, sb; } epair_t;
 static int env_pairs_(const mg_model* m, const oenv_t* ev, int ground, int L, int fb, epair_t* out, int cap) {
     static const int pb[4][4] = {{-1, 0, 1, 2}, {-1, -1, 3, 4}, {-1, -1, -1, 5}, {-1, -1, -1, -1}};
     int n = 0, k, j, t, l, sa, sb;
+    const int* LIp = ev->art_tmpl >= 0
+        ? m->tmpl_link_i + (size_t)m->artic_tmpl_i[(size_t)ev->art_tmpl * MG_ATMPL_I_N + 0] * MG_LINK_I_N : NULL;
 #define OE_PUSH(A_, SA_, B_, SB_) do { if (n < cap) { out[n].a = (A_); out[n].sa = (SA_); out[n].b = (B_); out[n].sb = (SB_); } n++; } while (0)
 #define OE_SHP(B_, S0_, NS_) do { const int* t_ = m->tmpl_body_i + (size_t)m->body_tmpl[B_] * MG_TBODY_I_N; S0_ = t_[0]; NS_ = t_[1]; } while (0)
     for (k = 0; k < ev->nf; ++k) {
@@ -637,7 +639,9 @@ static int env_pairs_(const mg_model* m, const oenv_t* ev, int ground, int L, in
     }
     for (l = fb ? 0 : 1; l < L; ++l) {     /* moving links (a floating base moves) */
         int sa0, nsa;
-        OE_SHP(ev->art_body + l, sa0, nsa);
+        const int bl = LIp[l * MG_LINK_I_N + 3];   /* the link's body; virtual links: none */
+        if (bl < 0) continue;
+        OE_SHP(ev->art_body + bl, sa0, nsa);
         for (sa = sa0; sa < sa0 + nsa; ++sa) {
             if (ground) OE_PUSH(l, sa, -1, -1);
             for (t = 0; t < ev->ns; ++t) {
@@ -1328,8 +1332,9 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     for (d = 0; d < D; ++d) { dof[(d0 + d) * 2 + 0] = q[d]; dof[(d0 + d) * 2 + 1] = u[d]; }
     for (l = 0; l < L; ++l) {
         const int p = LI[l * MG_LINK_I_N + 0], jt = LI[l * MG_LINK_I_N + 1], dj = LI[l * MG_LINK_I_N + 2];
-        const float* M = m->body_mass + (size_t)(b0 + l) * MG_MASS_N;
-        float* so = state + (size_t)(b0 + l) * MG_STATE_N;
+        const int bl = LI[l * MG_LINK_I_N + 3];      /* -1: virtual link (no body) */
+        const float* M = link_mass_(m, LI, b0, l);
+        float* so = bl >= 0 ? state + (size_t)(b0 + bl) * MG_STATE_N : NULL;
         v3_t ww, vw, com = V(M[8], M[9], M[10]);
         if (p < 0) {
             const q4_t qc = Q(-q0.x, -q0.y, -q0.z, q0.w);
@@ -1344,15 +1349,16 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             xl[l] = add3(xl[p], qrot_(ql[p], rr));
             vl[l] = svadd_(xmot_(mt_(qmat_(qrel)), rr, vl[p]), svmul_(sj, qdj));
         }
+        if (!so) continue;
         ww = qrot_(ql[l], vl[l].w);
         vw = qrot_(ql[l], add3(vl[l].v, cross3(vl[l].w, com)));
         so[0] = xl[l].x; so[1] = xl[l].y; so[2] = xl[l].z;
         so[3] = ql[l].x; so[4] = ql[l].y; so[5] = ql[l].z; so[6] = ql[l].w;
         so[7] = vw.x; so[8] = vw.y; so[9] = vw.z;
         so[10] = ww.x; so[11] = ww.y; so[12] = ww.z;
-        cforce[(size_t)(b0 + l) * 3 + 0] = lsum[l].x * P->inv_dt;
-        cforce[(size_t)(b0 + l) * 3 + 1] = lsum[l].y * P->inv_dt;
-        cforce[(size_t)(b0 + l) * 3 + 2] = lsum[l].z * P->inv_dt;
+        cforce[(size_t)(b0 + bl) * 3 + 0] = lsum[l].x * P->inv_dt;
+        cforce[(size_t)(b0 + bl) * 3 + 1] = lsum[l].y * P->inv_dt;
+        cforce[(size_t)(b0 + bl) * 3 + 2] = lsum[l].z * P->inv_dt;
     }
     return 0;
 }
@@ -1423,12 +1429,6 @@ static int classify_envs_(const mg_model* m, oenv_t* envs, char* owned) {
                 if (ai[0] == r0) { ev->art_body = r0; ev->art_dof = ai[1]; ev->art_tmpl = ai[2]; }
             }
             if (ev->art_body < 0) { n = -1; break; }
-            {   /* ball joints (virtual links) step in the articulation kernel only */
-                const int* ti = m->artic_tmpl_i + (size_t)ev->art_tmpl * MG_ATMPL_I_N;
-                for (i = 0; i < ti[1]; ++i)
-                    if (m->tmpl_link_i[(size_t)(ti[0] + i) * MG_LINK_I_N + 3] != i) n = -1;
-                if (n < 0) break;
-            }
             owned[r0] = 1;
         }
         ev->nf = nf;

@@ -263,18 +263,33 @@ class Joint:
         self.damping = 0.0
         self.friction = 0.0
         self.armature = None      # per-joint armature (MJCF), else AssetOptions.armature
+        # hinges applied before this one on the same body (an MJCF body with
+        # several joints, assets/mjcf/nv_humanoid.xml:53-54): each its own DOF,
+        # about its axis in the body frame as rotated by the hinges before it;
+        # they share this joint's origin (p, q)
+        self.pre = []
 
     @property
     def has_dof(self):
         return self.ndof > 0
 
     @property
-    def ndof(self):
-        """DOFs of the joint: 1 revolute / prismatic, 3 spherical (rotations about the
-        joint frame's x, y, z axes), 0 otherwise."""
+    def own_ndof(self):
+        """DOFs of the joint itself: 1 revolute / prismatic, 3 spherical (rotations
+        about the joint frame's x, y, z axes), 0 otherwise."""
         if self.type in (T.JOINT_REVOLUTE, T.JOINT_PRISMATIC):
             return 1
         return 3 if self.type == T.JOINT_BALL else 0
+
+    @property
+    def ndof(self):
+        """DOFs between the body and its parent: the pre-hinges' and its own."""
+        return len(self.pre) + self.own_ndof
+
+    @property
+    def chain(self):
+        """The joints a body hangs by, in application (and DOF) order."""
+        return self.pre + [self]
 
 
 class MassProps:
@@ -311,20 +326,26 @@ class Asset:
 
     # ---- derived structure
     @property
+    def api_joints(self):
+        """Joints as the joint API lists them (get_asset_joint_*): every joint of
+        every body, a multi-joint MJCF body's hinges one by one."""
+        return [c for j in self.joints for c in j.chain]
+
+    @property
     def dof_joints(self):
         """The joint of every DOF, in DOF order (a spherical joint three times)."""
-        return [j for j in self.joints for _ in range(j.ndof)]
+        return [c for j in self.joints for c in j.chain for _ in range(c.own_ndof)]
 
     @property
     def dof_names(self):
         """DOF names: the joint's name; a spherical joint's three DOFs get
         `<joint>_0/_1/_2` (x, y, z of its frame; naming unpinned by the reference)."""
         out = []
-        for j in self.joints:
-            if j.ndof == 1:
-                out.append(j.name)
+        for c in self.api_joints:
+            if c.own_ndof == 1:
+                out.append(c.name)
             else:
-                out.extend("%s_%d" % (j.name, k) for k in range(j.ndof))
+                out.extend("%s_%d" % (c.name, k) for k in range(c.own_ndof))
         return out
 
     @property
@@ -931,8 +952,9 @@ class _Attr:
 
 def load_mjcf(asset_root, filename, options):
     """MuJoCo MJCF import (assets/mjcf/nv_ant.xml, examples/apply_forces.py:67):
-    the body tree under <worldbody>, hinge / slide joints (one per body; angles in
-    degrees unless <compiler angle="radian">), a <freejoint> / free joint on the
+    the body tree under <worldbody>, hinge / slide / ball joints (several hinges
+    per body as a chain, nv_humanoid.xml:53-54; angles in degrees unless
+    <compiler angle="radian">), a <freejoint> / free joint on the
     root (a floating base unless AssetOptions.fix_base_link), sphere / capsule /
     box geoms (fromto capsules; cylinders as capsules), mass properties from the
     geoms at their density (default 1000) unless the body has an <inertial>,
@@ -987,36 +1009,51 @@ def load_mjcf(asset_root, filename, options):
             raise ValueError("MJCF %s: joints on the root body other than a free joint" % path)
         if parent_idx is not None and free:
             raise ValueError("MJCF %s: free joint below the root" % path)
-        if len(hinge) > 1:
-            raise ValueError("MJCF %s: body %s has %d joints (one per body supported)" % (path, body.name, len(hinge)))
         shift = np.zeros(3)
         if parent_idx is not None:
-            jt = T.JOINT_FIXED
-            j = Joint(hinge[0].get("name") if hinge else body.name + "_fixed", jt, parent_idx, idx)
-            j.p, j.q = bp, bq
-            if hinge:
-                ja = defaults.attrs(hinge[0], hinge[0].get("class", cls))
-                typ = ja.get("type", "hinge")
-                if typ not in ("hinge", "slide", "ball"):
-                    raise ValueError("MJCF %s: joint type %s unsupported" % (path, typ))
-                j.type = {"hinge": T.JOINT_REVOLUTE, "slide": T.JOINT_PRISMATIC, "ball": T.JOINT_BALL}[typ]
-                ax = np.array(_mj_floats(ja.get("axis"), (0, 0, 1)), dtype=np.float64)
-                j.axis = ax / np.linalg.norm(ax)
-                anchor = np.array(_mj_floats(ja.get("pos"), (0, 0, 0)), dtype=np.float64)
-                if np.any(anchor != 0.0):
-                    shift = anchor
-                    j.p = bp + _qmat(bq) @ anchor
-                rng = _mj_floats(ja.get("range"))
-                limited = ja.get("limited", "auto")
-                if rng is not None and limited in ("true", "auto") and typ != "ball":   # a cone limit: not modelled
-                    s = k_ang if typ == "hinge" else 1.0
-                    j.has_limits, j.lower, j.upper = True, rng[0] * s, rng[1] * s
-                j.damping = float(ja.get("damping", 0.0))
-                j.friction = float(ja.get("frictionloss", 0.0))
-                j.velocity = MJCF_MAX_JOINT_VELOCITY
-                if ja.get("armature") is not None:
-                    j.armature = float(ja.get("armature"))
-                joint_of_name[j.name] = j
+            # one joint per hinge / slide / ball element, in declaration order; a
+            # body with several (nv_humanoid.xml:53-54, three hips at :61-63) hangs
+            # by all of them: the last is the body's joint, the ones before it its
+            # pre-hinges (each about its axis in the body frame as turned by the
+            # ones before, MuJoCo's order), sharing one anchor
+            chain = []
+            anchors = []
+            for hj in (hinge or [None]):
+                j = Joint(hj.get("name") if hj is not None else body.name + "_fixed", T.JOINT_FIXED, parent_idx, idx)
+                j.p, j.q = bp, bq
+                anchor = np.zeros(3)
+                if hj is not None:
+                    ja = defaults.attrs(hj, hj.get("class", cls))
+                    typ = ja.get("type", "hinge")
+                    if typ not in ("hinge", "slide", "ball"):
+                        raise ValueError("MJCF %s: joint type %s unsupported" % (path, typ))
+                    if len(hinge) > 1 and typ != "hinge":
+                        raise ValueError("MJCF %s: body %s: several joints, not all hinges (%s)" % (path, body.name, typ))
+                    j.type = {"hinge": T.JOINT_REVOLUTE, "slide": T.JOINT_PRISMATIC, "ball": T.JOINT_BALL}[typ]
+                    ax = np.array(_mj_floats(ja.get("axis"), (0, 0, 1)), dtype=np.float64)
+                    j.axis = ax / np.linalg.norm(ax)
+                    anchor = np.array(_mj_floats(ja.get("pos"), (0, 0, 0)), dtype=np.float64)
+                    rng = _mj_floats(ja.get("range"))
+                    limited = ja.get("limited", "auto")
+                    if rng is not None and limited in ("true", "auto") and typ != "ball":   # a cone limit: not modelled
+                        sc = k_ang if typ == "hinge" else 1.0
+                        j.has_limits, j.lower, j.upper = True, rng[0] * sc, rng[1] * sc
+                    j.damping = float(ja.get("damping", 0.0))
+                    j.friction = float(ja.get("frictionloss", 0.0))
+                    j.velocity = MJCF_MAX_JOINT_VELOCITY
+                    if ja.get("armature") is not None:
+                        j.armature = float(ja.get("armature"))
+                    joint_of_name[j.name] = j
+                chain.append(j)
+                anchors.append(anchor)
+            if any(np.any(a != anchors[0]) for a in anchors[1:]):
+                raise ValueError("MJCF %s: body %s: its joints have different anchors (pos)" % (path, body.name))
+            if np.any(anchors[0] != 0.0):
+                shift = anchors[0]
+                for j in chain:
+                    j.p = bp + _qmat(bq) @ shift
+            j = chain[-1]
+            j.pre = chain[:-1]
             asset.joints.append(j)
         shapes = geom_shapes(bel, cls, shift)
         body.shapes = shapes
@@ -1057,11 +1094,12 @@ def load_mjcf(asset_root, filename, options):
         for mo in act:
             if mo.tag not in ("motor", "general"):
                 continue
-            j = joint_of_name.get(mo.get("joint"))
-            cr = _mj_floats(mo.get("ctrlrange"))
-            if j is None or cr is None or mo.get("ctrllimited", "true") == "false":
+            ma = defaults.attrs(mo, mo.get("class", "main"))     # <default><motor ctrlrange=...> applies
+            j = joint_of_name.get(ma.get("joint"))
+            cr = _mj_floats(ma.get("ctrlrange"))
+            if j is None or cr is None or ma.get("ctrllimited", "true") == "false":
                 continue
-            gear = _mj_floats(mo.get("gear"), (1.0,))[0]
+            gear = _mj_floats(ma.get("gear"), (1.0,))[0]
             j.effort = abs(gear) * max(abs(cr[0]), abs(cr[1]))
     asset.warnings = warnings
     asset.path = path

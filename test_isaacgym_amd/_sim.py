@@ -241,9 +241,15 @@ class Sim:
             qj = float(a.dof_state[d, 0]) if d >= 0 else 0.0
             qrel = j.q.copy()
             rr = j.p.copy()
+            for k, pj in enumerate(j.pre):      # pre-hinges of a multi-joint body, in order
+                th = float(a.dof_state[d + k, 0])
+                s, c = np.sin(0.5 * th), np.cos(0.5 * th)
+                qrel = _qmul(qrel, np.array([pj.axis[0] * s, pj.axis[1] * s, pj.axis[2] * s, c]))
+            d = d + len(j.pre) if d >= 0 else d
+            qj = float(a.dof_state[d, 0]) if d >= 0 and j.own_ndof else 0.0
             if j.type == T.JOINT_REVOLUTE:
                 s, c = np.sin(0.5 * qj), np.cos(0.5 * qj)
-                qrel = _qmul(j.q, np.array([j.axis[0] * s, j.axis[1] * s, j.axis[2] * s, c]))
+                qrel = _qmul(qrel, np.array([j.axis[0] * s, j.axis[1] * s, j.axis[2] * s, c]))
             elif j.type == T.JOINT_BALL:
                 # rotations about the joint frame's x, y, z in turn (the three
                 # packed links of build_model)
@@ -366,6 +372,20 @@ class Sim:
                         j = asset.joints[b - 1]
                         d = asset.dof_of_body(b)
                         parent = link_of[j.parent]
+                        for k, pj in enumerate(j.pre):
+                            # pre-hinges of a multi-joint body: virtual revolute
+                            # links (body -1), the first at the joint origin
+                            f = np.zeros(N.MG_LINK_F_N, dtype=np.float32)
+                            f[3:7] = (0, 0, 0, 1)
+                            if k == 0:
+                                f[0:3] = j.p
+                                f[3:7] = j.q
+                            f[7:10] = pj.axis
+                            lf.append(f)
+                            li.append([parent, T.JOINT_REVOLUTE, d + k, -1])
+                            parent = len(lf) - 1 - nl0
+                        if j.pre:
+                            d = d + len(j.pre)
                         if j.type == T.JOINT_BALL:
                             # three revolute links about the joint frame's x, y, z:
                             # two virtual (body -1), then the child body
@@ -381,8 +401,10 @@ class Sim:
                                 parent = len(lf) - 1 - nl0
                         else:
                             f = np.zeros(N.MG_LINK_F_N, dtype=np.float32)
-                            f[0:3] = j.p
-                            f[3:7] = j.q
+                            f[3:7] = (0, 0, 0, 1)
+                            if not j.pre:
+                                f[0:3] = j.p
+                                f[3:7] = j.q
                             f[7:10] = j.axis
                             li.append([parent, j.type if j.type in (T.JOINT_FIXED, T.JOINT_REVOLUTE,
                                                                     T.JOINT_PRISMATIC) else T.JOINT_FIXED, d, b])

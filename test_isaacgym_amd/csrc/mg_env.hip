@@ -961,8 +961,10 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         const int b = ei[3 + fk];
         uv = St[(7 + fc) * nb + b];
     }
+    // link ln's body (-1: a virtual link of a ball / multi-axis joint, no mass)
+    const int blk = ln < L ? A.link_i[ln * MG_LINK_I_N + 3] : -1;
     LinkC lk = {};
-    if (ln < L) lk = load_link(A.mass, nb, b0 + ln);
+    if (blk >= 0) lk = load_link(A.mass, nb, b0 + blk);
     __syncthreads();
     // the DOF lane's joint: link, revolute flag
     const int mylink = is_dof ? S.dlink[ln] : 0;
@@ -1412,8 +1414,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         }
     }
     __syncthreads();
-    if (live && ln < L) {
-        const int b = b0 + ln;
+    if (live && blk >= 0) {
+        const int b = b0 + blk;
         const Q4 ql = S.ql[ln];
         const V3 xl = S.xl[ln];
         const SV vl = sv6(S.va[ln]);

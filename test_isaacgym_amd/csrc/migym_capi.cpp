@@ -478,7 +478,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                             "env %d: %zu articulations / %zu free / %zu static bodies in contact range; the "
                             "coupled step supports 1 / %d / %d", e, art.size(), fr.size(), stc.size(),
                             MG_ENV_MAXF, MG_ENV_MAXS);
-            int art_nl = 0, art_nd = 0, art_fb = 0;
+            int art_nl = 0, art_nd = 0, art_fb = 0, art_fl = 0;
             if (!art.empty()) {
                 const int k = artic_of_root[m->actor_root_body[art[0]]];
                 const int t = k >= 0 ? m->artic_i[(size_t)k * MG_ARTIC_I_N + 2] : -1;
@@ -489,10 +489,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                 const int fl = m->artic_tmpl_i[t * MG_ATMPL_I_N + 0];
                 if (fl < 0 || art_nl < 1 || fl + art_nl > m->num_tmpl_links)
                     return fail(MG_ERR_ARG, "env %d: bad articulation template %d", e, t);
-                for (int l = 0; l < art_nl; ++l)
-                    if (m->tmpl_link_i[(size_t)(fl + l) * MG_LINK_I_N + 3] != l)
-                        return fail(MG_ERR_UNSUPPORTED, "env %d: ball joints (virtual links) in the coupled per-env "
-                                    "step (contacts between actors, or a floating base)", e);
+                art_fl = fl;
             }
             if (art_nd + 6 * art_fb + 6 * (int)fr.size() > MG_ENV_G)
                 return fail(MG_ERR_UNSUPPORTED, "env %d: %d DOFs%s + %zu free bodies exceed the %d velocity slots of "
@@ -567,8 +564,11 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                 }
             }
             for (int l = art_fb ? 0 : 1; l < art_nl; ++l) {     // moving links (a floating base moves)
+                // the link's body (virtual links of ball / multi-axis joints: none)
+                const int bl = m->tmpl_link_i[(size_t)(art_fl + l) * MG_LINK_I_N + 3];
+                if (bl < 0) continue;
                 int sa0, nsa;
-                shp(row[0] + l, &sa0, &nsa);
+                shp(row[0] + bl, &sa0, &nsa);
                 for (int sa = sa0; sa < sa0 + nsa; ++sa) {
                     if (ground) push(l, sa, -1, -1);
                     for (int t = 0; t < (int)stc.size(); ++t) {
@@ -690,9 +690,6 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                 for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_step.push_back(ai[j]);
                 g.step_count++;
             }
-            if (coupled_body[ai[0]] && g.nbody != g.nl)
-                return fail(MG_ERR_UNSUPPORTED, "articulation %d: ball joints in the coupled per-env step (an env "
-                            "with contacts between actors, or a floating base)", k);
             for (int l = 0; l < g.nbody; ++l) {
                 if (placed[ai[0] + l]) return fail(MG_ERR_ARG, "articulation %d overlaps another body", k);
                 placed[ai[0] + l] = 1;

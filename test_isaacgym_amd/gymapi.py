@@ -272,19 +272,19 @@ class Gym:
         return self.get_asset_rigid_body_dict(asset).get(name, _T.INVALID_HANDLE)
 
     def get_asset_joint_count(self, asset):
-        return len(asset.joints)
+        return len(asset.api_joints)
 
     def get_asset_joint_name(self, asset, i):
-        return asset.joints[i].name
+        return asset.api_joints[i].name
 
     def get_asset_joint_names(self, asset):
-        return [j.name for j in asset.joints]
+        return [j.name for j in asset.api_joints]
 
     def get_asset_joint_dict(self, asset):
-        return {j.name: i for i, j in enumerate(asset.joints)}
+        return {j.name: i for i, j in enumerate(asset.api_joints)}
 
     def get_asset_joint_type(self, asset, i):
-        return asset.joints[i].type
+        return asset.api_joints[i].type
 
     def find_asset_joint_index(self, asset, name):
         return self.get_asset_joint_dict(asset).get(name, _T.INVALID_HANDLE)
@@ -429,13 +429,13 @@ class Gym:
         return _T.INVALID_HANDLE if h < 0 else self.find_actor_rigid_body_handle(env, h, body_name)
 
     def get_actor_joint_count(self, env, handle):
-        return len(self._actor(env, handle).asset.joints)
+        return len(self._actor(env, handle).asset.api_joints)
 
     def get_actor_joint_names(self, env, handle):
-        return [j.name for j in self._actor(env, handle).asset.joints]
+        return [j.name for j in self._actor(env, handle).asset.api_joints]
 
     def get_actor_joint_dict(self, env, handle):
-        return {j.name: i for i, j in enumerate(self._actor(env, handle).asset.joints)}
+        return {j.name: i for i, j in enumerate(self._actor(env, handle).asset.api_joints)}
 
     def get_actor_joint_handle(self, env, handle, index):
         return index
@@ -564,13 +564,20 @@ class Gym:
             N.check(N.lib.mg_refresh_dof_state(sim.native, ds.ctypes.data, 1, sim.stream()), "refresh")
         return rb, ds[:sim.num_dofs]
 
+    def _host_dof_state(self, sim):
+        """Current DOF state (nd, 2) on the host (no rigid-body download)."""
+        ds = np.zeros((max(sim.num_dofs, 1), 2), dtype=np.float32)
+        if sim.num_dofs:
+            N.check(N.lib.mg_refresh_dof_state(sim.native, ds.ctypes.data, 1, sim.stream()), "refresh")
+        return ds[:sim.num_dofs]
+
     def get_actor_dof_states(self, env, handle, flags=_T.STATE_ALL):
         a = self._actor(env, handle)
         out = np.zeros(a.num_dofs, dtype=DofState.dtype)
         if not env.sim.finalized:
             out["pos"], out["vel"] = a.dof_state[:, 0], a.dof_state[:, 1]
             return out
-        _, ds = self._host_state(env.sim)
+        ds = self._host_dof_state(env.sim) if env.sim.native else self._host_state(env.sim)[1]
         sl = ds[a.global_dof:a.global_dof + a.num_dofs]
         out["pos"], out["vel"] = sl[:, 0], sl[:, 1]
         return out
@@ -586,9 +593,12 @@ class Gym:
         if sim.finalized and sim.native and a.num_dofs:
             # start from the actor's current device state, so the column that
             # `flags` does not select keeps its simulated value (Isaac Gym leaves it
-            # untouched: examples/joint_monkey.py:251 sets STATE_POS every frame)
-            _, ds = self._host_state(sim)
-            cur = ds[a.global_dof:a.global_dof + a.num_dofs].copy()
+            # untouched: examples/joint_monkey.py:251 sets STATE_POS every frame);
+            # both columns selected: nothing to merge, no download
+            if (flags & _T.STATE_ALL) == _T.STATE_ALL:
+                cur = a.dof_state.copy()
+            else:
+                cur = self._host_dof_state(sim)[a.global_dof:a.global_dof + a.num_dofs].copy()
             if flags & _T.STATE_POS:
                 cur[:, 0] = a.dof_state[:, 0]
             if flags & _T.STATE_VEL:

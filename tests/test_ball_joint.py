@@ -223,21 +223,52 @@ def test_spherical_pendulum_invariants(gym, tmp_path):
     assert abs(l32 - 1.0) < 0.35 * abs(l8 - 1.0) and abs(e32) < 0.35 * abs(e8)
 
 
-def test_coupled_step_refuses_ball_joint(gym, tmp_path):
-    """A ball-joint articulation touching another actor would need the coupled
-    per-env step, which keeps one body per link: refused, not mis-stepped."""
-    d = str(tmp_path)
-    sim = _sim(gym)
+def _coupled_scene(gym, d, n, gpu=False, seed=0):
+    """A ball-joint pendulum (tilted, swinging) over a free box resting on a
+    static slab in the same collision group: the env steps in the coupled per-env
+    kernel, whose links now include the ball joint's two virtual links."""
+    sim = _sim(gym, gpu=gpu)
     opts = gymapi.AssetOptions()
     opts.fix_base_link = True
     asset = gym.load_asset(sim, d, _urdf(d, "b.urdf", prismatic=False), opts)
-    box = gym.create_box(sim, 0.1, 0.1, 0.1, gymapi.AssetOptions())
-    env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 2), 1)
-    gym.create_actor(env, asset, gymapi.Transform(gymapi.Vec3(0, 0, 1.5)), "ball", 0, 0)
-    gym.create_actor(env, box, gymapi.Transform(gymapi.Vec3(0, 0, 0.8)), "box", 0, 0)
+    box = gym.create_box(sim, 0.3, 0.3, 0.2, gymapi.AssetOptions())
+    fixed = gymapi.AssetOptions()
+    fixed.fix_base_link = True
+    slab = gym.create_box(sim, 1.0, 1.0, 0.1, fixed)
+    rng = np.random.RandomState(seed)
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 2), 8)
+        h = gym.create_actor(env, asset, gymapi.Transform(gymapi.Vec3(0, 0, 1.4)), "ball", i, 0)
+        props = gym.get_actor_dof_properties(env, h)
+        props["driveMode"][:] = gymapi.DOF_MODE_NONE
+        gym.set_actor_dof_properties(env, h, props)
+        st = np.zeros(3, dtype=gymapi.DofState.dtype)
+        st["pos"] = [0.9 + rng.uniform(-0.05, 0.05), rng.uniform(-0.1, 0.1), 0.0]
+        gym.set_actor_dof_states(env, h, st, gymapi.STATE_ALL)
+        gym.create_actor(env, box, gymapi.Transform(gymapi.Vec3(0, 0.05 * rng.uniform(-1, 1), 0.75)), "box", i, 0)
+        gym.create_actor(env, slab, gymapi.Transform(gymapi.Vec3(0, 0, 0.6)), "slab", i, 0)
+    return sim
+
+
+def test_coupled_step_ball_joint(gym, tmp_path):
+    """The bob (5 kg, 0.5 m below the pivot) swings down onto the box (18 kg)
+    on the slab: the coupled step, with the ball joint's virtual links, stops it
+    on the box (without the box it swings through to the other side) while the
+    slab holds the box up and the bob stays on its sphere."""
+    sim = _coupled_scene(gym, str(tmp_path), 1)
     A = sim.build_model()
-    with pytest.raises(RuntimeError):
-        oracle.step(sim.mg_params(), sim.mg_model(), A["body_state0"].copy(), A["dof_state0"].copy())
+    p, m = sim.mg_params(), sim.mg_model()
+    st, dof = A["body_state0"].copy(), A["dof_state0"].copy()
+    box0 = st[2, 0:3].copy()
+    pivot = st[0, 0:3].copy()
+    for _ in range(90):
+        oracle.step(p, m, st, dof)
+        com = st[1, 0:3] + _qrot(st[1, 3:7], np.array([0.0, 0.0, -0.5]))
+        assert abs(np.linalg.norm(com - pivot) - 0.5) < 1e-4
+    assert np.all(np.isfinite(st)) and np.all(np.isfinite(dof))
+    assert dof[0, 0] > 0.3                                          # caught by the box, not swung through
+    assert abs(st[2, 2] - box0[2]) < 0.02                           # the slab holds the box
+    assert np.linalg.norm(st[2, 0:2] - box0[0:2]) < 0.05
 
 
 # ------------------------------------------------------------------ GPU
@@ -298,3 +329,25 @@ def test_ball_joint_jacobian_mass_matrix_gpu(gym, tmp_path):
         q = A["dof_state0"][i * 6:(i + 1) * 6, 0].astype(np.float64)
         assert np.abs(J[i] - art.jacobian(base, q)).max() < 1e-4
         assert np.abs(M[i] - art.mass_matrix(base, q, b0)).max() < 1e-3 * max(1.0, np.abs(M[i]).max())
+
+
+@pytest.mark.gpu
+def test_coupled_ball_joint_parity_gpu(gym, tmp_path):
+    """The coupled scene above, 64 envs: k_env_step bit for bit the oracle."""
+    n, steps = 64, 60
+    sim = _coupled_scene(gym, str(tmp_path), n, gpu=True, seed=2)
+    gym.prepare_sim(sim)
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    ds = sim.model_arrays["dof_state0"].copy()
+    for _ in range(steps):
+        gym.simulate(sim)
+        oracle.step(p, m, st, ds)
+    gym.refresh_dof_state_tensor(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    got_d, got = dof.cpu().numpy(), rb.cpu().numpy()
+    assert np.all(np.isfinite(got))
+    assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()

@@ -1,0 +1,178 @@
+"""MJCF bodies with several joints:
+assets/mjcf/nv_humanoid.xml:53-54 (abdomen_z + abdomen_y on lower_waist) and
+:61-63 (three hips on each thigh), the default asset of examples/joint_monkey.py:35.
+
+A body hanging by k hinges is k kernel links: k - 1 virtual (no body, no mass)
+and the body's own, each hinge about its axis in the body frame as turned by
+the hinges before it (MuJoCo's order), sharing one anchor — the same packing as
+a ball joint's three rotations (include/migym.h MG_LINK_I_N).
+
+CPU: the importer's counts, names, efforts and link packing against the
+reference file; a two-hinge body steps exactly like the same chain written as a
+URDF with a massless link between two revolute joints. GPU: k_artic_lanes and
+k_env_step (the two-hinge arm swinging onto a box) bit for bit the oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from isaacgym import gymapi, gymtorch
+import oracle
+from conftest import REFERENCE
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HUMANOID_DOFS = ["abdomen_z", "abdomen_y", "abdomen_x", "right_hip_x", "right_hip_z", "right_hip_y", "right_knee",
+                 "right_ankle_y", "right_ankle_x", "left_hip_x", "left_hip_z", "left_hip_y", "left_knee",
+                 "left_ankle_y", "left_ankle_x", "right_shoulder1", "right_shoulder2", "right_elbow",
+                 "left_shoulder1", "left_shoulder2", "left_elbow"]
+
+
+def _sim(gym, gpu=False, gravity=-9.8):
+    sp = gymapi.SimParams()
+    sp.up_axis = gymapi.UP_AXIS_Z
+    sp.gravity = gymapi.Vec3(0, 0, gravity)
+    sp.dt, sp.substeps = 1.0 / 60.0, 2
+    sp.physx.solver_type = 1
+    sp.physx.num_position_iterations = 6
+    sp.physx.num_velocity_iterations = 1
+    sp.use_gpu_pipeline = gpu
+    return gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+
+
+def _humanoid(gym, root):
+    sim = _sim(gym)
+    a = gym.load_asset(sim, root, "mjcf/" + ("nv_humanoid.xml" if root != os.path.join(ROOT, "assets")
+                                             else "humanoid.xml"), gymapi.AssetOptions())
+    return sim, a
+
+
+@pytest.mark.parametrize("where", ["repo", "reference"])
+def test_nv_humanoid_loads(gym, where):
+    root = os.path.join(ROOT, "assets") if where == "repo" else os.path.join(REFERENCE, "assets")
+    if where == "reference" and not os.path.exists(os.path.join(root, "mjcf", "nv_humanoid.xml")):
+        pytest.skip("reference tree absent")
+    sim, a = _humanoid(gym, root)
+    assert a is not None
+    assert gym.get_asset_rigid_body_count(a) == 16 and gym.get_asset_dof_count(a) == 21
+    assert gym.get_asset_dof_names(a) == HUMANOID_DOFS
+    names = gym.get_asset_joint_names(a)
+    assert "abdomen_z" in names and "abdomen_y" in names and names.index("abdomen_z") + 1 == names.index("abdomen_y")
+    props = gym.get_asset_dof_properties(a)
+    # motor gear x the <default><motor ctrlrange="-1 1"> (nv_humanoid.xml:8, :141-161)
+    assert props["effort"][HUMANOID_DOFS.index("abdomen_y")] == pytest.approx(67.5)
+    assert props["effort"][HUMANOID_DOFS.index("right_hip_y")] == pytest.approx(135.0)
+    assert props["effort"][HUMANOID_DOFS.index("right_knee")] == pytest.approx(90.0)
+    assert props["lower"][0] == pytest.approx(np.radians(-45)) and props["upper"][1] == pytest.approx(np.radians(30))
+    assert props["armature"][0] == pytest.approx(0.02)          # big_stiff_joint class
+    env = gym.create_env(sim, gymapi.Vec3(-2, -2, 0), gymapi.Vec3(2, 2, 2), 1)
+    gym.create_actor(env, a, gymapi.Transform(gymapi.Vec3(0, 0, 1.4)), "h", 0, 0)
+    A = sim.build_model()
+    li = A["tmpl_link_i"]
+    # 16 bodies + 9 virtual links: abdomen 1, hips 2 + 2, ankles 1 + 1, shoulders 1 + 1
+    assert li.shape[0] == 25 and int((li[:, 3] < 0).sum()) == 9
+    assert sorted(li[li[:, 3] >= 0, 3].tolist()) == list(range(16))
+
+
+def _two_hinge_mjcf(d):
+    xml = ('<mujoco><worldbody><body name="base" pos="0 0 1.2"><geom type="box" size="0.05 0.05 0.05"/>'
+           '<body name="arm" pos="0 0 -0.05"><joint name="hz" type="hinge" axis="0 0 1" pos="0 0 0"/>'
+           '<joint name="hy" type="hinge" axis="0 1 0" pos="0 0 0"/>'
+           '<inertial pos="0.3 0 -0.2" mass="2" diaginertia="0.02 0.03 0.04"/>'
+           '<geom type="sphere" size="0.08" pos="0.3 0 -0.2" density="0"/></body></body></worldbody></mujoco>')
+    with open(os.path.join(d, "two.xml"), "w") as f:
+        f.write(xml)
+    return "two.xml"
+
+
+def _two_hinge_urdf(d):
+    """The same chain as a URDF: a massless link between two revolute joints."""
+    urdf = ('<robot name="two"><link name="base"><inertial><mass value="1"/><inertia ixx="0.01" iyy="0.01" '
+            'izz="0.01" ixy="0" ixz="0" iyz="0"/></inertial><collision><geometry><box size="0.1 0.1 0.1"/>'
+            '</geometry></collision></link>'
+            '<link name="mid"><inertial><mass value="0"/><inertia ixx="0" iyy="0" izz="0" ixy="0" ixz="0" '
+            'iyz="0"/></inertial></link>'
+            '<link name="arm"><inertial><origin xyz="0.3 0 -0.2"/><mass value="2"/><inertia ixx="0.02" iyy="0.03" '
+            'izz="0.04" ixy="0" ixz="0" iyz="0"/></inertial><collision><origin xyz="0.3 0 -0.2"/><geometry>'
+            '<sphere radius="0.08"/></geometry></collision></link>'
+            '<joint name="hz" type="continuous"><origin xyz="0 0 -0.05"/><axis xyz="0 0 1"/><parent link="base"/>'
+            '<child link="mid"/></joint>'
+            '<joint name="hy" type="continuous"><axis xyz="0 1 0"/><parent link="mid"/><child link="arm"/></joint>'
+            '</robot>')
+    with open(os.path.join(d, "two.urdf"), "w") as f:
+        f.write(urdf)
+    return "two.urdf"
+
+
+def _arm_scene(gym, d, fname, n=1, gpu=False, box=False):
+    sim = _sim(gym, gpu=gpu)
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    asset = gym.load_asset(sim, d, fname, opts)
+    cube = gym.create_box(sim, 0.2, 0.2, 0.2, gymapi.AssetOptions()) if box else None
+    fixed = gymapi.AssetOptions()
+    fixed.fix_base_link = True
+    slab = gym.create_box(sim, 1.2, 1.2, 0.1, fixed) if box else None
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 2), 8)
+        h = gym.create_actor(env, asset, gymapi.Transform(gymapi.Vec3(0, 0, 0)), "arm", i, 0)
+        props = gym.get_actor_dof_properties(env, h)
+        props["driveMode"][:] = gymapi.DOF_MODE_NONE
+        gym.set_actor_dof_properties(env, h, props)
+        st = np.zeros(2, dtype=gymapi.DofState.dtype)
+        st["pos"] = [0.4 + 0.01 * i, -0.3]
+        st["vel"] = [1.5, 0.0]
+        gym.set_actor_dof_states(env, h, st, gymapi.STATE_ALL)
+        if box:
+            gym.create_actor(env, cube, gymapi.Transform(gymapi.Vec3(0.25, 0.25, 0.7)), "cube", i, 0)
+            gym.create_actor(env, slab, gymapi.Transform(gymapi.Vec3(0, 0, 0.55)), "slab", i, 0)
+    return sim, asset
+
+
+def test_two_hinge_body_matches_urdf_chain(gym, tmp_path):
+    d = str(tmp_path)
+    sm, am = _arm_scene(gym, d, _two_hinge_mjcf(d))
+    su, au = _arm_scene(gym, d, _two_hinge_urdf(d))
+    assert gym.get_asset_rigid_body_count(am) == 2 and gym.get_asset_rigid_body_count(au) == 3
+    assert gym.get_asset_dof_names(am) == ["hz", "hy"] == gym.get_asset_dof_names(au)
+    A, B = sm.build_model(), su.build_model()
+    assert A["tmpl_link_i"][:, 3].tolist() == [0, -1, 1]
+    pm, mm_ = sm.mg_params(), sm.mg_model()
+    pu, mu = su.mg_params(), su.mg_model()
+    sa, da = A["body_state0"].copy(), A["dof_state0"].copy()
+    sb, db = B["body_state0"].copy(), B["dof_state0"].copy()
+    assert np.allclose(sa[1], sb[2], atol=1e-6)              # same initial pose of the arm
+    for _ in range(120):
+        oracle.step(pm, mm_, sa, da)
+        oracle.step(pu, mu, sb, db)
+    assert np.abs(da - db).max() < 1e-4
+    assert np.abs(sa[1] - sb[2]).max() < 1e-4
+    assert abs(da[0, 0] - 0.4) > 0.5                          # it moved
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("box", [False, True])
+def test_two_hinge_parity_gpu(gym, tmp_path, box):
+    """box=False: k_artic_lanes; box=True: the arm swings onto a cube on a slab
+    (coupled per-env step with a virtual link)."""
+    d = str(tmp_path)
+    n, steps = 64, 60
+    sim, _ = _arm_scene(gym, d, _two_hinge_mjcf(d), n=n, gpu=True, box=box)
+    gym.prepare_sim(sim)
+    from test_isaacgym_amd import _native as N
+    assert (N.lib.mg_num_coupled_envs(sim.native) > 0) == box
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    ds = sim.model_arrays["dof_state0"].copy()
+    for _ in range(steps):
+        gym.simulate(sim)
+        oracle.step(p, m, st, ds)
+    gym.refresh_dof_state_tensor(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    got_d, got = dof.cpu().numpy(), rb.cpu().numpy()
+    assert np.all(np.isfinite(got)) and np.abs(got_d[:, 1]).max() > 0.1
+    assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+    torch.cuda.synchronize()

@@ -1,17 +1,21 @@
-"""Writes assets/mjcf/ant.xml: the physics content of the reference's
-assets/mjcf/nv_ant.xml (compiler, defaults, the body / joint / geom tree,
+"""Writes assets/mjcf/<name>.xml: the physics content of one of the
+reference's MJCF assets (compiler, defaults, the body / joint / geom tree,
 motor actuators) re-serialized without rendering-only elements (textures,
-materials, lights, colours), so the GPU box, which has no /root/reference, can
-load the same ant (examples/apply_forces.py:67). Run in this container:
-    python tools/make_ant_asset.py [/root/reference/assets/mjcf/nv_ant.xml]
+materials, lights, cameras, sites, colours), so the GPU box, which has no
+/root/reference, can load the same model:
+    assets/mjcf/ant.xml       <- nv_ant.xml      (examples/apply_forces.py:67)
+    assets/mjcf/humanoid.xml  <- nv_humanoid.xml (examples/joint_monkey.py:35)
+Run in this container:
+    python tools/make_mjcf_asset.py            (both)
+    python tools/make_mjcf_asset.py SRC.xml DST_NAME
 """
 import os
 import sys
 import xml.etree.ElementTree as ET
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = sys.argv[1] if len(sys.argv) > 1 else "/root/reference/assets/mjcf/nv_ant.xml"
-DST = os.path.join(ROOT, "assets", "mjcf", "ant.xml")
+REF = "/root/reference/assets/mjcf"
+JOBS = [(os.path.join(REF, "nv_ant.xml"), "ant"), (os.path.join(REF, "nv_humanoid.xml"), "humanoid")]
 KEEP_ATTR = {"rgba", "material", "texture", "condim", "margin"}
 
 
@@ -24,9 +28,10 @@ def strip(el):
     return out
 
 
-def main():
+def convert(SRC, name):
+    DST = os.path.join(ROOT, "assets", "mjcf", name + ".xml")
     src = ET.parse(SRC).getroot()
-    dst = ET.Element("mujoco", {"model": src.get("model", "ant")})
+    dst = ET.Element("mujoco", {"model": src.get("model", name)})
     for tag in ("compiler", "default", "worldbody", "actuator"):
         el = src.find(tag)
         if el is None:
@@ -43,4 +48,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    for src, name in ([(sys.argv[1], sys.argv[2])] if len(sys.argv) > 2 else JOBS):
+        convert(src, name)
