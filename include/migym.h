@@ -66,7 +66,7 @@ extern "C" {
 #define MG_JOINT_FIXED     0
 #define MG_JOINT_REVOLUTE  1
 #define MG_JOINT_PRISMATIC 2
-#define MG_JOINT_BALL      3   /* never in tmpl_link_i: packed as three revolute links */
+#define MG_JOINT_BALL      3   /* never in tmpl_link_i: packed as three revolute links (tmpl_link_f[10]) */
 
 /* DOF drive modes — values of gymapi.DofDriveMode */
 #define MG_DOF_MODE_NONE   0
@@ -81,14 +81,18 @@ extern "C" {
 #define MG_TBODY_I_N       4  /* shape_start, shape_count, pad, pad */
 #define MG_SHAPE_STRIDE   16  /* type, size[3], p[3], q[4], friction, restitution, pad[3] */
 #define MG_DOFPROP_N      12  /* mode, kp, kd, effort, max_vel, lower, upper, has_limits, armature, friction, pad[2] */
-#define MG_LINK_F_N       16  /* joint origin p[3], q[4] (parent link frame), axis[3] (joint frame), pad[6] */
+#define MG_LINK_F_N       16  /* joint origin p[3], q[4] (parent link frame), axis[3] (joint frame),
+                                  ball place [1] (0: none, 1..3: a ball joint's links), pad[5] */
 /* parent (local, -1 root), joint type, dof (local, -1 none), body (local body index of the
  * link, -1 for a virtual link). Kernel links drive at most one DOF each: a spherical
  * (JOINT_BALL) joint is packed as three revolute links about the joint frame's x, y, z
  * axes, the first two virtual (no body, no mass: test13_camera_spherical_joint.py's
- * dof_spherical_joint_test.urdf). Real links carry body indices 0, 1, 2, ... in link
- * order; templates with virtual links step in the articulation kernel only (not the
- * coupled per-env step). */
+ * dof_spherical_joint_test.urdf), marked by tmpl_link_f[10] = 1, 2, 3: its DOF
+ * positions are the rotation vector of the joint (exponential coordinates, test13
+ * quat2expcoord), the first link turning by exp of all three and the other two not at
+ * all, so the three rates are the child frame's angular velocity; an MJCF body with
+ * several hinges is likewise one virtual link per extra hinge. Real links carry body
+ * indices 0, 1, 2, ... in link order. */
 #define MG_LINK_I_N        4
 #define MG_ARTIC_I_N       4  /* first_body, first_dof, tmpl, pad */
 /* first_link (into tmpl_link_*), num_links, num_dofs, fixed_base. fixed_base 0: a

@@ -528,19 +528,73 @@ static q4_t qaxang_(v3_t a, float th) {
     return Q(a.x * s, a.y * s, a.z * s, c);
 }
 
-/* joint transform of link l at (q, qd): relative rotation/translation, S, vJ */
-static void joint_(const float* lf, int jt, float qj, q4_t* qrel, v3_t* rr, sv_t* S) {
+/* ---- ball joints in exponential coordinates (mg_spatial.h q_exp / q_log /
+ * ball_step / link_joint, op for op): DOF positions = the rotation vector of
+ * the child joint frame, velocities = its angular velocity in the child frame
+ * (test13_camera_spherical_joint.py:243-256, quat2expcoord) */
+static q4_t qexp_(v3_t th) {
+    const float t2 = dot3(th, th);
+    float t, s, c, k;
+    if (!(t2 > 0.0f)) return Q(0.0f, 0.0f, 0.0f, 1.0f);
+    t = sqrtf(t2);
+    sincos_(0.5f * t, &s, &c);
+    k = s / t;
+    return Q(th.x * k, th.y * k, th.z * k, c);
+}
+static float atan_small_(float u) {
+    const float u2 = u * u;
+    float p = 1.0f / 19.0f;
+    p = 1.0f / 17.0f - u2 * p;
+    p = 1.0f / 15.0f - u2 * p;
+    p = 1.0f / 13.0f - u2 * p;
+    p = 1.0f / 11.0f - u2 * p;
+    p = 1.0f / 9.0f - u2 * p;
+    p = 1.0f / 7.0f - u2 * p;
+    p = 1.0f / 5.0f - u2 * p;
+    p = 1.0f / 3.0f - u2 * p;
+    p = 1.0f - u2 * p;
+    return u * p;
+}
+static float atan01_(float t) {
+    if (t > 0.41421356f) return 0.78539816f + atan_small_((t - 1.0f) / (t + 1.0f));
+    return atan_small_(t);
+}
+static v3_t qlog_(q4_t q) {
+    float v2, vn, ha, k;
+    if (q.w < 0.0f) q = Q(-q.x, -q.y, -q.z, -q.w);
+    v2 = q.x * q.x + q.y * q.y + q.z * q.z;
+    if (!(v2 > 0.0f)) return V(0.0f, 0.0f, 0.0f);
+    vn = sqrtf(v2);
+    ha = vn <= q.w ? atan01_(vn / q.w) : 1.57079633f - atan01_(q.w / vn);
+    k = (2.0f * ha) / vn;
+    return V(q.x * k, q.y * k, q.z * k);
+}
+static v3_t ball_step_(v3_t th, v3_t dth) { return qlog_(qnorm_(qmul_(qexp_(th), qexp_(dth)))); }
+
+/* joint transform of link l at (q, qd): relative rotation/translation, S, vJ.
+ * q: the articulation's DOF positions (a ball joint's first link reads three) */
+static void joint_(const float* lf, int jt, const float* q, int dj, q4_t* qrel, v3_t* rr, sv_t* S) {
     const v3_t po = V(lf[0], lf[1], lf[2]);
     const q4_t qo = Q(lf[3], lf[4], lf[5], lf[6]);
     const v3_t ax = V(lf[7], lf[8], lf[9]);
+    const int ball = (int)lf[10];
+    const float qj = dj >= 0 ? q[dj] : 0.0f;
     *qrel = qo; *rr = po; *S = sv0();
     if (jt == MG_JOINT_REVOLUTE) {
-        *qrel = qmul_(qo, qaxang_(ax, qj));
+        if (ball == 1) *qrel = qmul_(qo, qexp_(V(q[dj], q[dj + 1], q[dj + 2])));
+        else if (ball == 0) *qrel = qmul_(qo, qaxang_(ax, qj));
         *S = SVc(ax, V(0.0f, 0.0f, 0.0f));
     } else if (jt == MG_JOINT_PRISMATIC) {
         *rr = add3(po, qrot_(qo, mul3(ax, qj)));
         *S = SVc(V(0.0f, 0.0f, 0.0f), ax);
     }
+}
+/* place of DOF d in a ball joint (1, 2, 3; 0: not a ball DOF) */
+static int dof_ball_(const float* LF, const int* LI, int L, int d) {
+    int l;
+    for (l = 0; l < L; ++l)
+        if (LI[l * MG_LINK_I_N + 2] == d) return (int)LF[l * MG_LINK_F_N + 10];
+    return 0;
 }
 
 #include "migym_oracle_env.c"
@@ -575,18 +629,31 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
         float tau0d[OR_MAXL], impd[OR_MAXL], mdiag[OR_MAXL];
         static __thread aba_ws_t W;   /* per thread: oracle_step_mt */
         aba_world_(P, m, LF, LI, L, D, b0, d0, q, qd, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd, 0, ext);
-        for (d = 0; d < D; ++d) {
-            const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
-            const float maxv = pr[4];
-            float wv = qd[d] + h * qdd[d], xv;
-            if (maxv > 0.0f) wv = fminf(fmaxf(wv, -maxv), maxv);
-            xv = q[d] + h * wv;
-            if (pr[7] != 0.0f) {
-                const float lo = pr[5], hi = pr[6];
-                if (xv < lo) { xv = lo; if (wv < 0.0f) wv = 0.0f; }
-                if (xv > hi) { xv = hi; if (wv > 0.0f) wv = 0.0f; }
+        {
+            float qn[OR_MAXL], wn[OR_MAXL];
+            for (d = 0; d < D; ++d) {
+                const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
+                const float maxv = pr[4];
+                float wv = qd[d] + h * qdd[d], xv;
+                if (maxv > 0.0f) wv = fminf(fmaxf(wv, -maxv), maxv);
+                xv = q[d] + h * wv;
+                if (pr[7] != 0.0f) {
+                    const float lo = pr[5], hi = pr[6];
+                    if (xv < lo) { xv = lo; if (wv < 0.0f) wv = 0.0f; }
+                    if (xv > hi) { xv = hi; if (wv > 0.0f) wv = 0.0f; }
+                }
+                qn[d] = xv; wn[d] = wv;
             }
-            q[d] = xv; qd[d] = wv;
+            for (d = 0; d < D; ++d) {   /* ball joints: th <- log(exp(th) exp(h w)) */
+                const int bk = dof_ball_(LF, LI, L, d);
+                if (bk > 0) {
+                    const int f = d - (bk - 1);
+                    const v3_t tn = ball_step_(V(q[f], q[f + 1], q[f + 2]),
+                                               V(h * wn[f], h * wn[f + 1], h * wn[f + 2]));
+                    qn[d] = bk == 1 ? tn.x : (bk == 2 ? tn.y : tn.z);
+                }
+            }
+            for (d = 0; d < D; ++d) { q[d] = qn[d]; qd[d] = wn[d]; }
         }
     }
     for (d = 0; d < D; ++d) { dof[(d0 + d) * 2 + 0] = q[d]; dof[(d0 + d) * 2 + 1] = qd[d]; }
@@ -600,8 +667,8 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
             ql[l] = q0; xl[l] = x0; v[l] = sv0();
         } else {
             q4_t qrel; v3_t rr; sv_t s;
-            const float qj = dj >= 0 ? q[dj] : 0.0f, qdj = dj >= 0 ? qd[dj] : 0.0f;
-            joint_(LF + l * MG_LINK_F_N, jt, qj, &qrel, &rr, &s);
+            const float qdj = dj >= 0 ? qd[dj] : 0.0f;
+            joint_(LF + l * MG_LINK_F_N, jt, q, dj, &qrel, &rr, &s);
             ql[l] = qnorm_(qmul_(ql[p], qrel));
             xl[l] = add3(xl[p], qrot_(ql[p], rr));
             v[l] = svadd_(xmot_(mt_(qmat_(qrel)), rr, v[p]), svmul_(s, qdj));

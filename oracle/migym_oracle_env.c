@@ -776,8 +776,11 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
                 const v3_t po = V(lf[0], lf[1], lf[2]), ax = V(lf[7], lf[8], lf[9]);
                 const q4_t qo = Q(lf[3], lf[4], lf[5], lf[6]);
                 const float qj = dj >= 0 ? q[dj] : 0.0f;
+                const int ball = (int)lf[10];       /* a ball joint's link (mg_spatial.h link_joint) */
                 qrl[l] = qo; rrl[l] = po;
-                if (jt == MG_JOINT_REVOLUTE) qrl[l] = qmul_(qo, qaxang_(ax, qj));
+                if (ball == 1) qrl[l] = qmul_(qo, qexp_(V(q[dj], q[dj + 1], q[dj + 2])));
+                else if (ball > 1) qrl[l] = qo;
+                else if (jt == MG_JOINT_REVOLUTE) qrl[l] = qmul_(qo, qaxang_(ax, qj));
                 else if (jt == MG_JOINT_PRISMATIC) rrl[l] = add3(po, qrot_(qo, mul3(ax, qj)));
             }
             for (l = 0; l < L; ++l) {
@@ -811,9 +814,17 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
                 const float qd = dj >= 0 ? u[dj] : 0.0f;
                 const sv_t v = sv6_(va[l]);
                 const sv_t vJ = svmul_(sv6_(xi[l]), qd);
+                const int ball = (int)LF[l * MG_LINK_F_N + 10];   /* ball joint: v_parent x vJ (mg_env.hip aba_vp) */
+                sv_t vb = v;
                 float Iv[6];
+                if (ball >= 2) {
+                    int pb = LI[l * MG_LINK_I_N + 0];
+                    pb = LI[pb * MG_LINK_I_N + 0];
+                    if (ball == 3) pb = LI[pb * MG_LINK_I_N + 0];
+                    vb = sv6_(va[pb]);
+                }
                 for (i = 0; i < 6; ++i) Iv[i] = dot6_(&Iw[l][i * 6], va[l]);
-                put6_(ccv[l], crm_(v, vJ));
+                put6_(ccv[l], crm_(vb, vJ));
                 {
                     sv_t pb = crf_(v, sv6_(Iv));
                     if (ext && LI[l * MG_LINK_I_N + 3] >= 0) {
@@ -1281,18 +1292,30 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         }
 
         /* ---- 5. integrate */
-        for (d = 0; d < D; ++d) {
-            const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
-            const float maxv = pr[4];
-            float w = u[d], x;
-            if (maxv > 0.0f) w = fminf(fmaxf(w, -maxv), maxv);
-            x = q[d] + dp[d];
-            if (pr[7] != 0.0f) {
-                const float lo = pr[5], hi = pr[6];
-                if (x < lo) { x = lo; if (w < 0.0f) w = 0.0f; }
-                if (x > hi) { x = hi; if (w > 0.0f) w = 0.0f; }
+        {
+            float qn[OE_G];
+            for (d = 0; d < D; ++d) {
+                const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
+                const float maxv = pr[4];
+                float w = u[d], x;
+                if (maxv > 0.0f) w = fminf(fmaxf(w, -maxv), maxv);
+                x = q[d] + dp[d];
+                if (pr[7] != 0.0f) {
+                    const float lo = pr[5], hi = pr[6];
+                    if (x < lo) { x = lo; if (w < 0.0f) w = 0.0f; }
+                    if (x > hi) { x = hi; if (w > 0.0f) w = 0.0f; }
+                }
+                qn[d] = x; u[d] = w;
             }
-            q[d] = x; u[d] = w;
+            for (d = 0; d < D; ++d) {   /* ball joints: th <- log(exp(th) exp(dpos)) */
+                const int bk = dof_ball_(LF, LI, L, d);
+                if (bk > 0) {
+                    const int f = d - (bk - 1);
+                    const v3_t tn = ball_step_(V(q[f], q[f + 1], q[f + 2]), V(dp[f], dp[f + 1], dp[f + 2]));
+                    qn[d] = bk == 1 ? tn.x : (bk == 2 ? tn.y : tn.z);
+                }
+            }
+            for (d = 0; d < D; ++d) q[d] = qn[d];
         }
         for (c = 0; c < nct; ++c) {
             v3_t imp;
@@ -1343,8 +1366,8 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             ql[l] = q0; xl[l] = x0; vl[l] = SVc(qrot_(qc, w), qrot_(qc, vo));
         } else {
             q4_t qrel; v3_t rr; sv_t sj;
-            const float qj = dj >= 0 ? q[dj] : 0.0f, qdj = dj >= 0 ? u[dj] : 0.0f;
-            joint_(LF + l * MG_LINK_F_N, jt, qj, &qrel, &rr, &sj);
+            const float qdj = dj >= 0 ? u[dj] : 0.0f;
+            joint_(LF + l * MG_LINK_F_N, jt, q, dj, &qrel, &rr, &sj);
             ql[l] = qnorm_(qmul_(ql[p], qrel));
             xl[l] = add3(xl[p], qrot_(ql[p], rr));
             vl[l] = svadd_(xmot_(mt_(qmat_(qrel)), rr, vl[p]), svmul_(sj, qdj));

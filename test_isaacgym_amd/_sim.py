@@ -251,12 +251,12 @@ class Sim:
                 s, c = np.sin(0.5 * qj), np.cos(0.5 * qj)
                 qrel = _qmul(qrel, np.array([j.axis[0] * s, j.axis[1] * s, j.axis[2] * s, c]))
             elif j.type == T.JOINT_BALL:
-                # rotations about the joint frame's x, y, z in turn (the three
-                # packed links of build_model)
-                for k in range(3):
-                    th = float(a.dof_state[d + k, 0])
-                    e = np.zeros(4)
-                    e[k], e[3] = np.sin(0.5 * th), np.cos(0.5 * th)
+                # exponential coordinates: the joint turns by exp(th), th the
+                # rotation vector of its three DOFs (mg_spatial.h q_exp)
+                th = np.array([float(a.dof_state[d + k, 0]) for k in range(3)])
+                t = float(np.linalg.norm(th))
+                if t > 0.0:
+                    e = np.array([*(th / t * np.sin(0.5 * t)), np.cos(0.5 * t)])
                     qrel = _qmul(qrel, e)
             elif j.type == T.JOINT_PRISMATIC:
                 rr = j.p + _qmat(j.q) @ (j.axis * qj)
@@ -396,6 +396,7 @@ class Sim:
                                     f[0:3] = j.p
                                     f[3:7] = j.q
                                 f[7 + k] = 1.0
+                                f[10] = k + 1     # place in the ball: the first link turns by exp(th)
                                 lf.append(f)
                                 li.append([parent, T.JOINT_REVOLUTE, d + k, b if k == 2 else -1])
                                 parent = len(lf) - 1 - nl0

@@ -59,11 +59,9 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
         const V3 po = v3(lf[0], lf[1], lf[2]);
         const Q4 qo = q4(lf[3], lf[4], lf[5], lf[6]);
         const V3 ax = v3(lf[7], lf[8], lf[9]);
-        const float qj = dof >= 0 ? A.dof_pos[d0 + dof] : 0.0f;
-        Q4 qrel = qo;
-        V3 rr = po;
-        if (jt == MG_JOINT_REVOLUTE) qrel = qmul(qo, q_axis_angle(ax, qj));
-        else if (jt == MG_JOINT_PRISMATIC) rr = vadd(po, qrot(qo, vscale(ax, qj)));
+        Q4 qrel;
+        V3 rr;
+        link_joint(jt, (int)lf[10], po, qo, ax, A.dof_pos + d0, dof, qrel, rr);
         S.qr[ln] = qrel;
         S.rr[ln] = rr;
     }

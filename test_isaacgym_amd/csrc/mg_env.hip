@@ -324,6 +324,21 @@ __device__ __forceinline__ bool cvx_pair(int ta, int tb) {
     return pa && pb && (ta == MG_SHAPE_CONVEX || tb == MG_SHAPE_CONVEX);
 }
 
+// place of DOF d in a ball joint (1, 2, 3; 0: not a ball DOF): link_f[10] of
+// the link it drives (mg_spatial.h, exponential coordinates)
+__device__ __forceinline__ int dof_ball(const MgEnvArgs& A, int LA, int d) {
+    int r = 0;
+    for (int l = 0; l < LA; ++l)
+        if (A.link_i[l * MG_LINK_I_N + 2] == d) r = (int)A.link_f[l * MG_LINK_F_N + 10];
+    return r;
+}
+// a ball DOF lane's new position: component k of log(exp(th) exp(dth)), th and
+// dth the three DOFs' values in q[] and dq[] (LDS), f the ball's first DOF
+__device__ __forceinline__ float ball_dof_step(const float* q, const float* dq, int f, int k) {
+    const V3 tn = ball_step(v3(q[f], q[f + 1], q[f + 2]), v3(dq[f], dq[f + 1], dq[f + 2]));
+    return k == 1 ? tn.x : (k == 2 ? tn.y : tn.z);
+}
+
 // substep-invariant per-lane constants: lane d < D holds DOF d's drive
 // properties and targets (link constants: LinkC, mg_world.h)
 struct DofC {
@@ -518,7 +533,18 @@ __device__ __forceinline__ void aba_vp(const MgEnvArgs& A, EnvLds& S, bool act, 
         const SV vJ = svscale(sv6(S.xi[ln]), qd);
         float Iv[6];
         for (int i = 0; i < 6; ++i) Iv[i] = dot6(&S.Iw[ln][i * 6], S.va[ln]);
-        put6(S.cc[ln], crm(v, vJ));
+        // a ball joint's later links: the velocity product with the ball's
+        // parent (its three axes are fixed in the child frame: the bias of the
+        // joint is v_parent x vJ, not the chain's v_{l-1} x vJ_l)
+        const int ball = (int)A.link_f[ln * MG_LINK_F_N + 10];
+        SV vb = v;
+        if (ball >= 2) {
+            int pb = A.link_i[ln * MG_LINK_I_N + 0];
+            pb = A.link_i[pb * MG_LINK_I_N + 0];
+            if (ball == 3) pb = A.link_i[pb * MG_LINK_I_N + 0];
+            vb = sv6(S.va[pb]);
+        }
+        put6(S.cc[ln], crm(vb, vJ));
         SV pb = crf(v, sv6(Iv));
         const int bl = A.link_i[ln * MG_LINK_I_N + 3];      // -1: virtual link
         if (A.ext && bl >= 0) {
@@ -563,11 +589,9 @@ __device__ __forceinline__ void aba_kin(const MgStep& P, const MgEnvArgs& A, Env
         const V3 po = v3(lf[0], lf[1], lf[2]);
         const Q4 qo = q4(lf[3], lf[4], lf[5], lf[6]);
         const V3 ax = v3(lf[7], lf[8], lf[9]);
-        const float qj = dof >= 0 ? S.q[dof] : 0.0f;
-        Q4 qrel = qo;
-        V3 rr = po;
-        if (jt == MG_JOINT_REVOLUTE) qrel = qmul(qo, q_axis_angle(ax, qj));
-        else if (jt == MG_JOINT_PRISMATIC) rr = vadd(po, qrot(qo, vscale(ax, qj)));
+        Q4 qrel;
+        V3 rr;
+        link_joint(jt, (int)lf[10], po, qo, ax, S.q, dof, qrel, rr);
         S.qr[ln] = qrel;
         S.rr[ln] = rr;
     }
@@ -867,6 +891,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     const int RB = (L > 0 && A.floating) ? 6 : 0;
     const int NS = D + RB;
     const bool is_dof = ln < D;
+    const int ballr = is_dof ? dof_ball(A, A.nl, ln) : 0;   // ball joints: exponential coordinates
+    const bool any_ball = __any(dof_ball(A, A.nl, ln % (A.ndof > 0 ? A.ndof : 1)) > 0);   // launch-uniform
     const bool is_root = ln >= D && ln < NS;
     const int rc = ln - D;
     const int fk = ln >= NS ? (ln - NS) / 6 : MAXF;
@@ -1307,7 +1333,10 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         __syncthreads();
         PH_MARK(4);
 
-        // ================= 5. integrate
+        // ================= 5. integrate (a ball joint's three lanes turn its
+        // rotation vector by its dpos together: ball_dof_step)
+        S.dpos[ln] = dp;
+        if (any_ball) __syncthreads();
         if (is_dof) {
             const float maxv = dc.maxv;
             float w = uv;
@@ -1318,10 +1347,10 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 if (x < lo) { x = lo; if (w < 0.0f) w = 0.0f; }
                 if (x > hi) { x = hi; if (w > 0.0f) w = 0.0f; }
             }
+            if (ballr > 0) x = ball_dof_step(S.q, S.dpos, ln - (ballr - 1), ballr);
             qv = x;
             uv = w;
         }
-        S.dpos[ln] = dp;
         __syncthreads();
         // contact impulse sums in contact order: link l on lane l, free body k on lane k
         if (live && (ln < L || ln < nfr)) {
@@ -1376,11 +1405,9 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         const V3 po = v3(lf[0], lf[1], lf[2]);
         const Q4 qo = q4(lf[3], lf[4], lf[5], lf[6]);
         const V3 ax = v3(lf[7], lf[8], lf[9]);
-        const float qj = dof >= 0 ? S.q[dof] : 0.0f;
-        Q4 qrel = qo;
-        V3 rr = po;
-        if (jt == MG_JOINT_REVOLUTE) qrel = qmul(qo, q_axis_angle(ax, qj));
-        else if (jt == MG_JOINT_PRISMATIC) rr = vadd(po, qrot(qo, vscale(ax, qj)));
+        Q4 qrel;
+        V3 rr;
+        link_joint(jt, (int)lf[10], po, qo, ax, S.q, dof, qrel, rr);
         S.qr[ln] = qrel;
         S.rr[ln] = rr;
     }
@@ -1478,6 +1505,8 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
     const float* pr = A.dof_props;
     const float h = P.h;
     const bool is_dof = ln < D;
+    const int ballr = is_dof ? dof_ball(A, LA, ln) : 0;   // ball joints: exponential coordinates
+    const bool any_ball = __any(dof_ball(A, LA, ln % (DA > 0 ? DA : 1)) > 0);   // launch-uniform
 
     V3 x0 = v3(0.0f, 0.0f, 0.0f), gw = v3(0.0f, 0.0f, 0.0f);
     Q4 q0 = q4(0.0f, 0.0f, 0.0f, 1.0f);
@@ -1536,15 +1565,24 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
             redo = ((fb >> (gi * G)) & 0xFFFFull) != 0ull;
             __syncthreads();
         }
-        // integrate the joint (DOF lane)
+        // integrate the joint (DOF lane); a ball joint's three lanes turn its
+        // rotation vector by h w together (ball_dof_step, S.dpos as scratch)
+        float w = 0.0f, x = 0.0f;
         if (is_dof) {
-            float w = uv + h * S.qdd[ln];
+            w = uv + h * S.qdd[ln];
             if (dc.maxv > 0.0f) w = fminf(fmaxf(w, -dc.maxv), dc.maxv);
-            float x = qv + h * w;
+            x = qv + h * w;
             if (dc.haslim) {
                 if (x < dc.lo) { x = dc.lo; if (w < 0.0f) w = 0.0f; }
                 if (x > dc.hi) { x = dc.hi; if (w > 0.0f) w = 0.0f; }
             }
+            S.dpos[ln] = h * w;
+        }
+        if (any_ball) {
+            __syncthreads();
+            if (ballr > 0) x = ball_dof_step(S.q, S.dpos, ln - (ballr - 1), ballr);
+        }
+        if (is_dof) {
             qv = x;
             uv = w;
         }
@@ -1569,17 +1607,12 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
         const V3 po = v3(lf[0], lf[1], lf[2]);
         const Q4 qo = q4(lf[3], lf[4], lf[5], lf[6]);
         const V3 ax = v3(lf[7], lf[8], lf[9]);
-        const float qj = dof >= 0 ? S.q[dof] : 0.0f;
-        Q4 qrel = qo;
-        V3 rr = po;
+        Q4 qrel;
+        V3 rr;
+        link_joint(jt, (int)lf[10], po, qo, ax, S.q, dof, qrel, rr);
         SV sj = svzero();
-        if (jt == MG_JOINT_REVOLUTE) {
-            qrel = qmul(qo, q_axis_angle(ax, qj));
-            sj = sv(ax, v3(0.0f, 0.0f, 0.0f));
-        } else if (jt == MG_JOINT_PRISMATIC) {
-            rr = vadd(po, qrot(qo, vscale(ax, qj)));
-            sj = sv(v3(0.0f, 0.0f, 0.0f), ax);
-        }
+        if (jt == MG_JOINT_REVOLUTE) sj = sv(ax, v3(0.0f, 0.0f, 0.0f));
+        else if (jt == MG_JOINT_PRISMATIC) sj = sv(v3(0.0f, 0.0f, 0.0f), ax);
         S.qr[ln] = qrel;
         S.rr[ln] = rr;
         put6(S.xi[ln], sj);

@@ -9,6 +9,7 @@
 // every function here in C with the same order.
 #pragma once
 #include "mg_math.h"
+#include "migym.h"
 
 struct SV { V3 w, v; };
 struct SI { M3 A, B, C; };
@@ -84,4 +85,70 @@ MG_HD Q4 q_axis_angle(V3 a, float th) {
     mg_sincos(ah, &s, &c);
     if (half < 0.0f) s = -s;
     return q4(a.x * s, a.y * s, a.z * s, c);
+}
+
+// ---- spherical (ball) joints in exponential coordinates ---------------------
+// A ball joint's three DOF positions are the rotation vector th of the child
+// joint frame relative to the parent's (test13_camera_spherical_joint.py:
+// 243-256 feeds targets through quat2expcoord), its velocities the relative
+// angular velocity in the child frame. It is packed as three revolute kernel
+// links about x, y, z (include/migym.h MG_LINK_F_N: link_f[10] = 1, 2, 3 is the
+// link's place in the ball): the first link's joint rotation is exp(th), the
+// other two turn by nothing, so the three motion axes are the child frame's
+// x, y, z and the three DOF rates its angular velocity components. No
+// gimbal lock: the coordinates are never Euler angles.
+// Only + - * / and sqrt (correctly rounded on both sides): oracle/migym_oracle.c
+// restates each function op for op.
+MG_HD Q4 q_exp(V3 th) {
+    const float t2 = vdot(th, th);
+    if (!(t2 > 0.0f)) return q4(0.0f, 0.0f, 0.0f, 1.0f);
+    const float t = sqrtf(t2);
+    float s, c;
+    mg_sincos(0.5f * t, &s, &c);
+    const float k = s / t;
+    return q4(th.x * k, th.y * k, th.z * k, c);
+}
+// atan(u) on |u| <= tan(pi/8): odd Taylor series to u^19 (error < 5e-10)
+MG_HD float mg_atan_small(float u) {
+    const float u2 = u * u;
+    float p = 1.0f / 19.0f;
+    p = 1.0f / 17.0f - u2 * p;
+    p = 1.0f / 15.0f - u2 * p;
+    p = 1.0f / 13.0f - u2 * p;
+    p = 1.0f / 11.0f - u2 * p;
+    p = 1.0f / 9.0f - u2 * p;
+    p = 1.0f / 7.0f - u2 * p;
+    p = 1.0f / 5.0f - u2 * p;
+    p = 1.0f / 3.0f - u2 * p;
+    p = 1.0f - u2 * p;
+    return u * p;
+}
+// atan(t) on [0, 1]: atan t = pi/4 + atan((t - 1) / (t + 1)) above tan(pi/8)
+MG_HD float mg_atan01(float t) {
+    if (t > 0.41421356f) return 0.78539816f + mg_atan_small((t - 1.0f) / (t + 1.0f));
+    return mg_atan_small(t);
+}
+// rotation vector of a unit quaternion (the rotation angle in [0, pi])
+MG_HD V3 q_log(Q4 q) {
+    if (q.w < 0.0f) q = q4(-q.x, -q.y, -q.z, -q.w);
+    const float v2 = q.x * q.x + q.y * q.y + q.z * q.z;
+    if (!(v2 > 0.0f)) return v3(0.0f, 0.0f, 0.0f);
+    const float vn = sqrtf(v2);
+    // half angle = atan2(vn, w), vn > 0, w >= 0
+    const float ha = vn <= q.w ? mg_atan01(vn / q.w) : 1.57079633f - mg_atan01(q.w / vn);
+    const float k = (2.0f * ha) / vn;
+    return v3(q.x * k, q.y * k, q.z * k);
+}
+// a ball joint turned by dth (child frame): log(exp(th) exp(dth))
+MG_HD V3 ball_step(V3 th, V3 dth) { return q_log(qnormalize(qmul(q_exp(th), q_exp(dth)))); }
+// link l's joint rotation qrel and offset rr from its origin (po, qo), axis ax
+// and the DOF positions q (indexed by local DOF): revolute, prismatic, or a ball
+// joint's first link (exp of its three DOFs) / later links (no turn)
+MG_HD void link_joint(int jt, int ball, V3 po, Q4 qo, V3 ax, const float* q, int dof, Q4& qrel, V3& rr) {
+    qrel = qo;
+    rr = po;
+    if (ball == 1) qrel = qmul(qo, q_exp(v3(q[dof], q[dof + 1], q[dof + 2])));
+    else if (ball > 1) qrel = qo;
+    else if (jt == MG_JOINT_REVOLUTE) qrel = qmul(qo, q_axis_angle(ax, dof >= 0 ? q[dof] : 0.0f));
+    else if (jt == MG_JOINT_PRISMATIC) rr = vadd(po, qrot(qo, vscale(ax, dof >= 0 ? q[dof] : 0.0f)));
 }

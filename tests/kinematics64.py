@@ -45,7 +45,15 @@ class Articulation:
             p, jt, d = int(self.li[l, 0]), int(self.li[l, 1]), int(self.li[l, 2])
             po, qo, ax = self.lf[l, 0:3], self.lf[l, 3:7], self.lf[l, 7:10]
             qrel, rr = qo.copy(), po.copy()
-            if jt == 1:
+            ball = int(round(self.lf[l, 10]))
+            if ball == 1:           # ball joint: exp of the rotation vector q[d..d+2]
+                th = np.asarray(q[d:d + 3], np.float64)
+                t = np.linalg.norm(th)
+                if t > 0:
+                    qrel = qmul(qo, np.array([*(th / t * np.sin(0.5 * t)), np.cos(0.5 * t)]))
+            elif ball > 1:          # its later links: no turn of their own
+                pass
+            elif jt == 1:
                 s, c = np.sin(0.5 * q[d]), np.cos(0.5 * q[d])
                 qrel = qmul(qo, np.array([ax[0] * s, ax[1] * s, ax[2] * s, c]))
             elif jt == 2:

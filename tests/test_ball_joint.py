@@ -3,13 +3,19 @@
 joints through massless-in-URDF links, one spherical joint to a sphere), the
 DOF state viewed as (num_envs, 6, 1) (test13 :266-269).
 
-A ball joint is three rotation DOFs about its joint frame's x, y, z axes, packed
-as three kernel links (two virtual: no body, no mass; include/migym.h
-MG_LINK_I_N). CPU tests check the oracle's physics against closed-form and
-revolute-joint references (the reference holds no output that exercises a
-spherical joint's dynamics: parity of the DOF coordinates to PhysX is unpinned,
-DESIGN.md §6); `-m gpu` tests check the HIP articulation kernel and the
-Jacobian / mass-matrix kernel against the oracle and float64 kinematics.
+A ball joint's three DOF positions are the rotation vector (exponential
+coordinates) of the child joint frame, as test13 feeds its targets
+(quat2expcoord, :243-256, :298); its velocities the angular velocity in the
+child frame. It is packed as three kernel links about x, y, z (two virtual: no
+body, no mass; include/migym.h MG_LINK_I_N), the first turning by exp(th), and
+integrated on SO(3): th <- log(exp(th) exp(h w)) — no gimbal lock. CPU tests
+check the oracle's physics against the reference's own coordinate conversion,
+closed-form and revolute-joint references and the conserved quantities of a
+conical swing through 90 degrees (the reference holds no output of a spherical
+joint's dynamics: parity with PhysX's integration is unpinned, DESIGN.md §6);
+`-m gpu` tests check the HIP articulation kernel, the coupled per-env kernel
+and the Jacobian / mass-matrix kernel against the oracle and float64
+kinematics.
 """
 import os
 
@@ -143,6 +149,43 @@ def test_mjcf_ball_joint(gym, tmp_path):
     assert A["tmpl_link_i"][:, 3].tolist() == [0, -1, -1, 1]
 
 
+def _quat2expcoord(q):
+    """test13_camera_spherical_joint.py:243-256 (the reference's own conversion of
+    a goal orientation into the spherical joint's DOF targets), restated."""
+    q = np.asarray(q, np.float64)
+    if q[-1] < 0:
+        q = -q
+    theta = 2.0 * np.arctan2(np.linalg.norm(q[:-1]), q[-1])
+    return q[:-1] / (np.sin(theta / 2.0) + 1e-7) * theta
+
+
+def test_dof_positions_are_exponential_coordinates(gym, tmp_path):
+    """test13 drives its spherical joint with dof_positions[3:] =
+    quat2expcoord(goal_quat) (:298): a ball joint set to those positions holds
+    the bob at goal_quat relative to the joint frame — at the host's initial
+    forward kinematics and after a step of the engine (no gravity, no drive) —
+    including rotations by more than 90 degrees about tilted axes."""
+    d = str(tmp_path)
+    rng = np.random.RandomState(4)
+    quats = []
+    for _ in range(6):
+        ax = rng.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        ang = rng.uniform(0.3, 3.0)
+        quats.append(np.array([*(ax * np.sin(0.5 * ang)), np.cos(0.5 * ang)]))
+    sim, _ = _scene(gym, d, len(quats), _urdf(d, "b.urdf"), gravity=0.0,
+                    init=lambda i: (np.r_[0.0, 0.0, 0.0, _quat2expcoord(quats[i])], np.zeros(6)))
+    A = sim.build_model()
+    p, m = sim.mg_params(), sim.mg_model()
+    st, dof = A["body_state0"].copy(), A["dof_state0"].copy()
+    oracle.step(p, m, st, dof)
+    for i, q in enumerate(quats):
+        for s in (A["body_state0"], st):
+            got = s[5 * i + 4, 3:7].astype(np.float64)          # the bob (fixed frame is identity)
+            assert min(np.abs(got - q).max(), np.abs(got + q).max()) < 2e-6
+        assert np.abs(dof[6 * i + 3:6 * i + 6, 0] - _quat2expcoord(q)).max() < 2e-5
+
+
 def test_rest_without_gravity_is_static(gym, tmp_path):
     """test13's setting (gravity 0, no drives): nothing moves, bit for bit."""
     sim, _ = _scene(gym, str(tmp_path), 2, _urdf(str(tmp_path), "b.urdf", bob_com=(0, 0, 0)), gravity=0.0)
@@ -170,10 +213,11 @@ def test_planar_swing_matches_revolute(gym, tmp_path):
     assert abs(dofr[0, 0] - th0) > 0.1                                  # it swung
 
 
-def _conical(gym, d, substeps, frames=240):
-    """Tilt 0.6 about x, rate 2 about the second axis (the joint frame's y turned
-    by the tilt: perpendicular to the pivot-COM line, so the bob moves
-    azimuthally). Returns (max |r - r0|, Lz(end) / Lz(start), energy drift)."""
+def _conical(gym, d, substeps, frames=240, tilt=0.6, rate=2.0):
+    """Tilt about x, angular velocity `rate` about the child frame's y (the joint
+    frame's y turned by the tilt: perpendicular to the pivot-COM line, so the
+    bob moves azimuthally). Returns (max |r - r0|, Lz(end) / Lz(start), energy
+    drift)."""
     sim = _sim(gym, substeps=substeps)
     opts = gymapi.AssetOptions()
     opts.fix_base_link = True
@@ -184,7 +228,7 @@ def _conical(gym, d, substeps, frames=240):
     props["driveMode"][:] = gymapi.DOF_MODE_NONE
     gym.set_actor_dof_properties(env, h, props)
     s0 = np.zeros(3, dtype=gymapi.DofState.dtype)
-    s0["pos"], s0["vel"] = [0.6, 0, 0], [0, 2, 0]
+    s0["pos"], s0["vel"] = [tilt, 0, 0], [0, rate, 0]
     gym.set_actor_dof_states(env, h, s0, gymapi.STATE_ALL)
     A = sim.build_model()
     p, m = sim.mg_params(), sim.mg_model()
@@ -212,15 +256,27 @@ def _conical(gym, d, substeps, frames=240):
 
 def test_spherical_pendulum_invariants(gym, tmp_path):
     """A conical swing: the bob stays on its sphere (the joint holds exactly),
-    and the vertical angular momentum and the energy — both conserved by the
-    continuous dynamics — drift at first order in the step (semi-implicit Euler
-    on the joint coordinates): 4x the substeps, ~1/4 the drift."""
+    and the vertical angular momentum and the energy — conserved by the
+    continuous dynamics — are kept: the joint is integrated on SO(3) in
+    exponential coordinates (th <- log(exp(th) exp(h w))), and the three axes'
+    velocity product is the ball's v_parent x vJ."""
     d = str(tmp_path)
-    dr8, l8, e8 = _conical(gym, d, 8)
-    dr32, l32, e32 = _conical(gym, d, 32)
-    assert dr8 < 1e-5 and dr32 < 1e-5
-    assert abs(l32 - 1.0) < 0.01 and abs(e32) < 0.05
-    assert abs(l32 - 1.0) < 0.35 * abs(l8 - 1.0) and abs(e32) < 0.35 * abs(e8)
+    for ss in (8, 32):
+        dr, lz, de = _conical(gym, d, ss)
+        assert dr < 1e-5
+        assert abs(lz - 1.0) < 1e-3 and abs(de) < 0.01      # 25 J of potential energy at the pivot depth
+
+
+@pytest.mark.parametrize("tilt", [1.4, 1.6, 2.2])
+def test_conical_swing_through_ninety_degrees(gym, tmp_path, tilt):
+    """Swings whose orientation passes and stays beyond 90 degrees from the rest
+    direction (1.6 and 2.2 rad of tilt: the bob above the pivot's horizontal),
+    where a triple-revolute (x-y-z) packing meets gimbal lock: the same
+    invariants hold."""
+    d = str(tmp_path)
+    dr, lz, de = _conical(gym, d, 16, frames=180, tilt=tilt, rate=4.0)
+    assert dr < 5e-5
+    assert abs(lz - 1.0) < 2e-3 and abs(de) < 0.05
 
 
 def _coupled_scene(gym, d, n, gpu=False, seed=0):
