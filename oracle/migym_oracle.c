@@ -32,7 +32,7 @@
 #include "../include/migym.h"
 
 #define OR_MAXC 8
-#define OR_MAXL 16
+#define OR_MAXL 32
 
 typedef struct { float x, y, z; } v3_t;
 typedef struct { float x, y, z, w; } q4_t;
@@ -628,7 +628,8 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
     for (st_ = 0; st_ < P->substeps; ++st_) {
         float tau0d[OR_MAXL], impd[OR_MAXL], mdiag[OR_MAXL];
         static __thread aba_ws_t W;   /* per thread: oracle_step_mt */
-        aba_world_(P, m, LF, LI, L, D, b0, d0, q, qd, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd, 0, ext);
+        aba_world_(P, m, LF, LI, L, D, b0, d0, q, qd, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd, 0, ext,
+                   (L > 16 || D > 16) ? 64 : 16);   /* k_artic_lanes' lane width (mg_env.hip mg_wide) */
         {
             float qn[OR_MAXL], wn[OR_MAXL];
             for (d = 0; d < D; ++d) {

@@ -11,8 +11,8 @@
 
 #define OE_MAXF 2
 #define OE_MAXS 4
-#define OE_MAXCT 16
-#define OE_F0 16
+#define OE_MAXCT 48   /* storage; an env uses MAXCT = 16, or 48 when 64 lanes wide (MG_ENV_MAXCT[_WIDE]) */
+#define OE_F0 64      /* participant ids (mg_internal.h MG_ENV_FREE0 ...) */
 #define OE_PMAX 4
 
 typedef struct { int type; v3_t c; m3_t R; v3_t h; const float* hv; } cshape_t;
@@ -581,9 +581,10 @@ typedef struct {
     int art_body, art_dof, art_tmpl, nf, free_b[OE_MAXF], ns, stat_b[OE_MAXS], mask;
 } oenv_t;
 
-#define OE_G 16
-#define OE_ST0 32
-#define OE_LIM0 64
+#define OE_GM 64      /* lanes of a wide env (mg_env.hip: G = 16, or 64 above 16 links / slots) */
+#define OE_SLOTS 32   /* velocity slots of a wide env (MG_ENV_SLOTS_WIDE) */
+#define OE_ST0 80
+#define OE_LIM0 128
 
 /* sum of 16 slots in the device's DPP order (mg_env.hip red16): row_ror 8,
  * row_ror 4, quad xor 2, quad xor 1; every lane ends with this value */
@@ -596,11 +597,17 @@ static float red16_(const float* v) {
     u1 = t[1] + t[3];
     return u0 + u1;
 }
-static float red16_prod_(const float* a, const float* b) {
-    float v[16];
-    int i;
-    for (i = 0; i < 16; ++i) v[i] = a[i] * b[i];
+/* the same over G = 16 or 64 lanes: G = 64 adds the four rows' sums as
+ * (r0 + r1) + (r2 + r3) (mg_env.hip redg) */
+static float red_(const float* v, int G) {
+    if (G == 64) return (red16_(v) + red16_(v + 16)) + (red16_(v + 32) + red16_(v + 48));
     return red16_(v);
+}
+static float redp_(const float* a, const float* b, int G) {
+    float v[OE_GM];
+    int i;
+    for (i = 0; i < G; ++i) v[i] = a[i] * b[i];
+    return red_(v, G);
 }
 
 typedef struct { int a, sa, b, sb; } epair_t;
@@ -756,7 +763,7 @@ typedef struct {
 static void aba_world_(const step_t* P, const mg_model* m, const float* LF, const int* LI, int L, int D, int b0,
                        int d0, const float* q, const float* u, const float* props, const float* tgt, v3_t x0, q4_t q0,
                        v3_t gw, aba_ws_t* W, float* qdd, float* mdiag, float* tau0d, float* impd, int fb,
-                       const float* ext) {
+                       const float* ext, int G) {
     const float h = P->h;
     q4_t* ql = W->ql; q4_t* qrl = W->qrl;
     v3_t* xl = W->xl; v3_t* zl = W->zl; v3_t* rrl = W->rrl;
@@ -917,9 +924,9 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
                 float a6[6];
                 for (i = 0; i < 6; ++i) a6[i] = va[p][i] + ccv[l][i];
                 if (dj >= 0) {
-                    float t16[16], acc;
-                    for (i = 0; i < 16; ++i) t16[i] = i < 6 ? Ua[l][i] * a6[i] : 0.0f;
-                    acc = (uu[l] - red16_(t16)) / Dd[l];
+                    float t16[OE_GM], acc;
+                    for (i = 0; i < OE_GM; ++i) t16[i] = i < 6 ? Ua[l][i] * a6[i] : 0.0f;
+                    acc = (uu[l] - red_(t16, G)) / Dd[l];
                     for (i = 0; i < 6; ++i) a6[i] = a6[i] + xi[l][i] * acc;
                     qdd[dj] = acc;
                 }
@@ -956,7 +963,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     v3_t x0 = V(0.0f, 0.0f, 0.0f), gw = V(0.0f, 0.0f, 0.0f);
     q4_t q0 = Q(0.0f, 0.0f, 0.0f, 1.0f);
     /* slots */
-    float q[OE_G], u[OE_G], dp[OE_G], qdd[OE_G], mdiag[OE_G], tau0d[OE_G], impd[OE_G];
+    float q[OE_GM], u[OE_GM], dp[OE_GM], qdd[OE_GM], mdiag[OE_GM], tau0d[OE_GM], impd[OE_GM];
     /* links */
     static __thread aba_ws_t W;   /* per thread: oracle_step_mt */
     v3_t* xl = W.xl; v3_t* zl = W.zl; q4_t* ql = W.ql;
@@ -964,9 +971,10 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     sv_t vl[OR_MAXL];
     float (*Iw)[36] = W.Iw;
     float (*xi)[6] = W.xi;
-    int amask[OR_MAXL], dlink[OE_G], drev[OE_G];
-    static __thread float Lc[OE_G][OE_G], Mi[OE_G][OE_G];
-    float invd[OE_G];
+    unsigned amask[OR_MAXL];
+    int dlink[OE_GM], drev[OE_GM];
+    static __thread float Lc[OE_SLOTS][OE_SLOTS], Mi[OE_SLOTS][OE_SLOTS];
+    float invd[OE_SLOTS];
     /* free bodies */
     v3_t fx[OE_MAXF], fxc[OE_MAXF], fcom[OE_MAXF], finvI[OE_MAXF], fext[OE_MAXF], text[OE_MAXF], fsum[OE_MAXF];
     q4_t fq[OE_MAXF], fiq[OE_MAXF];
@@ -976,12 +984,15 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     int ca[OE_MAXCT], cb[OE_MAXCT];
     v3_t cp[OE_MAXCT], cd[OE_MAXCT][3];
     float cs0[OE_MAXCT], cmu[OE_MAXCT], ce[OE_MAXCT], cvn0[OE_MAXCT], ck[OE_MAXCT][3], clam[OE_MAXCT][3];
-    static __thread float Jr[OE_MAXCT * 3][OE_G], Wr[OE_MAXCT * 3][OE_G];
+    static __thread float Jr[OE_MAXCT * 3][OE_GM], Wr[OE_MAXCT * 3][OE_GM];
     int d, l, k, c, i, j, st_, it;
-    if (L > OR_MAXL || NS + 6 * nfr > OE_G || nfr > OE_MAXF) return -1;
+    /* lanes: 16, or 64 for an env of more than 16 links / velocity slots (migym_capi.cpp groups) */
+    const int G = (L > 16 || NS + 6 * nfr > 16) ? 64 : 16;
+    const int MAXCT = G == 64 ? 48 : 16;
+    if (L > OR_MAXL || NS + 6 * nfr > OE_SLOTS || nfr > OE_MAXF) return -1;
     npair = env_pairs_(m, ev, P->ground, L, fb, pairs, OE_MAXPAIRS);
     if (npair > OE_MAXPAIRS) return -1;
-    for (i = 0; i < OE_G; ++i) { q[i] = 0.0f; u[i] = 0.0f; dp[i] = 0.0f; }
+    for (i = 0; i < OE_GM; ++i) { q[i] = 0.0f; u[i] = 0.0f; dp[i] = 0.0f; }
     if (L > 0) {
         const float* s0 = state + (size_t)b0 * MG_STATE_N;
         const float grav_on = m->tmpl_body_f[(size_t)m->body_tmpl[b0] * MG_TBODY_F_N + 4];
@@ -991,7 +1002,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     }
     for (l = 0; l < L; ++l) {
         const int p = LI[l * MG_LINK_I_N + 0], dj = LI[l * MG_LINK_I_N + 2];
-        amask[l] = (p >= 0 ? amask[p] : 0) | (dj >= 0 ? (1 << dj) : 0);
+        amask[l] = (p >= 0 ? amask[p] : 0u) | (dj >= 0 ? (1u << dj) : 0u);
         if (dj >= 0) { dlink[dj] = l; drev[dj] = LI[l * MG_LINK_I_N + 1] == MG_JOINT_REVOLUTE ? 1 : 0; }
         lsum[l] = V(0.0f, 0.0f, 0.0f);
     }
@@ -1034,7 +1045,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         int nct = 0, link_rows = 0;
         /* ---- 1. unconstrained motion: world-frame ABA about x0 (mg_env.hip aba_world) */
         if (L > 0) aba_world_(P, m, LF, LI, L, D, b0, d0, q, u, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd, fb,
-                              ext);
+                              ext, G);
         for (k = 0; k < nfr; ++k) {
             const int s0 = NS + 6 * k;
             const s3_t Iw = sym_rdrt_(qmat_(qmul_(fq[k], fiq[k])), finvI[k]);
@@ -1061,7 +1072,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             u[d] = w;
         }
         for (d = D; d < NS; ++d) u[d] = W.ru[d - D];
-        for (i = 0; i < OE_G; ++i) dp[i] = 0.0f;
+        for (i = 0; i < OE_GM; ++i) dp[i] = 0.0f;
 
         /* ---- 2. narrow phase, pair order */
         for (i = 0; i < npair; ++i) {
@@ -1101,7 +1112,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 rest = 0.5f * (sha[12] + shb[12]);
             }
             for (j = 0; j < o.n; ++j) {
-                if (nct < OE_MAXCT) {
+                if (nct < MAXCT) {
                     ca[nct] = pp->a;
                     cb[nct] = pp->b;
                     cp[nct] = o.p[j];
@@ -1125,7 +1136,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 const float mg = 0.05f * (hi - lo);
                 if (q1 - lo < mg || hi - q1 < mg) {
                     const int sgn = (q1 - lo) < (hi - q1) ? 1 : -1;
-                    if (nct < OE_MAXCT) {
+                    if (nct < MAXCT) {
                         ca[nct] = OE_LIM0 + d;
                         cb[nct] = sgn;
                         cp[nct] = V(0.0f, 0.0f, 0.0f);
@@ -1208,12 +1219,12 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 float* J = Jr[c * 3 + rw];
                 float* W = Wr[c * 3 + rw];
                 int ln;
-                for (ln = 0; ln < OE_G; ++ln) {
+                for (ln = 0; ln < G; ++ln) {
                     float Jv = 0.0f, Wv = 0.0f;
                     if (a >= OE_LIM0) {
                         if (rw == 0 && ln == a - OE_LIM0) Jv = (float)b;
                     } else if (ln < D) {
-                        if (a < OE_F0 && ((amask[a] >> ln) & 1)) {
+                        if (a < OE_F0 && ln < 32 && ((amask[a] >> ln) & 1u)) {
                             const int jl = dlink[ln];
                             Jv = drev[ln] ? dot3(cross3(zl[jl], sub3(p, xl[jl])), dir) : dot3(zl[jl], dir);
                         }
@@ -1247,12 +1258,12 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     }
                 }
                 {
-                    const float den = red16_prod_(J, W);
+                    const float den = redp_(J, W, G);
                     ck[c][rw] = den > 0.0f ? 1.0f / den : 0.0f;
                 }
                 clam[c][rw] = 0.0f;
             }
-            cvn0[c] = red16_prod_(Jr[c * 3], u);
+            cvn0[c] = redp_(Jr[c * 3], u, G);
         }
 
         /* ---- 4. TGS */
@@ -1260,7 +1271,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             const int pos = it < P->npos;
             int ln;
             for (c = 0; c < nct; ++c) {
-                const float s = cs0[c] + red16_prod_(Jr[c * 3], dp);
+                const float s = cs0[c] + redp_(Jr[c * 3], dp, G);
                 float tg, lam, dl, nl;
                 if (pos) {
                     tg = -s * P->inv_sub;
@@ -1270,10 +1281,10 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     if (ce[c] > 0.0f && cvn0[c] < -P->bounce) tg = fmaxf(tg, -ce[c] * cvn0[c]);
                 }
                 lam = clam[c][0];
-                dl = ck[c][0] * (tg - red16_prod_(Jr[c * 3], u));
+                dl = ck[c][0] * (tg - redp_(Jr[c * 3], u, G));
                 nl = fmaxf(lam + dl, 0.0f);
                 dl = nl - lam;
-                for (ln = 0; ln < OE_G; ++ln) u[ln] = u[ln] + Wr[c * 3][ln] * dl;
+                for (ln = 0; ln < G; ++ln) u[ln] = u[ln] + Wr[c * 3][ln] * dl;
                 clam[c][0] = nl;
             }
             for (c = 0; c < nct; ++c) {
@@ -1281,19 +1292,19 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 int rw;
                 for (rw = 1; rw < 3; ++rw) {
                     const float lam = clam[c][rw];
-                    const float nl = fminf(fmaxf(lam - ck[c][rw] * red16_prod_(Jr[c * 3 + rw], u), -lim), lim);
+                    const float nl = fminf(fmaxf(lam - ck[c][rw] * redp_(Jr[c * 3 + rw], u, G), -lim), lim);
                     const float dl = nl - lam;
-                    for (ln = 0; ln < OE_G; ++ln) u[ln] = u[ln] + Wr[c * 3 + rw][ln] * dl;
+                    for (ln = 0; ln < G; ++ln) u[ln] = u[ln] + Wr[c * 3 + rw][ln] * dl;
                     clam[c][rw] = nl;
                 }
             }
             if (pos)
-                for (ln = 0; ln < OE_G; ++ln) dp[ln] = dp[ln] + u[ln] * P->sub;
+                for (ln = 0; ln < G; ++ln) dp[ln] = dp[ln] + u[ln] * P->sub;
         }
 
         /* ---- 5. integrate */
         {
-            float qn[OE_G];
+            float qn[OE_GM];
             for (d = 0; d < D; ++d) {
                 const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
                 const float maxv = pr[4];

@@ -54,42 +54,51 @@ extern "C" int mg_debug_env_phase_reset(void) {
 
 namespace {
 
-constexpr int G = MG_ENV_G;
-constexpr int EPW = 64 / G;           // envs per wavefront
-constexpr int MAXCT = MG_ENV_MAXCT;
+// G: lanes per env, a template parameter of the kernels: 16 (4 envs per
+// wavefront, DPP row reductions) or 64 (one env per wavefront: articulations of
+// more than 16 links or velocity slots, the MJCF humanoid's 25 links and 27
+// slots; reductions by row, then readlane across the four rows)
+constexpr int G16 = MG_ENV_G;
+// contacts per env per substep: 16, or 48 in a 64-lane env (a humanoid on the
+// ground has ~35 capsule end caps; the rows then live partly in scratch)
+template <int G>
+constexpr int maxct() { return G == 64 ? MG_ENV_MAXCT_WIDE : MG_ENV_MAXCT; }
 constexpr int MAXF = MG_ENV_MAXF;
 constexpr int F0 = MG_ENV_FREE0;
 constexpr int ST0 = MG_ENV_STATIC0;
 constexpr int LIM0 = MG_ENV_LIMIT0;
 constexpr int NPB = 64;               // candidate pairs per screening block
 
+template <int MAXL, int G>
 struct EnvLds {
+    static constexpr int NDM = G > 32 ? 32 : G;   // velocity slots of the M_eff solve
+    static constexpr int MAXCT = maxct<G>();
     float q[G], u[G], qdd[G], dpos[G], mdiag[G];
-    V3 xl[MG_MAX_LINKS], zl[MG_MAX_LINKS];
-    Q4 ql[MG_MAX_LINKS];
-    int amask[MG_MAX_LINKS];         // DOF bits of the joints on the path root -> l
+    V3 xl[MAXL], zl[MAXL];
+    Q4 ql[MAXL];
+    unsigned amask[MAXL];            // DOF bits of the joints on the path root -> l
     int dlink[G];                    // link whose joint is DOF d
     int drev[G];                     // DOF d is revolute
     V3 fx[MAXF], fxc[MAXF];
     Q4 fq[MAXF];
     float finvm[MAXF];
     S3 fIw[MAXF];
-    float Lc[G][G];                  // M_eff, assembled by the DOF lanes
+    float Lc[NDM][NDM];              // M_eff, assembled by the DOF lanes
     int ca[MAXCT], cb[MAXCT];
     V3 cp[MAXCT], cd[MAXCT][3];      // point, (n, t1, t2)
     float cs0[MAXCT], cmu[MAXCT], ce[MAXCT], cvn0[MAXCT];
     float ck[MAXCT][3], clam[MAXCT][3];
     int nct, link_rows;
     // world-frame articulated-body quantities (about the base origin x0)
-    float Iw[MG_MAX_LINKS][36];      // spatial inertia -> articulated / composite inertia, row-major 6x6
-    float xi[MG_MAX_LINKS][6];       // joint motion axis (w, v at x0)
-    float va[MG_MAX_LINKS][6];       // link velocity, then acceleration
-    float cc[MG_MAX_LINKS][6];       // velocity-product acceleration
-    float pa[MG_MAX_LINKS][6];       // bias force
-    float Ua[MG_MAX_LINKS][6];       // IA xi
-    float Dd[MG_MAX_LINKS], uu[MG_MAX_LINKS];
-    Q4 qr[MG_MAX_LINKS];             // joint rotation / offset relative to the parent
-    V3 rr[MG_MAX_LINKS];
+    float Iw[MAXL][36];              // spatial inertia -> articulated / composite inertia, row-major 6x6
+    float xi[MAXL][6];               // joint motion axis (w, v at x0)
+    float va[MAXL][6];               // link velocity, then acceleration
+    float cc[MAXL][6];               // velocity-product acceleration
+    float pa[MAXL][6];               // bias force
+    float Ua[MAXL][6];               // IA xi
+    float Dd[MAXL], uu[MAXL];
+    Q4 qr[MAXL];                     // joint rotation / offset relative to the parent
+    V3 rr[MAXL];
     float tau0[G], imp[G], arm[G];
     float ru[6];                     // floating root: (w, v_O) after the unconstrained update
     int npl[NPB];                    // candidate pairs that passed the screen
@@ -110,6 +119,17 @@ __device__ __forceinline__ float red16(float v) {
     v = v + dpp<0xB1>(v);    // quad_perm [1,0,3,2]
     return v;
 }
+// the same over a G-lane env: G = 64 adds the four row sums read lane by lane,
+// (r0 + r1) + (r2 + r3) (oracle: red_)
+__device__ __forceinline__ float rdlane(float v, int k) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+template <int G>
+__device__ __forceinline__ float redg(float v) {
+    v = red16(v);
+    if constexpr (G == 64) return (rdlane(v, 0) + rdlane(v, 16)) + (rdlane(v, 32) + rdlane(v, 48));
+    return v;
+}
 // lane k of the 16-lane row, to every lane of the row (DPP row_newbcast:k,
 // a VALU operand modifier on gfx950: no LDS round trip). k must fold to a
 // constant (fully unrolled loops).
@@ -124,6 +144,12 @@ __device__ __forceinline__ float bcast16(float v, int k) {
     case 12: return dpp<0x15C>(v); case 13: return dpp<0x15D>(v);
     case 14: return dpp<0x15E>(v); default: return dpp<0x15F>(v);
     }
+}
+// lane k of the env to every lane of it (G = 64: readlane, k wave-uniform)
+template <int G>
+__device__ __forceinline__ float bcastg(float v, int k) {
+    if constexpr (G == 64) return rdlane(v, k);
+    return bcast16(v, k);
 }
 
 // ---- cooperative convex-convex narrow phase ---------------------------------
@@ -166,33 +192,61 @@ __device__ __forceinline__ void minkey_step(float& s, int& id) {
     const int i2 = dppi<CTRL>(id);
     if (s2 < s || (s2 == s && i2 < id)) { s = s2; id = i2; }
 }
-// the smallest (s, id) of the 16-lane row, in every lane of the row
+// the smallest (s, id) of the env's lanes, in every lane (G = 64: the rows'
+// minima read lane by lane; min with ties by id is order-free)
+template <int G>
 __device__ __forceinline__ void grp_minkey(float& s, int& id) {
     minkey_step<0x128>(s, id);   // row_ror:8
     minkey_step<0x124>(s, id);   // row_ror:4
     minkey_step<0x4E>(s, id);    // quad_perm [2,3,0,1]
     minkey_step<0xB1>(s, id);    // quad_perm [1,0,3,2]
+    if constexpr (G == 64) {
+        float bs = rdlane(s, 0);
+        int bi = __builtin_amdgcn_readlane(id, 0);
+#pragma unroll
+        for (int r = 16; r < 64; r += 16) {
+            const float s2 = rdlane(s, r);
+            const int i2 = __builtin_amdgcn_readlane(id, r);
+            if (s2 < bs || (s2 == bs && i2 < bi)) { bs = s2; bi = i2; }
+        }
+        s = bs;
+        id = bi;
+    }
 }
 template <int CTRL>
 __device__ __forceinline__ void bounds_step(V3& lo, V3& hi) {
     lo = v3(fminf(lo.x, dpp<CTRL>(lo.x)), fminf(lo.y, dpp<CTRL>(lo.y)), fminf(lo.z, dpp<CTRL>(lo.z)));
     hi = v3(fmaxf(hi.x, dpp<CTRL>(hi.x)), fmaxf(hi.y, dpp<CTRL>(hi.y)), fmaxf(hi.z, dpp<CTRL>(hi.z)));
 }
-// vertex bounds over the row (min / max are exact: order-free)
+// vertex bounds over the env's lanes (min / max are exact: order-free)
+template <int G>
 __device__ __forceinline__ void grp_bounds(V3& lo, V3& hi) {
     bounds_step<0x128>(lo, hi);
     bounds_step<0x124>(lo, hi);
     bounds_step<0x4E>(lo, hi);
     bounds_step<0xB1>(lo, hi);
+    if constexpr (G == 64) {
+        V3 l = lo, h = hi;
+#pragma unroll
+        for (int r = 16; r < 64; r += 16) {
+            l = v3(fminf(l.x, rdlane(lo.x, r)), fminf(l.y, rdlane(lo.y, r)), fminf(l.z, rdlane(lo.z, r)));
+            h = v3(fmaxf(h.x, rdlane(hi.x, r)), fmaxf(h.y, rdlane(hi.y, r)), fmaxf(h.z, rdlane(hi.z, r)));
+        }
+        lo = v3(rdlane(l.x, 0), rdlane(l.y, 0), rdlane(l.z, 0));
+        hi = v3(rdlane(h.x, 0), rdlane(h.y, 0), rdlane(h.z, 0));
+    }
 }
-__device__ __forceinline__ unsigned grp_ballot(bool b, int gi) {
-    return (unsigned)((__ballot(b) >> (gi * G)) & 0xFFFFull);
+// ballot of the env's lanes (bit ln)
+template <int G>
+__device__ __forceinline__ unsigned long long grp_ballot(bool b, int gi) {
+    if constexpr (G == 64) return __ballot(b);
+    return (__ballot(b) >> (gi * G)) & 0xFFFFull;
 }
 // X's edges against Y on the group, into each lane's queue (order = edge index).
 // A lane's edges (e = ln + 16 k, at most 3 MG_HULL_MAX_VERTS / 16 = 6) in two
 // batches of 3: all the batch's edge ids, then all its endpoints are loaded
 // before any is tested (two dependent round trips per batch, not two per edge)
-constexpr int CE_PER_LANE = (3 * MG_HULL_MAX_VERTS + G - 1) / G;
+template <int G>
 __device__ __forceinline__ void coop_edges(const CShape& X, const CShape& Y, float margin, bool onY, V3 lo, V3 hi,
                                            int ln, CandQ& Q) {
     V3 t;
@@ -200,6 +254,7 @@ __device__ __forceinline__ void coop_edges(const CShape& X, const CShape& Y, flo
     float ry;
     if (!cvx_edges_gate(X, Y, margin, lo, hi, t, M, ry)) return;
     const int ne = cvx_ne(X);
+    constexpr int CE_PER_LANE = (3 * MG_HULL_MAX_VERTS + G - 1) / G;
 #pragma unroll
     for (int k0 = 0; k0 < CE_PER_LANE; k0 += 3) {
         if (ln + G * k0 >= ne) break;
@@ -229,6 +284,7 @@ __device__ __forceinline__ void coop_edges(const CShape& X, const CShape& Y, flo
 }
 // X's vertices (i = ln + 16 k, at most 2 per lane) against Y's planes, into the
 // lane's queue (order idbase + i); both vertices loaded before either is tested
+template <int G>
 __device__ __forceinline__ void coop_vertices(const CShape& X, const CShape& Y, float margin, bool onY, int idbase,
                                               int ln, CandQ& Q, V3& lo, V3& hi) {
     const int nv = cvx_nv(X);
@@ -255,6 +311,7 @@ __device__ __forceinline__ void coop_vertices(const CShape& X, const CShape& Y, 
     }
 }
 // every lane of the group calls it with the same pair (group-uniform control)
+template <int G>
 __device__ void coop_convex_convex(const CShape& A, const CShape& B, float margin, int ln, int gi, PairOut& o) {
 #ifdef MG_ENV_PHASE_TIMING
     unsigned long long ph_sub = clock64();
@@ -262,18 +319,19 @@ __device__ void coop_convex_convex(const CShape& A, const CShape& B, float margi
     CandQ Q;
     Q.n = 0;
     V3 loA = v3(1e30f, 1e30f, 1e30f), hiA = v3(-1e30f, -1e30f, -1e30f), loB = loA, hiB = hiA;
-    coop_vertices(A, B, margin, false, 0, ln, Q, loA, hiA);     // A's vertices by B's planes
-    coop_vertices(B, A, margin, true, 64, ln, Q, loB, hiB);     // B's vertices by A's planes
+    coop_vertices<G>(A, B, margin, false, 0, ln, Q, loA, hiA);     // A's vertices by B's planes
+    coop_vertices<G>(B, A, margin, true, 64, ln, Q, loB, hiB);     // B's vertices by A's planes
     PH_SUB(12);
-    if (grp_ballot(Q.n > 0, gi) == 0u) {
+    if (grp_ballot<G>(Q.n > 0, gi) == 0ull) {
         // no vertex candidate: edge crossings (convex_convex's order of passes)
-        grp_bounds(loA, hiA);
-        grp_bounds(loB, hiB);
+        grp_bounds<G>(loA, hiA);
+        grp_bounds<G>(loB, hiB);
         if (A.type == MG_SHAPE_BOX && B.type != MG_SHAPE_BOX) {
-            coop_edges(B, A, margin, true, loB, hiB, ln, Q);
+            coop_edges<G>(B, A, margin, true, loB, hiB, ln, Q);
         } else {
-            coop_edges(A, B, margin, false, loA, hiA, ln, Q);
-            if (B.type != MG_SHAPE_BOX && grp_ballot(Q.n > 0, gi) == 0u) coop_edges(B, A, margin, true, loB, hiB, ln, Q);
+            coop_edges<G>(A, B, margin, false, loA, hiA, ln, Q);
+            if (B.type != MG_SHAPE_BOX && grp_ballot<G>(Q.n > 0, gi) == 0ull)
+                coop_edges<G>(B, A, margin, true, loB, hiB, ln, Q);
         }
         PH_COUNT(15, 1);
     }
@@ -282,36 +340,38 @@ __device__ void coop_convex_convex(const CShape& A, const CShape& B, float margi
     o.n = 0;
 #pragma unroll
     for (int r = 0; r < MG_PAIR_MAXC; ++r) {
-        if (grp_ballot(Q.n > 0, gi) == 0u) break;     // group-uniform: nothing left
+        if (grp_ballot<G>(Q.n > 0, gi) == 0ull) break;     // group-uniform: nothing left
         float s = Q.n > 0 ? Q.s[0] : 3.0e38f;
         int id = Q.n > 0 ? Q.id[0] : 0x7fffffff;
-        grp_minkey(s, id);
-        const unsigned m = grp_ballot(Q.n > 0 && Q.id[0] == id, gi);
-        const int owner = m ? __ffs(m) - 1 : 0;
+        grp_minkey<G>(s, id);
+        const unsigned long long m = grp_ballot<G>(Q.n > 0 && Q.id[0] == id, gi);
+        const int owner = m ? __ffsll(m) - 1 : 0;
         const V3 p = v3(__shfl(Q.p[0].x, owner, G), __shfl(Q.p[0].y, owner, G), __shfl(Q.p[0].z, owner, G));
         const V3 n = v3(__shfl(Q.nrm[0].x, owner, G), __shfl(Q.nrm[0].y, owner, G), __shfl(Q.nrm[0].z, owner, G));
-        if (m != 0u && ln == owner) {           // pop the head
+        if (m != 0ull && ln == owner) {         // pop the head
 #pragma unroll
             for (int k = 0; k + 1 < MG_PAIR_MAXC; ++k) {
                 Q.s[k] = Q.s[k + 1]; Q.id[k] = Q.id[k + 1]; Q.p[k] = Q.p[k + 1]; Q.nrm[k] = Q.nrm[k + 1];
             }
             Q.n = Q.n - 1;
         }
-        if (m != 0u) pair_push(o, p, n, s);
+        if (m != 0ull) pair_push(o, p, n, s);
     }
     PH_SUB(14);
 }
 // lane k's placed shape, to every lane of the group (ds_bpermute: no global
 // round trips for the pair record, the shape rows and the poses)
+template <int G>
 __device__ __forceinline__ V3 shfl3(V3 v, int k) { return v3(__shfl(v.x, k, G), __shfl(v.y, k, G), __shfl(v.z, k, G)); }
+template <int G>
 __device__ __forceinline__ CShape shfl_shape(const CShape& c, int k) {
     CShape r;
     r.type = __shfl(c.type, k, G);
-    r.c = shfl3(c.c, k);
-    r.R.c0 = shfl3(c.R.c0, k);
-    r.R.c1 = shfl3(c.R.c1, k);
-    r.R.c2 = shfl3(c.R.c2, k);
-    r.h = shfl3(c.h, k);
+    r.c = shfl3<G>(c.c, k);
+    r.R.c0 = shfl3<G>(c.R.c0, k);
+    r.R.c1 = shfl3<G>(c.R.c1, k);
+    r.R.c2 = shfl3<G>(c.R.c2, k);
+    r.h = shfl3<G>(c.h, k);
     const unsigned long long hp = (unsigned long long)(uintptr_t)c.hv;
     const unsigned lo = __shfl((unsigned)(hp & 0xFFFFFFFFull), k, G), hi = __shfl((unsigned)(hp >> 32), k, G);
     r.hv = (const float*)(uintptr_t)(((unsigned long long)hi << 32) | lo);
@@ -352,7 +412,8 @@ struct FreeC {
 };
 
 // pose of a pair participant: link l (< F0), free body F0 + k, static body ST0 + s
-__device__ __forceinline__ void pair_pose(const EnvLds& S, int id, V3& x, Q4& q) {
+template <class SL>
+__device__ __forceinline__ void pair_pose(const SL& S, int id, V3& x, Q4& q) {
     if (id >= ST0) { x = S.sx[id - ST0]; q = S.sq[id - ST0]; }
     else if (id >= F0) { x = S.fx[id - F0]; q = S.fq[id - F0]; }
     else { x = S.xl[id]; q = S.ql[id]; }
@@ -522,8 +583,8 @@ MG_HD void spd6_solve(const float* M, const float* b, float* x) {
 // aba_refresh restores the world inertias and bias forces the previous inward
 // pass accumulated into, and the link velocities its outward pass overwrote
 // (recomputed: the same values bit for bit).
-template <int MAXL>
-__device__ __forceinline__ void aba_vp(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0,
+template <int MAXL, int G>
+__device__ __forceinline__ void aba_vp(const MgEnvArgs& A, EnvLds<MAXL, G>& S, bool act, int ln, int LA, V3 x0,
                                        const LinkC& lk, int b0) {
     // ---- velocity-product terms (lane l)
     if (act && ln < LA) {
@@ -563,8 +624,8 @@ __device__ __forceinline__ void aba_vp(const MgEnvArgs& A, EnvLds& S, bool act, 
 // link velocities (lanes 0..5, one component each) from the joint speeds: the
 // outward pass of aba_dyn leaves accelerations in S.va, so a re-solve
 // recomputes them before its velocity-product terms
-template <int MAXL>
-__device__ __forceinline__ void aba_vel(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA) {
+template <int MAXL, int G>
+__device__ __forceinline__ void aba_vel(const MgEnvArgs& A, EnvLds<MAXL, G>& S, bool act, int ln, int LA) {
     const bool fb = A.floating != 0;
     const int DA = A.ndof;
     if (act && ln < 6) {
@@ -578,8 +639,8 @@ __device__ __forceinline__ void aba_vel(const MgEnvArgs& A, EnvLds& S, bool act,
     __syncthreads();
 }
 
-template <int MAXL>
-__device__ __forceinline__ void aba_kin(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0,
+template <int MAXL, int G>
+__device__ __forceinline__ void aba_kin(const MgStep& P, const MgEnvArgs& A, EnvLds<MAXL, G>& S, bool act, int ln, int LA, V3 x0,
                                         Q4 q0, const LinkC& lk, int b0) {
     // ---- joint transforms (lane l)
     if (act && ln < LA && ln > 0) {
@@ -628,20 +689,20 @@ __device__ __forceinline__ void aba_kin(const MgStep& P, const MgEnvArgs& A, Env
         world_inertia(lk, S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
     }
     __syncthreads();
-    aba_vel<MAXL>(A, S, act, ln, LA);
-    aba_vp<MAXL>(A, S, act, ln, LA, x0, lk, b0);
+    aba_vel<MAXL, G>(A, S, act, ln, LA);
+    aba_vp<MAXL, G>(A, S, act, ln, LA, x0, lk, b0);
 }
 
-template <int MAXL>
-__device__ __forceinline__ void aba_refresh(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0,
+template <int MAXL, int G>
+__device__ __forceinline__ void aba_refresh(const MgEnvArgs& A, EnvLds<MAXL, G>& S, bool act, int ln, int LA, V3 x0,
                                             const LinkC& lk, int b0) {
     if (act && ln < LA) world_inertia(lk, S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
-    aba_vel<MAXL>(A, S, act, ln, LA);
-    aba_vp<MAXL>(A, S, act, ln, LA, x0, lk, b0);
+    aba_vel<MAXL, G>(A, S, act, ln, LA);
+    aba_vp<MAXL, G>(A, S, act, ln, LA, x0, lk, b0);
 }
 
-template <int MAXL>
-__device__ __forceinline__ void aba_dyn(const MgStep& P, const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, V3 x0,
+template <int MAXL, int G>
+__device__ __forceinline__ void aba_dyn(const MgStep& P, const MgEnvArgs& A, EnvLds<MAXL, G>& S, bool act, int ln, int LA, V3 x0,
                                         V3 gw, const DofC& dc, bool is_dof, bool xm, bool xp, int b0) {
     const float h = P.h;
     const bool fb = A.floating != 0;
@@ -742,7 +803,7 @@ __device__ __forceinline__ void aba_dyn(const MgStep& P, const MgEnvArgs& A, Env
         float a = 0.0f;
         if (act && ln < 6) a = S.va[p][ln] + S.cc[l][ln];
         if (dof >= 0) {
-            const float t = red16(act && ln < 6 ? S.Ua[l][ln] * a : 0.0f);
+            const float t = redg<G>(act && ln < 6 ? S.Ua[l][ln] * a : 0.0f);
             if (act) {
                 const float acc = (S.uu[l] - t) / S.Dd[l];
                 if (ln < 6) a = a + S.xi[l][ln] * acc;
@@ -764,8 +825,8 @@ __device__ __forceinline__ void aba_dyn(const MgStep& P, const MgEnvArgs& A, Env
 // Called by every lane; `act` selects the envs that work. ND: static bound on D.
 // Floating base: the root slots DA..DA+5 (unit spatial axes at x0) extend the
 // matrix to NA = DA + 6: M[root r][root c] = IC_0[r][c], M[d][root r] = (IC_l xi_l)[r].
-template <int MAXL, int ND>
-__device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool act, int ln, int LA, int DA, V3 x0, const LinkC& lk,
+template <int MAXL, int ND, int G>
+__device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds<MAXL, G>& S, bool act, int ln, int LA, int DA, V3 x0, const LinkC& lk,
                            float (&mcol)[ND]) {
     const bool fb = A.floating != 0;
     const int NA = fb ? DA + 6 : DA;
@@ -815,7 +876,7 @@ __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool a
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
         if (j < NA) {
-            const float dj = bcast16(sqrtf(a[j]), j);
+            const float dj = bcastg<G>(sqrtf(a[j]), j);
             invd[j] = 1.0f / dj;
             if (ln == j) a[j] = dj;
             else if (ln > j) a[j] = a[j] * invd[j];
@@ -823,7 +884,7 @@ __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool a
 #pragma unroll
             for (int k = j + 1; k < ND; ++k)
                 if (k < NA) {
-                    const float lk = bcast16(col, k);        // L[k][j]
+                    const float lk = bcastg<G>(col, k);        // L[k][j]
                     if (ln >= k) a[k] = a[k] - col * lk;
                 }
         }
@@ -834,7 +895,7 @@ __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool a
         if (i < NA) {
             float t = i == ln ? 1.0f : 0.0f;
 #pragma unroll
-            for (int k = 0; k < i; ++k) t = t - bcast16(a[k], i) * mcol[k];
+            for (int k = 0; k < i; ++k) t = t - bcastg<G>(a[k], i) * mcol[k];
             mcol[i] = t * invd[i];
         }
     }
@@ -844,7 +905,7 @@ __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool a
             float t = mcol[i];
 #pragma unroll
             for (int k = i + 1; k < ND; ++k)
-                if (k < NA) t = t - bcast16(a[i], k) * mcol[k];
+                if (k < NA) t = t - bcastg<G>(a[i], k) * mcol[k];
             mcol[i] = t * invd[i];
         }
     }
@@ -854,7 +915,7 @@ __device__ __forceinline__ void meff_world(const MgEnvArgs& A, EnvLds& S, bool a
 // LDS for the whole kernel: the serial loops of the kinematic scan and the
 // inward / outward passes read them per link, and from HBM / L2 every such read
 // was a dependent round trip on the critical path (S2: ~4 us of a 24.9 us step).
-template <int MAXL>
+template <int MAXL, int G>
 __device__ __forceinline__ void stage_links(MgEnvArgs& A) {
     __shared__ float s_lf[MAXL * MG_LINK_F_N];
     __shared__ int s_li[MAXL * MG_LINK_I_N];
@@ -866,15 +927,17 @@ __device__ __forceinline__ void stage_links(MgEnvArgs& A) {
     A.link_i = s_li;
 }
 
-template <int MAXL>
+template <int MAXL, int G>
 __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
-    __shared__ EnvLds shm[EPW];
-    stage_links<MAXL>(A);
+    constexpr int EPW = 64 / G;          // envs per wavefront
+    constexpr int MAXCT = maxct<G>();
+    __shared__ EnvLds<MAXL, G> shm[EPW];
+    stage_links<MAXL, G>(A);
     const int gi = threadIdx.x / G;
     const int ln = threadIdx.x % G;
     const int e = blockIdx.x * EPW + gi;
     const bool live = e < A.ne;
-    EnvLds& S = shm[gi];
+    EnvLds<MAXL, G>& S = shm[gi];
     const int* ei = A.env_i + (size_t)(live ? e : 0) * MG_ENV_I_N;
     const int b0 = ei[0], d0 = ei[1];
     const int nfr = live ? ei[2] : 0;
@@ -920,7 +983,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         for (int l = 0; l < L; ++l) {
             const int* li = A.link_i + l * MG_LINK_I_N;
             const int p = li[0], dof = li[2];
-            S.amask[l] = (p >= 0 ? S.amask[p] : 0) | (dof >= 0 ? (1 << dof) : 0);
+            S.amask[l] = (p >= 0 ? S.amask[p] : 0u) | (dof >= 0 ? (1u << dof) : 0u);
             if (dof >= 0) {
                 S.dlink[dof] = l;
                 S.drev[dof] = li[1] == MG_JOINT_REVOLUTE ? 1 : 0;
@@ -995,7 +1058,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     // the DOF lane's joint: link, revolute flag
     const int mylink = is_dof ? S.dlink[ln] : 0;
     const bool myrev = is_dof && S.drev[ln] != 0;
-    constexpr int ND = MAXL <= 4 ? 4 : G;
+    constexpr int ND = MAXL <= 4 ? 4 : (G > 32 ? 32 : G);
     float mcol[ND];                  // column ln of M_eff^-1 (DOF lanes)
 #pragma unroll
     for (int k = 0; k < ND; ++k) mcol[k] = 0.0f;
@@ -1010,11 +1073,11 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         if (LA > 0) {
             bool xm = false, xp = false;     // this DOF runs at constant +-effort
             bool redo = live && L > 0;
-            aba_kin<MAXL>(P, A, S, redo, ln, LA, x0, q0, lk, b0);
+            aba_kin<MAXL, G>(P, A, S, redo, ln, LA, x0, q0, lk, b0);
             for (int att = 0; att < 2; ++att) {
                 if (!__any(redo)) break;
-                if (att > 0) aba_refresh<MAXL>(A, S, redo, ln, LA, x0, lk, b0);
-                aba_dyn<MAXL>(P, A, S, redo, ln, LA, x0, gw, dc, is_dof, xm, xp, b0);
+                if (att > 0) aba_refresh<MAXL, G>(A, S, redo, ln, LA, x0, lk, b0);
+                aba_dyn<MAXL, G>(P, A, S, redo, ln, LA, x0, gw, dc, is_dof, xm, xp, b0);
                 // drives whose implicit force exceeds the effort limit
                 bool flip = false;
                 if (redo && is_dof && dc.eff > 0.0f && S.imp[ln] != 0.0f) {
@@ -1022,8 +1085,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     if (actf > dc.eff) { xm = true; xp = true; flip = true; }
                     else if (actf < -dc.eff) { xm = true; flip = true; }
                 }
-                const unsigned long long fb = __ballot(flip);
-                redo = ((fb >> (gi * G)) & 0xFFFFull) != 0ull;
+                redo = grp_ballot<G>(flip, gi) != 0ull;
                 __syncthreads();
             }
         }
@@ -1086,9 +1148,9 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     if (pb >= 0) pair_pose(S, pb, xb, qb);
                     near = pair_near(P, sha, xa, qa, pb >= 0 ? A.shapes + sb * MG_SHAPE_STRIDE : sha, xb, qb, pb < 0);
                 }
-                const unsigned gm = (unsigned)((__ballot(near) >> (gi * G)) & 0xFFFFull);
-                if (near) S.npl[nnear + __popc(gm & ((1u << ln) - 1u))] = pi;
-                nnear += __popc(gm);
+                const unsigned long long gm = grp_ballot<G>(near, gi);
+                if (near) S.npl[nnear + __popcll(gm & ((1ull << ln) - 1ull))] = pi;
+                nnear += __popcll(gm);
             }
             __syncthreads();
             PH_MARK(8);
@@ -1131,13 +1193,13 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 }
                 // this round's convex pairs, one at a time on the whole group (in
                 // lane order; the result goes to the pair's own lane)
-                unsigned cm = grp_ballot(coop, gi);
-                while (__any(cm != 0u)) {
-                    if (cm != 0u) {                       // group-uniform
-                        const int k = __ffs(cm) - 1;
-                        cm &= cm - 1u;
+                unsigned long long cm = grp_ballot<G>(coop, gi);
+                while (__any(cm != 0ull)) {
+                    if (cm != 0ull) {                     // group-uniform
+                        const int k = __ffsll(cm) - 1;
+                        cm &= cm - 1ull;
                         PairOut t;
-                        coop_convex_convex(shfl_shape(cA, k), shfl_shape(cB, k), P.contact_offset, ln, gi, t);
+                        coop_convex_convex<G>(shfl_shape<G>(cA, k), shfl_shape<G>(cB, k), P.contact_offset, ln, gi, t);
                         if (ln == k) o = t;
                     }
                 }
@@ -1216,7 +1278,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 
         // ================= 3. rows
         const bool link_rows = live && S.link_rows != 0;
-        if (LA > 0 && __any(link_rows)) meff_world<MAXL, ND>(A, S, link_rows, ln, LA, DA, x0, lk, mcol);
+        if (LA > 0 && __any(link_rows)) meff_world<MAXL, ND, G>(A, S, link_rows, ln, LA, DA, x0, lk, mcol);
         PH_MARK(2);
         // this DOF lane's joint axis and origin at the substep start
         const V3 myz = S.zl[mylink], myx = S.xl[mylink];
@@ -1238,7 +1300,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     if (a >= LIM0) {
                         if (rw == 0 && ln == a - LIM0) J = (float)b;
                     } else if (is_dof) {
-                        if (a < F0 && ((S.amask[a] >> ln) & 1))
+                        if (a < F0 && ln < 32 && ((S.amask[a] >> ln) & 1u))
                             J = myrev ? vdot(vcross(myz, vsub(p, myx)), dir) : vdot(myz, dir);
                     } else if (is_root) {
                         if (a < F0) J = rc < 3 ? v3c(vcross(vsub(p, x0), dir), rc) : v3c(dir, rc - 3);
@@ -1262,16 +1324,16 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         float w = 0.0f;
 #pragma unroll
                         for (int k = 0; k < ND; ++k)
-                            if (k < NA) w = w + mcol[k] * bcast16(J, k);
+                            if (k < NA) w = w + mcol[k] * bcastg<G>(J, k);
                         if (is_dof || is_root) W = w;
                     }
                     Jr[c * 3 + rw] = J;
                     Wr[c * 3 + rw] = W;
-                    const float den = red16(J * W);
+                    const float den = redg<G>(J * W);
                     const float kk = den > 0.0f ? 1.0f / den : 0.0f;
                     if (ln == 0) S.ck[c][rw] = kk;
                 }
-                const float vn0 = red16(Jr[c * 3] * uv);
+                const float vn0 = redg<G>(Jr[c * 3] * uv);
                 if (ln == 0) S.cvn0[c] = vn0;
             }
         }
@@ -1285,7 +1347,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 #pragma unroll
             for (int c = 0; c < MAXCT; ++c) {
                 if (c < nct) {
-                    const float s = S.cs0[c] + red16(Jr[c * 3] * dp);
+                    const float s = S.cs0[c] + redg<G>(Jr[c * 3] * dp);
                     float tgt;
                     if (pos) {
                         tgt = -s * P.inv_sub;
@@ -1298,7 +1360,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     // every lane of the env holds the same lambdas (red16 and
                     // the LDS operands are the same in all 16 lanes)
                     const float lm = lam[c * 3];
-                    float dl = S.ck[c][0] * (tgt - red16(Jr[c * 3] * uv));
+                    float dl = S.ck[c][0] * (tgt - redg<G>(Jr[c * 3] * uv));
                     const float nl = fmaxf(lm + dl, 0.0f);
                     dl = nl - lm;
                     uv = uv + Wr[c * 3] * dl;
@@ -1312,7 +1374,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 #pragma unroll
                     for (int rw = 1; rw < 3; ++rw) {
                         const float lm = lam[c * 3 + rw];
-                        const float nl = fminf(fmaxf(lm - S.ck[c][rw] * red16(Jr[c * 3 + rw] * uv), -lim), lim);
+                        const float nl = fminf(fmaxf(lm - S.ck[c][rw] * redg<G>(Jr[c * 3 + rw] * uv), -lim), lim);
                         const float dl = nl - lm;
                         uv = uv + Wr[c * 3 + rw] * dl;
                         lam[c * 3 + rw] = nl;
@@ -1480,18 +1542,19 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 // — and the link states by forward kinematics. Restated by
 // oracle/migym_oracle.c:artic_step (aba_world_ + the same integration and
 // outputs).
-template <int MAXL>
+template <int MAXL, int G>
 __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
-    __shared__ EnvLds shm[EPW];
+    constexpr int EPW = 64 / G;          // envs per wavefront
+    __shared__ EnvLds<MAXL, G> shm[EPW];
     const int gi = threadIdx.x / G;
     const int ln = threadIdx.x % G;
     const int a = blockIdx.x * EPW + gi;
     const bool live = a < AA.na;
-    EnvLds& S = shm[gi];
+    EnvLds<MAXL, G>& S = shm[gi];
     MgEnvArgs A{};
     A.nb = AA.nb; A.nd = AA.nd; A.nl = AA.nl; A.ndof = AA.ndof; A.floating = 0;
     A.link_f = AA.link_f; A.link_i = AA.link_i;
-    stage_links<MAXL>(A);
+    stage_links<MAXL, G>(A);
     A.state = AA.state; A.mass = AA.mass; A.body_tmpl = AA.body_tmpl; A.tbf = AA.tbf;
     A.dof_pos = AA.dof_pos; A.dof_vel = AA.dof_vel; A.dof_tpos = AA.dof_tpos; A.dof_tvel = AA.dof_tvel;
     A.dof_force = AA.dof_force; A.dof_props = AA.dof_props; A.ext = AA.ext; A.cforce = AA.cforce;
@@ -1549,11 +1612,11 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
         __syncthreads();
         bool xm = false, xp = false;     // this DOF runs at constant +-effort
         bool redo = live;
-        aba_kin<MAXL>(P, A, S, redo, ln, LA, x0, q0, lk, b0);
+        aba_kin<MAXL, G>(P, A, S, redo, ln, LA, x0, q0, lk, b0);
         for (int att = 0; att < 2; ++att) {
             if (!__any(redo)) break;
-            if (att > 0) aba_refresh<MAXL>(A, S, redo, ln, LA, x0, lk, b0);
-            aba_dyn<MAXL>(P, A, S, redo, ln, LA, x0, gw, dc, is_dof, xm, xp, b0);
+            if (att > 0) aba_refresh<MAXL, G>(A, S, redo, ln, LA, x0, lk, b0);
+            aba_dyn<MAXL, G>(P, A, S, redo, ln, LA, x0, gw, dc, is_dof, xm, xp, b0);
             // drives whose implicit force exceeds the effort limit
             bool flip = false;
             if (redo && is_dof && dc.eff > 0.0f && S.imp[ln] != 0.0f) {
@@ -1561,8 +1624,7 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
                 if (actf > dc.eff) { xm = true; xp = true; flip = true; }
                 else if (actf < -dc.eff) { xm = true; flip = true; }
             }
-            const unsigned long long fb = __ballot(flip);
-            redo = ((fb >> (gi * G)) & 0xFFFFull) != 0ull;
+            redo = grp_ballot<G>(flip, gi) != 0ull;
             __syncthreads();
         }
         // integrate the joint (DOF lane); a ball joint's three lanes turn its
@@ -1918,9 +1980,14 @@ __global__ void __launch_bounds__(64, 1) k_artic_chain(MgStep P, MgArticArgs AA)
 
 }  // namespace
 
+// lanes per env / articulation: 16 (4 per wavefront) up to 16 links and 16
+// velocity slots; 64 (one per wavefront) up to MG_MAX_LINKS links and
+// MG_ENV_SLOTS_WIDE slots
+static bool mg_wide(int nl, int slots) { return nl > 16 || slots > 16; }
+
 hipError_t mg_launch_artic_lanes(const MgStep& P, const MgArticArgs& A, hipStream_t s) {
     if (A.na <= 0) return hipSuccess;
-    if (!A.fixed_base || A.nl > MG_MAX_LINKS || A.ndof > G) return hipErrorNotSupported;
+    if (!A.fixed_base || A.nl > MG_MAX_LINKS || A.ndof > MG_ENV_SLOTS_WIDE) return hipErrorNotSupported;
     if (A.chain && A.nl >= 2 && A.nl <= 4) {   // serial chain, one DOF per moving link
         const int cb = (A.na + 63) / 64;
         if (A.nl == 2) MG_LAUNCH((k_artic_chain<2>), dim3(cb), dim3(64), 0, s, P, A);
@@ -1928,22 +1995,31 @@ hipError_t mg_launch_artic_lanes(const MgStep& P, const MgArticArgs& A, hipStrea
         else MG_LAUNCH((k_artic_chain<4>), dim3(cb), dim3(64), 0, s, P, A);
         return hipGetLastError();
     }
-    const int blocks = (A.na + EPW - 1) / EPW;
+    if (mg_wide(A.nl, A.ndof)) {
+        MG_LAUNCH((k_artic_lanes<MG_MAX_LINKS, 64>), dim3(A.na), dim3(64), 0, s, P, A);
+        return hipGetLastError();
+    }
+    const int blocks = (A.na + 3) / 4;
     if (A.nl <= 4 && A.ndof <= 4)
-        MG_LAUNCH((k_artic_lanes<4>), dim3(blocks), dim3(64), 0, s, P, A);
+        MG_LAUNCH((k_artic_lanes<4, G16>), dim3(blocks), dim3(64), 0, s, P, A);
     else
-        MG_LAUNCH((k_artic_lanes<MG_MAX_LINKS>), dim3(blocks), dim3(64), 0, s, P, A);
+        MG_LAUNCH((k_artic_lanes<16, G16>), dim3(blocks), dim3(64), 0, s, P, A);
     return hipGetLastError();
 }
 
 hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s) {
     if (A.ne <= 0) return hipSuccess;
-    const int blocks = (A.ne + EPW - 1) / EPW;
+    // velocity slots: DOFs, the floating root's 6, 6 per free body (at most MG_ENV_MAXF)
+    const int slots = A.ndof + (A.floating ? 6 : 0) + 6 * A.max_free;
+    if (A.nl > MG_MAX_LINKS || slots > MG_ENV_SLOTS_WIDE) return hipErrorNotSupported;
+    if (mg_wide(A.nl, slots)) {
+        MG_LAUNCH((k_env_step<MG_MAX_LINKS, 64>), dim3(A.ne), dim3(64), 0, s, P, A);
+        return hipGetLastError();
+    }
+    const int blocks = (A.ne + 3) / 4;
     if (A.nl <= 4 && A.ndof <= 4 && !A.floating)
-        MG_LAUNCH((k_env_step<4>), dim3(blocks), dim3(64), 0, s, P, A);
-    else if (A.nl <= MG_MAX_LINKS && A.ndof <= G)
-        MG_LAUNCH((k_env_step<MG_MAX_LINKS>), dim3(blocks), dim3(64), 0, s, P, A);
+        MG_LAUNCH((k_env_step<4, G16>), dim3(blocks), dim3(64), 0, s, P, A);
     else
-        return hipErrorNotSupported;
+        MG_LAUNCH((k_env_step<16, G16>), dim3(blocks), dim3(64), 0, s, P, A);
     return hipGetLastError();
 }

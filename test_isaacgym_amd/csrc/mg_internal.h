@@ -11,8 +11,8 @@
 #include "../../include/migym.h"
 
 #define MG_MAX_CONTACTS 8     // contact slots per free body per substep
-#define MG_MAX_LINKS    16    // articulation links handled per lane
-#define MG_MAX_DOFS     16
+#define MG_MAX_LINKS    32    // articulation links (more than 16: the 64-lane kernels)
+#define MG_MAX_DOFS     32
 
 // Per-simulate constants derived on the host from mg_sim_params
 // (one copy, passed by value as a kernel argument).
@@ -109,13 +109,15 @@ struct MgArticArgs {
 // link l = l (link 0, the fixed base, only as b), free body k = MG_ENV_FREE0 + k,
 // static body s = MG_ENV_STATIC0 + s, ground = -1.
 #define MG_ENV_I_N    16
-#define MG_ENV_G      16     // lanes per env
+#define MG_ENV_G      16     // lanes per env (envs of more links / slots: 64, one per wavefront)
+#define MG_ENV_SLOTS_WIDE 32 // velocity slots of a 64-lane env (its M_eff solve)
 #define MG_ENV_MAXF    2
 #define MG_ENV_MAXS    4
 #define MG_ENV_MAXCT  16     // contacts per env per substep
-#define MG_ENV_FREE0  16
-#define MG_ENV_STATIC0 32
-#define MG_ENV_LIMIT0  64     // joint-limit row of DOF d: a = MG_ENV_LIMIT0 + d, b = +1 lower / -1 upper
+#define MG_ENV_MAXCT_WIDE 48 // ... in a 64-lane env
+#define MG_ENV_FREE0  64     // participant ids: links 0..MG_MAX_LINKS-1 below
+#define MG_ENV_STATIC0 80
+#define MG_ENV_LIMIT0 128     // joint-limit row of DOF d: a = MG_ENV_LIMIT0 + d, b = +1 lower / -1 upper
 
 struct MgEnvArgs {
     int          ne;          // envs in this launch
@@ -124,6 +126,7 @@ struct MgEnvArgs {
     const int*   pairs;       // [..][4] candidate shape pairs (env_i[14], [15])
     int          nl, ndof;    // articulation template of this launch (0 links: none)
     int          floating;    // the template has a floating base: 6 root velocity slots after the DOFs
+    int          max_free;    // most free bodies of one env in this launch (6 velocity slots each)
     const float* link_f;
     const int*   link_i;
     float*       state;

@@ -66,6 +66,7 @@ struct ArticGroup {
 // coupled envs (mg_env.hip) of one articulation template (tmpl -1: none)
 struct EnvGroup {
     int tmpl, first_link, nl, ndof, floating;
+    int max_free;        // most free bodies of one env of the group (velocity slots)
     int offset, count;   // rows of d_env
 };
 
@@ -491,9 +492,10 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                     return fail(MG_ERR_ARG, "env %d: bad articulation template %d", e, t);
                 art_fl = fl;
             }
-            if (art_nd + 6 * art_fb + 6 * (int)fr.size() > MG_ENV_G)
-                return fail(MG_ERR_UNSUPPORTED, "env %d: %d DOFs%s + %zu free bodies exceed the %d velocity slots of "
-                            "the coupled step", e, art_nd, art_fb ? " + a floating base" : "", fr.size(), MG_ENV_G);
+            if (art_nd + 6 * art_fb + 6 * (int)fr.size() > MG_ENV_SLOTS_WIDE || art_nl > MG_MAX_LINKS)
+                return fail(MG_ERR_UNSUPPORTED, "env %d: %d links, %d DOFs%s + %zu free bodies exceed the %d links / %d "
+                            "velocity slots of the coupled step", e, art_nl, art_nd, art_fb ? " + a floating base" : "",
+                            fr.size(), MG_MAX_LINKS, MG_ENV_SLOTS_WIDE);
             std::array<int, MG_ENV_I_N> row;
             row.fill(0);
             row[0] = -1;
@@ -711,7 +713,10 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     // coupled env rows: internal slots, grouped by articulation template (-1 first)
     std::vector<int> env_flat;
     s->env_groups.clear();
-    for (int t = -1; t < m->num_artic_tmpls; ++t) {
+    // (and by lane width: an env of more than 16 links or velocity slots runs
+    // 64 lanes wide, mg_env.hip; the oracle decides per env the same way)
+    for (int t = -1; t < m->num_artic_tmpls; ++t)
+    for (int wide = 0; wide < 2; ++wide) {
         EnvGroup g{};
         g.tmpl = t;
         if (t >= 0) {
@@ -723,7 +728,10 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         g.offset = (int)env_flat.size() / MG_ENV_I_N;
         for (size_t r = 0; r < env_rows.size(); ++r) {
             if (env_tmpl[r] != t) continue;
+            const int slots = (t >= 0 ? g.ndof + 6 * g.floating : 0) + 6 * env_rows[r][2];
+            if ((g.nl > 16 || slots > 16) != (wide != 0)) continue;
             std::array<int, MG_ENV_I_N> row = env_rows[r];
+            g.max_free = std::max(g.max_free, row[2]);
             if (row[0] >= 0) row[0] = perm[row[0]];
             for (int i = 0; i < row[2]; ++i) row[3 + i] = perm[row[3 + i]];
             for (int i = 0; i < row[7]; ++i) row[8 + i] = perm[row[8 + i]];
@@ -950,6 +958,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.nl = g.tmpl >= 0 ? g.nl : 0;
         A.ndof = g.tmpl >= 0 ? g.ndof : 0;
         A.floating = g.tmpl >= 0 ? g.floating : 0;
+        A.max_free = g.max_free;
         A.link_f = s->d_link_f + (size_t)(g.tmpl >= 0 ? g.first_link : 0) * MG_LINK_F_N;
         A.link_i = s->d_link_i + (size_t)(g.tmpl >= 0 ? g.first_link : 0) * MG_LINK_I_N;
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;

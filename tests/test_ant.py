@@ -128,24 +128,76 @@ def test_ant_settles_and_jumps(gym):
     assert np.all(st[0::9, 2] > z + 0.1)
 
 
-def test_floating_base_needs_slots(gym):
-    """D + 6 (floating base) + 6 per free body must fit the 16 lanes: the ant
-    (8 DOFs + root) with one free box is 20 slots and is refused loudly by the
-    oracle (the library refuses the same model at upload)."""
-    sp = scenes.ant_sim_params(False)
+def _ant_and_box(gym, n=1, gpu=False):
+    sp = scenes.ant_sim_params(gpu)
     sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
     plane = gymapi.PlaneParams()
     plane.normal = gymapi.Vec3(0, 0, 1)
     gym.add_ground(sim, plane)
     ant = gym.load_asset(sim, scenes.ASSET_ROOT, "mjcf/ant.xml", gymapi.AssetOptions())
     box = gym.create_box(sim, 0.2, 0.2, 0.2, gymapi.AssetOptions())
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-2, -2, 0), gymapi.Vec3(2, 2, 2), 8)
+        gym.create_actor(env, ant, gymapi.Transform(gymapi.Vec3(0, 0, 1)), "ant", i, 0)
+        gym.create_actor(env, box, gymapi.Transform(gymapi.Vec3(0.25 + 0.002 * i, 0, 1.4)), "box", i, 0)
+    return sim
+
+
+def test_floating_base_wide_env(gym):
+    """D + 6 (floating base) + 6 per free body above 16 velocity slots: the ant
+    (8 DOFs + root) with a free box is 20 slots and steps in the 64-lane coupled
+    kernel (mg_env.hip G = 64; the oracle reduces over 64 lanes the same way):
+    the box drops onto the ant. More than 32 slots (the humanoid's 27 + a box)
+    is refused loudly by the oracle (the library refuses it at upload)."""
+    sim = _ant_and_box(gym)
+    A = sim.build_model()
+    p, m = sim.mg_params(), sim.mg_model()
+    st, ds = A["body_state0"].copy(), A["dof_state0"].copy()
+    for _ in range(60):
+        oracle.step(p, m, st, ds, props=A["dof_props"])
+    assert np.all(np.isfinite(st)) and np.all(np.isfinite(ds))
+    assert st[9, 2] < 1.39 and st[9, 2] > 0.05                  # fell, onto the ant or the ground
+    sp = scenes.ant_sim_params(False)
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim, plane)
+    hum = gym.load_asset(sim, scenes.ASSET_ROOT, "mjcf/humanoid.xml", gymapi.AssetOptions())
+    box = gym.create_box(sim, 0.2, 0.2, 0.2, gymapi.AssetOptions())
     env = gym.create_env(sim, gymapi.Vec3(-2, -2, 0), gymapi.Vec3(2, 2, 2), 1)
-    gym.create_actor(env, ant, gymapi.Transform(gymapi.Vec3(0, 0, 1)), "ant", 0, 0)
+    gym.create_actor(env, hum, gymapi.Transform(gymapi.Vec3(0, 0, 1.4)), "h", 0, 0)
     gym.create_actor(env, box, gymapi.Transform(gymapi.Vec3(1, 0, 0.2)), "box", 0, 0)
     A = sim.build_model()
     with pytest.raises(RuntimeError):
         oracle.step(sim.mg_params(), sim.mg_model(), A["body_state0"].copy(), A["dof_state0"].copy(),
                     props=A["dof_props"])
+
+
+@pytest.mark.gpu
+def test_ant_with_box_wide_parity_gpu(gym):
+    """The ant + box envs of test_floating_base_wide_env (64 lanes per env) on
+    the GPU, 64 envs x 60 frames: bit for bit the oracle."""
+    import torch  # noqa: F401
+    n = 64
+    sim = _ant_and_box(gym, n, gpu=True)
+    gym.prepare_sim(sim)
+    from test_isaacgym_amd import _native as N
+    assert N.lib.mg_num_coupled_envs(sim.native) == n
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    ds = sim.model_arrays["dof_state0"].copy()
+    props = sim.model_arrays["dof_props"]
+    for _ in range(60):
+        gym.simulate(sim)
+        oracle.step(p, m, st, ds, props=props)
+    gym.refresh_dof_state_tensor(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    got_d, got = dof.cpu().numpy(), rb.cpu().numpy()
+    assert np.all(np.isfinite(got))
+    assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
 
 
 @pytest.mark.gpu

@@ -176,3 +176,61 @@ def test_two_hinge_parity_gpu(gym, tmp_path, box):
     assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
     assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
     torch.cuda.synchronize()
+
+
+def _humanoid_drop(gym, n=1, gpu=False):
+    from test_isaacgym_amd import scenes
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, scenes.ant_sim_params(gpu))
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim, plane)
+    hum = gym.load_asset(sim, os.path.join(ROOT, "assets"), "mjcf/humanoid.xml", gymapi.AssetOptions())
+    rng = np.random.RandomState(1)
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-2, -2, 0), gymapi.Vec3(2, 2, 2), 8)
+        q = gymapi.Quat.from_axis_angle(gymapi.Vec3(0, 0, 1), float(rng.uniform(-3, 3)))
+        gym.create_actor(env, hum, gymapi.Transform(gymapi.Vec3(0, 0, 1.3 + 0.05 * rng.uniform()), q), "h", i, 0)
+    return sim
+
+
+def test_humanoid_drop_settles(gym):
+    """nv_humanoid (floating base, 21 DOFs in 25 kernel links: 27 velocity slots,
+    the 64-lane coupled kernel) dropped on the ground: it falls, lands and stays
+    above the ground, its state finite."""
+    sim = _humanoid_drop(gym)
+    A = sim.build_model()
+    p, m = sim.mg_params(), sim.mg_model()
+    st, ds = A["body_state0"].copy(), A["dof_state0"].copy()
+    z0 = float(st[0, 2])
+    for _ in range(120):
+        oracle.step(p, m, st, ds, props=A["dof_props"])
+    assert np.all(np.isfinite(st)) and np.all(np.isfinite(ds))
+    assert float(st[0, 2]) < z0 - 0.2                      # it fell
+    assert float(st[:, 2].min()) > -0.05                    # nothing through the ground
+    assert np.abs(st[:, 7:10]).max() < 5.0                  # and it is not flying apart
+
+
+@pytest.mark.gpu
+def test_humanoid_drop_parity_gpu(gym):
+    """64 humanoids dropped on the ground, 60 frames: k_env_step<32, 64> bit for
+    bit the oracle (rigid-body and DOF state)."""
+    n = 64
+    sim = _humanoid_drop(gym, n, gpu=True)
+    gym.prepare_sim(sim)
+    from test_isaacgym_amd import _native as N
+    assert N.lib.mg_num_coupled_envs(sim.native) == n
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    ds = sim.model_arrays["dof_state0"].copy()
+    props = sim.model_arrays["dof_props"]
+    for _ in range(60):
+        gym.simulate(sim)
+        oracle.step(p, m, st, ds, props=props)
+    gym.refresh_dof_state_tensor(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    got_d, got = dof.cpu().numpy(), rb.cpu().numpy()
+    assert np.all(np.isfinite(got)) and float(got[:, 2].min()) > -0.05
+    assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
