@@ -471,6 +471,48 @@ class Gym:
         d = self.get_actor_dof_dict(env, handle)
         return self.get_actor_dof_index(env, handle, d[name], domain) if name in d else _T.INVALID_HANDLE
 
+    def get_dof_frame(self, env, dof_handle):
+        """examples/joint_monkey.py:255-259: the world origin and axis of a DOF's
+        joint at the current state (forward kinematics of the packed links from
+        the actor's root pose and DOF positions; a ball joint's or pre-hinge's
+        virtual links included)."""
+        a, d = self._dof_owner(env, dof_handle)
+        sim = env.sim
+        sim.finalize()
+        A = sim.model_arrays
+        rb, ds = self._host_state(sim)
+        q = ds[a.global_dof:a.global_dof + a.num_dofs, 0].astype(np.float64)
+        root = rb[a.global_body].astype(np.float64)
+        k = [i for i, r in enumerate(A["artic_i"]) if r[0] == a.global_body][0]
+        ti = A["artic_tmpl_i"][A["artic_i"][k][2]]
+        lf = A["tmpl_link_f"][ti[0]:ti[0] + ti[1]].astype(np.float64)
+        li = A["tmpl_link_i"][ti[0]:ti[0] + ti[1]]
+        from ._assets import _qmat, _qmul
+        ps, qs = [root[0:3]], [root[3:7] / np.linalg.norm(root[3:7])]
+        for l in range(1, len(li)):
+            p, jt, dj = int(li[l, 0]), int(li[l, 1]), int(li[l, 2])
+            po, qo, ax = lf[l, 0:3], lf[l, 3:7], lf[l, 7:10]
+            org = ps[p] + _qmat(qs[p]) @ po
+            qj = _qmul(qs[p], qo)                       # the joint frame (before its own motion)
+            if dj == d:
+                axis = _qmat(qj) @ ax
+                return _T.DofFrame(_T.Vec3(*org), _T.Vec3(*axis))
+            qrel, rr = qo, po
+            ball = int(round(lf[l, 10]))
+            if ball == 1:
+                th = q[dj:dj + 3]
+                t = np.linalg.norm(th)
+                if t > 0:
+                    qrel = _qmul(qo, np.array([*(th / t * np.sin(0.5 * t)), np.cos(0.5 * t)]))
+            elif ball == 0 and jt == _T.JOINT_REVOLUTE and dj >= 0:
+                qrel = _qmul(qo, np.array([*(ax * np.sin(0.5 * q[dj])), np.cos(0.5 * q[dj])]))
+            elif jt == _T.JOINT_PRISMATIC and dj >= 0:
+                rr = po + _qmat(qo) @ (ax * q[dj])
+            ps.append(ps[p] + _qmat(qs[p]) @ rr)
+            qn = _qmul(qs[p], qrel)
+            qs.append(qn / np.linalg.norm(qn))
+        raise IndexError("DOF %d has no joint" % d)
+
     def _dof_owner(self, env, dof_handle):
         for a in env.actors:
             if a.dof_offset <= dof_handle < a.dof_offset + a.num_dofs:

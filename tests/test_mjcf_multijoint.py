@@ -234,3 +234,47 @@ def test_humanoid_drop_parity_gpu(gym):
     assert np.all(np.isfinite(got)) and float(got[:, 2].min()) > -0.05
     assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
     assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+
+
+@pytest.mark.gpu
+def test_fixed_humanoid_pd_parity_gpu(gym):
+    """joint_monkey's setting (examples/joint_monkey.py:95-96: fix_base_link):
+    32 fixed-base humanoids under gravity with PD drives on random targets —
+    k_artic_lanes<32, 64> (25 links, 21 DOFs: one articulation per wavefront)
+    bit for bit the oracle."""
+    n = 32
+    sim = _sim(gym, gpu=True)
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    hum = gym.load_asset(sim, os.path.join(ROOT, "assets"), "mjcf/humanoid.xml", opts)
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-2, -2, 0), gymapi.Vec3(2, 2, 2), 8)
+        h = gym.create_actor(env, hum, gymapi.Transform(gymapi.Vec3(0, 0, 1.5)), "h", i, 1)
+        props = gym.get_actor_dof_properties(env, h)
+        props["driveMode"][:] = gymapi.DOF_MODE_POS
+        props["stiffness"][:] = 200.0
+        props["damping"][:] = 10.0
+        gym.set_actor_dof_properties(env, h, props)
+    gym.prepare_sim(sim)
+    from test_isaacgym_amd import _native as N
+    assert N.lib.mg_num_coupled_envs(sim.native) == 0
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    ds = sim.model_arrays["dof_state0"].copy()
+    props = sim.model_arrays["dof_props"]
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+    rng = np.random.RandomState(2)
+    for _ in range(40):
+        tgt[:, 0] = rng.uniform(-0.6, 0.6, size=ds.shape[0]).astype(np.float32)
+        assert gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(
+            torch.from_numpy(tgt[:, 0].copy()).to("cuda:0")))
+        gym.simulate(sim)
+        oracle.step(p, m, st, ds, tgt=tgt, props=props)
+    gym.refresh_dof_state_tensor(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    got_d, got = dof.cpu().numpy(), rb.cpu().numpy()
+    assert np.all(np.isfinite(got)) and np.abs(got_d[:, 1]).max() > 0.1
+    assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()

@@ -132,3 +132,23 @@ def test_test13_spherical_joint_setup(monkeypatch):
     assert li[4:, 2].tolist() == [3, 4, 5] and li[4:, 0].tolist() == [3, 4, 5]
     assert A["artic_tmpl_i"][0, 1] == 7 and A["artic_tmpl_i"][0, 2] == 6
     assert gym.get_sim_rigid_body_count(sim) == 5 * ns["num_envs"]
+
+
+@pytest.mark.skipif(has_gpu(), reason="CPU-container variant")
+def test_joint_monkey_humanoid_setup(monkeypatch):
+    """examples/joint_monkey.py unmodified with its default asset, nv_humanoid
+    (:35, MJCF bodies with several hinges): 36 fixed-base humanoids, 21 DOFs
+    each, default DOF states set per actor (:203) — the setup the GPU steps in
+    the 64-lane articulation kernel (25 links)."""
+    path = os.path.join(REFERENCE, "examples", "joint_monkey.py")
+    monkeypatch.setattr(sys, "argv", [path, "--show_axis"])
+    ns, err = _exec_script(path, os.path.join(REFERENCE, "examples"), monkeypatch)
+    assert err is not None
+    gym, asset, sim = ns["gym"], ns["asset"], ns["sim"]
+    assert gym.get_asset_dof_count(asset) == 21 and gym.get_asset_rigid_body_count(asset) == 16
+    assert len(ns["envs"]) == ns["num_envs"] and gym.get_sim_dof_count(sim) == 21 * ns["num_envs"]
+    assert sim.model_arrays["artic_tmpl_i"][0, 1] == 25
+    # the DOF frame joint_monkey draws (:255-259): abdomen_z's axis is the torso's local z
+    env, h = ns["envs"][0], ns["actor_handles"][0]
+    fr = gym.get_dof_frame(env, gym.get_actor_dof_handle(env, h, 0))
+    assert abs((fr.axis.x ** 2 + fr.axis.y ** 2 + fr.axis.z ** 2) - 1.0) < 1e-6
