@@ -11,6 +11,11 @@ every actor reads the (2N, 13) f32 root tensor once (fully coalesced) plus the
 int32 selection and root-body index per row.
 
 usage: python profiles/collect_pmc.py FETCH.csv WRITE.csv ENVS OUT.json
+       python profiles/collect_pmc.py FETCH.csv WRITE.csv ENVS OUT.json --kernel k_artic_chain \
+              --bytes-per-env 532 --factor-from profiles/r03_pmc_rigid_262144.json
+(the second form: another kernel of a run without a calibration kernel, its
+FETCH_SIZE scaled by the read factor calibrated in the named S1 summary of the
+same GPU session — dword SoA loads like the step kernel's)
 """
 import csv
 import json
@@ -24,17 +29,34 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
-        for key in ("k_rigid_step", "k_scatter_rows", "k_gather_rows", "k_artic_step"):
+        for key in ("k_rigid_step", "k_scatter_rows", "k_gather_rows", "k_artic_step", "k_artic_chain"):
             if key in name:
                 name = key
         acc[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
 
 
+def other_kernel(f, nf, w, envs, out, kernel, bpe, factor_from):
+    cal = json.load(open(factor_from))
+    factor = cal["read_factor_calibrated"]
+    key = [k for k in f if kernel in k][0]
+    read = f[key] * 1024.0 * factor
+    write = w[[k for k in w if kernel in k][0]] * 1024.0
+    res = {"envs": envs, "kernel": kernel, "fetch_kib_raw": f[key], "write_kib_raw": write / 1024.0,
+           "read_factor_calibrated": factor, "calibration": "from %s (%s)" % (factor_from, cal["calibration"]),
+           "hbm_bytes_per_launch": read + write, "algorithmic_bytes_per_launch": bpe * envs, "launches": nf[key]}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
 def main():
     fetch_csv, write_csv, envs, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
     f, nf = per_kernel(fetch_csv, "FETCH_SIZE")
     w, _ = per_kernel(write_csv, "WRITE_SIZE")
+    if "--kernel" in sys.argv:
+        a = sys.argv
+        return other_kernel(f, nf, w, envs, out, a[a.index("--kernel") + 1], int(a[a.index("--bytes-per-env") + 1]),
+                            a[a.index("--factor-from") + 1])
     actors = 2 * envs
     # bench.py --pmc-calibrate: indexed sets of every actor (the fused step reads a
     # full set itself): the (2N, 13) rows, the int32 selection and root-body index

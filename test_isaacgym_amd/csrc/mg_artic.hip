@@ -46,6 +46,7 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
     const int ei = live ? e : 0;
     const int b0 = A.artic_i[ei * MG_ARTIC_I_N + 0];
     const int d0 = A.artic_i[ei * MG_ARTIC_I_N + 1];
+    const int ls = A.artic_i[ei * MG_ARTIC_I_N + 3];     // link stride (migym_capi.cpp)
     const int nb = A.nb;
     const int L = A.nl, D = A.ndof;
     const float* St = A.state;
@@ -104,7 +105,7 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
         // a virtual link (ball joint, body -1) has no mass
         if (mm && (ln > 0 || fb)) {
             if (li[3] >= 0) {
-                world_inertia(load_link(A.mass, nb, b0 + li[3]), S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
+                world_inertia(load_link(A.mass, nb, b0 + li[3] * ls), S.ql[ln], S.xl[ln], x0, S.Iw[ln]);
             } else {
                 for (int k = 0; k < 36; ++k) S.Iw[ln][k] = 0.0f;
             }

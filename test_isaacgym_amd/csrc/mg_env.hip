@@ -1737,7 +1737,7 @@ __global__ void __launch_bounds__(64, 1) k_artic_chain(MgStep P, MgArticArgs AA)
     const int a = blockIdx.x * 64 + threadIdx.x;
     const bool live = a < AA.na;
     const int* ai = AA.artic_i + (size_t)(live ? a : 0) * MG_ARTIC_I_N;
-    const int b0 = ai[0], d0 = ai[1];
+    const int b0 = ai[0], d0 = ai[1], ls = ai[3];   // link l: body b0 + l * ls (migym_capi.cpp)
     const int nb = AA.nb, nd = AA.nd;
     float* St = AA.state;
     const float* pr = AA.dof_props;
@@ -1784,7 +1784,7 @@ __global__ void __launch_bounds__(64, 1) k_artic_chain(MgStep P, MgArticArgs AA)
     }
     LinkC lk[NL];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) lk[l] = load_link(AA.mass, nb, b0 + l);
+    for (int l = 0; l < NL; ++l) lk[l] = load_link(AA.mass, nb, b0 + l * ls);
 
     for (int st = 0; st < P.substeps; ++st) {
         // ---- kinematics (aba_kin): joint transforms, scan, axes, inertias
@@ -1827,7 +1827,7 @@ __global__ void __launch_bounds__(64, 1) k_artic_chain(MgStep P, MgArticArgs AA)
                 put6(cc[l], crm(v, vJ));
                 SV pb = crf(v, sv6(Iv));
                 if (AA.ext) {
-                    const int b = b0 + l;
+                    const int b = b0 + l * ls;
                     const V3 f = v3(AA.ext[0 * nb + b], AA.ext[1 * nb + b], AA.ext[2 * nb + b]);
                     const V3 t = v3(AA.ext[3 * nb + b], AA.ext[4 * nb + b], AA.ext[5 * nb + b]);
                     const V3 c = vsub(vadd(xl[l], qrot(ql[l], lk[l].com)), x0);
@@ -1967,7 +1967,7 @@ __global__ void __launch_bounds__(64, 1) k_artic_chain(MgStep P, MgArticArgs AA)
             xlv = vadd(xlv, qrot(qlp, rr));
             vl = svadd(x_motion(m3t(qmat(qrel)), rr, vl), svscale(sj, uv[l - 1]));
         }
-        const int b = b0 + l;
+        const int b = b0 + l * ls;
         const V3 ww = qrot(ql, vl.w);
         const V3 vw = qrot(ql, vadd(vl.v, vcross(vl.w, lk[l].com)));
         St[0 * nb + b] = xlv.x; St[1 * nb + b] = xlv.y; St[2 * nb + b] = xlv.z;

@@ -682,22 +682,46 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         g.count = 0;
         g.step_offset = (int)artic_step.size() / MG_ARTIC_I_N;
         g.step_count = 0;
+        // Link stride (row field 3): link l of an instance is body first + l * stride.
+        // Instances that step in k_artic_chain (one lane per articulation) are laid
+        // out link-major in blocks of 64, the kernel's wavefront: link l of the
+        // block's instances are 64 consecutive slots, so every per-link load and
+        // store of a wave is one contiguous 256-B access (link-contiguous storage
+        // strides the lanes nl * 4 B apart). Everything else: stride 1.
+        const bool blocked = g.chain && g.nl >= 2 && g.nl <= 4;
+        std::vector<int> blk_k, blk_sorted, blk_step;
         for (int k = 0; k < m->num_artics; ++k) {
             const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;
             if (ai[2] != t) continue;
             if (ai[0] < 0 || ai[0] + g.nbody > nb || ai[1] < 0 || ai[1] + g.ndof > nd)
                 return fail(MG_ERR_ARG, "articulation %d out of range", k);
-            for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_sorted.push_back(ai[j]);
-            if (!coupled_body[ai[0]]) {
-                for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_step.push_back(ai[j]);
+            const bool cpl = coupled_body[ai[0]] != 0;
+            const bool blk = blocked && !cpl;
+            if (blk) {
+                blk_k.push_back(k);
+                blk_sorted.push_back((int)artic_sorted.size());
+                blk_step.push_back((int)artic_step.size());
+            }
+            for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_sorted.push_back(j == 3 ? 1 : ai[j]);
+            if (!cpl) {
+                for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_step.push_back(j == 3 ? 1 : ai[j]);
                 g.step_count++;
             }
             for (int l = 0; l < g.nbody; ++l) {
                 if (placed[ai[0] + l]) return fail(MG_ERR_ARG, "articulation %d overlaps another body", k);
                 placed[ai[0] + l] = 1;
-                order.push_back(ai[0] + l);
+                if (!blk) order.push_back(ai[0] + l);
             }
             g.count++;
+        }
+        for (size_t i0 = 0; i0 < blk_k.size(); i0 += 64) {
+            const int cnt = (int)std::min<size_t>(64, blk_k.size() - i0);
+            for (int l = 0; l < g.nbody; ++l)
+                for (int j = 0; j < cnt; ++j) order.push_back(m->artic_i[(size_t)blk_k[i0 + j] * MG_ARTIC_I_N] + l);
+            for (int j = 0; j < cnt; ++j) {
+                artic_sorted[blk_sorted[i0 + j] + 3] = cnt;
+                artic_step[blk_step[i0 + j] + 3] = cnt;
+            }
         }
         if (!g.fixed_base && g.step_count > 0)
             return fail(MG_ERR_UNSUPPORTED, "articulation template %d: a floating base steps in the coupled "

@@ -76,6 +76,12 @@ if has pmc; then
         > gpurun_out/pmc_${c}_$n.log 2>&1 || { tail -20 gpurun_out/pmc_${c}_$n.log; exit 1; }
     done
   done
+  for n in ${PMC_GIMBAL_SIZES:-262144}; do          # S2: k_artic_chain (tools/kbench_gimbal.py)
+    for c in FETCH_SIZE WRITE_SIZE; do
+      timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmcg_${c}_$n -o run --output-format csv -- \
+        python tools/kbench_gimbal.py $n > gpurun_out/pmcg_${c}_$n.log 2>&1 || { tail -20 gpurun_out/pmcg_${c}_$n.log; exit 1; }
+    done
+  done
   echo pmc done
 fi
 if has kbench; then
