@@ -25,9 +25,10 @@ synchronize, repeated `--repeats` times; `value` uses the median repeat of the
 per-repeat maximum over ranks.
 
 Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel
-(k_rigid_step, one launch per simulate) at SURVEY.md §8d's algorithmic bytes:
+(k_rigid_step1, one launch per simulate) at SURVEY.md §8d's algorithmic bytes:
 376 B per env per simulate (2 bodies x (state in 52 + state out 52 + mass
-properties 44 + shape 40)), over its average duration from the kernel's own
+properties 44 + shape 40)), plus 208 B when the refresh is fused into the step
+(the rigid-body and root rows it then writes), over its average duration from the kernel's own
 dispatch timestamps (hipExtLaunchKernelGGL start / stop events on the simulate
 stream, the interval rocprofv3 reports). `large_n` repeats that at 262,144 envs,
 where the kernel leaves the latency regime. `cpu_baseline` times the C
@@ -50,6 +51,9 @@ METRIC = "env-steps/sec (whole node), 4096 servo envs; 1/2/4/8-GPU scaling"
 ENVS_PER_GPU = 4096
 LARGE_N = 262144
 SIM_BYTES_PER_ENV = 376          # simulate share of the 688 B/env-step
+# with the refresh fused into the step (STEP_FUSION_STEP_OUT) the kernel also
+# writes each body's rigid-body row and its actor's root row: + 2 x (52 + 52) B
+SIM_OUT_BYTES_PER_ENV = SIM_BYTES_PER_ENV + 2 * (52 + 52)
 STEP_BYTES_PER_ENV = 688         # whole tensor-API step
 S2_BYTES_PER_ENV = 532           # SURVEY.md §8d S2 (servo-arm gimbal)
 S2_LARGE_N = 262144
@@ -148,8 +152,10 @@ def kernel_stats(sim, n_launches, run):
 
 STEP_FUSION_NOTE = ("opt-in step fusion (gym.set_step_fusion(sim, STEP_FUSION_ALL)): every step writes the "
                     "action into the source before its set and never touches it again before simulate, so "
-                    "the deferred read equals Isaac Gym's copy-at-set (checked by version counters); off by "
-                    "default in the library")
+                    "the deferred read equals Isaac Gym's copy-at-set (checked by version counters); the step "
+                    "kernel writes the bound root / rigid-body tensors itself and the refreshes after it "
+                    "launch nothing (STEP_OUT); every API call of the loop is still made; off by default "
+                    "in the library")
 
 
 def fuse_in_capture(sim):
@@ -173,8 +179,11 @@ def load_pmc(name):
     return None, None
 
 
-def rigid_roofline(n, kern_ms, kmin, launches, segment):
-    bytes_launch = SIM_BYTES_PER_ENV * n
+def rigid_roofline(n, kern_ms, kmin, launches, segment, step_out=True):
+    """step_out: the timed launches ran with STEP_FUSION_STEP_OUT (the kernel
+    writes the bound rigid-body and root tensors: SIM_OUT_BYTES_PER_ENV)."""
+    bpe = SIM_OUT_BYTES_PER_ENV if step_out else SIM_BYTES_PER_ENV
+    bytes_launch = bpe * n
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms else None
     pmc, pmc_file = load_pmc("rigid_%d" % n)
     return {"bound": "hbm", "kernel": "k_rigid_step1",
@@ -183,7 +192,10 @@ def rigid_roofline(n, kern_ms, kmin, launches, segment):
             "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
             "traffic_source": pmc_file,
             "algorithmic_bytes_per_launch": bytes_launch,
-            "algorithmic_bytes_per_env": SIM_BYTES_PER_ENV,
+            "algorithmic_bytes_per_env": bpe,
+            "algorithmic_bytes_note": ("376 B simulate share (SURVEY.md §8d) + the rigid-body and root rows the "
+                                       "kernel writes with the refresh fused into it (2 x (52 + 52) B)"
+                                       if step_out else "376 B simulate share (SURVEY.md §8d)"),
             "kernel_ms_avg": kern_ms, "kernel_ms_min": kmin, "kernel_launches_timed": launches,
             "kernel_timing": "dispatch timestamps of every k_rigid_step launch (hipExtLaunchKernelGGL start/stop "
                              "events, the interval rocprofv3 reports) over %s" % segment}
@@ -607,7 +619,7 @@ def large_n_rate(n, steps, dev, use_graph=True):
             "roofline": rigid_roofline(n, kms, kmin, used, "%d eager steps after a 10-step warm-up" % used),
             "roofline_unfused": rigid_roofline(n, ukms, ukmin, uused,
                                                "%d eager steps with step fusion off (scatter launch, then the "
-                                               "step kernel on the SoA state)" % uused)}
+                                               "step kernel on the SoA state)" % uused, step_out=False)}
 
 
 # --------------------------------------------------------------------------- dry run (no GPU)

@@ -323,6 +323,15 @@ float       mg_last_render_ms(mg_sim* sim);
  * it the caller guarantees every captured set is consumed by a simulate in the
  * same capture (e.g. set -> simulate -> refresh per captured step, as bench.py). */
 #define MG_FUSE_IN_CAPTURE  8
+/* MG_FUSE_STEP_OUT: with targets bound by mg_bind_refresh_targets, on a sim whose
+ * bodies are all single-shape free bodies and actor roots (the servo scene),
+ * mg_simulate's step kernel writes the new state into the bound root and
+ * rigid-body tensors itself, and a refresh of either bound tensor is then served
+ * without a launch while no set has changed the state (the refresh fused into
+ * the step). The bound tensors thus hold the new state from the simulate on, not
+ * from the refresh; the gymapi layer rebinds (forcing a gather) when a bound
+ * tensor was written between the simulate and its refresh. */
+#define MG_FUSE_STEP_OUT    16
 int32_t     mg_set_fusion(mg_sim* sim, int32_t flags);
 int32_t     mg_bind_refresh_targets(mg_sim* sim, float* root_dst, float* rigid_body_dst);
 

@@ -57,6 +57,9 @@ def main():
         a = sys.argv
         return other_kernel(f, nf, w, envs, out, a[a.index("--kernel") + 1], int(a[a.index("--bytes-per-env") + 1]),
                             a[a.index("--factor-from") + 1])
+    # bench.py's S1 kernel: 376 B simulate share + 208 B of rigid-body and root
+    # rows with the refresh fused into the step (STEP_FUSION_STEP_OUT, bench default)
+    bpe = int(sys.argv[sys.argv.index("--bytes-per-env") + 1]) if "--bytes-per-env" in sys.argv else 584
     actors = 2 * envs
     # bench.py --pmc-calibrate: indexed sets of every actor (the fused step reads a
     # full set itself): the (2N, 13) rows, the int32 selection and root-body index
@@ -73,7 +76,8 @@ def main():
         "calibration": "k_scatter_rows reads %d B per launch; FETCH_SIZE %.1f KiB" % (known_read,
                                                                                    f["k_scatter_rows"]),
         "hbm_bytes_per_launch": rigid_read + rigid_write,
-        "algorithmic_bytes_per_launch": 376 * envs,
+        "algorithmic_bytes_per_launch": bpe * envs,
+        "algorithmic_bytes_per_env": bpe,
         "launches": nf["k_rigid_step"],
         "all_kernels_fetch_kib": f,
         "all_kernels_write_kib": w,

@@ -147,8 +147,9 @@ class Sim:
         self.epoch = 0
         self.held_src = []     # fused sets: (tensor, torch version at the set, setter), until the next simulate
         # step fusion (gym.set_step_fusion; opt-in, MIGYM_STEP_FUSION sets the default)
-        self.fusion = int(os.environ.get("MIGYM_STEP_FUSION", "0") or 0) & 15
+        self.fusion = int(os.environ.get("MIGYM_STEP_FUSION", "0") or 0) & 31
         self.rb_paired_version = None   # rb tensor version after a fused root refresh filled it
+        self.root_out_version = None    # root tensor version after a simulate wrote it (STEP_OUT)
         self.mm_cache = {}
         self._renderer = None
         self.cam_version = 0       # bumped by every camera change (render tables are rebuilt)

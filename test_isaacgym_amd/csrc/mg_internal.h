@@ -61,6 +61,12 @@ struct MgRigidArgs {
     int          ntb;         // template bodies
     const float* root_src;    // fused root-state set: [na][13] rows, or null
     const int*   root_row;    // [nb] internal slot -> actor row of root_src (-1: none)
+    // refresh fused into the step (MG_FUSE_STEP_OUT): the bound rigid-body and
+    // root tensors written by the step kernel itself, or null
+    float*       out_rb;      // [nb][13] rigid-body tensor (global body order)
+    float*       out_root;    // [na][13] actor root tensor
+    const int*   out_body;    // [nb] internal slot -> global body (rigid-body row)
+    const int*   out_root_row;// [nb] internal slot -> actor row (-1: not a root)
 };
 
 // Articulation step arguments (lane = articulation instance).

@@ -748,9 +748,16 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
 // __launch_bounds__(64, 3): at most 168 VGPRs, so three waves share a SIMD in
 // large launches (the Gauss-Seidel chains are latency-bound: more resident
 // waves, not more lanes, fill the SIMD); free of scratch at that budget. The
-// general ground basis needs more registers: two waves.
+// packed-pair variant of one-round launches spills 24 B/lane at 168 VGPRs; a
+// two-wave budget (171 VGPRs, no scratch) measured slower on the same box
+// (4096 envs: min 9.96 vs 9.20 us, tools/kbench.py A/B, r03), so it keeps three.
+// The general ground basis needs more registers: two waves.
+#ifndef MG_RIGID1_ROUND_WAVES
+#define MG_RIGID1_ROUND_WAVES 3
+#endif
 template <bool UPZ, bool LDS_T, bool WIDE>
-__global__ void __launch_bounds__(64, UPZ ? 3 : 2) k_rigid_step1(MgStep P, MgRigidArgs A) {
+__global__ void __launch_bounds__(64, UPZ && WIDE ? 3 : (UPZ ? MG_RIGID1_ROUND_WAVES : 2))
+k_rigid_step1(MgStep P, MgRigidArgs A) {
     extern __shared__ float s_trec[];
     const int i = (WIDE ? gridDim.x - 1 - blockIdx.x : blockIdx.x) * 64 + threadIdx.x;
     const bool live = i < A.nf;
@@ -823,6 +830,21 @@ __global__ void __launch_bounds__(64, UPZ ? 3 : 2) k_rigid_step1(MgStep P, MgRig
     A.cforce[0 * nb + bo] = fsum.x * P.inv_dt;
     A.cforce[1 * nb + bo] = fsum.y * P.inv_dt;
     A.cforce[2 * nb + bo] = fsum.z * P.inv_dt;
+    if (A.out_rb) {
+        // the refresh fused into the step: the same 13 values into the bound
+        // rigid-body row and, for a root body, its actor's root row (the rows the
+        // paired gather k_gather_rb_root would write from the SoA state)
+        const float o[MG_STATE_N] = {x.x, x.y, x.z, q.x, q.y, q.z, q.w, v.x, v.y, v.z, w.x, w.y, w.z};
+        float* R = A.out_rb + (size_t)A.out_body[bo] * MG_STATE_N;
+#pragma unroll
+        for (int k = 0; k < MG_STATE_N; ++k) R[k] = o[k];
+        const int rr = A.out_root_row[bo];
+        if (rr >= 0) {
+            float* Ro = A.out_root + (size_t)rr * MG_STATE_N;
+#pragma unroll
+            for (int k = 0; k < MG_STATE_N; ++k) Ro[k] = o[k];
+        }
+    }
 }
 
 template <bool UPZ, int MAXC, bool MULTI>
@@ -867,6 +889,7 @@ hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream
     const bool upz = mg_step_is_upz(P);
     MgRigidArgs A1 = A, A2 = A;
     A2.root_src = nullptr;   // fused root sets only with single-shape bodies (migym_capi.cpp)
+    A2.out_rb = nullptr;     // so is the fused refresh (MG_FUSE_STEP_OUT)
     A1.nf = A.nf1;
     A2.nf = A.nf - A.nf1;
     if (A.free_ids) {
@@ -884,8 +907,8 @@ hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream
         // CU). Such a launch is issue-bound, not latency-bound: it dispatches
         // longest-first (back to front: the free-body order, migym_capi.cpp) and
         // solves with the scalar rows (tgs_z's packed pairs save latency, not
-        // issue slots: tools/gpu_ab_var.sh).
-        const bool wide = blocks > mg_cu_count() * 4 * (upz ? 3 : 2);
+        // issue slots: DESIGN.md §3.2).
+        const bool wide = blocks > mg_cu_count() * 4 * (upz ? MG_RIGID1_ROUND_WAVES : 2);
         const size_t lds = (size_t)A.ntb * MG_TREC_N * sizeof(float);
 #define MG_K1(U, L) \
     do { \

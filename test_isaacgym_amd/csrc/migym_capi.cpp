@@ -116,7 +116,8 @@ struct mg_sim {
     unsigned long long pend_root_cap = 0, pend_tgt_cap[3] = {0, 0, 0}, rb_cap = 0;
     float* bind_root = nullptr;
     float* bind_rb = nullptr;
-    long long state_gen = 0, rb_gen = -1;
+    long long state_gen = 0, rb_gen = -1, out_gen = -1;   // out_gen: bound tensors written by the step
+    unsigned long long out_cap = 0;
     int* d_actor_dof = nullptr;   // [na+1]
     float* d_cforce = nullptr;    // [3][nb]
     float* d_ext = nullptr;       // [6][nb]
@@ -996,6 +997,11 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         hipError_t e = mg_launch_env_step(P, A, st);
         if (e != hipSuccess) return fail(MG_ERR_DEVICE, "coupled env step launch: %s", hipGetErrorString(e));
     }
+    // the refresh fused into the step (MG_FUSE_STEP_OUT): every body is a
+    // single-shape free body and actor root of this launch
+    const unsigned long long step_cid = capture_id(st);
+    const bool step_out = (s->fusion & MG_FUSE_STEP_OUT) && fuse_here(s, step_cid) && s->bind_root && s->bind_rb &&
+                          s->roots_free && s->nf1 == s->nb && s->na > 0;
     if (s->nf_rigid > 0) {
         MgRigidArgs A{};
         A.nf = s->nf_rigid; A.nf1 = s->nf1; A.nb = s->nb; A.free_ids = nullptr;   // internal slots 0..nf-1
@@ -1009,6 +1015,12 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
             A.root_row = s->d_root_row;
             s->pend_root = nullptr;
         }
+        if (step_out) {
+            A.out_rb = s->bind_rb;
+            A.out_root = s->bind_root;
+            A.out_body = s->d_free_global;     // internal slot -> global body
+            A.out_root_row = s->d_root_row;
+        }
         HIP_TRY(mg_launch_rigid_step(P, A, st));
     }
     if (int rc_ = flush_root(s, st)) return rc_;   // a root set with no free-body launch
@@ -1017,6 +1029,10 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
             if (int rc_ = flush_tgt(s, k, st)) return rc_;
     for (int k = 0; k < 3; ++k) s->pend_tgt[k] = nullptr;   // read (and written through) by the step
     s->state_gen++;
+    if (step_out) {
+        s->out_gen = s->rb_gen = s->state_gen;
+        s->out_cap = s->rb_cap = step_cid;
+    }
     if (s->ext_pending) {
         HIP_TRY(hipMemsetAsync(s->d_ext, 0, (size_t)s->nb * 6 * sizeof(float), st));
         s->ext_pending = false;
@@ -1047,7 +1063,7 @@ int32_t mg_fetch_results(mg_sim* s, int32_t wait) {
 int32_t mg_set_fusion(mg_sim* s, int32_t flags) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
     const int32_t prev = s->fusion;
-    s->fusion = flags & (MG_FUSE_ROOT_SET | MG_FUSE_REFRESH | MG_FUSE_DOF_TARGETS | MG_FUSE_IN_CAPTURE);
+    s->fusion = flags & (MG_FUSE_ROOT_SET | MG_FUSE_REFRESH | MG_FUSE_DOF_TARGETS | MG_FUSE_IN_CAPTURE | MG_FUSE_STEP_OUT);
     return prev;
 }
 
@@ -1056,6 +1072,7 @@ int32_t mg_bind_refresh_targets(mg_sim* s, float* root_dst, float* rigid_body_ds
     s->bind_root = root_dst;
     s->bind_rb = rigid_body_dst;
     s->rb_gen = -1;
+    s->out_gen = -1;
     return MG_OK;
 }
 
@@ -1112,6 +1129,9 @@ int32_t mg_refresh_actor_root_state(mg_sim* s, float* dst, int32_t dst_host, voi
     HIP_TRY(hipSetDevice(s->device));
     if (int rc_ = flush_root(s, st)) return rc_;
     const unsigned long long cid = capture_id(st);
+    if (!dst_host && dst && dst == s->bind_root && (s->fusion & MG_FUSE_STEP_OUT) && s->out_gen == s->state_gen &&
+        s->out_cap == cid)
+        return MG_OK;   // written by the step kernel (MG_FUSE_STEP_OUT)
     if (!dst_host && dst && dst == s->bind_root && s->bind_rb && (s->fusion & MG_FUSE_REFRESH) &&
         fuse_here(s, cid) && s->na > 0) {
         // the bound root and rigid-body tensors in one launch
@@ -1130,8 +1150,9 @@ int32_t mg_refresh_rigid_body_state(mg_sim* s, float* dst, int32_t dst_host, voi
     HIP_TRY(hipSetDevice(s->device));
     if (int rc_ = flush_root(s, st)) return rc_;
     const bool bound = !dst_host && dst && dst == s->bind_rb;
-    if (bound && (s->fusion & MG_FUSE_REFRESH) && s->rb_gen == s->state_gen && s->rb_cap == capture_id(st))
-        return MG_OK;   // served by the paired gather of the same capture (or eagerly)
+    if (bound && (s->fusion & (MG_FUSE_REFRESH | MG_FUSE_STEP_OUT)) && s->rb_gen == s->state_gen &&
+        s->rb_cap == capture_id(st))
+        return MG_OK;   // served by the paired gather / the step kernel of the same capture (or eagerly)
     const int rc = refresh_rows(s, s->d_state, s->nb, MG_STATE_N, s->d_perm, s->nb, dst, dst_host, st);
     if (rc == MG_OK && bound) {
         s->rb_gen = s->state_gen;

@@ -67,7 +67,8 @@ STEP_FUSION_ROOT_SET = 1
 STEP_FUSION_REFRESH = 2
 STEP_FUSION_DOF_TARGETS = 4
 STEP_FUSION_IN_CAPTURE = 8
-STEP_FUSION_ALL = 15
+STEP_FUSION_STEP_OUT = 16
+STEP_FUSION_ALL = 31
 
 
 _FUSED_KIND = {"mg_set_actor_root_state": "root", "mg_set_dof_position_target": "tgt0",
@@ -166,6 +167,11 @@ class Gym:
         _check_held(sim, "simulate")
         N.check(N.lib.mg_simulate(h, sim.stream()), "mg_simulate")
         sim.held_src = []
+        if sim.fusion & STEP_FUSION_STEP_OUT and "root" in sim.tensors:
+            # the step kernel may have written the bound root / rigid-body tensors
+            # (MG_FUSE_STEP_OUT): a write to them before their refresh forces a gather
+            sim.root_out_version = sim.tensors["root"]._version
+            sim.rb_paired_version = sim.tensors["rb"]._version
         sim.epoch += 1
         sim.frame += 1
         sim.time += sim.params.dt
@@ -175,8 +181,10 @@ class Gym:
         (include/migym.h mg_set_fusion; STEP_FUSION_* flags, 0 = off, the
         default). With it, a full device-resident set_actor_root_state_tensor /
         set_dof_*_target_tensor / set_dof_actuation_force_tensor is read by the
-        next simulate instead of at the set call, and a root-state refresh also
-        refreshes the rigid-body tensor. Isaac Gym copies the source at the set
+        next simulate instead of at the set call, a root-state refresh also
+        refreshes the rigid-body tensor (STEP_FUSION_REFRESH), and on a sim of
+        single-shape free bodies simulate writes both state tensors itself, the
+        refreshes then launching nothing (STEP_FUSION_STEP_OUT). Isaac Gym copies the source at the set
         call (SURVEY.md §8b Ownership), so a source written between its set and
         the simulate that consumes it raises MigymError instead of being read
         (torch version counters); the environment variable MIGYM_STEP_FUSION sets
@@ -859,11 +867,16 @@ class Gym:
         h = sim.require_native(what)
         if key in ("root", "rb"):
             _check_held(sim, what, ("root",))      # flushes a pending root set
-        if key == "rb" and sim.rb_paired_version is not None and t._version != sim.rb_paired_version:
-            # the user wrote the rigid-body tensor after the paired root refresh
-            # filled it: re-gather it (rebinding clears the served-by-root mark)
-            N.check(N.lib.mg_bind_refresh_targets(h, sim.tensors["root"].data_ptr(), t.data_ptr()),
+        stale = ((key == "rb" and sim.rb_paired_version is not None and t._version != sim.rb_paired_version) or
+                 (key == "root" and sim.root_out_version is not None and t._version != sim.root_out_version))
+        if stale:
+            # the user wrote the tensor after the paired root refresh or the step
+            # (STEP_FUSION_STEP_OUT) filled it: re-gather it (rebinding clears the
+            # served-without-launch marks)
+            N.check(N.lib.mg_bind_refresh_targets(h, sim.tensors["root"].data_ptr(), sim.tensors["rb"].data_ptr()),
                     "mg_bind_refresh_targets")
+        if key == "root":
+            sim.root_out_version = None
         N.check(fn(h, t.data_ptr(), 1 if t.device.type == "cpu" else 0, sim.stream()), what)
         if key == "root" and sim.fusion & STEP_FUSION_REFRESH:
             sim.rb_paired_version = sim.tensors["rb"]._version

@@ -134,6 +134,70 @@ def test_fused_step_matches_unfused(gym):
     assert torch.equal(root, want)
 
 
+def test_step_out_fusion(gym):
+    """STEP_FUSION_STEP_OUT (the refresh fused into the step, include/migym.h
+    MG_FUSE_STEP_OUT): simulate writes the bound root and rigid-body tensors
+    itself. Eager and in a captured hipGraph the tensors equal the unfused
+    set / simulate / refresh sequence bit for bit; a tensor the user writes
+    between simulate and its refresh is re-gathered by the refresh (Isaac Gym's
+    refresh overwrites it); the rigid-body refresh serves the step's rows."""
+    n, steps, chunk = 256, 12, 4
+    acts = scenes.servo_actions(n, steps, DEV, seed=11)
+    sims = []
+    for fusion in (gymapi.STEP_FUSION_ALL, 0):
+        sim, _ = scenes.servo_scene(gym, n)
+        gym.prepare_sim(sim)
+        gym.set_step_fusion(sim, fusion)
+        sims.append((sim, _tensors(gym, sim)))
+        gym.refresh_actor_root_state_tensor(sim)
+
+    def step(sim, root, k):
+        root[:, 3:10] = acts[k]
+        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.simulate(sim)
+        gym.fetch_results(sim, False)
+        gym.refresh_actor_root_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+
+    (sa, (ra, rba, _, _)), (sb, (rb_, rbb, _, _)) = sims
+    for k in range(chunk):            # eager
+        step(sa, ra, k)
+        step(sb, rb_, k)
+        torch.cuda.synchronize()
+        assert torch.equal(ra, rb_) and torch.equal(rba, rbb), "eager step %d" % k
+    # captured: `chunk` steps per graph, replayed; the unfused sim steps eagerly
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            for j in range(chunk):
+                step(sa, ra, chunk + j)
+    torch.cuda.current_stream().wait_stream(side)
+    g.replay()
+    for j in range(chunk):
+        step(sb, rb_, chunk + j)
+    torch.cuda.synchronize()
+    assert torch.equal(ra, rb_) and torch.equal(rba, rbb), "captured steps"
+    # a write between simulate and refresh: the refresh restores the state
+    for sim, (root, rb, _, _) in sims:
+        root[:, 3:10] = acts[2 * chunk]
+        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.simulate(sim)
+        root.fill_(-3.0)
+        rb[:, 5] = 9.0
+        gym.refresh_actor_root_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+    torch.cuda.synchronize()
+    assert torch.equal(ra, rb_) and torch.equal(rba, rbb), "refresh after a user write"
+    assert not torch.any(ra == -3.0)
+    # the refreshes after the step read the same rows the step wrote
+    roots = torch.as_tensor(sa.model_arrays["actor_root_body"], device=DEV, dtype=torch.long)
+    assert torch.equal(rba[roots], ra)
+    for sim, _ in sims:
+        gym.destroy_sim(sim)
+
+
 def test_step_fusion_copy_at_set_contract(gym):
     """Isaac Gym reads a set_*_tensor source during the set call (SURVEY.md §8b
     Ownership). With step fusion off (the default) a source written after its
