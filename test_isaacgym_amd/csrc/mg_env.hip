@@ -31,7 +31,7 @@
 
 #ifdef MG_ENV_PHASE_TIMING
 // profiling build only: per-phase shader-clock cycles summed over waves
-__device__ unsigned long long g_env_phase[16];
+__device__ unsigned long long g_env_phase[24];
 #define PH_T0() unsigned long long ph_t = clock64()
 #define PH_MARK(k) do { const unsigned long long t_ = clock64(); \
     if (threadIdx.x == 0) atomicAdd(&g_env_phase[k], t_ - ph_t); ph_t = t_; } while (0)
@@ -42,7 +42,7 @@ extern "C" int mg_debug_env_phase(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_env_phase), sizeof(g_env_phase)) == hipSuccess ? 0 : -1;
 }
 extern "C" int mg_debug_env_phase_reset(void) {
-    unsigned long long z[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[24] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_env_phase), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #else
@@ -50,6 +50,16 @@ extern "C" int mg_debug_env_phase_reset(void) {
 #define PH_MARK(k) do { } while (0)
 #define PH_COUNT(k, v) do { } while (0)
 #define PH_SUB(k) do { } while (0)
+#endif
+// np_collide's parts (profiling build): pair setup, one-lane pair tests, the
+// cooperative convex loop, contact placement
+#ifdef MG_ENV_PHASE_TIMING
+#define PH_NP0() unsigned long long ph_np = clock64()
+#define PH_NP(k) do { const unsigned long long t_ = clock64(); \
+    if (threadIdx.x == 0) atomicAdd(&g_env_phase[k], t_ - ph_np); ph_np = t_; } while (0)
+#else
+#define PH_NP0() do { } while (0)
+#define PH_NP(k) do { } while (0)
 #endif
 
 namespace {
@@ -312,7 +322,8 @@ __device__ __forceinline__ void coop_vertices(const CShape& X, const CShape& Y, 
 }
 // every lane of the group calls it with the same pair (group-uniform control)
 template <int G>
-__device__ void coop_convex_convex(const CShape& A, const CShape& B, float margin, int ln, int gi, PairOut& o) {
+__device__ __forceinline__ void coop_convex_convex(const CShape& A, const CShape& B, float margin, int ln, int gi,
+                                                   PairOut& o) {
 #ifdef MG_ENV_PHASE_TIMING
     unsigned long long ph_sub = clock64();
 #endif
@@ -1155,6 +1166,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             __syncthreads();
             PH_MARK(8);
             for (int rb = 0; __any(rb < nnear); rb += G) {
+                PH_NP0();
                 PairOut o;
                 o.n = 0;
                 float mu = 0.0f, rest = 0.0f;
@@ -1191,6 +1203,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         rest = 0.5f * (sha[12] + shb[12]);
                     }
                 }
+                PH_NP(18);
                 // this round's convex pairs, one at a time on the whole group (in
                 // lane order; the result goes to the pair's own lane)
                 unsigned long long cm = grp_ballot<G>(coop, gi);
@@ -1201,8 +1214,10 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         PairOut t;
                         coop_convex_convex<G>(shfl_shape<G>(cA, k), shfl_shape<G>(cB, k), P.contact_offset, ln, gi, t);
                         if (ln == k) o = t;
+                        if (ln == k) PH_COUNT(16, t.n == 0 ? 1 : 0);   // convex pairs without a contact
                     }
                 }
+                PH_NP(19);
                 // exclusive prefix sum of the counts over the 16 lanes
                 int incl = o.n;
 #pragma unroll
@@ -1228,6 +1243,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     }
                 }
                 base += total;
+                PH_NP(20);
             }
             __syncthreads();
             PH_MARK(9);

@@ -51,12 +51,13 @@ def run(n, warm=150, steps=100):
             used = N.lib.mg_step_time_stats(sim.native, steps, ctypes.byref(avg), ctypes.byref(lo), None)
             phases = None
             if hasattr(N.lib, "mg_debug_env_phase"):
-                buf = (ctypes.c_ulonglong * 16)()
+                buf = (ctypes.c_ulonglong * 24)()
                 N.lib.mg_debug_env_phase(buf)
                 waves = (n + 3) // 4
                 names = ["unconstrained", "narrowphase_rest", "crba_minv", "rows", "tgs", "integrate", "setup",
                          "outputs", "np_screen", "np_collide", "pairs_tested", "pairs_with_hull",
-                         "coop_vertices", "coop_edges", "coop_merge", "coop_edge_passes"]
+                         "coop_vertices", "coop_edges", "coop_merge", "coop_edge_passes",
+                         "coop_pairs_no_contact", "unused17", "np_setup_and_one_lane_tests", "np_coop_loop", "np_placement"]
                 phases = {nm: buf[i] / waves / steps for i, nm in enumerate(names)}   # cycles per wave per frame
         if k == warm - 1 and hasattr(N.lib, "mg_debug_env_phase_reset"):
             torch.cuda.synchronize()
