@@ -123,7 +123,11 @@ typedef struct mg_sim_params {
     float   ground_static_friction;
     float   ground_dynamic_friction;
     float   ground_restitution;
-    int32_t reserved[8];
+    float   friction_offset_threshold;      /* PhysXParams.friction_offset_threshold: contacts farther apart
+                                               than this do not seed friction anchors */
+    float   friction_correlation_distance;  /* PhysXParams.friction_correlation_distance: anchor spacing and
+                                               the drift at which an anchor is dropped */
+    int32_t reserved[6];
 } mg_sim_params;
 
 /* The packed scene, built by the host scene builder at prepare_sim / first

@@ -8,6 +8,7 @@ header of migym_oracle.c and DESIGN.md §4.
 import ctypes
 import os
 import subprocess
+import weakref
 
 import numpy as np
 
@@ -25,9 +26,9 @@ def _load():
     lib = ctypes.CDLL(LIB)
     vp = ctypes.c_void_p
     lib.oracle_step.restype = ctypes.c_int
-    lib.oracle_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
+    lib.oracle_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
     lib.oracle_step_mt.restype = ctypes.c_int
-    lib.oracle_step_mt.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
+    lib.oracle_step_mt.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
     return lib
 
 
@@ -45,12 +46,39 @@ def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
-def step(sim_params, model, state, dof, tgt=None, props=None, ext=None, cforce=None, body_range=None):
+# The coupled step's friction patches are simulation state
+# kept from step to step, as the device keeps them: one float32 row of
+# FC_N = 128 pairs x (16 + 1) floats per env (migym_oracle_env.c OE_FC_N).
+FC_N = 128 * (16 + 1)
+_caches = {}
+
+
+def contact_cache(model):
+    """A fresh (no patch yet) friction-patch cache for `model`."""
+    return np.zeros((max(int(model.num_envs), 1), FC_N), dtype=np.float32)
+
+
+def _cache_for(state, model):
+    """The cache that goes with a state array: the one a caller stepping the
+    same `state` in place used on the previous step (the device keeps its
+    patches inside the sim the same way)."""
+    key = id(state)
+    ent = _caches.get(key)
+    if ent is not None and ent[0]() is state and ent[1].shape[0] >= int(model.num_envs):
+        return ent[1]
+    c = contact_cache(model)
+    _caches[key] = (weakref.ref(state, lambda _r, k=key: _caches.pop(k, None)), c)
+    return c
+
+
+def step(sim_params, model, state, dof, tgt=None, props=None, ext=None, cforce=None, body_range=None,
+         contact_cache=None):
     """One gym.simulate() on the host, in place.
 
     sim_params: _native.MgSimParams; model: _native.MgModel (its arrays alive);
     state [nb,13] f32, dof [nd,2] f32 (updated in place); tgt [nd,3]; props [nd,12];
-    ext [nb,6]; cforce [nb,3] (written). Returns cforce.
+    ext [nb,6]; cforce [nb,3] (written); contact_cache: the friction patches
+    (default: the ones kept with this `state` array). Returns cforce.
     """
     nb = state.shape[0]
     nd = dof.shape[0]
@@ -66,14 +94,18 @@ def step(sim_params, model, state, dof, tgt=None, props=None, ext=None, cforce=N
     props_c = None if props is None else np.ascontiguousarray(props, dtype=np.float32)
     ext_c = None if ext is None else np.ascontiguousarray(ext, dtype=np.float32)
     assert cforce.dtype == np.float32 and cforce.flags.c_contiguous and cforce.shape == (nb, 3)
+    fc = _cache_for(state, model) if contact_cache is None else contact_cache
+    assert fc.dtype == np.float32 and fc.flags.c_contiguous and fc.shape[1] == FC_N
+    assert fc.shape[0] >= int(model.num_envs)
     rc = lib().oracle_step(ctypes.addressof(sim_params), ctypes.addressof(model), _ptr(state), _ptr(dof),
-                           _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), int(b0), int(b1))
+                           _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), _ptr(fc), int(b0), int(b1))
     if rc != 0:
         raise RuntimeError("oracle_step: unsupported model")
     return cforce
 
 
-def step_threads(sim_params, model, state, dof, nthreads, tgt=None, props=None, ext=None, cforce=None):
+def step_threads(sim_params, model, state, dof, nthreads, tgt=None, props=None, ext=None, cforce=None,
+                 contact_cache=None):
     """step() on `nthreads` host threads (oracle_step_mt, OpenMP): the same
     result; the CPU baseline of bench.py."""
     nb, nd = state.shape[0], dof.shape[0]
@@ -86,8 +118,9 @@ def step_threads(sim_params, model, state, dof, nthreads, tgt=None, props=None, 
     tgt_c = np.ascontiguousarray(tgt, dtype=np.float32)
     props_c = None if props is None else np.ascontiguousarray(props, dtype=np.float32)
     ext_c = None if ext is None else np.ascontiguousarray(ext, dtype=np.float32)
+    fc = _cache_for(state, model) if contact_cache is None else contact_cache
     rc = lib().oracle_step_mt(ctypes.addressof(sim_params), ctypes.addressof(model), _ptr(state), _ptr(dof),
-                              _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), int(nthreads))
+                              _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), _ptr(fc), int(nthreads))
     if rc != 0:
         raise RuntimeError("oracle_step_mt: unsupported model")
     return cforce

@@ -134,6 +134,7 @@ typedef struct {
     int ground;
     v3_t n, t1, t2;
     float pd, mu_g, e_g;
+    float fot, corr;   /* friction_offset_threshold, friction_correlation_distance (friction anchors) */
 } step_t;
 
 static step_t make_step_(const mg_sim_params* p) {
@@ -164,6 +165,8 @@ static step_t make_step_(const mg_sim_params* p) {
     P.t2 = V(ny * t1z - nz * t1y, nz * t1x - nx * t1z, nx * t1y - ny * t1x);
     P.mu_g = p->ground_dynamic_friction;
     P.e_g = p->ground_restitution;
+    P.fot = p->friction_offset_threshold;
+    P.corr = p->friction_correlation_distance;
     return P;
 }
 
@@ -693,12 +696,14 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
  * One gym.simulate() over the whole model, AoS host arrays:
  *   state [nb][13] in/out, dof [nd][2] in/out, tgt [nd][3] (target pos, target
  *   vel, actuation force), props [nd][12] (NULL = model->dof_props),
- *   ext [nb][6] world force/torque at the COM or NULL, cforce [nb][3] out.
+ *   ext [nb][6] world force/torque at the COM or NULL, cforce [nb][3] out,
+ *   fcache: the coupled step's friction patches, [num_envs][OE_FC_N] floats
+ *   kept by the caller from step to step (zeros: no patch yet; NULL: none kept).
  * Bodies in [body_begin, body_end) only (a bounded CPU-baseline sample);
  * articulations are stepped when their root lies in that range. Returns 0, or
  * -1 for an unsupported model. */
 int oracle_step(const mg_sim_params* p, const mg_model* m, float* state, float* dof, const float* tgt,
-                const float* props, const float* ext, float* cforce, int body_begin, int body_end) {
+                const float* props, const float* ext, float* cforce, float* fcache, int body_begin, int body_end) {
     step_t P = make_step_(p);
     int b, k, ne, rc = 0;
     oenv_t* envs = NULL;
@@ -713,7 +718,7 @@ int oracle_step(const mg_sim_params* p, const mg_model* m, float* state, float* 
     for (k = 0; k < ne; ++k) {
         const int first = envs[k].art_body >= 0 ? envs[k].art_body : envs[k].free_b[0];
         if (first < body_begin || first >= body_end) continue;
-        if (env_step_(&P, m, &envs[k], state, dof, tgt, props, ext, cforce) != 0) { rc = -1; goto done; }
+        if (env_step_(&P, m, &envs[k], state, dof, tgt, props, ext, cforce, fcache) != 0) { rc = -1; goto done; }
     }
     for (k = 0; k < m->num_artics; ++k) {
         const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;
@@ -736,7 +741,7 @@ done:
  * and free bodies are independent, so each of the three loops is split across
  * the threads after one classification; results equal oracle_step's. */
 int oracle_step_mt(const mg_sim_params* p, const mg_model* m, float* state, float* dof, const float* tgt,
-                   const float* props, const float* ext, float* cforce, int nthreads) {
+                   const float* props, const float* ext, float* cforce, float* fcache, int nthreads) {
     step_t P = make_step_(p);
     int ne, rc = 0;
     oenv_t* envs = NULL;
@@ -755,7 +760,7 @@ int oracle_step_mt(const mg_sim_params* p, const mg_model* m, float* state, floa
             int k, b;
 #pragma omp for schedule(dynamic, 16)
             for (k = 0; k < ne; ++k)
-                if (env_step_(&P, m, &envs[k], state, dof, tgt, props, ext, cforce) != 0) bad = 1;
+                if (env_step_(&P, m, &envs[k], state, dof, tgt, props, ext, cforce, fcache) != 0) bad = 1;
 #pragma omp for schedule(static)
             for (k = 0; k < m->num_artics; ++k) {
                 const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;

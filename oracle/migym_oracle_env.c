@@ -14,6 +14,13 @@
 #define OE_MAXCT 48   /* storage; an env uses MAXCT = 16, or 48 when 64 lanes wide (MG_ENV_MAXCT[_WIDE]) */
 #define OE_F0 64      /* participant ids (mg_internal.h MG_ENV_FREE0 ...) */
 #define OE_PMAX 4
+/* friction patches (mg_internal.h MG_FP_*): record floats, pairs per env that
+ * keep theirs, normal tolerance; the cache row of an env holds OE_FPP records
+ * of OE_FP_N floats plus a held flag each */
+#define OE_FP_N 16
+#define OE_FPP 128
+#define OE_FP_COS 0.999f
+#define OE_FC_N (OE_FPP * (OE_FP_N + 1))
 
 typedef struct { int type; v3_t c; m3_t R; v3_t h; const float* hv; } cshape_t;
 typedef struct { int n; v3_t p[OE_PMAX]; v3_t nrm[OE_PMAX]; float sep[OE_PMAX]; } pair_t;
@@ -491,8 +498,64 @@ static int sphere_near_box_(v3_t c, float r, const float* shb, v3_t xb, q4_t qb,
     const float rr = r + off;
     return dot3(e, e) < rr * rr * 1.0001f + 1e-6f;
 }
+/* shape-frame box of a box / hull (migym_capi.cpp shape_obb): o[0..2] centre, o[3..5] half extents */
+static void shape_obb_(const float* sh, const float* hulls, float* o) {
+    int k, i, c;
+    for (k = 0; k < 6; ++k) o[k] = 0.0f;
+    if ((int)sh[0] == MG_SHAPE_CONVEX) {
+        const float* hv = hulls + (int)sh[2];
+        const int nv = (int)hv[0];
+        float lo[3], hi[3];
+        for (c = 0; c < 3; ++c) { lo[c] = hv[MG_HULL_HEADER + c]; hi[c] = lo[c]; }
+        for (i = 1; i < nv; ++i)
+            for (c = 0; c < 3; ++c) {
+                const float v = hv[MG_HULL_HEADER + 3 * i + c];
+                lo[c] = v < lo[c] ? v : lo[c];
+                hi[c] = hi[c] < v ? v : hi[c];
+            }
+        for (c = 0; c < 3; ++c) { o[c] = 0.5f * (lo[c] + hi[c]); o[3 + c] = 0.5f * (hi[c] - lo[c]); }
+    } else {   /* box (the screen's only other participant) */
+        o[3] = sh[1]; o[4] = sh[2]; o[5] = sh[3];
+    }
+}
+/* mg_env.hip obb_apart: the two shape-frame boxes separated along one of their
+ * six face axes by more than the contact offset plus a rounding slack */
+static int obb_apart_(const float* sha, v3_t xa, q4_t qa, const float* shb, v3_t xb, q4_t qb, const float* hulls,
+                      float off) {
+    float oa[6], ob[6], C[3][3], slack, rb, ra;
+    const m3_t Ra = qmat_(qmul_(qa, Q(sha[7], sha[8], sha[9], sha[10])));
+    const m3_t Rb = qmat_(qmul_(qb, Q(shb[7], shb[8], shb[9], shb[10])));
+    v3_t ca, cb, d, A3[3], B3[3];
+    float eA[3], eB[3];
+    int i, j, apart = 0;
+    shape_obb_(sha, hulls, oa);
+    shape_obb_(shb, hulls, ob);
+    ca = add3(add3(xa, qrot_(qa, V(sha[4], sha[5], sha[6]))), mv_(Ra, V(oa[0], oa[1], oa[2])));
+    cb = add3(add3(xb, qrot_(qb, V(shb[4], shb[5], shb[6]))), mv_(Rb, V(ob[0], ob[1], ob[2])));
+    for (i = 0; i < 3; ++i) { eA[i] = oa[3 + i]; eB[i] = ob[3 + i]; }
+    d = sub3(cb, ca);
+    slack = off + 1e-5f * (1.0f + (eA[0] + eA[1] + eA[2]) + (eB[0] + eB[1] + eB[2]) +
+                           (fabsf(d.x) + fabsf(d.y) + fabsf(d.z)));
+    A3[0] = Ra.c0; A3[1] = Ra.c1; A3[2] = Ra.c2;
+    B3[0] = Rb.c0; B3[1] = Rb.c1; B3[2] = Rb.c2;
+    for (i = 0; i < 3; ++i)
+        for (j = 0; j < 3; ++j) C[i][j] = fabsf(dot3(A3[i], B3[j]));
+    for (i = 0; i < 3; ++i) {
+        rb = eB[0] * C[i][0] + eB[1] * C[i][1] + eB[2] * C[i][2];
+        apart = apart || fabsf(dot3(d, A3[i])) > eA[i] + rb + slack;
+    }
+    for (j = 0; j < 3; ++j) {
+        ra = eA[0] * C[0][j] + eA[1] * C[1][j] + eA[2] * C[2][j];
+        apart = apart || fabsf(dot3(d, B3[j])) > eB[j] + ra + slack;
+    }
+    return apart;
+}
+static int cvx_pair_(int ta, int tb) {
+    const int pa = ta == MG_SHAPE_BOX || ta == MG_SHAPE_CONVEX, pb = tb == MG_SHAPE_BOX || tb == MG_SHAPE_CONVEX;
+    return pa && pb && (ta == MG_SHAPE_CONVEX || tb == MG_SHAPE_CONVEX);
+}
 static int pair_near_(const step_t* P, const float* sha, v3_t xa, q4_t qa, const float* shb, v3_t xb, q4_t qb,
-                      int ground) {
+                      int ground, const float* hulls) {
     const v3_t cA = add3(xa, qrot_(qa, V(sha[4], sha[5], sha[6])));
     const float rA = bound_radius_(sha);
     v3_t cB, d;
@@ -505,6 +568,7 @@ static int pair_near_(const step_t* P, const float* sha, v3_t xa, q4_t qa, const
     if (!(dot3(d, d) < rr * rr * 1.0001f + 1e-6f)) return 0;
     if ((int)shb[0] == MG_SHAPE_BOX && !sphere_near_box_(cA, rA, shb, xb, qb, P->co)) return 0;
     if ((int)sha[0] == MG_SHAPE_BOX && !sphere_near_box_(cB, rB, sha, xa, qa, P->co)) return 0;
+    if (cvx_pair_((int)sha[0], (int)shb[0]) && obb_apart_(sha, xa, qa, shb, xb, qb, hulls, P->co)) return 0;
     return 1;
 }
 
@@ -517,6 +581,63 @@ static void tangents_(v3_t n, v3_t* t1, v3_t* t2) {
     t = mul3(t, inv);
     *t1 = t;
     *t2 = cross3(n, t);
+}
+
+/* Friction patch of one shape pair (mg_env.hip patch_update):
+ * PhysX patch friction — up to two anchors fixed on both bodies, kept while
+ * the normal holds (cos >= OE_FP_COS) and the anchor's two copies stay within
+ * the correlation distance, grown from the contacts in emitted order (the
+ * first within the friction offset threshold, then the first farther than the
+ * correlation distance from anchor 0). */
+typedef struct { int cnt; v3_t nA, aA[2], aB[2]; } patch_t;
+static v3_t qrot_inv_(q4_t q, v3_t v) { return qrot_(Q(-q.x, -q.y, -q.z, q.w), v); }
+static void patch_load_(patch_t* R, const float* r) {
+    int k;
+    R->cnt = (int)r[0];
+    R->nA = V(r[1], r[2], r[3]);
+    for (k = 0; k < 2; ++k) {
+        R->aA[k] = V(r[4 + 6 * k], r[5 + 6 * k], r[6 + 6 * k]);
+        R->aB[k] = V(r[7 + 6 * k], r[8 + 6 * k], r[9 + 6 * k]);
+    }
+}
+static void patch_store_(const patch_t* R, float* r) {
+    int k;
+    r[0] = (float)R->cnt;
+    r[1] = R->nA.x; r[2] = R->nA.y; r[3] = R->nA.z;
+    for (k = 0; k < 2; ++k) {
+        r[4 + 6 * k] = R->aA[k].x; r[5 + 6 * k] = R->aA[k].y; r[6 + 6 * k] = R->aA[k].z;
+        r[7 + 6 * k] = R->aB[k].x; r[8 + 6 * k] = R->aB[k].y; r[9 + 6 * k] = R->aB[k].z;
+    }
+}
+static void patch_update_(patch_t* R, v3_t xa, q4_t qa, v3_t xb, q4_t qb, const pair_t* o, float fot, float corr) {
+    const v3_t n0 = o->nrm[0];
+    const float c2 = corr * corr;
+    int cnt = R->cnt, k, j;
+    patch_t N;
+    if (cnt > 0 && dot3(qrot_(qa, R->nA), n0) < OE_FP_COS) cnt = 0;
+    N.cnt = 0;
+    N.aA[0] = N.aA[1] = N.aB[0] = N.aB[1] = V(0.0f, 0.0f, 0.0f);
+    for (k = 0; k < cnt && k < 2; ++k) {
+        const v3_t d = sub3(add3(xa, qrot_(qa, R->aA[k])), add3(xb, qrot_(qb, R->aB[k])));
+        if (dot3(d, d) <= c2) { N.aA[N.cnt] = R->aA[k]; N.aB[N.cnt] = R->aB[k]; N.cnt++; }
+    }
+    for (j = 0; j < o->n; ++j) {
+        const v3_t p = o->p[j];
+        int add;
+        if (!(N.cnt < 2 && o->sep[j] <= fot)) continue;
+        add = N.cnt == 0;
+        if (N.cnt == 1) {
+            const v3_t d = sub3(p, add3(xa, qrot_(qa, N.aA[0])));
+            add = dot3(d, d) > c2;
+        }
+        if (add) {
+            N.aA[N.cnt] = qrot_inv_(qa, sub3(p, xa));
+            N.aB[N.cnt] = qrot_inv_(qb, sub3(p, xb));
+            N.cnt++;
+        }
+    }
+    N.nA = qrot_inv_(qa, n0);
+    *R = N;
 }
 
 static cshape_t place_(const float* sh, v3_t x, q4_t q, const float* hulls) {
@@ -579,6 +700,7 @@ static void ground_pair_(const step_t* P, const cshape_t* s, pair_t* o) {
 /* env description, as the library's env_i row but with global body ids */
 typedef struct {
     int art_body, art_dof, art_tmpl, nf, free_b[OE_MAXF], ns, stat_b[OE_MAXS], mask;
+    int env;   /* model env index (friction patch cache row) */
 } oenv_t;
 
 #define OE_GM 64      /* lanes of a wide env (mg_env.hip: G = 16, or 64 above 16 links / slots) */
@@ -948,7 +1070,7 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
 }
 
 static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float* state, float* dof, const float* tgt,
-                     const float* props, const float* ext, float* cforce) {
+                     const float* props, const float* ext, float* cforce, float* fcache) {
     const int b0 = ev->art_body, d0 = ev->art_dof, nfr = ev->nf;
     const int* ti = ev->art_tmpl >= 0 ? m->artic_tmpl_i + (size_t)ev->art_tmpl * MG_ATMPL_I_N : NULL;
     const int L = ti ? ti[1] : 0, D = ti ? ti[2] : 0;
@@ -983,7 +1105,13 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     /* contacts and rows */
     int ca[OE_MAXCT], cb[OE_MAXCT];
     v3_t cp[OE_MAXCT], cd[OE_MAXCT][3];
-    float cs0[OE_MAXCT], cmu[OE_MAXCT], ce[OE_MAXCT], cvn0[OE_MAXCT], ck[OE_MAXCT][3], clam[OE_MAXCT][3];
+    float cs0[OE_MAXCT], ce[OE_MAXCT], cvn0[OE_MAXCT], ck[OE_MAXCT][3], clam[OE_MAXCT][3];
+    /* friction anchors (mg_env.hip EnvLds apt ...): row k's point, tangents in cd[k][1..2] */
+    v3_t apt[OE_MAXCT];
+    float ae[OE_MAXCT][2], amu[OE_MAXCT], psum[OE_MAXCT];
+    int aa[OE_MAXCT], ab[OE_MAXCT], alast[OE_MAXCT], apair[OE_MAXCT], pstart[OE_MAXCT];
+    char held[OE_FPP];
+    float* fcr = fcache ? fcache + (size_t)ev->env * OE_FC_N : NULL;
     static __thread float Jr[OE_MAXCT * 3][OE_GM], Wr[OE_MAXCT * 3][OE_GM];
     int d, l, k, c, i, j, st_, it;
     /* lanes: 16, or 64 for an env of more than 16 links / velocity slots (migym_capi.cpp groups) */
@@ -1042,7 +1170,13 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     }
 
     for (st_ = 0; st_ < P->substeps; ++st_) {
-        int nct = 0, link_rows = 0;
+        int nct = 0, link_rows = 0, nanc = 0;
+        /* the pairs that held a patch at the end of the last substep */
+        for (i = 0; i < OE_FPP; ++i) {
+            held[i] = fcr ? fcr[(size_t)i * (OE_FP_N + 1) + OE_FP_N] != 0.0f : 0;
+            if (fcr) fcr[(size_t)i * (OE_FP_N + 1) + OE_FP_N] = 0.0f;
+        }
+        for (c = 0; c < OE_MAXCT; ++c) pstart[c] = 0;
         /* ---- 1. unconstrained motion: world-frame ABA about x0 (mg_env.hip aba_world) */
         if (L > 0) aba_world_(P, m, LF, LI, L, D, b0, d0, q, u, props, tgt, x0, q0, gw, &W, qdd, mdiag, tau0d, impd, fb,
                               ext, G);
@@ -1088,7 +1222,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             sA = place_(sha, xa, qa, m->hulls);
             o.n = 0;
             if (pp->b < 0) {
-                if (!pair_near_(P, sha, xa, qa, sha, xa, qa, 1)) continue;
+                if (!pair_near_(P, sha, xa, qa, sha, xa, qa, 1, m->hulls)) continue;
                 ground_pair_(P, &sA, &o);
                 mu = 0.5f * (sha[11] + P->mu_g);
                 rest = 0.5f * (sha[12] + P->e_g);
@@ -1105,27 +1239,63 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     xb = xl[pp->b];
                     qb = ql[pp->b];
                 }
-                if (!pair_near_(P, sha, xa, qa, shb, xb, qb, 0)) continue;
+                if (!pair_near_(P, sha, xa, qa, shb, xb, qb, 0, m->hulls)) continue;
                 sB = place_(shb, xb, qb, m->hulls);
                 collide_(&sA, &sB, P->co, &o);
                 mu = 0.5f * (sha[11] + shb[11]);
                 rest = 0.5f * (sha[12] + shb[12]);
             }
-            for (j = 0; j < o.n; ++j) {
-                if (nct < MAXCT) {
-                    ca[nct] = pp->a;
-                    cb[nct] = pp->b;
-                    cp[nct] = o.p[j];
-                    cd[nct][0] = o.nrm[j];
-                    tangents_(o.nrm[j], &cd[nct][1], &cd[nct][2]);
-                    cs0[nct] = o.sep[j] - P->ro;
-                    cmu[nct] = mu;
-                    ce[nct] = rest;
-                    if (pp->a < OE_F0) link_rows = 1;
-                    nct++;
+            {
+                const int slot0 = nct;
+                for (j = 0; j < o.n; ++j) {
+                    if (nct < MAXCT) {
+                        ca[nct] = pp->a;
+                        cb[nct] = pp->b;
+                        cp[nct] = o.p[j];
+                        cd[nct][0] = o.nrm[j];
+                        cs0[nct] = o.sep[j] - P->ro;
+                        ce[nct] = rest;
+                        if (pp->a < OE_F0) link_rows = 1;
+                        nct++;
+                    }
+                }
+                /* the pair's friction patch (mg_env.hip: its first contact placed) */
+                if (o.n > 0 && slot0 < MAXCT) {
+                    patch_t R;
+                    v3_t pxb = V(0.0f, 0.0f, 0.0f), t1, t2;
+                    q4_t pqb = Q(0.0f, 0.0f, 0.0f, 1.0f);
+                    const int last = (slot0 + o.n < MAXCT ? slot0 + o.n : MAXCT) - 1;
+                    if (pp->b >= 0) { pxb = xb; pqb = qb; }
+                    R.cnt = 0;
+                    if (i < OE_FPP && held[i]) patch_load_(&R, fcr + (size_t)i * (OE_FP_N + 1));
+                    patch_update_(&R, xa, qa, pxb, pqb, &o, P->fot, P->corr);
+                    if (i < OE_FPP && fcr) {
+                        patch_store_(&R, fcr + (size_t)i * (OE_FP_N + 1));
+                        fcr[(size_t)i * (OE_FP_N + 1) + OE_FP_N] = 1.0f;
+                    }
+                    pstart[slot0] = 1;
+                    tangents_(o.nrm[0], &t1, &t2);
+                    for (j = 0; j < R.cnt; ++j) {
+                        if (nanc < MAXCT) {
+                            const v3_t wA = add3(xa, qrot_(qa, R.aA[j])), wB = add3(pxb, qrot_(pqb, R.aB[j]));
+                            const v3_t dr = sub3(wA, wB);
+                            apt[nanc] = wA;
+                            cd[nanc][1] = t1;
+                            cd[nanc][2] = t2;
+                            ae[nanc][0] = dot3(dr, t1);
+                            ae[nanc][1] = dot3(dr, t2);
+                            amu[nanc] = R.cnt == 2 ? 0.5f * mu : mu;
+                            aa[nanc] = pp->a;
+                            ab[nanc] = pp->b;
+                            alast[nanc] = last;
+                            apair[nanc] = i;
+                        }
+                        nanc++;
+                    }
                 }
             }
         }
+        if (nanc > MAXCT) nanc = MAXCT;
 
         /* joint-limit rows (mg_env.hip): DOF order, after the contacts */
         for (d = 0; d < D; ++d) {
@@ -1141,10 +1311,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                         cb[nct] = sgn;
                         cp[nct] = V(0.0f, 0.0f, 0.0f);
                         cd[nct][0] = V(0.0f, 0.0f, 0.0f);
-                        cd[nct][1] = V(0.0f, 0.0f, 0.0f);
-                        cd[nct][2] = V(0.0f, 0.0f, 0.0f);
                         cs0[nct] = sgn > 0 ? q[d] - lo : hi - q[d];
-                        cmu[nct] = 0.0f;
                         ce[nct] = 0.0f;
                         link_rows = 1;
                         nct++;
@@ -1210,15 +1377,17 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 }
             }
         }
-        for (c = 0; c < nct; ++c) {
-            const int a = ca[c], b = cb[c];
-            const v3_t p = cp[c];
+        /* row 0 of slot c: contact c's normal; rows 1, 2: anchor c's friction rows */
+        for (c = 0; c < (nct > nanc ? nct : nanc); ++c) {
             int rw;
             for (rw = 0; rw < 3; ++rw) {
+                const int a = rw == 0 ? ca[c] : aa[c], b = rw == 0 ? cb[c] : ab[c];
+                const v3_t p = rw == 0 ? cp[c] : apt[c];
                 const v3_t dir = cd[c][rw];
                 float* J = Jr[c * 3 + rw];
                 float* W = Wr[c * 3 + rw];
                 int ln;
+                if (rw == 0 ? c >= nct : c >= nanc) continue;
                 for (ln = 0; ln < G; ++ln) {
                     float Jv = 0.0f, Wv = 0.0f;
                     if (a >= OE_LIM0) {
@@ -1263,13 +1432,42 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 }
                 clam[c][rw] = 0.0f;
             }
-            cvn0[c] = redp_(Jr[c * 3], u, G);
+            if (c < nct) cvn0[c] = redp_(Jr[c * 3], u, G);
         }
 
         /* ---- 4. TGS */
         for (it = 0; it < P->npos + P->nvel; ++it) {
             const int pos = it < P->npos;
             int ln;
+            /* friction first, then the normal rows (mg_env.hip: non-penetration has the last word);
+             * the anchors' bound is the patch's normal impulse of the previous sweep */
+            {   /* running sums restarting at a patch's first contact */
+                float run = 0.0f;
+                for (c = 0; c < nct; ++c) {
+                    run = pstart[c] ? clam[c][0] : run + clam[c][0];
+                    psum[c] = run;
+                }
+            }
+            for (c = 0; c < nanc; ++c) {   /* anchors: close the drift, share mu N of the patch */
+                const float lim = amu[c] * psum[alast[c]];
+                int rw;
+                for (rw = 1; rw < 3; ++rw) {
+                    const float lam = clam[c][rw];
+                    float tg = 0.0f, raw, nl, dl;
+                    if (pos) {
+                        const float s = ae[c][rw - 1] + redp_(Jr[c * 3 + rw], dp, G);
+                        tg = fminf(fmaxf(-s * (0.8f * P->inv_h), -P->maxdep), P->maxdep);
+                    }
+                    raw = lam + ck[c][rw] * (tg - redp_(Jr[c * 3 + rw], u, G));
+                    nl = fminf(fmaxf(raw, -lim), lim);
+                    /* slipping in the last iteration: the patch lets go of its anchors */
+                    if (it == P->npos + P->nvel - 1 && (raw > lim || raw < -lim) && apair[c] < OE_FPP && fcr)
+                        fcr[(size_t)apair[c] * (OE_FP_N + 1)] = 0.0f;
+                    dl = nl - lam;
+                    for (ln = 0; ln < G; ++ln) u[ln] = u[ln] + Wr[c * 3 + rw][ln] * dl;
+                    clam[c][rw] = nl;
+                }
+            }
             for (c = 0; c < nct; ++c) {
                 const float s = cs0[c] + redp_(Jr[c * 3], dp, G);
                 float tg, lam, dl, nl;
@@ -1286,17 +1484,6 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 dl = nl - lam;
                 for (ln = 0; ln < G; ++ln) u[ln] = u[ln] + Wr[c * 3][ln] * dl;
                 clam[c][0] = nl;
-            }
-            for (c = 0; c < nct; ++c) {
-                const float lim = cmu[c] * clam[c][0];
-                int rw;
-                for (rw = 1; rw < 3; ++rw) {
-                    const float lam = clam[c][rw];
-                    const float nl = fminf(fmaxf(lam - ck[c][rw] * redp_(Jr[c * 3 + rw], u, G), -lim), lim);
-                    const float dl = nl - lam;
-                    for (ln = 0; ln < G; ++ln) u[ln] = u[ln] + Wr[c * 3 + rw][ln] * dl;
-                    clam[c][rw] = nl;
-                }
             }
             if (pos)
                 for (ln = 0; ln < G; ++ln) dp[ln] = dp[ln] + u[ln] * P->sub;
@@ -1328,15 +1515,17 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
             }
             for (d = 0; d < D; ++d) q[d] = qn[d];
         }
-        for (c = 0; c < nct; ++c) {
+        /* contact impulse sums: normal impulses in contact order, then the anchors' friction */
+        for (c = 0; c < nct + nanc; ++c) {
+            const int fr_ = c >= nct, kk = fr_ ? c - nct : c;
+            const int a = fr_ ? aa[kk] : ca[kk], b = fr_ ? ab[kk] : cb[kk];
             v3_t imp;
-            if (ca[c] >= OE_LIM0) continue;
-            imp = mul3(cd[c][0], clam[c][0]);
-            imp = mad3(imp, cd[c][1], clam[c][1]);
-            imp = mad3(imp, cd[c][2], clam[c][2]);
-            if (ca[c] >= OE_F0) fsum[ca[c] - OE_F0] = add3(fsum[ca[c] - OE_F0], imp);
-            else lsum[ca[c]] = add3(lsum[ca[c]], imp);
-            if (cb[c] >= OE_F0 && cb[c] < OE_ST0) fsum[cb[c] - OE_F0] = sub3(fsum[cb[c] - OE_F0], imp);
+            if (a >= OE_LIM0) continue;
+            if (fr_) imp = mad3(mul3(cd[kk][1], clam[kk][1]), cd[kk][2], clam[kk][2]);
+            else imp = mul3(cd[kk][0], clam[kk][0]);
+            if (a >= OE_F0) fsum[a - OE_F0] = add3(fsum[a - OE_F0], imp);
+            else lsum[a] = add3(lsum[a], imp);
+            if (b >= OE_F0 && b < OE_ST0) fsum[b - OE_F0] = sub3(fsum[b - OE_F0], imp);
         }
         if (fb) {   /* floating root: the origin moves by dpos_v, the orientation turns by dpos_w */
             x0 = add3(x0, V(dp[D + 3], dp[D + 4], dp[D + 5]));
@@ -1456,6 +1645,7 @@ static int classify_envs_(const mg_model* m, oenv_t* envs, char* owned) {
         if (!coupled) continue;
         if (nart_all > 1 || nf_all > OE_MAXF || ns_all > OE_MAXS) { n = -1; break; }
         ev->art_body = -1; ev->art_dof = 0; ev->art_tmpl = -1;
+        ev->env = e;
         if (nart == 1) {
             const int r0 = m->actor_root_body[art[0]];
             for (i = 0; i < m->num_artics; ++i) {

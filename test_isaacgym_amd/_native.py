@@ -54,7 +54,9 @@ class MgSimParams(ctypes.Structure):
         ("ground_static_friction", ctypes.c_float),
         ("ground_dynamic_friction", ctypes.c_float),
         ("ground_restitution", ctypes.c_float),
-        ("reserved", ctypes.c_int32 * 8),
+        ("friction_offset_threshold", ctypes.c_float),
+        ("friction_correlation_distance", ctypes.c_float),
+        ("reserved", ctypes.c_int32 * 6),
     ]
 
 

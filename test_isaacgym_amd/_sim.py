@@ -177,6 +177,8 @@ class Sim:
         mp.rest_offset = float(px.rest_offset)
         mp.bounce_threshold_velocity = float(px.bounce_threshold_velocity)
         mp.max_depenetration_velocity = float(px.max_depenetration_velocity)
+        mp.friction_offset_threshold = float(px.friction_offset_threshold)
+        mp.friction_correlation_distance = float(px.friction_correlation_distance)
         if self.plane is not None:
             n = self.plane.normal.normalize()
             mp.has_ground = 1

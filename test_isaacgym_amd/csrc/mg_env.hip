@@ -96,7 +96,7 @@ struct EnvLds {
     float Lc[NDM][NDM];              // M_eff, assembled by the DOF lanes
     int ca[MAXCT], cb[MAXCT];
     V3 cp[MAXCT], cd[MAXCT][3];      // point, (n, t1, t2)
-    float cs0[MAXCT], cmu[MAXCT], ce[MAXCT], cvn0[MAXCT];
+    float cs0[MAXCT], ce[MAXCT], cvn0[MAXCT];
     float ck[MAXCT][3], clam[MAXCT][3];
     int nct, link_rows;
     // world-frame articulated-body quantities (about the base origin x0)
@@ -114,6 +114,16 @@ struct EnvLds {
     int npl[NPB];                    // candidate pairs that passed the screen
     V3 sx[MG_ENV_MAXS];              // static bodies: pose (they do not move in the step)
     Q4 sq[MG_ENV_MAXS];
+    // friction anchors (patch friction): anchor k's point (its
+    // A copy, world), drift of its two copies along the patch tangents
+    // (cd[k][1], cd[k][2]), Coulomb share mu / anchors, participants a | b << 16,
+    // last contact of its patch | pair index << 8
+    V3 apt[MAXCT];
+    float ae[MAXCT][2], amu[MAXCT];
+    int aab[MAXCT], alast[MAXCT];
+    float psum[MAXCT];               // running normal impulse of each contact's patch
+    unsigned fpv[MG_FP_W], fpn[MG_FP_W];   // pairs holding a patch: last substep, this one
+    unsigned long long pstart;       // contacts that open a patch
 };
 
 // sum over the 16 lanes of a DPP row, the same value in every lane:
@@ -390,7 +400,7 @@ __device__ __forceinline__ CShape shfl_shape(const CShape& c, int k) {
 }
 // the pairs convex_convex handles (collide's dispatch): box / hull against box /
 // hull, at least one hull (box-box is SAT)
-__device__ __forceinline__ bool cvx_pair(int ta, int tb) {
+MG_HD bool cvx_pair(int ta, int tb) {
     const bool pa = ta == MG_SHAPE_BOX || ta == MG_SHAPE_CONVEX, pb = tb == MG_SHAPE_BOX || tb == MG_SHAPE_CONVEX;
     return pa && pb && (ta == MG_SHAPE_CONVEX || tb == MG_SHAPE_CONVEX);
 }
@@ -524,7 +534,45 @@ MG_HD bool sphere_near_box(V3 c, float r, const float* shb, V3 xb, Q4 qb, float 
     const float rr = r + off;
     return vdot(e, e) < rr * rr * 1.0001f + 1e-6f;
 }
-MG_HD bool pair_near(const MgStep& P, const float* sha, V3 xa, Q4 qa, const float* shb, V3 xb, Q4 qb, bool ground) {
+// Oriented boxes of two box / hull shapes (ob: the shape-frame box of the
+// shape, centre then half extents, migym_capi.cpp shape_obb) separated along one
+// of their six face axes by more than the contact offset (plus a rounding
+// slack): no point of one comes within the offset of the other, so neither
+// convex_convex's vertex nor its edge pass can place a contact. A bounding
+// sphere is loose around a long Franka link hull; half of the hull pairs that
+// passed the sphere screens had no contact (profiles/r03_env_phase_p.json).
+MG_HD bool obb_apart(const float* sha, V3 xa, Q4 qa, const float* oa, const float* shb, V3 xb, Q4 qb,
+                     const float* ob, float off) {
+    const M3 Ra = qmat(qmul(qa, q4(sha[7], sha[8], sha[9], sha[10])));
+    const M3 Rb = qmat(qmul(qb, q4(shb[7], shb[8], shb[9], shb[10])));
+    const V3 ca = vadd(vadd(xa, qrot(qa, v3(sha[4], sha[5], sha[6]))), mmul(Ra, v3(oa[0], oa[1], oa[2])));
+    const V3 cb = vadd(vadd(xb, qrot(qb, v3(shb[4], shb[5], shb[6]))), mmul(Rb, v3(ob[0], ob[1], ob[2])));
+    const V3 ea = v3(oa[3], oa[4], oa[5]), eb = v3(ob[3], ob[4], ob[5]);
+    const V3 d = vsub(cb, ca);
+    const float slack = off + 1e-5f * (1.0f + (ea.x + ea.y + ea.z) + (eb.x + eb.y + eb.z) +
+                                       (fabsf(d.x) + fabsf(d.y) + fabsf(d.z)));
+    const V3 A3[3] = {Ra.c0, Ra.c1, Ra.c2}, B3[3] = {Rb.c0, Rb.c1, Rb.c2};
+    const float eA[3] = {ea.x, ea.y, ea.z}, eB[3] = {eb.x, eb.y, eb.z};
+    float C[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) C[i][j] = fabsf(vdot(A3[i], B3[j]));
+    bool apart = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float rb = eB[0] * C[i][0] + eB[1] * C[i][1] + eB[2] * C[i][2];
+        apart = apart || fabsf(vdot(d, A3[i])) > eA[i] + rb + slack;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const float ra = eA[0] * C[0][j] + eA[1] * C[1][j] + eA[2] * C[2][j];
+        apart = apart || fabsf(vdot(d, B3[j])) > eB[j] + ra + slack;
+    }
+    return apart;
+}
+MG_HD bool pair_near(const MgStep& P, const float* sha, V3 xa, Q4 qa, const float* shb, V3 xb, Q4 qb, bool ground,
+                     const float* oa, const float* ob) {
     const V3 cA = vadd(xa, qrot(qa, v3(sha[4], sha[5], sha[6])));
     const float rA = bound_radius(sha);
     if (ground) return vdot(v3(P.n[0], P.n[1], P.n[2]), cA) + P.pd - rA < P.contact_offset;
@@ -535,7 +583,89 @@ MG_HD bool pair_near(const MgStep& P, const float* sha, V3 xa, Q4 qa, const floa
     if (!(vdot(d, d) < rr * rr * 1.0001f + 1e-6f)) return false;
     if ((int)shb[0] == MG_SHAPE_BOX && !sphere_near_box(cA, rA, shb, xb, qb, P.contact_offset)) return false;
     if ((int)sha[0] == MG_SHAPE_BOX && !sphere_near_box(cB, rB, sha, xa, qa, P.contact_offset)) return false;
+    if (oa && cvx_pair((int)sha[0], (int)shb[0]) && obb_apart(sha, xa, qa, oa, shb, xb, qb, ob, P.contact_offset))
+        return false;
     return true;
+}
+
+// ---- friction patches -------------------------------------
+// PhysX friction is patch friction: a shape pair's friction rows act at up to
+// two anchors, each fixed on both bodies, kept from substep to substep and
+// from step to step while the pair stays in contact (Isaac Gym exposes its two
+// parameters, examples/franka_cube_ik_osc.py:124-125). Per substep, on the
+// pair's lane: the patch is dropped when its normal turned (cos <
+// MG_FP_NORMAL_COS); an anchor is dropped when its two copies drifted apart by
+// more than the correlation distance; then anchors grow from this substep's
+// contacts in emitted order — the first contact within the friction offset
+// threshold, then the first one farther than the correlation distance from
+// anchor 0 — fixed on both bodies at the contact point. The friction rows of
+// an anchor close the drift of its two copies along the patch tangents (TGS
+// position target, like a normal row's separation) and share the patch's
+// Coulomb bound mu * (sum of its contacts' normal impulses) equally; a patch
+// whose bound clamps a row in the last iteration is slipping and re-anchors at
+// the next substep. Oracle: patch_update_ (migym_oracle_env.c).
+struct Patch {
+    int cnt;
+    V3 nA;          // patch normal in A's body frame
+    V3 aA[2], aB[2];
+};
+MG_HD void patch_load(Patch& R, const float* r) {
+    R.cnt = (int)r[0];
+    R.nA = v3(r[1], r[2], r[3]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        R.aA[k] = v3(r[4 + 6 * k], r[5 + 6 * k], r[6 + 6 * k]);
+        R.aB[k] = v3(r[7 + 6 * k], r[8 + 6 * k], r[9 + 6 * k]);
+    }
+}
+MG_HD void patch_store(const Patch& R, float* r) {
+    r[0] = (float)R.cnt;
+    r[1] = R.nA.x; r[2] = R.nA.y; r[3] = R.nA.z;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        r[4 + 6 * k] = R.aA[k].x; r[5 + 6 * k] = R.aA[k].y; r[6 + 6 * k] = R.aA[k].z;
+        r[7 + 6 * k] = R.aB[k].x; r[8 + 6 * k] = R.aB[k].y; r[9 + 6 * k] = R.aB[k].z;
+    }
+}
+// R: the pair's patch of the last substep (cnt 0: none) -> this substep's
+MG_HD void patch_update(Patch& R, V3 xa, Q4 qa, V3 xb, Q4 qb, const PairOut& o, float fot, float corr) {
+    const V3 n0 = o.nrm[0];
+    const float c2 = corr * corr;
+    int cnt = R.cnt;
+    if (cnt > 0 && vdot(qrot(qa, R.nA), n0) < MG_FP_NORMAL_COS) cnt = 0;
+    Patch N;
+    N.cnt = 0;
+    N.aA[0] = N.aA[1] = N.aB[0] = N.aB[1] = v3(0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (k < cnt) {
+            const V3 d = vsub(vadd(xa, qrot(qa, R.aA[k])), vadd(xb, qrot(qb, R.aB[k])));
+            if (vdot(d, d) <= c2) {
+                if (N.cnt == 0) { N.aA[0] = R.aA[k]; N.aB[0] = R.aB[k]; }
+                else { N.aA[1] = R.aA[k]; N.aB[1] = R.aB[k]; }
+                N.cnt = N.cnt + 1;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < MG_PAIR_MAXC; ++j) {
+        if (j < o.n && N.cnt < 2 && o.sep[j] <= fot) {
+            const V3 p = o.p[j];
+            bool add = N.cnt == 0;
+            if (N.cnt == 1) {
+                const V3 d = vsub(p, vadd(xa, qrot(qa, N.aA[0])));
+                add = vdot(d, d) > c2;
+            }
+            if (add) {
+                const V3 la = qrot_inv(qa, vsub(p, xa)), lb = qrot_inv(qb, vsub(p, xb));
+                if (N.cnt == 0) { N.aA[0] = la; N.aB[0] = lb; }
+                else { N.aA[1] = la; N.aB[1] = lb; }
+                N.cnt = N.cnt + 1;
+            }
+        }
+    }
+    N.nA = qrot_inv(qa, n0);
+    R = N;
 }
 
 // x = M^-1 b for a symmetric positive definite 6x6 M (row-major): left-looking
@@ -1001,6 +1131,11 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             }
         }
     }
+    if (ln < MG_FP_W) {   // friction patches held at the end of the last step
+        S.fpv[ln] = live ? A.fp_mask[(size_t)e * MG_FP_W + ln] : 0u;
+        S.fpn[ln] = 0u;
+    }
+    if (ln == 0) S.pstart = 0ull;
     if (live && ln < ei[7]) {
         const int b = ei[8 + ln];
         S.sx[ln] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
@@ -1142,7 +1277,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         //     has no contact within the margin);
         // (b) the full pair test on the survivors, one per lane per round,
         //     contacts placed by a 16-lane prefix sum in pair order.
-        int base = 0;
+        int base = 0, abase = 0;   // contacts, friction anchors placed so far
         for (int blk = 0; __any(blk < npair); blk += NPB) {
             int nnear = 0;
 #pragma unroll
@@ -1157,7 +1292,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     Q4 qa, qb = q4(0.0f, 0.0f, 0.0f, 1.0f);
                     pair_pose(S, pa, xa, qa);
                     if (pb >= 0) pair_pose(S, pb, xb, qb);
-                    near = pair_near(P, sha, xa, qa, pb >= 0 ? A.shapes + sb * MG_SHAPE_STRIDE : sha, xb, qb, pb < 0);
+                    near = pair_near(P, sha, xa, qa, pb >= 0 ? A.shapes + sb * MG_SHAPE_STRIDE : sha, xb, qb, pb < 0,
+                                     A.shape_obb + sa * MG_OBB_N, A.shape_obb + (pb >= 0 ? sb : sa) * MG_OBB_N);
                 }
                 const unsigned long long gm = grp_ballot<G>(near, gi);
                 if (near) S.npl[nnear + __popcll(gm & ((1ull << ln) - 1ull))] = pi;
@@ -1170,12 +1306,13 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 PairOut o;
                 o.n = 0;
                 float mu = 0.0f, rest = 0.0f;
-                int pa = 0, pb = -1;
+                int pa = 0, pb = -1, pidx = 0;
                 bool coop = false;
                 CShape cA = {}, cB = {};
                 if (rb + ln < nnear) {
                     PH_COUNT(10, 1);
-                    const int* pp = A.pairs + (size_t)(pair0 + S.npl[rb + ln]) * 4;
+                    pidx = S.npl[rb + ln];
+                    const int* pp = A.pairs + (size_t)(pair0 + pidx) * 4;
                     pa = pp[0];
                     const int sa = pp[1];
                     pb = pp[2];
@@ -1235,14 +1372,62 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         S.cb[c] = pb;
                         S.cp[c] = o.p[j];
                         S.cd[c][0] = o.nrm[j];
-                        env_tangents(o.nrm[j], &S.cd[c][1], &S.cd[c][2]);
                         S.cs0[c] = o.sep[j] - P.rest_offset;
-                        S.cmu[c] = mu;
                         S.ce[c] = rest;
                         if (pa < F0) S.link_rows = 1;
                     }
                 }
                 base += total;
+                // the pair's friction patch (its first contact placed): anchors
+                // kept from the last substep or grown from these contacts
+                Patch R;
+                R.cnt = 0;
+                V3 pxa = v3(0.0f, 0.0f, 0.0f), pxb = v3(0.0f, 0.0f, 0.0f);
+                Q4 pqa = q4(0.0f, 0.0f, 0.0f, 1.0f), pqb = q4(0.0f, 0.0f, 0.0f, 1.0f);
+                if (o.n > 0 && slot0 < MAXCT) {
+                    pair_pose(S, pa, pxa, pqa);
+                    if (pb >= 0) pair_pose(S, pb, pxb, pqb);
+                    float* rec = A.fpatch + (size_t)(pair0 + pidx) * MG_FP_N;
+                    const bool held = pidx < MG_FP_MAXP && ((S.fpv[pidx >> 5] >> (pidx & 31)) & 1u);
+                    if (held) patch_load(R, rec);
+                    patch_update(R, pxa, pqa, pxb, pqb, o, P.fric_offset, P.fric_corr);
+                    if (pidx < MG_FP_MAXP) {
+                        patch_store(R, rec);
+                        atomicOr(&S.fpn[pidx >> 5], 1u << (pidx & 31));
+                    }
+                    atomicOr(&S.pstart, 1ull << slot0);
+                }
+                int ain = R.cnt;
+#pragma unroll
+                for (int off = 1; off < G; off <<= 1) {
+                    const int t = __shfl_up(ain, off, G);
+                    if (ln >= off) ain += t;
+                }
+                const int atot = __shfl(ain, G - 1, G);
+                const int ak0 = abase + ain - R.cnt;
+                if (R.cnt > 0) {
+                    const V3 n0 = o.nrm[0];
+                    V3 t1, t2;
+                    env_tangents(n0, &t1, &t2);
+                    const int last = (slot0 + o.n < MAXCT ? slot0 + o.n : MAXCT) - 1;
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int k = ak0 + j;
+                        if (j < R.cnt && k < MAXCT) {
+                            const V3 wA = vadd(pxa, qrot(pqa, R.aA[j])), wB = vadd(pxb, qrot(pqb, R.aB[j]));
+                            const V3 dr = vsub(wA, wB);
+                            S.apt[k] = wA;
+                            S.cd[k][1] = t1;
+                            S.cd[k][2] = t2;
+                            S.ae[k][0] = vdot(dr, t1);
+                            S.ae[k][1] = vdot(dr, t2);
+                            S.amu[k] = R.cnt == 2 ? 0.5f * mu : mu;
+                            S.aab[k] = (pa & 0xFFFF) | (pb << 16);
+                            S.alast[k] = last | (pidx << 8);
+                        }
+                    }
+                }
+                abase += atot;
                 PH_NP(20);
             }
             __syncthreads();
@@ -1279,16 +1464,14 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 S.cb[c] = sgn;
                 S.cp[c] = v3(0.0f, 0.0f, 0.0f);
                 S.cd[c][0] = v3(0.0f, 0.0f, 0.0f);
-                S.cd[c][1] = v3(0.0f, 0.0f, 0.0f);
-                S.cd[c][2] = v3(0.0f, 0.0f, 0.0f);
                 S.cs0[c] = s0;
-                S.cmu[c] = 0.0f;
                 S.ce[c] = 0.0f;
                 S.link_rows = 1;
             }
             base += total;
         }
         const int nct = base < MAXCT ? base : MAXCT;
+        const int nanc = abase < MAXCT ? abase : MAXCT;
         __syncthreads();
         PH_MARK(1);
 
@@ -1306,11 +1489,15 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 Wr[c * 3 + rw] = 0.0f;
                 lam[c * 3 + rw] = 0.0f;
             }
-            if (c < nct) {
-                const int a = S.ca[c], b = S.cb[c];
-                const V3 p = S.cp[c];
+            // row 0: contact c's normal; rows 1, 2: anchor c's friction rows
+            const bool cn = c < nct, cf = c < nanc;
+            if (cn || cf) {
 #pragma unroll
                 for (int rw = 0; rw < 3; ++rw) {
+                    if (rw == 0 ? !cn : !cf) continue;
+                    const int ab = rw == 0 ? 0 : S.aab[c];
+                    const int a = rw == 0 ? S.ca[c] : (ab & 0xFFFF), b = rw == 0 ? S.cb[c] : (ab >> 16);
+                    const V3 p = rw == 0 ? S.cp[c] : S.apt[c];
                     const V3 dir = S.cd[c][rw];
                     float J = 0.0f, W = 0.0f;
                     if (a >= LIM0) {
@@ -1349,8 +1536,10 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     const float kk = den > 0.0f ? 1.0f / den : 0.0f;
                     if (ln == 0) S.ck[c][rw] = kk;
                 }
-                const float vn0 = redg<G>(Jr[c * 3] * uv);
-                if (ln == 0) S.cvn0[c] = vn0;
+                if (cn) {
+                    const float vn0 = redg<G>(Jr[c * 3] * uv);
+                    if (ln == 0) S.cvn0[c] = vn0;
+                }
             }
         }
         __syncthreads();
@@ -1358,8 +1547,47 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 
         // ================= 4. TGS (the lambdas are kept by lane 0 in LDS; every
         // lane of the env computes the same value)
+        bool slip = false;   // anchor ln's friction bound clamped in the last iteration
         for (int it = 0; it < P.npos + P.nvel; ++it) {
             const bool pos = it < P.npos;
+            // friction first, then the normal rows, so that non-penetration has
+            // the last word in every sweep. The anchors' bound
+            // is the patch's normal impulse of the previous sweep: running sums
+            // in contact order, restarting at the contact that opens a patch
+            {
+                const unsigned long long ps = S.pstart;
+                float run = 0.0f;
+#pragma unroll
+                for (int c = 0; c < MAXCT; ++c) {
+                    if (c < nct) {
+                        run = ((ps >> c) & 1ull) ? lam[c * 3] : run + lam[c * 3];
+                        if (ln == 0) S.psum[c] = run;
+                    }
+                }
+            }
+            __syncthreads();
+            const bool last_it = it == P.npos + P.nvel - 1;
+#pragma unroll
+            for (int c = 0; c < MAXCT; ++c) {
+                if (c < nanc) {
+                    const float lim = S.amu[c] * S.psum[S.alast[c] & 0xFF];
+#pragma unroll
+                    for (int rw = 1; rw < 3; ++rw) {
+                        float tgt = 0.0f;
+                        if (pos) {   // close 80 % of the drift of the anchor's two copies per substep
+                            const float s = S.ae[c][rw - 1] + redg<G>(Jr[c * 3 + rw] * dp);
+                            tgt = fminf(fmaxf(-s * (0.8f * P.inv_h), -P.max_depen), P.max_depen);
+                        }
+                        const float lm = lam[c * 3 + rw];
+                        const float raw = lm + S.ck[c][rw] * (tgt - redg<G>(Jr[c * 3 + rw] * uv));
+                        const float nl = fminf(fmaxf(raw, -lim), lim);
+                        if (last_it && ln == c && (raw > lim || raw < -lim)) slip = true;
+                        const float dl = nl - lm;
+                        uv = uv + Wr[c * 3 + rw] * dl;
+                        lam[c * 3 + rw] = nl;
+                    }
+                }
+            }
 #pragma unroll
             for (int c = 0; c < MAXCT; ++c) {
                 if (c < nct) {
@@ -1383,30 +1611,22 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     lam[c * 3] = nl;
                 }
             }
-#pragma unroll
-            for (int c = 0; c < MAXCT; ++c) {
-                if (c < nct) {
-                    const float lim = S.cmu[c] * lam[c * 3];
-#pragma unroll
-                    for (int rw = 1; rw < 3; ++rw) {
-                        const float lm = lam[c * 3 + rw];
-                        const float nl = fminf(fmaxf(lm - S.ck[c][rw] * redg<G>(Jr[c * 3 + rw] * uv), -lim), lim);
-                        const float dl = nl - lm;
-                        uv = uv + Wr[c * 3 + rw] * dl;
-                        lam[c * 3 + rw] = nl;
-                    }
-                }
-            }
             if (pos) dp = dp + uv * P.sub;
         }
         if (ln == 0) {
 #pragma unroll
-            for (int c = 0; c < MAXCT; ++c)
-                if (c < nct) {
-                    S.clam[c][0] = lam[c * 3];
+            for (int c = 0; c < MAXCT; ++c) {
+                if (c < nct) S.clam[c][0] = lam[c * 3];
+                if (c < nanc) {
                     S.clam[c][1] = lam[c * 3 + 1];
                     S.clam[c][2] = lam[c * 3 + 2];
                 }
+            }
+        }
+        // a slipping patch lets go of its anchors (regrown at the next substep)
+        if (live && slip && ln < nanc) {
+            const int pidx = S.alast[ln] >> 8;
+            if (pidx < MG_FP_MAXP) A.fpatch[(size_t)(pair0 + pidx) * MG_FP_N] = 0.0f;
         }
         __syncthreads();
         PH_MARK(4);
@@ -1431,17 +1651,21 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         }
         __syncthreads();
         // contact impulse sums in contact order: link l on lane l, free body k on lane k
+        // (normal impulses in contact order, then the anchors' friction impulses)
         if (live && (ln < L || ln < nfr)) {
-            for (int c = 0; c < nct; ++c) {
-                const int a = S.ca[c], b = S.cb[c];
+            for (int c = 0; c < nct + nanc; ++c) {
+                const bool fr_ = c >= nct;
+                const int k = fr_ ? c - nct : c;
+                const int ab = fr_ ? S.aab[k] : 0;
+                const int a = fr_ ? (ab & 0xFFFF) : S.ca[k], b = fr_ ? (ab >> 16) : S.cb[k];
                 if (a >= LIM0) continue;
                 const bool on_link = ln < L && a == ln;
                 const bool on_fa = ln < nfr && a == F0 + ln;
                 const bool on_fb = ln < nfr && b == F0 + ln;
                 if (on_link || on_fa || on_fb) {
-                    V3 imp = vscale(S.cd[c][0], S.clam[c][0]);
-                    imp = vmad(imp, S.cd[c][1], S.clam[c][1]);
-                    imp = vmad(imp, S.cd[c][2], S.clam[c][2]);
+                    V3 imp;
+                    if (fr_) imp = vmad(vscale(S.cd[k][1], S.clam[k][1]), S.cd[k][2], S.clam[k][2]);
+                    else imp = vscale(S.cd[k][0], S.clam[k][0]);
                     if (on_link) lsum = vadd(lsum, imp);
                     if (on_fa) fsum = vadd(fsum, imp);
                     if (on_fb) fsum = vsub(fsum, imp);
@@ -1463,11 +1687,17 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             S.fq[k] = qintegrate(S.fq[k], dth);
             S.fx[k] = vsub(xc1, qrot(S.fq[k], fr.com));
         }
+        if (ln < MG_FP_W) {   // this substep's patches are the next one's
+            S.fpv[ln] = S.fpn[ln];
+            S.fpn[ln] = 0u;
+        }
+        if (ln == 0) S.pstart = 0ull;
         __syncthreads();
         PH_MARK(5);
     }
 
     // ---- outputs
+    if (live && ln < MG_FP_W) A.fp_mask[(size_t)e * MG_FP_W + ln] = S.fpv[ln];
     S.q[ln] = qv;
     S.u[ln] = uv;
     if (is_dof) {

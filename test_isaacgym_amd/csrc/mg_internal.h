@@ -30,6 +30,8 @@ struct MgStep {
     float pd;         // ground plane offset: dot(n, x) + pd = 0
     float t1[3], t2[3];   // ground tangent basis
     float mu_ground, e_ground;
+    float fric_offset;   // friction_offset_threshold (coupled step: friction anchors)
+    float fric_corr;     // friction_correlation_distance
 };
 
 // Compact per-template record of the single-shape free-body kernel (built at
@@ -125,6 +127,17 @@ struct MgArticArgs {
 #define MG_ENV_STATIC0 80
 #define MG_ENV_LIMIT0 128     // joint-limit row of DOF d: a = MG_ENV_LIMIT0 + d, b = +1 lower / -1 upper
 
+// Friction patches of the coupled step (mg_env.hip): one
+// record per candidate shape pair (global pair index), MG_FP_N floats: anchor
+// count, the patch normal in A's body frame, then per anchor its point in A's
+// and in B's body frame; an env's pairs 0..MG_FP_MAXP-1 keep theirs across
+// substeps and steps (bit set in the env's MG_FP_W-word mask), later pairs
+// re-anchor every substep.
+#define MG_FP_N 16
+#define MG_FP_W 4
+#define MG_FP_MAXP (32 * MG_FP_W)
+#define MG_FP_NORMAL_COS 0.999f
+#define MG_OBB_N 8   // shape_obb record: centre[3], half extents[3], pad[2]
 struct MgEnvArgs {
     int          ne;          // envs in this launch
     int          nb, nd;
@@ -142,6 +155,9 @@ struct MgEnvArgs {
     const int*   tbi;
     const float* shapes;
     const float* hulls;       // convex hull records (MG_SHAPE_CONVEX)
+    const float* shape_obb;   // [num_shapes][MG_OBB_N] shape-frame box: centre, half extents (pair screen)
+    float*       fpatch;      // [num pairs][MG_FP_N] friction patch records (persistent)
+    unsigned*    fp_mask;     // [ne][MG_FP_W] pairs whose record holds a patch (persistent)
     float*       dof_pos;
     float*       dof_vel;
     const float* dof_tpos;

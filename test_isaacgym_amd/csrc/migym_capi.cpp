@@ -96,6 +96,7 @@ struct mg_sim {
     int* d_tbi = nullptr;
     float* d_shapes = nullptr;
     float* d_hulls = nullptr;     // convex hull records (MG_SHAPE_CONVEX)
+    float* d_shape_obb = nullptr; // [ns][MG_OBB_N] shape-frame boxes (coupled step's pair screen)
     int* d_actor_root = nullptr;  // [na] internal slot of each actor's root body
     int* d_body_actor = nullptr;  // [nb] global body -> the actor it is the root of, or -1
     // Step fusion (mg_set_fusion): a device-resident, non-indexed root-state set
@@ -133,6 +134,8 @@ struct mg_sim {
     int* d_artic_step = nullptr;  // [..][4] instances stepped by k_artic_chain / k_artic_lanes
     int* d_env = nullptr;         // [n_coupled][MG_ENV_I_N] coupled envs, by group
     int* d_pairs = nullptr;       // [..][4] candidate shape pairs of the coupled envs
+    float* d_fpatch = nullptr;    // [pairs][MG_FP_N] friction patch records (coupled step, persistent)
+    unsigned* d_fp_mask = nullptr;   // [n_coupled][MG_FP_W] pairs holding a patch
     int n_coupled = 0;
     std::vector<EnvGroup> env_groups;
 
@@ -192,6 +195,8 @@ MgStep make_step(const mg_sim_params& p) {
     P.rest_offset = p.rest_offset;
     P.max_depen = p.max_depenetration_velocity;
     P.bounce_thresh = p.bounce_threshold_velocity;
+    P.fric_offset = p.friction_offset_threshold;
+    P.fric_corr = p.friction_correlation_distance;
     P.has_ground = p.has_ground;
     const float nx = p.ground_normal[0], ny = p.ground_normal[1], nz = p.ground_normal[2];
     P.n[0] = nx; P.n[1] = ny; P.n[2] = nz;
@@ -314,10 +319,40 @@ int set_dof_columns(mg_sim* s, const float* src, int src_host, int ncol, float* 
     return MG_OK;
 }
 
+// Shape-frame box of a shape (the coupled step's pair screen, mg_env.hip
+// obb_apart; oracle: shape_obb_): centre and half extents; a hull's from the
+// min / max of its vertices
+void shape_obb(const float* sh, const float* hulls, float* o) {
+    const int t = (int)sh[0];
+    for (int k = 0; k < MG_OBB_N; ++k) o[k] = 0.0f;
+    if (t == MG_SHAPE_CONVEX && hulls) {
+        const float* hv = hulls + (int)sh[2];
+        const int nv = (int)hv[0];
+        float lo[3], hi[3];
+        for (int c = 0; c < 3; ++c) { lo[c] = hv[MG_HULL_HEADER + c]; hi[c] = lo[c]; }
+        for (int i = 1; i < nv; ++i)
+            for (int c = 0; c < 3; ++c) {
+                const float v = hv[MG_HULL_HEADER + 3 * i + c];
+                lo[c] = std::min(lo[c], v);
+                hi[c] = std::max(hi[c], v);
+            }
+        for (int c = 0; c < 3; ++c) {
+            o[c] = 0.5f * (lo[c] + hi[c]);
+            o[3 + c] = 0.5f * (hi[c] - lo[c]);
+        }
+    } else if (t == MG_SHAPE_BOX) {
+        o[3] = sh[1]; o[4] = sh[2]; o[5] = sh[3];
+    } else if (t == MG_SHAPE_CAPSULE) {
+        o[3] = sh[1] + sh[2]; o[4] = sh[1]; o[5] = sh[1];
+    } else {
+        o[3] = sh[1]; o[4] = sh[1]; o[5] = sh[1];
+    }
+}
+
 void free_all(mg_sim* s) {
-    void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls,
+    void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls, s->d_shape_obb,
                     s->d_actor_root, s->d_root_row, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
-                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
+                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_fp_mask, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
                     s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -861,6 +896,12 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     }
     HIP_TRY(h2d(s->d_shapes, m->shapes, (size_t)s->ns * MG_SHAPE_STRIDE * sizeof(float)));
     if (m->hulls) HIP_TRY(h2d(s->d_hulls, m->hulls, (size_t)m->num_hull_floats * sizeof(float)));
+    {
+        std::vector<float> obb((size_t)std::max(s->ns, 1) * MG_OBB_N, 0.0f);
+        for (int k = 0; k < s->ns; ++k) shape_obb(m->shapes + (size_t)k * MG_SHAPE_STRIDE, m->hulls, &obb[(size_t)k * MG_OBB_N]);
+        HIP_TRY(dalloc(&s->d_shape_obb, obb.size()));
+        HIP_TRY(h2d(s->d_shape_obb, obb.data(), obb.size() * sizeof(float)));
+    }
     HIP_TRY(h2d(s->d_actor_root, root_int.data(), (size_t)na * sizeof(int)));
     {
         std::vector<int> body_actor(nb, -1);
@@ -897,6 +938,13 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(h2d(s->d_artic_step, artic_step.data(), artic_step.size() * sizeof(int)));
     HIP_TRY(h2d(s->d_env, env_flat.data(), env_flat.size() * sizeof(int)));
     HIP_TRY(h2d(s->d_pairs, pairs.data(), pairs.size() * sizeof(int)));
+    {   // no friction patch yet: every pair starts without anchors
+        const size_t np = std::max<size_t>(pairs.size() / 4, 1), nm = (size_t)std::max(s->n_coupled, 1) * MG_FP_W;
+        HIP_TRY(dalloc(&s->d_fpatch, np * MG_FP_N));
+        HIP_TRY(dalloc(&s->d_fp_mask, nm));
+        HIP_TRY(hipMemset(s->d_fpatch, 0, np * MG_FP_N * sizeof(float)));
+        HIP_TRY(hipMemset(s->d_fp_mask, 0, nm * sizeof(unsigned)));
+    }
     HIP_TRY(h2d(s->d_link_f, m->tmpl_link_f, (size_t)s->ntl * MG_LINK_F_N * sizeof(float)));
     HIP_TRY(h2d(s->d_link_i, m->tmpl_link_i, (size_t)s->ntl * MG_LINK_I_N * sizeof(int)));
     HIP_TRY(hipDeviceSynchronize());
@@ -980,6 +1028,8 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.ne = g.count; A.nb = s->nb; A.nd = s->nd;
         A.env_i = s->d_env + (size_t)g.offset * MG_ENV_I_N;
         A.pairs = s->d_pairs;
+        A.fpatch = s->d_fpatch;
+        A.fp_mask = s->d_fp_mask + (size_t)g.offset * MG_FP_W;
         A.nl = g.tmpl >= 0 ? g.nl : 0;
         A.ndof = g.tmpl >= 0 ? g.ndof : 0;
         A.floating = g.tmpl >= 0 ? g.floating : 0;
@@ -988,6 +1038,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.link_i = s->d_link_i + (size_t)(g.tmpl >= 0 ? g.first_link : 0) * MG_LINK_I_N;
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
         A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes; A.hulls = s->d_hulls;
+        A.shape_obb = s->d_shape_obb;
         A.dof_pos = s->d_dof; A.dof_vel = s->d_dof + s->nd;
         A.dof_tpos = s->d_dof_tgt; A.dof_tvel = s->d_dof_tgt + s->nd; A.dof_force = s->d_dof_tgt + 2 * (size_t)s->nd;
         fused_targets(s, A.dof_tpos, A.dof_tvel, A.dof_force, A.tpos_w, A.tvel_w, A.force_w);

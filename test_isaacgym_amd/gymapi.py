@@ -105,17 +105,20 @@ _warned_physx = set()
 
 
 def _warn_unmodelled_physx(params):
-    """PhysX patch-friction parameters the solver does not model
-    (examples/franka_cube_ik_osc.py:124-125 sets both): friction rows are one
-    anchor per contact point, so these have no effect.
-    Said once per parameter and value, on stderr — never dropped silently."""
+    """PhysX patch-friction parameters (examples/franka_cube_ik_osc.py:124-125
+    sets both) drive the friction anchors of the coupled per-env step (bodies
+    touching other bodies or an articulation); a free body
+    stepping alone against the ground plane keeps one friction anchor per
+    contact point, where they have no effect. Said once per parameter and
+    value, on stderr — never dropped silently."""
     px = params.physx
     for name in ("friction_offset_threshold", "friction_correlation_distance"):
         val = float(getattr(px, name))
         if val != float(getattr(_PHYSX_DEFAULTS, name)) and (name, val) not in _warned_physx:
             _warned_physx.add((name, val))
-            print("*** migym: physx.%s = %g is not modelled (friction anchors are the contact points "
-                  "themselves; DESIGN.md §3.2)" % (name, val), file=sys.stderr)
+            print("*** migym: physx.%s = %g drives the friction anchors of coupled envs only; free bodies "
+                  "alone on the ground plane keep per-point friction (DESIGN.md §3.6.1)" % (name, val),
+                  file=sys.stderr)
 
 
 class Gym:

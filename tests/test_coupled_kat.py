@@ -148,3 +148,89 @@ def test_franka_joint_held_at_limit(gym):
     assert abs(dof[3, 0] - hi) < 5e-3
     assert abs(dof[3, 1]) < 0.05
     assert np.all(np.isfinite(st))
+
+
+def _cube_on_table(gym, corr=None):
+    sim = _sim(gym)
+    if corr is not None:
+        sim.params.physx.friction_correlation_distance = corr
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    table = gym.create_box(sim, 0.6, 1.0, 0.4, opts)
+    # a flat tile (10 x 10 x 2 cm, 0.2 kg): a sideways push at its centre tips
+    # it only above 5 m g, so it slides rather than tips at mu m g = m g
+    cube = gym.create_box(sim, 0.1, 0.1, 0.02, gymapi.AssetOptions())
+    env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 1)
+    gym.create_actor(env, table, gymapi.Transform(gymapi.Vec3(0.5, 0, 0.2)), "table", 0, 0)
+    gym.create_actor(env, cube, gymapi.Transform(gymapi.Vec3(0.45, 0.1, 0.41)), "tile", 0, 0)
+    A = sim.build_model()
+    return sim, A, sim.mg_params(), sim.mg_model()
+
+
+def _patch(fc, pair=None):
+    """(anchor count, held, record floats) of an env-0 pair in an oracle cache
+    (default: the one pair holding a patch — the cube on the table)"""
+    if pair is None:
+        held = [i for i in range(128) if fc[0, i * 17 + 16] != 0.0]
+        assert len(held) == 1, held
+        pair = held[0]
+    r = fc[0, pair * 17:(pair + 1) * 17]
+    return int(r[0]), r[16] != 0.0, r
+
+
+@pytest.mark.parametrize("push", [0.5, 0.8, 1.2])
+def test_friction_anchor_holds_or_slides(gym, push):
+    """DESIGN.md §3.6.1 (patch friction): a tile (m g = 1.96 N, mu = 1) on the
+    table pushed sideways by a constant force. Below mu m g the friction
+    anchors hold it: after a sub-0.3 mm give in the first steps it does not
+    move at all, the patch's two anchors kept step after step, bit for bit;
+    above it the patch slips (anchors dropped and regrown) and the cube
+    accelerates at (F - mu m g) / m."""
+    sim, A, p, m = _cube_on_table(gym)
+    st = A["body_state0"].copy()
+    dof = A["dof_state0"].copy()
+    fc = oracle.contact_cache(m)
+    mass = 1000.0 * 0.1 * 0.1 * 0.02
+    for _ in range(30):   # settle
+        oracle.step(p, m, st, dof, contact_cache=fc)
+    cnt, held, _ = _patch(fc)
+    assert cnt == 2 and held
+    ext = np.zeros((2, 6), np.float32)
+    F = push * mass * G
+    ext[1, 0] = F
+    x0 = float(st[1, 0])
+    frames = 120 if push < 1.0 else 30
+    xs, recs = [], []
+    for _ in range(frames):
+        oracle.step(p, m, st, dof, ext=ext, contact_cache=fc)
+        xs.append(float(st[1, 0]))
+        recs.append(_patch(fc))
+    if push < 1.0:
+        assert abs(xs[-1] - x0) < 3e-4
+        assert abs(xs[-1] - xs[60]) < 2e-5
+        assert all(c == 2 and h for c, h, _ in recs[60:])
+        assert np.array_equal(recs[-1][2], recs[60][2])      # the same anchors, bit for bit
+    else:
+        t = frames / 60.0
+        d_expect = 0.5 * (F - mass * G) / mass * t * t
+        assert abs((xs[-1] - x0) - d_expect) < 0.1 * d_expect
+        assert abs(st[1, 2] - 0.41) < 1e-3                  # slides flat on the table
+
+
+def test_friction_anchor_spacing(gym):
+    """The second anchor is the first contact farther than the correlation
+    distance from the first; with a correlation distance above the cube's
+    diagonal a single anchor carries the patch (and the whole Coulomb bound),
+    and the tile still rests."""
+    for corr, want in ((0.025, 2), (0.3, 1)):
+        sim, A, p, m = _cube_on_table(gym, corr)
+        st = A["body_state0"].copy()
+        dof = A["dof_state0"].copy()
+        fc = oracle.contact_cache(m)
+        for _ in range(60):
+            oracle.step(p, m, st, dof, contact_cache=fc)
+        cnt, held, r = _patch(fc)
+        assert held and cnt == want, (corr, cnt)
+        if cnt == 2:
+            assert np.linalg.norm(r[4:7] - r[10:13]) > corr
+        assert abs(st[1, 2] - 0.41) < 1e-4 and np.linalg.norm(st[1, 0:2] - [0.45, 0.1]) < 1e-4

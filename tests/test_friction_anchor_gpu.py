@@ -1,0 +1,99 @@
+"""Friction anchors of the coupled step on the device:
+k_env_step's patch records, anchor rows and slip release against the oracle's
+restatement (oracle/migym_oracle_env.c patch_update_), bit for bit.
+
+64 envs of a tile on a table, each yawed differently and pushed sideways every
+frame by its own force from 0.3 to 1.4 mu m g (held by its anchors, or
+slipping and re-anchoring), through gym.apply_rigid_body_force_tensors — the
+device keeps its patches inside the sim, the oracle in the cache that goes with
+its state array.
+"""
+import numpy as np
+import pytest
+import torch
+
+from isaacgym import gymapi, gymtorch
+import oracle
+
+pytestmark = pytest.mark.gpu
+G = 9.8
+
+
+def _scene(gym, n):
+    sp = gymapi.SimParams()
+    sp.up_axis = gymapi.UP_AXIS_Z
+    sp.gravity = gymapi.Vec3(0, 0, -G)
+    sp.dt = 1.0 / 60.0
+    sp.substeps = 2
+    sp.use_gpu_pipeline = True
+    sp.physx.solver_type = 1
+    sp.physx.num_position_iterations = 8
+    sp.physx.num_velocity_iterations = 1
+    sp.physx.contact_offset = 0.001
+    sp.physx.rest_offset = 0.0
+    sp.physx.friction_offset_threshold = 0.001
+    sp.physx.friction_correlation_distance = 0.0005
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim, plane)
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    table = gym.create_box(sim, 0.6, 1.0, 0.4, opts)
+    tile = gym.create_box(sim, 0.1, 0.1, 0.02, gymapi.AssetOptions())
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 8)
+        gym.create_actor(env, table, gymapi.Transform(gymapi.Vec3(0.5, 0, 0.2)), "table", i, 0)
+        pose = gymapi.Transform(gymapi.Vec3(0.45, 0.1, 0.4101))
+        pose.r = gymapi.Quat.from_axis_angle(gymapi.Vec3(0, 0, 1), 0.1 * i)
+        gym.create_actor(env, tile, pose, "tile", i, 0)
+    gym.prepare_sim(sim)
+    return sim
+
+
+def test_friction_anchor_push_parity_gpu(gym):
+    from test_isaacgym_amd import _native as N
+    n, frames = 64, 90
+    sim = _scene(gym, n)
+    assert N.lib.mg_num_coupled_envs(sim.native) == n
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    dof = np.zeros((0, 2), np.float32)
+    mass = 1000.0 * 0.1 * 0.1 * 0.02
+    push = np.linspace(0.3, 1.4, n).astype(np.float32) * np.float32(mass * G)
+    yaw = 0.7 * np.arange(n)
+    f = torch.zeros((n, 2, 3), device="cuda:0")
+    t = torch.zeros((n, 2, 3), device="cuda:0")
+    ext = np.zeros((2 * n, 6), np.float32)
+    moved = np.zeros(n)
+    for k in range(frames):
+        on = k >= 20                       # settle, then push
+        fx = (push * np.cos(yaw)).astype(np.float32) if on else np.zeros(n, np.float32)
+        fy = (push * np.sin(yaw)).astype(np.float32) if on else np.zeros(n, np.float32)
+        f[:, 1, 0] = torch.from_numpy(fx).cuda()
+        f[:, 1, 1] = torch.from_numpy(fy).cuda()
+        assert gym.apply_rigid_body_force_tensors(sim, gymtorch.unwrap_tensor(f), gymtorch.unwrap_tensor(t),
+                                                  gymapi.ENV_SPACE)
+        ext[1::2, 0] = fx
+        ext[1::2, 1] = fy
+        gym.simulate(sim)
+        gym.fetch_results(sim, True)
+        cf = oracle.step(p, m, st, dof, ext=ext)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_net_contact_force_tensor(sim)
+        got = rb.cpu().numpy()
+        if not np.array_equal(got, st):
+            bad = np.argwhere(got != st)
+            pytest.fail("frame %d: first differing body/field %s, max |diff| %g"
+                        % (k, bad[:3].tolist(), np.abs(got - st).max()))
+        assert np.array_equal(ncf.cpu().numpy(), cf), "frame %d: net contact force" % k
+        if k == 19:
+            x20 = got[1::2, 0:2].copy()
+    moved = np.linalg.norm(got[1::2, 0:2] - x20, axis=1)
+    held = push < 0.8 * mass * G
+    slid = push > 1.1 * mass * G
+    assert held.any() and slid.any()
+    assert np.all(moved[held] < 1e-3)             # held in place by the anchors
+    assert np.all(moved[slid] > 0.02)             # slipping patches slide

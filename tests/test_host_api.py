@@ -215,13 +215,14 @@ def test_set_actor_dof_states_keeps_unselected_column(gym):
     assert np.allclose(gym.get_actor_dof_states(envs[0], 0, gymapi.STATE_ALL)["vel"], 0.0)
 
 
-def test_unmodelled_friction_parameters_warn(gym, capsys):
-    """franka_cube_ik_osc.py:124-125's patch-friction parameters are
-    not modelled; create_sim says so on stderr instead of dropping them."""
+def test_friction_parameters_scope_is_stated(gym, capsys):
+    """franka_cube_ik_osc.py:124-125's patch-friction parameters drive the
+    coupled step's friction anchors but not the lone free-body
+    kernel; create_sim says so on stderr instead of dropping them silently."""
     sp = scenes.franka_sim_params(False)
     sp.physx.friction_offset_threshold = 0.0011
     sp.physx.friction_correlation_distance = 0.00051
     assert gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp) is not None
     err = capsys.readouterr().err
-    assert "friction_offset_threshold = 0.0011 is not modelled" in err
-    assert "friction_correlation_distance = 0.00051 is not modelled" in err
+    assert "friction_offset_threshold = 0.0011 drives the friction anchors of coupled envs only" in err
+    assert "friction_correlation_distance = 0.00051 drives the friction anchors of coupled envs only" in err
