@@ -1069,6 +1069,30 @@ static void aba_world_(const step_t* P, const mg_model* m, const float* LF, cons
     }
 }
 
+/* the TGS normal rows of one sweep, in contact order (mg_env.hip normal_pass) */
+static void normal_pass_(const step_t* P, int nct, const float* cs0, const float* ce, const float* cvn0,
+                         float (*ck)[3], float (*clam)[3], float (*Jr)[OE_GM], float (*Wr)[OE_GM], float* u,
+                         const float* dp, int G, int pos) {
+    int c, ln;
+    for (c = 0; c < nct; ++c) {
+        const float s = cs0[c] + redp_(Jr[c * 3], dp, G);
+        float tg, lam, dl, nl;
+        if (pos) {
+            tg = -s * P->inv_sub;
+            if (s < 0.0f) tg = fminf(tg, P->maxdep);
+        } else {
+            tg = s > 0.0f ? -s * P->inv_h : 0.0f;
+            if (ce[c] > 0.0f && cvn0[c] < -P->bounce) tg = fmaxf(tg, -ce[c] * cvn0[c]);
+        }
+        lam = clam[c][0];
+        dl = ck[c][0] * (tg - redp_(Jr[c * 3], u, G));
+        nl = fmaxf(lam + dl, 0.0f);
+        dl = nl - lam;
+        for (ln = 0; ln < G; ++ln) u[ln] = u[ln] + Wr[c * 3][ln] * dl;
+        clam[c][0] = nl;
+    }
+}
+
 static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float* state, float* dof, const float* tgt,
                      const float* props, const float* ext, float* cforce, float* fcache) {
     const int b0 = ev->art_body, d0 = ev->art_dof, nfr = ev->nf;
@@ -1109,7 +1133,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     /* friction anchors (mg_env.hip EnvLds apt ...): row k's point, tangents in cd[k][1..2] */
     v3_t apt[OE_MAXCT];
     float ae[OE_MAXCT][2], amu[OE_MAXCT], psum[OE_MAXCT];
-    int aa[OE_MAXCT], ab[OE_MAXCT], alast[OE_MAXCT], apair[OE_MAXCT], pstart[OE_MAXCT];
+    int aa[OE_MAXCT], ab[OE_MAXCT], alast[OE_MAXCT], apair[OE_MAXCT], apart[OE_MAXCT], pstart[OE_MAXCT];
     char held[OE_FPP];
     float* fcr = fcache ? fcache + (size_t)ev->env * OE_FC_N : NULL;
     static __thread float Jr[OE_MAXCT * 3][OE_GM], Wr[OE_MAXCT * 3][OE_GM];
@@ -1284,7 +1308,9 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                             cd[nanc][2] = t2;
                             ae[nanc][0] = dot3(dr, t1);
                             ae[nanc][1] = dot3(dr, t2);
-                            amu[nanc] = R.cnt == 2 ? 0.5f * mu : mu;
+                            amu[nanc] = mu;
+                            /* the patch's other anchor, when it has a row: 1 next, 2 previous */
+                            apart[nanc] = R.cnt == 2 ? (j == 0 ? (nanc + 1 < MAXCT ? 1 : 0) : 2) : 0;
                             aa[nanc] = pp->a;
                             ab[nanc] = pp->b;
                             alast[nanc] = last;
@@ -1439,8 +1465,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
         for (it = 0; it < P->npos + P->nvel; ++it) {
             const int pos = it < P->npos;
             int ln;
-            /* friction first, then the normal rows (mg_env.hip: non-penetration has the last word);
-             * the anchors' bound is the patch's normal impulse of the previous sweep */
+            normal_pass_(P, nct, cs0, ce, cvn0, ck, clam, Jr, Wr, u, dp, G, pos);
             {   /* running sums restarting at a patch's first contact */
                 float run = 0.0f;
                 for (c = 0; c < nct; ++c) {
@@ -1449,9 +1474,12 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 }
             }
             for (c = 0; c < nanc; ++c) {   /* anchors: close the drift, share mu N of the patch */
-                const float lim = amu[c] * psum[alast[c]];
+                const float mun = amu[c] * psum[alast[c]];
                 int rw;
                 for (rw = 1; rw < 3; ++rw) {
+                    /* the patch's budget mu N per direction, less its other anchor's impulse */
+                    const float other = apart[c] == 1 ? clam[c + 1][rw] : (apart[c] == 2 ? clam[c - 1][rw] : 0.0f);
+                    const float lim = fmaxf(mun - fabsf(other), 0.0f);
                     const float lam = clam[c][rw];
                     float tg = 0.0f, raw, nl, dl;
                     if (pos) {
@@ -1468,23 +1496,8 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     clam[c][rw] = nl;
                 }
             }
-            for (c = 0; c < nct; ++c) {
-                const float s = cs0[c] + redp_(Jr[c * 3], dp, G);
-                float tg, lam, dl, nl;
-                if (pos) {
-                    tg = -s * P->inv_sub;
-                    if (s < 0.0f) tg = fminf(tg, P->maxdep);
-                } else {
-                    tg = s > 0.0f ? -s * P->inv_h : 0.0f;
-                    if (ce[c] > 0.0f && cvn0[c] < -P->bounce) tg = fmaxf(tg, -ce[c] * cvn0[c]);
-                }
-                lam = clam[c][0];
-                dl = ck[c][0] * (tg - redp_(Jr[c * 3], u, G));
-                nl = fmaxf(lam + dl, 0.0f);
-                dl = nl - lam;
-                for (ln = 0; ln < G; ++ln) u[ln] = u[ln] + Wr[c * 3][ln] * dl;
-                clam[c][0] = nl;
-            }
+            /* the last position sweep and the velocity sweeps end with the normal rows again (mg_env.hip) */
+            if (it >= P->npos - 1) normal_pass_(P, nct, cs0, ce, cvn0, ck, clam, Jr, Wr, u, dp, G, pos);
             if (pos)
                 for (ln = 0; ln < G; ++ln) dp[ln] = dp[ln] + u[ln] * P->sub;
         }

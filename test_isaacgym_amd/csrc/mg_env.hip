@@ -116,8 +116,8 @@ struct EnvLds {
     Q4 sq[MG_ENV_MAXS];
     // friction anchors (patch friction): anchor k's point (its
     // A copy, world), drift of its two copies along the patch tangents
-    // (cd[k][1], cd[k][2]), Coulomb share mu / anchors, participants a | b << 16,
-    // last contact of its patch | pair index << 8
+    // (cd[k][1], cd[k][2]), friction coefficient, participants a | b << 16, last
+    // contact of its patch | partner anchor (1: next, 2: previous) << 8 | pair << 10
     V3 apt[MAXCT];
     float ae[MAXCT][2], amu[MAXCT];
     int aab[MAXCT], alast[MAXCT];
@@ -1421,9 +1421,11 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                             S.cd[k][2] = t2;
                             S.ae[k][0] = vdot(dr, t1);
                             S.ae[k][1] = vdot(dr, t2);
-                            S.amu[k] = R.cnt == 2 ? 0.5f * mu : mu;
+                            // the patch's other anchor, when it has a row
+                            const int pc = R.cnt == 2 ? (j == 0 ? (k + 1 < MAXCT ? 1 : 0) : 2) : 0;
+                            S.amu[k] = mu;
                             S.aab[k] = (pa & 0xFFFF) | (pb << 16);
-                            S.alast[k] = last | (pidx << 8);
+                            S.alast[k] = last | (pc << 8) | (pidx << 10);
                         }
                     }
                 }
@@ -1550,10 +1552,34 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         bool slip = false;   // anchor ln's friction bound clamped in the last iteration
         for (int it = 0; it < P.npos + P.nvel; ++it) {
             const bool pos = it < P.npos;
-            // friction first, then the normal rows, so that non-penetration has
-            // the last word in every sweep. The anchors' bound
-            // is the patch's normal impulse of the previous sweep: running sums
-            // in contact order, restarting at the contact that opens a patch
+            // the normal rows (every lane of the env holds the same lambdas: red16
+            // and the LDS operands are the same in all 16 lanes)
+            auto normal_pass = [&]() {
+#pragma unroll
+                for (int c = 0; c < MAXCT; ++c) {
+                    if (c < nct) {
+                        const float s = S.cs0[c] + redg<G>(Jr[c * 3] * dp);
+                        float tgt;
+                        if (pos) {
+                            tgt = -s * P.inv_sub;
+                            if (s < 0.0f) tgt = fminf(tgt, P.max_depen);
+                        } else {
+                            tgt = s > 0.0f ? -s * P.inv_h : 0.0f;
+                            const float ev = S.ce[c], vn0 = S.cvn0[c];
+                            if (ev > 0.0f && vn0 < -P.bounce_thresh) tgt = fmaxf(tgt, -ev * vn0);
+                        }
+                        const float lm = lam[c * 3];
+                        float dl = S.ck[c][0] * (tgt - redg<G>(Jr[c * 3] * uv));
+                        const float nl = fmaxf(lm + dl, 0.0f);
+                        dl = nl - lm;
+                        uv = uv + Wr[c * 3] * dl;
+                        lam[c * 3] = nl;
+                    }
+                }
+            };
+            normal_pass();
+            // each patch's normal impulse: running sums in contact order,
+            // restarting at the contact that opens a patch
             {
                 const unsigned long long ps = S.pstart;
                 float run = 0.0f;
@@ -1570,9 +1596,17 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 #pragma unroll
             for (int c = 0; c < MAXCT; ++c) {
                 if (c < nanc) {
-                    const float lim = S.amu[c] * S.psum[S.alast[c] & 0xFF];
+                    const int al = S.alast[c];
+                    const int pc = (al >> 8) & 3;
+                    const float mun = S.amu[c] * S.psum[al & 0xFF];
 #pragma unroll
                     for (int rw = 1; rw < 3; ++rw) {
+                        // the patch's Coulomb budget mu N per direction, less what its
+                        // other anchor holds along it (current impulse)
+                        float other = 0.0f;
+                        if (c + 1 < MAXCT && pc == 1) other = lam[(c + 1) * 3 + rw];
+                        if (c >= 1 && pc == 2) other = lam[(c - 1) * 3 + rw];
+                        const float lim = fmaxf(mun - fabsf(other), 0.0f);
                         float tgt = 0.0f;
                         if (pos) {   // close 80 % of the drift of the anchor's two copies per substep
                             const float s = S.ae[c][rw - 1] + redg<G>(Jr[c * 3 + rw] * dp);
@@ -1588,29 +1622,11 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     }
                 }
             }
-#pragma unroll
-            for (int c = 0; c < MAXCT; ++c) {
-                if (c < nct) {
-                    const float s = S.cs0[c] + redg<G>(Jr[c * 3] * dp);
-                    float tgt;
-                    if (pos) {
-                        tgt = -s * P.inv_sub;
-                        if (s < 0.0f) tgt = fminf(tgt, P.max_depen);
-                    } else {
-                        tgt = s > 0.0f ? -s * P.inv_h : 0.0f;
-                        const float ev = S.ce[c], vn0 = S.cvn0[c];
-                        if (ev > 0.0f && vn0 < -P.bounce_thresh) tgt = fmaxf(tgt, -ev * vn0);
-                    }
-                    // every lane of the env holds the same lambdas (red16 and
-                    // the LDS operands are the same in all 16 lanes)
-                    const float lm = lam[c * 3];
-                    float dl = S.ck[c][0] * (tgt - redg<G>(Jr[c * 3] * uv));
-                    const float nl = fmaxf(lm + dl, 0.0f);
-                    dl = nl - lm;
-                    uv = uv + Wr[c * 3] * dl;
-                    lam[c * 3] = nl;
-                }
-            }
+            // the last position sweep and the velocity sweeps end with the normal
+            // rows again: a friction bound the size of a grip cannot drag a body
+            // into a unilateral contact that eight Gauss-Seidel sweeps would not
+            // converge
+            if (it >= P.npos - 1) normal_pass();
             if (pos) dp = dp + uv * P.sub;
         }
         if (ln == 0) {
@@ -1625,7 +1641,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         }
         // a slipping patch lets go of its anchors (regrown at the next substep)
         if (live && slip && ln < nanc) {
-            const int pidx = S.alast[ln] >> 8;
+            const int pidx = S.alast[ln] >> 10;
             if (pidx < MG_FP_MAXP) A.fpatch[(size_t)(pair0 + pidx) * MG_FP_N] = 0.0f;
         }
         __syncthreads();

@@ -755,8 +755,11 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
 #ifndef MG_RIGID1_ROUND_WAVES
 #define MG_RIGID1_ROUND_WAVES 3
 #endif
+#ifndef MG_RIGID1_WIDE_WAVES
+#define MG_RIGID1_WIDE_WAVES 3
+#endif
 template <bool UPZ, bool LDS_T, bool WIDE>
-__global__ void __launch_bounds__(64, UPZ && WIDE ? 3 : (UPZ ? MG_RIGID1_ROUND_WAVES : 2))
+__global__ void __launch_bounds__(64, UPZ && WIDE ? MG_RIGID1_WIDE_WAVES : (UPZ ? MG_RIGID1_ROUND_WAVES : 2))
 k_rigid_step1(MgStep P, MgRigidArgs A) {
     extern __shared__ float s_trec[];
     const int i = (WIDE ? gridDim.x - 1 - blockIdx.x : blockIdx.x) * 64 + threadIdx.x;
@@ -817,32 +820,62 @@ k_rigid_step1(MgStep P, MgRigidArgs A) {
         G.t2 = v3(P.t2[0], P.t2[1], P.t2[2]);
         rigid_body1<!WIDE>(G, P, T, x, q, v, w, fsum, invm, invI, iq, com, A.ext != nullptr, fext, text, A.hulls);
     }
-    if (!live) return;
     // the output addresses are recomputed here (an opaque copy of the slot)
     // rather than kept live in registers across the frame
     int bo = b;
     asm volatile("" : "+v"(bo));
-    float* So = A.state;
-    So[0 * nb + bo] = x.x; So[1 * nb + bo] = x.y; So[2 * nb + bo] = x.z;
-    So[3 * nb + bo] = q.x; So[4 * nb + bo] = q.y; So[5 * nb + bo] = q.z; So[6 * nb + bo] = q.w;
-    So[7 * nb + bo] = v.x; So[8 * nb + bo] = v.y; So[9 * nb + bo] = v.z;
-    So[10 * nb + bo] = w.x; So[11 * nb + bo] = w.y; So[12 * nb + bo] = w.z;
-    A.cforce[0 * nb + bo] = fsum.x * P.inv_dt;
-    A.cforce[1 * nb + bo] = fsum.y * P.inv_dt;
-    A.cforce[2 * nb + bo] = fsum.z * P.inv_dt;
-    if (A.out_rb) {
+    if (live) {
+        float* So = A.state;
+        So[0 * nb + bo] = x.x; So[1 * nb + bo] = x.y; So[2 * nb + bo] = x.z;
+        So[3 * nb + bo] = q.x; So[4 * nb + bo] = q.y; So[5 * nb + bo] = q.z; So[6 * nb + bo] = q.w;
+        So[7 * nb + bo] = v.x; So[8 * nb + bo] = v.y; So[9 * nb + bo] = v.z;
+        So[10 * nb + bo] = w.x; So[11 * nb + bo] = w.y; So[12 * nb + bo] = w.z;
+        A.cforce[0 * nb + bo] = fsum.x * P.inv_dt;
+        A.cforce[1 * nb + bo] = fsum.y * P.inv_dt;
+        A.cforce[2 * nb + bo] = fsum.z * P.inv_dt;
+    }
+    if (A.out_rb && !WIDE) {
         // the refresh fused into the step: the same 13 values into the bound
         // rigid-body row and, for a root body, its actor's root row (the rows the
         // paired gather k_gather_rb_root would write from the SoA state)
+        if (live) {
+            const float o[MG_STATE_N] = {x.x, x.y, x.z, q.x, q.y, q.z, q.w, v.x, v.y, v.z, w.x, w.y, w.z};
+            float* R = A.out_rb + (size_t)A.out_body[bo] * MG_STATE_N;
+#pragma unroll
+            for (int k = 0; k < MG_STATE_N; ++k) R[k] = o[k];
+            const int rr = A.out_root_row[bo];
+            if (rr >= 0) {
+                float* Ro = A.out_root + (size_t)rr * MG_STATE_N;
+#pragma unroll
+                for (int k = 0; k < MG_STATE_N; ++k) Ro[k] = o[k];
+            }
+        }
+    } else if (A.out_rb) {   // launch-uniform
+        // Wide launches are issue-bound, and the rows are 52-B AoS records, every
+        // other one per wave (the wave holds one template: UAVs or cars): written
+        // lane by lane, each store instruction touches 64 rows 104 B apart. The
+        // wave's rows are transposed through LDS instead, so that store k writes
+        // elements k*64 .. k*64+63 of the wave's 64 x 13 block — runs of
+        // consecutive floats, five rows each (262k envs: 46.9 -> 45.6 us; a
+        // one-round launch is latency-bound and pays the LDS round trip: 10.2 ->
+        // 11.3 us at 4096, so it keeps the direct stores).
+        __shared__ float s_out[64 * 16];
+        __shared__ int s_dst[2][64];
+        const int l = threadIdx.x;
         const float o[MG_STATE_N] = {x.x, x.y, x.z, q.x, q.y, q.z, q.w, v.x, v.y, v.z, w.x, w.y, w.z};
-        float* R = A.out_rb + (size_t)A.out_body[bo] * MG_STATE_N;
 #pragma unroll
-        for (int k = 0; k < MG_STATE_N; ++k) R[k] = o[k];
-        const int rr = A.out_root_row[bo];
-        if (rr >= 0) {
-            float* Ro = A.out_root + (size_t)rr * MG_STATE_N;
+        for (int k = 0; k < MG_STATE_N; ++k) s_out[l * 16 + k] = o[k];
+        s_dst[0][l] = live ? A.out_body[bo] : -1;
+        s_dst[1][l] = live ? A.out_root_row[bo] : -1;
+        __syncthreads();
 #pragma unroll
-            for (int k = 0; k < MG_STATE_N; ++k) Ro[k] = o[k];
+        for (int k = 0; k < MG_STATE_N; ++k) {
+            const int e = k * 64 + l;
+            const int row = e / MG_STATE_N, col = e - row * MG_STATE_N;
+            const float val = s_out[row * 16 + col];
+            const int d0 = s_dst[0][row], d1 = s_dst[1][row];
+            if (d0 >= 0) A.out_rb[(size_t)d0 * MG_STATE_N + col] = val;
+            if (d1 >= 0) A.out_root[(size_t)d1 * MG_STATE_N + col] = val;
         }
     }
 }

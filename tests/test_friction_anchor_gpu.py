@@ -3,8 +3,9 @@ k_env_step's patch records, anchor rows and slip release against the oracle's
 restatement (oracle/migym_oracle_env.c patch_update_), bit for bit.
 
 64 envs of a tile on a table, each yawed differently and pushed sideways every
-frame by its own force from 0.3 to 1.4 mu m g (held by its anchors, or
-slipping and re-anchoring), through gym.apply_rigid_body_force_tensors — the
+frame by its own force from 0.3 to 2 mu m g (held by its anchors, or
+slipping and re-anchoring; the per-direction bound of the tangent rows holds
+up to sqrt(2) mu m g along a diagonal of the patch basis), through gym.apply_rigid_body_force_tensors — the
 device keeps its patches inside the sim, the oracle in the cache that goes with
 its state array.
 """
@@ -62,7 +63,7 @@ def test_friction_anchor_push_parity_gpu(gym):
     st = sim.model_arrays["body_state0"].copy()
     dof = np.zeros((0, 2), np.float32)
     mass = 1000.0 * 0.1 * 0.1 * 0.02
-    push = np.linspace(0.3, 1.4, n).astype(np.float32) * np.float32(mass * G)
+    push = np.linspace(0.3, 2.0, n).astype(np.float32) * np.float32(mass * G)
     yaw = 0.7 * np.arange(n)
     f = torch.zeros((n, 2, 3), device="cuda:0")
     t = torch.zeros((n, 2, 3), device="cuda:0")
@@ -92,8 +93,8 @@ def test_friction_anchor_push_parity_gpu(gym):
         if k == 19:
             x20 = got[1::2, 0:2].copy()
     moved = np.linalg.norm(got[1::2, 0:2] - x20, axis=1)
-    held = push < 0.8 * mass * G
-    slid = push > 1.1 * mass * G
+    held = push < 0.9 * mass * G
+    slid = push > 1.5 * mass * G
     assert held.any() and slid.any()
     assert np.all(moved[held] < 1e-3)             # held in place by the anchors
     assert np.all(moved[slid] > 0.02)             # slipping patches slide

@@ -1,7 +1,7 @@
 """Kernel microbenchmark: average k_rigid_step duration (HIP events around each
 launch) for the servo scene at several env counts, for the library selected
 by MIGYM_LIB (default: the in-tree build). KB_FUSION sets gym.set_step_fusion's
-flags (default 15, as bench.py). Prints one JSON line per size."""
+flags (default 15; 31 adds the refresh fused into the step, as bench.py). Prints one JSON line per size."""
 import ctypes
 import json
 import os
@@ -22,6 +22,7 @@ def run(n, steps=200, warm=20):
     N.lib.mg_set_kernel_timing(sim.native, 1)
     gym.set_step_fusion(sim, int(os.environ.get("KB_FUSION", "15")))   # bench.py's setting
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))   # bound: KB_FUSION=31 fuses the refresh
     acts = scenes.servo_actions(n, 32, "cuda:0", seed=0)
     gym.refresh_actor_root_state_tensor(sim)
     for k in range(warm + steps):
