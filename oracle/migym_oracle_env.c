@@ -1306,8 +1306,11 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                             apt[nanc] = wA;
                             cd[nanc][1] = t1;
                             cd[nanc][2] = t2;
-                            ae[nanc][0] = dot3(dr, t1);
-                            ae[nanc][1] = dot3(dr, t2);
+                            {   /* position sweeps: close 80 % of the substep-start drift */
+                                const float kd = 0.8f * P->inv_h;
+                                ae[nanc][0] = fminf(fmaxf(-dot3(dr, t1) * kd, -P->maxdep), P->maxdep);
+                                ae[nanc][1] = fminf(fmaxf(-dot3(dr, t2) * kd, -P->maxdep), P->maxdep);
+                            }
                             amu[nanc] = mu;
                             /* the patch's other anchor, when it has a row: 1 next, 2 previous */
                             apart[nanc] = R.cnt == 2 ? (j == 0 ? (nanc + 1 < MAXCT ? 1 : 0) : 2) : 0;
@@ -1481,11 +1484,8 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     const float other = apart[c] == 1 ? clam[c + 1][rw] : (apart[c] == 2 ? clam[c - 1][rw] : 0.0f);
                     const float lim = fmaxf(mun - fabsf(other), 0.0f);
                     const float lam = clam[c][rw];
-                    float tg = 0.0f, raw, nl, dl;
-                    if (pos) {
-                        const float s = ae[c][rw - 1] + redp_(Jr[c * 3 + rw], dp, G);
-                        tg = fminf(fmaxf(-s * (0.8f * P->inv_h), -P->maxdep), P->maxdep);
-                    }
+                    const float tg = pos ? ae[c][rw - 1] : 0.0f;
+                    float raw, nl, dl;
                     raw = lam + ck[c][rw] * (tg - redp_(Jr[c * 3 + rw], u, G));
                     nl = fminf(fmaxf(raw, -lim), lim);
                     /* slipping in the last iteration: the patch lets go of its anchors */

@@ -115,7 +115,8 @@ struct EnvLds {
     V3 sx[MG_ENV_MAXS];              // static bodies: pose (they do not move in the step)
     Q4 sq[MG_ENV_MAXS];
     // friction anchors (patch friction): anchor k's point (its
-    // A copy, world), drift of its two copies along the patch tangents
+    // A copy, world), position-sweep target velocities closing the drift of its
+    // two copies along the patch tangents
     // (cd[k][1], cd[k][2]), friction coefficient, participants a | b << 16, last
     // contact of its patch | partner anchor (1: next, 2: previous) << 8 | pair << 10
     V3 apt[MAXCT];
@@ -1419,8 +1420,11 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                             S.apt[k] = wA;
                             S.cd[k][1] = t1;
                             S.cd[k][2] = t2;
-                            S.ae[k][0] = vdot(dr, t1);
-                            S.ae[k][1] = vdot(dr, t2);
+                            // position sweeps' target velocity along t1, t2: close 80 %
+                            // of the substep-start drift of the anchor's two copies
+                            const float kd = 0.8f * P.inv_h;
+                            S.ae[k][0] = fminf(fmaxf(-vdot(dr, t1) * kd, -P.max_depen), P.max_depen);
+                            S.ae[k][1] = fminf(fmaxf(-vdot(dr, t2) * kd, -P.max_depen), P.max_depen);
                             // the patch's other anchor, when it has a row
                             const int pc = R.cnt == 2 ? (j == 0 ? (k + 1 < MAXCT ? 1 : 0) : 2) : 0;
                             S.amu[k] = mu;
@@ -1607,11 +1611,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         if (c + 1 < MAXCT && pc == 1) other = lam[(c + 1) * 3 + rw];
                         if (c >= 1 && pc == 2) other = lam[(c - 1) * 3 + rw];
                         const float lim = fmaxf(mun - fabsf(other), 0.0f);
-                        float tgt = 0.0f;
-                        if (pos) {   // close 80 % of the drift of the anchor's two copies per substep
-                            const float s = S.ae[c][rw - 1] + redg<G>(Jr[c * 3 + rw] * dp);
-                            tgt = fminf(fmaxf(-s * (0.8f * P.inv_h), -P.max_depen), P.max_depen);
-                        }
+                        const float tgt = pos ? S.ae[c][rw - 1] : 0.0f;   // drift closing (position sweeps)
                         const float lm = lam[c * 3 + rw];
                         const float raw = lm + S.ck[c][rw] * (tgt - redg<G>(Jr[c * 3 + rw] * uv));
                         const float nl = fminf(fmaxf(raw, -lim), lim);

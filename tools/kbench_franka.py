@@ -71,7 +71,9 @@ def run(n, warm=150, steps=100):
                  ea=ea.cpu().numpy())
     lifted = float((maxz > 0.55).float().mean())
     bz = rb[bi, 2]
-    sunk = int(((bz > 0.3) & (bz < 0.4225 - 0.005) & (rb[bi, 7:10].norm(dim=1) < 0.05)).sum())
+    rel = rb[bi, 0:2] - rb[bi - 1, 0:2]       # from the table centre (tests/test_franka_gpu.py)
+    over = (rel[:, 0].abs() < 0.3 - 0.0225) & (rel[:, 1].abs() < 0.5 - 0.0225)
+    sunk = int(((bz > 0.3) & (bz < 0.4225 - 0.005) & (rb[bi, 7:10].norm(dim=1) < 0.05) & over).sum())
     gym.destroy_sim(sim)
     return {"lib": os.path.basename(N.LIB_PATH), "envs": n, "kernel_us_avg": 1e3 * avg.value,
             "kernel_us_min": 1e3 * lo.value, "launches": used, "window": [warm, warm + steps],
