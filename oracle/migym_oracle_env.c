@@ -1194,7 +1194,9 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     }
 
     for (st_ = 0; st_ < P->substeps; ++st_) {
-        int nct = 0, link_rows = 0, nanc = 0;
+        int nct = 0, link_rows = 0, nanc = 0, npatch = 0;
+        int ppair[OE_MAXCT], pslot[OE_MAXCT], pnum[OE_MAXCT];
+        float pmu[OE_MAXCT];
         /* the pairs that held a patch at the end of the last substep */
         for (i = 0; i < OE_FPP; ++i) {
             held[i] = fcr ? fcr[(size_t)i * (OE_FP_N + 1) + OE_FP_N] != 0.0f : 0;
@@ -1283,45 +1285,67 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                         nct++;
                     }
                 }
-                /* the pair's friction patch (mg_env.hip: its first contact placed) */
+                /* the pair's friction patch (mg_env.hip: its first contact placed), in pair order */
                 if (o.n > 0 && slot0 < MAXCT) {
-                    patch_t R;
-                    v3_t pxb = V(0.0f, 0.0f, 0.0f), t1, t2;
-                    q4_t pqb = Q(0.0f, 0.0f, 0.0f, 1.0f);
-                    const int last = (slot0 + o.n < MAXCT ? slot0 + o.n : MAXCT) - 1;
-                    if (pp->b >= 0) { pxb = xb; pqb = qb; }
-                    R.cnt = 0;
-                    if (i < OE_FPP && held[i]) patch_load_(&R, fcr + (size_t)i * (OE_FP_N + 1));
-                    patch_update_(&R, xa, qa, pxb, pqb, &o, P->fot, P->corr);
-                    if (i < OE_FPP && fcr) {
-                        patch_store_(&R, fcr + (size_t)i * (OE_FP_N + 1));
-                        fcr[(size_t)i * (OE_FP_N + 1) + OE_FP_N] = 1.0f;
-                    }
-                    pstart[slot0] = 1;
-                    tangents_(o.nrm[0], &t1, &t2);
-                    for (j = 0; j < R.cnt; ++j) {
-                        if (nanc < MAXCT) {
-                            const v3_t wA = add3(xa, qrot_(qa, R.aA[j])), wB = add3(pxb, qrot_(pqb, R.aB[j]));
-                            const v3_t dr = sub3(wA, wB);
-                            apt[nanc] = wA;
-                            cd[nanc][1] = t1;
-                            cd[nanc][2] = t2;
-                            {   /* position sweeps: close 80 % of the substep-start drift */
-                                const float kd = 0.8f * P->inv_h;
-                                ae[nanc][0] = fminf(fmaxf(-dot3(dr, t1) * kd, -P->maxdep), P->maxdep);
-                                ae[nanc][1] = fminf(fmaxf(-dot3(dr, t2) * kd, -P->maxdep), P->maxdep);
-                            }
-                            amu[nanc] = mu;
-                            /* the patch's other anchor, when it has a row: 1 next, 2 previous */
-                            apart[nanc] = R.cnt == 2 ? (j == 0 ? (nanc + 1 < MAXCT ? 1 : 0) : 2) : 0;
-                            aa[nanc] = pp->a;
-                            ab[nanc] = pp->b;
-                            alast[nanc] = last;
-                            apair[nanc] = i;
-                        }
-                        nanc++;
-                    }
+                    ppair[npatch] = i;
+                    pslot[npatch] = slot0;
+                    pnum[npatch] = o.n < MAXCT - slot0 ? o.n : MAXCT - slot0;
+                    pmu[npatch] = mu;
+                    npatch++;
                 }
+            }
+        }
+        /* friction patches (mg_env.hip: the pass after the narrow phase, one per lane) */
+        for (k = 0; k < npatch; ++k) {
+            const int slot0 = pslot[k], pn = pnum[k], ip = ppair[k];
+            const int a = ca[slot0], b = cb[slot0];
+            patch_t R;
+            pair_t o;
+            v3_t pxa, pxb = V(0.0f, 0.0f, 0.0f), t1, t2;
+            q4_t pqa, pqb = Q(0.0f, 0.0f, 0.0f, 1.0f);
+            o.n = pn;
+            for (j = 0; j < pn; ++j) { o.p[j] = cp[slot0 + j]; o.nrm[j] = cd[slot0 + j][0]; o.sep[j] = cs0[slot0 + j]; }
+            if (a >= OE_F0) { pxa = fx[a - OE_F0]; pqa = fq[a - OE_F0]; }
+            else { pxa = xl[a]; pqa = ql[a]; }
+            if (b >= OE_ST0) {
+                const float* ss = state + (size_t)ev->stat_b[b - OE_ST0] * MG_STATE_N;
+                pxb = V(ss[0], ss[1], ss[2]);
+                pqb = qnorm_(Q(ss[3], ss[4], ss[5], ss[6]));
+            } else if (b >= OE_F0) {
+                pxb = fx[b - OE_F0];
+                pqb = fq[b - OE_F0];
+            } else if (b >= 0) {
+                pxb = xl[b];
+                pqb = ql[b];
+            }
+            R.cnt = 0;
+            if (ip < OE_FPP && held[ip]) patch_load_(&R, fcr + (size_t)ip * (OE_FP_N + 1));
+            patch_update_(&R, pxa, pqa, pxb, pqb, &o, P->fot, P->corr);
+            if (ip < OE_FPP && fcr) {
+                patch_store_(&R, fcr + (size_t)ip * (OE_FP_N + 1));
+                fcr[(size_t)ip * (OE_FP_N + 1) + OE_FP_N] = 1.0f;
+            }
+            pstart[slot0] = 1;
+            tangents_(o.nrm[0], &t1, &t2);
+            for (j = 0; j < R.cnt; ++j) {
+                if (nanc < MAXCT) {
+                    const v3_t wA = add3(pxa, qrot_(pqa, R.aA[j])), wB = add3(pxb, qrot_(pqb, R.aB[j]));
+                    const v3_t dr = sub3(wA, wB);
+                    const float kd = 0.8f * P->inv_h;   /* position sweeps: close 80 % of the substep-start drift */
+                    apt[nanc] = wA;
+                    cd[nanc][1] = t1;
+                    cd[nanc][2] = t2;
+                    ae[nanc][0] = fminf(fmaxf(-dot3(dr, t1) * kd, -P->maxdep), P->maxdep);
+                    ae[nanc][1] = fminf(fmaxf(-dot3(dr, t2) * kd, -P->maxdep), P->maxdep);
+                    amu[nanc] = pmu[k];
+                    /* the patch's other anchor, when it has a row: 1 next, 2 previous */
+                    apart[nanc] = R.cnt == 2 ? (j == 0 ? (nanc + 1 < MAXCT ? 1 : 0) : 2) : 0;
+                    aa[nanc] = a;
+                    ab[nanc] = b;
+                    alast[nanc] = slot0 + pn - 1;
+                    apair[nanc] = ip;
+                }
+                nanc++;
             }
         }
         if (nanc > MAXCT) nanc = MAXCT;

@@ -123,6 +123,7 @@ struct EnvLds {
     float ae[MAXCT][2], amu[MAXCT];
     int aab[MAXCT], alast[MAXCT];
     float psum[MAXCT];               // running normal impulse of each contact's patch
+    int ppair[MAXCT];                // patch k: pair index << 10 | first contact << 4 | its placed contacts
     unsigned fpv[MG_FP_W], fpn[MG_FP_W];   // pairs holding a patch: last substep, this one
     unsigned long long pstart;       // contacts that open a patch
 };
@@ -1278,7 +1279,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         //     has no contact within the margin);
         // (b) the full pair test on the survivors, one per lane per round,
         //     contacts placed by a 16-lane prefix sum in pair order.
-        int base = 0, abase = 0;   // contacts, friction anchors placed so far
+        int base = 0, npatch = 0;   // contacts, friction patches placed so far
         for (int blk = 0; __any(blk < npair); blk += NPB) {
             int nnear = 0;
 #pragma unroll
@@ -1306,7 +1307,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 PH_NP0();
                 PairOut o;
                 o.n = 0;
-                float mu = 0.0f, rest = 0.0f;
+                float rest = 0.0f;
                 int pa = 0, pb = -1, pidx = 0;
                 bool coop = false;
                 CShape cA = {}, cB = {};
@@ -1324,7 +1325,6 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         Q4 qa;
                         pair_pose(S, pa, xa, qa);
                         ground_pair(P, place_shape(sha, xa, qa, A.hulls), o);
-                        mu = 0.5f * (sha[11] + P.mu_ground);
                         rest = 0.5f * (sha[12] + P.e_ground);
                     } else {
                         const float* shb = A.shapes + sb * MG_SHAPE_STRIDE;
@@ -1337,7 +1337,6 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         cB = place_shape(shb, xb, qb, A.hulls);
                         if (!coop) collide(cA, cB, P.contact_offset, o);
                         PH_COUNT(11, ((int)sha[0] == MG_SHAPE_CONVEX || (int)shb[0] == MG_SHAPE_CONVEX) ? 1 : 0);
-                        mu = 0.5f * (sha[11] + shb[11]);
                         rest = 0.5f * (sha[12] + shb[12]);
                     }
                 }
@@ -1379,65 +1378,98 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     }
                 }
                 base += total;
-                // the pair's friction patch (its first contact placed): anchors
-                // kept from the last substep or grown from these contacts
-                Patch R;
-                R.cnt = 0;
-                V3 pxa = v3(0.0f, 0.0f, 0.0f), pxb = v3(0.0f, 0.0f, 0.0f);
-                Q4 pqa = q4(0.0f, 0.0f, 0.0f, 1.0f), pqb = q4(0.0f, 0.0f, 0.0f, 1.0f);
-                if (o.n > 0 && slot0 < MAXCT) {
-                    pair_pose(S, pa, pxa, pqa);
-                    if (pb >= 0) pair_pose(S, pb, pxb, pqb);
-                    float* rec = A.fpatch + (size_t)(pair0 + pidx) * MG_FP_N;
-                    const bool held = pidx < MG_FP_MAXP && ((S.fpv[pidx >> 5] >> (pidx & 31)) & 1u);
-                    if (held) patch_load(R, rec);
-                    patch_update(R, pxa, pqa, pxb, pqb, o, P.fric_offset, P.fric_corr);
-                    if (pidx < MG_FP_MAXP) {
-                        patch_store(R, rec);
-                        atomicOr(&S.fpn[pidx >> 5], 1u << (pidx & 31));
-                    }
-                    atomicOr(&S.pstart, 1ull << slot0);
-                }
-                int ain = R.cnt;
+                // the pair's friction patch (its first contact placed), in pair
+                // order; updated after the narrow phase, one patch per lane
+                const int pn = (o.n > 0 && slot0 < MAXCT) ? 1 : 0;
+                int pin = pn;
 #pragma unroll
                 for (int off = 1; off < G; off <<= 1) {
-                    const int t = __shfl_up(ain, off, G);
-                    if (ln >= off) ain += t;
+                    const int t = __shfl_up(pin, off, G);
+                    if (ln >= off) pin += t;
                 }
-                const int atot = __shfl(ain, G - 1, G);
-                const int ak0 = abase + ain - R.cnt;
-                if (R.cnt > 0) {
-                    const V3 n0 = o.nrm[0];
-                    V3 t1, t2;
-                    env_tangents(n0, &t1, &t2);
-                    const int last = (slot0 + o.n < MAXCT ? slot0 + o.n : MAXCT) - 1;
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const int k = ak0 + j;
-                        if (j < R.cnt && k < MAXCT) {
-                            const V3 wA = vadd(pxa, qrot(pqa, R.aA[j])), wB = vadd(pxb, qrot(pqb, R.aB[j]));
-                            const V3 dr = vsub(wA, wB);
-                            S.apt[k] = wA;
-                            S.cd[k][1] = t1;
-                            S.cd[k][2] = t2;
-                            // position sweeps' target velocity along t1, t2: close 80 %
-                            // of the substep-start drift of the anchor's two copies
-                            const float kd = 0.8f * P.inv_h;
-                            S.ae[k][0] = fminf(fmaxf(-vdot(dr, t1) * kd, -P.max_depen), P.max_depen);
-                            S.ae[k][1] = fminf(fmaxf(-vdot(dr, t2) * kd, -P.max_depen), P.max_depen);
-                            // the patch's other anchor, when it has a row
-                            const int pc = R.cnt == 2 ? (j == 0 ? (k + 1 < MAXCT ? 1 : 0) : 2) : 0;
-                            S.amu[k] = mu;
-                            S.aab[k] = (pa & 0xFFFF) | (pb << 16);
-                            S.alast[k] = last | (pc << 8) | (pidx << 10);
-                        }
-                    }
-                }
-                abase += atot;
+                if (pn) S.ppair[npatch + pin - 1] = (pidx << 10) | (slot0 << 4) | (o.n < MAXCT - slot0 ? o.n : MAXCT - slot0);
+                npatch += __shfl(pin, G - 1, G);
                 PH_NP(20);
             }
             __syncthreads();
             PH_MARK(9);
+        }
+        // friction patches, one per lane: anchors kept from
+        // the last substep or grown from the patch's placed contacts
+        int abase = 0;
+        {
+            Patch R;
+            R.cnt = 0;
+            V3 pxa = v3(0.0f, 0.0f, 0.0f), pxb = v3(0.0f, 0.0f, 0.0f), n0 = v3(0.0f, 0.0f, 1.0f);
+            Q4 pqa = q4(0.0f, 0.0f, 0.0f, 1.0f), pqb = q4(0.0f, 0.0f, 0.0f, 1.0f);
+            int pidx = 0, slot0 = 0, pn = 0, pa = 0, pb = -1;
+            float mu = 0.0f;
+            if (live && ln < npatch) {
+                const int pp = S.ppair[ln];
+                pidx = pp >> 10;
+                slot0 = (pp >> 4) & 63;
+                pn = pp & 15;
+                pa = S.ca[slot0];
+                pb = S.cb[slot0];
+                const int* pr = A.pairs + (size_t)(pair0 + pidx) * 4;
+                const float fa = A.shapes[pr[1] * MG_SHAPE_STRIDE + 11];
+                mu = pb < 0 ? 0.5f * (fa + P.mu_ground) : 0.5f * (fa + A.shapes[pr[3] * MG_SHAPE_STRIDE + 11]);
+                PairOut o;
+                o.n = pn;
+#pragma unroll
+                for (int j = 0; j < MG_PAIR_MAXC; ++j) {
+                    const int c = j < pn ? slot0 + j : slot0;
+                    o.p[j] = S.cp[c];
+                    o.nrm[j] = S.cd[c][0];
+                    o.sep[j] = S.cs0[c];   // separation beyond the rest offset
+                }
+                n0 = o.nrm[0];
+                pair_pose(S, pa, pxa, pqa);
+                if (pb >= 0) pair_pose(S, pb, pxb, pqb);
+                float* rec = A.fpatch + (size_t)(pair0 + pidx) * MG_FP_N;
+                const bool held = pidx < MG_FP_MAXP && ((S.fpv[pidx >> 5] >> (pidx & 31)) & 1u);
+                if (held) patch_load(R, rec);
+                patch_update(R, pxa, pqa, pxb, pqb, o, P.fric_offset, P.fric_corr);
+                if (pidx < MG_FP_MAXP) {
+                    patch_store(R, rec);
+                    atomicOr(&S.fpn[pidx >> 5], 1u << (pidx & 31));
+                }
+                atomicOr(&S.pstart, 1ull << slot0);
+            }
+            int ain = R.cnt;
+#pragma unroll
+            for (int off = 1; off < G; off <<= 1) {
+                const int t = __shfl_up(ain, off, G);
+                if (ln >= off) ain += t;
+            }
+            abase = __shfl(ain, G - 1, G);
+            const int ak0 = ain - R.cnt;
+            if (R.cnt > 0) {
+                V3 t1, t2;
+                env_tangents(n0, &t1, &t2);
+                const int last = slot0 + pn - 1;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int k = ak0 + j;
+                    if (j < R.cnt && k < MAXCT) {
+                        const V3 wA = vadd(pxa, qrot(pqa, R.aA[j])), wB = vadd(pxb, qrot(pqb, R.aB[j]));
+                        const V3 dr = vsub(wA, wB);
+                        S.apt[k] = wA;
+                        S.cd[k][1] = t1;
+                        S.cd[k][2] = t2;
+                        // position sweeps' target velocity along t1, t2: close 80 %
+                        // of the substep-start drift of the anchor's two copies
+                        const float kd = 0.8f * P.inv_h;
+                        S.ae[k][0] = fminf(fmaxf(-vdot(dr, t1) * kd, -P.max_depen), P.max_depen);
+                        S.ae[k][1] = fminf(fmaxf(-vdot(dr, t2) * kd, -P.max_depen), P.max_depen);
+                        // the patch's other anchor, when it has a row
+                        const int pc = R.cnt == 2 ? (j == 0 ? (k + 1 < MAXCT ? 1 : 0) : 2) : 0;
+                        S.amu[k] = mu;
+                        S.aab[k] = (pa & 0xFFFF) | (pb << 16);
+                        S.alast[k] = last | (pc << 8) | (pidx << 10);
+                    }
+                }
+            }
         }
         // joint-limit rows (PhysX solves limits as constraints): a DOF whose
         // predicted position q + h u lies within 5% of its range of a limit gets
