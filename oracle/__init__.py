@@ -143,6 +143,20 @@ def collide(a, b, margin, hull_a=None, hull_b=None):
     return out[:n]
 
 
+def obb_apart(a, b, margin, hull_a=None, hull_b=None):
+    """The coupled step's OBB pair screen (oracle_obb_apart = mg_env.hip
+    obb_apart) on two shapes in collide()'s format: True when it rejects them."""
+    L = lib()
+    vp = ctypes.c_void_p
+    L.oracle_obb_apart.restype = ctypes.c_int
+    L.oracle_obb_apart.argtypes = [vp, vp, vp, vp, ctypes.c_float]
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    ha = None if hull_a is None else np.ascontiguousarray(hull_a, dtype=np.float32)
+    hb = None if hull_b is None else np.ascontiguousarray(hull_b, dtype=np.float32)
+    return bool(L.oracle_obb_apart(a.ctypes.data, _ptr(ha), b.ctypes.data, _ptr(hb), float(margin)))
+
+
 def render(sim_params, state, body_tmpl, tbi, shapes, env_body_first, color, seg, cam, hulls=None):
     """One camera on the host (oracle_render, migym_oracle_render.c): returns
     (rgba (H, W, 4) uint8, depth (H, W) f32, seg (H, W) int32). state is the

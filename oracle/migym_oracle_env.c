@@ -520,16 +520,14 @@ static void shape_obb_(const float* sh, const float* hulls, float* o) {
 }
 /* mg_env.hip obb_apart: the two shape-frame boxes separated along one of their
  * six face axes by more than the contact offset plus a rounding slack */
-static int obb_apart_(const float* sha, v3_t xa, q4_t qa, const float* shb, v3_t xb, q4_t qb, const float* hulls,
-                      float off) {
-    float oa[6], ob[6], C[3][3], slack, rb, ra;
+static int obb_apart_boxes_(const float* sha, v3_t xa, q4_t qa, const float* oa, const float* shb, v3_t xb, q4_t qb,
+                            const float* ob, float off) {
+    float C[3][3], slack, rb, ra;
     const m3_t Ra = qmat_(qmul_(qa, Q(sha[7], sha[8], sha[9], sha[10])));
     const m3_t Rb = qmat_(qmul_(qb, Q(shb[7], shb[8], shb[9], shb[10])));
     v3_t ca, cb, d, A3[3], B3[3];
     float eA[3], eB[3];
     int i, j, apart = 0;
-    shape_obb_(sha, hulls, oa);
-    shape_obb_(shb, hulls, ob);
     ca = add3(add3(xa, qrot_(qa, V(sha[4], sha[5], sha[6]))), mv_(Ra, V(oa[0], oa[1], oa[2])));
     cb = add3(add3(xb, qrot_(qb, V(shb[4], shb[5], shb[6]))), mv_(Rb, V(ob[0], ob[1], ob[2])));
     for (i = 0; i < 3; ++i) { eA[i] = oa[3 + i]; eB[i] = ob[3 + i]; }
@@ -549,6 +547,13 @@ static int obb_apart_(const float* sha, v3_t xa, q4_t qa, const float* shb, v3_t
         apart = apart || fabsf(dot3(d, B3[j])) > eB[j] + ra + slack;
     }
     return apart;
+}
+static int obb_apart_(const float* sha, v3_t xa, q4_t qa, const float* shb, v3_t xb, q4_t qb, const float* hulls,
+                      float off) {
+    float oa[6], ob[6];
+    shape_obb_(sha, hulls, oa);
+    shape_obb_(shb, hulls, ob);
+    return obb_apart_boxes_(sha, xa, qa, oa, shb, xb, qb, ob, off);
 }
 static int cvx_pair_(int ta, int tb) {
     const int pa = ta == MG_SHAPE_BOX || ta == MG_SHAPE_CONVEX, pb = tb == MG_SHAPE_BOX || tb == MG_SHAPE_CONVEX;
@@ -1712,6 +1717,20 @@ static int classify_envs_(const mg_model* m, oenv_t* envs, char* owned) {
     free(start);
     free(list);
     return n;
+}
+
+/* The OBB pair screen as a test entry point (shapes as oracle_collide2's, hull
+ * records ha / hb): 1 when mg_env.hip's obb_apart rejects the pair. */
+int oracle_obb_apart(const float* a, const float* ha, const float* b, const float* hb, float off) {
+    float sa[MG_SHAPE_STRIDE] = {0}, sb[MG_SHAPE_STRIDE] = {0}, oa[6], ob[6];
+    sa[0] = a[0]; sa[1] = a[8]; sa[2] = 0.0f; sa[3] = a[10]; sa[10] = 1.0f;
+    sb[0] = b[0]; sb[1] = b[8]; sb[2] = 0.0f; sb[3] = b[10]; sb[10] = 1.0f;
+    if ((int)a[0] == MG_SHAPE_BOX) sa[2] = a[9];
+    if ((int)b[0] == MG_SHAPE_BOX) sb[2] = b[9];
+    shape_obb_(sa, ha, oa);
+    shape_obb_(sb, hb, ob);
+    return obb_apart_boxes_(sa, V(a[1], a[2], a[3]), Q(a[4], a[5], a[6], a[7]), oa,
+                            sb, V(b[1], b[2], b[3]), Q(b[4], b[5], b[6], b[7]), ob, off);
 }
 
 /* Narrow phase as a test entry point: shapes given as [type, c.xyz, q.xyzw,

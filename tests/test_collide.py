@@ -316,3 +316,40 @@ def test_reference_franka_meshes_become_hulls():
     assert all(4 <= len(s.hull.verts) <= 32 and len(s.hull.planes) <= 64 for s in shapes)
     # mass from the hulls at density 1000 (no <inertial> in the URDF)
     assert a.mass_props[1].mass == __import__("pytest").approx(1000 * shapes[1].hull.volume, rel=1e-9)
+
+
+def test_obb_screen_never_drops_a_contact():
+    """The coupled step's OBB pair screen (mg_env.hip obb_apart, DESIGN.md §3.6
+    step 2) against the narrow phase it guards: over random poses of a random
+    hull against a box and against another hull, near contact, every pair the
+    screen rejects yields no contact from the full test (it only removes work),
+    and it does reject the pairs that are clearly apart along a face axis."""
+    from test_isaacgym_amd import _assets
+    rng = np.random.RandomState(7)
+    hull = _assets.make_hull(rng.normal(size=(60, 3)) * np.array([0.08, 0.02, 0.03]))
+    rec = hull.record()
+    rad = float(np.max(np.linalg.norm(hull.verts, axis=1)))
+    hb = (0.05, 0.05, 0.05)
+    rejected = kept_empty = 0
+    for k in range(3000):
+        qa = rng.normal(size=4)
+        qb = rng.normal(size=4)
+        qa /= np.linalg.norm(qa)
+        qb /= np.linalg.norm(qb)
+        d = rng.normal(size=3)
+        d *= rng.uniform(0.0, 0.25) / np.linalg.norm(d)
+        A = _shape(CONVEX, (0.0, 0.0, 0.0), tuple(qa), (rad, 0, 0))
+        if k % 2:
+            B = _shape(1, tuple(d), tuple(qb), hb)
+            out = oracle.collide(A, B, 0.01, hull_a=rec)
+            apart = oracle.obb_apart(A, B, 0.01, hull_a=rec)
+        else:
+            B = _shape(CONVEX, tuple(d), tuple(qb), (rad, 0, 0))
+            out = oracle.collide(A, B, 0.01, hull_a=rec, hull_b=rec)
+            apart = oracle.obb_apart(A, B, 0.01, hull_a=rec, hull_b=rec)
+        if apart:
+            rejected += 1
+            assert len(out) == 0, (k, out)
+        elif len(out) == 0:
+            kept_empty += 1
+    assert rejected > 500          # the screen removes a good share of the near-miss pairs
