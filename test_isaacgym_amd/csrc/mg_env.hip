@@ -2026,7 +2026,10 @@ __device__ __forceinline__ float red6_tree(const float* v) {
 // kernel spends ~40 % of its cycles waiting on the serial scan / inward /
 // outward steps of a 4-link chain.
 template <int NL>
-__global__ void __launch_bounds__(64, 1) k_artic_chain(MgStep P, MgArticArgs AA) {
+#ifndef MG_CHAIN_WAVES
+#define MG_CHAIN_WAVES 1
+#endif
+__global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, MgArticArgs AA) {
     constexpr int D = NL - 1;
     const int a = blockIdx.x * 64 + threadIdx.x;
     const bool live = a < AA.na;
