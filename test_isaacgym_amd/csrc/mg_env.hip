@@ -1700,23 +1700,27 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         __syncthreads();
         // contact impulse sums in contact order: link l on lane l, free body k on lane k
         // (normal impulses in contact order, then the anchors' friction impulses)
+        // (unrolled over the static bounds, so the LDS reads of all rows issue
+        // together instead of one dependent round trip per row)
         if (live && (ln < L || ln < nfr)) {
-            for (int c = 0; c < nct + nanc; ++c) {
-                const bool fr_ = c >= nct;
-                const int k = fr_ ? c - nct : c;
-                const int ab = fr_ ? S.aab[k] : 0;
-                const int a = fr_ ? (ab & 0xFFFF) : S.ca[k], b = fr_ ? (ab >> 16) : S.cb[k];
-                if (a >= LIM0) continue;
-                const bool on_link = ln < L && a == ln;
-                const bool on_fa = ln < nfr && a == F0 + ln;
-                const bool on_fb = ln < nfr && b == F0 + ln;
-                if (on_link || on_fa || on_fb) {
-                    V3 imp;
-                    if (fr_) imp = vmad(vscale(S.cd[k][1], S.clam[k][1]), S.cd[k][2], S.clam[k][2]);
-                    else imp = vscale(S.cd[k][0], S.clam[k][0]);
-                    if (on_link) lsum = vadd(lsum, imp);
-                    if (on_fa) fsum = vadd(fsum, imp);
-                    if (on_fb) fsum = vsub(fsum, imp);
+#pragma unroll
+            for (int c = 0; c < 2 * MAXCT; ++c) {
+                const bool fr_ = c >= MAXCT;
+                const int k = fr_ ? c - MAXCT : c;
+                if (fr_ ? k < nanc : k < nct) {
+                    const int ab = fr_ ? S.aab[k] : 0;
+                    const int a = fr_ ? (ab & 0xFFFF) : S.ca[k], b = fr_ ? (ab >> 16) : S.cb[k];
+                    const bool on_link = a < LIM0 && ln < L && a == ln;
+                    const bool on_fa = a < LIM0 && ln < nfr && a == F0 + ln;
+                    const bool on_fb = a < LIM0 && ln < nfr && b == F0 + ln;
+                    if (on_link || on_fa || on_fb) {
+                        V3 imp;
+                        if (fr_) imp = vmad(vscale(S.cd[k][1], S.clam[k][1]), S.cd[k][2], S.clam[k][2]);
+                        else imp = vscale(S.cd[k][0], S.clam[k][0]);
+                        if (on_link) lsum = vadd(lsum, imp);
+                        if (on_fa) fsum = vadd(fsum, imp);
+                        if (on_fb) fsum = vsub(fsum, imp);
+                    }
                 }
             }
         }
