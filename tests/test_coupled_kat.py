@@ -234,3 +234,28 @@ def test_friction_anchor_spacing(gym):
         if cnt == 2:
             assert np.linalg.norm(r[4:7] - r[10:13]) > corr
         assert abs(st[1, 2] - 0.41) < 1e-4 and np.linalg.norm(st[1, 0:2] - [0.45, 0.1]) < 1e-4
+
+
+def test_friction_anchor_teleport_reanchors(gym):
+    """a caller that teleports a body needs no reset of the
+    friction patches — an anchor whose two copies end up farther apart than the
+    correlation distance is dropped. A resting tile moved 5 cm sideways in the
+    state (set_actor_root_state's effect) keeps its new place: its patch is
+    re-anchored there instead of pulling it back towards the old anchors."""
+    sim, A, p, m = _cube_on_table(gym)
+    st = A["body_state0"].copy()
+    dof = A["dof_state0"].copy()
+    fc = oracle.contact_cache(m)
+    for _ in range(30):
+        oracle.step(p, m, st, dof, contact_cache=fc)
+    _, _, before = _patch(fc)
+    before = before.copy()
+    st[1, 0] += 0.05
+    x1 = float(st[1, 0])
+    for _ in range(30):
+        oracle.step(p, m, st, dof, contact_cache=fc)
+    cnt, held, after = _patch(fc)
+    assert cnt == 2 and held
+    assert not np.allclose(after[7:10], before[7:10])     # B-side (table) copies moved with the tile
+    assert abs(float(st[1, 0]) - x1) < 1e-4                # not pulled back 5 cm
+    assert np.linalg.norm(st[1, 7:10]) < 5e-3
