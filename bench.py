@@ -579,14 +579,15 @@ def large_n_rate(n, steps, dev, use_graph=True):
         gym.refresh_dof_state_tensor(sim)
 
     gym.refresh_actor_root_state_tensor(sim)
-    for k in range(10):
+    warm = 30        # the clocks and caches settle before the kernel-timing segment
+    for k in range(warm):
         step(k)
     kms, kmin, used = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
-                                   lambda: [step(10 + k) for k in range(KERNEL_TIMED_LAUNCHES)])
+                                   lambda: [step(warm + k) for k in range(KERNEL_TIMED_LAUNCHES)])
     chunk = graph_chunk(steps, acts.shape[0])
     assert acts.shape[0] % chunk == 0
     graphs = None
-    base = -(-(10 + KERNEL_TIMED_LAUNCHES) // chunk) * chunk
+    base = -(-(warm + KERNEL_TIMED_LAUNCHES) // chunk) * chunk
     if use_graph:
         try:
             graphs = capture_chunks(step, acts.shape[0], chunk)
@@ -616,7 +617,7 @@ def large_n_rate(n, steps, dev, use_graph=True):
     gym.destroy_sim(sim)
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps, "steps": steps,
             "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graphs is not None else "eager",
-            "roofline": rigid_roofline(n, kms, kmin, used, "%d eager steps after a 10-step warm-up" % used),
+            "roofline": rigid_roofline(n, kms, kmin, used, "%d eager steps after a %d-step warm-up" % (used, warm)),
             "roofline_unfused": rigid_roofline(n, ukms, ukmin, uused,
                                                "%d eager steps with step fusion off (scatter launch, then the "
                                                "step kernel on the SoA state)" % uused, step_out=False)}
