@@ -327,17 +327,38 @@ float       mg_last_render_ms(mg_sim* sim);
  * it the caller guarantees every captured set is consumed by a simulate in the
  * same capture (e.g. set -> simulate -> refresh per captured step, as bench.py). */
 #define MG_FUSE_IN_CAPTURE  8
-/* MG_FUSE_STEP_OUT: with targets bound by mg_bind_refresh_targets, on a sim whose
- * bodies are all single-shape free bodies and actor roots (the servo scene),
- * mg_simulate's step kernel writes the new state into the bound root and
- * rigid-body tensors itself, and a refresh of either bound tensor is then served
- * without a launch while no set has changed the state (the refresh fused into
- * the step). The bound tensors thus hold the new state from the simulate on, not
- * from the refresh; the gymapi layer rebinds (forcing a gather) when a bound
- * tensor was written between the simulate and its refresh. */
+/* MG_FUSE_STEP_OUT: with targets bound by mg_bind_refresh_targets /
+ * mg_bind_dof_refresh_target, on a sim whose bodies are all stepped by kernels
+ * that write their own rows (mg_step_out_supported: single-shape free bodies —
+ * the servo scene — and fixed-base serial chains of 2..4 links that touch
+ * nothing — the S2 gimbal), mg_simulate's step kernels write the new state into
+ * the bound root, rigid-body and DOF-state tensors themselves, and a refresh of
+ * a bound tensor is then served without a launch while no set has changed the
+ * state (the refresh fused into the step). The bound tensors thus hold the new
+ * state from the simulate on, not from the refresh; the gymapi layer rebinds
+ * (forcing a gather) when a bound tensor was written between the simulate and
+ * its refresh. */
 #define MG_FUSE_STEP_OUT    16
 int32_t     mg_set_fusion(mg_sim* sim, int32_t flags);
+/* replaces gym.acquire_actor_root_state_tensor / acquire_rigid_body_state_tensor's
+ * persistent buffers as refresh targets (test10_servo_vecenv.py:372-374,394-395) */
 int32_t     mg_bind_refresh_targets(mg_sim* sim, float* root_dst, float* rigid_body_dst);
+/* the persistent DOF-state tensor of gym.acquire_dof_state_tensor
+ * (test12_add_joint.py.py:129; test13_camera_spherical_joint.py:266-269) as the
+ * target MG_FUSE_STEP_OUT writes; NULL unbinds */
+int32_t     mg_bind_dof_refresh_target(mg_sim* sim, float* dof_dst);
+/* 1 when every body of the uploaded model is stepped by a kernel that writes its
+ * own refresh rows (MG_FUSE_STEP_OUT applies), else 0 */
+int32_t     mg_step_out_supported(mg_sim* sim);
+/* 1 when the last mg_set_actor_root_state / mg_set_dof_*_target /
+ * mg_set_dof_actuation_force call deferred its read of the source to the next
+ * mg_simulate (MG_FUSE_ROOT_SET / MG_FUSE_DOF_TARGETS), 0 when it copied it
+ * during the call (Isaac Gym's copy-at-set) */
+int32_t     mg_last_set_deferred(mg_sim* sim);
+/* drop the deferred sets not yet read (the gymapi layer, when a deferred set's
+ * source was written before the simulate that would read it: it raises, and the
+ * set is not applied with data newer than the set call) */
+int32_t     mg_discard_pending_sets(mg_sim* sim);
 
 /* ---- introspection for tests and the bench ------------------------------- */
 /* Kernel timing is opt-in (default off): while on, every eager simulate() and

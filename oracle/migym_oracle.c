@@ -603,6 +603,285 @@ static int dof_ball_(const float* LF, const int* LI, int L, int d) {
 #include "migym_oracle_env.c"
 #include "migym_oracle_render.c"
 
+/* ---- serial chains: mg_chain.hip k_artic_chain, op for
+ * op — the joint-space form (composite inertias, recursive Newton-Euler bias,
+ * LDL^T of M + diag(armature + implicit drive)), explicit fmaf where the kernel
+ * has them. Templates: fixed base, 2..4 links, link l's parent l - 1 and DOF
+ * l - 1 (revolute or prismatic), one body per link (migym_capi.cpp g.chain). */
+typedef struct { float xx, yy, zz, xy, xz, yz; v3_t h; float m; } ri_t;
+typedef struct { float m; v3_t com; float ib[6]; } clink_t;
+
+static v3_t fcross_(v3_t a, v3_t b) {
+    return V(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+static sv_t ri_mul_(const ri_t* I, sv_t x) {
+    const v3_t t = fcross_(I->h, x.v), s = fcross_(I->h, x.w);
+    return SVc(V(fmaf(I->xx, x.w.x, fmaf(I->xy, x.w.y, fmaf(I->xz, x.w.z, t.x))),
+                 fmaf(I->xy, x.w.x, fmaf(I->yy, x.w.y, fmaf(I->yz, x.w.z, t.y))),
+                 fmaf(I->xz, x.w.x, fmaf(I->yz, x.w.y, fmaf(I->zz, x.w.z, t.z)))),
+               V(fmaf(I->m, x.v.x, -s.x), fmaf(I->m, x.v.y, -s.y), fmaf(I->m, x.v.z, -s.z)));
+}
+static ri_t ri_add_(const ri_t* a, const ri_t* b) {
+    ri_t r;
+    r.xx = a->xx + b->xx; r.yy = a->yy + b->yy; r.zz = a->zz + b->zz;
+    r.xy = a->xy + b->xy; r.xz = a->xz + b->xz; r.yz = a->yz + b->yz;
+    r.h = add3(a->h, b->h);
+    r.m = a->m + b->m;
+    return r;
+}
+static float sdot_(sv_t a, sv_t b) {
+    return fmaf(a.v.z, b.v.z, fmaf(a.v.y, b.v.y, fmaf(a.v.x, b.v.x, fmaf(a.w.z, b.w.z, fmaf(a.w.y, b.w.y, a.w.x * b.w.x)))));
+}
+static sv_t crm_f_(sv_t a, sv_t b) { return SVc(fcross_(a.w, b.w), add3(fcross_(a.w, b.v), fcross_(a.v, b.w))); }
+static sv_t crf_f_(sv_t a, sv_t f) { return SVc(add3(fcross_(a.w, f.w), fcross_(a.v, f.v)), fcross_(a.w, f.v)); }
+static clink_t chain_link_(const float* M) {
+    clink_t k;
+    const m3_t R = qmat_(Q(M[4], M[5], M[6], M[7]));
+    const v3_t u0 = mul3(R.c0, M[1] > 0.0f ? 1.0f / M[1] : 0.0f);
+    const v3_t u1 = mul3(R.c1, M[2] > 0.0f ? 1.0f / M[2] : 0.0f);
+    const v3_t u2 = mul3(R.c2, M[3] > 0.0f ? 1.0f / M[3] : 0.0f);
+    k.m = M[11];
+    k.com = V(M[8], M[9], M[10]);
+    k.ib[0] = fmaf(u0.x, R.c0.x, fmaf(u1.x, R.c1.x, u2.x * R.c2.x));
+    k.ib[1] = fmaf(u0.y, R.c0.y, fmaf(u1.y, R.c1.y, u2.y * R.c2.y));
+    k.ib[2] = fmaf(u0.z, R.c0.z, fmaf(u1.z, R.c1.z, u2.z * R.c2.z));
+    k.ib[3] = fmaf(u0.x, R.c0.y, fmaf(u1.x, R.c1.y, u2.x * R.c2.y));
+    k.ib[4] = fmaf(u0.x, R.c0.z, fmaf(u1.x, R.c1.z, u2.x * R.c2.z));
+    k.ib[5] = fmaf(u0.y, R.c0.z, fmaf(u1.y, R.c1.z, u2.y * R.c2.z));
+    return k;
+}
+static ri_t world_ri_(const clink_t* K, q4_t ql, v3_t xl, v3_t x0, v3_t* cout) {
+    const m3_t R = qmat_(ql);
+    const float* b = K->ib;
+    const float ib[3][3] = {{b[0], b[3], b[4]}, {b[3], b[1], b[5]}, {b[4], b[5], b[2]}};
+    const float r[3][3] = {{R.c0.x, R.c1.x, R.c2.x}, {R.c0.y, R.c1.y, R.c2.y}, {R.c0.z, R.c1.z, R.c2.z}};
+    float t[3][3];
+    int i, j;
+    v3_t c, h;
+    ri_t I;
+    for (i = 0; i < 3; ++i)
+        for (j = 0; j < 3; ++j) t[i][j] = fmaf(r[i][2], ib[2][j], fmaf(r[i][1], ib[1][j], r[i][0] * ib[0][j]));
+#define OR_IC(i, j) fmaf(t[i][2], r[j][2], fmaf(t[i][1], r[j][1], t[i][0] * r[j][0]))
+    c = sub3(add3(xl, qrot_(ql, K->com)), x0);
+    h = mul3(c, K->m);
+    I.xx = fmaf(h.y, c.y, fmaf(h.z, c.z, OR_IC(0, 0)));
+    I.yy = fmaf(h.x, c.x, fmaf(h.z, c.z, OR_IC(1, 1)));
+    I.zz = fmaf(h.x, c.x, fmaf(h.y, c.y, OR_IC(2, 2)));
+    I.xy = fmaf(-h.x, c.y, OR_IC(0, 1));
+    I.xz = fmaf(-h.x, c.z, OR_IC(0, 2));
+    I.yz = fmaf(-h.y, c.z, OR_IC(1, 2));
+#undef OR_IC
+    I.h = h;
+    I.m = K->m;
+    *cout = c;
+    return I;
+}
+static void chain_fk_(const float* lf, int jt, float qj, q4_t qp, v3_t xp, q4_t* ql, v3_t* xl) {
+    const v3_t po = V(lf[0], lf[1], lf[2]), ax = V(lf[7], lf[8], lf[9]);
+    const q4_t qo = Q(lf[3], lf[4], lf[5], lf[6]);
+    q4_t qrel = qo;
+    v3_t rr = po;
+    if (jt == MG_JOINT_REVOLUTE) qrel = qmul_(qo, qaxang_(ax, qj));
+    else if (jt == MG_JOINT_PRISMATIC) rr = add3(po, qrot_(qo, mul3(ax, qj)));
+    *ql = qnorm_(qmul_(qp, qrel));
+    *xl = add3(xp, qrot_(qp, rr));
+}
+static sv_t chain_axis_(const float* lf, int jt, q4_t ql, v3_t xl, v3_t x0) {
+    const v3_t z = qrot_(ql, V(lf[7], lf[8], lf[9]));
+    return jt == MG_JOINT_REVOLUTE ? SVc(z, fcross_(sub3(xl, x0), z)) : SVc(V(0.0f, 0.0f, 0.0f), z);
+}
+static void chain_drive_(const float* pr, const float* tg, float q, float u, float h, int xm, int xp,
+                         float* tau0, float* imp) {
+    const int mode = (int)pr[0];
+    const float kp = pr[1], kd = pr[2], eff = pr[3];
+    float tau = 0.0f, im = 0.0f;
+    if (mode == MG_DOF_MODE_POS) {
+        tau = kp * (tg[0] - q - h * u) + kd * (tg[1] - u);
+        im = h * kd + h * h * kp;
+    } else if (mode == MG_DOF_MODE_VEL) {
+        tau = kd * (tg[1] - u);
+        im = h * kd;
+    } else if (mode == MG_DOF_MODE_EFFORT) {
+        tau = tg[2];
+    }
+    if (eff > 0.0f) {
+        if (xm) {
+            tau = xp ? eff : -eff;
+            im = 0.0f;
+        } else if (im == 0.0f) {
+            tau = fminf(fmaxf(tau, -eff), eff);
+        }
+    }
+    *tau0 = tau;
+    *imp = im;
+}
+/* (M + diag(arm + imp)) x = b, LDL^T, M by its upper triangle */
+static void chain_solve_(int D, float M[3][3], const float* arm, const float* imp, const float* b, float* x) {
+    float L[3][3], Ld[3][3], r[3], y[3];
+    int i, j, k;
+    for (j = 0; j < D; ++j) {
+        float dj = M[j][j] + (arm[j] + imp[j]);
+        for (k = 0; k < j; ++k) dj = fmaf(-L[j][k], Ld[j][k], dj);
+        r[j] = 1.0f / dj;
+        for (i = j + 1; i < D; ++i) {
+            float sm = M[j][i];
+            for (k = 0; k < j; ++k) sm = fmaf(-L[i][k], Ld[j][k], sm);
+            Ld[i][j] = sm;
+            L[i][j] = sm * r[j];
+        }
+    }
+    for (i = 0; i < D; ++i) {
+        float t = b[i];
+        for (k = 0; k < i; ++k) t = fmaf(-L[i][k], y[k], t);
+        y[i] = t;
+    }
+    for (i = D - 1; i >= 0; --i) {
+        float t = y[i] * r[i];
+        for (k = i + 1; k < D; ++k) t = fmaf(-L[k][i], x[k], t);
+        x[i] = t;
+    }
+}
+/* 1 when the template steps in k_artic_chain (migym_capi.cpp g.chain, 2..4 links) */
+static int is_chain_(const int* LI, int L, int D, int fixed_base) {
+    int l;
+    if (!fixed_base || L < 2 || L > 4 || D != L - 1 || LI[0] != -1 || LI[3] != 0) return 0;
+    for (l = 1; l < L; ++l) {
+        const int* li = LI + l * MG_LINK_I_N;
+        if (li[0] != l - 1 || li[2] != l - 1 || li[3] != l) return 0;
+        if (li[1] != MG_JOINT_REVOLUTE && li[1] != MG_JOINT_PRISMATIC) return 0;
+    }
+    return 1;
+}
+static void chain_step_(const step_t* P, const mg_model* m, const float* LF, const int* LI, int L, int b0, int d0,
+                        float* state, float* dof, const float* tgt, const float* props, const float* ext) {
+    const int D = L - 1;
+    const float h = P->h;
+    const float* s0 = state + (size_t)b0 * MG_STATE_N;
+    const v3_t x0 = V(s0[0], s0[1], s0[2]);
+    const q4_t q0 = qnorm_(Q(s0[3], s0[4], s0[5], s0[6]));
+    const float grav_on = m->tmpl_body_f[(size_t)m->body_tmpl[b0] * MG_TBODY_F_N + 4];
+    const v3_t gw = grav_on != 0.0f ? V(P->g[0], P->g[1], P->g[2]) : V(0.0f, 0.0f, 0.0f);
+    float qv[3], uv[3], arm[3];
+    clink_t lk[4];
+    int l, d, st_, j, i;
+    for (d = 0; d < D; ++d) {
+        qv[d] = dof[(d0 + d) * 2 + 0];
+        uv[d] = dof[(d0 + d) * 2 + 1];
+        arm[d] = props[(size_t)(d0 + d) * MG_DOFPROP_N + 8];
+    }
+    for (l = 1; l < L; ++l) lk[l] = chain_link_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N);
+    for (st_ = 0; st_ < P->substeps; ++st_) {
+        sv_t xi[3];
+        ri_t Il[3];
+        float Cb[3], M[3][3], qdd[3], tau0[3], imp[3], rhs[3];
+        int xm[3], xpl[3], flip = 0;
+        {
+            q4_t qp = q0;
+            v3_t xp = x0;
+            sv_t vp = sv0(), ap = SVc(V(0.0f, 0.0f, 0.0f), V(-gw.x, -gw.y, -gw.z));
+            for (l = 1; l < L; ++l) {
+                const float* lf = LF + l * MG_LINK_F_N;
+                const int jt = LI[l * MG_LINK_I_N + 1];
+                q4_t ql;
+                v3_t xl, c;
+                sv_t x, vJ, v, acc, f;
+                ri_t I;
+                chain_fk_(lf, jt, qv[l - 1], qp, xp, &ql, &xl);
+                x = chain_axis_(lf, jt, ql, xl, x0);
+                vJ = svmul_(x, uv[l - 1]);
+                v = svadd_(vp, vJ);
+                acc = svadd_(ap, crm_f_(v, vJ));
+                I = world_ri_(&lk[l], ql, xl, x0, &c);
+                {
+                    const sv_t Iv = ri_mul_(&I, v);
+                    f = svadd_(ri_mul_(&I, acc), crf_f_(v, Iv));
+                }
+                if (ext) {
+                    const float* e = ext + (size_t)(b0 + l) * 6;
+                    const v3_t fe = V(e[0], e[1], e[2]), te = V(e[3], e[4], e[5]);
+                    f = SVc(sub3(f.w, add3(te, cross3(c, fe))), sub3(f.v, fe));
+                }
+                xi[l - 1] = x;
+                Il[l - 1] = I;
+                for (j = 0; j < l; ++j) Cb[j] = j == l - 1 ? sdot_(x, f) : Cb[j] + sdot_(xi[j], f);
+                qp = ql; xp = xl; vp = v; ap = acc;
+            }
+        }
+        {
+            ri_t IC = Il[D - 1];
+            for (j = D - 1; j >= 0; --j) {
+                sv_t Fm;
+                if (j < D - 1) IC = ri_add_(&Il[j], &IC);
+                Fm = ri_mul_(&IC, xi[j]);
+                for (i = 0; i <= j; ++i) M[i][j] = sdot_(xi[i], Fm);
+            }
+        }
+        for (d = 0; d < D; ++d) {
+            const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
+            xm[d] = 0; xpl[d] = 0;
+            chain_drive_(pr, tgt + (size_t)(d0 + d) * 3, qv[d], uv[d], h, 0, 0, &tau0[d], &imp[d]);
+            rhs[d] = tau0[d] - Cb[d];
+        }
+        chain_solve_(D, M, arm, imp, rhs, qdd);
+        for (d = 0; d < D; ++d) {
+            const float eff = props[(size_t)(d0 + d) * MG_DOFPROP_N + 3];
+            if (eff > 0.0f && imp[d] != 0.0f) {
+                const float actf = tau0[d] - imp[d] * qdd[d];
+                if (actf > eff) { xm[d] = 1; xpl[d] = 1; flip = 1; }
+                else if (actf < -eff) { xm[d] = 1; flip = 1; }
+            }
+        }
+        if (flip) {
+            for (d = 0; d < D; ++d) {
+                chain_drive_(props + (size_t)(d0 + d) * MG_DOFPROP_N, tgt + (size_t)(d0 + d) * 3, qv[d], uv[d], h,
+                             xm[d], xpl[d], &tau0[d], &imp[d]);
+                rhs[d] = tau0[d] - Cb[d];
+            }
+            chain_solve_(D, M, arm, imp, rhs, qdd);
+        }
+        for (d = 0; d < D; ++d) {
+            const float* pr = props + (size_t)(d0 + d) * MG_DOFPROP_N;
+            const float maxv = pr[4];
+            float wv = uv[d] + h * qdd[d], xv;
+            if (maxv > 0.0f) wv = fminf(fmaxf(wv, -maxv), maxv);
+            xv = qv[d] + h * wv;
+            if (pr[7] != 0.0f) {
+                if (xv < pr[5]) { xv = pr[5]; if (wv < 0.0f) wv = 0.0f; }
+                if (xv > pr[6]) { xv = pr[6]; if (wv > 0.0f) wv = 0.0f; }
+            }
+            qv[d] = xv;
+            uv[d] = wv;
+        }
+    }
+    for (d = 0; d < D; ++d) { dof[(d0 + d) * 2 + 0] = qv[d]; dof[(d0 + d) * 2 + 1] = uv[d]; }
+    {
+        q4_t qp = q0;
+        v3_t xp = x0;
+        sv_t vp = sv0();
+        for (l = 0; l < L; ++l) {
+            float* so = state + (size_t)(b0 + l) * MG_STATE_N;
+            q4_t ql = q0;
+            v3_t xl = x0, ww = V(0.0f, 0.0f, 0.0f), vw = V(0.0f, 0.0f, 0.0f);
+            if (l > 0) {
+                const float* lf = LF + l * MG_LINK_F_N;
+                const int jt = LI[l * MG_LINK_I_N + 1];
+                sv_t v;
+                v3_t cw;
+                chain_fk_(lf, jt, qv[l - 1], qp, xp, &ql, &xl);
+                v = svadd_(vp, svmul_(chain_axis_(lf, jt, ql, xl, x0), uv[l - 1]));
+                cw = add3(sub3(xl, x0), qrot_(ql, lk[l].com));
+                ww = v.w;
+                vw = add3(v.v, fcross_(v.w, cw));
+                qp = ql; xp = xl; vp = v;
+            }
+            so[0] = xl.x; so[1] = xl.y; so[2] = xl.z;
+            so[3] = ql.x; so[4] = ql.y; so[5] = ql.z; so[6] = ql.w;
+            so[7] = vw.x; so[8] = vw.y; so[9] = vw.z;
+            so[10] = ww.x; so[11] = ww.y; so[12] = ww.z;
+        }
+    }
+}
+
 /* ---- articulation: the world-frame articulated-body
  * algorithm (aba_world_, with the implicit drives and the effort-limit
  * re-solve), then the joint integration of an articulation without contacts
@@ -627,6 +906,10 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
     const v3_t gw = grav_on != 0.0f ? V(P->g[0], P->g[1], P->g[2]) : V(0.0f, 0.0f, 0.0f);
     int d, l, st_;
     if (!fixed_base || L > OR_MAXL) return -1;
+    if (is_chain_(LI, L, D, fixed_base)) {   /* mg_chain.hip k_artic_chain */
+        chain_step_(P, m, LF, LI, L, b0, d0, state, dof, tgt, props, ext);
+        return 0;
+    }
     for (d = 0; d < D; ++d) { q[d] = dof[(d0 + d) * 2 + 0]; qd[d] = dof[(d0 + d) * 2 + 1]; qdd[d] = 0.0f; }
     for (st_ = 0; st_ < P->substeps; ++st_) {
         float tau0d[OR_MAXL], impd[OR_MAXL], mdiag[OR_MAXL];

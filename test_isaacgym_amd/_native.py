@@ -131,6 +131,10 @@ def _load():
         "mg_set_kernel_timing": (i32, [vp, i32]),
         "mg_set_fusion": (i32, [vp, i32]),
         "mg_bind_refresh_targets": (i32, [vp, vp, vp]),
+        "mg_bind_dof_refresh_target": (i32, [vp, vp]),
+        "mg_step_out_supported": (i32, [vp]),
+        "mg_last_set_deferred": (i32, [vp]),
+        "mg_discard_pending_sets": (i32, [vp]),
         "mg_last_step_ms": (ctypes.c_float, [vp]),
         "mg_step_time_stats": (i32, [vp, i32, vp, vp, vp]),
         "mg_num_free_bodies": (i32, [vp]),
@@ -159,7 +163,8 @@ EXPORTED_SYMBOLS = (
     "mg_refresh_net_contact_force", "mg_set_actor_root_state", "mg_set_rigid_body_state",
     "mg_set_dof_state", "mg_set_dof_position_target", "mg_set_dof_velocity_target",
     "mg_set_dof_actuation_force", "mg_set_dof_props", "mg_apply_rigid_body_force",
-    "mg_refresh_jacobian", "mg_refresh_mass_matrix", "mg_set_kernel_timing", "mg_set_fusion", "mg_bind_refresh_targets", "mg_last_step_ms", "mg_step_time_stats", "mg_num_free_bodies",
+    "mg_refresh_jacobian", "mg_refresh_mass_matrix", "mg_set_kernel_timing", "mg_set_fusion", "mg_bind_refresh_targets",
+    "mg_bind_dof_refresh_target", "mg_step_out_supported", "mg_last_set_deferred", "mg_discard_pending_sets", "mg_last_step_ms", "mg_step_time_stats", "mg_num_free_bodies",
     "mg_num_articulations",
     "mg_num_coupled_envs", "mg_refresh_jacobian_mass_matrix",
     "mg_set_render_bodies", "mg_snapshot_render_state", "mg_render_cameras", "mg_last_render_ms",

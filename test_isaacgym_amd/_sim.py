@@ -150,6 +150,7 @@ class Sim:
         self.fusion = int(os.environ.get("MIGYM_STEP_FUSION", "0") or 0) & 31
         self.rb_paired_version = None   # rb tensor version after a fused root refresh filled it
         self.root_out_version = None    # root tensor version after a simulate wrote it (STEP_OUT)
+        self.dof_out_version = None     # DOF tensor version after a simulate wrote it (STEP_OUT)
         self.mm_cache = {}
         self._renderer = None
         self.cam_version = 0       # bumped by every camera change (render tables are rebuilt)
@@ -483,6 +484,9 @@ class Sim:
             if root.is_cuda and rb.is_cuda and root.numel() and rb.numel():
                 N.check(N.lib.mg_bind_refresh_targets(handle, root.data_ptr(), rb.data_ptr()),
                         "mg_bind_refresh_targets")
+            dof = self.tensors["dof"]
+            if dof.is_cuda and dof.numel():   # written by the step itself under STEP_FUSION_STEP_OUT
+                N.check(N.lib.mg_bind_dof_refresh_target(handle, dof.data_ptr()), "mg_bind_dof_refresh_target")
             N.lib.mg_set_fusion(handle, self.fusion)
             # actor DOF targets / props set before prepare
             self._push_dof_targets_all()

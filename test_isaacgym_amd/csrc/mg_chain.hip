@@ -1,0 +1,489 @@
+// mg_chain.hip — k_artic_chain: the S2 servo-arm step (SURVEY.md §8d S2,
+// test12_add_joint.py.py:69-98's dof_test_camera.urdf gimbal): fixed-base
+// serial chains of 1..3 moving links, link l driven by DOF l - 1 (revolute or
+// prismatic), not touching anything. One lane per articulation, everything in
+// registers; the per-template joint constants are wave-uniform (scalar loads).
+//
+// Per substep, all spatial quantities in the world frame
+// about the base origin x0, so no spatial transform appears anywhere:
+//   forward, l = 1..D: joint transform, pose (ql, xl), motion axis xi_l,
+//     velocity v_l = v_{l-1} + xi_l u_l, velocity-product acceleration
+//     c_l = v_l x xi_l u_l, bias acceleration a_l = a_{l-1} + c_l (a_0 = -g),
+//     the link's rigid inertia I_l in compact form (10 floats: A, h = m c, m)
+//     and its bias force f_l = I_l a_l + v_l x* I_l v_l - f_ext;
+//     and the bias C_j += xi_j . f_l for j <= l (recursive Newton-Euler at
+//     qdd = 0: C_j = xi_j . sum_{k >= j} f_k, in the order the f_k appear);
+//   backward, l = D..1: composite inertia IC_l = I_l + IC_{l+1} (a sum of rigid
+//     inertias is again compact), F = IC_l xi_l, M_il = xi_i . F (i <= l);
+//   (M + diag(armature + h kd + h^2 kp)) qdd = tau0 - C by LDL^T: the implicit
+//     PD drive of §3.3, exact for the linearised drive; a drive whose implicit
+//     torque tau0 - (h kd + h^2 kp) qdd exceeds its effort limit is re-solved as
+//     a constant torque at the limit — a new diagonal and right-hand side only,
+//     the kinematics, inertias and bias forces are not recomputed;
+//   semi-implicit Euler with the speed and limit clamps.
+// This is the joint-space form of the articulated-body recursion (same qdd up
+// to rounding). For a 3-link chain with implicit drives it does ~1/2 of the
+// articulated-body pass's arithmetic, and a re-solve (every step of the S2
+// bench: kp 50 against a 10 N m limit) costs ~60 operations instead of a
+// second inward / outward pass. Register footprint: three compact inertias,
+// axes and bias forces (21 floats per link) instead of 6x6 articulated
+// inertias.
+//
+// With the refresh fused into the step (MG_FUSE_STEP_OUT) the kernel also
+// writes the bound DOF-state rows, rigid-body rows and the base's actor-root
+// row (the rows refresh_*_state_tensor would gather), with 16-B stores where
+// the rows of an articulation are contiguous and aligned.
+// Restated op for op by oracle/migym_oracle.c chain_step_ (explicit fmaf where
+// the kernel uses it, -ffp-contract=off elsewhere): bit-identical results.
+#include "mg_internal.h"
+#include "mg_spatial.h"
+#include "mg_world.h"
+
+namespace {
+
+// compact rigid spatial inertia about x0 in world axes:
+// [A, [h]x; [h]x^T, m 1], A symmetric (xx, yy, zz, xy, xz, yz), h = m (c - x0)
+struct RI {
+    float xx, yy, zz, xy, xz, yz;
+    V3 h;
+    float m;
+};
+
+// element idx of field `f` of an SoA array of row stride `n`: unsigned 32-bit
+// lane offsets from a wave-uniform field base, so the compiler addresses
+// every field with one VGPR offset (saddr) instead of a 64-bit address per
+// field (52 of them in the output pass: 248 -> 202 VGPRs)
+template <class T>
+__device__ __forceinline__ T& fld(T* base, int f, int n, int idx) {
+    return (base + (size_t)f * (unsigned)n)[(unsigned)idx];
+}
+
+// a x b with one rounding per component
+__device__ __forceinline__ V3 fcross(V3 a, V3 b) {
+    return v3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+// I x = (A w + h x v, m v - h x w)
+__device__ __forceinline__ SV ri_mul(const RI& I, SV x) {
+    const V3 t = fcross(I.h, x.v);
+    const V3 s = fcross(I.h, x.w);
+    return sv(v3(fmaf(I.xx, x.w.x, fmaf(I.xy, x.w.y, fmaf(I.xz, x.w.z, t.x))),
+                 fmaf(I.xy, x.w.x, fmaf(I.yy, x.w.y, fmaf(I.yz, x.w.z, t.y))),
+                 fmaf(I.xz, x.w.x, fmaf(I.yz, x.w.y, fmaf(I.zz, x.w.z, t.z)))),
+              v3(fmaf(I.m, x.v.x, -s.x), fmaf(I.m, x.v.y, -s.y), fmaf(I.m, x.v.z, -s.z)));
+}
+__device__ __forceinline__ RI ri_add(const RI& a, const RI& b) {
+    RI r;
+    r.xx = a.xx + b.xx; r.yy = a.yy + b.yy; r.zz = a.zz + b.zz;
+    r.xy = a.xy + b.xy; r.xz = a.xz + b.xz; r.yz = a.yz + b.yz;
+    r.h = vadd(a.h, b.h);
+    r.m = a.m + b.m;
+    return r;
+}
+__device__ __forceinline__ float sdot(SV a, SV b) {
+    return fmaf(a.v.z, b.v.z, fmaf(a.v.y, b.v.y, fmaf(a.v.x, b.v.x, fmaf(a.w.z, b.w.z, fmaf(a.w.y, b.w.y, a.w.x * b.w.x)))));
+}
+// motion x motion, motion x force
+__device__ __forceinline__ SV crm_f(SV a, SV b) { return sv(fcross(a.w, b.w), vadd(fcross(a.w, b.v), fcross(a.v, b.w))); }
+__device__ __forceinline__ SV crf_f(SV a, SV f) { return sv(vadd(fcross(a.w, f.w), fcross(a.v, f.v)), fcross(a.w, f.v)); }
+
+// a moving link's mass constants: mass, COM and the rotational inertia about
+// the COM in link axes (symmetric: xx, yy, zz, xy, xz, yz), built once per
+// launch from the principal moments and frame (MG_MASS_N row)
+struct ChainLink {
+    float m;
+    V3 com;
+    float ib[6];
+};
+__device__ __forceinline__ ChainLink load_chain_link(const float* Ms, int nb, int b) {
+    ChainLink k;
+    k.m = fld(Ms, 11, nb, b);
+    k.com = v3(fld(Ms, 8, nb, b), fld(Ms, 9, nb, b), fld(Ms, 10, nb, b));
+    const M3 R = qmat(q4(fld(Ms, 4, nb, b), fld(Ms, 5, nb, b), fld(Ms, 6, nb, b), fld(Ms, 7, nb, b)));
+    const float ix = fld(Ms, 1, nb, b), iy = fld(Ms, 2, nb, b), iz = fld(Ms, 3, nb, b);
+    const V3 u0 = vscale(R.c0, ix > 0.0f ? 1.0f / ix : 0.0f);
+    const V3 u1 = vscale(R.c1, iy > 0.0f ? 1.0f / iy : 0.0f);
+    const V3 u2 = vscale(R.c2, iz > 0.0f ? 1.0f / iz : 0.0f);
+    k.ib[0] = fmaf(u0.x, R.c0.x, fmaf(u1.x, R.c1.x, u2.x * R.c2.x));
+    k.ib[1] = fmaf(u0.y, R.c0.y, fmaf(u1.y, R.c1.y, u2.y * R.c2.y));
+    k.ib[2] = fmaf(u0.z, R.c0.z, fmaf(u1.z, R.c1.z, u2.z * R.c2.z));
+    k.ib[3] = fmaf(u0.x, R.c0.y, fmaf(u1.x, R.c1.y, u2.x * R.c2.y));
+    k.ib[4] = fmaf(u0.x, R.c0.z, fmaf(u1.x, R.c1.z, u2.x * R.c2.z));
+    k.ib[5] = fmaf(u0.y, R.c0.z, fmaf(u1.y, R.c1.z, u2.y * R.c2.z));
+    return k;
+}
+
+// the link's rigid inertia about x0 (world axes); c = its COM - x0
+__device__ __forceinline__ RI world_ri(const ChainLink& K, Q4 ql, V3 xl, V3 x0, V3& c) {
+    const M3 R = qmat(ql);
+    // T = R Ib (rows of R: (c0.i, c1.i, c2.i)), Ic = T R^T
+    const float* b = K.ib;   // xx yy zz xy xz yz
+    const float ib[3][3] = {{b[0], b[3], b[4]}, {b[3], b[1], b[5]}, {b[4], b[5], b[2]}};
+    const float r[3][3] = {{R.c0.x, R.c1.x, R.c2.x}, {R.c0.y, R.c1.y, R.c2.y}, {R.c0.z, R.c1.z, R.c2.z}};
+    float t[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) t[i][j] = fmaf(r[i][2], ib[2][j], fmaf(r[i][1], ib[1][j], r[i][0] * ib[0][j]));
+#define MG_IC(i, j) fmaf(t[i][2], r[j][2], fmaf(t[i][1], r[j][1], t[i][0] * r[j][0]))
+    c = vsub(vadd(xl, qrot(ql, K.com)), x0);
+    const V3 h = vscale(c, K.m);
+    RI I;
+    // R Ib R^T + m (|c|^2 1 - c c^T)
+    I.xx = fmaf(h.y, c.y, fmaf(h.z, c.z, MG_IC(0, 0)));
+    I.yy = fmaf(h.x, c.x, fmaf(h.z, c.z, MG_IC(1, 1)));
+    I.zz = fmaf(h.x, c.x, fmaf(h.y, c.y, MG_IC(2, 2)));
+    I.xy = fmaf(-h.x, c.y, MG_IC(0, 1));
+    I.xz = fmaf(-h.x, c.z, MG_IC(0, 2));
+    I.yz = fmaf(-h.y, c.z, MG_IC(1, 2));
+#undef MG_IC
+    I.h = h;
+    I.m = K.m;
+    return I;
+}
+
+// link l's pose from its parent's: joint rotation / offset at DOF position qj
+__device__ __forceinline__ void chain_fk(int jt, V3 po, Q4 qo, V3 ax, float qj, Q4 qp, V3 xp, Q4& ql, V3& xl) {
+    Q4 qrel = qo;
+    V3 rr = po;
+    if (jt == MG_JOINT_REVOLUTE) qrel = qmul(qo, q_axis_angle(ax, qj));
+    else if (jt == MG_JOINT_PRISMATIC) rr = vadd(po, qrot(qo, vscale(ax, qj)));
+    ql = qnormalize(qmul(qp, qrel));
+    xl = vadd(xp, qrot(qp, rr));
+}
+// joint l's motion axis about x0
+__device__ __forceinline__ SV chain_axis(int jt, V3 ax, Q4 ql, V3 xl, V3 x0) {
+    const V3 z = qrot(ql, ax);
+    return jt == MG_JOINT_REVOLUTE ? sv(z, fcross(vsub(xl, x0), z)) : sv(v3(0.0f, 0.0f, 0.0f), z);
+}
+
+struct ChainDof {
+    int mode, haslim;
+    float kp, kd, eff, maxv, lo, hi, arm, tpos, tvel, force;
+};
+
+// drive torque tau0 and implicit inertia imp of one DOF (xm:
+// effort-limited on the re-solve, xp: at +effort)
+__device__ __forceinline__ void chain_drive(const ChainDof& c, float q, float u, float h, bool xm, bool xp,
+                                            float& tau0, float& imp) {
+    float tau = 0.0f, im = 0.0f;
+    if (c.mode == MG_DOF_MODE_POS) {
+        tau = c.kp * (c.tpos - q - h * u) + c.kd * (c.tvel - u);
+        im = h * c.kd + h * h * c.kp;
+    } else if (c.mode == MG_DOF_MODE_VEL) {
+        tau = c.kd * (c.tvel - u);
+        im = h * c.kd;
+    } else if (c.mode == MG_DOF_MODE_EFFORT) {
+        tau = c.force;
+    }
+    if (c.eff > 0.0f) {
+        if (xm) {
+            tau = xp ? c.eff : -c.eff;
+            im = 0.0f;
+        } else if (im == 0.0f) {
+            tau = fminf(fmaxf(tau, -c.eff), c.eff);
+        }
+    }
+    tau0 = tau;
+    imp = im;
+}
+
+// (M + diag(arm + imp)) x = b by LDL^T; M given by its upper triangle M[i][j], i <= j
+template <int D>
+__device__ __forceinline__ void chain_solve(const float (&M)[D][D], const float* arm, const float* imp,
+                                            const float* b, float* x) {
+    float L[D][D], Ld[D][D], r[D], y[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        float dj = M[j][j] + (arm[j] + imp[j]);
+#pragma unroll
+        for (int k = 0; k < j; ++k) dj = fmaf(-L[j][k], Ld[j][k], dj);
+        r[j] = 1.0f / dj;
+#pragma unroll
+        for (int i = j + 1; i < D; ++i) {
+            float s = M[j][i];
+#pragma unroll
+            for (int k = 0; k < j; ++k) s = fmaf(-L[i][k], Ld[j][k], s);
+            Ld[i][j] = s;
+            L[i][j] = s * r[j];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        float t = b[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) t = fmaf(-L[i][k], y[k], t);
+        y[i] = t;
+    }
+#pragma unroll
+    for (int i = D - 1; i >= 0; --i) {
+        float t = y[i] * r[i];
+#pragma unroll
+        for (int k = i + 1; k < D; ++k) t = fmaf(-L[k][i], x[k], t);
+        x[i] = t;
+    }
+}
+
+// contiguous stores of n floats from registers; 16-B stores when dst is aligned
+template <int N>
+__device__ __forceinline__ void store_row(float* dst, const float (&v)[N]) {
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+#pragma unroll
+        for (int k = 0; k + 4 <= N; k += 4)
+            *reinterpret_cast<float4*>(dst + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+#pragma unroll
+        for (int k = N & ~3; k < N; ++k) dst[k] = v[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < N; ++k) dst[k] = v[k];
+    }
+}
+
+#ifndef MG_CHAIN_WAVES
+#define MG_CHAIN_WAVES 2
+#endif
+// EXT: external wrenches this step (apply_rigid_body_force_tensors)
+template <int NL, bool EXT>
+__global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, MgArticArgs AA) {
+    constexpr int D = NL - 1;
+    const int a = blockIdx.x * 64 + threadIdx.x;
+    const bool live = a < AA.na;
+    const int* ai = AA.artic_i + (size_t)(live ? a : 0) * MG_ARTIC_I_N;
+    const int b0 = ai[0], d0 = ai[1], ls = ai[3];   // link l: body b0 + l * ls (migym_capi.cpp)
+    const int nb = AA.nb, nd = AA.nd;
+    float* St = AA.state;
+    const float* pr = AA.dof_props;
+    const float h = P.h;
+
+    // template joint constants (wave-uniform)
+    V3 po[NL], ax[NL];
+    Q4 qo[NL];
+    int jt[NL];
+#pragma unroll
+    for (int l = 1; l < NL; ++l) {
+        const float* lf = AA.link_f + l * MG_LINK_F_N;
+        po[l] = v3(lf[0], lf[1], lf[2]);
+        qo[l] = q4(lf[3], lf[4], lf[5], lf[6]);
+        ax[l] = v3(lf[7], lf[8], lf[9]);
+        jt[l] = AA.link_i[l * MG_LINK_I_N + 1];
+    }
+    const V3 x0 = v3(fld(St, 0, nb, b0), fld(St, 1, nb, b0), fld(St, 2, nb, b0));
+    const Q4 q0 = qnormalize(q4(fld(St, 3, nb, b0), fld(St, 4, nb, b0), fld(St, 5, nb, b0), fld(St, 6, nb, b0)));
+    const V3 gw = AA.tbf[fld(AA.body_tmpl, 0, 0, b0) * MG_TBODY_F_N + 4] != 0.0f ? v3(P.g[0], P.g[1], P.g[2]) : v3(0.0f, 0.0f, 0.0f);
+    float qv[D], uv[D], arm[D];
+    ChainDof dc[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const int gd = d0 + d;
+        qv[d] = fld(AA.dof_pos, 0, 0, gd);
+        uv[d] = fld(AA.dof_vel, 0, 0, gd);
+        dc[d].mode = (int)fld(pr, 0, nd, gd);
+        dc[d].kp = fld(pr, 1, nd, gd);
+        dc[d].kd = fld(pr, 2, nd, gd);
+        dc[d].eff = fld(pr, 3, nd, gd);
+        dc[d].maxv = fld(pr, 4, nd, gd);
+        dc[d].lo = fld(pr, 5, nd, gd);
+        dc[d].hi = fld(pr, 6, nd, gd);
+        dc[d].haslim = fld(pr, 7, nd, gd) != 0.0f;
+        arm[d] = fld(pr, 8, nd, gd);
+        dc[d].tpos = fld(AA.dof_tpos, 0, 0, gd);
+        dc[d].tvel = fld(AA.dof_tvel, 0, 0, gd);
+        dc[d].force = fld(AA.dof_force, 0, 0, gd);
+        if (live) {   // fused target sets: write through (the only lane of this DOF)
+            if (AA.tpos_w) fld(AA.tpos_w, 0, 0, gd) = dc[d].tpos;
+            if (AA.tvel_w) fld(AA.tvel_w, 0, 0, gd) = dc[d].tvel;
+            if (AA.force_w) fld(AA.force_w, 0, 0, gd) = dc[d].force;
+        }
+    }
+    ChainLink lk[NL];
+#pragma unroll
+    for (int l = 1; l < NL; ++l) lk[l] = load_chain_link(AA.mass, nb, b0 + l * ls);
+
+    for (int st = 0; st < P.substeps; ++st) {
+        // ---- forward: poses, axes, velocities, inertias, bias forces
+        SV xi[D];
+        RI Il[D];
+        float Cb[D];   // bias C_j = xi_j . sum_{k >= j} f_k, accumulated as f_k appears
+        {
+            Q4 qp = q0;
+            V3 xp = x0;
+            SV vp = svzero();
+            SV ap = sv(v3(0.0f, 0.0f, 0.0f), v3(-gw.x, -gw.y, -gw.z));
+#pragma unroll
+            for (int l = 1; l < NL; ++l) {
+                Q4 ql;
+                V3 xl;
+                chain_fk(jt[l], po[l], qo[l], ax[l], qv[l - 1], qp, xp, ql, xl);
+                const SV x = chain_axis(jt[l], ax[l], ql, xl, x0);
+                const SV vJ = svscale(x, uv[l - 1]);
+                const SV v = svadd(vp, vJ);
+                const SV acc = svadd(ap, crm_f(v, vJ));
+                V3 c;
+                const RI I = world_ri(lk[l], ql, xl, x0, c);
+                SV f = svadd(ri_mul(I, acc), crf_f(v, ri_mul(I, v)));
+                if constexpr (EXT) {   // external wrench at the COM (apply_rigid_body_force_tensors)
+                    const int b = b0 + l * ls;
+                    const V3 fe = v3(fld(AA.ext, 0, nb, b), fld(AA.ext, 1, nb, b), fld(AA.ext, 2, nb, b));
+                    const V3 te = v3(fld(AA.ext, 3, nb, b), fld(AA.ext, 4, nb, b), fld(AA.ext, 5, nb, b));
+                    f = sv(vsub(f.w, vadd(te, vcross(c, fe))), vsub(f.v, fe));
+                }
+                xi[l - 1] = x;
+                Il[l - 1] = I;
+#pragma unroll
+                for (int j = 0; j < l; ++j) Cb[j] = j == l - 1 ? sdot(x, f) : Cb[j] + sdot(xi[j], f);
+                qp = ql;
+                xp = xl;
+                vp = v;
+                ap = acc;
+            }
+        }
+        // ---- backward: composite inertias -> joint-space inertia M, bias C
+        float M[D][D];
+        {
+            RI IC = Il[D - 1];
+#pragma unroll
+            for (int j = D - 1; j >= 0; --j) {
+                if (j < D - 1) IC = ri_add(Il[j], IC);
+                const SV Fm = ri_mul(IC, xi[j]);
+#pragma unroll
+                for (int i = 0; i <= j; ++i) M[i][j] = sdot(xi[i], Fm);
+            }
+        }
+        // ---- drives and the solve; one re-solve with effort-limited drives
+        float qdd[D], tau0[D], imp[D], rhs[D];
+        bool xm[D], xp[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            xm[d] = false;
+            xp[d] = false;
+            chain_drive(dc[d], qv[d], uv[d], h, false, false, tau0[d], imp[d]);
+            rhs[d] = tau0[d] - Cb[d];
+        }
+        chain_solve<D>(M, arm, imp, rhs, qdd);
+        bool flip = false;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            if (dc[d].eff > 0.0f && imp[d] != 0.0f) {
+                const float actf = tau0[d] - imp[d] * qdd[d];
+                if (actf > dc[d].eff) { xm[d] = true; xp[d] = true; flip = true; }
+                else if (actf < -dc[d].eff) { xm[d] = true; flip = true; }
+            }
+        }
+        if (__any(flip)) {   // lanes without a flip solve the same system again
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                chain_drive(dc[d], qv[d], uv[d], h, xm[d], xp[d], tau0[d], imp[d]);
+                rhs[d] = tau0[d] - Cb[d];
+            }
+            chain_solve<D>(M, arm, imp, rhs, qdd);
+        }
+        // ---- integrate the joints
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            float w = uv[d] + h * qdd[d];
+            if (dc[d].maxv > 0.0f) w = fminf(fmaxf(w, -dc[d].maxv), dc[d].maxv);
+            float x = qv[d] + h * w;
+            if (dc[d].haslim) {
+                if (x < dc[d].lo) { x = dc[d].lo; if (w < 0.0f) w = 0.0f; }
+                if (x > dc[d].hi) { x = dc[d].hi; if (w > 0.0f) w = 0.0f; }
+            }
+            qv[d] = x;
+            uv[d] = w;
+        }
+    }
+    if (!live) return;
+    // ---- outputs: DOF state; link states by forward kinematics at (q, qd)
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        fld(AA.dof_pos, 0, 0, d0 + d) = qv[d];
+        fld(AA.dof_vel, 0, 0, d0 + d) = uv[d];
+    }
+    if (AA.out_dof) {
+        float o[2 * D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) { o[2 * d] = qv[d]; o[2 * d + 1] = uv[d]; }
+        float* R = AA.out_dof + (size_t)d0 * 2;
+        if ((reinterpret_cast<uintptr_t>(R) & 7) == 0) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) *reinterpret_cast<float2*>(R + 2 * d) = make_float2(o[2 * d], o[2 * d + 1]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2 * D; ++k) R[k] = o[k];
+        }
+    }
+    float rows[NL * MG_STATE_N];
+    {
+        Q4 qp = q0;
+        V3 xp = x0;
+        SV vp = svzero();
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            Q4 ql = q0;
+            V3 xl = x0;
+            V3 ww = v3(0.0f, 0.0f, 0.0f), vw = v3(0.0f, 0.0f, 0.0f);
+            if (l > 0) {
+                chain_fk(jt[l], po[l], qo[l], ax[l], qv[l - 1], qp, xp, ql, xl);
+                const SV v = svadd(vp, svscale(chain_axis(jt[l], ax[l], ql, xl, x0), uv[l - 1]));
+                // COM velocity: v_O + w x (COM - x0)
+                const V3 cw = vadd(vsub(xl, x0), qrot(ql, lk[l].com));
+                ww = v.w;
+                vw = vadd(v.v, fcross(v.w, cw));
+                qp = ql;
+                xp = xl;
+                vp = v;
+            }
+            const int b = b0 + l * ls;
+            float* r = rows + l * MG_STATE_N;
+            r[0] = xl.x; r[1] = xl.y; r[2] = xl.z;
+            r[3] = ql.x; r[4] = ql.y; r[5] = ql.z; r[6] = ql.w;
+            r[7] = vw.x; r[8] = vw.y; r[9] = vw.z;
+            r[10] = ww.x; r[11] = ww.y; r[12] = ww.z;
+#pragma unroll
+            for (int k = 0; k < MG_STATE_N; ++k) fld(St, k, nb, b) = r[k];
+        }
+    }
+    // the refresh fused into the step: rigid-body rows (the articulation's
+    // bodies are consecutive rows of the tensor) and the base's actor-root row
+    if (AA.out_rb) {
+        const int g0 = fld(AA.out_body, 0, 0, b0);
+        bool contiguous = true;
+#pragma unroll
+        for (int l = 1; l < NL; ++l) contiguous = contiguous && fld(AA.out_body, 0, 0, b0 + l * ls) == g0 + l;
+        if (contiguous) {
+            store_row(AA.out_rb + (size_t)g0 * MG_STATE_N, rows);
+        } else {
+#pragma unroll
+            for (int l = 0; l < NL; ++l) {
+                float* R = AA.out_rb + (size_t)fld(AA.out_body, 0, 0, b0 + l * ls) * MG_STATE_N;
+#pragma unroll
+                for (int k = 0; k < MG_STATE_N; ++k) R[k] = rows[l * MG_STATE_N + k];
+            }
+        }
+    }
+    if (AA.out_root) {
+        const int rr = fld(AA.out_root_row, 0, 0, b0);
+        if (rr >= 0) {
+            float* R = AA.out_root + (size_t)rr * MG_STATE_N;
+#pragma unroll
+            for (int k = 0; k < MG_STATE_N; ++k) R[k] = rows[k];
+        }
+    }
+}
+
+}  // namespace
+
+// serial chains of 2..4 links (fixed base, link l driven by DOF l - 1)
+hipError_t mg_launch_artic_chain(const MgStep& P, const MgArticArgs& A, hipStream_t s) {
+    if (A.na <= 0) return hipSuccess;
+    if (!A.chain || A.nl < 2 || A.nl > 4) return hipErrorNotSupported;
+    const int cb = (A.na + 63) / 64;
+#define MG_KC(NL)                                                                        \
+    do {                                                                                 \
+        if (A.ext) MG_LAUNCH((k_artic_chain<NL, true>), dim3(cb), dim3(64), 0, s, P, A); \
+        else MG_LAUNCH((k_artic_chain<NL, false>), dim3(cb), dim3(64), 0, s, P, A);      \
+    } while (0)
+    if (A.nl == 2) MG_KC(2);
+    else if (A.nl == 3) MG_KC(3);
+    else MG_KC(4);
+#undef MG_KC
+    return hipGetLastError();
+}

@@ -2011,274 +2011,6 @@ __global__ void __launch_bounds__(64) k_artic_lanes(MgStep P, MgArticArgs AA) {
     }
 }
 
-// red16 of (v0..v5, 0, ..., 0) in the DPP tree's order (row_ror 8, row_ror 4,
-// quad perms; oracle red16_): the same adds, zeros included
-__device__ __forceinline__ float red6_tree(const float* v) {
-    const float z = 0.0f;
-    const float s0 = v[0] + z, s1 = v[1] + z, s2 = v[2] + z, s3 = v[3] + z, s4 = v[4] + z, s5 = v[5] + z;
-    const float s6 = z + z, s7 = z + z;
-    const float t0 = s0 + s4, t1 = s1 + s5, t2 = s2 + s6, t3 = s3 + s7;
-    return (t0 + t2) + (t1 + t3);
-}
-
-// Short serial chains (the S2 gimbal: a fixed base and NL - 1 <= 3 moving
-// links, link l driven by DOF l - 1): one lane per articulation, everything in
-// registers. The same world-frame articulated-body algorithm as k_artic_lanes
-// (aba_kin / aba_dyn / aba_refresh, and oracle aba_world_) expression by
-// expression — only the distribution over lanes differs, so the results are
-// bit-identical — without its LDS round trips and barriers: the lane-parallel
-// kernel spends ~40 % of its cycles waiting on the serial scan / inward /
-// outward steps of a 4-link chain.
-template <int NL>
-#ifndef MG_CHAIN_WAVES
-#define MG_CHAIN_WAVES 1
-#endif
-__global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, MgArticArgs AA) {
-    constexpr int D = NL - 1;
-    const int a = blockIdx.x * 64 + threadIdx.x;
-    const bool live = a < AA.na;
-    const int* ai = AA.artic_i + (size_t)(live ? a : 0) * MG_ARTIC_I_N;
-    const int b0 = ai[0], d0 = ai[1], ls = ai[3];   // link l: body b0 + l * ls (migym_capi.cpp)
-    const int nb = AA.nb, nd = AA.nd;
-    float* St = AA.state;
-    const float* pr = AA.dof_props;
-    const float h = P.h;
-
-    V3 po[NL], ax[NL];
-    Q4 qo[NL];
-    int jt[NL];
-#pragma unroll
-    for (int l = 1; l < NL; ++l) {
-        const float* lf = AA.link_f + l * MG_LINK_F_N;
-        po[l] = v3(lf[0], lf[1], lf[2]);
-        qo[l] = q4(lf[3], lf[4], lf[5], lf[6]);
-        ax[l] = v3(lf[7], lf[8], lf[9]);
-        jt[l] = AA.link_i[l * MG_LINK_I_N + 1];
-    }
-    const V3 x0 = v3(St[0 * nb + b0], St[1 * nb + b0], St[2 * nb + b0]);
-    const Q4 q0 = qnormalize(q4(St[3 * nb + b0], St[4 * nb + b0], St[5 * nb + b0], St[6 * nb + b0]));
-    const V3 gw = AA.tbf[AA.body_tmpl[b0] * MG_TBODY_F_N + 4] != 0.0f ? v3(P.g[0], P.g[1], P.g[2]) : v3(0.0f, 0.0f, 0.0f);
-    float qv[D], uv[D];
-    DofC dc[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        const int gd = d0 + d;
-        qv[d] = AA.dof_pos[gd];
-        uv[d] = AA.dof_vel[gd];
-        dc[d].mode = (int)pr[0 * nd + gd];
-        dc[d].kp = pr[1 * nd + gd];
-        dc[d].kd = pr[2 * nd + gd];
-        dc[d].eff = pr[3 * nd + gd];
-        dc[d].maxv = pr[4 * nd + gd];
-        dc[d].lo = pr[5 * nd + gd];
-        dc[d].hi = pr[6 * nd + gd];
-        dc[d].haslim = pr[7 * nd + gd] != 0.0f;
-        dc[d].arm = pr[8 * nd + gd];
-        dc[d].tpos = AA.dof_tpos[gd];
-        dc[d].tvel = AA.dof_tvel[gd];
-        dc[d].force = AA.dof_force[gd];
-        if (live) {   // fused target sets: write through (the only lane of this DOF)
-            if (AA.tpos_w) AA.tpos_w[gd] = dc[d].tpos;
-            if (AA.tvel_w) AA.tvel_w[gd] = dc[d].tvel;
-            if (AA.force_w) AA.force_w[gd] = dc[d].force;
-        }
-    }
-    LinkC lk[NL];
-#pragma unroll
-    for (int l = 0; l < NL; ++l) lk[l] = load_link(AA.mass, nb, b0 + l * ls);
-
-    for (int st = 0; st < P.substeps; ++st) {
-        // ---- kinematics (aba_kin): joint transforms, scan, axes, inertias
-        Q4 ql[NL];
-        V3 xl[NL];
-        float xi[NL][6], Iw[NL][36], va[NL][6], cc[NL][6], pa[NL][6];
-        ql[0] = q0;
-        xl[0] = x0;
-#pragma unroll
-        for (int l = 1; l < NL; ++l) {
-            const float qj = qv[l - 1];
-            Q4 qrel = qo[l];
-            V3 rr = po[l];
-            if (jt[l] == MG_JOINT_REVOLUTE) qrel = qmul(qo[l], q_axis_angle(ax[l], qj));
-            else if (jt[l] == MG_JOINT_PRISMATIC) rr = vadd(po[l], qrot(qo[l], vscale(ax[l], qj)));
-            ql[l] = qnormalize(qmul(ql[l - 1], qrel));
-            xl[l] = vadd(xl[l - 1], qrot(ql[l - 1], rr));
-            const V3 z = qrot(ql[l], ax[l]);
-            const SV x = jt[l] == MG_JOINT_REVOLUTE ? sv(z, vcross(vsub(xl[l], x0), z)) : sv(v3(0.0f, 0.0f, 0.0f), z);
-            put6(xi[l], x);
-        }
-        // velocities and velocity-product terms (aba_vel / aba_vp), and the
-        // world inertias: computed again by a re-solve (aba_refresh)
-        auto vel_vp = [&]() {
-#pragma unroll
-            for (int l = 1; l < NL; ++l) world_inertia(lk[l], ql[l], xl[l], x0, Iw[l]);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) va[0][i] = 0.0f;
-#pragma unroll
-            for (int l = 1; l < NL; ++l)
-#pragma unroll
-                for (int i = 0; i < 6; ++i) va[l][i] = va[l - 1][i] + xi[l][i] * uv[l - 1];
-#pragma unroll
-            for (int l = 1; l < NL; ++l) {
-                const SV v = sv6(va[l]);
-                const SV vJ = svscale(sv6(xi[l]), uv[l - 1]);
-                float Iv[6];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) Iv[i] = dot6(&Iw[l][i * 6], va[l]);
-                put6(cc[l], crm(v, vJ));
-                SV pb = crf(v, sv6(Iv));
-                if (AA.ext) {
-                    const int b = b0 + l * ls;
-                    const V3 f = v3(AA.ext[0 * nb + b], AA.ext[1 * nb + b], AA.ext[2 * nb + b]);
-                    const V3 t = v3(AA.ext[3 * nb + b], AA.ext[4 * nb + b], AA.ext[5 * nb + b]);
-                    const V3 c = vsub(vadd(xl[l], qrot(ql[l], lk[l].com)), x0);
-                    pb = sv(vsub(pb.w, vadd(t, vcross(c, f))), vsub(pb.v, f));
-                }
-                put6(pa[l], pb);
-            }
-        };
-        vel_vp();
-        bool xm[D], xp[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) { xm[d] = false; xp[d] = false; }
-        float qdd[D];
-        bool redo = live;
-        for (int att = 0; att < 2; ++att) {
-            if (!__any(redo)) break;
-            if (att > 0) vel_vp();
-            // ---- drive terms (aba_dyn)
-            float tau0[D], imp[D];
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                float tau = 0.0f, im = 0.0f;
-                if (dc[d].mode == MG_DOF_MODE_POS) {
-                    tau = dc[d].kp * (dc[d].tpos - qv[d] - h * uv[d]) + dc[d].kd * (dc[d].tvel - uv[d]);
-                    im = h * dc[d].kd + h * h * dc[d].kp;
-                } else if (dc[d].mode == MG_DOF_MODE_VEL) {
-                    tau = dc[d].kd * (dc[d].tvel - uv[d]);
-                    im = h * dc[d].kd;
-                } else if (dc[d].mode == MG_DOF_MODE_EFFORT) {
-                    tau = dc[d].force;
-                }
-                if (dc[d].eff > 0.0f) {
-                    if (xm[d]) {
-                        tau = xp[d] ? dc[d].eff : -dc[d].eff;
-                        im = 0.0f;
-                    } else if (im == 0.0f) {
-                        tau = fminf(fmaxf(tau, -dc[d].eff), dc[d].eff);
-                    }
-                }
-                tau0[d] = tau;
-                imp[d] = im;
-            }
-            // ---- inward pass
-            float Ua[NL][6], Dd[NL], uu[NL];
-#pragma unroll
-            for (int l = NL - 1; l >= 1; --l) {
-                const int d = l - 1;
-#pragma unroll
-                for (int i = 0; i < 6; ++i) Ua[l][i] = dot6(&Iw[l][i * 6], xi[l]);
-                const float Dv = dot6(xi[l], Ua[l]) + dc[d].arm + imp[d];
-                const float uvv = tau0[d] - dot6(xi[l], pa[l]);
-                const float invD = 1.0f / Dv;
-                const float uinvD = uvv * invD;
-#pragma unroll
-                for (int e = 0; e < 36; ++e) Iw[l][e] = Iw[l][e] - Ua[l][e / 6] * (Ua[l][e % 6] * invD);
-                Dd[l] = Dv;
-                uu[l] = uvv;
-                if (l - 1 > 0) {
-                    const int p = l - 1;
-#pragma unroll
-                    for (int i = 0; i < 6; ++i) {
-                        float pv = pa[l][i] + dot6(&Iw[l][i * 6], cc[l]);
-                        pv = pv + Ua[l][i] * uinvD;
-                        pa[p][i] = pa[p][i] + pv;
-                    }
-#pragma unroll
-                    for (int e = 0; e < 36; ++e) Iw[p][e] = Iw[p][e] + Iw[l][e];
-                }
-            }
-            // ---- outward pass (va now holds accelerations)
-            va[0][0] = 0.0f; va[0][1] = 0.0f; va[0][2] = 0.0f;
-            va[0][3] = -gw.x; va[0][4] = -gw.y; va[0][5] = -gw.z;
-#pragma unroll
-            for (int l = 1; l < NL; ++l) {
-                float a6[6], t6[6];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) a6[i] = va[l - 1][i] + cc[l][i];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) t6[i] = Ua[l][i] * a6[i];
-                const float acc = (uu[l] - red6_tree(t6)) / Dd[l];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) va[l][i] = a6[i] + xi[l][i] * acc;
-                qdd[l - 1] = acc;
-            }
-            // drives whose implicit force exceeds the effort limit
-            bool flip = false;
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                if (redo && dc[d].eff > 0.0f && imp[d] != 0.0f) {
-                    const float actf = tau0[d] - imp[d] * qdd[d];
-                    if (actf > dc[d].eff) { xm[d] = true; xp[d] = true; flip = true; }
-                    else if (actf < -dc[d].eff) { xm[d] = true; flip = true; }
-                }
-            }
-            redo = flip;
-        }
-        // ---- integrate the joints
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            float w = uv[d] + h * qdd[d];
-            if (dc[d].maxv > 0.0f) w = fminf(fmaxf(w, -dc[d].maxv), dc[d].maxv);
-            float x = qv[d] + h * w;
-            if (dc[d].haslim) {
-                if (x < dc[d].lo) { x = dc[d].lo; if (w < 0.0f) w = 0.0f; }
-                if (x > dc[d].hi) { x = dc[d].hi; if (w > 0.0f) w = 0.0f; }
-            }
-            qv[d] = x;
-            uv[d] = w;
-        }
-    }
-    if (!live) return;
-    // ---- outputs: DOF state; link states by forward kinematics at (q, qd)
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        AA.dof_pos[d0 + d] = qv[d];
-        AA.dof_vel[d0 + d] = uv[d];
-    }
-    Q4 ql = q0, qlp = q0;
-    V3 xlv = x0;
-    SV vl = svzero();
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-        if (l > 0) {
-            const float qj = qv[l - 1];
-            Q4 qrel = qo[l];
-            V3 rr = po[l];
-            SV sj = svzero();
-            if (jt[l] == MG_JOINT_REVOLUTE) {
-                qrel = qmul(qo[l], q_axis_angle(ax[l], qj));
-                sj = sv(ax[l], v3(0.0f, 0.0f, 0.0f));
-            } else if (jt[l] == MG_JOINT_PRISMATIC) {
-                rr = vadd(po[l], qrot(qo[l], vscale(ax[l], qj)));
-                sj = sv(v3(0.0f, 0.0f, 0.0f), ax[l]);
-            }
-            qlp = ql;
-            ql = qnormalize(qmul(qlp, qrel));
-            xlv = vadd(xlv, qrot(qlp, rr));
-            vl = svadd(x_motion(m3t(qmat(qrel)), rr, vl), svscale(sj, uv[l - 1]));
-        }
-        const int b = b0 + l * ls;
-        const V3 ww = qrot(ql, vl.w);
-        const V3 vw = qrot(ql, vadd(vl.v, vcross(vl.w, lk[l].com)));
-        St[0 * nb + b] = xlv.x; St[1 * nb + b] = xlv.y; St[2 * nb + b] = xlv.z;
-        St[3 * nb + b] = ql.x; St[4 * nb + b] = ql.y; St[5 * nb + b] = ql.z; St[6 * nb + b] = ql.w;
-        St[7 * nb + b] = vw.x; St[8 * nb + b] = vw.y; St[9 * nb + b] = vw.z;
-        St[10 * nb + b] = ww.x; St[11 * nb + b] = ww.y; St[12 * nb + b] = ww.z;
-        AA.cforce[0 * nb + b] = 0.0f; AA.cforce[1 * nb + b] = 0.0f; AA.cforce[2 * nb + b] = 0.0f;
-    }
-}
-
 }  // namespace
 
 // lanes per env / articulation: 16 (4 per wavefront) up to 16 links and 16
@@ -2289,13 +2021,8 @@ static bool mg_wide(int nl, int slots) { return nl > 16 || slots > 16; }
 hipError_t mg_launch_artic_lanes(const MgStep& P, const MgArticArgs& A, hipStream_t s) {
     if (A.na <= 0) return hipSuccess;
     if (!A.fixed_base || A.nl > MG_MAX_LINKS || A.ndof > MG_ENV_SLOTS_WIDE) return hipErrorNotSupported;
-    if (A.chain && A.nl >= 2 && A.nl <= 4) {   // serial chain, one DOF per moving link
-        const int cb = (A.na + 63) / 64;
-        if (A.nl == 2) MG_LAUNCH((k_artic_chain<2>), dim3(cb), dim3(64), 0, s, P, A);
-        else if (A.nl == 3) MG_LAUNCH((k_artic_chain<3>), dim3(cb), dim3(64), 0, s, P, A);
-        else MG_LAUNCH((k_artic_chain<4>), dim3(cb), dim3(64), 0, s, P, A);
-        return hipGetLastError();
-    }
+    if (A.chain && A.nl >= 2 && A.nl <= 4)   // serial chain, one DOF per moving link (mg_chain.hip)
+        return mg_launch_artic_chain(P, A, s);
     if (mg_wide(A.nl, A.ndof)) {
         MG_LAUNCH((k_artic_lanes<MG_MAX_LINKS, 64>), dim3(A.na), dim3(64), 0, s, P, A);
         return hipGetLastError();

@@ -101,6 +101,13 @@ struct MgArticArgs {
     const float* dof_props;   // [12][nd]
     const float* ext;         // [6][nb] or null
     float*       cforce;      // [3][nb]
+    // refresh fused into the step (MG_FUSE_STEP_OUT, k_artic_chain): the bound
+    // tensors the kernel writes itself, or null
+    float*       out_rb;      // [nb][13] rigid-body tensor (global body order)
+    float*       out_root;    // [na][13] actor root tensor
+    float*       out_dof;     // [nd][2] DOF state tensor
+    const int*   out_body;    // [nb] internal slot -> global body
+    const int*   out_root_row;// [nb] internal slot -> actor row (-1: not a root)
 };
 
 // Coupled per-env step (mg_env.hip): MG_ENV_G lanes per env, one lane per
@@ -241,6 +248,7 @@ hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s
 hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream_t s);
 hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream_t s);
 hipError_t mg_launch_artic_lanes(const MgStep& P, const MgArticArgs& A, hipStream_t s);
+hipError_t mg_launch_artic_chain(const MgStep& P, const MgArticArgs& A, hipStream_t s);
 hipError_t mg_launch_gather_rows(const float* soa, int stride, int ncol, const int* ids, int n,
                                  float* aos, hipStream_t s);
 hipError_t mg_launch_gather_rb_root(const float* soa, int stride, int ncol, const int* perm, int nb, float* rb,

@@ -834,23 +834,25 @@ k_rigid_step1(MgStep P, MgRigidArgs A) {
         A.cforce[1 * nb + bo] = fsum.y * P.inv_dt;
         A.cforce[2 * nb + bo] = fsum.z * P.inv_dt;
     }
-    if (A.out_rb && !WIDE) {
+    if ((A.out_rb || A.out_root) && !WIDE) {
         // the refresh fused into the step: the same 13 values into the bound
         // rigid-body row and, for a root body, its actor's root row (the rows the
         // paired gather k_gather_rb_root would write from the SoA state)
         if (live) {
             const float o[MG_STATE_N] = {x.x, x.y, x.z, q.x, q.y, q.z, q.w, v.x, v.y, v.z, w.x, w.y, w.z};
-            float* R = A.out_rb + (size_t)A.out_body[bo] * MG_STATE_N;
+            if (A.out_rb) {
+                float* R = A.out_rb + (size_t)A.out_body[bo] * MG_STATE_N;
 #pragma unroll
-            for (int k = 0; k < MG_STATE_N; ++k) R[k] = o[k];
-            const int rr = A.out_root_row[bo];
+                for (int k = 0; k < MG_STATE_N; ++k) R[k] = o[k];
+            }
+            const int rr = A.out_root ? A.out_root_row[bo] : -1;
             if (rr >= 0) {
                 float* Ro = A.out_root + (size_t)rr * MG_STATE_N;
 #pragma unroll
                 for (int k = 0; k < MG_STATE_N; ++k) Ro[k] = o[k];
             }
         }
-    } else if (A.out_rb) {   // launch-uniform
+    } else if (A.out_rb || A.out_root) {   // launch-uniform
         // Wide launches are issue-bound, and the rows are 52-B AoS records, every
         // other one per wave (the wave holds one template: UAVs or cars): written
         // lane by lane, each store instruction touches 64 rows 104 B apart. The
@@ -865,8 +867,8 @@ k_rigid_step1(MgStep P, MgRigidArgs A) {
         const float o[MG_STATE_N] = {x.x, x.y, x.z, q.x, q.y, q.z, q.w, v.x, v.y, v.z, w.x, w.y, w.z};
 #pragma unroll
         for (int k = 0; k < MG_STATE_N; ++k) s_out[l * 16 + k] = o[k];
-        s_dst[0][l] = live ? A.out_body[bo] : -1;
-        s_dst[1][l] = live ? A.out_root_row[bo] : -1;
+        s_dst[0][l] = live && A.out_rb ? A.out_body[bo] : -1;
+        s_dst[1][l] = live && A.out_root ? A.out_root_row[bo] : -1;
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < MG_STATE_N; ++k) {
@@ -923,6 +925,7 @@ hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream
     MgRigidArgs A1 = A, A2 = A;
     A2.root_src = nullptr;   // fused root sets only with single-shape bodies (migym_capi.cpp)
     A2.out_rb = nullptr;     // so is the fused refresh (MG_FUSE_STEP_OUT)
+    A2.out_root = nullptr;
     A1.nf = A.nf1;
     A2.nf = A.nf - A.nf1;
     if (A.free_ids) {

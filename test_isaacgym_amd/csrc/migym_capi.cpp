@@ -117,8 +117,21 @@ struct mg_sim {
     unsigned long long pend_root_cap = 0, pend_tgt_cap[3] = {0, 0, 0}, rb_cap = 0;
     float* bind_root = nullptr;
     float* bind_rb = nullptr;
+    float* bind_dof = nullptr;    // the persistent DOF-state tensor (mg_bind_dof_refresh_target)
     long long state_gen = 0, rb_gen = -1, out_gen = -1;   // out_gen: bound tensors written by the step
     unsigned long long out_cap = 0;
+    // DOF state generation (simulate, mg_set_dof_state) and the one the step
+    // wrote into the bound DOF tensor (MG_FUSE_STEP_OUT)
+    long long dof_sgen = 0, dof_gen = -1;
+    unsigned long long dof_cap = 0;
+    // MG_FUSE_STEP_OUT covers the sim: every body is stepped by a kernel that
+    // writes its rows (single-shape free bodies in k_rigid_step1, links of
+    // uncoupled serial chains in k_artic_chain), so the refreshes after a
+    // simulate can be served by the step itself
+    bool step_out_ok = false;
+    int* d_slot_global = nullptr; // [nb] internal slot -> global body (rigid-body tensor row)
+    int* d_slot_actor = nullptr;  // [nb] internal slot -> actor row it is the root of, or -1
+    int last_set_deferred = 0;    // the last mg_set_* left its source to be read by the next simulate
     int* d_actor_dof = nullptr;   // [na+1]
     float* d_cforce = nullptr;    // [3][nb]
     float* d_ext = nullptr;       // [6][nb]
@@ -351,7 +364,7 @@ void shape_obb(const float* sh, const float* hulls, float* o) {
 
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls, s->d_shape_obb,
-                    s->d_actor_root, s->d_root_row, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
+                    s->d_actor_root, s->d_root_row, s->d_slot_global, s->d_slot_actor, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
                     s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_fp_mask, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
                     s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
@@ -924,6 +937,24 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         HIP_TRY(dalloc(&s->d_root_row, (size_t)std::max(nb, 1)));
         HIP_TRY(h2d(s->d_root_row, row.data(), (size_t)nb * sizeof(int)));
     }
+    {
+        // rows the step kernels write with the refresh fused into them
+        // (MG_FUSE_STEP_OUT): internal slot -> rigid-body row / actor row
+        std::vector<int> slot_actor(nb, -1);
+        for (int a = 0; a < na; ++a) slot_actor[root_int[a]] = a;
+        HIP_TRY(dalloc(&s->d_slot_global, (size_t)std::max(nb, 1)));
+        HIP_TRY(h2d(s->d_slot_global, order.data(), (size_t)nb * sizeof(int)));
+        HIP_TRY(dalloc(&s->d_slot_actor, (size_t)std::max(nb, 1)));
+        HIP_TRY(h2d(s->d_slot_actor, slot_actor.data(), (size_t)nb * sizeof(int)));
+        long long covered = s->nf1 == s->nf_rigid && s->nf_rigid == s->nf ? s->nf1 : -1;
+        for (const ArticGroup& g : s->groups) {
+            if (covered < 0) break;
+            if (g.count == 0) continue;
+            if (!(g.chain && g.nl >= 2 && g.nl <= 4) || g.step_count != g.count) covered = -1;
+            else covered += (long long)g.step_count * g.nbody;
+        }
+        s->step_out_ok = s->n_coupled == 0 && nb > 0 && covered == nb;
+    }
     HIP_TRY(h2d(s->d_actor_dof, m->actor_dof, (size_t)(na + 1) * sizeof(int)));
     HIP_TRY(hipMemset(s->d_cforce, 0, (size_t)nb * 3 * sizeof(float)));
     HIP_TRY(hipMemset(s->d_ext, 0, (size_t)nb * 6 * sizeof(float)));
@@ -1005,6 +1036,12 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         timer.cap = mg_sim::kKern;
         mg_timer = &timer;
     }
+    // the refresh fused into the step (MG_FUSE_STEP_OUT): every body's rows are
+    // written by the kernel that steps it (s->step_out_ok), into the bound
+    // tensors (each one optional)
+    const unsigned long long step_cid = capture_id(st);
+    const bool step_out = (s->fusion & MG_FUSE_STEP_OUT) && fuse_here(s, step_cid) && s->step_out_ok &&
+                          (s->bind_root || s->bind_rb || s->bind_dof);
     for (const ArticGroup& g : s->groups) {
         if (g.step_count == 0) continue;
         MgArticArgs A{};
@@ -1020,6 +1057,13 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.dof_props = s->d_dof_props;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
         A.cforce = s->d_cforce;
+        if (step_out) {   // chain groups only (s->step_out_ok)
+            A.out_rb = s->bind_rb;
+            A.out_root = s->bind_root;
+            A.out_dof = s->bind_dof;
+            A.out_body = s->d_slot_global;
+            A.out_root_row = s->d_slot_actor;
+        }
         hipError_t e = mg_launch_artic_step(P, A, st);
         if (e != hipSuccess) return fail(MG_ERR_DEVICE, "articulation step launch: %s", hipGetErrorString(e));
     }
@@ -1048,11 +1092,6 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         hipError_t e = mg_launch_env_step(P, A, st);
         if (e != hipSuccess) return fail(MG_ERR_DEVICE, "coupled env step launch: %s", hipGetErrorString(e));
     }
-    // the refresh fused into the step (MG_FUSE_STEP_OUT): every body is a
-    // single-shape free body and actor root of this launch
-    const unsigned long long step_cid = capture_id(st);
-    const bool step_out = (s->fusion & MG_FUSE_STEP_OUT) && fuse_here(s, step_cid) && s->bind_root && s->bind_rb &&
-                          s->roots_free && s->nf1 == s->nb && s->na > 0;
     if (s->nf_rigid > 0) {
         MgRigidArgs A{};
         A.nf = s->nf_rigid; A.nf1 = s->nf1; A.nb = s->nb; A.free_ids = nullptr;   // internal slots 0..nf-1
@@ -1069,8 +1108,8 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         if (step_out) {
             A.out_rb = s->bind_rb;
             A.out_root = s->bind_root;
-            A.out_body = s->d_free_global;     // internal slot -> global body
-            A.out_root_row = s->d_root_row;
+            A.out_body = s->d_slot_global;     // internal slot -> global body
+            A.out_root_row = s->d_slot_actor;
         }
         HIP_TRY(mg_launch_rigid_step(P, A, st));
     }
@@ -1080,9 +1119,11 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
             if (int rc_ = flush_tgt(s, k, st)) return rc_;
     for (int k = 0; k < 3; ++k) s->pend_tgt[k] = nullptr;   // read (and written through) by the step
     s->state_gen++;
+    s->dof_sgen++;
     if (step_out) {
-        s->out_gen = s->rb_gen = s->state_gen;
-        s->out_cap = s->rb_cap = step_cid;
+        if (s->bind_root) { s->out_gen = s->state_gen; s->out_cap = step_cid; }
+        if (s->bind_rb) { s->rb_gen = s->state_gen; s->rb_cap = step_cid; }
+        if (s->bind_dof) { s->dof_gen = s->dof_sgen; s->dof_cap = step_cid; }
     }
     if (s->ext_pending) {
         HIP_TRY(hipMemsetAsync(s->d_ext, 0, (size_t)s->nb * 6 * sizeof(float), st));
@@ -1126,6 +1167,24 @@ int32_t mg_bind_refresh_targets(mg_sim* s, float* root_dst, float* rigid_body_ds
     s->out_gen = -1;
     return MG_OK;
 }
+
+int32_t mg_bind_dof_refresh_target(mg_sim* s, float* dof_dst) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    s->bind_dof = dof_dst;
+    s->dof_gen = -1;
+    return MG_OK;
+}
+
+int32_t mg_discard_pending_sets(mg_sim* s) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    s->pend_root = nullptr;
+    for (int k = 0; k < 3; ++k) s->pend_tgt[k] = nullptr;
+    return MG_OK;
+}
+
+int32_t mg_step_out_supported(mg_sim* s) { return s && s->uploaded && s->step_out_ok ? 1 : 0; }
+
+int32_t mg_last_set_deferred(mg_sim* s) { return s ? s->last_set_deferred : 0; }
 
 int32_t mg_set_kernel_timing(mg_sim* s, int32_t on) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
@@ -1213,6 +1272,9 @@ int32_t mg_refresh_rigid_body_state(mg_sim* s, float* dst, int32_t dst_host, voi
 }
 int32_t mg_refresh_dof_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
+    if (!dst_host && dst && dst == s->bind_dof && (s->fusion & MG_FUSE_STEP_OUT) && s->dof_gen == s->dof_sgen &&
+        s->dof_cap == capture_id((hipStream_t)stream))
+        return MG_OK;   // written by the step kernel (MG_FUSE_STEP_OUT)
     return refresh_rows(s, s->d_dof, s->nd, 2, nullptr, s->nd, dst, dst_host, (hipStream_t)stream);
 }
 int32_t mg_refresh_net_contact_force(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
@@ -1231,11 +1293,13 @@ int32_t mg_set_actor_root_state(mg_sim* s, const float* src, int32_t src_host, c
     const int* didx;
     s->state_gen++;
     const unsigned long long cid = capture_id(st);
+    s->last_set_deferred = 0;
     if (!src_host && !idx && s->roots_free && (s->fusion & MG_FUSE_ROOT_SET) && fuse_here(s, cid)) {
         if (s->pend_root && s->pend_root_cap != cid)
             if (int rc_ = flush_root(s, st)) return rc_;
         s->pend_root = src;   // read by the next simulate (a later full set replaces it)
         s->pend_root_cap = cid;
+        s->last_set_deferred = 1;
         return MG_OK;
     }
     if (int rc_ = flush_root(s, st)) return rc_;
@@ -1266,6 +1330,8 @@ int32_t mg_set_rigid_body_state(mg_sim* s, const float* src, int32_t src_host, v
 int32_t mg_set_dof_state(mg_sim* s, const float* src, int32_t src_host, const int32_t* idx, int32_t n_idx,
                          void* stream) {
     if (!s || !s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    s->dof_sgen++;
+    s->last_set_deferred = 0;
     return set_dof_columns(s, src, src_host, 2, s->d_dof, s->d_dof + s->nd, idx, n_idx, (hipStream_t)stream);
 }
 // column k of the DOF targets; a device-resident full set is read by the next
@@ -1278,11 +1344,13 @@ static int32_t set_dof_target(mg_sim* s, int k, const float* src, int32_t src_ho
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(s->device));
     const unsigned long long cid = capture_id(st);
+    s->last_set_deferred = 0;
     if (!src_host && !idx && (s->fusion & MG_FUSE_DOF_TARGETS) && fuse_here(s, cid)) {
         if (s->pend_tgt[k] && s->pend_tgt_cap[k] != cid)
             if (int rc_ = flush_tgt(s, k, st)) return rc_;
         s->pend_tgt[k] = src;
         s->pend_tgt_cap[k] = cid;
+        s->last_set_deferred = 1;
         return MG_OK;
     }
     if (int rc_ = flush_tgt(s, k, st)) return rc_;

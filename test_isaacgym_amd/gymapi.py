@@ -91,7 +91,11 @@ def _check_held(sim, what, kinds=None):
             keep.append((t, ver, setter, kind))
             continue
         if t._version != ver:
+            # the pending sets are dropped on both sides: none is applied with data
+            # newer than its set call, and a retry does not meet this one again
             sim.held_src = []
+            if sim.native:
+                N.lib.mg_discard_pending_sets(sim.native)
             raise N.MigymError(
                 "%s: the tensor passed to %s was modified before the simulate that reads it; with step "
                 "fusion on (gym.set_step_fusion) a full device set is read at the next simulate, not at the "
@@ -171,10 +175,11 @@ class Gym:
         N.check(N.lib.mg_simulate(h, sim.stream()), "mg_simulate")
         sim.held_src = []
         if sim.fusion & STEP_FUSION_STEP_OUT and "root" in sim.tensors:
-            # the step kernel may have written the bound root / rigid-body tensors
-            # (MG_FUSE_STEP_OUT): a write to them before their refresh forces a gather
+            # the step kernels may have written the bound root / rigid-body / DOF
+            # tensors (MG_FUSE_STEP_OUT): a write to them before their refresh forces a gather
             sim.root_out_version = sim.tensors["root"]._version
             sim.rb_paired_version = sim.tensors["rb"]._version
+            sim.dof_out_version = sim.tensors["dof"]._version
         sim.epoch += 1
         sim.frame += 1
         sim.time += sim.params.dt
@@ -878,8 +883,12 @@ class Gym:
             # served-without-launch marks)
             N.check(N.lib.mg_bind_refresh_targets(h, sim.tensors["root"].data_ptr(), sim.tensors["rb"].data_ptr()),
                     "mg_bind_refresh_targets")
+        if key == "dof" and sim.dof_out_version is not None and t._version != sim.dof_out_version:
+            N.check(N.lib.mg_bind_dof_refresh_target(h, t.data_ptr()), "mg_bind_dof_refresh_target")
         if key == "root":
             sim.root_out_version = None
+        elif key == "dof":
+            sim.dof_out_version = None
         N.check(fn(h, t.data_ptr(), 1 if t.device.type == "cpu" else 0, sim.stream()), what)
         if key == "root" and sim.fusion & STEP_FUSION_REFRESH:
             sim.rb_paired_version = sim.tensors["rb"]._version
@@ -938,11 +947,14 @@ class Gym:
             it = it.contiguous()
             rc = fn(sim.require_native(what), t.data_ptr(), host, it.data_ptr(), n, sim.stream())
         else:
-            rc = fn(sim.require_native(what), t.data_ptr(), host, None, 0, sim.stream())
-            # a fused set (opt-in: STEP_FUSION_ROOT_SET / _DOF_TARGETS) is read by
-            # the next simulate: keep its tensor alive until then and remember its
-            # version, so a write to it before that read raises (_check_held)
-            if kind is not None and sim.fusion:
+            h = sim.require_native(what)
+            rc = fn(h, t.data_ptr(), host, None, 0, sim.stream())
+            # a fused set (opt-in: STEP_FUSION_ROOT_SET / _DOF_TARGETS) whose read
+            # the library deferred to the next simulate: keep its tensor alive
+            # until then and remember its version, so a write to it before that
+            # read raises (_check_held); a set the library copied at the call
+            # (host source, a flag not set, a scene it cannot fuse) holds nothing
+            if kind is not None and rc == N.MG_OK and N.lib.mg_last_set_deferred(h):
                 sim.held_src.append((t, t._version, what, kind))
         if rc != N.MG_OK:
             print("*** migym: %s: %s" % (what, N.last_error()), file=sys.stderr)

@@ -25,7 +25,7 @@
 #                tools/kbench.py at $AB_SIZES (default 4096 262144), twice
 #   default: pytest,smoke,bench,prof
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-tag=${1:-r03}
+tag=${1:-r04}
 steps=${2:-pytest,smoke,bench,prof}
 kexpr=${3:-}
 mkdir -p gpurun_out
@@ -92,6 +92,8 @@ fi
 if has kgimbal; then
   timeout -k 10 300 python tools/kbench_gimbal.py 4096 32768 262144 \
     > gpurun_out/kgimbal_$tag.jsonl 2> gpurun_out/kgimbal_$tag.err || { tail -20 gpurun_out/kgimbal_$tag.err; exit 1; }
+  MIGYM_KB_FUSED=1 timeout -k 10 300 python tools/kbench_gimbal.py 4096 32768 262144 \
+    >> gpurun_out/kgimbal_$tag.jsonl 2>> gpurun_out/kgimbal_$tag.err || { tail -20 gpurun_out/kgimbal_$tag.err; exit 1; }
   cat gpurun_out/kgimbal_$tag.jsonl
 fi
 if has kfranka; then
