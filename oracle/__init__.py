@@ -26,9 +26,9 @@ def _load():
     lib = ctypes.CDLL(LIB)
     vp = ctypes.c_void_p
     lib.oracle_step.restype = ctypes.c_int
-    lib.oracle_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
+    lib.oracle_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
     lib.oracle_step_mt.restype = ctypes.c_int
-    lib.oracle_step_mt.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
+    lib.oracle_step_mt.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
     return lib
 
 
@@ -46,16 +46,29 @@ def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
-# The coupled step's friction patches are simulation state
-# kept from step to step, as the device keeps them: one float32 row of
-# FC_N = 128 pairs x (16 + 1) floats per env (migym_oracle_env.c OE_FC_N).
+# Friction patches are simulation state kept from
+# step to step, as the device keeps them: per env, the coupled step's pairs —
+# FC_N = 128 pairs x (16 + 1) floats (migym_oracle_env.c OE_FC_N) — and per
+# body, a free body's ground patch — BC_N = 16 floats (migym_oracle.c OR_GP_N).
 FC_N = 128 * (16 + 1)
+BC_N = 16
 _caches = {}
+
+
+class ContactCache:
+    """The friction patches of one simulation (zeros: no patch yet)."""
+
+    def __init__(self, model):
+        self.env = np.zeros((max(int(model.num_envs), 1), FC_N), dtype=np.float32)
+        self.body = np.zeros((max(int(model.num_bodies), 1), BC_N), dtype=np.float32)
+
+    def fits(self, model):
+        return self.env.shape[0] >= int(model.num_envs) and self.body.shape[0] >= int(model.num_bodies)
 
 
 def contact_cache(model):
     """A fresh (no patch yet) friction-patch cache for `model`."""
-    return np.zeros((max(int(model.num_envs), 1), FC_N), dtype=np.float32)
+    return ContactCache(model)
 
 
 def _cache_for(state, model):
@@ -64,7 +77,7 @@ def _cache_for(state, model):
     patches inside the sim the same way)."""
     key = id(state)
     ent = _caches.get(key)
-    if ent is not None and ent[0]() is state and ent[1].shape[0] >= int(model.num_envs):
+    if ent is not None and ent[0]() is state and ent[1].fits(model):
         return ent[1]
     c = contact_cache(model)
     _caches[key] = (weakref.ref(state, lambda _r, k=key: _caches.pop(k, None)), c)
@@ -95,10 +108,10 @@ def step(sim_params, model, state, dof, tgt=None, props=None, ext=None, cforce=N
     ext_c = None if ext is None else np.ascontiguousarray(ext, dtype=np.float32)
     assert cforce.dtype == np.float32 and cforce.flags.c_contiguous and cforce.shape == (nb, 3)
     fc = _cache_for(state, model) if contact_cache is None else contact_cache
-    assert fc.dtype == np.float32 and fc.flags.c_contiguous and fc.shape[1] == FC_N
-    assert fc.shape[0] >= int(model.num_envs)
+    assert fc.fits(model)
     rc = lib().oracle_step(ctypes.addressof(sim_params), ctypes.addressof(model), _ptr(state), _ptr(dof),
-                           _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), _ptr(fc), int(b0), int(b1))
+                           _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), _ptr(fc.env), _ptr(fc.body),
+                           int(b0), int(b1))
     if rc != 0:
         raise RuntimeError("oracle_step: unsupported model")
     return cforce
@@ -119,8 +132,10 @@ def step_threads(sim_params, model, state, dof, nthreads, tgt=None, props=None, 
     props_c = None if props is None else np.ascontiguousarray(props, dtype=np.float32)
     ext_c = None if ext is None else np.ascontiguousarray(ext, dtype=np.float32)
     fc = _cache_for(state, model) if contact_cache is None else contact_cache
+    assert fc.fits(model)
     rc = lib().oracle_step_mt(ctypes.addressof(sim_params), ctypes.addressof(model), _ptr(state), _ptr(dof),
-                              _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), _ptr(fc), int(nthreads))
+                              _ptr(tgt_c), _ptr(props_c), _ptr(ext_c), _ptr(cforce), _ptr(fc.env), _ptr(fc.body),
+                              int(nthreads))
     if rc != 0:
         raise RuntimeError("oracle_step_mt: unsupported model")
     return cforce

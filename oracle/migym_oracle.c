@@ -175,6 +175,8 @@ static step_t make_step_(const mg_sim_params* p) {
  * written out explicitly (as the device's BasisZ specialisation). */
 typedef struct { int upz; v3_t n, t1, t2; } basis_t;
 static float b_dn(const basis_t* B, v3_t v) { return B->upz ? v.z : dot3(B->n, v); }
+static float b_d1(const basis_t* B, v3_t v) { return B->upz ? v.y : dot3(B->t1, v); }
+static float b_d2(const basis_t* B, v3_t v) { return B->upz ? -v.x : dot3(B->t2, v); }
 static v3_t b_addn(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x, v.y, v.z + s) : mad3(v, B->n, s); }
 static v3_t b_add1(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x, v.y + s, v.z) : mad3(v, B->t1, s); }
 static v3_t b_add2(const basis_t* B, v3_t v, float s) { return B->upz ? V(v.x - s, v.y, v.z) : mad3(v, B->t2, s); }
@@ -368,7 +370,97 @@ static int shape_candidates(const step_t* P, const basis_t* B, const float* sh, 
     return n;
 }
 
-static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st, const float* ext, float* cf) {
+/* ---- friction patch of a free body on the ground plane:
+ * mg_rigid.hip ground_patch_update, op for op. PhysX patch friction as the
+ * coupled step's (§3.6.1, migym_oracle_env.c patch_update_) with the ground as
+ * the static second body (its copy of an anchor is a world point): up to two
+ * anchors kept while the normal holds and the copies stay within the
+ * correlation distance, grown from this substep's contacts in slot order. The
+ * record (16 floats, the coupled record's layout) persists from step to step:
+ * bcache[b]. */
+#define OR_GP_N 16
+#define OR_FP_COS 0.999f
+typedef struct { int cnt; v3_t nA, aA[2], aB[2]; } gpatch_t;
+static v3_t qrot_inv0_(q4_t q, v3_t v) { return qrot_(Q(-q.x, -q.y, -q.z, q.w), v); }
+static void gpatch_load_(gpatch_t* R, const float* r) {
+    int k;
+    R->cnt = (int)r[0];
+    R->nA = V(r[1], r[2], r[3]);
+    for (k = 0; k < 2; ++k) {
+        R->aA[k] = V(r[4 + 6 * k], r[5 + 6 * k], r[6 + 6 * k]);
+        R->aB[k] = V(r[7 + 6 * k], r[8 + 6 * k], r[9 + 6 * k]);
+    }
+}
+static void gpatch_store_(const gpatch_t* R, float* r) {
+    int k;
+    r[0] = (float)R->cnt;
+    if (R->cnt == 0) return;   /* the device writes the rest only when anchors are held */
+    r[1] = R->nA.x; r[2] = R->nA.y; r[3] = R->nA.z;
+    for (k = 0; k < 2; ++k) {
+        r[4 + 6 * k] = R->aA[k].x; r[5 + 6 * k] = R->aA[k].y; r[6 + 6 * k] = R->aA[k].z;
+        r[7 + 6 * k] = R->aB[k].x; r[8 + 6 * k] = R->aB[k].y; r[9 + 6 * k] = R->aB[k].z;
+    }
+}
+static void gpatch_update_(gpatch_t* R, v3_t x, q4_t q, v3_t n0, const v3_t* p, const float* s0, const int* on,
+                           float fot, float corr) {
+    const float c2 = corr * corr;
+    int cnt = R->cnt, k, j, kept;
+    gpatch_t N;
+    if (cnt > 0 && dot3(qrot_(q, R->nA), n0) < OR_FP_COS) cnt = 0;
+    N.cnt = 0;
+    N.aA[0] = N.aA[1] = N.aB[0] = N.aB[1] = V(0.0f, 0.0f, 0.0f);
+    for (k = 0; k < 2; ++k) {
+        if (k < cnt) {
+            const v3_t d = sub3(add3(x, qrot_(q, R->aA[k])), R->aB[k]);
+            if (dot3(d, d) <= c2) {
+                if (N.cnt == 0) { N.aA[0] = R->aA[k]; N.aB[0] = R->aB[k]; }
+                else { N.aA[1] = R->aA[k]; N.aB[1] = R->aB[k]; }
+                N.cnt = N.cnt + 1;
+            }
+        }
+    }
+    kept = N.cnt;   /* anchors kept from the last substep */
+    /* growth (PhysX growPatches, as mg_rigid.hip ground_patch_update) */
+    {
+        const int grow = N.cnt < 2;
+        v3_t w0 = N.cnt > 0 ? add3(x, qrot_(q, N.aA[0])) : V(0.0f, 0.0f, 0.0f), w1 = V(0.0f, 0.0f, 0.0f);
+        float dd = 0.0f;
+        for (j = 0; j < 4; ++j) {
+            if (grow && on[j] && s0[j] <= fot) {
+                const v3_t pj = p[j];
+                int put = -1;
+                if (N.cnt == 0) {
+                    put = 0;
+                } else if (N.cnt == 1) {
+                    const v3_t d = sub3(pj, w0);
+                    const float d2 = dot3(d, d);
+                    if (d2 > c2) { put = 1; dd = d2; }
+                } else {
+                    const v3_t e0 = sub3(pj, w0), e1 = sub3(pj, w1);
+                    const float d0 = dot3(e0, e0), d1 = dot3(e1, e1);
+                    if (d0 > d1) {
+                        if (d0 > dd) { put = 1; dd = d0; }
+                    } else if (d1 > dd) {
+                        put = 0;
+                        dd = d1;
+                    }
+                }
+                if (put >= 0) {
+                    const v3_t la = qrot_inv0_(q, sub3(pj, x));
+                    if (put == 0) { N.aA[0] = la; N.aB[0] = pj; w0 = pj; }
+                    else { N.aA[1] = la; N.aB[1] = pj; w1 = pj; }
+                    if (N.cnt <= put) N.cnt = put + 1;
+                }
+            }
+        }
+    }
+    N.nA = kept > 0 ? R->nA : qrot_inv0_(q, n0);   /* the creation normal while an anchor is kept */
+    *R = N;
+}
+
+/* pr: the body's ground-patch record (OR_GP_N floats), or NULL (none kept) */
+static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st, const float* ext, float* cf,
+                            float* pr) {
     const float* M = m->body_mass + (size_t)b * MG_MASS_N;
     const int tb = m->body_tmpl[b];
     const float* tf = m->tmpl_body_f + (size_t)tb * MG_TBODY_F_N;
@@ -391,12 +483,16 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
     B.n = P->n; B.t1 = P->t1; B.t2 = P->t2;
     B.upz = P->n.x == 0.0f && P->n.y == 0.0f && P->n.z == 1.0f && P->t1.x == 0.0f && P->t1.y == 1.0f &&
             P->t1.z == 0.0f && P->t2.x == -1.0f && P->t2.y == 0.0f && P->t2.z == 0.0f;
+    gpatch_t R;
     if (ext) { fext = V(ext[0], ext[1], ext[2]); text = V(ext[3], ext[4], ext[5]); }
+    R.cnt = 0;
+    if (pr && nsh == 1 && P->ground) gpatch_load_(&R, pr);
     q = qnorm_(q);
     for (st_ = 0; st_ < P->substeps; ++st_) {
         const s3_t Iw = sym_rdrt_(qmat_(inertia_frame_(q, iq)), invI);
         const v3_t xc = com_world_(x, q, com);
         slot_t sl[OR_MAXC];
+        v3_t cp[4];   /* single-shape bodies: contact point of slot k */
         int j, it;
         v3_t dx = V(0.0f, 0.0f, 0.0f), dth = V(0.0f, 0.0f, 0.0f);
         if (tf[4] != 0.0f) v = mad3(v, V(P->g[0], P->g[1], P->g[2]), h);
@@ -426,6 +522,7 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                     ns.r = sub3(cd[k].p, xc); ns.s0 = cd[k].sep - P->ro; ns.mu = mu; ns.e = e; ns.on = 1;
                     if (nsh == 1) {
                         sl[cd[k].k] = ns;          /* static slot: candidate k -> slot k (of 4) */
+                        cp[cd[k].k] = cd[k].p;
                     } else if (nc < OR_MAXC) {     /* shift register: newest in slot 0 */
                         for (j = OR_MAXC - 1; j > 0; --j) sl[j] = sl[j - 1];
                         sl[0] = ns;
@@ -435,13 +532,26 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
             }
         }
         if (nsh <= 1) {
-            /* single-shape bodies (k_rigid_step1): once any of the 4 static slots
-             * is in contact, all 4 are solved, an inactive one with r = 0, s0 = 0
-             * and zero effective masses (so its rows apply zero impulse) */
+            /* single-shape bodies (k_rigid_step1): the ground patch (anchors kept
+             * or grown from this substep's contacts), then — once any of the 4
+             * static slots is in contact — all 4 normal rows are solved, an
+             * inactive one with r = 0, s0 = 0 and zero effective masses (so its
+             * rows apply zero impulse), with the patch's anchors as the friction
+             * rows (an absent anchor likewise) */
             int any = 0;
             for (j = 0; j < 4; ++j) any = any || sl[j].on;
             if (any) {
-                float mu = 0.0f, e = 0.0f;
+                float s0c[4];
+                int onc[4];
+                for (j = 0; j < 4; ++j) { onc[j] = sl[j].on; s0c[j] = sl[j].on ? sl[j].s0 : 0.0f; }
+                gpatch_update_(&R, x, q, B.n, cp, s0c, onc, P->fot, P->corr);
+            } else {
+                R.cnt = 0;
+            }
+            if (any) {
+                float mu = 0.0f, e = 0.0f, ak[2][2], al[2][2], ae[2][2], share;
+                int slip = 0, a;
+                v3_t arr[2];
                 if (nsh == 1) {
                     const float* sh = m->shapes + (size_t)sh0 * MG_SHAPE_STRIDE;
                     mu = 0.5f * (sh[11] + P->mu_g);
@@ -454,14 +564,100 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                     {
                         const v3_t r = sl[j].r;
                         sl[j].kn = act ? 1.0f / (invm + b_kn(&B, r, b_iwn(&B, &Iw, r))) : 0.0f;
-                        sl[j].kt1 = act ? 1.0f / (invm + b_k1(&B, r, b_iw1(&B, &Iw, r))) : 0.0f;
-                        sl[j].kt2 = act ? 1.0f / (invm + b_k2(&B, r, b_iw2(&B, &Iw, r))) : 0.0f;
                     }
-                    sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
+                    sl[j].ln = 0.0f;
                     sl[j].vn0 = b_vn(&B, v, w, sl[j].r);
                     sl[j].on = 1;
                 }
+                /* anchor rows: the anchor's body copy, tangents t1, t2; position
+                 * sweeps close 80 % of the substep-start drift of its two copies */
+                for (a = 0; a < 2; ++a) {
+                    const int act = a < R.cnt;
+                    v3_t r = V(0.0f, 0.0f, 0.0f);
+                    float e1 = 0.0f, e2 = 0.0f;
+                    if (act) {
+                        const v3_t wa = add3(x, qrot_(q, R.aA[a]));
+                        const v3_t dr = sub3(wa, R.aB[a]);
+                        const float kd = 0.8f * P->inv_h;
+                        r = sub3(wa, xc);
+                        e1 = fminf(fmaxf(-b_d1(&B, dr) * kd, -P->maxdep), P->maxdep);
+                        e2 = fminf(fmaxf(-b_d2(&B, dr) * kd, -P->maxdep), P->maxdep);
+                    }
+                    arr[a] = r;
+                    ak[a][0] = act ? 1.0f / (invm + b_k1(&B, r, b_iw1(&B, &Iw, r))) : 0.0f;
+                    ak[a][1] = act ? 1.0f / (invm + b_k2(&B, r, b_iw2(&B, &Iw, r))) : 0.0f;
+                    ae[a][0] = e1; ae[a][1] = e2;
+                    al[a][0] = 0.0f; al[a][1] = 0.0f;
+                }
+                /* each anchor of a two-anchor patch holds half of the patch's
+                 * Coulomb budget mu N per direction (symmetric: a box sliding on
+                 * its diagonal anchors exerts no yaw torque; the two saturate at
+                 * mu N together) */
+                share = R.cnt == 2 ? 0.5f : 1.0f;
+                for (it = 0; it < P->npos + P->nvel; ++it) {
+                    const int pos = it < P->npos, last = it == P->npos + P->nvel - 1;
+                    float psum;
+                    for (j = 0; j < 4; ++j) {
+                        const float sj = b_ps(&B, sl[j].s0, dx, dth, sl[j].r);
+                        contact_normal(&B, &sl[j], &v, &w, invm, &Iw,
+                                       pos ? pos_target_(P, sj) : vel_target_(P, sj, sl[j].e, sl[j].vn0));
+                    }
+                    /* the patch's normal impulse, in slot order */
+                    psum = sl[0].ln;
+                    for (j = 1; j < 4; ++j) psum = psum + sl[j].ln;
+                    for (a = 0; a < 2; ++a) {
+                        const float mun = mu * psum;
+                        int rw;
+                        for (rw = 0; rw < 2; ++rw) {
+                            const float lim = share * mun;
+                            const float tgt = pos ? ae[a][rw] : 0.0f;
+                            const float vt = rw == 0 ? b_v1(&B, v, w, arr[a]) : b_v2(&B, v, w, arr[a]);
+                            const float raw = fmaf(ak[a][rw], tgt - vt, al[a][rw]);
+                            const float nl = clamp_sym_(raw, lim);
+                            const float dl = nl - al[a][rw];
+                            if (last && (raw > lim || raw < -lim)) slip = 1;
+                            al[a][rw] = nl;
+                            if (rw == 0) {
+                                v = b_f1(&B, v, dl, invm);
+                                w = fmad3_(w, b_iw1(&B, &Iw, arr[a]), dl);
+                            } else {
+                                v = b_f2(&B, v, dl, invm);
+                                w = fmad3_(w, b_iw2(&B, &Iw, arr[a]), dl);
+                            }
+                        }
+                    }
+                    /* the last position sweep and the velocity sweeps end with the
+                     * normal rows again (as the coupled step, §3.6.1) */
+                    if (it >= P->npos - 1) {
+                        for (j = 0; j < 4; ++j) {
+                            const float sj = b_ps(&B, sl[j].s0, dx, dth, sl[j].r);
+                            contact_normal(&B, &sl[j], &v, &w, invm, &Iw,
+                                           pos ? pos_target_(P, sj) : vel_target_(P, sj, sl[j].e, sl[j].vn0));
+                        }
+                    }
+                    if (pos) {
+                        dx = fmad3_(dx, v, P->sub);
+                        dth = fmad3_(dth, w, P->sub);
+                    }
+                }
+                for (j = 0; j < 4; ++j) fsum = b_addn(&B, fsum, sl[j].ln);
+                for (a = 0; a < 2; ++a) {
+                    fsum = b_add1(&B, fsum, al[a][0]);
+                    fsum = b_add2(&B, fsum, al[a][1]);
+                }
+                if (slip) R.cnt = 0;   /* a slipping patch lets go (regrown at the next substep) */
+            } else {
+                for (it = 0; it < P->npos; ++it) {
+                    dx = fmad3_(dx, v, P->sub);
+                    dth = fmad3_(dth, w, P->sub);
+                }
             }
+            {
+                const v3_t xc1 = add3(xc, dx);
+                q = qint_(q, dth);
+                x = origin_from_com_(xc1, q, com);
+            }
+            continue;
         }
         for (j = 0; j < OR_MAXC; ++j) {
             if (!sl[j].on || nsh <= 1) continue;
@@ -510,6 +706,7 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
     st[7] = v.x; st[8] = v.y; st[9] = v.z;
     st[10] = w.x; st[11] = w.y; st[12] = w.z;
     cf[0] = fsum.x * P->inv_dt; cf[1] = fsum.y * P->inv_dt; cf[2] = fsum.z * P->inv_dt;
+    if (pr && nsh == 1 && P->ground) gpatch_store_(&R, pr);
 }
 
 /* ---- spatial algebra ----------------------------------- */
@@ -981,12 +1178,14 @@ static int artic_step(const step_t* P, const mg_model* m, const int* ai, float* 
  *   vel, actuation force), props [nd][12] (NULL = model->dof_props),
  *   ext [nb][6] world force/torque at the COM or NULL, cforce [nb][3] out,
  *   fcache: the coupled step's friction patches, [num_envs][OE_FC_N] floats
- *   kept by the caller from step to step (zeros: no patch yet; NULL: none kept).
+ *   kept by the caller from step to step (zeros: no patch yet; NULL: none kept),
+ *   bcache: the free bodies' ground patches, [num_bodies][OR_GP_N], likewise.
  * Bodies in [body_begin, body_end) only (a bounded CPU-baseline sample);
  * articulations are stepped when their root lies in that range. Returns 0, or
  * -1 for an unsupported model. */
 int oracle_step(const mg_sim_params* p, const mg_model* m, float* state, float* dof, const float* tgt,
-                const float* props, const float* ext, float* cforce, float* fcache, int body_begin, int body_end) {
+                const float* props, const float* ext, float* cforce, float* fcache, float* bcache, int body_begin,
+                int body_end) {
     step_t P = make_step_(p);
     int b, k, ne, rc = 0;
     oenv_t* envs = NULL;
@@ -1011,7 +1210,7 @@ int oracle_step(const mg_sim_params* p, const mg_model* m, float* state, float* 
     for (b = body_begin; b < body_end; ++b) {
         if (m->body_kind[b] != MG_BODY_FREE || owned[b]) continue;
         rigid_body_step(&P, m, b, state + (size_t)b * MG_STATE_N, ext ? ext + (size_t)b * 6 : NULL,
-                        cforce + (size_t)b * 3);
+                        cforce + (size_t)b * 3, bcache ? bcache + (size_t)b * OR_GP_N : NULL);
     }
 done:
     free(envs);
@@ -1024,7 +1223,7 @@ done:
  * and free bodies are independent, so each of the three loops is split across
  * the threads after one classification; results equal oracle_step's. */
 int oracle_step_mt(const mg_sim_params* p, const mg_model* m, float* state, float* dof, const float* tgt,
-                   const float* props, const float* ext, float* cforce, float* fcache, int nthreads) {
+                   const float* props, const float* ext, float* cforce, float* fcache, float* bcache, int nthreads) {
     step_t P = make_step_(p);
     int ne, rc = 0;
     oenv_t* envs = NULL;
@@ -1054,7 +1253,7 @@ int oracle_step_mt(const mg_sim_params* p, const mg_model* m, float* state, floa
             for (b = 0; b < m->num_bodies; ++b) {
                 if (m->body_kind[b] != MG_BODY_FREE || owned[b]) continue;
                 rigid_body_step(&P, m, b, state + (size_t)b * MG_STATE_N, ext ? ext + (size_t)b * 6 : NULL,
-                                cforce + (size_t)b * 3);
+                                cforce + (size_t)b * 3, bcache ? bcache + (size_t)b * OR_GP_N : NULL);
             }
         }
         if (bad) rc = -1;

@@ -617,7 +617,7 @@ static void patch_store_(const patch_t* R, float* r) {
 static void patch_update_(patch_t* R, v3_t xa, q4_t qa, v3_t xb, q4_t qb, const pair_t* o, float fot, float corr) {
     const v3_t n0 = o->nrm[0];
     const float c2 = corr * corr;
-    int cnt = R->cnt, k, j;
+    int cnt = R->cnt, k, j, kept;
     patch_t N;
     if (cnt > 0 && dot3(qrot_(qa, R->nA), n0) < OE_FP_COS) cnt = 0;
     N.cnt = 0;
@@ -626,22 +626,42 @@ static void patch_update_(patch_t* R, v3_t xa, q4_t qa, v3_t xb, q4_t qb, const 
         const v3_t d = sub3(add3(xa, qrot_(qa, R->aA[k])), add3(xb, qrot_(qb, R->aB[k])));
         if (dot3(d, d) <= c2) { N.aA[N.cnt] = R->aA[k]; N.aB[N.cnt] = R->aB[k]; N.cnt++; }
     }
-    for (j = 0; j < o->n; ++j) {
-        const v3_t p = o->p[j];
-        int add;
-        if (!(N.cnt < 2 && o->sep[j] <= fot)) continue;
-        add = N.cnt == 0;
-        if (N.cnt == 1) {
-            const v3_t d = sub3(p, add3(xa, qrot_(qa, N.aA[0])));
-            add = dot3(d, d) > c2;
-        }
-        if (add) {
-            N.aA[N.cnt] = qrot_inv_(qa, sub3(p, xa));
-            N.aB[N.cnt] = qrot_inv_(qb, sub3(p, xb));
-            N.cnt++;
+    kept = N.cnt;   /* anchors kept from the last substep */
+    /* growth (PhysX growPatches, as mg_env.hip patch_update) */
+    {
+        const int grow = N.cnt < 2;
+        v3_t w0 = N.cnt > 0 ? add3(xa, qrot_(qa, N.aA[0])) : V(0.0f, 0.0f, 0.0f), w1 = V(0.0f, 0.0f, 0.0f);
+        float dd = 0.0f;
+        for (j = 0; j < o->n; ++j) {
+            if (grow && o->sep[j] <= fot) {
+                const v3_t pj = o->p[j];
+                int put = -1;
+                if (N.cnt == 0) {
+                    put = 0;
+                } else if (N.cnt == 1) {
+                    const v3_t d = sub3(pj, w0);
+                    const float d2 = dot3(d, d);
+                    if (d2 > c2) { put = 1; dd = d2; }
+                } else {
+                    const v3_t e0 = sub3(pj, w0), e1 = sub3(pj, w1);
+                    const float d0 = dot3(e0, e0), d1 = dot3(e1, e1);
+                    if (d0 > d1) {
+                        if (d0 > dd) { put = 1; dd = d0; }
+                    } else if (d1 > dd) {
+                        put = 0;
+                        dd = d1;
+                    }
+                }
+                if (put >= 0) {
+                    const v3_t la = qrot_inv_(qa, sub3(pj, xa)), lb = qrot_inv_(qb, sub3(pj, xb));
+                    if (put == 0) { N.aA[0] = la; N.aB[0] = lb; w0 = pj; }
+                    else { N.aA[1] = la; N.aB[1] = lb; w1 = pj; }
+                    if (N.cnt <= put) N.cnt = put + 1;
+                }
+            }
         }
     }
-    N.nA = qrot_inv_(qa, n0);
+    N.nA = kept > 0 ? R->nA : qrot_inv_(qa, n0);   /* the creation normal while an anchor is kept */
     *R = N;
 }
 
@@ -1509,9 +1529,8 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                 const float mun = amu[c] * psum[alast[c]];
                 int rw;
                 for (rw = 1; rw < 3; ++rw) {
-                    /* the patch's budget mu N per direction, less its other anchor's impulse */
-                    const float other = apart[c] == 1 ? clam[c + 1][rw] : (apart[c] == 2 ? clam[c - 1][rw] : 0.0f);
-                    const float lim = fmaxf(mun - fabsf(other), 0.0f);
+                    /* half the patch's budget mu N per direction for each of two anchors */
+                    const float lim = (apart[c] ? 0.5f : 1.0f) * mun;
                     const float lam = clam[c][rw];
                     const float tg = pos ? ae[c][rw - 1] : 0.0f;
                     float raw, nl, dl;

@@ -11,6 +11,7 @@ Index maps (bit-exact contract):
 Tensor frame: global sim frame; env i's origin is its grid cell.
 """
 import ctypes
+import sys
 import os
 
 import numpy as np
@@ -28,6 +29,26 @@ def _raw_stream(device):
 if hasattr(torch._C, "_cuda_getCurrentRawStream"):
     _raw_stream = torch._C._cuda_getCurrentRawStream      # noqa: F811  (one C call, no Stream object)
 
+
+
+_warned_multishape = [False]
+
+
+def _warn_multishape_friction(A):
+    """Friction is PhysX's patch friction (anchors, physx.friction_offset_threshold
+    / friction_correlation_distance) for single-shape free bodies on the ground
+    and for every coupled env; a free body of several
+    shapes stepping alone on the ground keeps one friction row pair per contact
+    point. Said once, on stderr — never silently."""
+    if _warned_multishape[0]:
+        return
+    kind, tmpl, tbi = A["body_kind"], A["body_tmpl"], A["tmpl_body_i"]
+    free = np.asarray(kind) == N.MG_BODY_FREE
+    if free.any() and (np.asarray(tbi)[np.asarray(tmpl)[free], 1] > 1).any():
+        _warned_multishape[0] = True
+        print("*** migym: free bodies with several collision shapes keep per-point friction against the ground "
+              "plane (patch friction: single-shape free bodies and coupled envs; DESIGN.md §3.2.1)",
+              file=sys.stderr)
 
 class Env:
     __slots__ = ("sim", "index", "lower", "upper", "per_row", "origin", "actors", "num_bodies", "num_dofs",
@@ -467,6 +488,7 @@ class Sim:
         if self.finalized:
             return
         A = self.build_model()
+        _warn_multishape_friction(A)
         dev = self.device
         self.tensors["root"] = torch.from_numpy(A["body_state0"][A["actor_root_body"]].copy()).to(dev)
         self.tensors["rb"] = torch.from_numpy(A["body_state0"].copy()).to(dev)

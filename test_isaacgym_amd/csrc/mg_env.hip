@@ -649,24 +649,48 @@ MG_HD void patch_update(Patch& R, V3 xa, Q4 qa, V3 xb, Q4 qb, const PairOut& o, 
             }
         }
     }
+    // growth (PhysX growPatches; mg_rigid.hip ground_patch_update): a patch
+    // still holding two anchors keeps them; otherwise the contacts within the
+    // friction offset threshold, in emitted order, give anchor 0, then anchor 1
+    // (the first farther than the correlation distance from anchor 0), then
+    // each later one replaces the anchor it is nearer to when it lies farther
+    // from the other than the two are apart (the anchors spread)
+    const int kept = N.cnt;   // anchors kept from the last substep
+    const bool grow = N.cnt < 2;
+    V3 w0 = N.cnt > 0 ? vadd(xa, qrot(qa, N.aA[0])) : v3(0.0f, 0.0f, 0.0f), w1 = v3(0.0f, 0.0f, 0.0f);
+    float dd = 0.0f;
 #pragma unroll
     for (int j = 0; j < MG_PAIR_MAXC; ++j) {
-        if (j < o.n && N.cnt < 2 && o.sep[j] <= fot) {
-            const V3 p = o.p[j];
-            bool add = N.cnt == 0;
-            if (N.cnt == 1) {
-                const V3 d = vsub(p, vadd(xa, qrot(qa, N.aA[0])));
-                add = vdot(d, d) > c2;
+        if (grow && j < o.n && o.sep[j] <= fot) {
+            const V3 pj = o.p[j];
+            int put = -1;
+            if (N.cnt == 0) {
+                put = 0;
+            } else if (N.cnt == 1) {
+                const V3 d = vsub(pj, w0);
+                const float d2 = vdot(d, d);
+                if (d2 > c2) { put = 1; dd = d2; }
+            } else {
+                const V3 e0 = vsub(pj, w0), e1 = vsub(pj, w1);
+                const float d0 = vdot(e0, e0), d1 = vdot(e1, e1);
+                if (d0 > d1) {
+                    if (d0 > dd) { put = 1; dd = d0; }
+                } else if (d1 > dd) {
+                    put = 0;
+                    dd = d1;
+                }
             }
-            if (add) {
-                const V3 la = qrot_inv(qa, vsub(p, xa)), lb = qrot_inv(qb, vsub(p, xb));
-                if (N.cnt == 0) { N.aA[0] = la; N.aB[0] = lb; }
-                else { N.aA[1] = la; N.aB[1] = lb; }
-                N.cnt = N.cnt + 1;
+            if (put >= 0) {
+                const V3 la = qrot_inv(qa, vsub(pj, xa)), lb = qrot_inv(qb, vsub(pj, xb));
+                if (put == 0) { N.aA[0] = la; N.aB[0] = lb; w0 = pj; }
+                else { N.aA[1] = la; N.aB[1] = lb; w1 = pj; }
+                if (N.cnt <= put) N.cnt = put + 1;
             }
         }
     }
-    N.nA = qrot_inv(qa, n0);
+    // the patch normal is the one the patch was created with while it keeps an
+    // anchor (a slowly tilting contact still drops it past MG_FP_NORMAL_COS)
+    N.nA = kept > 0 ? R.nA : qrot_inv(qa, n0);
     R = N;
 }
 
@@ -1637,12 +1661,9 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     const float mun = S.amu[c] * S.psum[al & 0xFF];
 #pragma unroll
                     for (int rw = 1; rw < 3; ++rw) {
-                        // the patch's Coulomb budget mu N per direction, less what its
-                        // other anchor holds along it (current impulse)
-                        float other = 0.0f;
-                        if (c + 1 < MAXCT && pc == 1) other = lam[(c + 1) * 3 + rw];
-                        if (c >= 1 && pc == 2) other = lam[(c - 1) * 3 + rw];
-                        const float lim = fmaxf(mun - fabsf(other), 0.0f);
+                        // the patch's Coulomb budget mu N per direction, half of it for
+                        // each of two anchors (symmetric; the two saturate at mu N)
+                        const float lim = (pc ? 0.5f : 1.0f) * mun;
                         const float tgt = pos ? S.ae[c][rw - 1] : 0.0f;   // drift closing (position sweeps)
                         const float lm = lam[c * 3 + rw];
                         const float raw = lm + S.ck[c][rw] * (tgt - redg<G>(Jr[c * 3 + rw] * uv));

@@ -69,6 +69,10 @@ struct MgRigidArgs {
     float*       out_root;    // [na][13] actor root tensor
     const int*   out_body;    // [nb] internal slot -> global body (rigid-body row)
     const int*   out_root_row;// [nb] internal slot -> actor row (-1: not a root)
+    // ground friction patches of the single-shape bodies (persistent, DESIGN.md
+    // §3.2.1): SoA [MG_FP_N][gstride], slot b = internal slot b < nf1
+    float*       gpatch;
+    int          gstride;
 };
 
 // Articulation step arguments (lane = articulation instance).

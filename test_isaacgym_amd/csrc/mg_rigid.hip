@@ -464,162 +464,125 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
 }
 
 // ---- single-shape bodies: k_rigid_step1 ------------------------------------
-// Slot of the branch-free solver: an inactive slot holds r = 0, s0 = 0 and zero
-// effective masses (kn = kt1 = kt2 = 0), so every row of it computes
-// ln = max(0 + 0 (tgt - vn), 0) = 0 and applies a zero impulse; its friction
-// limit mu ln is 0. Friction and restitution are per body (one shape).
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 pk2(float a, float b) {
-    f2 r;
-    r.x = a;
-    r.y = b;
-    return r;
-}
-__device__ __forceinline__ f2 bc2(float a) { return pk2(a, a); }
-__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-
-struct Slot1 {
-    V3 r;
-    float s0, kn, kt1, kt2, ln, lt1, lt2, vn0;
-    // Iw (r x n), Iw (r x t1), Iw (r x t2) as register pairs (x, y) + z; InZ
-    // pairs In.z with 1/m (tgs_z's Z = (w.z, v.z) update)
-    f2 InW, InZ, I1W, I2W;
-    float I1z, I2z;
+// Friction is PhysX's patch friction, as in the coupled
+// step (§3.6.1): the body-ground pair's contacts form one patch whose friction
+// acts at up to two anchors, each fixed on the body (body frame) and on the
+// ground (world point), kept from substep to substep and from step to step
+// while the body's copy stays within the correlation distance of the ground's
+// and the normal holds (cos >= MG_FP_NORMAL_COS in the body frame); anchors grow
+// from this substep's contacts in slot order and spread over the patch
+// (ground_patch_update). The record (MG_FP_N floats, the coupled record's layout) lives in
+// HBM, SoA [MG_FP_N][nf1]: field 0 (the anchor count) is written every step,
+// the rest only while anchors are held; a body that cannot touch the ground at
+// the step's start (the far skip below) does not read it — its first substep
+// has no contact, which drops any patch.
+struct GPatch {
+    int cnt;
+    V3 nA;          // patch normal in the body frame
+    V3 aA[2];       // anchor on the body (body frame)
+    V3 aB[2];       // anchor on the ground (world)
 };
-__device__ __forceinline__ V3 slot_in(const Slot1& c) { return v3(c.InW.x, c.InW.y, c.InZ.x); }
-__device__ __forceinline__ V3 slot_i1(const Slot1& c) { return v3(c.I1W.x, c.I1W.y, c.I1z); }
-__device__ __forceinline__ V3 slot_i2(const Slot1& c) { return v3(c.I2W.x, c.I2W.y, c.I2z); }
+__device__ __forceinline__ void ground_patch_update(GPatch& R, V3 x, Q4 q, V3 n0, const V3 (&p)[4],
+                                                    const float (&s0)[4], const bool (&on)[4], float fot,
+                                                    float corr) {
+    const float c2 = corr * corr;
+    int cnt = R.cnt;
+    if (cnt > 0 && vdot(qrot(q, R.nA), n0) < MG_FP_NORMAL_COS) cnt = 0;
+    GPatch N;
+    N.cnt = 0;
+    N.aA[0] = N.aA[1] = N.aB[0] = N.aB[1] = v3(0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (k < cnt) {
+            const V3 d = vsub(vadd(x, qrot(q, R.aA[k])), R.aB[k]);
+            if (vdot(d, d) <= c2) {
+                if (N.cnt == 0) { N.aA[0] = R.aA[k]; N.aB[0] = R.aB[k]; }
+                else { N.aA[1] = R.aA[k]; N.aB[1] = R.aB[k]; }
+                N.cnt = N.cnt + 1;
+            }
+        }
+    }
+    // growth (PhysX growPatches): a patch still holding two anchors keeps them;
+    // otherwise contacts within the friction offset threshold, in slot order,
+    // give anchor 0, then anchor 1 (the first farther than the correlation
+    // distance from anchor 0), then each later one replaces the anchor it is
+    // nearer to when it lies farther from the other than the two are apart —
+    // the anchors spread over the contact patch (a box's bottom face: a
+    // diagonal, so friction along either axis exerts no yaw torque)
+    const int kept = N.cnt;   // anchors kept from the last substep
+    const bool grow = N.cnt < 2;
+    V3 w0 = N.cnt > 0 ? vadd(x, qrot(q, N.aA[0])) : v3(0.0f, 0.0f, 0.0f), w1 = v3(0.0f, 0.0f, 0.0f);
+    float dd = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (grow && on[j] && s0[j] <= fot) {
+            const V3 pj = p[j];
+            int put = -1;
+            if (N.cnt == 0) {
+                put = 0;
+            } else if (N.cnt == 1) {
+                const V3 d = vsub(pj, w0);
+                const float d2 = vdot(d, d);
+                if (d2 > c2) { put = 1; dd = d2; }
+            } else {
+                const V3 e0 = vsub(pj, w0), e1 = vsub(pj, w1);
+                const float d0 = vdot(e0, e0), d1 = vdot(e1, e1);
+                if (d0 > d1) {
+                    if (d0 > dd) { put = 1; dd = d0; }
+                } else if (d1 > dd) {
+                    put = 0;
+                    dd = d1;
+                }
+            }
+            if (put >= 0) {
+                const V3 la = qrot_inv(q, vsub(pj, x));
+                if (put == 0) { N.aA[0] = la; N.aB[0] = pj; w0 = pj; }
+                else { N.aA[1] = la; N.aB[1] = pj; w1 = pj; }
+                if (N.cnt <= put) N.cnt = put + 1;
+            }
+        }
+    }
+    // the patch normal is the one the patch was created with while it keeps an
+    // anchor (a slowly tilting contact still drops it past MG_FP_NORMAL_COS)
+    N.nA = kept > 0 ? R.nA : qrot_inv(q, n0);
+    R = N;
+}
+
+// Normal row of the branch-free solver: an inactive slot holds r = 0, s0 = 0
+// and kn = 0, so it computes ln = max(0 + 0 (tgt - vn), 0) = 0 and applies a
+// zero impulse. Anchor rows likewise (k = 0, r = 0: raw 0 within any bound).
+struct NRow {
+    V3 r, In;                 // contact point - COM; Iw (r x n)
+    float s0, kn, ln, vn0;
+};
+struct ARow {
+    V3 r, I1, I2;             // anchor (body copy) - COM; Iw (r x t1), Iw (r x t2)
+    float k1, k2, l1, l2;     // effective masses, accumulated impulses along t1, t2
+    float e1, e2;             // position-sweep target velocities (drift closing)
+};
 
 template <class B>
-__device__ __forceinline__ void row_normal1(const B& G, Slot1& c, V3& v, V3& w, float invm, float tgt) {
+__device__ __forceinline__ void row_normal1(const B& G, NRow& c, V3& v, V3& w, float invm, float tgt) {
     const float vn = G.vn(v, w, c.r);
     const float nl = fmaxf(fmaf(c.kn, tgt - vn, c.ln), 0.0f);
     const float dl = nl - c.ln;
     c.ln = nl;
     v = G.fn(v, dl, invm);
-    w = fmad3(w, slot_in(c), dl);
-}
-
-template <class B>
-__device__ __forceinline__ void row_friction1(const B& G, Slot1& c, V3& v, V3& w, float invm, float mu) {
-    const float lim = mu * c.ln;
-    const float n1 = clamp_sym(fmaf(-c.kt1, G.v1(v, w, c.r), c.lt1), lim);
-    const float d1 = n1 - c.lt1;
-    c.lt1 = n1;
-    v = G.f1(v, d1, invm);
-    w = fmad3(w, slot_i1(c), d1);
-    const float n2 = clamp_sym(fmaf(-c.kt2, G.v2(v, w, c.r), c.lt2), lim);
-    const float d2 = n2 - c.lt2;
-    c.lt2 = n2;
-    v = G.f2(v, d2, invm);
-    w = fmad3(w, slot_i2(c), d2);
-}
-
-// ---- +Z ground: the solver on packed f32 pairs -------------------------------
-// The same rows as row_normal1 / row_friction1 with BasisZ, but the velocity
-// state lives in register pairs W = (w.x, w.y), Z = (w.z, v.z), V = (v.x, v.y)
-// (and the motion delta in DW = (dth.x, dth.y), DZ = (dth.z, dx.z), DV = (dx.x,
-// dx.y)), so one v_pk_fma_f32 applies two of a row's impulse updates, and the
-// separations of two slots are evaluated by one packed instruction chain. Every
-// component is the same correctly rounded fma / add / mul as the scalar form
-// (a packed op is two independent IEEE ops), so the result is bit-identical to
-// row_normal1 / row_friction1 and to the oracle; only the issue count drops
-// (large launches are VALU-issue bound: DESIGN.md §3.2).
-
-__device__ __forceinline__ void tgs_z(const MgStep& P, Slot1 (&sl)[4], V3& v, V3& w, V3& dx, V3& dth, float invm,
-                                      float mu, float e) {
-    f2 W = pk2(w.x, w.y), Z = pk2(w.z, v.z), V = pk2(v.x, v.y);
-    f2 DW = pk2(dth.x, dth.y), DZ = pk2(dth.z, dx.z), DV = pk2(dx.x, dx.y);
-    f2 S0[2], RY[2], NRX[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        S0[h] = pk2(sl[2 * h].s0, sl[2 * h + 1].s0);
-        RY[h] = pk2(sl[2 * h].r.y, sl[2 * h + 1].r.y);
-        NRX[h] = pk2(-sl[2 * h].r.x, -sl[2 * h + 1].r.x);
-    }
-    // separations of slots (2h, 2h+1): s0 + dx.z + dth.x r.y - dth.y r.x (BasisZ::ps)
-    auto sep = [&](int h) {
-        f2 a = S0[h] + bc2(DZ.y);
-        a = pfma(bc2(DW.x), RY[h], a);
-        return pfma(bc2(DW.y), NRX[h], a);
-    };
-    auto normal = [&](int j, float tgt) {
-        const float nrx = (j & 1) ? NRX[j >> 1].y : NRX[j >> 1].x;
-        const float ry = (j & 1) ? RY[j >> 1].y : RY[j >> 1].x;
-        const float vn = fmaf(W.y, nrx, fmaf(W.x, ry, Z.y));
-        const float nl = fmaxf(fmaf(sl[j].kn, tgt - vn, sl[j].ln), 0.0f);
-        const float dl = nl - sl[j].ln;
-        sl[j].ln = nl;
-        W = pfma(sl[j].InW, bc2(dl), W);
-        Z = pfma(sl[j].InZ, bc2(dl), Z);
-    };
-    auto friction = [&](int j) {
-        const float rx = sl[j].r.x, ry = sl[j].r.y, nrz = -sl[j].r.z;
-        const float lim = mu * sl[j].ln;
-        const float n1 = clamp_sym(fmaf(-sl[j].kt1, fmaf(Z.x, rx, fmaf(W.x, nrz, V.y)), sl[j].lt1), lim);
-        const float d1 = n1 - sl[j].lt1;
-        sl[j].lt1 = n1;
-        V.y = fmaf(d1, invm, V.y);
-        W = pfma(sl[j].I1W, bc2(d1), W);
-        Z.x = fmaf(sl[j].I1z, d1, Z.x);
-        const float n2 = clamp_sym(fmaf(-sl[j].kt2, fmaf(Z.x, ry, fmaf(W.y, nrz, -V.x)), sl[j].lt2), lim);
-        const float d2 = n2 - sl[j].lt2;
-        sl[j].lt2 = n2;
-        V.x = fmaf(-d2, invm, V.x);
-        W = pfma(sl[j].I2W, bc2(d2), W);
-        Z.x = fmaf(sl[j].I2z, d2, Z.x);
-    };
-    const f2 nsub = bc2(-P.inv_sub), psub = bc2(P.sub);
-    auto pos_iter = [&]() {
-        const f2 t0 = sep(0) * nsub, t1 = sep(1) * nsub;   // -s / sub of each slot
-        normal(0, fminf(t0.x, P.max_depen));
-        normal(1, fminf(t0.y, P.max_depen));
-        normal(2, fminf(t1.x, P.max_depen));
-        normal(3, fminf(t1.y, P.max_depen));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) friction(j);
-        DV = pfma(V, psub, DV);
-        DW = pfma(W, psub, DW);
-        DZ = pfma(Z, psub, DZ);
-    };
-    int it = 0;
-    for (; it + 1 < P.npos; it += 2) {
-        pos_iter();
-        pos_iter();
-    }
-    if (it < P.npos) pos_iter();
-    if (P.nvel > 0) {
-        const f2 s01 = sep(0), s23 = sep(1);
-        const float sj[4] = {s01.x, s01.y, s23.x, s23.y};
-        float tg[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) tg[j] = vel_target(P, sj[j], e, sl[j].vn0);
-        for (int it = 0; it < P.nvel; ++it) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) normal(j, tg[j]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) friction(j);
-        }
-    }
-    v = v3(V.x, V.y, Z.y);
-    w = v3(W.x, W.y, Z.x);
-    dx = v3(DV.x, DV.y, DZ.y);
-    dth = v3(DW.x, DW.y, DZ.x);
+    w = fmad3(w, c.In, dl);
 }
 
 // T: this body's compact template record (MG_TREC_N floats: MG_TBODY_F_N
 // template floats, then the shape record; shape type < 0 when it has none).
+// R: the ground patch at the step's start (cnt 0: none), at its end on return.
 template <bool PACK, class B>
 __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const float* T, V3& x, Q4& q, V3& v,
                                             V3& w, V3& fsum, float invm, V3 invI, Q4 iq, V3 com, bool has_ext,
-                                            V3 fext, V3 text, const float* hulls) {
+                                            V3 fext, V3 text, const float* hulls, float* gp, int gstride) {
     const float lin_damp = T[0], ang_damp = T[1], max_lv = T[2], max_av = T[3], grav_on = T[4];
-    // the shape record in registers: read from LDS once (one wait), not per substep
-    float sh[MG_SHAPE_STRIDE];
-#pragma unroll
-    for (int k = 0; k < 14; ++k) sh[k] = T[MG_TBODY_F_N + k];
-#pragma unroll
-    for (int k = 14; k < MG_SHAPE_STRIDE; ++k) sh[k] = 0.0f;
+    // the shape record stays in the template record (LDS when staged) and is
+    // read by each substep's candidate search: registers are scarcer than LDS
+    // reads at three waves per SIMD
+    const float* sh = T + MG_TBODY_F_N;
     const bool has_shape = P.has_ground && sh[0] >= 0.0f;
     const float rho = sh[13];   // bounding radius about the body origin (< 0: none)
     const float h = P.h;
@@ -629,6 +592,29 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
     const float max_av2 = max_av * max_av;
     const float mu = 0.5f * (sh[11] + P.mu_ground);
     const float e = 0.5f * (sh[12] + P.e_ground);
+    const V3 n0 = v3(P.n[0], P.n[1], P.n[2]);
+    // the ground patch kept from the last step: read only by a body that can
+    // touch the ground at this step's start (otherwise its first substep has no
+    // contact and drops the patch, whatever the record holds)
+    GPatch R;
+    R.cnt = 0;
+    R.nA = R.aA[0] = R.aA[1] = R.aB[0] = R.aB[1] = v3(0.0f, 0.0f, 0.0f);
+    {
+        const float clear = G.dn(x) + P.pd;
+        const bool far = rho >= 0.0f && clear - rho > P.contact_offset + 1e-3f * (1.0f + fabsf(clear) + rho);
+        if (gp && has_shape && !far) {
+            float r[MG_FP_N];
+#pragma unroll
+            for (int k = 0; k < MG_FP_N; ++k) r[k] = gp[(size_t)k * gstride];
+            R.cnt = (int)r[0];
+            R.nA = v3(r[1], r[2], r[3]);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                R.aA[k] = v3(r[4 + 6 * k], r[5 + 6 * k], r[6 + 6 * k]);
+                R.aB[k] = v3(r[7 + 6 * k], r[8 + 6 * k], r[9 + 6 * k]);
+            }
+        }
+    }
 
     q = qnormalize(q);
     for (int st = 0; st < P.substeps; ++st) {
@@ -651,13 +637,15 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
         }
 
         // 2. ground contacts: candidate k of the shape -> slot k
-        Slot1 sl[4];
+        NRow sl[4];
         bool on[4];
+        V3 cp[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             on[j] = false;
             sl[j].r = v3(0.0f, 0.0f, 0.0f);
             sl[j].s0 = 0.0f;
+            cp[j] = v3(0.0f, 0.0f, 0.0f);
         }
         // a body clearing the plane by more than its bounding radius (plus a
         // rounding margin far above the candidates' own error) has no candidate
@@ -670,66 +658,116 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
                     on[k] = true;
                     sl[k].r = vsub(p, xc);
                     sl[k].s0 = sep - P.rest_offset;
+                    cp[k] = p;
                 }
             });
         bool any = false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) any = any || on[j];
+        // the friction patch of this substep (no contact: none)
+        if (any) {
+            float cs0[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cs0[j] = sl[j].s0;
+            ground_patch_update(R, x, q, n0, cp, cs0, on, P.fric_offset, P.fric_corr);
+        } else {
+            R.cnt = 0;
+        }
 
         // 3. TGS (skipped by a wave in which no body touches the ground)
         V3 dx = v3(0.0f, 0.0f, 0.0f), dth = v3(0.0f, 0.0f, 0.0f);
         if (__any(any)) {
-            // contact constants (inactive slots: r = 0, so In = I1 = I2 = 0, k = 0)
+            // contact constants (inactive slots: r = 0, so In = 0, kn = 0)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const V3 In = G.iwn(Iw, sl[j].r), I1 = G.iw1(Iw, sl[j].r), I2 = G.iw2(Iw, sl[j].r);
-                sl[j].InW = pk2(In.x, In.y);
-                sl[j].InZ = pk2(In.z, invm);
-                sl[j].I1W = pk2(I1.x, I1.y);
-                sl[j].I2W = pk2(I2.x, I2.y);
-                sl[j].I1z = I1.z;
-                sl[j].I2z = I2.z;
-                sl[j].kn = on[j] ? 1.0f / (invm + G.kn(sl[j].r, In)) : 0.0f;
-                sl[j].kt1 = on[j] ? 1.0f / (invm + G.k1(sl[j].r, I1)) : 0.0f;
-                sl[j].kt2 = on[j] ? 1.0f / (invm + G.k2(sl[j].r, I2)) : 0.0f;
-                sl[j].ln = 0.0f; sl[j].lt1 = 0.0f; sl[j].lt2 = 0.0f;
+                sl[j].In = G.iwn(Iw, sl[j].r);
+                sl[j].kn = on[j] ? 1.0f / (invm + G.kn(sl[j].r, sl[j].In)) : 0.0f;
+                sl[j].ln = 0.0f;
                 sl[j].vn0 = G.vn(v, w, sl[j].r);
             }
-            if constexpr (B::kPacked && PACK) {
-                tgs_z(P, sl, v, w, dx, dth, invm, mu, e);
-            } else {
-                auto pos_iter = [&]() {
+            // anchor rows at the anchors' body copies; the position sweeps close
+            // 80 % of the substep-start drift of their two copies
+            ARow an[2];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        row_normal1(G, sl[j], v, w, invm, pos_target(P, G.ps(sl[j].s0, dx, dth, sl[j].r)));
+            for (int a = 0; a < 2; ++a) {
+                const bool act = a < R.cnt;
+                V3 r = v3(0.0f, 0.0f, 0.0f);
+                float e1 = 0.0f, e2 = 0.0f;
+                if (act) {
+                    const V3 wa = vadd(x, qrot(q, R.aA[a]));
+                    const V3 dr = vsub(wa, R.aB[a]);
+                    const float kd = 0.8f * P.inv_h;
+                    r = vsub(wa, xc);
+                    e1 = fminf(fmaxf(-G.d1(dr) * kd, -P.max_depen), P.max_depen);
+                    e2 = fminf(fmaxf(-G.d2(dr) * kd, -P.max_depen), P.max_depen);
+                }
+                an[a].r = r;
+                an[a].I1 = G.iw1(Iw, r);
+                an[a].I2 = G.iw2(Iw, r);
+                an[a].k1 = act ? 1.0f / (invm + G.k1(r, an[a].I1)) : 0.0f;
+                an[a].k2 = act ? 1.0f / (invm + G.k2(r, an[a].I2)) : 0.0f;
+                an[a].l1 = 0.0f;
+                an[a].l2 = 0.0f;
+                an[a].e1 = e1;
+                an[a].e2 = e2;
+            }
+            bool slip = false;
+            // each anchor of a two-anchor patch holds half of the patch's Coulomb
+            // budget mu N per direction: symmetric (a box sliding on its diagonal
+            // anchors exerts no yaw torque), and the two saturate at mu N together
+            const float share = R.cnt == 2 ? 0.5f : 1.0f;
+            const int nit = P.npos + P.nvel;
+            for (int it = 0; it < nit; ++it) {
+                const bool pos = it < P.npos, last = it == nit - 1;
+                auto normals = [&]() {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) row_friction1(G, sl[j], v, w, invm, mu);
+                    for (int j = 0; j < 4; ++j) {
+                        const float sj = G.ps(sl[j].s0, dx, dth, sl[j].r);
+                        row_normal1(G, sl[j], v, w, invm, pos ? pos_target(P, sj) : vel_target(P, sj, e, sl[j].vn0));
+                    }
+                };
+                normals();
+                // the patch's normal impulse (slot order)
+                const float mun = mu * (((sl[0].ln + sl[1].ln) + sl[2].ln) + sl[3].ln);
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    {
+                        const float lim = share * mun;
+                        const float raw = fmaf(an[a].k1, (pos ? an[a].e1 : 0.0f) - G.v1(v, w, an[a].r), an[a].l1);
+                        const float nl = clamp_sym(raw, lim);
+                        const float dl = nl - an[a].l1;
+                        slip = slip || (last && (raw > lim || raw < -lim));
+                        an[a].l1 = nl;
+                        v = G.f1(v, dl, invm);
+                        w = fmad3(w, an[a].I1, dl);
+                    }
+                    {
+                        const float lim = share * mun;
+                        const float raw = fmaf(an[a].k2, (pos ? an[a].e2 : 0.0f) - G.v2(v, w, an[a].r), an[a].l2);
+                        const float nl = clamp_sym(raw, lim);
+                        const float dl = nl - an[a].l2;
+                        slip = slip || (last && (raw > lim || raw < -lim));
+                        an[a].l2 = nl;
+                        v = G.f2(v, dl, invm);
+                        w = fmad3(w, an[a].I2, dl);
+                    }
+                }
+                // the last position sweep and the velocity sweeps end with the
+                // normal rows again (the coupled step's order)
+                if (it >= P.npos - 1) normals();
+                if (pos) {
                     dx = fmad3(dx, v, P.sub);
                     dth = fmad3(dth, w, P.sub);
-                };
-                // two iterations per trip: the accumulated impulses alternate between
-                // two register sets instead of being copied back every iteration
-                int it = 0;
-                for (; it + 1 < P.npos; it += 2) {
-                    pos_iter();
-                    pos_iter();
-                }
-                if (it < P.npos) pos_iter();
-                for (int it = 0; it < P.nvel; ++it) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        row_normal1(G, sl[j], v, w, invm,
-                                    vel_target(P, G.ps(sl[j].s0, dx, dth, sl[j].r), e, sl[j].vn0));
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) row_friction1(G, sl[j], v, w, invm, mu);
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                fsum = G.addn(fsum, sl[j].ln);
-                fsum = G.add1(fsum, sl[j].lt1);
-                fsum = G.add2(fsum, sl[j].lt2);
+            for (int j = 0; j < 4; ++j) fsum = G.addn(fsum, sl[j].ln);
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                fsum = G.add1(fsum, an[a].l1);
+                fsum = G.add2(fsum, an[a].l2);
             }
+            if (slip) R.cnt = 0;   // a slipping patch lets go (regrown at the next substep)
         } else {
             // no solver pass: the motion delta is the substep's free flight
             for (int it = 0; it < P.npos; ++it) {
@@ -742,6 +780,17 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
         const V3 xc1 = vadd(xc, dx);
         q = qintegrate(q, dth);
         x = origin_from_com(xc1, q, com);
+    }
+    // the patch for the next step: the anchor count always, the anchors while held
+    if (gp && has_shape) {
+        gp[0] = (float)R.cnt;
+        if (R.cnt > 0) {
+            const float r[MG_FP_N] = {0.0f, R.nA.x, R.nA.y, R.nA.z,
+                                      R.aA[0].x, R.aA[0].y, R.aA[0].z, R.aB[0].x, R.aB[0].y, R.aB[0].z,
+                                      R.aA[1].x, R.aA[1].y, R.aA[1].z, R.aB[1].x, R.aB[1].y, R.aB[1].z};
+#pragma unroll
+            for (int k = 1; k < MG_FP_N; ++k) gp[(size_t)k * gstride] = r[k];
+        }
     }
 }
 
@@ -811,14 +860,19 @@ k_rigid_step1(MgStep P, MgRigidArgs A) {
     const Q4 iq = q4(mr[4], mr[5], mr[6], mr[7]);
     const V3 com = v3(mr[8], mr[9], mr[10]);
     V3 fsum = v3(0.0f, 0.0f, 0.0f);
+    // this body's ground-patch record (slot b of the SoA [MG_FP_N][gstride] table)
+    // and its LDS copy during the frame
+    float* gp = live && A.gpatch ? A.gpatch + b : nullptr;
     if constexpr (UPZ) {
-        rigid_body1<!WIDE>(BasisZ{}, P, T, x, q, v, w, fsum, invm, invI, iq, com, A.ext != nullptr, fext, text, A.hulls);
+        rigid_body1<!WIDE>(BasisZ{}, P, T, x, q, v, w, fsum, invm, invI, iq, com, A.ext != nullptr, fext, text, A.hulls,
+                           gp, A.gstride);
     } else {
         BasisGen G;
         G.n = v3(P.n[0], P.n[1], P.n[2]);
         G.t1 = v3(P.t1[0], P.t1[1], P.t1[2]);
         G.t2 = v3(P.t2[0], P.t2[1], P.t2[2]);
-        rigid_body1<!WIDE>(G, P, T, x, q, v, w, fsum, invm, invI, iq, com, A.ext != nullptr, fext, text, A.hulls);
+        rigid_body1<!WIDE>(G, P, T, x, q, v, w, fsum, invm, invI, iq, com, A.ext != nullptr, fext, text, A.hulls, gp,
+                           A.gstride);
     }
     // the output addresses are recomputed here (an opaque copy of the slot)
     // rather than kept live in registers across the frame
@@ -926,6 +980,7 @@ hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream
     A2.root_src = nullptr;   // fused root sets only with single-shape bodies (migym_capi.cpp)
     A2.out_rb = nullptr;     // so is the fused refresh (MG_FUSE_STEP_OUT)
     A2.out_root = nullptr;
+    A2.gpatch = nullptr;     // ground patches: single-shape bodies (multi-shape ones keep per-point rows)
     A1.nf = A.nf1;
     A2.nf = A.nf - A.nf1;
     if (A.free_ids) {

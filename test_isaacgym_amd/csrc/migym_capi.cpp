@@ -148,6 +148,7 @@ struct mg_sim {
     int* d_env = nullptr;         // [n_coupled][MG_ENV_I_N] coupled envs, by group
     int* d_pairs = nullptr;       // [..][4] candidate shape pairs of the coupled envs
     float* d_fpatch = nullptr;    // [pairs][MG_FP_N] friction patch records (coupled step, persistent)
+    float* d_gpatch = nullptr;    // [MG_FP_N][nf1] ground patches of the single-shape free bodies (persistent)
     unsigned* d_fp_mask = nullptr;   // [n_coupled][MG_FP_W] pairs holding a patch
     int n_coupled = 0;
     std::vector<EnvGroup> env_groups;
@@ -365,7 +366,7 @@ void shape_obb(const float* sh, const float* hulls, float* o) {
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls, s->d_shape_obb,
                     s->d_actor_root, s->d_root_row, s->d_slot_global, s->d_slot_actor, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
-                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_fp_mask, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
+                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_fp_mask, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
                     s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -975,6 +976,9 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         HIP_TRY(dalloc(&s->d_fp_mask, nm));
         HIP_TRY(hipMemset(s->d_fpatch, 0, np * MG_FP_N * sizeof(float)));
         HIP_TRY(hipMemset(s->d_fp_mask, 0, nm * sizeof(unsigned)));
+        const size_t ng = (size_t)std::max(s->nf1, 1) * MG_FP_N;   // no ground patch yet
+        HIP_TRY(dalloc(&s->d_gpatch, ng));
+        HIP_TRY(hipMemset(s->d_gpatch, 0, ng * sizeof(float)));
     }
     HIP_TRY(h2d(s->d_link_f, m->tmpl_link_f, (size_t)s->ntl * MG_LINK_F_N * sizeof(float)));
     HIP_TRY(h2d(s->d_link_i, m->tmpl_link_i, (size_t)s->ntl * MG_LINK_I_N * sizeof(int)));
@@ -1098,6 +1102,8 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
         A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes; A.hulls = s->d_hulls;
         A.trec = s->d_trec; A.ntb = s->ntb;
+        A.gpatch = s->d_gpatch;
+        A.gstride = std::max(s->nf1, 1);
         A.ext = s->ext_pending ? s->d_ext : nullptr;
         A.cforce = s->d_cforce;
         if (s->pend_root) {   // the deferred root set, read by the step kernel

@@ -104,27 +104,6 @@ def _check_held(sim, what, kinds=None):
     sim.held_src = keep
 
 
-_PHYSX_DEFAULTS = _T.PhysXParams()
-_warned_physx = set()
-
-
-def _warn_unmodelled_physx(params):
-    """PhysX patch-friction parameters (examples/franka_cube_ik_osc.py:124-125
-    sets both) drive the friction anchors of the coupled per-env step (bodies
-    touching other bodies or an articulation); a free body
-    stepping alone against the ground plane keeps one friction anchor per
-    contact point, where they have no effect. Said once per parameter and
-    value, on stderr — never dropped silently."""
-    px = params.physx
-    for name in ("friction_offset_threshold", "friction_correlation_distance"):
-        val = float(getattr(px, name))
-        if val != float(getattr(_PHYSX_DEFAULTS, name)) and (name, val) not in _warned_physx:
-            _warned_physx.add((name, val))
-            print("*** migym: physx.%s = %g drives the friction anchors of coupled envs only; free bodies "
-                  "alone on the ground plane keep per-point friction (DESIGN.md §3.6.1)" % (name, val),
-                  file=sys.stderr)
-
-
 class Gym:
     def __init__(self):
         self._sims = []
@@ -138,7 +117,6 @@ class Gym:
         if type != _T.SIM_PHYSX:
             print("*** migym: only the PhysX-style rigid solver is available (SIM_FLEX requested)", file=sys.stderr)
             return None
-        _warn_unmodelled_physx(params)
         sim = Sim(compute_device, graphics_device, type, params)
         self._sims.append(sim)
         return sim
@@ -153,7 +131,6 @@ class Gym:
         return sim.params
 
     def set_sim_params(self, sim, params):
-        _warn_unmodelled_physx(params)
         sim.params = params
         if sim.native:
             N.check(N.lib.mg_set_sim_params(sim.native, ctypes.byref(sim.mg_params())), "mg_set_sim_params")

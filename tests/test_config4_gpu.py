@@ -57,27 +57,30 @@ def test_config4_sharded_equals_single_sim(tmp_path):
 
 
 def test_config4_single_sim_step_matches_oracle():
-    """32768 envs (65536 bodies, 1024 waves of k_rigid_step1): 3 frames from the
-    initial state, then every step compared with oracle.step on the device's own
-    input state, bit for bit."""
+    """32768 envs (65536 bodies, 1024 waves of k_rigid_step1): 5 frames of
+    random teleports from the initial state, the oracle stepping alongside (its
+    ground patches kept from step to step like the device's), bit for bit every
+    frame — state and net contact force."""
     gym = gymapi.acquire_gym()
     n = WORLD * ENVS_PER_RANK
-    sim, root, rb = _single_sim(gym, n, 3)
+    sim, root, rb = _single_sim(gym, n, 0)
     ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))
-    acts = scenes.servo_actions(n, 2, "cuda:0", seed=12)
+    acts = scenes.servo_actions(n, 5, "cuda:0", seed=12)
     p, m = sim.mg_params(), sim.mg_model()
-    for k in range(2):
+    cc = oracle.contact_cache(m)
+    st = sim.model_arrays["body_state0"].copy()
+    roots = sim.model_arrays["actor_root_body"]
+    for k in range(5):
         root[:, 3:10] = acts[k]
         assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
-        gym.refresh_rigid_body_state_tensor(sim)
-        inp = rb.cpu().numpy().copy()
         gym.simulate(sim)
         gym.fetch_results(sim, True)
         gym.refresh_rigid_body_state_tensor(sim)
         gym.refresh_net_contact_force_tensor(sim)
         gym.refresh_actor_root_state_tensor(sim)
+        st[roots, 3:10] = acts[k].cpu().numpy()
+        cf = oracle.step(p, m, st, np.zeros((0, 2), np.float32), contact_cache=cc)
         got = rb.cpu().numpy()
-        cf = oracle.step(p, m, inp, np.zeros((0, 2), np.float32))
-        assert np.array_equal(got, inp), "step %d: max |diff| %g" % (k, np.abs(got - inp).max())
-        assert np.array_equal(ncf.cpu().numpy(), cf)
+        assert np.array_equal(got, st), "frame %d: max |diff| %g" % (k, np.abs(got - st).max())
+        assert np.array_equal(ncf.cpu().numpy(), cf), "frame %d: contact force" % k
     gym.destroy_sim(sim)

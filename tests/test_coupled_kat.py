@@ -170,6 +170,7 @@ def _cube_on_table(gym, corr=None):
 def _patch(fc, pair=None):
     """(anchor count, held, record floats) of an env-0 pair in an oracle cache
     (default: the one pair holding a patch — the cube on the table)"""
+    fc = fc.env
     if pair is None:
         held = [i for i in range(128) if fc[0, i * 17 + 16] != 0.0]
         assert len(held) == 1, held

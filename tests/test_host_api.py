@@ -215,14 +215,33 @@ def test_set_actor_dof_states_keeps_unselected_column(gym):
     assert np.allclose(gym.get_actor_dof_states(envs[0], 0, gymapi.STATE_ALL)["vel"], 0.0)
 
 
-def test_friction_parameters_scope_is_stated(gym, capsys):
-    """franka_cube_ik_osc.py:124-125's patch-friction parameters drive the
-    coupled step's friction anchors but not the lone free-body
-    kernel; create_sim says so on stderr instead of dropping them silently."""
+def test_friction_parameters_scope_is_stated(gym, capsys, tmp_path):
+    """physx.friction_offset_threshold / friction_correlation_distance
+    (franka_cube_ik_osc.py:124-125; test10 leaves them at Isaac Gym's defaults)
+    drive the friction anchors of single-shape free bodies on the ground and of
+    the coupled step: no notice for such scenes. A
+    free body of several collision shapes alone on the ground keeps per-point
+    friction, and the first sim holding one says so on stderr."""
+    from test_isaacgym_amd import _sim as S
+    S._warned_multishape[0] = False
     sp = scenes.franka_sim_params(False)
     sp.physx.friction_offset_threshold = 0.0011
     sp.physx.friction_correlation_distance = 0.00051
-    assert gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp) is not None
-    err = capsys.readouterr().err
-    assert "friction_offset_threshold = 0.0011 drives the friction anchors of coupled envs only" in err
-    assert "friction_correlation_distance = 0.00051 drives the friction anchors of coupled envs only" in err
+    sim, _ = scenes.servo_scene(gym, 4, use_gpu_pipeline=False)
+    sim.finalize()
+    assert "per-point friction" not in capsys.readouterr().err
+    urdf = tmp_path / "two_boxes.urdf"
+    urdf.write_text('<robot name="two"><link name="l"><inertial><mass value="1"/>'
+                    '<inertia ixx="0.1" iyy="0.1" izz="0.1" ixy="0" ixz="0" iyz="0"/></inertial>'
+                    '<collision><origin xyz="0.2 0 0"/><geometry><box size="0.2 0.2 0.2"/></geometry></collision>'
+                    '<collision><origin xyz="-0.2 0 0"/><geometry><box size="0.2 0.2 0.2"/></geometry></collision>'
+                    '</link></robot>')
+    sim2 = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim2, plane)
+    asset = gym.load_asset(sim2, str(tmp_path), "two_boxes.urdf", gymapi.AssetOptions())
+    env = gym.create_env(sim2, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 1)
+    gym.create_actor(env, asset, gymapi.Transform(gymapi.Vec3(0, 0, 0.5)), "two", 0, 0)
+    sim2.finalize()
+    assert "free bodies with several collision shapes keep per-point friction" in capsys.readouterr().err

@@ -44,6 +44,7 @@ def test_servo_single_step_parity(gym):
     root, rb, _, ncf = _tensors(gym, sim)
     acts = scenes.servo_actions(n, steps, DEV, seed=1)
     p, m = sim.mg_params(), sim.mg_model()
+    cc = oracle.contact_cache(m)      # the ground patches persist from step to step, as on the device
     gym.refresh_actor_root_state_tensor(sim)
     worst = 0.0
     exact = True
@@ -58,7 +59,7 @@ def test_servo_single_step_parity(gym):
         gym.refresh_net_contact_force_tensor(sim)
         gym.refresh_actor_root_state_tensor(sim)
         got = rb.cpu().numpy()
-        cf = oracle.step(p, m, inp, np.zeros((0, 2), np.float32))
+        cf = oracle.step(p, m, inp, np.zeros((0, 2), np.float32), contact_cache=cc)
         assert np.all(_close(got, inp)), "step %d: max |diff| %g" % (k, np.abs(got - inp).max())
         assert np.all(_close(ncf.cpu().numpy(), cf))
         worst = max(worst, float(np.abs(got - inp).max()))
@@ -76,6 +77,7 @@ def test_servo_large_launch_step_parity(gym):
     root, rb, _, ncf = _tensors(gym, sim)
     acts = scenes.servo_actions(n, steps, DEV, seed=3)
     p, m = sim.mg_params(), sim.mg_model()
+    cc = oracle.contact_cache(m)
     gym.refresh_actor_root_state_tensor(sim)
     for k in range(steps):
         root[:, 3:10] = acts[k]
@@ -87,7 +89,7 @@ def test_servo_large_launch_step_parity(gym):
         gym.refresh_rigid_body_state_tensor(sim)
         gym.refresh_net_contact_force_tensor(sim)
         got = rb.cpu().numpy()
-        cf = oracle.step(p, m, inp, np.zeros((0, 2), np.float32))
+        cf = oracle.step(p, m, inp, np.zeros((0, 2), np.float32), contact_cache=cc)
         assert np.array_equal(got, inp), "step %d: max |diff| %g" % (k, np.abs(got - inp).max())
         assert np.array_equal(ncf.cpu().numpy(), cf)
 
