@@ -81,6 +81,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-franka", action="store_true", help="skip the secondary S3 Franka cube-pick measurement")
     ap.add_argument("--no-cameras", action="store_true", help="skip the secondary S5 camera-render measurement")
     ap.add_argument("--no-large-n", action="store_true", help="skip the 262,144-env S1 kernel leg")
+    ap.add_argument("--no-default-legs", action="store_true",
+                    help="skip the S1 library-default (fusion off) and CPU-pipeline legs")
     ap.add_argument("--pmc-calibrate", action="store_true",
                     help="before the warm-up, 4 indexed root-state sets of every actor (k_scatter_rows: the "
                          "known-volume kernel profiles/collect_pmc.py calibrates FETCH_SIZE on)")
@@ -553,21 +555,27 @@ def camera_rate(n, steps, warmup, dev, use_graph=True, width=1600, height=900):
             "env0_non_sky_fraction": lit, "sampled_cameras_non_sky_fraction": lit_all}
 
 
-def large_n_rate(n, steps, dev, use_graph=True):
-    """S1 at `n` envs on one GPU (SURVEY.md §8d's large-N regime point): the same
-    tensor-API step; k_rigid_step's own duration over KERNEL_TIMED_LAUNCHES eager
-    launches, and the graph-replayed step rate."""
+def s1_rate(n, steps, dev, use_graph=True, fused=True, seed=1, unfused_kernel=False):
+    """S1 at `n` envs on one GPU: the same tensor-API step as the headline;
+    k_rigid_step's own duration over KERNEL_TIMED_LAUNCHES eager launches and the
+    graph-replayed step rate. fused=False runs the library default (no step
+    fusion: the set is a scatter launch, the refreshes are gathers), which is
+    what an unmodified test10 gets. unfused_kernel: also time the kernel with
+    fusion off (the large-N leg's A/B)."""
     import torch
     from isaacgym import gymapi, gymtorch
     from test_isaacgym_amd import scenes
     gym = gymapi.acquire_gym()
     sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
     gym.prepare_sim(sim)
-    fuse_in_capture(sim)
+    if fused:
+        fuse_in_capture(sim)
+    else:
+        gym.set_step_fusion(sim, 0)
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     gym.acquire_rigid_body_state_tensor(sim)
     gym.acquire_dof_state_tensor(sim)
-    acts = scenes.servo_actions(n, 16, dev, seed=1)
+    acts = scenes.servo_actions(n, 16, dev, seed=seed)
 
     def step(k):
         root[:, 3:10] = acts[k % acts.shape[0]]
@@ -594,7 +602,8 @@ def large_n_rate(n, steps, dev, use_graph=True):
             graphs[(base // chunk) % len(graphs)].replay()
             base += chunk
         except Exception as ex:
-            print("*** bench: large-N hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
+            print("*** bench: S1 (%d envs) hipGraph capture failed (%s); timing the eager loop" % (n, ex),
+                  file=sys.stderr)
             graphs = None
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -606,21 +615,71 @@ def large_n_rate(n, steps, dev, use_graph=True):
             step(base + k)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    # the same kernel without the fused root-state read (mg_set_fusion 0: the set
-    # is a scatter launch and the step reads the SoA state): at this size the
-    # fused read costs the kernel the user rows' other-template halves (test10's
-    # actor rows alternate UAV / vehicle, whose waves run apart: DESIGN.md §3.2)
-    prev = gym.set_step_fusion(sim, 0)
-    ukms, ukmin, uused = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
-                                      lambda: [step(k) for k in range(KERNEL_TIMED_LAUNCHES)])
-    gym.set_step_fusion(sim, prev)
+    out = {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps, "steps": steps,
+           "step_fusion": "STEP_FUSION_ALL" if fused else "off (library default)",
+           "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graphs is not None else "eager",
+           "roofline": rigid_roofline(n, kms, kmin, used, "%d eager steps after a %d-step warm-up" % (used, warm),
+                                      step_out=fused)}
+    if unfused_kernel:
+        # the same kernel without the fused root-state read (mg_set_fusion 0: the set
+        # is a scatter launch and the step reads the SoA state): at this size the
+        # fused read costs the kernel the user rows' other-template halves (test10's
+        # actor rows alternate UAV / vehicle, whose waves run apart: DESIGN.md §3.2)
+        prev = gym.set_step_fusion(sim, 0)
+        ukms, ukmin, uused = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
+                                          lambda: [step(k) for k in range(KERNEL_TIMED_LAUNCHES)])
+        gym.set_step_fusion(sim, prev)
+        out["roofline_unfused"] = rigid_roofline(n, ukms, ukmin, uused,
+                                                 "%d eager steps with step fusion off (scatter launch, then the "
+                                                 "step kernel on the SoA state)" % uused, step_out=False)
+    gym.destroy_sim(sim)
+    return out
+
+
+def large_n_rate(n, steps, dev, use_graph=True):
+    """S1 at `n` envs (SURVEY.md §8d's large-N regime point), fused as the headline."""
+    return s1_rate(n, steps, dev, use_graph, fused=True, seed=1, unfused_kernel=True)
+
+
+def s1_cpu_pipeline_rate(n, steps, warmup):
+    """test10_servo_vecenv.py's own mode (:130 sets physx.use_gpu only; SURVEY.md
+    §0.7): use_gpu_pipeline False, so the state tensors are host tensors. One step
+    = the actions written into the host root tensor, set (H2D), simulate,
+    fetch_results(sim, True), refresh root / rigid-body / DOF (D2H), the eager
+    Python loop (host tensors cannot be captured). The physics is the same GPU
+    step; the difference to the GPU pipeline is the PCIe mirror and the sync."""
+    from isaacgym import gymapi, gymtorch
+    from test_isaacgym_amd import scenes
+    gym = gymapi.acquire_gym()
+    sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=False)
+    gym.prepare_sim(sim)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    gym.acquire_rigid_body_state_tensor(sim)
+    gym.acquire_dof_state_tensor(sim)
+    assert root.device.type == "cpu"
+    acts = scenes.servo_actions(n, 16, "cpu", seed=2)
+
+    def step(k):
+        root[:, 3:10] = acts[k % acts.shape[0]]
+        gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        gym.simulate(sim)
+        gym.fetch_results(sim, True)
+        gym.refresh_actor_root_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_dof_state_tensor(sim)
+
+    gym.refresh_actor_root_state_tensor(sim)
+    for k in range(warmup):
+        step(k)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(warmup + k)
+    el = time.perf_counter() - t0
     gym.destroy_sim(sim)
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps, "steps": steps,
-            "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graphs is not None else "eager",
-            "roofline": rigid_roofline(n, kms, kmin, used, "%d eager steps after a %d-step warm-up" % (used, warm)),
-            "roofline_unfused": rigid_roofline(n, ukms, ukmin, uused,
-                                               "%d eager steps with step fusion off (scatter launch, then the "
-                                               "step kernel on the SoA state)" % uused, step_out=False)}
+            "pipeline": "CPU (host state tensors, H2D set / D2H refresh, fetch_results(sim, True))",
+            "timed_loop": "eager Python loop (host tensors)",
+            "bytes_over_pcie_per_step": n * 2 * 13 * 4 * 3}
 
 
 # --------------------------------------------------------------------------- dry run (no GPU)
@@ -867,6 +926,9 @@ def main():
     if world == 1:
         if not args.no_large_n:
             out["large_n"] = large_n_rate(args.large_n, 64, dev, not args.eager)
+        if not args.no_default_legs:
+            out["s1_default"] = s1_rate(ENVS_PER_GPU, min(args.steps, 300), dev, not args.eager, fused=False, seed=3)
+            out["s1_cpu_pipeline"] = s1_cpu_pipeline_rate(1024, 100, 10)
         if not args.no_gimbal:
             out["s2_servo_arm"] = gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
             if not args.no_large_n:

@@ -246,7 +246,7 @@ int32_t     mg_apply_rigid_body_force(mg_sim* sim, const float* force, const flo
  * Jacobian (instances, L-1, 6, D) — link 1..L-1, rows [linear velocity of the
  * link frame origin; angular velocity] in the world frame, one column per DOF;
  * mass matrix (instances, D, D) — joint-space inertia by the composite-rigid-
- * body algorithm, joint armature not included. Floating base (D + 6 <= 16):
+ * body algorithm, joint armature not included. Floating base (D + 6 <= 32):
  * six root columns first (linear velocity of the base-link origin, then
  * angular velocity, world axes), Jacobian (instances, L, 6, D + 6) over every
  * link, mass matrix (instances, D + 6, D + 6). At the current state. */

@@ -550,7 +550,7 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
             }
             if (any) {
                 float mu = 0.0f, e = 0.0f, ak[2][2], al[2][2], ae[2][2], share;
-                int slip = 0, a;
+                int clamped[2][2] = {{0, 0}, {0, 0}}, a;
                 v3_t arr[2];
                 if (nsh == 1) {
                     const float* sh = m->shapes + (size_t)sh0 * MG_SHAPE_STRIDE;
@@ -615,7 +615,7 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                             const float raw = fmaf(ak[a][rw], tgt - vt, al[a][rw]);
                             const float nl = clamp_sym_(raw, lim);
                             const float dl = nl - al[a][rw];
-                            if (last && (raw > lim || raw < -lim)) slip = 1;
+                            clamped[a][rw] = last && (raw > lim || raw < -lim);
                             al[a][rw] = nl;
                             if (rw == 0) {
                                 v = b_f1(&B, v, dl, invm);
@@ -645,7 +645,14 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                     fsum = b_add1(&B, fsum, al[a][0]);
                     fsum = b_add2(&B, fsum, al[a][1]);
                 }
-                if (slip) R.cnt = 0;   /* a slipping patch lets go (regrown at the next substep) */
+                /* a slipping patch lets go (regrown at the next substep): every
+                 * anchor it holds clamped along one direction in the last sweep
+                 * (mg_rigid.hip) */
+                {
+                    const int one = R.cnt < 2;
+                    if ((clamped[0][0] && (clamped[1][0] || one)) || (clamped[0][1] && (clamped[1][1] || one)))
+                        R.cnt = 0;
+                }
             } else {
                 for (it = 0; it < P->npos; ++it) {
                     dx = fmad3_(dx, v, P->sub);

@@ -311,11 +311,82 @@ static void aabb_add_(v3_t* lo, v3_t* hi, v3_t v) {
     *lo = V(fminf(lo->x, v.x), fminf(lo->y, v.y), fminf(lo->z, v.z));
     *hi = V(fmaxf(hi->x, v.x), fmaxf(hi->y, v.y), fmaxf(hi->z, v.z));
 }
+/* one edge (X-local endpoints la, lb; t, M: X's centre and axes in Y's frame,
+ * ry: Y's bounding radius + margin) -> at most one candidate (mg_collide.h
+ * cvx_edge_one) */
+static void cvx_edge_one_(const cshape_t* Y, float margin, int onY, v3_t t, m3_t M, float ry, v3_t la, v3_t lb,
+                          pair_t* D, float etol) {
+    const int nf = cvx_nf_(Y);
+    int f;
+    v3_t al, ab, dc, p;
+    float t0 = 0.0f, t1 = 1.0f, tm, sv, tc;
+    al = add3(t, mv_(M, la));
+    ab = sub3(add3(t, mv_(M, lb)), al);
+    tc = fminf(fmaxf(-dot3(al, ab) / dot3(ab, ab), 0.0f), 1.0f);
+    dc = add3(al, mul3(ab, tc));
+    if (dot3(dc, dc) > ry * ry) return;
+    for (f = 0; f < nf; ++f) {
+        v3_t nl;
+        float dl, sa, sb;
+        cvx_plane_l_(Y, f, &nl, &dl);
+        sa = (dot3(nl, al) - dl) - margin;
+        sb = (dot3(nl, add3(al, ab)) - dl) - margin;
+        if (sa >= 0.0f && sb >= 0.0f) { t0 = 1.0f; t1 = 0.0f; }
+        else if (sa >= 0.0f) t0 = fmaxf(t0, sa / (sa - sb));
+        else if (sb >= 0.0f) t1 = fminf(t1, sa / (sa - sb));
+        if (!(t0 < t1)) break;
+    }
+    if (!(t0 < t1)) return;
+    tm = 0.5f * (t0 + t1);
+    if (Y->type == MG_SHAPE_BOX) {   /* near a box edge: edge-edge normal (mg_collide.h) */
+        const v3_t mm = add3(al, mul3(ab, tm));
+        const float ex = fabsf(mm.x) - Y->h.x, ey = fabsf(mm.y) - Y->h.y, ez = fabsf(mm.z) - Y->h.z;
+        int k = 0;
+        float ek = ex, e1, e2;
+        if (ey < ek) { k = 1; ek = ey; }
+        if (ez < ek) k = 2;
+        e1 = k == 0 ? ey : ex;
+        e2 = k == 2 ? ey : ez;
+        if (e1 > -etol && e2 > -etol) {   /* etol: the near-edge band (the margin but for capsules) */
+            const v3_t dk = V(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
+            const v3_t p0 = V(k == 0 ? 0.0f : (mm.x < 0.0f ? -Y->h.x : Y->h.x),
+                              k == 1 ? 0.0f : (mm.y < 0.0f ? -Y->h.y : Y->h.y),
+                              k == 2 ? 0.0f : (mm.z < 0.0f ? -Y->h.z : Y->h.z));
+            const v3_t nn = cross3(ab, dk);
+            const float l2 = dot3(nn, nn);
+            if (l2 > 1e-12f * dot3(ab, ab)) {
+                v3_t n = mul3(nn, 1.0f / sqrtf(l2));
+                v3_t r;
+                float svv;
+                if (dot3(n, p0) < 0.0f) n = mul3(n, -1.0f);
+                r = sub3(al, p0);
+                svv = dot3(n, r);
+                if (svv < margin) {
+                    const float bq = dot3(ab, dk), aq = dot3(ab, ab);
+                    const float den = aq - bq * bq;
+                    const float ts = fminf(fmaxf((bq * dot3(dk, r) - dot3(ab, r)) / den, 0.0f), 1.0f);
+                    const v3_t pp = add3(Y->c, mv_(Y->R, add3(al, mul3(ab, ts))));
+                    const v3_t nw = mv_(Y->R, n);
+                    if (onY) deep4_add_(D, svv, sub3(pp, mul3(nw, svv)), mul3(nw, -1.0f));
+                    else deep4_add_(D, svv, pp, nw);
+                }
+                return;
+            }
+        }
+    }
+    p = add3(Y->c, mv_(Y->R, add3(al, mul3(ab, tm))));
+    sv = cvx_sd_(Y, p, &f);
+    if (sv < margin) {
+        const v3_t n = cvx_normal_(Y, f);
+        if (onY) deep4_add_(D, sv, sub3(p, mul3(n, sv)), mul3(n, -1.0f));
+        else deep4_add_(D, sv, p, n);
+    }
+}
 static void cvx_edges_vs_(const cshape_t* X, const cshape_t* Y, float margin, int onY, pair_t* D, v3_t lo, v3_t hi) {
     const v3_t t = mtv_(Y->R, sub3(X->c, Y->c));
     const float rx = cvx_radius_(X) + margin, ry = cvx_radius_(Y) + margin;
     m3_t M;
-    int e, f, ne, nf;
+    int e, ne;
     if (Y->type == MG_SHAPE_BOX) {
         const v3_t dq = V(t.x - fminf(fmaxf(t.x, -Y->h.x), Y->h.x), t.y - fminf(fmaxf(t.y, -Y->h.y), Y->h.y),
                           t.z - fminf(fmaxf(t.z, -Y->h.z), Y->h.z));
@@ -332,73 +403,10 @@ static void cvx_edges_vs_(const cshape_t* X, const cshape_t* Y, float margin, in
             return;
     }
     ne = cvx_ne_(X);
-    nf = cvx_nf_(Y);
     for (e = 0; e < ne; ++e) {
         int ia, ib;
-        v3_t al, ab, dc, p;
-        float t0 = 0.0f, t1 = 1.0f, tm, sv, tc;
         cvx_edge_ids_(X, e, &ia, &ib);
-        al = add3(t, mv_(M, cvx_vertex_l_(X, ia)));
-        ab = sub3(add3(t, mv_(M, cvx_vertex_l_(X, ib))), al);
-        tc = fminf(fmaxf(-dot3(al, ab) / dot3(ab, ab), 0.0f), 1.0f);
-        dc = add3(al, mul3(ab, tc));
-        if (dot3(dc, dc) > ry * ry) continue;
-        for (f = 0; f < nf; ++f) {
-            v3_t nl;
-            float dl, sa, sb;
-            cvx_plane_l_(Y, f, &nl, &dl);
-            sa = (dot3(nl, al) - dl) - margin;
-            sb = (dot3(nl, add3(al, ab)) - dl) - margin;
-            if (sa >= 0.0f && sb >= 0.0f) { t0 = 1.0f; t1 = 0.0f; }
-            else if (sa >= 0.0f) t0 = fmaxf(t0, sa / (sa - sb));
-            else if (sb >= 0.0f) t1 = fminf(t1, sa / (sa - sb));
-            if (!(t0 < t1)) break;
-        }
-        if (!(t0 < t1)) continue;
-        tm = 0.5f * (t0 + t1);
-        if (Y->type == MG_SHAPE_BOX) {   /* near a box edge: edge-edge normal (mg_collide.h) */
-            const v3_t mm = add3(al, mul3(ab, tm));
-            const float ex = fabsf(mm.x) - Y->h.x, ey = fabsf(mm.y) - Y->h.y, ez = fabsf(mm.z) - Y->h.z;
-            int k = 0;
-            float ek = ex, e1, e2;
-            if (ey < ek) { k = 1; ek = ey; }
-            if (ez < ek) k = 2;
-            e1 = k == 0 ? ey : ex;
-            e2 = k == 2 ? ey : ez;
-            if (e1 > -margin && e2 > -margin) {
-                const v3_t dk = V(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
-                const v3_t p0 = V(k == 0 ? 0.0f : (mm.x < 0.0f ? -Y->h.x : Y->h.x),
-                                  k == 1 ? 0.0f : (mm.y < 0.0f ? -Y->h.y : Y->h.y),
-                                  k == 2 ? 0.0f : (mm.z < 0.0f ? -Y->h.z : Y->h.z));
-                const v3_t nn = cross3(ab, dk);
-                const float l2 = dot3(nn, nn);
-                if (l2 > 1e-12f * dot3(ab, ab)) {
-                    v3_t n = mul3(nn, 1.0f / sqrtf(l2));
-                    v3_t r;
-                    float svv;
-                    if (dot3(n, p0) < 0.0f) n = mul3(n, -1.0f);
-                    r = sub3(al, p0);
-                    svv = dot3(n, r);
-                    if (svv < margin) {
-                        const float bq = dot3(ab, dk), aq = dot3(ab, ab);
-                        const float den = aq - bq * bq;
-                        const float ts = fminf(fmaxf((bq * dot3(dk, r) - dot3(ab, r)) / den, 0.0f), 1.0f);
-                        const v3_t pp = add3(Y->c, mv_(Y->R, add3(al, mul3(ab, ts))));
-                        const v3_t nw = mv_(Y->R, n);
-                        if (onY) deep4_add_(D, svv, sub3(pp, mul3(nw, svv)), mul3(nw, -1.0f));
-                        else deep4_add_(D, svv, pp, nw);
-                    }
-                    continue;
-                }
-            }
-        }
-        p = add3(Y->c, mv_(Y->R, add3(al, mul3(ab, tm))));
-        sv = cvx_sd_(Y, p, &f);
-        if (sv < margin) {
-            const v3_t n = cvx_normal_(Y, f);
-            if (onY) deep4_add_(D, sv, sub3(p, mul3(n, sv)), mul3(n, -1.0f));
-            else deep4_add_(D, sv, p, n);
-        }
+        cvx_edge_one_(Y, margin, onY, t, M, ry, cvx_vertex_l_(X, ia), cvx_vertex_l_(X, ib), D, margin);
     }
 }
 static void convex_convex_(const cshape_t* A, const cshape_t* B, float margin, pair_t* o) {
@@ -441,10 +449,49 @@ static void sph_cvx_(v3_t s, float r, const cshape_t* B, float margin, pair_t* o
     ppush_(o, sub3(s, mul3(n, r)), n, sep);
 }
 
+/* a capsule's axis segment against a box or hull Y (mg_collide.h
+ * capsule_segment_convex): clipped by Y's planes pushed out by radius + margin,
+ * at most one candidate, moved to the capsule's surface */
+static void capsule_segment_convex_(const cshape_t* C, const cshape_t* Y, float margin, pair_t* o) {
+    const float r = C->h.x, mr = margin + r;
+    v3_t t;
+    m3_t M;
+    pair_t D;
+    if (!(C->h.y > 0.0f)) return;
+    t = mtv_(Y->R, sub3(C->c, Y->c));
+    M.c0 = mtv_(Y->R, C->R.c0);
+    M.c1 = mtv_(Y->R, C->R.c1);
+    M.c2 = mtv_(Y->R, C->R.c2);
+    D.n = 0;
+    cvx_edge_one_(Y, mr, 0, t, M, cvx_radius_(Y) + mr, V(-C->h.y, 0.0f, 0.0f), V(C->h.y, 0.0f, 0.0f), &D, margin);
+    if (D.n > 0) ppush_(o, sub3(D.p[0], mul3(D.nrm[0], r)), D.nrm[0], D.sep[0] - r);
+}
+static v3_t seg_closest_(v3_t a, v3_t b, v3_t p) {
+    const v3_t ab = sub3(b, a);
+    const float l2 = dot3(ab, ab);
+    const float t = l2 > 0.0f ? fminf(fmaxf(dot3(sub3(p, a), ab) / l2, 0.0f), 1.0f) : 0.0f;
+    return add3(a, mul3(ab, t));
+}
+static void seg_seg_closest_(v3_t a0, v3_t a1, v3_t b0, v3_t b1, v3_t* pa, v3_t* pb) {
+    const v3_t d1 = sub3(a1, a0), d2 = sub3(b1, b0), r = sub3(a0, b0);
+    const float a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+    const float c = dot3(d1, r), b = dot3(d1, d2);
+    const float den = a * e - b * b;
+    float s = 0.0f, t;
+    if (a > 0.0f && den > 1e-12f * a * e) s = fminf(fmaxf((b * f - c * e) / den, 0.0f), 1.0f);
+    t = e > 0.0f ? (b * s + f) / e : 0.0f;
+    if (t < 0.0f || t > 1.0f) {
+        t = fminf(fmaxf(t, 0.0f), 1.0f);
+        s = a > 0.0f ? fminf(fmaxf((b * t - c) / a, 0.0f), 1.0f) : 0.0f;
+    }
+    *pa = add3(a0, mul3(d1, s));
+    *pb = add3(b0, mul3(d2, t));
+}
+
 static void collide_(const cshape_t* A, const cshape_t* B, float margin, pair_t* o) {
-    v3_t ca[2], cb[2];
+    v3_t ca[2], cb[2], pa, pb;
     float ra, rb;
-    int na, nbs, k, m;
+    int na, nbs, k;
     if (A->type == MG_SHAPE_BOX && B->type == MG_SHAPE_BOX) { box_box_(A, B, margin, o); return; }
     na = A->type == MG_SHAPE_CAPSULE ? 2 : 1;
     nbs = B->type == MG_SHAPE_CAPSULE ? 2 : 1;
@@ -454,32 +501,41 @@ static void collide_(const cshape_t* A, const cshape_t* B, float margin, pair_t*
     cb[0] = B->type == MG_SHAPE_CAPSULE ? sub3(B->c, mul3(B->R.c0, B->h.y)) : B->c;
     cb[1] = add3(B->c, mul3(B->R.c0, B->h.y));
     if (A->type == MG_SHAPE_CONVEX || B->type == MG_SHAPE_CONVEX) {
-        const int pa = A->type == MG_SHAPE_BOX || A->type == MG_SHAPE_CONVEX;
-        const int pb = B->type == MG_SHAPE_BOX || B->type == MG_SHAPE_CONVEX;
+        const int pa_ = A->type == MG_SHAPE_BOX || A->type == MG_SHAPE_CONVEX;
+        const int pb_ = B->type == MG_SHAPE_BOX || B->type == MG_SHAPE_CONVEX;
         pair_t t;
-        if (pa && pb) { convex_convex_(A, B, margin, o); return; }
-        if (pb) {
+        if (pa_ && pb_) { convex_convex_(A, B, margin, o); return; }
+        if (pb_) {
             for (k = 0; k < na; ++k) sph_cvx_(ca[k], ra, B, margin, o);
+            if (A->type == MG_SHAPE_CAPSULE) capsule_segment_convex_(A, B, margin, o);
             return;
         }
         t.n = 0;
         for (k = 0; k < nbs; ++k) sph_cvx_(cb[k], rb, A, margin, &t);
+        if (B->type == MG_SHAPE_CAPSULE) capsule_segment_convex_(B, A, margin, &t);
         for (k = 0; k < t.n; ++k) ppush_(o, add3(t.p[k], mul3(t.nrm[k], t.sep[k])), mul3(t.nrm[k], -1.0f), t.sep[k]);
         return;
     }
     if (B->type == MG_SHAPE_BOX) {
         for (k = 0; k < na; ++k) sph_box_(ca[k], ra, B, margin, o);
+        if (A->type == MG_SHAPE_CAPSULE) capsule_segment_convex_(A, B, margin, o);
         return;
     }
     if (A->type == MG_SHAPE_BOX) {
         pair_t t;
         t.n = 0;
         for (k = 0; k < nbs; ++k) sph_box_(cb[k], rb, A, margin, &t);
+        if (B->type == MG_SHAPE_CAPSULE) capsule_segment_convex_(B, A, margin, &t);
         for (k = 0; k < t.n; ++k) ppush_(o, add3(t.p[k], mul3(t.nrm[k], t.sep[k])), mul3(t.nrm[k], -1.0f), t.sep[k]);
         return;
     }
-    for (k = 0; k < na; ++k)
-        for (m = 0; m < nbs; ++m) sph_sph_(ca[k], ra, cb[m], rb, margin, o);
+    /* spheres and capsules: closest points of the axis segments, one contact */
+    pa = A->c;
+    pb = B->c;
+    if (A->type == MG_SHAPE_CAPSULE && B->type == MG_SHAPE_CAPSULE) seg_seg_closest_(ca[0], ca[1], cb[0], cb[1], &pa, &pb);
+    else if (A->type == MG_SHAPE_CAPSULE) pa = seg_closest_(ca[0], ca[1], B->c);
+    else if (B->type == MG_SHAPE_CAPSULE) pb = seg_closest_(cb[0], cb[1], A->c);
+    sph_sph_(pa, ra, pb, rb, margin, o);
 }
 
 /* pair screen (mg_env.hip pair_near): part of the narrow phase's definition */
@@ -1159,6 +1215,7 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
     v3_t apt[OE_MAXCT];
     float ae[OE_MAXCT][2], amu[OE_MAXCT], psum[OE_MAXCT];
     int aa[OE_MAXCT], ab[OE_MAXCT], alast[OE_MAXCT], apair[OE_MAXCT], apart[OE_MAXCT], pstart[OE_MAXCT];
+    int aclamp[OE_MAXCT][2];
     char held[OE_FPP];
     float* fcr = fcache ? fcache + (size_t)ev->env * OE_FC_N : NULL;
     static __thread float Jr[OE_MAXCT * 3][OE_GM], Wr[OE_MAXCT * 3][OE_GM];
@@ -1536,12 +1593,19 @@ static int env_step_(const step_t* P, const mg_model* m, const oenv_t* ev, float
                     float raw, nl, dl;
                     raw = lam + ck[c][rw] * (tg - redp_(Jr[c * 3 + rw], u, G));
                     nl = fminf(fmaxf(raw, -lim), lim);
-                    /* slipping in the last iteration: the patch lets go of its anchors */
-                    if (it == P->npos + P->nvel - 1 && (raw > lim || raw < -lim) && apair[c] < OE_FPP && fcr)
-                        fcr[(size_t)apair[c] * (OE_FP_N + 1)] = 0.0f;
+                    if (it == P->npos + P->nvel - 1) aclamp[c][rw - 1] = raw > lim || raw < -lim;
                     dl = nl - lam;
                     for (ln = 0; ln < G; ++ln) u[ln] = u[ln] + Wr[c * 3 + rw][ln] * dl;
                     clam[c][rw] = nl;
+                }
+            }
+            /* slipping in the last iteration: every anchor of the patch clamped
+             * along one direction; the patch lets go of its anchors */
+            if (it == P->npos + P->nvel - 1) {
+                for (c = 0; c < nanc; ++c) {
+                    const int o = apart[c] == 1 ? c + 1 : (apart[c] == 2 ? c - 1 : c);
+                    if (((aclamp[c][0] && aclamp[o][0]) || (aclamp[c][1] && aclamp[o][1])) && apair[c] < OE_FPP && fcr)
+                        fcr[(size_t)apair[c] * (OE_FP_N + 1)] = 0.0f;
                 }
             }
             /* the last position sweep and the velocity sweeps end with the normal rows again (mg_env.hip) */

@@ -17,7 +17,9 @@
 namespace {
 
 // Lane-parallel Jacobian and mass matrix: JG = 16 lanes per articulation, 4
-// articulations per wavefront, per-articulation kinematics staged in LDS.
+// articulations per wavefront (JG = 32, 2 per wavefront, for more than 16
+// links — virtual links included — or generalized velocities: the MJCF
+// humanoid's 21 DOFs + 6 root columns), per-articulation kinematics staged in LDS.
 // Lane l: joint transform, world motion axis xi_l (about the base origin x0)
 // and world inertia of link l; lane 0: the forward-kinematics scan; lane d:
 // Jacobian column d for every link (nonzero where joint d is on the link's
@@ -25,24 +27,25 @@ namespace {
 // lane i: row i of M, M_ij = xi_j . IC_i xi_i for j on the path of i (RBDA
 // Table 6.2 in one frame: no spatial transforms). Float64 textbook kinematics
 // check it (tests/test_franka_gpu.py, tests/test_gimbal_*).
-constexpr int JG = 16;
-constexpr int JEPW = 64 / JG;
-
+template <int JG>
 struct JacLds {
     Q4 qr[MG_MAX_LINKS], ql[MG_MAX_LINKS];
     V3 rr[MG_MAX_LINKS], xl[MG_MAX_LINKS], zl[MG_MAX_LINKS];
     float xi[MG_MAX_LINKS][6];
     float Iw[MG_MAX_LINKS][36];
     float M[JG][JG];
-    int amask[MG_MAX_LINKS];
+    unsigned amask[MG_MAX_LINKS];
 };
 
+template <int JG>
 __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac, float* mm) {
-    __shared__ JacLds shm[JEPW];
+    constexpr int JEPW = 64 / JG;
+    static_assert(JG >= 16 && JG <= 32 && MG_MAX_LINKS <= 32, "lanes own links, DOFs and M rows");
+    __shared__ JacLds<JG> shm[JEPW];
     const int gi = threadIdx.x / JG, ln = threadIdx.x % JG;
     const int e = blockIdx.x * JEPW + gi;
     const bool live = e < A.na;
-    JacLds& S = shm[gi];
+    JacLds<JG>& S = shm[gi];
     const int ei = live ? e : 0;
     const int b0 = A.artic_i[ei * MG_ARTIC_I_N + 0];
     const int d0 = A.artic_i[ei * MG_ARTIC_I_N + 1];
@@ -75,12 +78,12 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
             if (p < 0) {
                 S.ql[l] = q0;
                 S.xl[l] = x0;
-                S.amask[l] = 0;
+                S.amask[l] = 0u;
             } else {
                 const Q4 qp = S.ql[p];
                 S.ql[l] = qnormalize(qmul(qp, S.qr[l]));
                 S.xl[l] = vadd(S.xl[p], qrot(qp, S.rr[l]));
-                S.amask[l] = S.amask[p] | (dof >= 0 ? (1 << dof) : 0);
+                S.amask[l] = S.amask[p] | (dof >= 0 ? (1u << dof) : 0u);
             }
         }
     }
@@ -218,14 +221,18 @@ __global__ void __launch_bounds__(64) k_artic_jac_mm_g(MgArticArgs A, float* jac
 //      minus the virtual links of ball joints), rows [linear xyz of the link
 //      frame origin, angular xyz] in the world frame, column d = DOF d;
 //   M: (instances, D, D): joint-space inertia without joint armature;
-// for a floating base (D + 6 <= 16) the 6 root columns come first — linear
+// for a floating base (D + 6 <= 32) the 6 root columns come first — linear
 // velocity of the base-link origin, then angular velocity, world axes:
 //   J: (instances, L, 6, D + 6), every link including the root;
 //   M: (instances, D + 6, D + 6) in the same generalized velocities.
 hipError_t mg_launch_jacobian(const MgArticArgs& A, float* jac, float* mm, hipStream_t s) {
     if (A.na <= 0) return hipSuccess;
-    if (A.nl > MG_MAX_LINKS || A.ndof + (A.fixed_base ? 0 : 6) > JG) return hipErrorNotSupported;
-    hipLaunchKernelGGL(k_artic_jac_mm_g, dim3((A.na + JEPW - 1) / JEPW), dim3(64), 0, s, A, jac, mm);
+    const int nc = A.ndof + (A.fixed_base ? 0 : 6);
+    if (A.nl > MG_MAX_LINKS || nc > 32) return hipErrorNotSupported;
+    if (A.nl <= 16 && nc <= 16)
+        hipLaunchKernelGGL(k_artic_jac_mm_g<16>, dim3((A.na + 3) / 4), dim3(64), 0, s, A, jac, mm);
+    else
+        hipLaunchKernelGGL(k_artic_jac_mm_g<32>, dim3((A.na + 1) / 2), dim3(64), 0, s, A, jac, mm);
     return hipGetLastError();
 }
 

@@ -4,7 +4,11 @@
 // Output convention: each contact is (point p on shape A, unit normal n pointing
 // from B towards A, separation sep — negative when penetrating). Boxes are
 // (centre, rotation columns, half extents); spheres (centre, radius); capsules
-// are replaced by their two end-cap spheres (documented approximation).
+// (centre, axis = local x, radius, half height): their two end-cap spheres plus,
+// against a box or hull, the axis segment clipped by the shape's planes pushed
+// out by radius + margin (one contact at the chord — at a box edge the
+// edge-edge contact), against a sphere or capsule the closest points of the
+// axis segments (round 4; round 3 had the caps only).
 // Convex hulls (MG_SHAPE_CONVEX, the importer's hull of a mesh, at most
 // MG_HULL_MAX_VERTS vertices) against boxes and hulls: vertex penetration both
 // ways — every vertex of one shape within the margin of the other, by the
@@ -492,8 +496,11 @@ MG_HD bool cvx_edges_gate(const CShape& X, const CShape& Y, float margin, V3 lo,
     }
     return cvx_ne(X) > 0;
 }
+// etol (>= 0): the band within which the chord's midpoint counts as near a box
+// edge, when it is not the clip margin (a capsule's segment is clipped with its
+// radius added to the margin, but is near an edge only within the margin)
 MG_HD void cvx_edge_one(const CShape& Y, float margin, bool onY, V3 t, const M3& M, float ry, V3 la, V3 lb,
-                        Deep4& D) {
+                        Deep4& D, float etol = -1.0f) {
     const int nf = cvx_nf(Y);
     const V3 al = vadd(t, mmul(M, la));
     const V3 ab = vsub(vadd(t, mmul(M, lb)), al);
@@ -526,7 +533,8 @@ MG_HD void cvx_edge_one(const CShape& Y, float margin, bool onY, V3 t, const M3&
         if (ey < ek) { k = 1; ek = ey; }
         if (ez < ek) k = 2;
         const float e1 = k == 0 ? ey : ex, e2 = k == 2 ? ey : ez;
-        if (e1 > -margin && e2 > -margin) {
+        const float et = etol >= 0.0f ? etol : margin;
+        if (e1 > -et && e2 > -et) {
             const V3 dk = v3(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
             const V3 p0 = v3(k == 0 ? 0.0f : (m.x < 0.0f ? -Y.h.x : Y.h.x),
                              k == 1 ? 0.0f : (m.y < 0.0f ? -Y.h.y : Y.h.y),
@@ -631,7 +639,50 @@ MG_HD void sphere_convex(V3 s, float r, const CShape& B, float margin, PairOut& 
     pair_push(o, vsub(s, vscale(n, r)), n, sep);
 }
 
-// generic dispatch; capsules are two end-cap spheres
+// a capsule's axis segment against a box or hull Y (capsule C: axis C.R.c0,
+// radius C.h.x, half height C.h.y): the segment as an edge of C, clipped by Y's
+// planes pushed out by radius + margin (cvx_edge_one) — a capsule lying across
+// a box edge midway between its caps, which its cap spheres miss — giving at
+// most one candidate, moved to the capsule's surface (point - n r, sep - r)
+MG_HD void capsule_segment_convex(const CShape& C, const CShape& Y, float margin, PairOut& o) {
+    if (!(C.h.y > 0.0f)) return;
+    const float r = C.h.x, mr = margin + r;
+    const V3 t = mtmul(Y.R, vsub(C.c, Y.c));
+    M3 M;
+    M.c0 = mtmul(Y.R, C.R.c0);
+    M.c1 = mtmul(Y.R, C.R.c1);
+    M.c2 = mtmul(Y.R, C.R.c2);
+    Deep4 D;
+    D.n = 0;
+    cvx_edge_one(Y, mr, false, t, M, cvx_radius(Y) + mr, v3(-C.h.y, 0.0f, 0.0f), v3(C.h.y, 0.0f, 0.0f), D, margin);
+    if (D.n > 0) pair_push(o, vsub(D.p[0], vscale(D.nrm[0], r)), D.nrm[0], D.s[0] - r);
+}
+// the point of segment [a, b] closest to p
+MG_HD V3 seg_closest(V3 a, V3 b, V3 p) {
+    const V3 ab = vsub(b, a);
+    const float l2 = vdot(ab, ab);
+    const float t = l2 > 0.0f ? fminf(fmaxf(vdot(vsub(p, a), ab) / l2, 0.0f), 1.0f) : 0.0f;
+    return vadd(a, vscale(ab, t));
+}
+// closest points of segments [a0, a1] and [b0, b1] (clamped line parameters:
+// s from the lines' closest points, t for that point, s again for that t)
+MG_HD void seg_seg_closest(V3 a0, V3 a1, V3 b0, V3 b1, V3& pa, V3& pb) {
+    const V3 d1 = vsub(a1, a0), d2 = vsub(b1, b0), r = vsub(a0, b0);
+    const float a = vdot(d1, d1), e = vdot(d2, d2), f = vdot(d2, r);
+    const float c = vdot(d1, r), b = vdot(d1, d2);
+    const float den = a * e - b * b;
+    float s = 0.0f;
+    if (a > 0.0f && den > 1e-12f * a * e) s = fminf(fmaxf((b * f - c * e) / den, 0.0f), 1.0f);
+    float t = e > 0.0f ? (b * s + f) / e : 0.0f;
+    if (t < 0.0f || t > 1.0f) {
+        t = fminf(fmaxf(t, 0.0f), 1.0f);
+        s = a > 0.0f ? fminf(fmaxf((b * t - c) / a, 0.0f), 1.0f) : 0.0f;
+    }
+    pa = vadd(a0, vscale(d1, s));
+    pb = vadd(b0, vscale(d2, t));
+}
+
+// generic dispatch
 MG_HD void collide(const CShape& A, const CShape& B, float margin, PairOut& o) {
     V3 ca[2], cb[2];
     float ra, rb;
@@ -651,11 +702,13 @@ MG_HD void collide(const CShape& A, const CShape& B, float margin, PairOut& o) {
         if (pa && pb) { convex_convex(A, B, margin, o); return; }
         if (pb) {                            // sphere / capsule A vs convex B
             for (int k = 0; k < na; ++k) sphere_convex(ca[k], ra, B, margin, o);
+            if (A.type == MG_SHAPE_CAPSULE) capsule_segment_convex(A, B, margin, o);
             return;
         }
         PairOut t;                           // convex A vs sphere / capsule B: swap roles
         t.n = 0;
         for (int k = 0; k < nbs; ++k) sphere_convex(cb[k], rb, A, margin, t);
+        if (B.type == MG_SHAPE_CAPSULE) capsule_segment_convex(B, A, margin, t);
 #pragma unroll
         for (int k = 0; k < MG_PAIR_MAXC; ++k)
             if (k < t.n) pair_push(o, vadd(t.p[k], vscale(t.nrm[k], t.sep[k])), vscale(t.nrm[k], -1.0f), t.sep[k]);
@@ -663,17 +716,24 @@ MG_HD void collide(const CShape& A, const CShape& B, float margin, PairOut& o) {
     }
     if (B.type == MG_SHAPE_BOX) {
         for (int k = 0; k < na; ++k) sphere_box(ca[k], ra, B, margin, o);
+        if (A.type == MG_SHAPE_CAPSULE) capsule_segment_convex(A, B, margin, o);
         return;
     }
     if (A.type == MG_SHAPE_BOX) {
         PairOut t;
         t.n = 0;
         for (int k = 0; k < nbs; ++k) sphere_box(cb[k], rb, A, margin, t);
+        if (B.type == MG_SHAPE_CAPSULE) capsule_segment_convex(B, A, margin, t);
 #pragma unroll
         for (int k = 0; k < MG_PAIR_MAXC; ++k)     // swap roles: point on A, normal from B to A
             if (k < t.n) pair_push(o, vadd(t.p[k], vscale(t.nrm[k], t.sep[k])), vscale(t.nrm[k], -1.0f), t.sep[k]);
         return;
     }
-    for (int k = 0; k < na; ++k)
-        for (int m = 0; m < nbs; ++m) sphere_sphere(ca[k], ra, cb[m], rb, margin, o);
+    // spheres and capsules: the closest points of the axis segments (a sphere's
+    // is its centre), one contact
+    V3 pa = A.c, pb = B.c;
+    if (A.type == MG_SHAPE_CAPSULE && B.type == MG_SHAPE_CAPSULE) seg_seg_closest(ca[0], ca[1], cb[0], cb[1], pa, pb);
+    else if (A.type == MG_SHAPE_CAPSULE) pa = seg_closest(ca[0], ca[1], B.c);
+    else if (B.type == MG_SHAPE_CAPSULE) pb = seg_closest(cb[0], cb[1], A.c);
+    sphere_sphere(pa, ra, pb, rb, margin, o);
 }

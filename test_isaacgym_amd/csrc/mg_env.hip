@@ -1609,7 +1609,9 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 
         // ================= 4. TGS (the lambdas are kept by lane 0 in LDS; every
         // lane of the env computes the same value)
-        bool slip = false;   // anchor ln's friction bound clamped in the last iteration
+        // anchors whose friction bound clamped a row in the last iteration, one
+        // bit per anchor, per direction (the same in every lane of the env)
+        unsigned long long clamp1 = 0ull, clamp2 = 0ull;
         for (int it = 0; it < P.npos + P.nvel; ++it) {
             const bool pos = it < P.npos;
             // the normal rows (every lane of the env holds the same lambdas: red16
@@ -1668,7 +1670,10 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         const float lm = lam[c * 3 + rw];
                         const float raw = lm + S.ck[c][rw] * (tgt - redg<G>(Jr[c * 3 + rw] * uv));
                         const float nl = fminf(fmaxf(raw, -lim), lim);
-                        if (last_it && ln == c && (raw > lim || raw < -lim)) slip = true;
+                        if (last_it && (raw > lim || raw < -lim)) {
+                            if (rw == 1) clamp1 |= 1ull << c;
+                            else clamp2 |= 1ull << c;
+                        }
                         const float dl = nl - lm;
                         uv = uv + Wr[c * 3 + rw] * dl;
                         lam[c * 3 + rw] = nl;
@@ -1692,7 +1697,15 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                 }
             }
         }
-        // a slipping patch lets go of its anchors (regrown at the next substep)
+        // a slipping patch lets go of its anchors (regrown at the next substep):
+        // every anchor it holds clamped along one direction (a Gauss-Seidel sweep
+        // may leave one of two anchors at its half budget while the other holds)
+        bool slip = false;
+        if (ln < nanc) {
+            const int pc = (S.alast[ln] >> 8) & 3;
+            const int o = pc == 1 ? ln + 1 : (pc == 2 ? ln - 1 : ln);
+            slip = ((((clamp1 >> ln) & (clamp1 >> o)) | ((clamp2 >> ln) & (clamp2 >> o))) & 1ull) != 0ull;
+        }
         if (live && slip && ln < nanc) {
             const int pidx = S.alast[ln] >> 10;
             if (pidx < MG_FP_MAXP) A.fpatch[(size_t)(pair0 + pidx) * MG_FP_N] = 0.0f;

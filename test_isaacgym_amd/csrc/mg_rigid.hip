@@ -711,7 +711,11 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
                 an[a].e1 = e1;
                 an[a].e2 = e2;
             }
-            bool slip = false;
+            // the anchors whose bound clamped a row in the last iteration, per
+            // anchor and direction: the patch slips when every anchor it holds is
+            // clamped along one direction (the Gauss-Seidel sweep may leave one of
+            // two anchors at its half budget while the other still holds)
+            bool c01 = false, c02 = false, c11 = false, c12 = false;
             // each anchor of a two-anchor patch holds half of the patch's Coulomb
             // budget mu N per direction: symmetric (a box sliding on its diagonal
             // anchors exerts no yaw torque), and the two saturate at mu N together
@@ -736,7 +740,8 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
                         const float raw = fmaf(an[a].k1, (pos ? an[a].e1 : 0.0f) - G.v1(v, w, an[a].r), an[a].l1);
                         const float nl = clamp_sym(raw, lim);
                         const float dl = nl - an[a].l1;
-                        slip = slip || (last && (raw > lim || raw < -lim));
+                        const bool cl = last && (raw > lim || raw < -lim);
+                        if (a == 0) c01 = cl; else c11 = cl;
                         an[a].l1 = nl;
                         v = G.f1(v, dl, invm);
                         w = fmad3(w, an[a].I1, dl);
@@ -746,7 +751,8 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
                         const float raw = fmaf(an[a].k2, (pos ? an[a].e2 : 0.0f) - G.v2(v, w, an[a].r), an[a].l2);
                         const float nl = clamp_sym(raw, lim);
                         const float dl = nl - an[a].l2;
-                        slip = slip || (last && (raw > lim || raw < -lim));
+                        const bool cl = last && (raw > lim || raw < -lim);
+                        if (a == 0) c02 = cl; else c12 = cl;
                         an[a].l2 = nl;
                         v = G.f2(v, dl, invm);
                         w = fmad3(w, an[a].I2, dl);
@@ -767,7 +773,9 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
                 fsum = G.add1(fsum, an[a].l1);
                 fsum = G.add2(fsum, an[a].l2);
             }
-            if (slip) R.cnt = 0;   // a slipping patch lets go (regrown at the next substep)
+            // a slipping patch lets go (regrown at the next substep)
+            const bool one = R.cnt < 2;
+            if ((c01 && (c11 || one)) || (c02 && (c12 || one))) R.cnt = 0;
         } else {
             // no solver pass: the motion delta is the substep's free flight
             for (int it = 0; it < P.npos; ++it) {

@@ -1414,7 +1414,7 @@ static int refresh_jac_mm(mg_sim* s, int32_t tmpl, float* jdst, float* mdst, int
         if (x.tmpl == tmpl) g = &x;
     if (!g) return fail(MG_ERR_ARG, "no articulation template %d", tmpl);
     const int nc = g->ndof + (g->fixed_base ? 0 : 6);
-    if (nc > 16) return fail(MG_ERR_UNSUPPORTED, "jacobian / mass matrix of more than 16 generalized velocities");
+    if (nc > 32) return fail(MG_ERR_UNSUPPORTED, "jacobian / mass matrix of more than 32 generalized velocities");
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
     const size_t jper = (size_t)(g->nbody - (g->fixed_base ? 1 : 0)) * 6 * nc, mper = (size_t)nc * nc;

@@ -144,13 +144,28 @@ def test_edge_edge_crossing():
     assert abs(out[0, 6] + 0.001) < 1e-4
 
 
-def test_capsule_as_two_spheres():
+def test_capsule_caps_and_segment():
+    """A capsule lying flat on a box face: its two cap contacts and the axis
+    segment's (the chord clipped by the box planes, at its midpoint), all at
+    zero separation with the normal +z."""
     cap = _shape(CAPSULE, (0, 0, 0.05), (0, 0, 0, 1), (0.05, 0.2, 0))
     box = _shape(BOX, (0, 0, -0.5), (0, 0, 0, 1), (1, 1, 0.5))
     out = oracle.collide(cap, box, 0.01)
-    assert len(out) == 2
+    assert len(out) == 3
     assert np.allclose(out[:, 6], 0.0, atol=1e-6)
-    assert np.allclose(sorted(out[:, 0]), [-0.2, 0.2], atol=1e-6)
+    assert np.allclose(sorted(out[:, 0]), [-0.2, 0.0, 0.2], atol=1e-6)
+    assert np.allclose(out[:, 3:6], [0, 0, 1], atol=1e-6)
+
+
+def test_capsule_across_narrow_box_segment_only():
+    """Both caps beyond a 0.1 m wide box: no cap contact, one segment contact
+    at the box's middle, penetration 1 mm (the cap spheres alone miss it)."""
+    cap = _shape(CAPSULE, (0, 0, 0.049), (0, 0, 0, 1), (0.05, 0.2, 0))
+    box = _shape(BOX, (0, 0, -0.5), (0, 0, 0, 1), (0.05, 1, 0.5))
+    out = oracle.collide(cap, box, 0.01)
+    assert len(out) == 1
+    assert abs(out[0, 0]) < 1e-6 and abs(out[0, 6] + 0.001) < 1e-6
+    assert np.allclose(out[0, 3:6], [0, 0, 1], atol=1e-6)
 
 
 # ---------------------------------------------------------------- convex hulls

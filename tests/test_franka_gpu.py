@@ -105,18 +105,35 @@ def test_franka_pick_lifts_cubes(gym, n):
     assert torch.isfinite(rb).all()
     frac = float((maxz > 0.55).float().mean())
     assert frac >= 0.5, "only %.2f of the cubes were lifted" % frac
-    # nothing sinks through the table or the ground: a cube is on the table
-    # (top at 0.4 m, cube half size 0.0225 m), in the gripper, or on the ground.
-    # "Inside the table" is below its top over its footprint: a cube the gripper
-    # holds beside the table edge below the top is not sunk (tools/diag_sunk.py
-    # found such cubes 0.335-0.355 m from the table centre, half extent 0.3 m)
+    # nothing sinks through the table or the ground. A cube whose footprint
+    # overlaps the table's (top at 0.4 m, half extents 0.3 / 0.5 m, cube half
+    # size 0.0225 m) must not rest below the top. A cube at rest below the top
+    # beside the table must be held by the gripper: a finger body (hand + 1,
+    # hand + 2) in contact (non-zero net contact force) within reach of the
+    # cube — 0.1 m from the finger's origin: its pad reaches 0.054 m along the
+    # hand axis, plus the cube's half-diagonal 0.039 m — and the cube itself in
+    # contact. (tools/diag_sunk.py found held cubes 0.335-0.355 m from the table
+    # centre; one wedged between a fingertip and the table's side face.)
+    ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))
+    gym.refresh_net_contact_force_tensor(sim)
     z = rb[bi, 2]
     assert float(z.min()) > 0.0
     still = rb[bi, 7:10].norm(dim=1) < 0.05
     rel = rb[bi, 0:2] - rb[bi - 1, 0:2]            # from the table centre (the body before the cube)
-    over = (rel[:, 0].abs() < 0.3 - 0.0225) & (rel[:, 1].abs() < 0.5 - 0.0225)
-    sunk = (z > 0.3) & (z < 0.4225 - 0.005) & still & over
+    overlap = (rel[:, 0].abs() < 0.3 + 0.0225) & (rel[:, 1].abs() < 0.5 + 0.0225)
+    below = (z > 0.3) & (z < 0.4225 - 0.005) & still
+    sunk = below & overlap
     assert int(sunk.sum()) == 0, "cubes at rest inside the table: %s" % z[sunk][:8].tolist()
+    hi = torch.tensor(info["hand_idxs"], device=DEV)
+    c = rb[bi, 0:3]
+    touching = ncf[bi].norm(dim=1) > 0.0
+    held = torch.zeros_like(touching)
+    for f_ in (hi + 1, hi + 2):
+        held |= ((rb[f_, 0:3] - c).norm(dim=1) < 0.1) & (ncf[f_].norm(dim=1) > 0.0)
+    loose = below & ~overlap & ~(held & touching)
+    assert int(loose.sum()) == 0, "cubes at rest below the table top, beside it, not held: %s" % (
+        torch.stack([z[loose], rel[loose, 0], rel[loose, 1]], 1)[:4].tolist())
+    assert int((below & ~overlap).sum()) <= n // 100    # a rare grip beside the table, not a pattern
 
 
 def test_franka_jacobian_mass_matrix_float64(gym):

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 G = 9.8
 
 
-def _scene(gym, n, corr=0.0005):
+def _scene(gym, n, corr=0.0005, yaw_step=0.1):
     sp = gymapi.SimParams()
     sp.up_axis = gymapi.UP_AXIS_Z
     sp.gravity = gymapi.Vec3(0, 0, -G)
@@ -46,7 +46,7 @@ def _scene(gym, n, corr=0.0005):
         env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 8)
         gym.create_actor(env, table, gymapi.Transform(gymapi.Vec3(0.5, 0, 0.2)), "table", i, 0)
         pose = gymapi.Transform(gymapi.Vec3(0.45, 0.1, 0.4101))
-        pose.r = gymapi.Quat.from_axis_angle(gymapi.Vec3(0, 0, 1), 0.1 * i)
+        pose.r = gymapi.Quat.from_axis_angle(gymapi.Vec3(0, 0, 1), yaw_step * i)
         gym.create_actor(env, tile, pose, "tile", i, 0)
     gym.prepare_sim(sim)
     return sim
@@ -105,3 +105,47 @@ def test_friction_anchor_push_parity_gpu(gym, corr):
     assert held.any() and slid.any()
     assert np.all(moved[held] < 1e-3)             # held in place by the anchors
     assert np.all(moved[slid] > 0.02)             # slipping patches slide
+
+
+def test_friction_anchor_basis_push_gpu(gym):
+    """Pushes along the patch's tangent basis (t1 = +y, t2 = -x for the +z
+    table top), where the per-direction budget is exact: held below 0.95 mu m g
+    (both anchors share the push; the patch slips only when both clamp), sliding
+    from 1.05 mu m g on at (F - mu m g) / m, bit for bit with the oracle."""
+    pushes = np.array([0.5, 0.9, 0.95, 1.05] * 2, np.float32)
+    along_y = np.arange(pushes.size) >= 4
+    n, settle, frames = pushes.size, 20, 60
+    sim = _scene(gym, n, yaw_step=0.0)
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    A = sim.model_arrays
+    mu = float(0.5 * (A["shapes"][0][11] + A["shapes"][1][11]))
+    st = A["body_state0"].copy()
+    dof = np.zeros((0, 2), np.float32)
+    mass = 1000.0 * 0.1 * 0.1 * 0.02
+    F = pushes * np.float32(mu * mass * G)
+    fx = np.where(along_y, 0.0, F).astype(np.float32)           # +x (toward the table's far edge)
+    fy = np.where(along_y, -F, 0.0).astype(np.float32)          # -y
+    f = torch.zeros((n, 2, 3), device="cuda:0")
+    t = torch.zeros((n, 2, 3), device="cuda:0")
+    ext = np.zeros((2 * n, 6), np.float32)
+    for k in range(settle + frames):
+        if k == settle:
+            f[:, 1, 0] = torch.from_numpy(fx).cuda()
+            f[:, 1, 1] = torch.from_numpy(fy).cuda()
+            ext[1::2, 0] = fx
+            ext[1::2, 1] = fy
+            x0 = st[1::2, 0:2].copy()
+        assert gym.apply_rigid_body_force_tensors(sim, gymtorch.unwrap_tensor(f), gymtorch.unwrap_tensor(t),
+                                                  gymapi.ENV_SPACE)
+        gym.simulate(sim)
+        oracle.step(p, m, st, dof, ext=ext)
+    gym.refresh_rigid_body_state_tensor(sim)
+    got = rb.cpu().numpy()
+    assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+    moved = np.linalg.norm(st[1::2, 0:2] - x0, axis=1)
+    held = pushes <= 0.95
+    assert np.all(moved[held] < 1e-3), moved[held]
+    tt = frames / 60.0
+    expect = 0.5 * (pushes[~held] - 1.0) * mu * G * tt * tt
+    assert np.all(np.abs(moved[~held] - expect) < 0.15 * expect), (moved[~held], expect)

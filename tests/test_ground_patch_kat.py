@@ -6,7 +6,7 @@ threshold and correlation distance left at Isaac Gym's defaults 0.04 / 0.025,
 ground mu 1) on the servo scene's ground vehicle (mass 100, the 7.5 x 3 x 2.5 m
 box proxy of its missing mesh):
 
-  - pushed along the ground's tangent basis it is held below mu m g (after a
+  - pushed along the ground's tangent basis it is held up to 0.95 mu m g (after a
     sub-millimetre give the same two anchors hold it, bit for bit) and slides
     above it — from 1.05 mu m g on — at (F - mu m g) / m;
   - pushed along a diagonal of the basis it holds up to sqrt(2) mu m g (the
@@ -56,7 +56,7 @@ def _settle(A, p, m, cc, frames=60):
     return st, dof
 
 
-@pytest.mark.parametrize("push", [0.5, 0.9, 1.05, 1.2])
+@pytest.mark.parametrize("push", [0.5, 0.9, 0.95, 1.05, 1.2])
 def test_vehicle_push_along_basis(gym, push):
     sim, A, p, m, mu = _vehicle(gym)
     cc = oracle.contact_cache(m)

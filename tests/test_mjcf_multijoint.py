@@ -278,3 +278,47 @@ def test_fixed_humanoid_pd_parity_gpu(gym):
     assert np.all(np.isfinite(got)) and np.abs(got_d[:, 1]).max() > 0.1
     assert np.array_equal(got_d, ds), "max |diff| %g" % np.abs(got_d - ds).max()
     assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
+
+
+@pytest.mark.gpu
+def test_humanoid_jacobian_mass_matrix_float64(gym):
+    """acquire_jacobian_tensor / acquire_mass_matrix_tensor of nv_humanoid
+    (floating base, 21 DOFs in 25 kernel links: more than 16 links and
+    generalized velocities, the 32-lane k_artic_jac_mm_g<32>):
+    (N, 16, 6, 27) and (N, 27, 27) at random root poses and joint angles against
+    float64 textbook kinematics (tests/kinematics64.py), rtol 1e-4."""
+    import kinematics64 as K
+    n = 8
+    sim = _humanoid_drop(gym, n, gpu=True)
+    gym.prepare_sim(sim)
+    jac = gymtorch.wrap_tensor(gym.acquire_jacobian_tensor(sim, "h"))
+    mm = gymtorch.wrap_tensor(gym.acquire_mass_matrix_tensor(sim, "h"))
+    assert tuple(jac.shape) == (n, 16, 6, 27) and tuple(mm.shape) == (n, 27, 27)
+    A = sim.model_arrays
+    rng = np.random.RandomState(4)
+    props = A["dof_props"][:21]
+    lo, hi = props[:, 5], props[:, 6]
+    q = (lo + (hi - lo) * rng.uniform(0.1, 0.9, (n, 21))).astype(np.float32)
+    ds = torch.zeros((21 * n, 2), dtype=torch.float32, device="cuda:0")
+    ds[:, 0] = torch.from_numpy(q.reshape(-1)).cuda()
+    gym.set_dof_state_tensor(sim, gymtorch.unwrap_tensor(ds))
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    gym.refresh_actor_root_state_tensor(sim)
+    quat = rng.normal(size=(n, 4))
+    quat /= np.linalg.norm(quat, axis=1, keepdims=True)
+    root[:, 3:7] = torch.from_numpy(quat.astype(np.float32)).cuda()
+    gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+    gym.refresh_jacobian_tensors(sim)
+    gym.refresh_mass_matrix_tensors(sim)
+    gym.refresh_actor_root_state_tensor(sim)
+    art = K.Articulation(A, 0)
+    J, M, R = jac.cpu().numpy(), mm.cpu().numpy(), root.cpu().numpy()
+    for e in range(n):
+        fb = int(A["artic_i"][e, 0])
+        base = R[e, 0:7].astype(np.float64)
+        Jr = art.jacobian_fb(base, q[e].astype(np.float64))
+        Mr = art.mass_matrix_fb(base, q[e].astype(np.float64), fb)
+        assert np.allclose(J[e], Jr, rtol=1e-4, atol=1e-5), np.abs(J[e] - Jr).max()
+        assert np.allclose(M[e], Mr, rtol=1e-4, atol=1e-4), np.abs(M[e] - Mr).max()
+        assert np.allclose(M[e], M[e].T, atol=1e-5)
+    gym.destroy_sim(sim)
