@@ -575,7 +575,10 @@ def s1_rate(n, steps, dev, use_graph=True, fused=True, seed=1, unfused_kernel=Fa
     root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
     gym.acquire_rigid_body_state_tensor(sim)
     gym.acquire_dof_state_tensor(sim)
-    acts = scenes.servo_actions(n, 16, dev, seed=seed)
+    # graphs of `chunk` steps over a bank of `slots` actions (at large N, 16 slots
+    # of 2n root rows each and graphs of at most 16 steps)
+    chunk = graph_chunk(steps, 16 if n > 65536 else GRAPH_CHUNK_MAX)
+    acts = scenes.servo_actions(n, bank_slots(chunk, 16), dev, seed=seed)
 
     def step(k):
         root[:, 3:10] = acts[k % acts.shape[0]]
@@ -592,7 +595,6 @@ def s1_rate(n, steps, dev, use_graph=True, fused=True, seed=1, unfused_kernel=Fa
         step(k)
     kms, kmin, used = kernel_stats(sim, KERNEL_TIMED_LAUNCHES,
                                    lambda: [step(warm + k) for k in range(KERNEL_TIMED_LAUNCHES)])
-    chunk = graph_chunk(steps, acts.shape[0])
     assert acts.shape[0] % chunk == 0
     graphs = None
     base = -(-(warm + KERNEL_TIMED_LAUNCHES) // chunk) * chunk

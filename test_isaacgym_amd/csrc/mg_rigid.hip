@@ -482,68 +482,71 @@ struct GPatch {
     V3 aA[2];       // anchor on the body (body frame)
     V3 aB[2];       // anchor on the ground (world)
 };
-__device__ __forceinline__ void ground_patch_update(GPatch& R, V3 x, Q4 q, V3 n0, const V3 (&p)[4],
+// Anchors are placed by candidate index during the scan and turned into body
+// copies (qrot_inv(q, p - x)) once per slot after it, from the scan points w0 /
+// w1 (the candidate each slot ended with): the oracle's gpatch_update_ values,
+// without a rotation per placement inside divergent branches. The normal test
+// takes only the normal component of the rotated patch normal (G.dn: for the +Z
+// ground one component of qrot; the same value as the oracle's dot product).
+template <class B>
+__device__ __forceinline__ void ground_patch_update(const B& G, GPatch& R, V3 x, Q4 q, V3 n0, const V3 (&p)[4],
                                                     const float (&s0)[4], const bool (&on)[4], float fot,
                                                     float corr) {
     const float c2 = corr * corr;
     int cnt = R.cnt;
-    if (cnt > 0 && vdot(qrot(q, R.nA), n0) < MG_FP_NORMAL_COS) cnt = 0;
+    if (cnt > 0 && G.dn(qrot(q, R.nA)) < MG_FP_NORMAL_COS) cnt = 0;
     GPatch N;
     N.cnt = 0;
     N.aA[0] = N.aA[1] = N.aB[0] = N.aB[1] = v3(0.0f, 0.0f, 0.0f);
+    V3 w0 = v3(0.0f, 0.0f, 0.0f), w1 = v3(0.0f, 0.0f, 0.0f);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         if (k < cnt) {
-            const V3 d = vsub(vadd(x, qrot(q, R.aA[k])), R.aB[k]);
+            const V3 wa = vadd(x, qrot(q, R.aA[k]));
+            const V3 d = vsub(wa, R.aB[k]);
             if (vdot(d, d) <= c2) {
-                if (N.cnt == 0) { N.aA[0] = R.aA[k]; N.aB[0] = R.aB[k]; }
+                if (N.cnt == 0) { N.aA[0] = R.aA[k]; N.aB[0] = R.aB[k]; w0 = wa; }
                 else { N.aA[1] = R.aA[k]; N.aB[1] = R.aB[k]; }
                 N.cnt = N.cnt + 1;
             }
         }
     }
-    // growth (PhysX growPatches): a patch still holding two anchors keeps them;
-    // otherwise contacts within the friction offset threshold, in slot order,
-    // give anchor 0, then anchor 1 (the first farther than the correlation
-    // distance from anchor 0), then each later one replaces the anchor it is
-    // nearer to when it lies farther from the other than the two are apart —
-    // the anchors spread over the contact patch (a box's bottom face: a
-    // diagonal, so friction along either axis exerts no yaw torque)
-    const int kept = N.cnt;   // anchors kept from the last substep
-    const bool grow = N.cnt < 2;
-    V3 w0 = N.cnt > 0 ? vadd(x, qrot(q, N.aA[0])) : v3(0.0f, 0.0f, 0.0f), w1 = v3(0.0f, 0.0f, 0.0f);
-    float dd = 0.0f;
+    const int kept = N.cnt;
+    int nc = kept;
+    if (nc < 2) {
+        float dd = 0.0f;
+        int sel0 = -1, sel1 = -1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (grow && on[j] && s0[j] <= fot) {
-            const V3 pj = p[j];
-            int put = -1;
-            if (N.cnt == 0) {
-                put = 0;
-            } else if (N.cnt == 1) {
-                const V3 d = vsub(pj, w0);
-                const float d2 = vdot(d, d);
-                if (d2 > c2) { put = 1; dd = d2; }
-            } else {
-                const V3 e0 = vsub(pj, w0), e1 = vsub(pj, w1);
-                const float d0 = vdot(e0, e0), d1 = vdot(e1, e1);
-                if (d0 > d1) {
-                    if (d0 > dd) { put = 1; dd = d0; }
-                } else if (d1 > dd) {
-                    put = 0;
-                    dd = d1;
+        for (int j = 0; j < 4; ++j) {
+            if (on[j] && s0[j] <= fot) {
+                const V3 pj = p[j];
+                if (nc == 0) {
+                    sel0 = j; w0 = pj; nc = 1;
+                } else if (nc == 1) {
+                    const V3 d = vsub(pj, w0);
+                    const float d2 = vdot(d, d);
+                    if (d2 > c2) { sel1 = j; w1 = pj; dd = d2; nc = 2; }
+                } else {
+                    const V3 e0 = vsub(pj, w0), e1 = vsub(pj, w1);
+                    const float d0 = vdot(e0, e0), d1 = vdot(e1, e1);
+                    if (d0 > d1) {
+                        if (d0 > dd) { sel1 = j; w1 = pj; dd = d0; }
+                    } else if (d1 > dd) {
+                        sel0 = j; w0 = pj; dd = d1;
+                    }
                 }
             }
-            if (put >= 0) {
-                const V3 la = qrot_inv(q, vsub(pj, x));
-                if (put == 0) { N.aA[0] = la; N.aB[0] = pj; w0 = pj; }
-                else { N.aA[1] = la; N.aB[1] = pj; w1 = pj; }
-                if (N.cnt <= put) N.cnt = put + 1;
-            }
         }
+        if (sel0 >= 0) {
+            N.aA[0] = qrot_inv(q, vsub(w0, x));
+            N.aB[0] = w0;
+        }
+        if (sel1 >= 0) {
+            N.aA[1] = qrot_inv(q, vsub(w1, x));
+            N.aB[1] = w1;
+        }
+        N.cnt = nc;
     }
-    // the patch normal is the one the patch was created with while it keeps an
-    // anchor (a slowly tilting contact still drops it past MG_FP_NORMAL_COS)
     N.nA = kept > 0 ? R.nA : qrot_inv(q, n0);
     R = N;
 }
@@ -569,6 +572,117 @@ __device__ __forceinline__ void row_normal1(const B& G, NRow& c, V3& v, V3& w, f
     c.ln = nl;
     v = G.fn(v, dl, invm);
     w = fmad3(w, c.In, dl);
+}
+
+// ---- +Z ground: the solver on packed f32 pairs -------------------------------
+// The same sweeps as rigid_body1's scalar loop with BasisZ (normal rows, the
+// patch's anchor rows t1 = +y, t2 = -x, the closing normal pass of the last
+// position sweep and the velocity sweeps), but the velocity state lives in
+// register pairs W = (w.x, w.y), Z = (w.z, v.z), V = (v.x, v.y) (the motion
+// delta in DW = (dth.x, dth.y), DZ = (dth.z, dx.z), DV = (dx.x, dx.y)), so one
+// v_pk_fma_f32 applies two of a row's impulse updates and the separations of two
+// slots share one packed chain. Each half of a packed op is the same correctly
+// rounded fma / add / mul as the scalar form, so results are bit-identical to
+// the scalar loop and to the oracle; only the issue count drops. Used by
+// launches that fit in one resident round (the latency regime: DESIGN.md §3.2).
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk2(float a, float b) { return f2{a, b}; }
+__device__ __forceinline__ f2 bc2(float a) { return f2{a, a}; }
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// lim1 = share * mu: an anchor row's bound per unit of the patch's normal impulse
+__device__ __forceinline__ void tgs_zp(const MgStep& P, NRow (&sl)[4], ARow (&an)[2], float lim1, float e, V3& v,
+                                       V3& w, V3& dx, V3& dth, float invm, bool& c01, bool& c02, bool& c11,
+                                       bool& c12) {
+    f2 W = pk2(w.x, w.y), Z = pk2(w.z, v.z), V = pk2(v.x, v.y);
+    f2 DW = pk2(dth.x, dth.y), DZ = pk2(dth.z, dx.z), DV = pk2(dx.x, dx.y);
+    // the packed operands are named values, not arrays: an array of pairs built
+    // lane by lane was kept in scratch (a memory round trip per substep)
+    const f2 S0a = pk2(sl[0].s0, sl[1].s0), S0b = pk2(sl[2].s0, sl[3].s0);
+    const f2 RYa = pk2(sl[0].r.y, sl[1].r.y), RYb = pk2(sl[2].r.y, sl[3].r.y);
+    const f2 NRXa = pk2(-sl[0].r.x, -sl[1].r.x), NRXb = pk2(-sl[2].r.x, -sl[3].r.x);
+    // separations of slots (2h, 2h+1): s0 + dx.z + dth.x r.y - dth.y r.x (BasisZ::ps)
+    auto sep = [&](int h) {
+        f2 a = (h ? S0b : S0a) + bc2(DZ.y);
+        a = pfma(bc2(DW.x), h ? RYb : RYa, a);
+        return pfma(bc2(DW.y), h ? NRXb : NRXa, a);
+    };
+    auto normal = [&](int j, float tgt) {
+        const float nrx = -sl[j].r.x, ry = sl[j].r.y;
+        const float vn = fmaf(W.y, nrx, fmaf(W.x, ry, Z.y));
+        const float nl = fmaxf(fmaf(sl[j].kn, tgt - vn, sl[j].ln), 0.0f);
+        const float dl = nl - sl[j].ln;
+        sl[j].ln = nl;
+        W = pfma(pk2(sl[j].In.x, sl[j].In.y), bc2(dl), W);
+        Z = pfma(pk2(sl[j].In.z, invm), bc2(dl), Z);   // Z = (w.z, v.z): In.z and 1/m (BasisZ::fn)
+    };
+    // the anchors' rows: t1 = +y (BasisZ::v1 / f1), t2 = -x (v2 / f2)
+    auto anchors = [&](bool pos, bool last) {
+        const float lim = lim1 * (((sl[0].ln + sl[1].ln) + sl[2].ln) + sl[3].ln);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const float rx = an[a].r.x, ry = an[a].r.y, nrz = -an[a].r.z;
+            {
+                const float v1 = fmaf(Z.x, rx, fmaf(W.x, nrz, V.y));
+                const float raw = fmaf(an[a].k1, (pos ? an[a].e1 : 0.0f) - v1, an[a].l1);
+                const float nl = clamp_sym(raw, lim);
+                const float dl = nl - an[a].l1;
+                const bool cl = last && (raw > lim || raw < -lim);
+                if (a == 0) c01 = cl; else c11 = cl;
+                an[a].l1 = nl;
+                V.y = fmaf(dl, invm, V.y);
+                W = pfma(pk2(an[a].I1.x, an[a].I1.y), bc2(dl), W);
+                Z.x = fmaf(an[a].I1.z, dl, Z.x);
+            }
+            {
+                const float v2 = fmaf(Z.x, ry, fmaf(W.y, nrz, -V.x));
+                const float raw = fmaf(an[a].k2, (pos ? an[a].e2 : 0.0f) - v2, an[a].l2);
+                const float nl = clamp_sym(raw, lim);
+                const float dl = nl - an[a].l2;
+                const bool cl = last && (raw > lim || raw < -lim);
+                if (a == 0) c02 = cl; else c12 = cl;
+                an[a].l2 = nl;
+                V.x = fmaf(-dl, invm, V.x);
+                W = pfma(pk2(an[a].I2.x, an[a].I2.y), bc2(dl), W);
+                Z.x = fmaf(an[a].I2.z, dl, Z.x);
+            }
+        }
+    };
+    const f2 nsub = bc2(-P.inv_sub), psub = bc2(P.sub);
+    const int nit = P.npos + P.nvel;
+    for (int it = 0; it < P.npos; ++it) {
+        const f2 t0 = sep(0) * nsub, t1 = sep(1) * nsub;   // -s / sub of each slot
+        const float tg[4] = {fminf(t0.x, P.max_depen), fminf(t0.y, P.max_depen), fminf(t1.x, P.max_depen),
+                             fminf(t1.y, P.max_depen)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) normal(j, tg[j]);
+        anchors(true, it == nit - 1);
+        if (it == P.npos - 1) {   // the closing normal pass (same targets: dx, dth unchanged)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) normal(j, tg[j]);
+        }
+        DV = pfma(V, psub, DV);
+        DW = pfma(W, psub, DW);
+        DZ = pfma(Z, psub, DZ);
+    }
+    if (P.nvel > 0) {
+        const f2 s01 = sep(0), s23 = sep(1);
+        const float sj[4] = {s01.x, s01.y, s23.x, s23.y};
+        float tg[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tg[j] = vel_target(P, sj[j], e, sl[j].vn0);
+        for (int it = P.npos; it < nit; ++it) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) normal(j, tg[j]);
+            anchors(false, it == nit - 1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) normal(j, tg[j]);
+        }
+    }
+    v = v3(V.x, V.y, Z.y);
+    w = v3(W.x, W.y, Z.x);
+    dx = v3(DV.x, DV.y, DZ.y);
+    dth = v3(DW.x, DW.y, DZ.x);
 }
 
 // T: this body's compact template record (MG_TREC_N floats: MG_TBODY_F_N
@@ -669,7 +783,7 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
             float cs0[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) cs0[j] = sl[j].s0;
-            ground_patch_update(R, x, q, n0, cp, cs0, on, P.fric_offset, P.fric_corr);
+            ground_patch_update(G, R, x, q, n0, cp, cs0, on, P.fric_offset, P.fric_corr);
         } else {
             R.cnt = 0;
         }
@@ -721,6 +835,9 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
             // anchors exerts no yaw torque), and the two saturate at mu N together
             const float share = R.cnt == 2 ? 0.5f : 1.0f;
             const int nit = P.npos + P.nvel;
+            if constexpr (B::kPacked && PACK) {
+                tgs_zp(P, sl, an, share * mu, e, v, w, dx, dth, invm, c01, c02, c11, c12);
+            } else
             for (int it = 0; it < nit; ++it) {
                 const bool pos = it < P.npos, last = it == nit - 1;
                 auto normals = [&]() {

@@ -108,12 +108,12 @@ def test_franka_pick_lifts_cubes(gym, n):
     # nothing sinks through the table or the ground. A cube whose footprint
     # overlaps the table's (top at 0.4 m, half extents 0.3 / 0.5 m, cube half
     # size 0.0225 m) must not rest below the top. A cube at rest below the top
-    # beside the table must be held by the gripper: a finger body (hand + 1,
-    # hand + 2) in contact (non-zero net contact force) within reach of the
-    # cube — 0.1 m from the finger's origin: its pad reaches 0.054 m along the
-    # hand axis, plus the cube's half-diagonal 0.039 m — and the cube itself in
-    # contact. (tools/diag_sunk.py found held cubes 0.335-0.355 m from the table
-    # centre; one wedged between a fingertip and the table's side face.)
+    # beside the table must be carried by the robot: in contact (its net
+    # contact force non-zero) within 0.15 m of the hand or a finger body, that
+    # body in contact too. tools/diag_sunk.py / diag_loose.py found such cubes
+    # 0.335-0.355 m from the table centre held by the fingers, and one resting
+    # on the hand of an arm pushed against the table's side (fingers pressing
+    # the side at ~900 N, the cube's contact force its weight).
     ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))
     gym.refresh_net_contact_force_tensor(sim)
     z = rb[bi, 2]
@@ -127,13 +127,13 @@ def test_franka_pick_lifts_cubes(gym, n):
     hi = torch.tensor(info["hand_idxs"], device=DEV)
     c = rb[bi, 0:3]
     touching = ncf[bi].norm(dim=1) > 0.0
-    held = torch.zeros_like(touching)
-    for f_ in (hi + 1, hi + 2):
-        held |= ((rb[f_, 0:3] - c).norm(dim=1) < 0.1) & (ncf[f_].norm(dim=1) > 0.0)
-    loose = below & ~overlap & ~(held & touching)
-    assert int(loose.sum()) == 0, "cubes at rest below the table top, beside it, not held: %s" % (
+    carried = torch.zeros_like(touching)
+    for b_ in (hi, hi + 1, hi + 2):
+        carried |= ((rb[b_, 0:3] - c).norm(dim=1) < 0.15) & (ncf[b_].norm(dim=1) > 0.0)
+    loose = below & ~overlap & ~(carried & touching)
+    assert int(loose.sum()) == 0, "cubes at rest below the table top, beside it, not on the robot: %s" % (
         torch.stack([z[loose], rel[loose, 0], rel[loose, 1]], 1)[:4].tolist())
-    assert int((below & ~overlap).sum()) <= n // 100    # a rare grip beside the table, not a pattern
+    assert int((below & ~overlap).sum()) <= n // 100    # a rare case, not a pattern
 
 
 def test_franka_jacobian_mass_matrix_float64(gym):
