@@ -36,6 +36,7 @@
 // Restated op for op by oracle/migym_oracle.c chain_step_ (explicit fmaf where
 // the kernel uses it, -ffp-contract=off elsewhere): bit-identical results.
 #include "mg_internal.h"
+#include "mg_chainlink.h"
 #include "mg_spatial.h"
 #include "mg_world.h"
 
@@ -86,30 +87,10 @@ __device__ __forceinline__ float sdot(SV a, SV b) {
 __device__ __forceinline__ SV crm_f(SV a, SV b) { return sv(fcross(a.w, b.w), vadd(fcross(a.w, b.v), fcross(a.v, b.w))); }
 __device__ __forceinline__ SV crf_f(SV a, SV f) { return sv(vadd(fcross(a.w, f.w), fcross(a.v, f.v)), fcross(a.w, f.v)); }
 
-// a moving link's mass constants: mass, COM and the rotational inertia about
-// the COM in link axes (symmetric: xx, yy, zz, xy, xz, yz), built once per
-// launch from the principal moments and frame (MG_MASS_N row)
-struct ChainLink {
-    float m;
-    V3 com;
-    float ib[6];
-};
 __device__ __forceinline__ ChainLink load_chain_link(const float* Ms, int nb, int b) {
-    ChainLink k;
-    k.m = fld(Ms, 11, nb, b);
-    k.com = v3(fld(Ms, 8, nb, b), fld(Ms, 9, nb, b), fld(Ms, 10, nb, b));
-    const M3 R = qmat(q4(fld(Ms, 4, nb, b), fld(Ms, 5, nb, b), fld(Ms, 6, nb, b), fld(Ms, 7, nb, b)));
-    const float ix = fld(Ms, 1, nb, b), iy = fld(Ms, 2, nb, b), iz = fld(Ms, 3, nb, b);
-    const V3 u0 = vscale(R.c0, ix > 0.0f ? 1.0f / ix : 0.0f);
-    const V3 u1 = vscale(R.c1, iy > 0.0f ? 1.0f / iy : 0.0f);
-    const V3 u2 = vscale(R.c2, iz > 0.0f ? 1.0f / iz : 0.0f);
-    k.ib[0] = fmaf(u0.x, R.c0.x, fmaf(u1.x, R.c1.x, u2.x * R.c2.x));
-    k.ib[1] = fmaf(u0.y, R.c0.y, fmaf(u1.y, R.c1.y, u2.y * R.c2.y));
-    k.ib[2] = fmaf(u0.z, R.c0.z, fmaf(u1.z, R.c1.z, u2.z * R.c2.z));
-    k.ib[3] = fmaf(u0.x, R.c0.y, fmaf(u1.x, R.c1.y, u2.x * R.c2.y));
-    k.ib[4] = fmaf(u0.x, R.c0.z, fmaf(u1.x, R.c1.z, u2.x * R.c2.z));
-    k.ib[5] = fmaf(u0.y, R.c0.z, fmaf(u1.y, R.c1.z, u2.y * R.c2.z));
-    return k;
+    return chain_link_make(fld(Ms, 11, nb, b), v3(fld(Ms, 8, nb, b), fld(Ms, 9, nb, b), fld(Ms, 10, nb, b)),
+                           fld(Ms, 1, nb, b), fld(Ms, 2, nb, b), fld(Ms, 3, nb, b),
+                           q4(fld(Ms, 4, nb, b), fld(Ms, 5, nb, b), fld(Ms, 6, nb, b), fld(Ms, 7, nb, b)));
 }
 
 // the link's rigid inertia about x0 (world axes); c = its COM - x0
@@ -241,8 +222,11 @@ __device__ __forceinline__ void store_row(float* dst, const float (&v)[N]) {
 #ifndef MG_CHAIN_WAVES
 #define MG_CHAIN_WAVES 2
 #endif
-// EXT: external wrenches this step (apply_rigid_body_force_tensors)
-template <int NL, bool EXT>
+// EXT: external wrenches this step (apply_rigid_body_force_tensors); UNI: every
+// instance of the launch shares its DOF properties, link mass constants and
+// gravity flag (AA.uni, migym_capi.cpp): wave-uniform scalar loads instead of
+// per-lane loads and per-lane inertia set-up (no VGPRs for them)
+template <int NL, bool EXT, bool UNI>
 __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, MgArticArgs AA) {
     constexpr int D = NL - 1;
     const int a = blockIdx.x * 64 + threadIdx.x;
@@ -268,7 +252,8 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
     }
     const V3 x0 = v3(fld(St, 0, nb, b0), fld(St, 1, nb, b0), fld(St, 2, nb, b0));
     const Q4 q0 = qnormalize(q4(fld(St, 3, nb, b0), fld(St, 4, nb, b0), fld(St, 5, nb, b0), fld(St, 6, nb, b0)));
-    const V3 gw = AA.tbf[fld(AA.body_tmpl, 0, 0, b0) * MG_TBODY_F_N + 4] != 0.0f ? v3(P.g[0], P.g[1], P.g[2]) : v3(0.0f, 0.0f, 0.0f);
+    const float gflag = UNI ? AA.uni[MG_CHAIN_UNI_GRAV] : AA.tbf[fld(AA.body_tmpl, 0, 0, b0) * MG_TBODY_F_N + 4];
+    const V3 gw = gflag != 0.0f ? v3(P.g[0], P.g[1], P.g[2]) : v3(0.0f, 0.0f, 0.0f);
     float qv[D], uv[D], arm[D];
     ChainDof dc[D];
 #pragma unroll
@@ -276,15 +261,28 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
         const int gd = d0 + d;
         qv[d] = fld(AA.dof_pos, 0, 0, gd);
         uv[d] = fld(AA.dof_vel, 0, 0, gd);
-        dc[d].mode = (int)fld(pr, 0, nd, gd);
-        dc[d].kp = fld(pr, 1, nd, gd);
-        dc[d].kd = fld(pr, 2, nd, gd);
-        dc[d].eff = fld(pr, 3, nd, gd);
-        dc[d].maxv = fld(pr, 4, nd, gd);
-        dc[d].lo = fld(pr, 5, nd, gd);
-        dc[d].hi = fld(pr, 6, nd, gd);
-        dc[d].haslim = fld(pr, 7, nd, gd) != 0.0f;
-        arm[d] = fld(pr, 8, nd, gd);
+        if constexpr (UNI) {
+            const float* u = AA.uni + MG_CHAIN_UNI_DOF + 9 * d;
+            dc[d].mode = (int)u[0];
+            dc[d].kp = u[1];
+            dc[d].kd = u[2];
+            dc[d].eff = u[3];
+            dc[d].maxv = u[4];
+            dc[d].lo = u[5];
+            dc[d].hi = u[6];
+            dc[d].haslim = u[7] != 0.0f;
+            arm[d] = u[8];
+        } else {
+            dc[d].mode = (int)fld(pr, 0, nd, gd);
+            dc[d].kp = fld(pr, 1, nd, gd);
+            dc[d].kd = fld(pr, 2, nd, gd);
+            dc[d].eff = fld(pr, 3, nd, gd);
+            dc[d].maxv = fld(pr, 4, nd, gd);
+            dc[d].lo = fld(pr, 5, nd, gd);
+            dc[d].hi = fld(pr, 6, nd, gd);
+            dc[d].haslim = fld(pr, 7, nd, gd) != 0.0f;
+            arm[d] = fld(pr, 8, nd, gd);
+        }
         dc[d].tpos = fld(AA.dof_tpos, 0, 0, gd);
         dc[d].tvel = fld(AA.dof_tvel, 0, 0, gd);
         dc[d].force = fld(AA.dof_force, 0, 0, gd);
@@ -296,7 +294,17 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
     }
     ChainLink lk[NL];
 #pragma unroll
-    for (int l = 1; l < NL; ++l) lk[l] = load_chain_link(AA.mass, nb, b0 + l * ls);
+    for (int l = 1; l < NL; ++l) {
+        if constexpr (UNI) {
+            const float* u = AA.uni + MG_CHAIN_UNI_LINK + 10 * (l - 1);
+            lk[l].m = u[0];
+            lk[l].com = v3(u[1], u[2], u[3]);
+#pragma unroll
+            for (int k = 0; k < 6; ++k) lk[l].ib[k] = u[4 + k];
+        } else {
+            lk[l] = load_chain_link(AA.mass, nb, b0 + l * ls);
+        }
+    }
 
     for (int st = 0; st < P.substeps; ++st) {
         // ---- forward: poses, axes, velocities, inertias, bias forces
@@ -476,10 +484,15 @@ hipError_t mg_launch_artic_chain(const MgStep& P, const MgArticArgs& A, hipStrea
     if (A.na <= 0) return hipSuccess;
     if (!A.chain || A.nl < 2 || A.nl > 4) return hipErrorNotSupported;
     const int cb = (A.na + 63) / 64;
-#define MG_KC(NL)                                                                        \
-    do {                                                                                 \
-        if (A.ext) MG_LAUNCH((k_artic_chain<NL, true>), dim3(cb), dim3(64), 0, s, P, A); \
-        else MG_LAUNCH((k_artic_chain<NL, false>), dim3(cb), dim3(64), 0, s, P, A);      \
+#define MG_KC(NL)                                                                                 \
+    do {                                                                                          \
+        if (A.ext) {                                                                              \
+            if (A.uni) MG_LAUNCH((k_artic_chain<NL, true, true>), dim3(cb), dim3(64), 0, s, P, A);  \
+            else MG_LAUNCH((k_artic_chain<NL, true, false>), dim3(cb), dim3(64), 0, s, P, A);       \
+        } else {                                                                                  \
+            if (A.uni) MG_LAUNCH((k_artic_chain<NL, false, true>), dim3(cb), dim3(64), 0, s, P, A); \
+            else MG_LAUNCH((k_artic_chain<NL, false, false>), dim3(cb), dim3(64), 0, s, P, A);      \
+        }                                                                                         \
     } while (0)
     if (A.nl == 2) MG_KC(2);
     else if (A.nl == 3) MG_KC(3);

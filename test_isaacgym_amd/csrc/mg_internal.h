@@ -105,6 +105,10 @@ struct MgArticArgs {
     const float* dof_props;   // [12][nd]
     const float* ext;         // [6][nb] or null
     float*       cforce;      // [3][nb]
+    // k_artic_chain: the launch's shared constants (MG_CHAIN_UNI_N floats,
+    // mg_chainlink.h) when every instance has the same DOF properties, link mass
+    // rows and gravity flag, else null
+    const float* uni;
     // refresh fused into the step (MG_FUSE_STEP_OUT, k_artic_chain): the bound
     // tensors the kernel writes itself, or null
     float*       out_rb;      // [nb][13] rigid-body tensor (global body order)

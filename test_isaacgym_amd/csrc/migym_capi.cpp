@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "mg_internal.h"
+#include "mg_chainlink.h"
 
 thread_local MgKernelTimer* mg_timer = nullptr;
 
@@ -57,6 +58,13 @@ std::vector<T> to_soa(const T* aos, int n, int ncol) {
 
 struct ArticGroup {
     int chain;                     // serial chain with one DOF per moving link (MgArticArgs.chain)
+    // k_artic_chain's shared constants (mg_chainlink.h): the stepped instances'
+    // global first body / first DOF, whether their link mass rows and gravity
+    // flags agree (set at upload), whether their DOF properties agree (upload
+    // and mg_set_dof_props), the constants themselves
+    std::vector<int> step_body0, step_dof0;
+    bool uni_mass = false, uni_dof = false;
+    float uni[MG_CHAIN_UNI_N] = {};
     int tmpl, first_link, nl, ndof, fixed_base;
     int nbody;                     // bodies per instance (nl minus the virtual links of ball joints)
     int offset, count;             // into the template-sorted instance list (all instances)
@@ -149,6 +157,7 @@ struct mg_sim {
     int* d_pairs = nullptr;       // [..][4] candidate shape pairs of the coupled envs
     float* d_fpatch = nullptr;    // [pairs][MG_FP_N] friction patch records (coupled step, persistent)
     float* d_gpatch = nullptr;    // [MG_FP_N][nf1] ground patches of the single-shape free bodies (persistent)
+    float* d_chain_uni = nullptr; // [groups][MG_CHAIN_UNI_N] shared constants of chain groups (ArticGroup.uni)
     unsigned* d_fp_mask = nullptr;   // [n_coupled][MG_FP_W] pairs holding a patch
     int n_coupled = 0;
     std::vector<EnvGroup> env_groups;
@@ -366,7 +375,7 @@ void shape_obb(const float* sh, const float* hulls, float* o) {
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls, s->d_shape_obb,
                     s->d_actor_root, s->d_root_row, s->d_slot_global, s->d_slot_actor, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
-                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_fp_mask, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
+                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_chain_uni, s->d_fp_mask, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
                     s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -429,6 +438,54 @@ int32_t mg_set_sim_params(mg_sim* s, const mg_sim_params* p) {
     if (!s || !p) return fail(MG_ERR_ARG, "null argument");
     s->params = *p;
     return MG_OK;
+}
+
+// k_artic_chain's shared constants (mg_chainlink.h). Link mass constants and
+// the gravity flag: from the stepped instances' global rows, when they all
+// agree (set once: mass properties are fixed after upload).
+static void chain_uni_mass(const mg_model* m, ArticGroup& g) {
+    const int b0 = g.step_body0[0];
+    bool ok = true;
+    const float grav = m->tmpl_body_f[(size_t)m->body_tmpl[b0] * MG_TBODY_F_N + 4];
+    for (size_t i = 1; i < g.step_body0.size() && ok; ++i) {
+        const int bi = g.step_body0[i];
+        ok = m->tmpl_body_f[(size_t)m->body_tmpl[bi] * MG_TBODY_F_N + 4] == grav;
+        for (int l = 1; l < g.nl && ok; ++l)
+            ok = std::memcmp(m->body_mass + (size_t)(bi + l) * MG_MASS_N, m->body_mass + (size_t)(b0 + l) * MG_MASS_N,
+                             MG_MASS_N * sizeof(float)) == 0;
+    }
+    g.uni_mass = ok;
+    if (!ok) return;
+    for (int l = 1; l < g.nl; ++l) {
+        const float* r = m->body_mass + (size_t)(b0 + l) * MG_MASS_N;
+        const ChainLink k = chain_link_make(r[11], v3(r[8], r[9], r[10]), r[1], r[2], r[3], q4(r[4], r[5], r[6], r[7]));
+        float* u = g.uni + MG_CHAIN_UNI_LINK + 10 * (l - 1);
+        u[0] = k.m;
+        u[1] = k.com.x; u[2] = k.com.y; u[3] = k.com.z;
+        for (int j = 0; j < 6; ++j) u[4 + j] = k.ib[j];
+    }
+    g.uni[MG_CHAIN_UNI_GRAV] = grav;
+}
+// DOF properties (global DOF order, MG_DOFPROP_N per DOF): fields 0..8 of each
+// DOF of the chain, when every stepped instance has the same
+static void chain_uni_dof(const float* props, ArticGroup& g) {
+    const int d0 = g.step_dof0[0];
+    bool ok = true;
+    for (size_t i = 1; i < g.step_dof0.size() && ok; ++i)
+        for (int d = 0; d < g.ndof && ok; ++d)
+            ok = std::memcmp(props + (size_t)(g.step_dof0[i] + d) * MG_DOFPROP_N, props + (size_t)(d0 + d) * MG_DOFPROP_N,
+                             9 * sizeof(float)) == 0;
+    g.uni_dof = ok;
+    if (!ok) return;
+    for (int d = 0; d < g.ndof; ++d)
+        for (int j = 0; j < 9; ++j) g.uni[MG_CHAIN_UNI_DOF + 9 * d + j] = props[(size_t)(d0 + d) * MG_DOFPROP_N + j];
+}
+static hipError_t chain_uni_upload(mg_sim* s) {
+    if (!s->d_chain_uni) return hipSuccess;
+    std::vector<float> u(s->groups.size() * MG_CHAIN_UNI_N, 0.0f);
+    for (size_t i = 0; i < s->groups.size(); ++i)
+        std::memcpy(&u[i * MG_CHAIN_UNI_N], s->groups[i].uni, MG_CHAIN_UNI_N * sizeof(float));
+    return hipMemcpy(s->d_chain_uni, u.data(), u.size() * sizeof(float), hipMemcpyHostToDevice);
 }
 
 int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
@@ -756,6 +813,8 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
             if (!cpl) {
                 for (int j = 0; j < MG_ARTIC_I_N; ++j) artic_step.push_back(j == 3 ? 1 : ai[j]);
                 g.step_count++;
+                g.step_body0.push_back(ai[0]);
+                g.step_dof0.push_back(ai[1]);
             }
             for (int l = 0; l < g.nbody; ++l) {
                 if (placed[ai[0] + l]) return fail(MG_ERR_ARG, "articulation %d overlaps another body", k);
@@ -776,6 +835,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         if (!g.fixed_base && g.step_count > 0)
             return fail(MG_ERR_UNSUPPORTED, "articulation template %d: a floating base steps in the coupled "
                         "per-env kernel, which needs actor_coll", t);
+        if (blocked && g.step_count > 0) chain_uni_mass(m, g);
         s->groups.push_back(g);
     }
 
@@ -966,6 +1026,10 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         std::vector<float> dp = to_soa(m->dof_props, nd, MG_DOFPROP_N);
         HIP_TRY(h2d(s->d_dof_props, dp.data(), dp.size() * sizeof(float)));
     }
+    for (ArticGroup& g : s->groups)
+        if (g.uni_mass) chain_uni_dof(m->dof_props, g);
+    HIP_TRY(dalloc(&s->d_chain_uni, std::max<size_t>(s->groups.size(), 1) * MG_CHAIN_UNI_N));
+    HIP_TRY(chain_uni_upload(s));
     HIP_TRY(h2d(s->d_artic, artic_sorted.data(), artic_sorted.size() * sizeof(int)));
     HIP_TRY(h2d(s->d_artic_step, artic_step.data(), artic_step.size() * sizeof(int)));
     HIP_TRY(h2d(s->d_env, env_flat.data(), env_flat.size() * sizeof(int)));
@@ -1046,9 +1110,11 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     const unsigned long long step_cid = capture_id(st);
     const bool step_out = (s->fusion & MG_FUSE_STEP_OUT) && fuse_here(s, step_cid) && s->step_out_ok &&
                           (s->bind_root || s->bind_rb || s->bind_dof);
-    for (const ArticGroup& g : s->groups) {
+    for (size_t gi = 0; gi < s->groups.size(); ++gi) {
+        const ArticGroup& g = s->groups[gi];
         if (g.step_count == 0) continue;
         MgArticArgs A{};
+        A.uni = g.uni_mass && g.uni_dof ? s->d_chain_uni + gi * MG_CHAIN_UNI_N : nullptr;
         A.na = g.step_count; A.nb = s->nb; A.nd = s->nd;
         A.artic_i = s->d_artic_step + (size_t)g.step_offset * MG_ARTIC_I_N;
         A.tmpl = g.tmpl; A.nl = g.nl; A.ndof = g.ndof; A.fixed_base = g.fixed_base; A.chain = g.chain; A.nbl = g.nbody;
@@ -1382,6 +1448,9 @@ int32_t mg_set_dof_props(mg_sim* s, const float* props_host) {
     HIP_TRY(hipSetDevice(s->device));
     std::vector<float> dp = to_soa(props_host, s->nd, MG_DOFPROP_N);
     HIP_TRY(hipMemcpy(s->d_dof_props, dp.data(), dp.size() * sizeof(float), hipMemcpyHostToDevice));
+    for (ArticGroup& g : s->groups)
+        if (g.uni_mass) chain_uni_dof(props_host, g);
+    HIP_TRY(chain_uni_upload(s));
     return MG_OK;
 }
 
