@@ -854,8 +854,13 @@ static clink_t chain_link_(const float* M) {
     k.ib[5] = fmaf(u0.y, R.c0.z, fmaf(u1.y, R.c1.z, u2.y * R.c2.z));
     return k;
 }
-static ri_t world_ri_(const clink_t* K, q4_t ql, v3_t xl, v3_t x0, v3_t* cout) {
-    const m3_t R = qmat_(ql);
+/* R v, one fused chain per component (mg_chain.hip rmul) */
+static v3_t rmul_(const m3_t* R, v3_t v) {
+    return V(fmaf(R->c2.x, v.z, fmaf(R->c1.x, v.y, R->c0.x * v.x)), fmaf(R->c2.y, v.z, fmaf(R->c1.y, v.y, R->c0.y * v.x)),
+             fmaf(R->c2.z, v.z, fmaf(R->c1.z, v.y, R->c0.z * v.x)));
+}
+static ri_t world_ri_(const clink_t* K, const m3_t* Rm, v3_t xl, v3_t x0, v3_t* cout) {
+    const m3_t R = *Rm;
     const float* b = K->ib;
     const float ib[3][3] = {{b[0], b[3], b[4]}, {b[3], b[1], b[5]}, {b[4], b[5], b[2]}};
     const float r[3][3] = {{R.c0.x, R.c1.x, R.c2.x}, {R.c0.y, R.c1.y, R.c2.y}, {R.c0.z, R.c1.z, R.c2.z}};
@@ -866,7 +871,7 @@ static ri_t world_ri_(const clink_t* K, q4_t ql, v3_t xl, v3_t x0, v3_t* cout) {
     for (i = 0; i < 3; ++i)
         for (j = 0; j < 3; ++j) t[i][j] = fmaf(r[i][2], ib[2][j], fmaf(r[i][1], ib[1][j], r[i][0] * ib[0][j]));
 #define OR_IC(i, j) fmaf(t[i][2], r[j][2], fmaf(t[i][1], r[j][1], t[i][0] * r[j][0]))
-    c = sub3(add3(xl, qrot_(ql, K->com)), x0);
+    c = sub3(add3(xl, rmul_(Rm, K->com)), x0);
     h = mul3(c, K->m);
     I.xx = fmaf(h.y, c.y, fmaf(h.z, c.z, OR_IC(0, 0)));
     I.yy = fmaf(h.x, c.x, fmaf(h.z, c.z, OR_IC(1, 1)));
@@ -880,18 +885,21 @@ static ri_t world_ri_(const clink_t* K, q4_t ql, v3_t xl, v3_t x0, v3_t* cout) {
     *cout = c;
     return I;
 }
-static void chain_fk_(const float* lf, int jt, float qj, q4_t qp, v3_t xp, q4_t* ql, v3_t* xl) {
+/* link pose from the parent's (orientation qp, rotation matrix Rp, origin xp);
+ * norm: renormalise (the output pass only, mg_chain.hip chain_fk<NORM>) */
+static void chain_fk_(const float* lf, int jt, float qj, q4_t qp, const m3_t* Rp, v3_t xp, int norm, q4_t* ql,
+                      v3_t* xl) {
     const v3_t po = V(lf[0], lf[1], lf[2]), ax = V(lf[7], lf[8], lf[9]);
     const q4_t qo = Q(lf[3], lf[4], lf[5], lf[6]);
     q4_t qrel = qo;
     v3_t rr = po;
     if (jt == MG_JOINT_REVOLUTE) qrel = qmul_(qo, qaxang_(ax, qj));
     else if (jt == MG_JOINT_PRISMATIC) rr = add3(po, qrot_(qo, mul3(ax, qj)));
-    *ql = qnorm_(qmul_(qp, qrel));
-    *xl = add3(xp, qrot_(qp, rr));
+    *ql = norm ? qnorm_(qmul_(qp, qrel)) : qmul_(qp, qrel);
+    *xl = add3(xp, rmul_(Rp, rr));
 }
-static sv_t chain_axis_(const float* lf, int jt, q4_t ql, v3_t xl, v3_t x0) {
-    const v3_t z = qrot_(ql, V(lf[7], lf[8], lf[9]));
+static sv_t chain_axis_(const float* lf, int jt, const m3_t* R, v3_t xl, v3_t x0) {
+    const v3_t z = rmul_(R, V(lf[7], lf[8], lf[9]));
     return jt == MG_JOINT_REVOLUTE ? SVc(z, fcross_(sub3(xl, x0), z)) : SVc(V(0.0f, 0.0f, 0.0f), z);
 }
 static void chain_drive_(const float* pr, const float* tg, float q, float u, float h, int xm, int xp,
@@ -963,6 +971,7 @@ static void chain_step_(const step_t* P, const mg_model* m, const float* LF, con
     const float* s0 = state + (size_t)b0 * MG_STATE_N;
     const v3_t x0 = V(s0[0], s0[1], s0[2]);
     const q4_t q0 = qnorm_(Q(s0[3], s0[4], s0[5], s0[6]));
+    const m3_t R0 = qmat_(q0);
     const float grav_on = m->tmpl_body_f[(size_t)m->body_tmpl[b0] * MG_TBODY_F_N + 4];
     const v3_t gw = grav_on != 0.0f ? V(P->g[0], P->g[1], P->g[2]) : V(0.0f, 0.0f, 0.0f);
     float qv[3], uv[3], arm[3];
@@ -976,11 +985,11 @@ static void chain_step_(const step_t* P, const mg_model* m, const float* LF, con
     for (l = 1; l < L; ++l) lk[l] = chain_link_(m->body_mass + (size_t)(b0 + l) * MG_MASS_N);
     for (st_ = 0; st_ < P->substeps; ++st_) {
         sv_t xi[3];
-        ri_t Il[3];
         float Cb[3], M[3][3], qdd[3], tau0[3], imp[3], rhs[3];
         int xm[3], xpl[3], flip = 0;
         {
             q4_t qp = q0;
+            m3_t Rp = R0;
             v3_t xp = x0;
             sv_t vp = sv0(), ap = SVc(V(0.0f, 0.0f, 0.0f), V(-gw.x, -gw.y, -gw.z));
             for (l = 1; l < L; ++l) {
@@ -990,12 +999,14 @@ static void chain_step_(const step_t* P, const mg_model* m, const float* LF, con
                 v3_t xl, c;
                 sv_t x, vJ, v, acc, f;
                 ri_t I;
-                chain_fk_(lf, jt, qv[l - 1], qp, xp, &ql, &xl);
-                x = chain_axis_(lf, jt, ql, xl, x0);
+                m3_t Rl;
+                chain_fk_(lf, jt, qv[l - 1], qp, &Rp, xp, 0, &ql, &xl);
+                Rl = qmat_(ql);
+                x = chain_axis_(lf, jt, &Rl, xl, x0);
                 vJ = svmul_(x, uv[l - 1]);
                 v = svadd_(vp, vJ);
                 acc = svadd_(ap, crm_f_(v, vJ));
-                I = world_ri_(&lk[l], ql, xl, x0, &c);
+                I = world_ri_(&lk[l], &Rl, xl, x0, &c);
                 {
                     const sv_t Iv = ri_mul_(&I, v);
                     f = svadd_(ri_mul_(&I, acc), crf_f_(v, Iv));
@@ -1006,18 +1017,17 @@ static void chain_step_(const step_t* P, const mg_model* m, const float* LF, con
                     f = SVc(sub3(f.w, add3(te, cross3(c, fe))), sub3(f.v, fe));
                 }
                 xi[l - 1] = x;
-                Il[l - 1] = I;
                 for (j = 0; j < l; ++j) Cb[j] = j == l - 1 ? sdot_(x, f) : Cb[j] + sdot_(xi[j], f);
-                qp = ql; xp = xl; vp = v; ap = acc;
-            }
-        }
-        {
-            ri_t IC = Il[D - 1];
-            for (j = D - 1; j >= 0; --j) {
-                sv_t Fm;
-                if (j < D - 1) IC = ri_add_(&Il[j], &IC);
-                Fm = ri_mul_(&IC, xi[j]);
-                for (i = 0; i <= j; ++i) M[i][j] = sdot_(xi[i], Fm);
+                /* joint-space inertia accumulated link by link (mg_chain.hip):
+                 * link l - 1 adds xi_i . (I xi_j) to M_ij for i <= j <= l - 1 */
+                for (j = 0; j < l; ++j) {
+                    const sv_t Fm = ri_mul_(&I, xi[j]);
+                    for (i = 0; i <= j; ++i) {
+                        const float mij = sdot_(xi[i], Fm);
+                        M[i][j] = j == l - 1 ? mij : M[i][j] + mij;
+                    }
+                }
+                qp = ql; Rp = Rl; xp = xl; vp = v; ap = acc;
             }
         }
         for (d = 0; d < D; ++d) {
@@ -1060,6 +1070,7 @@ static void chain_step_(const step_t* P, const mg_model* m, const float* LF, con
     for (d = 0; d < D; ++d) { dof[(d0 + d) * 2 + 0] = qv[d]; dof[(d0 + d) * 2 + 1] = uv[d]; }
     {
         q4_t qp = q0;
+        m3_t Rp = R0;
         v3_t xp = x0;
         sv_t vp = sv0();
         for (l = 0; l < L; ++l) {
@@ -1071,12 +1082,14 @@ static void chain_step_(const step_t* P, const mg_model* m, const float* LF, con
                 const int jt = LI[l * MG_LINK_I_N + 1];
                 sv_t v;
                 v3_t cw;
-                chain_fk_(lf, jt, qv[l - 1], qp, xp, &ql, &xl);
-                v = svadd_(vp, svmul_(chain_axis_(lf, jt, ql, xl, x0), uv[l - 1]));
-                cw = add3(sub3(xl, x0), qrot_(ql, lk[l].com));
+                m3_t Rl;
+                chain_fk_(lf, jt, qv[l - 1], qp, &Rp, xp, 1, &ql, &xl);
+                Rl = qmat_(ql);
+                v = svadd_(vp, svmul_(chain_axis_(lf, jt, &Rl, xl, x0), uv[l - 1]));
+                cw = add3(sub3(xl, x0), rmul_(&Rl, lk[l].com));
                 ww = v.w;
                 vw = add3(v.v, fcross_(v.w, cw));
-                qp = ql; xp = xl; vp = v;
+                qp = ql; Rp = Rl; xp = xl; vp = v;
             }
             so[0] = xl.x; so[1] = xl.y; so[2] = xl.z;
             so[3] = ql.x; so[4] = ql.y; so[5] = ql.z; so[6] = ql.w;

@@ -13,8 +13,8 @@
 //     and its bias force f_l = I_l a_l + v_l x* I_l v_l - f_ext;
 //     and the bias C_j += xi_j . f_l for j <= l (recursive Newton-Euler at
 //     qdd = 0: C_j = xi_j . sum_{k >= j} f_k, in the order the f_k appear);
-//   backward, l = D..1: composite inertia IC_l = I_l + IC_{l+1} (a sum of rigid
-//     inertias is again compact), F = IC_l xi_l, M_il = xi_i . F (i <= l);
+//   and the joint-space inertia M_ij = xi_i . IC_j xi_j (IC_j = sum_{k >= j} I_k)
+//     accumulated in the same pass: link k adds xi_i . (I_k xi_j) for i <= j <= k;
 //   (M + diag(armature + h kd + h^2 kp)) qdd = tau0 - C by LDL^T: the implicit
 //     PD drive of §3.3, exact for the linearised drive; a drive whose implicit
 //     torque tau0 - (h kd + h^2 kp) qdd exceeds its effort limit is re-solved as
@@ -93,9 +93,15 @@ __device__ __forceinline__ ChainLink load_chain_link(const float* Ms, int nb, in
                            q4(fld(Ms, 4, nb, b), fld(Ms, 5, nb, b), fld(Ms, 6, nb, b), fld(Ms, 7, nb, b)));
 }
 
+// R v, one fused chain per component (the link's rotation matrix R = qmat(ql)
+// is formed once per link and pass, and rotates the COM, the joint axis and the
+// child's joint offset: three quaternion rotations fewer per link)
+__device__ __forceinline__ V3 rmul(const M3& R, V3 v) {
+    return v3(fmaf(R.c2.x, v.z, fmaf(R.c1.x, v.y, R.c0.x * v.x)), fmaf(R.c2.y, v.z, fmaf(R.c1.y, v.y, R.c0.y * v.x)),
+              fmaf(R.c2.z, v.z, fmaf(R.c1.z, v.y, R.c0.z * v.x)));
+}
 // the link's rigid inertia about x0 (world axes); c = its COM - x0
-__device__ __forceinline__ RI world_ri(const ChainLink& K, Q4 ql, V3 xl, V3 x0, V3& c) {
-    const M3 R = qmat(ql);
+__device__ __forceinline__ RI world_ri(const ChainLink& K, const M3& R, V3 xl, V3 x0, V3& c) {
     // T = R Ib (rows of R: (c0.i, c1.i, c2.i)), Ic = T R^T
     const float* b = K.ib;   // xx yy zz xy xz yz
     const float ib[3][3] = {{b[0], b[3], b[4]}, {b[3], b[1], b[5]}, {b[4], b[5], b[2]}};
@@ -106,7 +112,7 @@ __device__ __forceinline__ RI world_ri(const ChainLink& K, Q4 ql, V3 xl, V3 x0, 
 #pragma unroll
         for (int j = 0; j < 3; ++j) t[i][j] = fmaf(r[i][2], ib[2][j], fmaf(r[i][1], ib[1][j], r[i][0] * ib[0][j]));
 #define MG_IC(i, j) fmaf(t[i][2], r[j][2], fmaf(t[i][1], r[j][1], t[i][0] * r[j][0]))
-    c = vsub(vadd(xl, qrot(ql, K.com)), x0);
+    c = vsub(vadd(xl, rmul(R, K.com)), x0);
     const V3 h = vscale(c, K.m);
     RI I;
     // R Ib R^T + m (|c|^2 1 - c c^T)
@@ -122,18 +128,23 @@ __device__ __forceinline__ RI world_ri(const ChainLink& K, Q4 ql, V3 xl, V3 x0, 
     return I;
 }
 
-// link l's pose from its parent's: joint rotation / offset at DOF position qj
-__device__ __forceinline__ void chain_fk(int jt, V3 po, Q4 qo, V3 ax, float qj, Q4 qp, V3 xp, Q4& ql, V3& xl) {
+// link l's pose from its parent's (orientation qp, rotation matrix Rp, origin
+// xp): joint rotation / offset at DOF position qj. Inside the substeps the
+// orientation is not renormalised (it is rebuilt from the joint angles and the
+// unit base orientation every pass: no drift); the output pass (NORM) is.
+template <bool NORM>
+__device__ __forceinline__ void chain_fk(int jt, V3 po, Q4 qo, V3 ax, float qj, Q4 qp, const M3& Rp, V3 xp, Q4& ql,
+                                         V3& xl) {
     Q4 qrel = qo;
     V3 rr = po;
     if (jt == MG_JOINT_REVOLUTE) qrel = qmul(qo, q_axis_angle(ax, qj));
     else if (jt == MG_JOINT_PRISMATIC) rr = vadd(po, qrot(qo, vscale(ax, qj)));
-    ql = qnormalize(qmul(qp, qrel));
-    xl = vadd(xp, qrot(qp, rr));
+    ql = NORM ? qnormalize(qmul(qp, qrel)) : qmul(qp, qrel);
+    xl = vadd(xp, rmul(Rp, rr));
 }
-// joint l's motion axis about x0
-__device__ __forceinline__ SV chain_axis(int jt, V3 ax, Q4 ql, V3 xl, V3 x0) {
-    const V3 z = qrot(ql, ax);
+// joint l's motion axis about x0 (R: the link's rotation matrix)
+__device__ __forceinline__ SV chain_axis(int jt, V3 ax, const M3& R, V3 xl, V3 x0) {
+    const V3 z = rmul(R, ax);
     return jt == MG_JOINT_REVOLUTE ? sv(z, fcross(vsub(xl, x0), z)) : sv(v3(0.0f, 0.0f, 0.0f), z);
 }
 
@@ -252,6 +263,7 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
     }
     const V3 x0 = v3(fld(St, 0, nb, b0), fld(St, 1, nb, b0), fld(St, 2, nb, b0));
     const Q4 q0 = qnormalize(q4(fld(St, 3, nb, b0), fld(St, 4, nb, b0), fld(St, 5, nb, b0), fld(St, 6, nb, b0)));
+    const M3 R0 = qmat(q0);
     const float gflag = UNI ? AA.uni[MG_CHAIN_UNI_GRAV] : AA.tbf[fld(AA.body_tmpl, 0, 0, b0) * MG_TBODY_F_N + 4];
     const V3 gw = gflag != 0.0f ? v3(P.g[0], P.g[1], P.g[2]) : v3(0.0f, 0.0f, 0.0f);
     float qv[D], uv[D], arm[D];
@@ -307,12 +319,17 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
     }
 
     for (int st = 0; st < P.substeps; ++st) {
-        // ---- forward: poses, axes, velocities, inertias, bias forces
+        // ---- forward: poses, axes, velocities, inertias, bias forces, and the
+        // joint-space inertia accumulated link by link: link k's rigid inertia
+        // I_k adds xi_i . (I_k xi_j) to M_ij for i <= j <= k (M_ij = xi_i . IC_j
+        // xi_j with IC_j = sum_{k >= j} I_k, summed over k in link order), so no
+        // inertia is kept past its own link (registers: three waves per SIMD)
         SV xi[D];
-        RI Il[D];
         float Cb[D];   // bias C_j = xi_j . sum_{k >= j} f_k, accumulated as f_k appears
+        float M[D][D];
         {
             Q4 qp = q0;
+            M3 Rp = R0;
             V3 xp = x0;
             SV vp = svzero();
             SV ap = sv(v3(0.0f, 0.0f, 0.0f), v3(-gw.x, -gw.y, -gw.z));
@@ -320,13 +337,14 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
             for (int l = 1; l < NL; ++l) {
                 Q4 ql;
                 V3 xl;
-                chain_fk(jt[l], po[l], qo[l], ax[l], qv[l - 1], qp, xp, ql, xl);
-                const SV x = chain_axis(jt[l], ax[l], ql, xl, x0);
+                chain_fk<false>(jt[l], po[l], qo[l], ax[l], qv[l - 1], qp, Rp, xp, ql, xl);
+                const M3 Rl = qmat(ql);
+                const SV x = chain_axis(jt[l], ax[l], Rl, xl, x0);
                 const SV vJ = svscale(x, uv[l - 1]);
                 const SV v = svadd(vp, vJ);
                 const SV acc = svadd(ap, crm_f(v, vJ));
                 V3 c;
-                const RI I = world_ri(lk[l], ql, xl, x0, c);
+                const RI I = world_ri(lk[l], Rl, xl, x0, c);
                 SV f = svadd(ri_mul(I, acc), crf_f(v, ri_mul(I, v)));
                 if constexpr (EXT) {   // external wrench at the COM (apply_rigid_body_force_tensors)
                     const int b = b0 + l * ls;
@@ -335,25 +353,22 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
                     f = sv(vsub(f.w, vadd(te, vcross(c, fe))), vsub(f.v, fe));
                 }
                 xi[l - 1] = x;
-                Il[l - 1] = I;
 #pragma unroll
                 for (int j = 0; j < l; ++j) Cb[j] = j == l - 1 ? sdot(x, f) : Cb[j] + sdot(xi[j], f);
+#pragma unroll
+                for (int j = 0; j < l; ++j) {
+                    const SV Fm = ri_mul(I, xi[j]);
+#pragma unroll
+                    for (int i = 0; i <= j; ++i) {
+                        const float mij = sdot(xi[i], Fm);
+                        M[i][j] = j == l - 1 ? mij : M[i][j] + mij;
+                    }
+                }
                 qp = ql;
+                Rp = Rl;
                 xp = xl;
                 vp = v;
                 ap = acc;
-            }
-        }
-        // ---- backward: composite inertias -> joint-space inertia M, bias C
-        float M[D][D];
-        {
-            RI IC = Il[D - 1];
-#pragma unroll
-            for (int j = D - 1; j >= 0; --j) {
-                if (j < D - 1) IC = ri_add(Il[j], IC);
-                const SV Fm = ri_mul(IC, xi[j]);
-#pragma unroll
-                for (int i = 0; i <= j; ++i) M[i][j] = sdot(xi[i], Fm);
             }
         }
         // ---- drives and the solve; one re-solve with effort-limited drives
@@ -418,9 +433,25 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
             for (int k = 0; k < 2 * D; ++k) R[k] = o[k];
         }
     }
-    float rows[NL * MG_STATE_N];
+    // link states by forward kinematics at (q, qd), each link's row stored as
+    // soon as it is formed: into the SoA state and, with the refresh fused into
+    // the step, into the bound rigid-body rows (the articulation's bodies are
+    // consecutive rows: 16-B stores streamed across the link boundaries, at most
+    // 3 floats carried to the next link) and the base's actor-root row
+    float* orb = nullptr;
+    bool contiguous = false;
+    if (AA.out_rb) {
+        const int g0 = fld(AA.out_body, 0, 0, b0);
+        contiguous = true;
+#pragma unroll
+        for (int l = 1; l < NL; ++l) contiguous = contiguous && fld(AA.out_body, 0, 0, b0 + l * ls) == g0 + l;
+        orb = AA.out_rb + (size_t)g0 * MG_STATE_N;
+        contiguous = contiguous && (reinterpret_cast<uintptr_t>(orb) & 15) == 0;
+    }
+    float carry[3] = {0.0f, 0.0f, 0.0f};
     {
         Q4 qp = q0;
+        M3 Rp = R0;
         V3 xp = x0;
         SV vp = svzero();
 #pragma unroll
@@ -429,51 +460,59 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
             V3 xl = x0;
             V3 ww = v3(0.0f, 0.0f, 0.0f), vw = v3(0.0f, 0.0f, 0.0f);
             if (l > 0) {
-                chain_fk(jt[l], po[l], qo[l], ax[l], qv[l - 1], qp, xp, ql, xl);
-                const SV v = svadd(vp, svscale(chain_axis(jt[l], ax[l], ql, xl, x0), uv[l - 1]));
+                chain_fk<true>(jt[l], po[l], qo[l], ax[l], qv[l - 1], qp, Rp, xp, ql, xl);
+                const M3 Rl = qmat(ql);
+                const SV v = svadd(vp, svscale(chain_axis(jt[l], ax[l], Rl, xl, x0), uv[l - 1]));
                 // COM velocity: v_O + w x (COM - x0)
-                const V3 cw = vadd(vsub(xl, x0), qrot(ql, lk[l].com));
+                const V3 cw = vadd(vsub(xl, x0), rmul(Rl, lk[l].com));
                 ww = v.w;
                 vw = vadd(v.v, fcross(v.w, cw));
                 qp = ql;
+                Rp = Rl;
                 xp = xl;
                 vp = v;
             }
             const int b = b0 + l * ls;
-            float* r = rows + l * MG_STATE_N;
-            r[0] = xl.x; r[1] = xl.y; r[2] = xl.z;
-            r[3] = ql.x; r[4] = ql.y; r[5] = ql.z; r[6] = ql.w;
-            r[7] = vw.x; r[8] = vw.y; r[9] = vw.z;
-            r[10] = ww.x; r[11] = ww.y; r[12] = ww.z;
+            const float r[MG_STATE_N] = {xl.x, xl.y, xl.z, ql.x, ql.y, ql.z, ql.w, vw.x, vw.y, vw.z, ww.x, ww.y, ww.z};
 #pragma unroll
             for (int k = 0; k < MG_STATE_N; ++k) fld(St, k, nb, b) = r[k];
-        }
-    }
-    // the refresh fused into the step: rigid-body rows (the articulation's
-    // bodies are consecutive rows of the tensor) and the base's actor-root row
-    if (AA.out_rb) {
-        const int g0 = fld(AA.out_body, 0, 0, b0);
-        bool contiguous = true;
+            if (AA.out_rb) {
+                if (contiguous) {
+                    // this link's floats after the carried ones: whole float4s
+                    // from the row start (l * 13 floats in), the rest carried
+                    const int c0 = (l * MG_STATE_N) & 3;               // floats carried in
+                    const int n = c0 + MG_STATE_N;                      // floats pending
+                    const int f4 = n / 4;                               // float4 stores now
+                    float* dst = orb + (l * MG_STATE_N - c0);
+                    auto pend = [&](int i) { return i < c0 ? carry[i] : r[i - c0]; };
 #pragma unroll
-        for (int l = 1; l < NL; ++l) contiguous = contiguous && fld(AA.out_body, 0, 0, b0 + l * ls) == g0 + l;
-        if (contiguous) {
-            store_row(AA.out_rb + (size_t)g0 * MG_STATE_N, rows);
-        } else {
+                    for (int k = 0; k < f4; ++k)
+                        *reinterpret_cast<float4*>(dst + 4 * k) =
+                            make_float4(pend(4 * k), pend(4 * k + 1), pend(4 * k + 2), pend(4 * k + 3));
 #pragma unroll
-            for (int l = 0; l < NL; ++l) {
-                float* R = AA.out_rb + (size_t)fld(AA.out_body, 0, 0, b0 + l * ls) * MG_STATE_N;
+                    for (int i = 0; i < n - 4 * f4; ++i) carry[i] = pend(4 * f4 + i);
+                } else {
+                    float* R = AA.out_rb + (size_t)fld(AA.out_body, 0, 0, b) * MG_STATE_N;
 #pragma unroll
-                for (int k = 0; k < MG_STATE_N; ++k) R[k] = rows[l * MG_STATE_N + k];
+                    for (int k = 0; k < MG_STATE_N; ++k) R[k] = r[k];
+                }
+            }
+            if (l == 0 && AA.out_root) {
+                const int rr = fld(AA.out_root_row, 0, 0, b0);
+                if (rr >= 0) {
+                    float* R = AA.out_root + (size_t)rr * MG_STATE_N;
+#pragma unroll
+                    for (int k = 0; k < MG_STATE_N; ++k) R[k] = r[k];
+                }
             }
         }
     }
-    if (AA.out_root) {
-        const int rr = fld(AA.out_root_row, 0, 0, b0);
-        if (rr >= 0) {
-            float* R = AA.out_root + (size_t)rr * MG_STATE_N;
+    // NL * 13 floats end on a float4 boundary only for NL = 4: the last link's
+    // remaining floats (NL < 4)
+    if (AA.out_rb && contiguous) {
+        constexpr int rem = (NL * MG_STATE_N) & 3;
 #pragma unroll
-            for (int k = 0; k < MG_STATE_N; ++k) R[k] = rows[k];
-        }
+        for (int i = 0; i < rem; ++i) orb[NL * MG_STATE_N - rem + i] = carry[i];
     }
 }
 
