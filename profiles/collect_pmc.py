@@ -29,7 +29,8 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
-        for key in ("k_rigid_step", "k_scatter_rows", "k_gather_rows", "k_artic_step", "k_artic_chain"):
+        for key in ("k_rigid_step", "k_scatter_rows", "k_gather_rb_root", "k_gather_rows", "k_artic_step",
+                    "k_artic_chain", "k_env_step"):
             if key in name:
                 name = key
         acc[name].append(float(r["Counter_Value"]))
@@ -67,6 +68,16 @@ def main():
     factor = known_read / (f["k_scatter_rows"] * 1024.0)
     rigid_read = f["k_rigid_step"] * 1024.0 * factor
     rigid_write = w["k_rigid_step"] * 1024.0
+    # WRITE_SIZE calibration: the paired refresh gather of
+    # the calibration sets writes the (2N, 13) root rows and the (2N, 13)
+    # rigid-body rows, 52-B rows in order (the same row pattern the fused step
+    # writes), a known volume
+    wcal = None
+    if "k_gather_rb_root" in w:
+        known_write = 2 * actors * 13 * 4
+        wcal = {"kernel": "k_gather_rb_root", "known_bytes": known_write,
+                "write_size_bytes": w["k_gather_rb_root"] * 1024.0,
+                "write_factor": known_write / (w["k_gather_rb_root"] * 1024.0)}
     res = {
         "envs": envs,
         "kernel": "k_rigid_step",
@@ -76,6 +87,7 @@ def main():
         "calibration": "k_scatter_rows reads %d B per launch; FETCH_SIZE %.1f KiB" % (known_read,
                                                                                    f["k_scatter_rows"]),
         "hbm_bytes_per_launch": rigid_read + rigid_write,
+        "write_calibration": wcal,
         "algorithmic_bytes_per_launch": bpe * envs,
         "algorithmic_bytes_per_env": bpe,
         "launches": nf["k_rigid_step"],
