@@ -43,18 +43,22 @@ struct PairOut {
     float sep[MG_PAIR_MAXC];
 };
 
+MG_HD V3 m3col(const M3& R, int i) { return vsel(i == 0, R.c0, vsel(i == 1, R.c1, R.c2)); }
 MG_HD float m3c(const M3& R, int i, int k) {      // component k of column i
-    const V3 c = i == 0 ? R.c0 : (i == 1 ? R.c1 : R.c2);
+    const V3 c = m3col(R, i);
     return k == 0 ? c.x : (k == 1 ? c.y : c.z);
 }
-MG_HD V3 m3col(const M3& R, int i) { return i == 0 ? R.c0 : (i == 1 ? R.c1 : R.c2); }
 MG_HD float v3c(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
 // static slot writes (no dynamic indexing: the record stays in registers)
 MG_HD void pair_push(PairOut& o, V3 p, V3 n, float sep) {
 #pragma unroll
-    for (int k = 0; k < MG_PAIR_MAXC; ++k)
-        if (o.n == k) { o.p[k] = p; o.nrm[k] = n; o.sep[k] = sep; }
+    for (int k = 0; k < MG_PAIR_MAXC; ++k) {
+        const bool put = o.n == k;
+        o.p[k] = vsel(put, p, o.p[k]);
+        o.nrm[k] = vsel(put, n, o.nrm[k]);
+        o.sep[k] = put ? sep : o.sep[k];
+    }
     if (o.n < MG_PAIR_MAXC) o.n = o.n + 1;
 }
 
@@ -371,12 +375,16 @@ MG_HD void deep4_add(Deep4& D, float s, V3 p, V3 n) {
 #pragma unroll
     for (int k = 0; k < MG_PAIR_MAXC; ++k)
         if (k < D.n && D.s[k] <= s) at = k + 1;
+    // every slot through selects, top down (an indexed insert kept the record
+    // in scratch)
 #pragma unroll
-    for (int k = MG_PAIR_MAXC - 1; k > 0; --k)
-        if (k > at) { D.s[k] = D.s[k - 1]; D.p[k] = D.p[k - 1]; D.nrm[k] = D.nrm[k - 1]; }
-#pragma unroll
-    for (int k = 0; k < MG_PAIR_MAXC; ++k)
-        if (k == at) { D.s[k] = s; D.p[k] = p; D.nrm[k] = n; }
+    for (int k = MG_PAIR_MAXC - 1; k >= 0; --k) {
+        const int km = k > 0 ? k - 1 : 0;
+        const bool sh = k > at, put = k == at;
+        D.s[k] = sh ? D.s[km] : (put ? s : D.s[k]);
+        D.p[k] = vsel(sh, D.p[km], vsel(put, p, D.p[k]));
+        D.nrm[k] = vsel(sh, D.nrm[km], vsel(put, n, D.nrm[k]));
+    }
     if (D.n < MG_PAIR_MAXC) D.n = D.n + 1;
 }
 MG_HD void deep4_emit(const Deep4& D, PairOut& o) {
@@ -692,22 +700,26 @@ MG_HD void collide(const CShape& A, const CShape& B, float margin, PairOut& o) {
     na = A.type == MG_SHAPE_CAPSULE ? 2 : 1;
     nbs = B.type == MG_SHAPE_CAPSULE ? 2 : 1;
     ra = A.h.x; rb = B.h.x;
-    ca[0] = A.type == MG_SHAPE_CAPSULE ? vsub(A.c, vscale(A.R.c0, A.h.y)) : A.c;
+    ca[0] = vsel(A.type == MG_SHAPE_CAPSULE, vsub(A.c, vscale(A.R.c0, A.h.y)), A.c);
     ca[1] = vadd(A.c, vscale(A.R.c0, A.h.y));
-    cb[0] = B.type == MG_SHAPE_CAPSULE ? vsub(B.c, vscale(B.R.c0, B.h.y)) : B.c;
+    cb[0] = vsel(B.type == MG_SHAPE_CAPSULE, vsub(B.c, vscale(B.R.c0, B.h.y)), B.c);
     cb[1] = vadd(B.c, vscale(B.R.c0, B.h.y));
     if (A.type == MG_SHAPE_CONVEX || B.type == MG_SHAPE_CONVEX) {
         const bool pa = A.type == MG_SHAPE_BOX || A.type == MG_SHAPE_CONVEX;
         const bool pb = B.type == MG_SHAPE_BOX || B.type == MG_SHAPE_CONVEX;
         if (pa && pb) { convex_convex(A, B, margin, o); return; }
         if (pb) {                            // sphere / capsule A vs convex B
-            for (int k = 0; k < na; ++k) sphere_convex(ca[k], ra, B, margin, o);
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (k < na) sphere_convex(ca[k], ra, B, margin, o);
             if (A.type == MG_SHAPE_CAPSULE) capsule_segment_convex(A, B, margin, o);
             return;
         }
         PairOut t;                           // convex A vs sphere / capsule B: swap roles
         t.n = 0;
-        for (int k = 0; k < nbs; ++k) sphere_convex(cb[k], rb, A, margin, t);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (k < nbs) sphere_convex(cb[k], rb, A, margin, t);
         if (B.type == MG_SHAPE_CAPSULE) capsule_segment_convex(B, A, margin, t);
 #pragma unroll
         for (int k = 0; k < MG_PAIR_MAXC; ++k)
@@ -715,14 +727,18 @@ MG_HD void collide(const CShape& A, const CShape& B, float margin, PairOut& o) {
         return;
     }
     if (B.type == MG_SHAPE_BOX) {
-        for (int k = 0; k < na; ++k) sphere_box(ca[k], ra, B, margin, o);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (k < na) sphere_box(ca[k], ra, B, margin, o);
         if (A.type == MG_SHAPE_CAPSULE) capsule_segment_convex(A, B, margin, o);
         return;
     }
     if (A.type == MG_SHAPE_BOX) {
         PairOut t;
         t.n = 0;
-        for (int k = 0; k < nbs; ++k) sphere_box(cb[k], rb, A, margin, t);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (k < nbs) sphere_box(cb[k], rb, A, margin, t);
         if (B.type == MG_SHAPE_CAPSULE) capsule_segment_convex(B, A, margin, t);
 #pragma unroll
         for (int k = 0; k < MG_PAIR_MAXC; ++k)     // swap roles: point on A, normal from B to A

@@ -198,12 +198,17 @@ __device__ __forceinline__ void candq_add(CandQ& Q, float s, int id, V3 p, V3 n)
 #pragma unroll
     for (int k = 0; k < MG_PAIR_MAXC; ++k)
         if (k < Q.n && Q.s[k] <= s) at = k + 1;
+    // every slot through selects, top down (an indexed insert kept the queue in
+    // scratch: a memory round trip per candidate)
 #pragma unroll
-    for (int k = MG_PAIR_MAXC - 1; k > 0; --k)
-        if (k > at) { Q.s[k] = Q.s[k - 1]; Q.id[k] = Q.id[k - 1]; Q.p[k] = Q.p[k - 1]; Q.nrm[k] = Q.nrm[k - 1]; }
-#pragma unroll
-    for (int k = 0; k < MG_PAIR_MAXC; ++k)
-        if (k == at) { Q.s[k] = s; Q.id[k] = id; Q.p[k] = p; Q.nrm[k] = n; }
+    for (int k = MG_PAIR_MAXC - 1; k >= 0; --k) {
+        const int km = k > 0 ? k - 1 : 0;
+        const bool sh = k > at, put = k == at;
+        Q.s[k] = sh ? Q.s[km] : (put ? s : Q.s[k]);
+        Q.id[k] = sh ? Q.id[km] : (put ? id : Q.id[k]);
+        Q.p[k] = vsel(sh, Q.p[km], vsel(put, p, Q.p[k]));
+        Q.nrm[k] = vsel(sh, Q.nrm[km], vsel(put, n, Q.nrm[k]));
+    }
     if (Q.n < MG_PAIR_MAXC) Q.n = Q.n + 1;
 }
 template <int CTRL>
@@ -492,9 +497,9 @@ MG_HD void ground_pair(const MgStep& P, const CShape& s, PairOut& o) {
         if (ad2 > best) ia = 2;
         const V3 a0 = vscale(s.R.c0, s.h.x), a1 = vscale(s.R.c1, s.h.y), a2 = vscale(s.R.c2, s.h.z);
         const float di = ia == 0 ? d0 : (ia == 1 ? d1 : d2);
-        const V3 ai = ia == 0 ? a0 : (ia == 1 ? a1 : a2);
-        const V3 e1 = ia == 0 ? a1 : a0;
-        const V3 e2 = ia == 2 ? a1 : a2;
+        const V3 ai = vsel(ia == 0, a0, vsel(ia == 1, a1, a2));
+        const V3 e1 = vsel(ia == 0, a1, a0);
+        const V3 e2 = vsel(ia == 2, a1, a2);
         const V3 cu = vadd(s.c, vscale(ai, di > 0.0f ? -1.0f : 1.0f));
         for (int k = 0; k < 4; ++k) {
             const float sx = (k & 1) ? 1.0f : -1.0f;
@@ -1559,7 +1564,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     if (rw == 0 ? !cn : !cf) continue;
                     const int ab = rw == 0 ? 0 : S.aab[c];
                     const int a = rw == 0 ? S.ca[c] : (ab & 0xFFFF), b = rw == 0 ? S.cb[c] : (ab >> 16);
-                    const V3 p = rw == 0 ? S.cp[c] : S.apt[c];
+                    const V3 p = vsel(rw == 0, S.cp[c], S.apt[c]);
                     const V3 dir = S.cd[c][rw];
                     float J = 0.0f, W = 0.0f;
                     if (a >= LIM0) {

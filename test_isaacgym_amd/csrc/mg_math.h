@@ -14,6 +14,9 @@ struct Q4 { float x, y, z, w; };
 struct M3 { V3 c0, c1, c2; };          // column-major 3x3
 
 MG_HD V3 v3(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+// c ? a : b per component: value selects (a ternary on V3 objects selects their
+// addresses, which keeps them in scratch memory on the device)
+MG_HD V3 vsel(bool c, V3 a, V3 b) { return v3(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
 MG_HD V3 vadd(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 MG_HD V3 vsub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 MG_HD V3 vscale(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }

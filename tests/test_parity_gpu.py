@@ -805,3 +805,46 @@ def test_hipgraph_replay_matches_eager(gym):
     assert np.array_equal(outs[0], outs[1]), "max |diff| %g" % np.abs(outs[0] - outs[1]).max()
     assert np.array_equal(outs[0], outs[2]), "max |diff| %g" % np.abs(outs[0] - outs[2]).max()
     assert np.array_equal(outs[0], outs[3]), "max |diff| %g" % np.abs(outs[0] - outs[3]).max()
+
+
+def test_gimbal_shared_and_mixed_props_parity(gym):
+    """k_artic_chain reads a template's DOF properties, link mass constants and
+    gravity flag as wave-uniform scalars while every instance agrees
+    (migym_capi.cpp chain_uni_*), per lane otherwise: 20 steps shared, 20 with
+    one gimbal's stiffness and effort changed through set_actor_dof_properties
+    (the per-lane path), 20 with it restored (shared again) — bit for bit the
+    oracle throughout."""
+    n, steps = 192, 60
+    sim, envs = scenes.gimbal_scene(gym, n)
+    gym.prepare_sim(sim)
+    _, rb, dof, _ = _tensors(gym, sim)
+    tg = scenes.gimbal_targets(n, steps, DEV, seed=9)
+    tg_h = tg.cpu().numpy()
+    p, m = sim.mg_params(), sim.mg_model()
+    A = sim.model_arrays
+    st = A["body_state0"].copy()
+    ds = A["dof_state0"].copy()
+    props = A["dof_props"].copy()
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+    env, h = envs[5], 0
+    base = gym.get_actor_dof_properties(env, h)
+    for k in range(steps):
+        if k in (20, 40):
+            pr = base.copy()
+            if k == 20:
+                pr["stiffness"][:] = 80.0
+                pr["effort"][:] = 4.0
+            assert gym.set_actor_dof_properties(env, h, pr)
+            d0 = 5 * 3
+            props[d0:d0 + 3, 1] = pr["stiffness"]
+            props[d0:d0 + 3, 3] = pr["effort"]
+        assert gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[k].contiguous()))
+        gym.simulate(sim)
+        tgt[:, 0] = tg_h[k]
+        oracle.step(p, m, st, ds, tgt=tgt, props=props)
+        if k in (19, 39, 59):
+            gym.refresh_dof_state_tensor(sim)
+            gym.refresh_rigid_body_state_tensor(sim)
+            got_d, got = dof.cpu().numpy(), rb.cpu().numpy()
+            assert np.array_equal(got_d, ds), "step %d: max |diff| %g" % (k, np.abs(got_d - ds).max())
+            assert np.array_equal(got, st), "step %d: max |diff| %g" % (k, np.abs(got - st).max())
