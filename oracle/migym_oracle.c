@@ -825,14 +825,6 @@ static sv_t ri_mul_(const ri_t* I, sv_t x) {
                  fmaf(I->xz, x.w.x, fmaf(I->yz, x.w.y, fmaf(I->zz, x.w.z, t.z)))),
                V(fmaf(I->m, x.v.x, -s.x), fmaf(I->m, x.v.y, -s.y), fmaf(I->m, x.v.z, -s.z)));
 }
-static ri_t ri_add_(const ri_t* a, const ri_t* b) {
-    ri_t r;
-    r.xx = a->xx + b->xx; r.yy = a->yy + b->yy; r.zz = a->zz + b->zz;
-    r.xy = a->xy + b->xy; r.xz = a->xz + b->xz; r.yz = a->yz + b->yz;
-    r.h = add3(a->h, b->h);
-    r.m = a->m + b->m;
-    return r;
-}
 static float sdot_(sv_t a, sv_t b) {
     return fmaf(a.v.z, b.v.z, fmaf(a.v.y, b.v.y, fmaf(a.v.x, b.v.x, fmaf(a.w.z, b.w.z, fmaf(a.w.y, b.w.y, a.w.x * b.w.x)))));
 }

@@ -72,14 +72,6 @@ __device__ __forceinline__ SV ri_mul(const RI& I, SV x) {
                  fmaf(I.xz, x.w.x, fmaf(I.yz, x.w.y, fmaf(I.zz, x.w.z, t.z)))),
               v3(fmaf(I.m, x.v.x, -s.x), fmaf(I.m, x.v.y, -s.y), fmaf(I.m, x.v.z, -s.z)));
 }
-__device__ __forceinline__ RI ri_add(const RI& a, const RI& b) {
-    RI r;
-    r.xx = a.xx + b.xx; r.yy = a.yy + b.yy; r.zz = a.zz + b.zz;
-    r.xy = a.xy + b.xy; r.xz = a.xz + b.xz; r.yz = a.yz + b.yz;
-    r.h = vadd(a.h, b.h);
-    r.m = a.m + b.m;
-    return r;
-}
 __device__ __forceinline__ float sdot(SV a, SV b) {
     return fmaf(a.v.z, b.v.z, fmaf(a.v.y, b.v.y, fmaf(a.v.x, b.v.x, fmaf(a.w.z, b.w.z, fmaf(a.w.y, b.w.y, a.w.x * b.w.x)))));
 }
@@ -440,12 +432,30 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
     // 3 floats carried to the next link) and the base's actor-root row
     float* orb = nullptr;
     bool contiguous = false;
+    // a full wave whose 64 articulations' rows form one contiguous block (consecutive
+    // actors, the S2 scene): the rows go through LDS and leave as 16-B stores of
+    // consecutive addresses, 1 KB per store instruction (per lane, a store would
+    // touch 64 rows 208 B apart)
+    constexpr int RW = NL * MG_STATE_N;            // floats of one articulation's rows
+    __shared__ __align__(16) float s_rows[64 * RW];
+    __shared__ __align__(16) float s_root[64 * MG_STATE_N];
+    bool wave_tr = false, root_tr = false;
     if (AA.out_rb) {
         const int g0 = fld(AA.out_body, 0, 0, b0);
         contiguous = true;
 #pragma unroll
         for (int l = 1; l < NL; ++l) contiguous = contiguous && fld(AA.out_body, 0, 0, b0 + l * ls) == g0 + l;
         orb = AA.out_rb + (size_t)g0 * MG_STATE_N;
+        // wave-uniform: every lane live, and a launch wider than the SIMDs can hold
+        // in one round (a latency-bound launch pays the LDS round trip: 4096
+        // gimbals 12.2 -> 12.8 us; 262,144: 50.4 -> 43.4 us)
+        const bool full = ((int)blockIdx.x + 1) * 64 <= AA.na && gridDim.x > 1024;
+        if (full) {
+            const int g00 = __builtin_amdgcn_readfirstlane(g0);
+            const float* wb = AA.out_rb + (size_t)g00 * MG_STATE_N;
+            wave_tr = __all(contiguous && g0 == g00 + NL * (int)threadIdx.x) &&
+                      (reinterpret_cast<uintptr_t>(wb) & 15) == 0;
+        }
         contiguous = contiguous && (reinterpret_cast<uintptr_t>(orb) & 15) == 0;
     }
     float carry[3] = {0.0f, 0.0f, 0.0f};
@@ -477,7 +487,10 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
 #pragma unroll
             for (int k = 0; k < MG_STATE_N; ++k) fld(St, k, nb, b) = r[k];
             if (AA.out_rb) {
-                if (contiguous) {
+                if (wave_tr) {
+#pragma unroll
+                    for (int k = 0; k < MG_STATE_N; ++k) s_rows[threadIdx.x * RW + l * MG_STATE_N + k] = r[k];
+                } else if (contiguous) {
                     // this link's floats after the carried ones: whole float4s
                     // from the row start (l * 13 floats in), the rest carried
                     const int c0 = (l * MG_STATE_N) & 3;               // floats carried in
@@ -499,7 +512,14 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
             }
             if (l == 0 && AA.out_root) {
                 const int rr = fld(AA.out_root_row, 0, 0, b0);
-                if (rr >= 0) {
+                // the wave's base rows one contiguous block as well: through LDS
+                const int rr0 = __builtin_amdgcn_readfirstlane(rr);
+                root_tr = wave_tr && __all(rr >= 0 && rr == rr0 + (int)threadIdx.x) &&
+                          (reinterpret_cast<uintptr_t>(AA.out_root + (size_t)rr0 * MG_STATE_N) & 15) == 0;
+                if (root_tr) {
+#pragma unroll
+                    for (int k = 0; k < MG_STATE_N; ++k) s_root[threadIdx.x * MG_STATE_N + k] = r[k];
+                } else if (rr >= 0) {
                     float* R = AA.out_root + (size_t)rr * MG_STATE_N;
 #pragma unroll
                     for (int k = 0; k < MG_STATE_N; ++k) R[k] = r[k];
@@ -507,9 +527,30 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
             }
         }
     }
+    if (wave_tr) {   // wave-uniform
+        __syncthreads();
+        float* wb = AA.out_rb + (size_t)__builtin_amdgcn_readfirstlane(fld(AA.out_body, 0, 0, b0)) * MG_STATE_N;
+        constexpr int N4 = 16 * RW;                 // float4s of the wave's block (64 * RW / 4)
+#pragma unroll
+        for (int j = 0; j < (N4 + 63) / 64; ++j) {
+            const int f4 = j * 64 + (int)threadIdx.x;
+            if (f4 < N4)
+                *reinterpret_cast<float4*>(wb + 4 * f4) = *reinterpret_cast<const float4*>(s_rows + 4 * f4);
+        }
+        if (root_tr) {   // wave-uniform
+            float* wr = AA.out_root + (size_t)__builtin_amdgcn_readfirstlane(fld(AA.out_root_row, 0, 0, b0)) *
+                                          MG_STATE_N;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {   // 64 x 13 floats = 208 float4s
+                const int f4 = j * 64 + (int)threadIdx.x;
+                if (f4 < 16 * MG_STATE_N)
+                    *reinterpret_cast<float4*>(wr + 4 * f4) = *reinterpret_cast<const float4*>(s_root + 4 * f4);
+            }
+        }
+    }
     // NL * 13 floats end on a float4 boundary only for NL = 4: the last link's
     // remaining floats (NL < 4)
-    if (AA.out_rb && contiguous) {
+    if (AA.out_rb && contiguous && !wave_tr) {
         constexpr int rem = (NL * MG_STATE_N) & 3;
 #pragma unroll
         for (int i = 0; i < rem; ++i) orb[NL * MG_STATE_N - rem + i] = carry[i];
