@@ -478,6 +478,7 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
 // has no contact, which drops any patch.
 struct GPatch {
     int cnt;
+    bool dirty;     // anchors / normal differ from the stored record (written back at the step's end)
     V3 nA;          // patch normal in the body frame
     V3 aA[2];       // anchor on the body (body frame)
     V3 aB[2];       // anchor on the ground (world)
@@ -548,6 +549,9 @@ __device__ __forceinline__ void ground_patch_update(const B& G, GPatch& R, V3 x,
         N.cnt = nc;
     }
     N.nA = kept > 0 ? R.nA : qrot_inv(q, n0);
+    // the stored record changes unless every held anchor was kept in place and
+    // none was placed (a resting body: most steps)
+    N.dirty = R.dirty || !(kept == R.cnt && nc == kept);
     R = N;
 }
 
@@ -712,6 +716,7 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
     // contact and drops the patch, whatever the record holds)
     GPatch R;
     R.cnt = 0;
+    R.dirty = false;
     R.nA = R.aA[0] = R.aA[1] = R.aB[0] = R.aB[1] = v3(0.0f, 0.0f, 0.0f);
     {
         const float clear = G.dn(x) + P.pd;
@@ -909,7 +914,7 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
     // the patch for the next step: the anchor count always, the anchors while held
     if (gp && has_shape) {
         gp[0] = (float)R.cnt;
-        if (R.cnt > 0) {
+        if (R.cnt > 0 && R.dirty) {
             const float r[MG_FP_N] = {0.0f, R.nA.x, R.nA.y, R.nA.z,
                                       R.aA[0].x, R.aA[0].y, R.aA[0].z, R.aB[0].x, R.aB[0].y, R.aB[0].z,
                                       R.aA[1].x, R.aA[1].y, R.aA[1].z, R.aB[1].x, R.aB[1].y, R.aB[1].z};
