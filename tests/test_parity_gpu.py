@@ -94,6 +94,35 @@ def test_servo_large_launch_step_parity(gym):
         assert np.array_equal(ncf.cpu().numpy(), cf)
 
 
+def test_servo_large_launch_fused_rows(gym):
+    """The wide launch with the refresh fused into the step (STEP_FUSION_ALL):
+    each wave writes its 64 rows through an LDS transpose (k_rigid_step1's wide
+    branch); the root and rigid-body tensors equal the unfused sequence's bit
+    for bit."""
+    n, steps = 131072, 3
+    acts = scenes.servo_actions(n, steps, DEV, seed=5)
+    sims = []
+    for fusion in (gymapi.STEP_FUSION_ALL, 0):
+        sim, _ = scenes.servo_scene(gym, n)
+        gym.prepare_sim(sim)
+        gym.set_step_fusion(sim, fusion)
+        sims.append((sim, _tensors(gym, sim)))
+        gym.refresh_actor_root_state_tensor(sim)
+    for k in range(steps):
+        for sim, (root, _, _, _) in sims:
+            root[:, 3:10] = acts[k]
+            assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+            gym.simulate(sim)
+            gym.refresh_actor_root_state_tensor(sim)
+            gym.refresh_rigid_body_state_tensor(sim)
+        torch.cuda.synchronize()
+        (ra, rba, _, _), (rb_, rbb, _, _) = sims[0][1], sims[1][1]
+        assert torch.equal(ra, rb_), "step %d: root state differs" % k
+        assert torch.equal(rba, rbb), "step %d: rigid-body state differs" % k
+    for sim, _ in sims:
+        gym.destroy_sim(sim)
+
+
 def test_fused_step_matches_unfused(gym):
     """Step fusion (mg_set_fusion): the root-state set read by the step kernel
     and the paired root + rigid-body refresh give the same tensors, bit for bit,
