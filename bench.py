@@ -194,6 +194,9 @@ def rigid_roofline(n, kern_ms, kmin, launches, segment, step_out=True):
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
             "traffic_source": pmc_file,
+            "traffic_read_write": ([pmc["fetch_kib_raw"] * 1024 * pmc["read_factor_calibrated"],
+                                    pmc["write_kib_raw"] * 1024 * pmc.get("write_calibration", {}).get("write_factor", 1.0)]
+                                   if pmc and "fetch_kib_raw" in pmc and "read_factor_calibrated" in pmc else None),
             "algorithmic_bytes_per_launch": bytes_launch,
             "algorithmic_bytes_per_env": bpe,
             "algorithmic_bytes_note": ("376 B simulate share (SURVEY.md §8d) + the rigid-body and root rows the "
@@ -201,7 +204,24 @@ def rigid_roofline(n, kern_ms, kmin, launches, segment, step_out=True):
                                        if step_out else "376 B simulate share (SURVEY.md §8d)"),
             "kernel_ms_avg": kern_ms, "kernel_ms_min": kmin, "kernel_launches_timed": launches,
             "kernel_timing": "dispatch timestamps of every k_rigid_step launch (hipExtLaunchKernelGGL start/stop "
-                             "events, the interval rocprofv3 reports) over %s" % segment}
+                             "events, the interval rocprofv3 reports) over %s" % segment,
+            "kernel_bytes_needed_per_env": kernel_bytes_needed(step_out)}
+
+
+def kernel_bytes_needed(step_out):
+    """What k_rigid_step1 itself must move per servo env (the
+    traffic accounting), beside SURVEY's 376 / 584 B pricing: the servo
+    templates' mass and shape rows are wave-uniform (0 B per body), while the
+    contact force and the ground-patch record (MG_FP_N = 16 floats per body:
+    the anchor count, read and written every step, and the normal plus two
+    anchor pairs, 60 B, read and written while the vehicle's patch is held)
+    are not in SURVEY's share."""
+    rd = {"state_in": 2 * 52, "patch_count": 2 * 4, "patch_anchors": 60}
+    wr = {"state_out": 2 * 52, "contact_force": 2 * 12, "patch_count": 2 * 4, "patch_anchors": 60}
+    if step_out:
+        wr["rigid_body_and_root_rows"] = 2 * (52 + 52)
+    return {"read": sum(rd.values()), "write": sum(wr.values()), "total": sum(rd.values()) + sum(wr.values()),
+            "read_parts": rd, "write_parts": wr}
 
 
 # --------------------------------------------------------------------------- CPU baseline
