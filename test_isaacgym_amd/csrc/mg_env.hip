@@ -1548,6 +1548,17 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         PH_MARK(2);
         // this DOF lane's joint axis and origin at the substep start
         const V3 myz = S.zl[mylink], myx = S.xl[mylink];
+        // a free body's slot: its inverse mass, COM and the row of its world
+        // inverse inertia this slot takes (read once, not per row)
+        float fb_im = 0.0f;
+        V3 fb_xc = v3(0.0f, 0.0f, 0.0f), fb_iw = v3(0.0f, 0.0f, 0.0f);
+        if (is_free) {
+            fb_im = S.finvm[fk];
+            fb_xc = S.fxc[fk];
+            const S3 I = S.fIw[fk];
+            fb_iw = fc == 3 ? v3(I.xx, I.xy, I.xz) : (fc == 4 ? v3(I.xy, I.yy, I.yz) : v3(I.xz, I.yz, I.zz));
+        }
+        // pass 1: every row's J (and a free body's W, its slots' M^-1 J)
 #pragma unroll
         for (int c = 0; c < MAXCT; ++c) {
 #pragma unroll
@@ -1577,29 +1588,61 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     } else if (is_free) {
                         const float sg = a == F0 + fk ? 1.0f : (b == F0 + fk ? -1.0f : 0.0f);
                         if (sg != 0.0f) {
-                            const V3 rd = vcross(vsub(p, S.fxc[fk]), dir);
                             if (fc < 3) {
                                 const float dc = fc == 0 ? dir.x : (fc == 1 ? dir.y : dir.z);
                                 J = sg * dc;
-                                W = sg * (S.finvm[fk] * dc);
+                                W = sg * (fb_im * dc);
                             } else {
-                                const V3 iw = symmul(S.fIw[fk], rd);
+                                // row fc - 3 of symmul(fIw, rd): the same products and sums
+                                const V3 rd = vcross(vsub(p, fb_xc), dir);
                                 J = sg * (fc == 3 ? rd.x : (fc == 4 ? rd.y : rd.z));
-                                W = sg * (fc == 3 ? iw.x : (fc == 4 ? iw.y : iw.z));
+                                W = sg * vdot(fb_iw, rd);
                             }
                         }
                     }
-                    if (link_rows) {
-                        // W = M_eff^-1 J over the DOF slots (J_k broadcast from lane k)
-                        float w = 0.0f;
-#pragma unroll
-                        for (int k = 0; k < ND; ++k)
-                            if (k < NA) w = w + mcol[k] * bcastg<G>(J, k);
-                        if (is_dof || is_root) W = w;
-                    }
                     Jr[c * 3 + rw] = J;
                     Wr[c * 3 + rw] = W;
-                    const float den = redg<G>(J * W);
+                }
+            }
+        }
+        // pass 2: W = M_eff^-1 J over the articulation's slots (J_k broadcast
+        // from lane k). Slot k outermost: M_eff^-1 entry k is read once for all
+        // rows and the rows' sums are independent chains (row-outer, each row
+        // was a chain of NA dependent adds behind NA AGPR reads). Every row's sum
+        // still runs k = 0, 1, ... from 0.0f: the same additions in the same
+        // order. Rows beyond the env's contacts hold J = 0 and are not used.
+        int cmax = nct > nanc ? nct : nanc;      // rows in use, the wave's maximum
+#pragma unroll
+        for (int off = G; off < 64; off <<= 1) {
+            const int t = __shfl_xor(cmax, off);
+            cmax = t > cmax ? t : cmax;
+        }
+        cmax = __builtin_amdgcn_readfirstlane(cmax);
+        if (link_rows && (is_dof || is_root)) {
+#pragma unroll
+            for (int k = 0; k < ND; ++k) {
+                if (k < NA) {
+                    const float m = mcol[k];
+#pragma unroll
+                    for (int c = 0; c < MAXCT; ++c) {
+                        if (c < cmax) {
+#pragma unroll
+                            for (int rw = 0; rw < 3; ++rw)
+                                Wr[c * 3 + rw] = Wr[c * 3 + rw] + m * bcastg<G>(Jr[c * 3 + rw], k);
+                        }
+                    }
+                }
+            }
+        }
+        // pass 3: each row's effective mass and a normal row's approach speed
+#pragma unroll
+        for (int c = 0; c < MAXCT; ++c) {
+            const bool cn = c < nct, cf = c < nanc;
+            if (cn || cf) {
+#pragma unroll
+                for (int rw = 0; rw < 3; ++rw) {
+                    if (rw == 0 ? !cn : !cf) continue;
+                    const float den = redg<G>(Jr[c * 3 + rw] * Wr[c * 3 + rw]);
                     const float kk = den > 0.0f ? 1.0f / den : 0.0f;
                     if (ln == 0) S.ck[c][rw] = kk;
                 }
