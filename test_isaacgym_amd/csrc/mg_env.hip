@@ -24,6 +24,8 @@
 // Static bodies and the fixed base link have no slots (infinite mass).
 // Restated in C by oracle/migym_oracle_env.c, with the same pair order, the
 // same reduction tree (red16) and the same evaluation order.
+#include <type_traits>
+
 #include "mg_internal.h"
 #include "mg_spatial.h"
 #include "mg_collide.h"
@@ -1618,21 +1620,27 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             cmax = t > cmax ? t : cmax;
         }
         cmax = __builtin_amdgcn_readfirstlane(cmax);
-        if (link_rows && (is_dof || is_root)) {
+        // (two straight-line variants by the wave's row count: a guard per
+        // contact inside the slot loop split it into 256 blocks, each reloading
+        // its operands from AGPRs)
+        auto wpass = [&](auto cm) {
+            constexpr int CM = decltype(cm)::value;
 #pragma unroll
             for (int k = 0; k < ND; ++k) {
                 if (k < NA) {
                     const float m = mcol[k];
 #pragma unroll
-                    for (int c = 0; c < MAXCT; ++c) {
-                        if (c < cmax) {
+                    for (int c = 0; c < CM; ++c) {
 #pragma unroll
-                            for (int rw = 0; rw < 3; ++rw)
-                                Wr[c * 3 + rw] = Wr[c * 3 + rw] + m * bcastg<G>(Jr[c * 3 + rw], k);
-                        }
+                        for (int rw = 0; rw < 3; ++rw)
+                            Wr[c * 3 + rw] = Wr[c * 3 + rw] + m * bcastg<G>(Jr[c * 3 + rw], k);
                     }
                 }
             }
+        };
+        if (link_rows && (is_dof || is_root)) {
+            if (cmax <= 8) wpass(std::integral_constant<int, (MAXCT < 8 ? MAXCT : 8)>{});
+            else wpass(std::integral_constant<int, MAXCT>{});
         }
         // pass 3: each row's effective mass and a normal row's approach speed
 #pragma unroll
