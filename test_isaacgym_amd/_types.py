@@ -471,8 +471,10 @@ class PlaneParams(_Params):
 
 class CameraProperties(_Params):
     def __init__(self):
-        self.width = 1920
-        self.height = 1080
+        # Isaac Gym's default sensor size: examples/domain_randomization.py:96-99
+        # leaves it unset and its images (examples/dr_output_images) are 1600 x 900
+        self.width = 1600
+        self.height = 900
         self.horizontal_fov = 90.0
         self.near_plane = 0.1
         self.far_plane = 1000.0

@@ -226,11 +226,12 @@ __device__ __forceinline__ void store_row(float* dst, const float (&v)[N]) {
 #define MG_CHAIN_WAVES 2
 #endif
 // EXT: external wrenches this step (apply_rigid_body_force_tensors); UNI: every
-// instance of the launch shares its DOF properties, link mass constants and
-// gravity flag (AA.uni, migym_capi.cpp): wave-uniform scalar loads instead of
-// per-lane loads and per-lane inertia set-up (no VGPRs for them)
-template <int NL, bool EXT, bool UNI>
-__global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, MgArticArgs AA) {
+// instance of the launch shares its link mass constants and gravity flag
+// (AA.uni, migym_capi.cpp; fixed after upload); UDOF: and its DOF properties
+// (wave-uniform scalar loads instead of per-lane loads and per-lane inertia
+// set-up: no VGPRs for them). s_rows / s_root: the kernel's LDS row staging.
+template <int NL, bool EXT, bool UNI, bool UDOF>
+__device__ __forceinline__ void chain_body(const MgStep& P, const MgArticArgs& AA, float* s_rows, float* s_root) {
     constexpr int D = NL - 1;
     const int a = blockIdx.x * 64 + threadIdx.x;
     const bool live = a < AA.na;
@@ -265,7 +266,7 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
         const int gd = d0 + d;
         qv[d] = fld(AA.dof_pos, 0, 0, gd);
         uv[d] = fld(AA.dof_vel, 0, 0, gd);
-        if constexpr (UNI) {
+        if constexpr (UDOF) {
             const float* u = AA.uni + MG_CHAIN_UNI_DOF + 9 * d;
             dc[d].mode = (int)u[0];
             dc[d].kp = u[1];
@@ -437,8 +438,6 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
     // consecutive addresses, 1 KB per store instruction (per lane, a store would
     // touch 64 rows 208 B apart)
     constexpr int RW = NL * MG_STATE_N;            // floats of one articulation's rows
-    __shared__ __align__(16) float s_rows[64 * RW];
-    __shared__ __align__(16) float s_root[64 * MG_STATE_N];
     bool wave_tr = false, root_tr = false;
     if (AA.out_rb) {
         const int g0 = fld(AA.out_body, 0, 0, b0);
@@ -554,6 +553,23 @@ __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, Mg
         constexpr int rem = (NL * MG_STATE_N) & 3;
 #pragma unroll
         for (int i = 0; i < rem; ++i) orb[NL * MG_STATE_N - rem + i] = carry[i];
+    }
+}
+
+// The DOF constants' uniformity is read at run time (AA.uni[MG_CHAIN_UNI_DOFOK],
+// one scalar load, the same branch for the whole launch): a hipGraph captured
+// while every instance shared them keeps stepping correctly after a
+// set_actor_dof_properties makes one differ, as the per-lane
+// path reads d_dof_props in place.
+template <int NL, bool EXT, bool UNI>
+__global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, MgArticArgs AA) {
+    __shared__ __align__(16) float s_rows[64 * NL * MG_STATE_N];
+    __shared__ __align__(16) float s_root[64 * MG_STATE_N];
+    if constexpr (UNI) {
+        if (AA.uni[MG_CHAIN_UNI_DOFOK] != 0.0f) chain_body<NL, EXT, true, true>(P, AA, s_rows, s_root);
+        else chain_body<NL, EXT, true, false>(P, AA, s_rows, s_root);
+    } else {
+        chain_body<NL, EXT, false, false>(P, AA, s_rows, s_root);
     }
 }
 

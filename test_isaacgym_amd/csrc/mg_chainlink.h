@@ -12,6 +12,8 @@
 #define MG_CHAIN_UNI_N    64   // uniform constants of a chain group: 3 links x 10, 3 DOFs x 9, gravity flag
 #define MG_CHAIN_UNI_LINK 0    // + (l - 1) * 10: m, com.xyz, ib[6]
 #define MG_CHAIN_UNI_DOF  30   // + d * 9: mode, kp, kd, effort, max_vel, lower, upper, has_limits, armature
+#define MG_CHAIN_UNI_DOFOK 62  // 1: the DOF constants above are valid (every instance shares them);
+                               // cleared by a later set_actor_dof_properties that makes them differ
 #define MG_CHAIN_UNI_GRAV 63   // the base body's gravity flag
 
 struct ChainLink {

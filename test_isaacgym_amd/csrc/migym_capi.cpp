@@ -476,6 +476,7 @@ static void chain_uni_dof(const float* props, ArticGroup& g) {
             ok = std::memcmp(props + (size_t)(g.step_dof0[i] + d) * MG_DOFPROP_N, props + (size_t)(d0 + d) * MG_DOFPROP_N,
                              9 * sizeof(float)) == 0;
     g.uni_dof = ok;
+    g.uni[MG_CHAIN_UNI_DOFOK] = ok ? 1.0f : 0.0f;   // read by the kernel (graph replays see changes)
     if (!ok) return;
     for (int d = 0; d < g.ndof; ++d)
         for (int j = 0; j < 9; ++j) g.uni[MG_CHAIN_UNI_DOF + 9 * d + j] = props[(size_t)(d0 + d) * MG_DOFPROP_N + j];
@@ -1114,7 +1115,9 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         const ArticGroup& g = s->groups[gi];
         if (g.step_count == 0) continue;
         MgArticArgs A{};
-        A.uni = g.uni_mass && g.uni_dof ? s->d_chain_uni + gi * MG_CHAIN_UNI_N : nullptr;
+        // the DOF part's validity is a flag in the block (MG_CHAIN_UNI_DOFOK), not
+        // a launch choice: a captured launch follows later set_dof_props
+        A.uni = g.uni_mass ? s->d_chain_uni + gi * MG_CHAIN_UNI_N : nullptr;
         A.na = g.step_count; A.nb = s->nb; A.nd = s->nd;
         A.artic_i = s->d_artic_step + (size_t)g.step_offset * MG_ARTIC_I_N;
         A.tmpl = g.tmpl; A.nl = g.nl; A.ndof = g.ndof; A.fixed_base = g.fixed_base; A.chain = g.chain; A.nbl = g.nbody;

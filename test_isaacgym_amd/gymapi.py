@@ -862,15 +862,21 @@ class Gym:
                     "mg_bind_refresh_targets")
         if key == "dof" and sim.dof_out_version is not None and t._version != sim.dof_out_version:
             N.check(N.lib.mg_bind_dof_refresh_target(h, t.data_ptr()), "mg_bind_dof_refresh_target")
-        if key == "root":
-            sim.root_out_version = None
-        elif key == "dof":
-            sim.dof_out_version = None
         N.check(fn(h, t.data_ptr(), 1 if t.device.type == "cpu" else 0, sim.stream()), what)
-        if key == "root" and sim.fusion & STEP_FUSION_REFRESH:
-            sim.rb_paired_version = sim.tensors["rb"]._version
+        # the tensor now holds the sim state, whether this refresh launched a
+        # gather or was served by the step / the paired gather: a later in-place
+        # write makes the next refresh rebind and gather again, as Isaac Gym's
+        # refresh overwrites it (write -> refresh -> write -> refresh)
+        # (device tensors only: a host tensor of the CPU pipeline is bound to nothing)
+        ver = t._version if t.is_cuda else None
+        if key == "root":
+            sim.root_out_version = ver
+            if sim.fusion & STEP_FUSION_REFRESH:
+                sim.rb_paired_version = sim.tensors["rb"]._version
+        elif key == "dof":
+            sim.dof_out_version = ver
         elif key == "rb":
-            sim.rb_paired_version = None
+            sim.rb_paired_version = ver
         return True
 
     def refresh_actor_root_state_tensor(self, sim):

@@ -449,3 +449,61 @@ def ant_scene(gym, num_envs, use_gpu_pipeline=True, device=0, asset_root=None, a
         envs.append(env)
         actors.append(a)
     return sim, {"num_bodies": nb, "envs": envs, "actors": actors, "asset": asset}
+
+
+# ------------------------------------------------------ domain randomization
+DR_CAM_POS = (0.0, 3.0, 3.0)
+DR_CAM_TARGET = (0.0, 0.0, -1.0)
+
+
+def dr_ant_scene(gym, num_envs=1, device=0, use_gpu_pipeline=False, asset_root=None, cam_offsets=None):
+    """examples/domain_randomization.py:36-128, restated as data: Isaac Gym's
+    default (y-up) sim with dt 1/60, 2 substeps, PhysX TGS 4/1 (:36-48), the
+    default ground plane (:60), per env the MJCF ant (assets/mjcf/ant.xml =
+    nv_ant.xml) at (0, 0.5, 0) rotated by Quat(-0.707107, 0, 0, 0.707107),
+    group i, filter 1 (:109-112), every DOF DOF_MODE_NONE with zero stiffness
+    and damping (:116-120), and a default camera sensor attached to the torso
+    at (0, 3, 3) (FOLLOW_TRANSFORM) then placed by set_camera_location at
+    (0, 3, 3) looking at (0, 0, -1) (:122-128); cam_offsets[e] = (y, z) moves
+    env e's camera to (0, 3 + y, 3 + z) as the loop's randomisation does
+    (:168-172). The script's textures, colours and lights are not restated
+    (they change no geometry). Returns (sim, envs, actors, cams)."""
+    sp = gymapi.SimParams()
+    sp.substeps = 2
+    sp.dt = 1.0 / 60.0
+    sp.physx.solver_type = 1
+    sp.physx.num_position_iterations = 4
+    sp.physx.num_velocity_iterations = 1
+    sp.use_gpu_pipeline = use_gpu_pipeline
+    sim = gym.create_sim(device, device, gymapi.SIM_PHYSX, sp)
+    gym.add_ground(sim, gymapi.PlaneParams())
+    ant = gym.load_asset(sim, asset_root or ASSET_ROOT, "mjcf/ant.xml", gymapi.AssetOptions())
+    if ant is None:
+        raise RuntimeError("failed to load the ant")
+    spacing = 0.75
+    lower, upper = gymapi.Vec3(-spacing, 0.0, -spacing), gymapi.Vec3(spacing, spacing, spacing)
+    envs, actors, cams = [], [], []
+    for i in range(num_envs):
+        env = gym.create_env(sim, lower, upper, 2)
+        pose = gymapi.Transform()
+        pose.p = gymapi.Vec3(0, 0.5, 0)
+        pose.r = gymapi.Quat(-0.707107, 0.0, 0.0, 0.707107)
+        a = gym.create_actor(env, ant, pose, "ant", i, 1)
+        props = gym.get_actor_dof_properties(env, a)
+        props["driveMode"].fill(gymapi.DOF_MODE_NONE)
+        props["stiffness"].fill(0.0)
+        props["damping"].fill(0.0)
+        gym.set_actor_dof_properties(env, a, props)
+        cp = gymapi.CameraProperties()
+        cp.enable_tensors = True
+        c = gym.create_camera_sensor(env, cp)
+        body = gym.get_actor_rigid_body_handle(env, a, 0)
+        cam_pos = gymapi.Vec3(*DR_CAM_POS)
+        gym.attach_camera_to_body(c, env, body, gymapi.Transform(p=cam_pos), gymapi.FOLLOW_TRANSFORM)
+        if cam_offsets is not None:
+            cam_pos = cam_pos + gymapi.Vec3(0.0, float(cam_offsets[i][0]), float(cam_offsets[i][1]))
+        gym.set_camera_location(c, env, cam_pos, gymapi.Vec3(*DR_CAM_TARGET))
+        envs.append(env)
+        actors.append(a)
+        cams.append(c)
+    return sim, envs, actors, cams

@@ -106,3 +106,114 @@ def test_vehicle_pushes_bitexact(gym):
     assert np.array_equal(got, st), "max |diff| %g" % np.abs(got - st).max()
     moved = np.abs(st[1::2, 0] - x0)
     assert np.all(moved[pushes < 1.0] < 2e-3) and np.all(moved[pushes > 1.0] > 0.05)
+
+
+def _yup_vehicle_scene(gym, n):
+    """Isaac Gym's default y-up sim (UP_AXIS_Y, gravity -y, plane normal +y) with
+    one ground vehicle per env: the ground-patch rows take the general-normal
+    path (mg_rigid.hip BasisGen anchors), not the packed +Z one."""
+    sp = scenes.servo_sim_params(True)
+    sp.up_axis = gymapi.UP_AXIS_Y
+    sp.gravity = gymapi.Vec3(0.0, -9.8, 0.0)
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 1, 0)
+    plane.static_friction = 1
+    plane.dynamic_friction = 1
+    gym.add_ground(sim, plane)
+    opts = gymapi.AssetOptions()
+    opts.armature = 0.01
+    veh = gym.load_asset(sim, scenes.ASSET_ROOT, "servo/ground_vehicle.urdf", opts)
+    rng = np.random.RandomState(3)
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-20, 0, -20), gymapi.Vec3(20, 20, 20), 8)
+        pose = gymapi.Transform()
+        pose.p = gymapi.Vec3(0.0, 1.6 + 0.1 * rng.rand(), 0.0)
+        pose.r = gymapi.Quat.from_axis_angle(gymapi.Vec3(0, 1, 0), float(rng.uniform(-np.pi, np.pi)))
+        gym.create_actor(env, veh, pose, "veh%d" % i, i, -1)
+    return sim
+
+
+def test_yup_ground_patch_pushes_bitexact(gym):
+    """y-up ground: vehicles land on the plane, are pushed along x / z at 0.5 /
+    0.9 / 1.1 / 1.5 mu m g (held below, sliding above), GPU == oracle bit for
+    bit including the net contact force, every frame."""
+    n, settle, frames = 64, 45, 45
+    sim = _yup_vehicle_scene(gym, n)
+    gym.prepare_sim(sim)
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    cc = oracle.contact_cache(m)
+    A = sim.model_arrays
+    st = A["body_state0"].copy()
+    dof = np.zeros((0, 2), np.float32)
+    for k in range(settle):
+        gym.simulate(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_net_contact_force_tensor(sim)
+        cf = oracle.step(p, m, st, dof, contact_cache=cc)
+        assert np.array_equal(rb.cpu().numpy(), st), "settle frame %d" % k
+        assert np.array_equal(ncf.cpu().numpy(), cf), "settle frame %d: contact force" % k
+    assert int((cc.body[:, 0] == 2.0).sum()) == n          # every vehicle rests on two anchors
+    mu = 0.5 * (float(A["shapes"][int(A["tmpl_body_i"][A["body_tmpl"][0]][0])][11]) + 1.0)
+    pushes = np.array([0.5, 0.9, 1.1, 1.5], np.float32)[np.arange(n) % 4]
+    force = np.zeros((n, 3), np.float32)
+    along_z = np.arange(n) % 8 >= 4
+    force[~along_z, 0] = pushes[~along_z] * mu * 100.0 * 9.8
+    force[along_z, 2] = pushes[along_z] * mu * 100.0 * 9.8
+    ext = np.zeros((n, 6), np.float32)
+    ext[:, 0:3] = force
+    ft = torch.from_numpy(force).to(DEV)
+    tq = torch.zeros_like(ft)
+    x0 = st[:, [0, 2]].copy()
+    for k in range(frames):
+        assert gym.apply_rigid_body_force_tensors(sim, gymtorch.unwrap_tensor(ft), gymtorch.unwrap_tensor(tq),
+                                                  gymapi.ENV_SPACE)
+        gym.simulate(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_net_contact_force_tensor(sim)
+        cf = oracle.step(p, m, st, dof, ext=ext, contact_cache=cc)
+        assert np.array_equal(rb.cpu().numpy(), st), "push frame %d: max |diff| %g" % (
+            k, np.abs(rb.cpu().numpy() - st).max())
+        assert np.array_equal(ncf.cpu().numpy(), cf), "push frame %d: contact force" % k
+    moved = np.linalg.norm(st[:, [0, 2]] - x0, axis=1)
+    assert np.all(moved[pushes < 1.0] < 2e-3) and np.all(moved[pushes > 1.0] > 0.05)
+
+
+def test_reset_in_place_keeps_patch_bitexact(gym):
+    """A root-state set that moves a resting vehicle by less than the friction
+    correlation distance (0.2 mm here, the default distance is 25 mm) keeps its
+    patch: the anchors are kept across teleports on purpose, as PhysX keeps a
+    pair's friction patches across setGlobalPose and drops an anchor only when
+    its two copies drift apart. A 5 cm move drops them. GPU
+    == oracle bit for bit, anchors included."""
+    n = 64
+    sim, _ = scenes.servo_scene(gym, n)
+    gym.prepare_sim(sim)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    cc = oracle.contact_cache(m)
+    st = sim.model_arrays["body_state0"].copy()
+    roots = sim.model_arrays["actor_root_body"]
+    dof = np.zeros((0, 2), np.float32)
+    for _ in range(60):
+        gym.simulate(sim)
+        oracle.step(p, m, st, dof, contact_cache=cc)
+    veh = roots[1::2]
+    assert np.all(cc.body[veh, 0] == 2.0)
+    before = cc.body[veh].copy()
+    gym.refresh_actor_root_state_tensor(sim)
+    for shift in (0.0002, 0.05):
+        root[1::2, 0] += shift
+        assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        st[veh, 0] += shift
+        for _ in range(3):
+            gym.simulate(sim)
+            oracle.step(p, m, st, dof, contact_cache=cc)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_actor_root_state_tensor(sim)
+        assert np.array_equal(rb.cpu().numpy(), st), "shift %g" % shift
+        if shift < 0.025:   # the held anchors are the ones made before the set, bit for bit
+            assert np.array_equal(cc.body[veh, 4:], before[:, 4:])

@@ -98,6 +98,17 @@ def test_gimbal_step_out_fusion(gym):
         gym.refresh_actor_root_state_tensor(sim)
     same("refresh after a user write")
     assert not torch.any(da == -3.0) and not torch.any(ra == -4.0)
+    # write -> refresh -> write -> refresh with no simulate between:
+    # the second refresh overwrites the user's values again, as Isaac Gym's does
+    for sim, (root, rb, dof) in sims:
+        dof.fill_(-5.0)
+        rb[:, 5] = 7.0
+        root.fill_(-6.0)
+        gym.refresh_dof_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_actor_root_state_tensor(sim)
+    same("second refresh after a user write")
+    assert not torch.any(da == -5.0) and not torch.any(ra == -6.0) and not torch.any(rba[:, 5] == 7.0)
     # a DOF-state set after the step: the next refresh shows the set, not the step's rows
     for sim, (root, rb, dof) in sims:
         gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[2 * chunk + 1]))
@@ -247,3 +258,100 @@ def test_raised_fused_set_is_discarded(gym):
         outs.append(dof.clone())
         gym.destroy_sim(sim)
     assert torch.equal(outs[0], outs[1])
+
+
+def test_gimbal_uniform_props_graph_replay(gym):
+    """a hipGraph captured while every gimbal shared its DOF
+    properties (k_artic_chain's wave-uniform constants) keeps stepping with the
+    right properties after set_actor_dof_properties makes one env differ, and
+    again after it is restored: the kernel reads the uniformity flag at run
+    time. Replays are bit for bit the oracle stepped with the same props."""
+    n, chunk = 128, 3
+    sim, envs = scenes.gimbal_scene(gym, n)
+    gym.prepare_sim(sim)
+    gym.set_step_fusion(sim, gymapi.STEP_FUSION_ALL)
+    _, rb, dof = _tensors(gym, sim)
+    tg = scenes.gimbal_targets(n, chunk, DEV, seed=13)
+    tg_h = tg.cpu().numpy()
+    p, m = sim.mg_params(), sim.mg_model()
+    A = sim.model_arrays
+    st = A["body_state0"].copy()
+    ds = A["dof_state0"].copy()
+    props = A["dof_props"].copy()
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+
+    def step(k):
+        gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[k]))
+        gym.simulate(sim)
+        gym.refresh_dof_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            for k in range(chunk):
+                step(k)
+    torch.cuda.current_stream().wait_stream(side)
+    env, h = envs[7], 0
+    base = gym.get_actor_dof_properties(env, h)
+    for phase in ("captured uniform", "one env differs", "restored"):
+        if phase != "captured uniform":
+            pr = base.copy()
+            if phase == "one env differs":
+                pr["stiffness"][:] = 400.0
+                pr["damping"][:] = 1.0
+                pr["effort"][:] = 3.0
+            assert gym.set_actor_dof_properties(env, h, pr)
+            props[7 * 3:7 * 3 + 3, 1] = pr["stiffness"]
+            props[7 * 3:7 * 3 + 3, 2] = pr["damping"]
+            props[7 * 3:7 * 3 + 3, 3] = pr["effort"]
+        g.replay()
+        for k in range(chunk):
+            tgt[:, 0] = tg_h[k]
+            oracle.step(p, m, st, ds, tgt=tgt, props=props)
+        torch.cuda.synchronize()
+        assert np.array_equal(dof.cpu().numpy(), ds), "%s: DOF state max |diff| %g" % (
+            phase, np.abs(dof.cpu().numpy() - ds).max())
+        assert np.array_equal(rb.cpu().numpy(), st), "%s: rigid-body state" % phase
+    gym.destroy_sim(sim)
+
+
+def test_gimbal_wide_launch_rows_through_lds(gym):
+    """more than 65,536 gimbals (a launch wider than one resident
+    round) takes k_artic_chain's full-wave LDS row path; 65,536 + 64*3 + 17 leaves
+    the last wave partly filled. Fused (STEP_FUSION_ALL) and unfused sims give
+    the same DOF, rigid-body and root tensors bit for bit, and both equal the
+    oracle."""
+    n, steps = 65536 + 64 * 3 + 17, 2
+    tg = scenes.gimbal_targets(n, steps, DEV, seed=23)
+    sims = []
+    for fusion in (gymapi.STEP_FUSION_ALL, 0):
+        sim, _ = scenes.gimbal_scene(gym, n)
+        gym.prepare_sim(sim)
+        gym.set_step_fusion(sim, fusion)
+        sims.append((sim, _tensors(gym, sim)))
+    (sa, (ra, rba, da)), (sb, (rb_, rbb, db)) = sims
+    p, m = sa.mg_params(), sa.mg_model()
+    st = sa.model_arrays["body_state0"].copy()
+    ds = sa.model_arrays["dof_state0"].copy()
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+    tg_h = tg.cpu().numpy()
+    for k in range(steps):
+        for sim, _ in sims:
+            gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[k]))
+            gym.simulate(sim)
+            gym.refresh_dof_state_tensor(sim)
+            gym.refresh_rigid_body_state_tensor(sim)
+            gym.refresh_actor_root_state_tensor(sim)
+        tgt[:, 0] = tg_h[k]
+        oracle.step(p, m, st, ds, tgt=tgt)
+        torch.cuda.synchronize()
+        assert torch.equal(da, db) and torch.equal(rba, rbb) and torch.equal(ra, rb_), "step %d: fused != unfused" % k
+    assert np.array_equal(da.cpu().numpy(), ds)
+    assert np.array_equal(rba.cpu().numpy(), st)
+    roots = torch.as_tensor(sa.model_arrays["actor_root_body"], device=DEV, dtype=torch.long)
+    assert torch.equal(rba[roots], ra)
+    for sim, _ in sims:
+        gym.destroy_sim(sim)

@@ -20,6 +20,7 @@
 #     sqenv      SQ counter passes of k_env_step (tools/kbench_franka.py 4096) + the phase-timing
 #                variant (tools/build_variant.sh envphase "-DMG_ENV_PHASE_TIMING", built beforehand)
 #     sqgimbal   SQ counter pass of k_artic_chain (tools/kbench_gimbal.py 4096 262144)
+#     sqgimbal4k SQ passes + kernel trace of k_artic_chain at 4096 gimbals alone
 #     sqrender   SQ + WRITE_SIZE passes of k_render (tools/kbench_render.py 1024 1600x900)
 #     ab         same-box A/B: in-tree libmigym.so vs tools/variants/libmigym_$AB_VARIANT.so on
 #                tools/kbench.py at $AB_SIZES (default 4096 262144), twice
@@ -128,6 +129,12 @@ if has sqenv; then
 fi
 if has sqgimbal; then
   sq_pass gimbal k_artic_chain "$SQ1" python tools/kbench_gimbal.py 4096 262144 || exit 1
+fi
+if has sqgimbal4k; then
+  sq_pass gimbal4k k_artic_chain "$SQ1" python tools/kbench_gimbal.py 4096 || exit 1
+  sq_pass gimbal4k_b k_artic_chain "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE GRBM_COUNT" python tools/kbench_gimbal.py 4096 || exit 1
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/ktr_gimbal4k_$tag -o run --output-format csv \
+    -- python tools/kbench_gimbal.py 4096 > gpurun_out/ktr_gimbal4k_$tag.log 2>&1 || { tail -5 gpurun_out/ktr_gimbal4k_$tag.log; exit 1; }
 fi
 if has sqrender; then
   sq_pass render k_render "$SQ1" python tools/kbench_render.py 1024 1600x900 || exit 1
