@@ -813,9 +813,12 @@ __device__ __forceinline__ void aba_vel(const MgEnvArgs& A, EnvLds<MAXL, G>& S, 
     __syncthreads();
 }
 
-template <int MAXL, int G>
-__device__ __forceinline__ void aba_kin(const MgStep& P, const MgEnvArgs& A, EnvLds<MAXL, G>& S, bool act, int ln, int LA, V3 x0,
-                                        Q4 q0, const LinkC& lk, int b0) {
+// joint transforms (lane l) and forward kinematics (lane 0) of the links
+// from the DOF positions S.q and the base pose (x0, q0): S.qr / S.rr, S.ql,
+// S.xl, S.zl. SL: the coupled step's LDS (EnvLds) or the narrow-phase
+// kernel's (NpLds) — the same operations in both, so the same bits.
+template <class SL>
+__device__ __forceinline__ void aba_fk(const MgEnvArgs& A, SL& S, bool act, int ln, int LA, V3 x0, Q4 q0) {
     // ---- joint transforms (lane l)
     if (act && ln < LA && ln > 0) {
         const float* lf = A.link_f + ln * MG_LINK_F_N;
@@ -849,6 +852,12 @@ __device__ __forceinline__ void aba_kin(const MgStep& P, const MgEnvArgs& A, Env
         }
     }
     __syncthreads();
+}
+
+template <int MAXL, int G>
+__device__ __forceinline__ void aba_kin(const MgStep& P, const MgEnvArgs& A, EnvLds<MAXL, G>& S, bool act, int ln, int LA, V3 x0,
+                                        Q4 q0, const LinkC& lk, int b0) {
+    aba_fk(A, S, act, ln, LA, x0, q0);
     // ---- axes and inertias (lane l)
     if (act && ln < LA) {
         const int* li = A.link_i + ln * MG_LINK_I_N;
@@ -1101,6 +1110,354 @@ __device__ __forceinline__ void stage_links(MgEnvArgs& A) {
     A.link_i = s_li;
 }
 
+// ---- the narrow phase as its own launch (round 5) ---------------------------
+// The coupled step of one substep is two launches: k_env_np (this kernel: the
+// link poses by forward kinematics, the pair screen, the narrow phase, contact
+// placement and the friction patches) and k_env_step (unconstrained motion,
+// limit rows, rows, TGS, integration). Round 4's single kernel held both in one
+// register allocation (512 VGPRs + 276 B of scratch per lane, one wave per
+// SIMD); split, the narrow phase runs with GN lanes per env (64: one env per
+// wave, the cooperative convex tests on 64 lanes, four waves per SIMD at 4096
+// envs) and hands its contacts to the step through a per-env table in HBM
+// (ctab, MG_CT_* below); the step's state between its substep launches goes
+// through a per-env carry record (qv, uv, the contact-force sums, the root and
+// free-body poses) bit for bit, so the arithmetic and its order are those of
+// the single kernel and of oracle/migym_oracle_env.c, unchanged.
+template <int MAXL, int MAXCT>
+struct NpLds {
+    float q[64];                     // DOF positions (aba_fk's link_joint)
+    V3 xl[MAXL], zl[MAXL], rr[MAXL];
+    Q4 ql[MAXL], qr[MAXL];
+    V3 fx[MAXF];
+    Q4 fq[MAXF];
+    V3 sx[MG_ENV_MAXS];
+    Q4 sq[MG_ENV_MAXS];
+    int npl[NPB];
+    int ca[MAXCT], cb[MAXCT];
+    V3 cp[MAXCT], cd[MAXCT][3];
+    float cs0[MAXCT], ce[MAXCT];
+    int ppair[MAXCT];
+    V3 apt[MAXCT];
+    float ae[MAXCT][2], amu[MAXCT];
+    int aab[MAXCT], alast[MAXCT];
+    unsigned fpv[MG_FP_W], fpn[MG_FP_W];
+    unsigned long long pstart;
+    int link_rows;
+};
+
+// contact table of one env (floats; ints stored by bit pattern): header, then
+// MAXCT contacts, then MAXCT anchors
+constexpr int MG_CT_HDR = 8;         // [0] contacts (uncapped), [1] anchors (uncapped), [2] link rows, [3..4] pstart
+constexpr int MG_CT_C = 10;          // ca, cb, cp.xyz, n.xyz, cs0, ce
+constexpr int MG_CT_A = 14;          // apt.xyz, t1.xyz, t2.xyz, ae0, ae1, amu, aab, alast
+template <int MAXCT>
+constexpr int ct_n() { return MG_CT_HDR + MAXCT * (MG_CT_C + MG_CT_A); }
+// carry record of one env between the substep launches of k_env_step
+constexpr int MG_CARRY_HDR = 24;     // x0 (3), q0 (4), free body k: x (3), q (4) at 7 + 7k
+constexpr int MG_CARRY_LANE = 8;     // per lane: qv, uv, lsum.xyz, fsum.xyz
+template <int G>
+constexpr int carry_n() { return MG_CARRY_HDR + MG_CARRY_LANE * G; }
+
+__device__ __forceinline__ float ibits(int v) { return __int_as_float(v); }
+__device__ __forceinline__ int fbits(float v) { return __float_as_int(v); }
+
+// MAXL, GM: the step kernel's link bound and lanes per env (its MAXCT); GN:
+// this kernel's lanes per env
+template <int MAXL, int GM, int GN>
+__global__ void __launch_bounds__(64) k_env_np(MgStep P, MgEnvArgs A) {
+    constexpr int G = GN;
+    constexpr int EPW = 64 / G;          // envs per wavefront
+    constexpr int MAXCT = maxct<GM>();
+    __shared__ NpLds<MAXL, MAXCT> shm[EPW];
+    stage_links<MAXL, G>(A);
+    const int gi = threadIdx.x / G;
+    const int ln = threadIdx.x % G;
+    const int e = blockIdx.x * EPW + gi;
+    const bool live = e < A.ne;
+    NpLds<MAXL, MAXCT>& S = shm[gi];
+    const int* ei = A.env_i + (size_t)(live ? e : 0) * MG_ENV_I_N;
+    const int b0 = ei[0], d0 = ei[1];
+    const int nfr = live ? ei[2] : 0;
+    const int pair0 = ei[14], npair = live ? ei[15] : 0;
+    const int L = (live && b0 >= 0) ? A.nl : 0;
+    const int D = (live && b0 >= 0) ? A.ndof : 0;
+    const int nb = A.nb;
+    const float* St = A.state;
+    const float* cy = A.carry + (size_t)(live ? e : 0) * carry_n<GM>();
+    const int LA = A.nl;
+    PH_T0();
+    // poses at the substep start: the first substep's from the state (the step
+    // kernel's own loads: quaternions normalised), later ones from the carry
+    V3 x0 = v3(0.0f, 0.0f, 0.0f);
+    Q4 q0 = q4(0.0f, 0.0f, 0.0f, 1.0f);
+    if (L > 0) {
+        if (A.sub == 0) {
+            x0 = v3(St[0 * nb + b0], St[1 * nb + b0], St[2 * nb + b0]);
+            q0 = qnormalize(q4(St[3 * nb + b0], St[4 * nb + b0], St[5 * nb + b0], St[6 * nb + b0]));
+        } else {
+            x0 = v3(cy[0], cy[1], cy[2]);
+            q0 = q4(cy[3], cy[4], cy[5], cy[6]);
+        }
+    }
+    if (ln < D) S.q[ln] = A.sub == 0 ? A.dof_pos[d0 + ln] : cy[MG_CARRY_HDR + MG_CARRY_LANE * ln];
+    if (live && ln < ei[7]) {
+        const int b = ei[8 + ln];
+        S.sx[ln] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
+        S.sq[ln] = qnormalize(q4(St[3 * nb + b], St[4 * nb + b], St[5 * nb + b], St[6 * nb + b]));
+    }
+    if (live && ln < nfr) {
+        if (A.sub == 0) {
+            const int b = ei[3 + ln];
+            S.fx[ln] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
+            S.fq[ln] = qnormalize(q4(St[3 * nb + b], St[4 * nb + b], St[5 * nb + b], St[6 * nb + b]));
+        } else {
+            const float* c = cy + 7 + 7 * ln;
+            S.fx[ln] = v3(c[0], c[1], c[2]);
+            S.fq[ln] = q4(c[3], c[4], c[5], c[6]);
+        }
+    }
+    if (ln < MG_FP_W) {   // friction patches held at the end of the last substep
+        S.fpv[ln] = live ? A.fp_mask[(size_t)e * MG_FP_W + ln] : 0u;
+        S.fpn[ln] = 0u;
+    }
+    if (ln == 0) {
+        S.pstart = 0ull;
+        S.link_rows = 0;
+    }
+    __syncthreads();
+    if (LA > 0) aba_fk(A, S, live && L > 0, ln, LA, x0, q0);
+    PH_MARK(6);
+
+    // ================= 2. narrow phase, per block of NPB candidate pairs:
+    // (a) bounding-sphere screen, one pair per lane, survivors compacted in
+    //     pair order into S.npl (the screen is conservative: a rejected pair
+    //     has no contact within the margin);
+    // (b) the full pair test on the survivors, one per lane per round,
+    //     contacts placed by a 16-lane prefix sum in pair order.
+    int base = 0, npatch = 0;   // contacts, friction patches placed so far
+    for (int blk = 0; __any(blk < npair); blk += NPB) {
+        int nnear = 0;
+#pragma unroll
+        for (int r = 0; r < NPB; r += G) {
+            const int pi = blk + r + ln;
+            bool near = false;
+            if (pi < npair) {
+                const int* pp = A.pairs + (size_t)(pair0 + pi) * 4;
+                const int pa = pp[0], sa = pp[1], pb = pp[2], sb = pp[3];
+                const float* sha = A.shapes + sa * MG_SHAPE_STRIDE;
+                V3 xa, xb = v3(0.0f, 0.0f, 0.0f);
+                Q4 qa, qb = q4(0.0f, 0.0f, 0.0f, 1.0f);
+                pair_pose(S, pa, xa, qa);
+                if (pb >= 0) pair_pose(S, pb, xb, qb);
+                near = pair_near(P, sha, xa, qa, pb >= 0 ? A.shapes + sb * MG_SHAPE_STRIDE : sha, xb, qb, pb < 0,
+                                 A.shape_obb + sa * MG_OBB_N, A.shape_obb + (pb >= 0 ? sb : sa) * MG_OBB_N);
+            }
+            const unsigned long long gm = grp_ballot<G>(near, gi);
+            if (near) S.npl[nnear + __popcll(gm & ((1ull << ln) - 1ull))] = pi;
+            nnear += __popcll(gm);
+        }
+        __syncthreads();
+        PH_MARK(8);
+        for (int rb = 0; __any(rb < nnear); rb += G) {
+            PH_NP0();
+            PairOut o;
+            o.n = 0;
+            float rest = 0.0f;
+            int pa = 0, pb = -1, pidx = 0;
+            bool coop = false;
+            CShape cA = {}, cB = {};
+            if (rb + ln < nnear) {
+                PH_COUNT(10, 1);
+                pidx = S.npl[rb + ln];
+                const int* pp = A.pairs + (size_t)(pair0 + pidx) * 4;
+                pa = pp[0];
+                const int sa = pp[1];
+                pb = pp[2];
+                const int sb = pp[3];
+                const float* sha = A.shapes + sa * MG_SHAPE_STRIDE;
+                if (pb < 0) {
+                    V3 xa;
+                    Q4 qa;
+                    pair_pose(S, pa, xa, qa);
+                    ground_pair(P, place_shape(sha, xa, qa, A.hulls), o);
+                    rest = 0.5f * (sha[12] + P.e_ground);
+                } else {
+                    const float* shb = A.shapes + sb * MG_SHAPE_STRIDE;
+                    coop = cvx_pair((int)sha[0], (int)shb[0]);
+                    V3 xa, xb;
+                    Q4 qa, qb;
+                    pair_pose(S, pa, xa, qa);
+                    pair_pose(S, pb, xb, qb);
+                    cA = place_shape(sha, xa, qa, A.hulls);
+                    cB = place_shape(shb, xb, qb, A.hulls);
+                    if (!coop) collide(cA, cB, P.contact_offset, o);
+                    PH_COUNT(11, ((int)sha[0] == MG_SHAPE_CONVEX || (int)shb[0] == MG_SHAPE_CONVEX) ? 1 : 0);
+                    rest = 0.5f * (sha[12] + shb[12]);
+                }
+            }
+            PH_NP(18);
+            // this round's convex pairs, one at a time on the whole group (in
+            // lane order; the result goes to the pair's own lane)
+            unsigned long long cm = grp_ballot<G>(coop, gi);
+            while (__any(cm != 0ull)) {
+                if (cm != 0ull) {                     // group-uniform
+                    const int k = __ffsll(cm) - 1;
+                    cm &= cm - 1ull;
+                    PairOut t;
+                    coop_convex_convex<G>(shfl_shape<G>(cA, k), shfl_shape<G>(cB, k), P.contact_offset, ln, gi, t);
+                    if (ln == k) o = t;
+                    if (ln == k) PH_COUNT(16, t.n == 0 ? 1 : 0);   // convex pairs without a contact
+                }
+            }
+            PH_NP(19);
+            // exclusive prefix sum of the counts over the 16 lanes
+            int incl = o.n;
+#pragma unroll
+            for (int off = 1; off < G; off <<= 1) {
+                const int t = __shfl_up(incl, off, G);
+                if (ln >= off) incl += t;
+            }
+            const int total = __shfl(incl, G - 1, G);
+            const int slot0 = base + incl - o.n;
+#pragma unroll
+            for (int j = 0; j < MG_PAIR_MAXC; ++j) {
+                const int c = slot0 + j;
+                if (j < o.n && c < MAXCT) {
+                    S.ca[c] = pa;
+                    S.cb[c] = pb;
+                    S.cp[c] = o.p[j];
+                    S.cd[c][0] = o.nrm[j];
+                    S.cs0[c] = o.sep[j] - P.rest_offset;
+                    S.ce[c] = rest;
+                    if (pa < F0) S.link_rows = 1;
+                }
+            }
+            base += total;
+            // the pair's friction patch (its first contact placed), in pair
+            // order; updated after the narrow phase, one patch per lane
+            const int pn = (o.n > 0 && slot0 < MAXCT) ? 1 : 0;
+            int pin = pn;
+#pragma unroll
+            for (int off = 1; off < G; off <<= 1) {
+                const int t = __shfl_up(pin, off, G);
+                if (ln >= off) pin += t;
+            }
+            if (pn) S.ppair[npatch + pin - 1] = (pidx << 10) | (slot0 << 4) | (o.n < MAXCT - slot0 ? o.n : MAXCT - slot0);
+            npatch += __shfl(pin, G - 1, G);
+            PH_NP(20);
+        }
+        __syncthreads();
+        PH_MARK(9);
+    }
+    // friction patches, one per lane: anchors kept from
+    // the last substep or grown from the patch's placed contacts
+    int abase = 0;
+    {
+        Patch R;
+        R.cnt = 0;
+        V3 pxa = v3(0.0f, 0.0f, 0.0f), pxb = v3(0.0f, 0.0f, 0.0f), n0 = v3(0.0f, 0.0f, 1.0f);
+        Q4 pqa = q4(0.0f, 0.0f, 0.0f, 1.0f), pqb = q4(0.0f, 0.0f, 0.0f, 1.0f);
+        int pidx = 0, slot0 = 0, pn = 0, pa = 0, pb = -1;
+        float mu = 0.0f;
+        if (live && ln < npatch) {
+            const int pp = S.ppair[ln];
+            pidx = pp >> 10;
+            slot0 = (pp >> 4) & 63;
+            pn = pp & 15;
+            pa = S.ca[slot0];
+            pb = S.cb[slot0];
+            const int* pr = A.pairs + (size_t)(pair0 + pidx) * 4;
+            const float fa = A.shapes[pr[1] * MG_SHAPE_STRIDE + 11];
+            mu = pb < 0 ? 0.5f * (fa + P.mu_ground) : 0.5f * (fa + A.shapes[pr[3] * MG_SHAPE_STRIDE + 11]);
+            PairOut o;
+            o.n = pn;
+#pragma unroll
+            for (int j = 0; j < MG_PAIR_MAXC; ++j) {
+                const int c = j < pn ? slot0 + j : slot0;
+                o.p[j] = S.cp[c];
+                o.nrm[j] = S.cd[c][0];
+                o.sep[j] = S.cs0[c];   // separation beyond the rest offset
+            }
+            n0 = o.nrm[0];
+            pair_pose(S, pa, pxa, pqa);
+            if (pb >= 0) pair_pose(S, pb, pxb, pqb);
+            float* rec = A.fpatch + (size_t)(pair0 + pidx) * MG_FP_N;
+            const bool held = pidx < MG_FP_MAXP && ((S.fpv[pidx >> 5] >> (pidx & 31)) & 1u);
+            if (held) patch_load(R, rec);
+            patch_update(R, pxa, pqa, pxb, pqb, o, P.fric_offset, P.fric_corr);
+            if (pidx < MG_FP_MAXP) {
+                patch_store(R, rec);
+                atomicOr(&S.fpn[pidx >> 5], 1u << (pidx & 31));
+            }
+            atomicOr(&S.pstart, 1ull << slot0);
+        }
+        int ain = R.cnt;
+#pragma unroll
+        for (int off = 1; off < G; off <<= 1) {
+            const int t = __shfl_up(ain, off, G);
+            if (ln >= off) ain += t;
+        }
+        abase = __shfl(ain, G - 1, G);
+        const int ak0 = ain - R.cnt;
+        if (R.cnt > 0) {
+            V3 t1, t2;
+            env_tangents(n0, &t1, &t2);
+            const int last = slot0 + pn - 1;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int k = ak0 + j;
+                if (j < R.cnt && k < MAXCT) {
+                    const V3 wA = vadd(pxa, qrot(pqa, R.aA[j])), wB = vadd(pxb, qrot(pqb, R.aB[j]));
+                    const V3 dr = vsub(wA, wB);
+                    S.apt[k] = wA;
+                    S.cd[k][1] = t1;
+                    S.cd[k][2] = t2;
+                    // position sweeps' target velocity along t1, t2: close 80 %
+                    // of the substep-start drift of the anchor's two copies
+                    const float kd = 0.8f * P.inv_h;
+                    S.ae[k][0] = fminf(fmaxf(-vdot(dr, t1) * kd, -P.max_depen), P.max_depen);
+                    S.ae[k][1] = fminf(fmaxf(-vdot(dr, t2) * kd, -P.max_depen), P.max_depen);
+                    // the patch's other anchor, when it has a row
+                    const int pc = R.cnt == 2 ? (j == 0 ? (k + 1 < MAXCT ? 1 : 0) : 2) : 0;
+                    S.amu[k] = mu;
+                    S.aab[k] = (pa & 0xFFFF) | (pb << 16);
+                    S.alast[k] = last | (pc << 8) | (pidx << 10);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // this substep's patches are the next one's; the contact table
+    if (live && ln < MG_FP_W) A.fp_mask[(size_t)e * MG_FP_W + ln] = S.fpn[ln];
+    if (live) {
+        float* ct = A.ctab + (size_t)e * ct_n<MAXCT>();
+        if (ln == 0) {
+            ct[0] = ibits(base);
+            ct[1] = ibits(abase);
+            ct[2] = ibits(S.link_rows);
+            ct[3] = ibits((int)(unsigned)(S.pstart & 0xFFFFFFFFull));
+            ct[4] = ibits((int)(unsigned)(S.pstart >> 32));
+        }
+        const int nc = base < MAXCT ? base : MAXCT, na = abase < MAXCT ? abase : MAXCT;
+        for (int c = ln; c < nc; c += G) {
+            float* r = ct + MG_CT_HDR + c * MG_CT_C;
+            r[0] = ibits(S.ca[c]); r[1] = ibits(S.cb[c]);
+            r[2] = S.cp[c].x; r[3] = S.cp[c].y; r[4] = S.cp[c].z;
+            r[5] = S.cd[c][0].x; r[6] = S.cd[c][0].y; r[7] = S.cd[c][0].z;
+            r[8] = S.cs0[c]; r[9] = S.ce[c];
+        }
+        for (int k = ln; k < na; k += G) {
+            float* r = ct + MG_CT_HDR + MAXCT * MG_CT_C + k * MG_CT_A;
+            r[0] = S.apt[k].x; r[1] = S.apt[k].y; r[2] = S.apt[k].z;
+            r[3] = S.cd[k][1].x; r[4] = S.cd[k][1].y; r[5] = S.cd[k][1].z;
+            r[6] = S.cd[k][2].x; r[7] = S.cd[k][2].y; r[8] = S.cd[k][2].z;
+            r[9] = S.ae[k][0]; r[10] = S.ae[k][1]; r[11] = S.amu[k];
+            r[12] = ibits(S.aab[k]); r[13] = ibits(S.alast[k]);
+        }
+    }
+    PH_MARK(1);
+}
+
 template <int MAXL, int G>
 __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     constexpr int EPW = 64 / G;          // envs per wavefront
@@ -1147,9 +1504,19 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     V3 gw = v3(0.0f, 0.0f, 0.0f);
     const int LA = A.nl, DA = A.ndof;           // launch-uniform loop bounds (barriers inside)
     const int NA = (LA > 0 && A.floating) ? DA + 6 : DA;   // articulation velocity slots
+    // one substep per launch (A.sub of P.substeps); the state of a later
+    // substep comes from the carry record the previous launch wrote
+    const bool first = A.sub == 0;
+    float* cy = A.carry + (size_t)(live ? e : 0) * carry_n<G>();
+    float* cyl = cy + MG_CARRY_HDR + MG_CARRY_LANE * ln;
     if (L > 0) {
-        x0 = v3(St[0 * nb + b0], St[1 * nb + b0], St[2 * nb + b0]);
-        q0 = qnormalize(q4(St[3 * nb + b0], St[4 * nb + b0], St[5 * nb + b0], St[6 * nb + b0]));
+        if (first) {
+            x0 = v3(St[0 * nb + b0], St[1 * nb + b0], St[2 * nb + b0]);
+            q0 = qnormalize(q4(St[3 * nb + b0], St[4 * nb + b0], St[5 * nb + b0], St[6 * nb + b0]));
+        } else {
+            x0 = v3(cy[0], cy[1], cy[2]);
+            q0 = q4(cy[3], cy[4], cy[5], cy[6]);
+        }
         const float grav_on = A.tbf[A.body_tmpl[b0] * MG_TBODY_F_N + 4];
         gw = grav_on != 0.0f ? gvec : v3(0.0f, 0.0f, 0.0f);
     }
@@ -1164,20 +1531,16 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             }
         }
     }
-    if (ln < MG_FP_W) {   // friction patches held at the end of the last step
-        S.fpv[ln] = live ? A.fp_mask[(size_t)e * MG_FP_W + ln] : 0u;
-        S.fpn[ln] = 0u;
-    }
-    if (ln == 0) S.pstart = 0ull;
-    if (live && ln < ei[7]) {
-        const int b = ei[8 + ln];
-        S.sx[ln] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
-        S.sq[ln] = qnormalize(q4(St[3 * nb + b], St[4 * nb + b], St[5 * nb + b], St[6 * nb + b]));
-    }
     if (live && ln < nfr) {
         const int b = ei[3 + ln];
-        S.fx[ln] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
-        S.fq[ln] = qnormalize(q4(St[3 * nb + b], St[4 * nb + b], St[5 * nb + b], St[6 * nb + b]));
+        if (first) {
+            S.fx[ln] = v3(St[0 * nb + b], St[1 * nb + b], St[2 * nb + b]);
+            S.fq[ln] = qnormalize(q4(St[3 * nb + b], St[4 * nb + b], St[5 * nb + b], St[6 * nb + b]));
+        } else {
+            const float* c = cy + 7 + 7 * ln;
+            S.fx[ln] = v3(c[0], c[1], c[2]);
+            S.fq[ln] = q4(c[3], c[4], c[5], c[6]);
+        }
         const float* Ms = A.mass;
         S.finvm[ln] = Ms[0 * nb + b];
         fr.invI = v3(Ms[1 * nb + b], Ms[2 * nb + b], Ms[3 * nb + b]);
@@ -1201,8 +1564,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     DofC dc = {};
     if (is_dof) {
         const int gd = d0 + ln;
-        qv = A.dof_pos[gd];
-        uv = A.dof_vel[gd];
+        qv = first ? A.dof_pos[gd] : cyl[0];
+        uv = first ? A.dof_vel[gd] : cyl[1];
         dc.mode = (int)pr[0 * nd + gd];
         dc.kp = pr[1 * nd + gd];
         dc.kd = pr[2 * nd + gd];
@@ -1215,19 +1578,23 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         dc.tpos = A.dof_tpos[gd];
         dc.tvel = A.dof_tvel[gd];
         dc.force = A.dof_force[gd];
-        if (A.tpos_w) A.tpos_w[gd] = dc.tpos;
-        if (A.tvel_w) A.tvel_w[gd] = dc.tvel;
-        if (A.force_w) A.force_w[gd] = dc.force;
+        if (first && A.tpos_w) A.tpos_w[gd] = dc.tpos;
+        if (first && A.tvel_w) A.tvel_w[gd] = dc.tvel;
+        if (first && A.force_w) A.force_w[gd] = dc.force;
     } else if (is_root) {
         // root slots: w and the velocity of the base origin v_O = v_com - w x (R c)
         const V3 w = v3(St[10 * nb + b0], St[11 * nb + b0], St[12 * nb + b0]);
         const V3 vc = v3(St[7 * nb + b0], St[8 * nb + b0], St[9 * nb + b0]);
         const V3 c0 = v3(A.mass[8 * nb + b0], A.mass[9 * nb + b0], A.mass[10 * nb + b0]);
         const V3 vo = vsub(vc, vcross(w, qrot(q0, c0)));
-        uv = rc < 3 ? v3c(w, rc) : v3c(vo, rc - 3);
+        uv = first ? (rc < 3 ? v3c(w, rc) : v3c(vo, rc - 3)) : cyl[1];
     } else if (is_free) {
         const int b = ei[3 + fk];
-        uv = St[(7 + fc) * nb + b];
+        uv = first ? St[(7 + fc) * nb + b] : cyl[1];
+    }
+    if (!first) {   // the contact-force sums of the earlier substeps
+        lsum = v3(cyl[2], cyl[3], cyl[4]);
+        fsum = v3(cyl[5], cyl[6], cyl[7]);
     }
     // link ln's body (-1: a virtual link of a ball / multi-axis joint, no mass)
     const int blk = ln < L ? A.link_i[ln * MG_LINK_I_N + 3] : -1;
@@ -1244,7 +1611,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     float Jr[MAXCT * 3], Wr[MAXCT * 3], lam[MAXCT * 3];
     PH_MARK(6);
 
-    for (int st = 0; st < P.substeps; ++st) {
+    {
         // ================= 1. unconstrained motion (lane 0)
         S.q[ln] = qv;
         S.u[ln] = uv;
@@ -1289,7 +1656,6 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             S.u[s0 + 0] = v.x; S.u[s0 + 1] = v.y; S.u[s0 + 2] = v.z;
             S.u[s0 + 3] = w.x; S.u[s0 + 4] = w.y; S.u[s0 + 5] = w.z;
         }
-        if (ln == 0) S.link_rows = 0;
         __syncthreads();
         if (is_dof) {
             const float maxv = dc.maxv;
@@ -1304,204 +1670,41 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         dp = 0.0f;
         PH_MARK(0);
 
-        // ================= 2. narrow phase, per block of NPB candidate pairs:
-        // (a) bounding-sphere screen, one pair per lane, survivors compacted in
-        //     pair order into S.npl (the screen is conservative: a rejected pair
-        //     has no contact within the margin);
-        // (b) the full pair test on the survivors, one per lane per round,
-        //     contacts placed by a 16-lane prefix sum in pair order.
-        int base = 0, npatch = 0;   // contacts, friction patches placed so far
-        for (int blk = 0; __any(blk < npair); blk += NPB) {
-            int nnear = 0;
-#pragma unroll
-            for (int r = 0; r < NPB; r += G) {
-                const int pi = blk + r + ln;
-                bool near = false;
-                if (pi < npair) {
-                    const int* pp = A.pairs + (size_t)(pair0 + pi) * 4;
-                    const int pa = pp[0], sa = pp[1], pb = pp[2], sb = pp[3];
-                    const float* sha = A.shapes + sa * MG_SHAPE_STRIDE;
-                    V3 xa, xb = v3(0.0f, 0.0f, 0.0f);
-                    Q4 qa, qb = q4(0.0f, 0.0f, 0.0f, 1.0f);
-                    pair_pose(S, pa, xa, qa);
-                    if (pb >= 0) pair_pose(S, pb, xb, qb);
-                    near = pair_near(P, sha, xa, qa, pb >= 0 ? A.shapes + sb * MG_SHAPE_STRIDE : sha, xb, qb, pb < 0,
-                                     A.shape_obb + sa * MG_OBB_N, A.shape_obb + (pb >= 0 ? sb : sa) * MG_OBB_N);
-                }
-                const unsigned long long gm = grp_ballot<G>(near, gi);
-                if (near) S.npl[nnear + __popcll(gm & ((1ull << ln) - 1ull))] = pi;
-                nnear += __popcll(gm);
-            }
-            __syncthreads();
-            PH_MARK(8);
-            for (int rb = 0; __any(rb < nnear); rb += G) {
-                PH_NP0();
-                PairOut o;
-                o.n = 0;
-                float rest = 0.0f;
-                int pa = 0, pb = -1, pidx = 0;
-                bool coop = false;
-                CShape cA = {}, cB = {};
-                if (rb + ln < nnear) {
-                    PH_COUNT(10, 1);
-                    pidx = S.npl[rb + ln];
-                    const int* pp = A.pairs + (size_t)(pair0 + pidx) * 4;
-                    pa = pp[0];
-                    const int sa = pp[1];
-                    pb = pp[2];
-                    const int sb = pp[3];
-                    const float* sha = A.shapes + sa * MG_SHAPE_STRIDE;
-                    if (pb < 0) {
-                        V3 xa;
-                        Q4 qa;
-                        pair_pose(S, pa, xa, qa);
-                        ground_pair(P, place_shape(sha, xa, qa, A.hulls), o);
-                        rest = 0.5f * (sha[12] + P.e_ground);
-                    } else {
-                        const float* shb = A.shapes + sb * MG_SHAPE_STRIDE;
-                        coop = cvx_pair((int)sha[0], (int)shb[0]);
-                        V3 xa, xb;
-                        Q4 qa, qb;
-                        pair_pose(S, pa, xa, qa);
-                        pair_pose(S, pb, xb, qb);
-                        cA = place_shape(sha, xa, qa, A.hulls);
-                        cB = place_shape(shb, xb, qb, A.hulls);
-                        if (!coop) collide(cA, cB, P.contact_offset, o);
-                        PH_COUNT(11, ((int)sha[0] == MG_SHAPE_CONVEX || (int)shb[0] == MG_SHAPE_CONVEX) ? 1 : 0);
-                        rest = 0.5f * (sha[12] + shb[12]);
-                    }
-                }
-                PH_NP(18);
-                // this round's convex pairs, one at a time on the whole group (in
-                // lane order; the result goes to the pair's own lane)
-                unsigned long long cm = grp_ballot<G>(coop, gi);
-                while (__any(cm != 0ull)) {
-                    if (cm != 0ull) {                     // group-uniform
-                        const int k = __ffsll(cm) - 1;
-                        cm &= cm - 1ull;
-                        PairOut t;
-                        coop_convex_convex<G>(shfl_shape<G>(cA, k), shfl_shape<G>(cB, k), P.contact_offset, ln, gi, t);
-                        if (ln == k) o = t;
-                        if (ln == k) PH_COUNT(16, t.n == 0 ? 1 : 0);   // convex pairs without a contact
-                    }
-                }
-                PH_NP(19);
-                // exclusive prefix sum of the counts over the 16 lanes
-                int incl = o.n;
-#pragma unroll
-                for (int off = 1; off < G; off <<= 1) {
-                    const int t = __shfl_up(incl, off, G);
-                    if (ln >= off) incl += t;
-                }
-                const int total = __shfl(incl, G - 1, G);
-                const int slot0 = base + incl - o.n;
-#pragma unroll
-                for (int j = 0; j < MG_PAIR_MAXC; ++j) {
-                    const int c = slot0 + j;
-                    if (j < o.n && c < MAXCT) {
-                        S.ca[c] = pa;
-                        S.cb[c] = pb;
-                        S.cp[c] = o.p[j];
-                        S.cd[c][0] = o.nrm[j];
-                        S.cs0[c] = o.sep[j] - P.rest_offset;
-                        S.ce[c] = rest;
-                        if (pa < F0) S.link_rows = 1;
-                    }
-                }
-                base += total;
-                // the pair's friction patch (its first contact placed), in pair
-                // order; updated after the narrow phase, one patch per lane
-                const int pn = (o.n > 0 && slot0 < MAXCT) ? 1 : 0;
-                int pin = pn;
-#pragma unroll
-                for (int off = 1; off < G; off <<= 1) {
-                    const int t = __shfl_up(pin, off, G);
-                    if (ln >= off) pin += t;
-                }
-                if (pn) S.ppair[npatch + pin - 1] = (pidx << 10) | (slot0 << 4) | (o.n < MAXCT - slot0 ? o.n : MAXCT - slot0);
-                npatch += __shfl(pin, G - 1, G);
-                PH_NP(20);
-            }
-            __syncthreads();
-            PH_MARK(9);
-        }
-        // friction patches, one per lane: anchors kept from
-        // the last substep or grown from the patch's placed contacts
-        int abase = 0;
+        // ================= 2. the contacts and friction anchors of k_env_np
+        // (this substep's narrow phase and patches, placed in pair order)
+        int base = 0, abase = 0;
         {
-            Patch R;
-            R.cnt = 0;
-            V3 pxa = v3(0.0f, 0.0f, 0.0f), pxb = v3(0.0f, 0.0f, 0.0f), n0 = v3(0.0f, 0.0f, 1.0f);
-            Q4 pqa = q4(0.0f, 0.0f, 0.0f, 1.0f), pqb = q4(0.0f, 0.0f, 0.0f, 1.0f);
-            int pidx = 0, slot0 = 0, pn = 0, pa = 0, pb = -1;
-            float mu = 0.0f;
-            if (live && ln < npatch) {
-                const int pp = S.ppair[ln];
-                pidx = pp >> 10;
-                slot0 = (pp >> 4) & 63;
-                pn = pp & 15;
-                pa = S.ca[slot0];
-                pb = S.cb[slot0];
-                const int* pr = A.pairs + (size_t)(pair0 + pidx) * 4;
-                const float fa = A.shapes[pr[1] * MG_SHAPE_STRIDE + 11];
-                mu = pb < 0 ? 0.5f * (fa + P.mu_ground) : 0.5f * (fa + A.shapes[pr[3] * MG_SHAPE_STRIDE + 11]);
-                PairOut o;
-                o.n = pn;
-#pragma unroll
-                for (int j = 0; j < MG_PAIR_MAXC; ++j) {
-                    const int c = j < pn ? slot0 + j : slot0;
-                    o.p[j] = S.cp[c];
-                    o.nrm[j] = S.cd[c][0];
-                    o.sep[j] = S.cs0[c];   // separation beyond the rest offset
-                }
-                n0 = o.nrm[0];
-                pair_pose(S, pa, pxa, pqa);
-                if (pb >= 0) pair_pose(S, pb, pxb, pqb);
-                float* rec = A.fpatch + (size_t)(pair0 + pidx) * MG_FP_N;
-                const bool held = pidx < MG_FP_MAXP && ((S.fpv[pidx >> 5] >> (pidx & 31)) & 1u);
-                if (held) patch_load(R, rec);
-                patch_update(R, pxa, pqa, pxb, pqb, o, P.fric_offset, P.fric_corr);
-                if (pidx < MG_FP_MAXP) {
-                    patch_store(R, rec);
-                    atomicOr(&S.fpn[pidx >> 5], 1u << (pidx & 31));
-                }
-                atomicOr(&S.pstart, 1ull << slot0);
+            const float* ct = A.ctab + (size_t)(live ? e : 0) * ct_n<MAXCT>();
+            base = live ? fbits(ct[0]) : 0;
+            abase = live ? fbits(ct[1]) : 0;
+            if (ln == 0) {
+                S.link_rows = live ? fbits(ct[2]) : 0;
+                S.pstart = live ? ((unsigned long long)(unsigned)fbits(ct[3]) |
+                                   ((unsigned long long)(unsigned)fbits(ct[4]) << 32)) : 0ull;
             }
-            int ain = R.cnt;
-#pragma unroll
-            for (int off = 1; off < G; off <<= 1) {
-                const int t = __shfl_up(ain, off, G);
-                if (ln >= off) ain += t;
+            const int nc = base < MAXCT ? base : MAXCT, na = abase < MAXCT ? abase : MAXCT;
+            for (int c = ln; c < nc; c += G) {
+                const float* r = ct + MG_CT_HDR + c * MG_CT_C;
+                S.ca[c] = fbits(r[0]);
+                S.cb[c] = fbits(r[1]);
+                S.cp[c] = v3(r[2], r[3], r[4]);
+                S.cd[c][0] = v3(r[5], r[6], r[7]);
+                S.cs0[c] = r[8];
+                S.ce[c] = r[9];
             }
-            abase = __shfl(ain, G - 1, G);
-            const int ak0 = ain - R.cnt;
-            if (R.cnt > 0) {
-                V3 t1, t2;
-                env_tangents(n0, &t1, &t2);
-                const int last = slot0 + pn - 1;
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int k = ak0 + j;
-                    if (j < R.cnt && k < MAXCT) {
-                        const V3 wA = vadd(pxa, qrot(pqa, R.aA[j])), wB = vadd(pxb, qrot(pqb, R.aB[j]));
-                        const V3 dr = vsub(wA, wB);
-                        S.apt[k] = wA;
-                        S.cd[k][1] = t1;
-                        S.cd[k][2] = t2;
-                        // position sweeps' target velocity along t1, t2: close 80 %
-                        // of the substep-start drift of the anchor's two copies
-                        const float kd = 0.8f * P.inv_h;
-                        S.ae[k][0] = fminf(fmaxf(-vdot(dr, t1) * kd, -P.max_depen), P.max_depen);
-                        S.ae[k][1] = fminf(fmaxf(-vdot(dr, t2) * kd, -P.max_depen), P.max_depen);
-                        // the patch's other anchor, when it has a row
-                        const int pc = R.cnt == 2 ? (j == 0 ? (k + 1 < MAXCT ? 1 : 0) : 2) : 0;
-                        S.amu[k] = mu;
-                        S.aab[k] = (pa & 0xFFFF) | (pb << 16);
-                        S.alast[k] = last | (pc << 8) | (pidx << 10);
-                    }
-                }
+            for (int q = ln; q < na; q += G) {
+                const float* r = ct + MG_CT_HDR + MAXCT * MG_CT_C + q * MG_CT_A;
+                S.apt[q] = v3(r[0], r[1], r[2]);
+                S.cd[q][1] = v3(r[3], r[4], r[5]);
+                S.cd[q][2] = v3(r[6], r[7], r[8]);
+                S.ae[q][0] = r[9];
+                S.ae[q][1] = r[10];
+                S.amu[q] = r[11];
+                S.aab[q] = fbits(r[12]);
+                S.alast[q] = fbits(r[13]);
             }
         }
+        __syncthreads();
         // joint-limit rows (PhysX solves limits as constraints): a DOF whose
         // predicted position q + h u lies within 5% of its range of a limit gets
         // one unilateral row towards the nearer limit, after the contacts
@@ -1829,17 +2032,28 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             S.fq[k] = qintegrate(S.fq[k], dth);
             S.fx[k] = vsub(xc1, qrot(S.fq[k], fr.com));
         }
-        if (ln < MG_FP_W) {   // this substep's patches are the next one's
-            S.fpv[ln] = S.fpn[ln];
-            S.fpn[ln] = 0u;
-        }
-        if (ln == 0) S.pstart = 0ull;
         __syncthreads();
         PH_MARK(5);
     }
+    if (!A.last) {   // to the next substep's launches (k_env_np, k_env_step)
+        if (live) {
+            if (ln == 0) {
+                cy[0] = x0.x; cy[1] = x0.y; cy[2] = x0.z;
+                cy[3] = q0.x; cy[4] = q0.y; cy[5] = q0.z; cy[6] = q0.w;
+            }
+            if (ln < nfr) {
+                float* c = cy + 7 + 7 * ln;
+                c[0] = S.fx[ln].x; c[1] = S.fx[ln].y; c[2] = S.fx[ln].z;
+                c[3] = S.fq[ln].x; c[4] = S.fq[ln].y; c[5] = S.fq[ln].z; c[6] = S.fq[ln].w;
+            }
+            cyl[0] = qv; cyl[1] = uv;
+            cyl[2] = lsum.x; cyl[3] = lsum.y; cyl[4] = lsum.z;
+            cyl[5] = fsum.x; cyl[6] = fsum.y; cyl[7] = fsum.z;
+        }
+        return;
+    }
 
     // ---- outputs
-    if (live && ln < MG_FP_W) A.fp_mask[(size_t)e * MG_FP_W + ln] = S.fpv[ln];
     S.q[ln] = qv;
     S.u[ln] = uv;
     if (is_dof) {
@@ -2130,14 +2344,29 @@ hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s
     // velocity slots: DOFs, the floating root's 6, 6 per free body (at most MG_ENV_MAXF)
     const int slots = A.ndof + (A.floating ? 6 : 0) + 6 * A.max_free;
     if (A.nl > MG_MAX_LINKS || slots > MG_ENV_SLOTS_WIDE) return hipErrorNotSupported;
-    if (mg_wide(A.nl, slots)) {
-        MG_LAUNCH((k_env_step<MG_MAX_LINKS, 64>), dim3(A.ne), dim3(64), 0, s, P, A);
-        return hipGetLastError();
-    }
+    // per substep: the narrow phase (one env per wavefront), then the step
+    const bool wide = mg_wide(A.nl, slots);
+    const bool small = A.nl <= 4 && A.ndof <= 4 && !A.floating;
     const int blocks = (A.ne + 3) / 4;
-    if (A.nl <= 4 && A.ndof <= 4 && !A.floating)
-        MG_LAUNCH((k_env_step<4, G16>), dim3(blocks), dim3(64), 0, s, P, A);
-    else
-        MG_LAUNCH((k_env_step<16, G16>), dim3(blocks), dim3(64), 0, s, P, A);
+    MgEnvArgs B = A;
+    for (int sub = 0; sub < P.substeps; ++sub) {
+        B.sub = sub;
+        B.last = sub == P.substeps - 1 ? 1 : 0;
+        if (wide) {
+            MG_LAUNCH((k_env_np<MG_MAX_LINKS, 64, 64>), dim3(A.ne), dim3(64), 0, s, P, B);
+            MG_LAUNCH((k_env_step<MG_MAX_LINKS, 64>), dim3(A.ne), dim3(64), 0, s, P, B);
+        } else if (small) {
+            MG_LAUNCH((k_env_np<4, G16, 64>), dim3(A.ne), dim3(64), 0, s, P, B);
+            MG_LAUNCH((k_env_step<4, G16>), dim3(blocks), dim3(64), 0, s, P, B);
+        } else {
+            MG_LAUNCH((k_env_np<16, G16, 64>), dim3(A.ne), dim3(64), 0, s, P, B);
+            MG_LAUNCH((k_env_step<16, G16>), dim3(blocks), dim3(64), 0, s, P, B);
+        }
+    }
     return hipGetLastError();
 }
+
+// floats of the per-env carry and contact-table records the launches above
+// need (migym_capi.cpp allocates them per coupled env at the widest group's size)
+extern "C" int mg_env_carry_floats(void) { return carry_n<64>(); }
+extern "C" int mg_env_ctab_floats(void) { return ct_n<MG_ENV_MAXCT_WIDE>(); }

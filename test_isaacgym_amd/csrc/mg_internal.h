@@ -184,6 +184,10 @@ struct MgEnvArgs {
     const float* dof_props;
     const float* ext;
     float*       cforce;
+    // one substep per launch pair (mg_env.hip k_env_np + k_env_step)
+    int          sub, last;   // this launch's substep; 1: the frame's last
+    float*       carry;       // [ne][carry] the step's state between its substep launches
+    float*       ctab;        // [ne][ctab] this substep's contacts and anchors (k_env_np -> k_env_step)
 };
 
 // Camera render (mg_render.hip). One device record per camera; a camera's
@@ -253,6 +257,8 @@ extern thread_local MgKernelTimer* mg_timer;
 // launchers (defined in the .hip files)
 hipError_t mg_launch_render(const MgRenderArgs& A, int nblocks, hipStream_t s);
 hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s);
+extern "C" int mg_env_carry_floats(void);   // per-env record sizes of the coupled step (mg_env.hip)
+extern "C" int mg_env_ctab_floats(void);
 hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream_t s);
 hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream_t s);
 hipError_t mg_launch_artic_lanes(const MgStep& P, const MgArticArgs& A, hipStream_t s);

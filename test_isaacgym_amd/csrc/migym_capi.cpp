@@ -159,6 +159,8 @@ struct mg_sim {
     float* d_gpatch = nullptr;    // [MG_FP_N][nf1] ground patches of the single-shape free bodies (persistent)
     float* d_chain_uni = nullptr; // [groups][MG_CHAIN_UNI_N] shared constants of chain groups (ArticGroup.uni)
     unsigned* d_fp_mask = nullptr;   // [n_coupled][MG_FP_W] pairs holding a patch
+    float* d_env_carry = nullptr;    // [n_coupled][mg_env_carry_floats] coupled step state between substep launches
+    float* d_env_ctab = nullptr;     // [n_coupled][mg_env_ctab_floats] contacts of one substep (k_env_np -> k_env_step)
     int n_coupled = 0;
     std::vector<EnvGroup> env_groups;
 
@@ -192,7 +194,7 @@ struct mg_sim {
     bool capturing = false;       // the last simulate was recorded into a graph
     // ring of per-simulate event pairs for live kernel timing (bench.py roofline)
     static constexpr int kRing = 256;
-    static constexpr int kKern = 4;   // kernels timed per simulate (dispatch timestamps)
+    static constexpr int kKern = 8;   // kernels timed per simulate (dispatch timestamps)
     hipEvent_t ring_b[kRing] = {}, ring_e[kRing] = {};
     hipEvent_t kern_b[kRing][kKern] = {}, kern_e[kRing][kKern] = {};
     int kern_n[kRing] = {};
@@ -375,7 +377,7 @@ void shape_obb(const float* sh, const float* hulls, float* o) {
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls, s->d_shape_obb,
                     s->d_actor_root, s->d_root_row, s->d_slot_global, s->d_slot_actor, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
-                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_chain_uni, s->d_fp_mask, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
+                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_chain_uni, s->d_fp_mask, s->d_env_carry, s->d_env_ctab, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
                     s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -1041,6 +1043,10 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         HIP_TRY(dalloc(&s->d_fp_mask, nm));
         HIP_TRY(hipMemset(s->d_fpatch, 0, np * MG_FP_N * sizeof(float)));
         HIP_TRY(hipMemset(s->d_fp_mask, 0, nm * sizeof(unsigned)));
+        // the coupled step's per-env records between its launches (mg_env.hip)
+        const size_t nc = (size_t)std::max(s->n_coupled, 1);
+        HIP_TRY(dalloc(&s->d_env_carry, nc * mg_env_carry_floats()));
+        HIP_TRY(dalloc(&s->d_env_ctab, nc * mg_env_ctab_floats()));
         const size_t ng = (size_t)std::max(s->nf1, 1) * MG_FP_N;   // no ground patch yet
         HIP_TRY(dalloc(&s->d_gpatch, ng));
         HIP_TRY(hipMemset(s->d_gpatch, 0, ng * sizeof(float)));
@@ -1147,6 +1153,8 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.pairs = s->d_pairs;
         A.fpatch = s->d_fpatch;
         A.fp_mask = s->d_fp_mask + (size_t)g.offset * MG_FP_W;
+        A.carry = s->d_env_carry + (size_t)g.offset * mg_env_carry_floats();
+        A.ctab = s->d_env_ctab + (size_t)g.offset * mg_env_ctab_floats();
         A.nl = g.tmpl >= 0 ? g.nl : 0;
         A.ndof = g.tmpl >= 0 ? g.ndof : 0;
         A.floating = g.tmpl >= 0 ? g.floating : 0;
