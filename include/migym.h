@@ -376,6 +376,15 @@ float       mg_last_step_ms(mg_sim* sim);
  * start / stop events, the interval rocprofv3 reports for the kernel). Returns
  * the count used, or < 0. */
 int32_t     mg_step_time_stats(mg_sim* sim, int32_t n, float* avg_ms, float* min_ms, float* max_ms);
+/* Diagnostics: copy n floats of the coupled step's per-env contact tables (what
+ * the narrow-phase launch k_env_np handed to k_env_step in the last substep
+ * run) from float offset `off` to host memory `dst`; synchronises the device.
+ * A group's envs are consecutive records of 8 + 24 MAXCT floats (MAXCT 16, 48
+ * for 64-lane envs) starting at the group's first coupled row x
+ * mg_env_ctab_floats(). */
+int32_t     mg_debug_copy_ctab(mg_sim* sim, int64_t off, int32_t n, float* dst);
+int         mg_env_ctab_floats(void);
+int         mg_env_carry_floats(void);
 /* Number of bodies advanced by the free-body kernel / articulations by the
  * articulation kernel in one simulate. */
 int32_t     mg_num_free_bodies(mg_sim* sim);

@@ -140,6 +140,9 @@ def _load():
         "mg_num_free_bodies": (i32, [vp]),
         "mg_num_articulations": (i32, [vp]),
         "mg_num_coupled_envs": (i32, [vp]),
+        "mg_debug_copy_ctab": (i32, [vp, ctypes.c_int64, i32, vp]),
+        "mg_env_ctab_floats": (i32, []),
+        "mg_env_carry_floats": (i32, []),
         "mg_set_render_bodies": (i32, [vp, vp, vp, vp]),
         "mg_snapshot_render_state": (i32, [vp, vp]),
         "mg_render_cameras": (i32, [vp, vp, i32, vp]),
@@ -168,6 +171,7 @@ EXPORTED_SYMBOLS = (
     "mg_num_articulations",
     "mg_num_coupled_envs", "mg_refresh_jacobian_mass_matrix",
     "mg_set_render_bodies", "mg_snapshot_render_state", "mg_render_cameras", "mg_last_render_ms",
+    "mg_debug_copy_ctab", "mg_env_ctab_floats", "mg_env_carry_floats",
 )
 
 

@@ -113,9 +113,6 @@ struct EnvLds {
     V3 rr[MAXL];
     float tau0[G], imp[G], arm[G];
     float ru[6];                     // floating root: (w, v_O) after the unconstrained update
-    int npl[NPB];                    // candidate pairs that passed the screen
-    V3 sx[MG_ENV_MAXS];              // static bodies: pose (they do not move in the step)
-    Q4 sq[MG_ENV_MAXS];
     // friction anchors (patch friction): anchor k's point (its
     // A copy, world), position-sweep target velocities closing the drift of its
     // two copies along the patch tangents
@@ -125,10 +122,21 @@ struct EnvLds {
     float ae[MAXCT][2], amu[MAXCT];
     int aab[MAXCT], alast[MAXCT];
     float psum[MAXCT];               // running normal impulse of each contact's patch
-    int ppair[MAXCT];                // patch k: pair index << 10 | first contact << 4 | its placed contacts
-    unsigned fpv[MG_FP_W], fpn[MG_FP_W];   // pairs holding a patch: last substep, this one
     unsigned long long pstart;       // contacts that open a patch
 };
+// the step kernel's LDS: a 64-lane env's rows (48 contacts x 3) do not fit in
+// registers beside the rest of the step (round 4: 1,872 B of scratch per lane):
+// their J and W in LDS [row][slot] (slots < 32), their impulses (the same in
+// every lane) too. 16-lane envs keep them in registers.
+template <int MAXL, int G>
+struct EnvStepLds : EnvLds<MAXL, G> {
+    static constexpr int MAXCT = maxct<G>();
+    float Jl[G == 64 ? MAXCT * 3 : 1][G == 64 ? 32 : 1];
+    float Wl[G == 64 ? MAXCT * 3 : 1][G == 64 ? 32 : 1];
+    float laml[G == 64 ? MAXCT * 3 : 1];
+};
+
+
 
 // sum over the 16 lanes of a DPP row, the same value in every lane:
 // ror 8, ror 4, quad xor 2, quad xor 1 (oracle: red16)
@@ -175,6 +183,35 @@ __device__ __forceinline__ float bcastg(float v, int k) {
     if constexpr (G == 64) return rdlane(v, k);
     return bcast16(v, k);
 }
+
+// a row's J of this lane's slot: registers (16-lane envs) or EnvLds::Jl (64)
+template <int G, int N>
+struct RowJ {
+    float v[N];
+    __device__ __forceinline__ float get(int r, int) const { return v[r]; }
+    __device__ __forceinline__ void set(int r, int, float x) { v[r] = x; }
+    __device__ __forceinline__ float lane(int r, int ln, int k) const { return bcastg<G>(v[r], k); }
+};
+template <int N>
+struct RowJ<64, N> {
+    float (*p)[32];
+    __device__ __forceinline__ float get(int r, int ln) const { return ln < 32 ? p[r][ln] : 0.0f; }
+    __device__ __forceinline__ void set(int r, int ln, float x) { if (ln < 32) p[r][ln] = x; }
+    __device__ __forceinline__ float lane(int r, int, int k) const { return p[r][k]; }   // k < 32: a slot
+};
+// a row's accumulated impulse (the same value in every lane of the env)
+template <int G, int N>
+struct RowL {
+    float v[N];
+    __device__ __forceinline__ float get(int r) const { return v[r]; }
+    __device__ __forceinline__ void set(int r, float x) { v[r] = x; }
+};
+template <int N>
+struct RowL<64, N> {
+    float* p;
+    __device__ __forceinline__ float get(int r) const { return p[r]; }
+    __device__ __forceinline__ void set(int r, float x) { p[r] = x; }
+};
 
 // ---- cooperative convex-convex narrow phase ---------------------------------
 // A pair of convex shapes (box or hull, at least one hull) on all 16 lanes of
@@ -1162,9 +1199,16 @@ __device__ __forceinline__ float ibits(int v) { return __int_as_float(v); }
 __device__ __forceinline__ int fbits(float v) { return __float_as_int(v); }
 
 // MAXL, GM: the step kernel's link bound and lanes per env (its MAXCT); GN:
-// this kernel's lanes per env
+// this kernel's lanes per env (16 or 64). MG_NP_WAVES: the occupancy budget
+// (waves per SIMD the register allocation must allow)
+#ifndef MG_NP_GN
+#define MG_NP_GN 16
+#endif
+#ifndef MG_NP_WAVES
+#define MG_NP_WAVES 1
+#endif
 template <int MAXL, int GM, int GN>
-__global__ void __launch_bounds__(64) k_env_np(MgStep P, MgEnvArgs A) {
+__global__ void __launch_bounds__(64, MG_NP_WAVES) k_env_np(MgStep P, MgEnvArgs A) {
     constexpr int G = GN;
     constexpr int EPW = 64 / G;          // envs per wavefront
     constexpr int MAXCT = maxct<GM>();
@@ -1226,7 +1270,7 @@ __global__ void __launch_bounds__(64) k_env_np(MgStep P, MgEnvArgs A) {
     }
     __syncthreads();
     if (LA > 0) aba_fk(A, S, live && L > 0, ln, LA, x0, q0);
-    PH_MARK(6);
+    PH_MARK(17);
 
     // ================= 2. narrow phase, per block of NPB candidate pairs:
     // (a) bounding-sphere screen, one pair per lane, survivors compacted in
@@ -1455,24 +1499,24 @@ __global__ void __launch_bounds__(64) k_env_np(MgStep P, MgEnvArgs A) {
             r[12] = ibits(S.aab[k]); r[13] = ibits(S.alast[k]);
         }
     }
-    PH_MARK(1);
+    PH_MARK(21);
 }
 
 template <int MAXL, int G>
 __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     constexpr int EPW = 64 / G;          // envs per wavefront
     constexpr int MAXCT = maxct<G>();
-    __shared__ EnvLds<MAXL, G> shm[EPW];
+    __shared__ EnvStepLds<MAXL, G> shm[EPW];
     stage_links<MAXL, G>(A);
     const int gi = threadIdx.x / G;
     const int ln = threadIdx.x % G;
     const int e = blockIdx.x * EPW + gi;
     const bool live = e < A.ne;
-    EnvLds<MAXL, G>& S = shm[gi];
+    EnvStepLds<MAXL, G>& S = shm[gi];
     const int* ei = A.env_i + (size_t)(live ? e : 0) * MG_ENV_I_N;
     const int b0 = ei[0], d0 = ei[1];
     const int nfr = live ? ei[2] : 0;
-    const int pair0 = ei[14], npair = live ? ei[15] : 0;
+    const int pair0 = ei[14];
     const int L = (live && b0 >= 0) ? A.nl : 0;
     const int D = (live && b0 >= 0) ? A.ndof : 0;
     const int nb = A.nb, nd = A.nd;
@@ -1608,7 +1652,13 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
     float mcol[ND];                  // column ln of M_eff^-1 (DOF lanes)
 #pragma unroll
     for (int k = 0; k < ND; ++k) mcol[k] = 0.0f;
-    float Jr[MAXCT * 3], Wr[MAXCT * 3], lam[MAXCT * 3];
+    RowJ<G, MAXCT * 3> Jr, Wr;
+    RowL<G, MAXCT * 3> lam;
+    if constexpr (G == 64) {
+        Jr.p = S.Jl;
+        Wr.p = S.Wl;
+        lam.p = S.laml;
+    }
     PH_MARK(6);
 
     {
@@ -1768,9 +1818,9 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         for (int c = 0; c < MAXCT; ++c) {
 #pragma unroll
             for (int rw = 0; rw < 3; ++rw) {
-                Jr[c * 3 + rw] = 0.0f;
-                Wr[c * 3 + rw] = 0.0f;
-                lam[c * 3 + rw] = 0.0f;
+                Jr.set(c * 3 + rw, ln, 0.0f);
+                Wr.set(c * 3 + rw, ln, 0.0f);
+                lam.set(c * 3 + rw, 0.0f);
             }
             // row 0: contact c's normal; rows 1, 2: anchor c's friction rows
             const bool cn = c < nct, cf = c < nanc;
@@ -1805,11 +1855,12 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                             }
                         }
                     }
-                    Jr[c * 3 + rw] = J;
-                    Wr[c * 3 + rw] = W;
+                    Jr.set(c * 3 + rw, ln, J);
+                    Wr.set(c * 3 + rw, ln, W);
                 }
             }
         }
+        if constexpr (G == 64) __syncthreads();   // the rows' J (EnvLds::Jl) of every slot
         // pass 2: W = M_eff^-1 J over the articulation's slots (J_k broadcast
         // from lane k). Slot k outermost: M_eff^-1 entry k is read once for all
         // rows and the rows' sums are independent chains (row-outer, each row
@@ -1836,7 +1887,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     for (int c = 0; c < CM; ++c) {
 #pragma unroll
                         for (int rw = 0; rw < 3; ++rw)
-                            Wr[c * 3 + rw] = Wr[c * 3 + rw] + m * bcastg<G>(Jr[c * 3 + rw], k);
+                            Wr.set(c * 3 + rw, ln, Wr.get(c * 3 + rw, ln) + m * Jr.lane(c * 3 + rw, ln, k));
                     }
                 }
             }
@@ -1853,12 +1904,12 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 #pragma unroll
                 for (int rw = 0; rw < 3; ++rw) {
                     if (rw == 0 ? !cn : !cf) continue;
-                    const float den = redg<G>(Jr[c * 3 + rw] * Wr[c * 3 + rw]);
+                    const float den = redg<G>(Jr.get(c * 3 + rw, ln) * Wr.get(c * 3 + rw, ln));
                     const float kk = den > 0.0f ? 1.0f / den : 0.0f;
                     if (ln == 0) S.ck[c][rw] = kk;
                 }
                 if (cn) {
-                    const float vn0 = redg<G>(Jr[c * 3] * uv);
+                    const float vn0 = redg<G>(Jr.get(c * 3, ln) * uv);
                     if (ln == 0) S.cvn0[c] = vn0;
                 }
             }
@@ -1879,7 +1930,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 #pragma unroll
                 for (int c = 0; c < MAXCT; ++c) {
                     if (c < nct) {
-                        const float s = S.cs0[c] + redg<G>(Jr[c * 3] * dp);
+                        const float s = S.cs0[c] + redg<G>(Jr.get(c * 3, ln) * dp);
                         float tgt;
                         if (pos) {
                             tgt = -s * P.inv_sub;
@@ -1889,12 +1940,12 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                             const float ev = S.ce[c], vn0 = S.cvn0[c];
                             if (ev > 0.0f && vn0 < -P.bounce_thresh) tgt = fmaxf(tgt, -ev * vn0);
                         }
-                        const float lm = lam[c * 3];
-                        float dl = S.ck[c][0] * (tgt - redg<G>(Jr[c * 3] * uv));
+                        const float lm = lam.get(c * 3);
+                        float dl = S.ck[c][0] * (tgt - redg<G>(Jr.get(c * 3, ln) * uv));
                         const float nl = fmaxf(lm + dl, 0.0f);
                         dl = nl - lm;
-                        uv = uv + Wr[c * 3] * dl;
-                        lam[c * 3] = nl;
+                        uv = uv + Wr.get(c * 3, ln) * dl;
+                        lam.set(c * 3, nl);
                     }
                 }
             };
@@ -1907,7 +1958,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
 #pragma unroll
                 for (int c = 0; c < MAXCT; ++c) {
                     if (c < nct) {
-                        run = ((ps >> c) & 1ull) ? lam[c * 3] : run + lam[c * 3];
+                        run = ((ps >> c) & 1ull) ? lam.get(c * 3) : run + lam.get(c * 3);
                         if (ln == 0) S.psum[c] = run;
                     }
                 }
@@ -1926,16 +1977,16 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                         // each of two anchors (symmetric; the two saturate at mu N)
                         const float lim = (pc ? 0.5f : 1.0f) * mun;
                         const float tgt = pos ? S.ae[c][rw - 1] : 0.0f;   // drift closing (position sweeps)
-                        const float lm = lam[c * 3 + rw];
-                        const float raw = lm + S.ck[c][rw] * (tgt - redg<G>(Jr[c * 3 + rw] * uv));
+                        const float lm = lam.get(c * 3 + rw);
+                        const float raw = lm + S.ck[c][rw] * (tgt - redg<G>(Jr.get(c * 3 + rw, ln) * uv));
                         const float nl = fminf(fmaxf(raw, -lim), lim);
                         if (last_it && (raw > lim || raw < -lim)) {
                             if (rw == 1) clamp1 |= 1ull << c;
                             else clamp2 |= 1ull << c;
                         }
                         const float dl = nl - lm;
-                        uv = uv + Wr[c * 3 + rw] * dl;
-                        lam[c * 3 + rw] = nl;
+                        uv = uv + Wr.get(c * 3 + rw, ln) * dl;
+                        lam.set(c * 3 + rw, nl);
                     }
                 }
             }
@@ -1949,10 +2000,10 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         if (ln == 0) {
 #pragma unroll
             for (int c = 0; c < MAXCT; ++c) {
-                if (c < nct) S.clam[c][0] = lam[c * 3];
+                if (c < nct) S.clam[c][0] = lam.get(c * 3);
                 if (c < nanc) {
-                    S.clam[c][1] = lam[c * 3 + 1];
-                    S.clam[c][2] = lam[c * 3 + 2];
+                    S.clam[c][1] = lam.get(c * 3 + 1);
+                    S.clam[c][2] = lam.get(c * 3 + 2);
                 }
             }
         }
@@ -2348,6 +2399,7 @@ hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s
     const bool wide = mg_wide(A.nl, slots);
     const bool small = A.nl <= 4 && A.ndof <= 4 && !A.floating;
     const int blocks = (A.ne + 3) / 4;
+    const int np_blocks = (A.ne + 64 / MG_NP_GN - 1) / (64 / MG_NP_GN);
     MgEnvArgs B = A;
     for (int sub = 0; sub < P.substeps; ++sub) {
         B.sub = sub;
@@ -2356,10 +2408,10 @@ hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s
             MG_LAUNCH((k_env_np<MG_MAX_LINKS, 64, 64>), dim3(A.ne), dim3(64), 0, s, P, B);
             MG_LAUNCH((k_env_step<MG_MAX_LINKS, 64>), dim3(A.ne), dim3(64), 0, s, P, B);
         } else if (small) {
-            MG_LAUNCH((k_env_np<4, G16, 64>), dim3(A.ne), dim3(64), 0, s, P, B);
+            MG_LAUNCH((k_env_np<4, G16, MG_NP_GN>), dim3(np_blocks), dim3(64), 0, s, P, B);
             MG_LAUNCH((k_env_step<4, G16>), dim3(blocks), dim3(64), 0, s, P, B);
         } else {
-            MG_LAUNCH((k_env_np<16, G16, 64>), dim3(A.ne), dim3(64), 0, s, P, B);
+            MG_LAUNCH((k_env_np<16, G16, MG_NP_GN>), dim3(np_blocks), dim3(64), 0, s, P, B);
             MG_LAUNCH((k_env_step<16, G16>), dim3(blocks), dim3(64), 0, s, P, B);
         }
     }

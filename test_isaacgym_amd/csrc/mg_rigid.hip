@@ -962,6 +962,13 @@ k_rigid_step1(MgStep P, MgRigidArgs A) {
     V3 v = v3(Si[7 * si], Si[8 * si], Si[9 * si]);
     V3 w = v3(Si[10 * si], Si[11 * si], Si[12 * si]);
     const int tb = A.body_tmpl[b];
+#ifdef MG_RIGID1_PREFETCH_OUT
+    // the fused refresh's row indices, in flight with the state loads (loaded at
+    // the end they were one more memory round trip before the last stores)
+    const bool fout = (A.out_rb || A.out_root) && !WIDE;
+    const int pre_ob = fout && A.out_rb ? A.out_body[b] : -1;
+    const int pre_or = fout && A.out_root ? A.out_root_row[b] : -1;
+#endif
     V3 fext = v3(0.0f, 0.0f, 0.0f), text = v3(0.0f, 0.0f, 0.0f);
     if (A.ext) {
         fext = v3(A.ext[0 * nb + b], A.ext[1 * nb + b], A.ext[2 * nb + b]);
@@ -1024,12 +1031,18 @@ k_rigid_step1(MgStep P, MgRigidArgs A) {
         // paired gather k_gather_rb_root would write from the SoA state)
         if (live) {
             const float o[MG_STATE_N] = {x.x, x.y, x.z, q.x, q.y, q.z, q.w, v.x, v.y, v.z, w.x, w.y, w.z};
+#ifdef MG_RIGID1_PREFETCH_OUT
+            const int ob = pre_ob;
+            const int rr = pre_or;
+#else
+            const int ob = A.out_rb ? A.out_body[bo] : -1;
+            const int rr = A.out_root ? A.out_root_row[bo] : -1;
+#endif
             if (A.out_rb) {
-                float* R = A.out_rb + (size_t)A.out_body[bo] * MG_STATE_N;
+                float* R = A.out_rb + (size_t)ob * MG_STATE_N;
 #pragma unroll
                 for (int k = 0; k < MG_STATE_N; ++k) R[k] = o[k];
             }
-            const int rr = A.out_root ? A.out_root_row[bo] : -1;
             if (rr >= 0) {
                 float* Ro = A.out_root + (size_t)rr * MG_STATE_N;
 #pragma unroll

@@ -1311,6 +1311,20 @@ int32_t mg_step_time_stats(mg_sim* s, int32_t n, float* avg_ms, float* min_ms, f
     return n;
 }
 
+// diagnostics (tools/diag_franka_env.py): n floats of the coupled step's
+// contact tables (k_env_np's output of the last substep run) from float offset
+// `off` (a group's envs are consecutive records of 8 + 24 MAXCT floats from
+// its offset x mg_env_ctab_floats(); MAXCT 16, or 48 in 64-lane groups)
+int32_t mg_debug_copy_ctab(mg_sim* s, int64_t off, int32_t n, float* dst) {
+    if (!s || !s->uploaded || !s->d_env_ctab || off < 0 || n < 0 || !dst) return fail(MG_ERR_ARG, "bad arguments");
+    const int64_t total = (int64_t)std::max(s->n_coupled, 1) * mg_env_ctab_floats();
+    if (off + n > total) return fail(MG_ERR_ARG, "range beyond the contact tables");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(dst, s->d_env_ctab + off, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+    return MG_OK;
+}
+
 int32_t mg_num_free_bodies(mg_sim* s) { return s ? s->nf : 0; }
 int32_t mg_num_articulations(mg_sim* s) { return s ? s->nartic : 0; }
 int32_t mg_num_coupled_envs(mg_sim* s) { return s ? s->n_coupled : 0; }

@@ -22,6 +22,9 @@
 #     sqgimbal   SQ counter pass of k_artic_chain (tools/kbench_gimbal.py 4096 262144)
 #     sqgimbal4k SQ passes + kernel trace of k_artic_chain at 4096 gimbals alone
 #     sqrender   SQ + WRITE_SIZE passes of k_render (tools/kbench_render.py 1024 1600x900)
+#     kfprof     rocprofv3 kernel trace of tools/kbench_franka.py (KB_FRAMES, default 300) for the
+#                in-tree library and each tools/variants/libmigym_$v.so of $AB_VARIANTS
+#     rphases    tools/kbench_rigid_phases.py 4096 (k_rigid_step1 under settings that drop one part)
 #     ab         same-box A/B: in-tree libmigym.so vs tools/variants/libmigym_$AB_VARIANT.so on
 #                tools/kbench.py at $AB_SIZES (default 4096 262144), twice
 #   default: pytest,smoke,bench,prof
@@ -139,6 +142,23 @@ fi
 if has sqrender; then
   sq_pass render k_render "$SQ1" python tools/kbench_render.py 1024 1600x900 || exit 1
   sq_pass render_w k_render "WRITE_SIZE GRBM_GUI_ACTIVE" python tools/kbench_render.py 1024 1600x900 || exit 1
+fi
+if has kfprof; then
+  for v in intree ${AB_VARIANTS:-}; do
+    lib=""
+    [ "$v" != intree ] && lib=tools/variants/libmigym_$v.so
+    MIGYM_LIB=$lib KB_FRAMES=${KB_FRAMES:-300} timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+      -d gpurun_out/kfprof_${v}_$tag -o run --output-format csv -- python tools/kbench_franka.py \
+      > gpurun_out/kfprof_${v}_$tag.log 2>&1 || { tail -5 gpurun_out/kfprof_${v}_$tag.log; exit 1; }
+    echo "== $v"; grep kernel_us gpurun_out/kfprof_${v}_$tag.log | cut -c1-200
+    f=$(find gpurun_out/kfprof_${v}_$tag -name '*kernel_stats.csv' | head -1); grep -E "k_env" "$f" | cut -c1-160
+    find gpurun_out/kfprof_${v}_$tag -name '*kernel_trace.csv' -delete   # large; the stats stay
+  done
+fi
+if has rphases; then
+  timeout -k 10 300 python tools/kbench_rigid_phases.py 4096 > gpurun_out/rphases_$tag.jsonl \
+    2> gpurun_out/rphases_$tag.err || { tail -20 gpurun_out/rphases_$tag.err; exit 1; }
+  cat gpurun_out/rphases_$tag.jsonl
 fi
 if has ab; then
   for r in 1 2; do

@@ -57,7 +57,8 @@ def run(n, warm=150, steps=100):
                 names = ["unconstrained", "narrowphase_rest", "crba_minv", "rows", "tgs", "integrate", "setup",
                          "outputs", "np_screen", "np_collide", "pairs_tested", "pairs_with_hull",
                          "coop_vertices", "coop_edges", "coop_merge", "coop_edge_passes",
-                         "coop_pairs_no_contact", "unused17", "np_setup_and_one_lane_tests", "np_coop_loop", "np_placement"]
+                         "coop_pairs_no_contact", "np_kernel_setup_fk", "np_setup_and_one_lane_tests", "np_coop_loop",
+                         "np_placement", "np_kernel_patches_out"]
                 phases = {nm: buf[i] / waves / steps for i, nm in enumerate(names)}   # cycles per wave per frame
         if k == warm - 1 and hasattr(N.lib, "mg_debug_env_phase_reset"):
             torch.cuda.synchronize()
