@@ -174,7 +174,7 @@ def fuse_in_capture(sim):
 def load_pmc(name):
     """Committed rocprofv3 PMC summary (profiles/<round>_pmc_<name>.json, newest
     round first, written by profiles/collect_pmc.py): (dict, file) or (None, None)."""
-    for rnd in ("r04", "r03", "r02", "r01"):
+    for rnd in ("r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", "%s_pmc_%s.json" % (rnd, name))
         if os.path.exists(path):
             with open(path) as f:
@@ -484,18 +484,20 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
     ach = S3_BYTES_PER_ENV * n / (kms * 1e-3) / 1e9 if kms else None
     pmc, pmc_file = load_pmc("env_step_%d" % n)
     out = {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
-           "kernel": "S3 coupled step (k_env_step<16>)", "kernel_ms_avg": kms, "kernel_ms_min": kmin,
+           "kernel": "S3 coupled step: per substep k_env_np<16,16,16> (narrow phase) + k_env_step<16,16>, "
+                     "2 substeps (the frame's kernels summed)", "kernel_ms_avg": kms, "kernel_ms_min": kmin,
            "kernel_launches_timed": used,
-           "roofline": {"bound": "hbm", "kernel": "k_env_step<16, 16>", "achieved": ach, "peak": HBM_PEAK_GBS,
+           "roofline": {"bound": "hbm", "kernel": "k_env_np + k_env_step (one frame)", "achieved": ach,
+                        "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": (ach / HBM_PEAK_GBS) if ach else None,
                         "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None, "traffic_source": pmc_file,
                         "algorithmic_bytes_per_launch": S3_BYTES_PER_ENV * n,
                         "algorithmic_bytes_per_env": S3_BYTES_PER_ENV,
                         "note": "SURVEY.md §8d S3: 5,844 B per env-step (rigid-body refresh, DOF state, targets and "
                                 "efforts, Jacobian, mass matrix, DOF / body constants, contact warm-start state) "
-                                "priced on the coupled step kernel's own dispatch-timestamp duration; the kernel is "
-                                "latency bound (one 16-lane env group per wavefront quarter, 1024 waves on 1024 "
-                                "SIMDs): DESIGN.md §5"},
+                                "priced on the frame's coupled-step kernels' summed dispatch-timestamp durations "
+                                "(two substeps, each a narrow-phase and a step launch); latency bound (16 lanes per "
+                                "env, 1024 waves per launch on 1024 SIMDs): DESIGN.md §3.6.2, §5"},
            "coupled_envs": int(N.lib.mg_num_coupled_envs(sim.native)),
            "cubes_lifted_frac": float(lifted.float().mean()),
            "controller": "OSC (franka_cube_ik_osc.py:59-79,348-410) on the device",

@@ -30,7 +30,7 @@ def per_kernel(path, counter):
             continue
         name = r["Kernel_Name"]
         for key in ("k_rigid_step", "k_scatter_rows", "k_gather_rb_root", "k_gather_rows", "k_artic_step",
-                    "k_artic_chain", "k_env_step"):
+                    "k_artic_chain", "k_env_step", "k_env_np"):
             if key in name:
                 name = key
         acc[name].append(float(r["Counter_Value"]))
@@ -50,10 +50,36 @@ def other_kernel(f, nf, w, envs, out, kernel, bpe, factor_from):
     print(json.dumps(res, indent=1))
 
 
+def frame_kernels(f, nf, w, envs, out, kernels, per_frame, bpe, factor_from):
+    """Several kernels that make up one frame (the S3 coupled step: k_env_np and
+    k_env_step, each launched once per substep): bytes per frame = per_frame x
+    the sum of the kernels' per-launch averages."""
+    cal = json.load(open(factor_from))
+    factor = cal["read_factor_calibrated"]
+    parts = {}
+    for k in kernels:
+        key = [x for x in f if k in x][0]
+        wk = [x for x in w if k in x][0]
+        parts[k] = {"fetch_kib_raw": f[key], "write_kib_raw": w[wk], "launches": nf[key],
+                    "hbm_bytes_per_launch": f[key] * 1024.0 * factor + w[wk] * 1024.0}
+    total = per_frame * sum(p["hbm_bytes_per_launch"] for p in parts.values())
+    res = {"envs": envs, "kernel": " + ".join(kernels), "launches_per_frame_each": per_frame, "per_kernel": parts,
+           "read_factor_calibrated": factor, "calibration": "from %s (%s)" % (factor_from, cal["calibration"]),
+           "hbm_bytes_per_launch": total, "hbm_bytes_note": "per frame (all the frame's coupled-step launches)",
+           "algorithmic_bytes_per_launch": bpe * envs}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
 def main():
     fetch_csv, write_csv, envs, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
     f, nf = per_kernel(fetch_csv, "FETCH_SIZE")
     w, _ = per_kernel(write_csv, "WRITE_SIZE")
+    if "--frame-kernels" in sys.argv:
+        a = sys.argv
+        return frame_kernels(f, nf, w, envs, out, a[a.index("--frame-kernels") + 1].split(","),
+                             int(a[a.index("--per-frame") + 1]), int(a[a.index("--bytes-per-env") + 1]),
+                             a[a.index("--factor-from") + 1])
     if "--kernel" in sys.argv:
         a = sys.argv
         return other_kernel(f, nf, w, envs, out, a[a.index("--kernel") + 1], int(a[a.index("--bytes-per-env") + 1]),

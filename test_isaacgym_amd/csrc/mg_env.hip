@@ -80,6 +80,21 @@ constexpr int F0 = MG_ENV_FREE0;
 constexpr int ST0 = MG_ENV_STATIC0;
 constexpr int LIM0 = MG_ENV_LIMIT0;
 constexpr int NPB = 64;               // candidate pairs per screening block
+// carry record of one env between the substep launches of k_env_step
+constexpr int MG_CARRY_HDR = 24;     // x0 (3), q0 (4), free body k: x (3), q (4) at 7 + 7k
+constexpr int MG_CARRY_LANE = 8;     // per lane: qv, uv, lsum.xyz, fsum.xyz
+constexpr int MG_CARRY_LINK = 7;     // per link (after the lanes): its pose at the next substep's start
+template <int G>
+constexpr int carry_n() { return MG_CARRY_HDR + MG_CARRY_LANE * G + MG_CARRY_LINK * MG_MAX_LINKS; }
+template <int G>
+constexpr int carry_link0() { return MG_CARRY_HDR + MG_CARRY_LANE * G; }
+// MG_ENV_FK_CARRY: a substep's launch leaves the link poses at the next
+// substep's start (forward kinematics of its integrated q, the same operations
+// the next launches would run) in the carry record, so the next substep's
+// k_env_np and k_env_step read them instead of each running the kinematic scan
+#ifndef MG_ENV_FK_CARRY
+#define MG_ENV_FK_CARRY 1
+#endif
 
 template <int MAXL, int G>
 struct EnvLds {
@@ -893,8 +908,26 @@ __device__ __forceinline__ void aba_fk(const MgEnvArgs& A, SL& S, bool act, int 
 
 template <int MAXL, int G>
 __device__ __forceinline__ void aba_kin(const MgStep& P, const MgEnvArgs& A, EnvLds<MAXL, G>& S, bool act, int ln, int LA, V3 x0,
-                                        Q4 q0, const LinkC& lk, int b0) {
-    aba_fk(A, S, act, ln, LA, x0, q0);
+                                        Q4 q0, const LinkC& lk, int b0, const float* poses = nullptr) {
+    if (poses) {
+        // the link poses forward kinematics would give (MG_ENV_FK_CARRY) and the
+        // joint axes from them, as aba_fk's scan forms them
+        if (act && ln < LA) {
+            const float* c = poses + MG_CARRY_LINK * ln;
+            const Q4 ql = q4(c[3], c[4], c[5], c[6]);
+            S.xl[ln] = v3(c[0], c[1], c[2]);
+            S.ql[ln] = ql;
+            if (A.link_i[ln * MG_LINK_I_N + 0] < 0) {
+                S.zl[ln] = v3(0.0f, 0.0f, 0.0f);
+            } else {
+                const float* lf = A.link_f + ln * MG_LINK_F_N;
+                S.zl[ln] = qrot(ql, v3(lf[7], lf[8], lf[9]));
+            }
+        }
+        __syncthreads();
+    } else {
+        aba_fk(A, S, act, ln, LA, x0, q0);
+    }
     // ---- axes and inertias (lane l)
     if (act && ln < LA) {
         const int* li = A.link_i + ln * MG_LINK_I_N;
@@ -1189,11 +1222,7 @@ constexpr int MG_CT_C = 10;          // ca, cb, cp.xyz, n.xyz, cs0, ce
 constexpr int MG_CT_A = 14;          // apt.xyz, t1.xyz, t2.xyz, ae0, ae1, amu, aab, alast
 template <int MAXCT>
 constexpr int ct_n() { return MG_CT_HDR + MAXCT * (MG_CT_C + MG_CT_A); }
-// carry record of one env between the substep launches of k_env_step
-constexpr int MG_CARRY_HDR = 24;     // x0 (3), q0 (4), free body k: x (3), q (4) at 7 + 7k
-constexpr int MG_CARRY_LANE = 8;     // per lane: qv, uv, lsum.xyz, fsum.xyz
-template <int G>
-constexpr int carry_n() { return MG_CARRY_HDR + MG_CARRY_LANE * G; }
+
 
 __device__ __forceinline__ float ibits(int v) { return __int_as_float(v); }
 __device__ __forceinline__ int fbits(float v) { return __float_as_int(v); }
@@ -1219,6 +1248,23 @@ __global__ void __launch_bounds__(64, MG_NP_WAVES) k_env_np(MgStep P, MgEnvArgs 
     const int e = blockIdx.x * EPW + gi;
     const bool live = e < A.ne;
     NpLds<MAXL, MAXCT>& S = shm[gi];
+    // the scene's shape records, shape boxes and hull table in LDS for the
+    // launch (the dynamic allocation, mg_launch_env_step, when they fit): the
+    // screen and the plane / vertex / edge scans read them over and over, and
+    // from L2 each batch was a dependent round trip
+    if (A.nhull >= 0) {
+        extern __shared__ float s_scene[];
+        float* sh_s = s_scene;
+        float* sh_o = sh_s + A.nshape * MG_SHAPE_STRIDE;
+        float* sh_h = sh_o + A.nshape * MG_OBB_N;
+        for (int k = threadIdx.x; k < A.nshape * MG_SHAPE_STRIDE; k += 64) sh_s[k] = A.shapes[k];
+        for (int k = threadIdx.x; k < A.nshape * MG_OBB_N; k += 64) sh_o[k] = A.shape_obb[k];
+        for (int k = threadIdx.x; k < A.nhull; k += 64) sh_h[k] = A.hulls[k];
+        __syncthreads();
+        A.shapes = sh_s;
+        A.shape_obb = sh_o;
+        A.hulls = sh_h;
+    }
     const int* ei = A.env_i + (size_t)(live ? e : 0) * MG_ENV_I_N;
     const int b0 = ei[0], d0 = ei[1];
     const int nfr = live ? ei[2] : 0;
@@ -1268,8 +1314,17 @@ __global__ void __launch_bounds__(64, MG_NP_WAVES) k_env_np(MgStep P, MgEnvArgs 
         S.pstart = 0ull;
         S.link_rows = 0;
     }
-    __syncthreads();
-    if (LA > 0) aba_fk(A, S, live && L > 0, ln, LA, x0, q0);
+    if (MG_ENV_FK_CARRY && A.sub > 0) {   // the link poses the last substep's step kernel left
+        if (live && ln < L) {
+            const float* c = cy + carry_link0<GM>() + MG_CARRY_LINK * ln;
+            S.xl[ln] = v3(c[0], c[1], c[2]);
+            S.ql[ln] = q4(c[3], c[4], c[5], c[6]);
+        }
+        __syncthreads();
+    } else {
+        __syncthreads();
+        if (LA > 0) aba_fk(A, S, live && L > 0, ln, LA, x0, q0);
+    }
     PH_MARK(17);
 
     // ================= 2. narrow phase, per block of NPB candidate pairs:
@@ -1669,7 +1724,8 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         if (LA > 0) {
             bool xm = false, xp = false;     // this DOF runs at constant +-effort
             bool redo = live && L > 0;
-            aba_kin<MAXL, G>(P, A, S, redo, ln, LA, x0, q0, lk, b0);
+            aba_kin<MAXL, G>(P, A, S, redo, ln, LA, x0, q0, lk, b0,
+                             (MG_ENV_FK_CARRY && !first) ? cy + carry_link0<G>() : nullptr);
             for (int att = 0; att < 2; ++att) {
                 if (!__any(redo)) break;
                 if (att > 0) aba_refresh<MAXL, G>(A, S, redo, ln, LA, x0, lk, b0);
@@ -2087,6 +2143,20 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
         PH_MARK(5);
     }
     if (!A.last) {   // to the next substep's launches (k_env_np, k_env_step)
+        if (MG_ENV_FK_CARRY && LA > 0) {
+            // the next substep's link poses: forward kinematics of the integrated q
+            // (S.q) about the moved root, the operations aba_fk would run there
+            S.q[ln] = qv;
+            __syncthreads();
+            aba_fk(A, S, live && L > 0, ln, LA, x0, q0);
+            if (live && ln < L) {
+                float* c = cy + carry_link0<G>() + MG_CARRY_LINK * ln;
+                const V3 xl = S.xl[ln];
+                const Q4 ql = S.ql[ln];
+                c[0] = xl.x; c[1] = xl.y; c[2] = xl.z;
+                c[3] = ql.x; c[4] = ql.y; c[5] = ql.z; c[6] = ql.w;
+            }
+        }
         if (live) {
             if (ln == 0) {
                 cy[0] = x0.x; cy[1] = x0.y; cy[2] = x0.z;
@@ -2401,17 +2471,27 @@ hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s
     const int blocks = (A.ne + 3) / 4;
     const int np_blocks = (A.ne + 64 / MG_NP_GN - 1) / (64 / MG_NP_GN);
     MgEnvArgs B = A;
+    // k_env_np's LDS copy of the scene's shapes, shape boxes and hulls (B.nhull =
+    // -1: too large, read from global memory)
+    size_t scene = ((size_t)A.nshape * (MG_SHAPE_STRIDE + MG_OBB_N) + (size_t)A.nhull) * sizeof(float);
+#ifndef MG_NP_SCENE_LDS_MAX
+#define MG_NP_SCENE_LDS_MAX (24 * 1024)
+#endif
+    if (scene > MG_NP_SCENE_LDS_MAX || A.nhull < 0) {
+        B.nhull = -1;
+        scene = 0;
+    }
     for (int sub = 0; sub < P.substeps; ++sub) {
         B.sub = sub;
         B.last = sub == P.substeps - 1 ? 1 : 0;
         if (wide) {
-            MG_LAUNCH((k_env_np<MG_MAX_LINKS, 64, 64>), dim3(A.ne), dim3(64), 0, s, P, B);
+            MG_LAUNCH((k_env_np<MG_MAX_LINKS, 64, 64>), dim3(A.ne), dim3(64), scene, s, P, B);
             MG_LAUNCH((k_env_step<MG_MAX_LINKS, 64>), dim3(A.ne), dim3(64), 0, s, P, B);
         } else if (small) {
-            MG_LAUNCH((k_env_np<4, G16, MG_NP_GN>), dim3(np_blocks), dim3(64), 0, s, P, B);
+            MG_LAUNCH((k_env_np<4, G16, MG_NP_GN>), dim3(np_blocks), dim3(64), scene, s, P, B);
             MG_LAUNCH((k_env_step<4, G16>), dim3(blocks), dim3(64), 0, s, P, B);
         } else {
-            MG_LAUNCH((k_env_np<16, G16, MG_NP_GN>), dim3(np_blocks), dim3(64), 0, s, P, B);
+            MG_LAUNCH((k_env_np<16, G16, MG_NP_GN>), dim3(np_blocks), dim3(64), scene, s, P, B);
             MG_LAUNCH((k_env_step<16, G16>), dim3(blocks), dim3(64), 0, s, P, B);
         }
     }

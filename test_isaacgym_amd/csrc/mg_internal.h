@@ -187,6 +187,7 @@ struct MgEnvArgs {
     // one substep per launch pair (mg_env.hip k_env_np + k_env_step)
     int          sub, last;   // this launch's substep; 1: the frame's last
     float*       carry;       // [ne][carry] the step's state between its substep launches
+    int          nhull, nshape;   // floats of the hull table, shape records (k_env_np's LDS staging)
     float*       ctab;        // [ne][ctab] this substep's contacts and anchors (k_env_np -> k_env_step)
 };
 

@@ -160,6 +160,7 @@ struct mg_sim {
     float* d_chain_uni = nullptr; // [groups][MG_CHAIN_UNI_N] shared constants of chain groups (ArticGroup.uni)
     unsigned* d_fp_mask = nullptr;   // [n_coupled][MG_FP_W] pairs holding a patch
     float* d_env_carry = nullptr;    // [n_coupled][mg_env_carry_floats] coupled step state between substep launches
+    int nhull_floats = 0;            // floats of the hull table (k_env_np stages it in LDS when small)
     float* d_env_ctab = nullptr;     // [n_coupled][mg_env_ctab_floats] contacts of one substep (k_env_np -> k_env_step)
     int n_coupled = 0;
     std::vector<EnvGroup> env_groups;
@@ -898,6 +899,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(dalloc(&s->d_trec, (size_t)s->ntb * MG_TREC_N));
     HIP_TRY(dalloc(&s->d_shapes, (size_t)s->ns * MG_SHAPE_STRIDE));
     HIP_TRY(dalloc(&s->d_hulls, (size_t)(m->hulls ? m->num_hull_floats : 0)));
+    s->nhull_floats = m->hulls ? m->num_hull_floats : 0;
     HIP_TRY(dalloc(&s->d_actor_root, na));
     HIP_TRY(dalloc(&s->d_actor_dof, na + 1));
     HIP_TRY(dalloc(&s->d_cforce, (size_t)nb * 3));
@@ -1164,6 +1166,8 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl;
         A.tbf = s->d_tbf; A.tbi = s->d_tbi; A.shapes = s->d_shapes; A.hulls = s->d_hulls;
         A.shape_obb = s->d_shape_obb;
+        A.nhull = s->nhull_floats;
+        A.nshape = s->ns;
         A.dof_pos = s->d_dof; A.dof_vel = s->d_dof + s->nd;
         A.dof_tpos = s->d_dof_tgt; A.dof_tvel = s->d_dof_tgt + s->nd; A.dof_force = s->d_dof_tgt + 2 * (size_t)s->nd;
         fused_targets(s, A.dof_tpos, A.dof_tvel, A.dof_force, A.tpos_w, A.tvel_w, A.force_w);

@@ -17,6 +17,7 @@ from isaacgym import gymapi, gymtorch
 from test_isaacgym_amd import franka_control, scenes
 import kinematics64 as K
 import oracle
+import franka_geom as FG
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -97,23 +98,57 @@ def test_franka_pick_lifts_cubes(gym, n):
     sim, info, rb, dof, jac, mm, ctl = _setup(gym, n)
     maxz = torch.zeros(n, device=DEV)
     bi = torch.tensor(info["box_idxs"], device=DEV)
+    hi = torch.tensor(info["hand_idxs"], device=DEV)
+    hulls = torch.stack([hi, hi + 1, hi + 2], 1)
+    A = sim.model_arrays
+    off = float(sim.params.physx.contact_offset)
+    # hand / finger hulls inside the table box (tests/franka_geom.py), every frame
+    deep_run = torch.zeros((2, n), dtype=torch.int64, device=DEV)   # consecutive frames deeper than 1 / 5 mm
+    worst_run = torch.zeros_like(deep_run)
+    worst = torch.zeros(n, dtype=torch.float64, device=DEV)
+    lim = torch.tensor([off, 0.005], dtype=torch.float64, device=DEV)[:, None]
     for f in range(frames):
         gym.simulate(sim)
         gym.fetch_results(sim, True)
         _control(gym, sim, info, rb, dof, jac, mm, ctl, n)
         maxz = torch.maximum(maxz, rb[bi, 2])
+        d = FG.penetration_depth(A, rb, hulls, bi - 1)
+        worst = torch.maximum(worst, d)
+        deep_run = torch.where(d[None, :] > lim, deep_run + 1, torch.zeros_like(deep_run))
+        worst_run = torch.maximum(worst_run, deep_run)
     assert torch.isfinite(rb).all()
+    # No hand or finger stays inside the table. With Isaac Gym's 1 mm contact
+    # offset (franka_cube_ik_osc.py:123) a hull moving at up to ~2 m/s enters
+    # the table by up to a substep's travel before its first contact exists (no
+    # speculative contacts; tools/diag_franka_env.py: 160 of 4096 envs pass 1 mm
+    # in some frame, the deepest 17.6 mm, a hand driven down at a cube on the
+    # floor), and a hand the controller presses onto the table top (up to
+    # ~4 kN) rests a little inside it (the position sweeps' residual); the
+    # contact rows keep both shallow and short.
+    stats = {"n": n, "worst_mm": round(1e3 * float(worst.max()), 2), "worst_env": int(worst.argmax()),
+             "envs_past_1mm": int((worst > off).sum()), "envs_past_5mm": int((worst > 0.005).sum()),
+             "longest_run_past_1mm": int(worst_run[0].max()), "longest_run_past_5mm": int(worst_run[1].max()),
+             "last_frame_worst_mm": round(1e3 * float(d.max()), 2)}
+    print("hull-in-table:", stats)
+    assert stats["worst_mm"] < 30.0, stats
+    assert stats["longest_run_past_5mm"] <= 3, stats
+    assert stats["last_frame_worst_mm"] <= 5.0, stats
     frac = float((maxz > 0.55).float().mean())
     assert frac >= 0.5, "only %.2f of the cubes were lifted" % frac
     # nothing sinks through the table or the ground. A cube whose footprint
     # overlaps the table's (top at 0.4 m, half extents 0.3 / 0.5 m, cube half
     # size 0.0225 m) must not rest below the top. A cube at rest below the top
-    # beside the table must be carried by the robot: in contact (its net
-    # contact force non-zero) within 0.15 m of the hand or a finger body, that
-    # body in contact too. tools/diag_sunk.py / diag_loose.py found such cubes
-    # 0.335-0.355 m from the table centre held by the fingers, and one resting
-    # on the hand of an arm pushed against the table's side (fingers pressing
-    # the side at ~900 N, the cube's contact force its weight).
+    # beside the table must be carried by the robot: the contacts the narrow
+    # phase handed to the step (mg_debug_copy_ctab) include one between the
+    # cube and a link of the arm. The one such cube at 4096 envs (env 3043,
+    # tools/diag_franka_env.py, profiles/r05_diag_franka.jsonl) was knocked off
+    # the table's edge and rests on the forearm (links 4 and 5), pressed
+    # against the table's -x face; the arm reached around the table's corner
+    # after it and is wedged between joint 2's upper limit (a constraint row)
+    # and the table — finger A closed and pressing the corner (~980 N: the
+    # OSC torques of up to 87 N m at short levers against the limit row's
+    # reaction), finger B open — with no hull inside the table. Carried by the
+    # arm, not by the fingers, so the fingers are not required.
     ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))
     gym.refresh_net_contact_force_tensor(sim)
     z = rb[bi, 2]
@@ -124,16 +159,27 @@ def test_franka_pick_lifts_cubes(gym, n):
     below = (z > 0.3) & (z < 0.4225 - 0.005) & still
     sunk = below & overlap
     assert int(sunk.sum()) == 0, "cubes at rest inside the table: %s" % z[sunk][:8].tolist()
-    hi = torch.tensor(info["hand_idxs"], device=DEV)
-    c = rb[bi, 0:3]
-    touching = ncf[bi].norm(dim=1) > 0.0
-    carried = torch.zeros_like(touching)
-    for b_ in (hi, hi + 1, hi + 2):
-        carried |= ((rb[b_, 0:3] - c).norm(dim=1) < 0.15) & (ncf[b_].norm(dim=1) > 0.0)
-    loose = below & ~overlap & ~(carried & touching)
-    assert int(loose.sum()) == 0, "cubes at rest below the table top, beside it, not on the robot: %s" % (
-        torch.stack([z[loose], rel[loose, 0], rel[loose, 1]], 1)[:4].tolist())
-    assert int((below & ~overlap).sum()) <= n // 100    # a rare case, not a pattern
+    beside = (below & ~overlap).nonzero().flatten().tolist()
+    for e in beside:
+        rows = _env_contacts(sim, e)
+        on_arm = [(a, b) for a, b, _ in rows if (a == 64 and 0 <= b < 16) or (b == 64 and 0 <= a < 16)]
+        assert on_arm, "env %d: cube at rest below the table top beside it with no contact on the arm: %s" % (
+            e, rows)
+    assert len(beside) <= max(n // 1000, 1)    # a rare case, not a pattern
+
+
+def _env_contacts(sim, e):
+    """Env e's contacts of the last substep as k_env_np handed them to the step
+    (participants a, b: link l, free body 64 + k, static 80 + s, ground -1;
+    separation): mg_debug_copy_ctab on the 16-lane group's records."""
+    import ctypes
+    from test_isaacgym_amd import _native as N
+    ct_n = 8 + 16 * 24
+    buf = (ctypes.c_float * ct_n)()
+    N.check(N.lib.mg_debug_copy_ctab(sim.native, e * ct_n, ct_n, buf), "mg_debug_copy_ctab")
+    a = np.frombuffer(buf, np.float32)
+    ib = a.view(np.int32)
+    return [(int(ib[8 + 10 * c]), int(ib[9 + 10 * c]), float(a[16 + 10 * c])) for c in range(min(int(ib[0]), 16))]
 
 
 def test_franka_jacobian_mass_matrix_float64(gym):
