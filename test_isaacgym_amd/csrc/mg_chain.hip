@@ -124,15 +124,26 @@ __device__ __forceinline__ RI world_ri(const ChainLink& K, const M3& R, V3 xl, V
 // xp): joint rotation / offset at DOF position qj. Inside the substeps the
 // orientation is not renormalised (it is rebuilt from the joint angles and the
 // unit base orientation every pass: no drift); the output pass (NORM) is.
+// chain_rel: the joint's rotation / offset in its parent (independent of the
+// parent's pose); chain_fk_rel: composed with the parent's pose
+__device__ __forceinline__ void chain_rel(int jt, V3 po, Q4 qo, V3 ax, float qj, Q4& qrel, V3& rr) {
+    qrel = qo;
+    rr = po;
+    if (jt == MG_JOINT_REVOLUTE) qrel = qmul(qo, q_axis_angle(ax, qj));
+    else if (jt == MG_JOINT_PRISMATIC) rr = vadd(po, qrot(qo, vscale(ax, qj)));
+}
+template <bool NORM>
+__device__ __forceinline__ void chain_fk_rel(Q4 qrel, V3 rr, Q4 qp, const M3& Rp, V3 xp, Q4& ql, V3& xl) {
+    ql = NORM ? qnormalize(qmul(qp, qrel)) : qmul(qp, qrel);
+    xl = vadd(xp, rmul(Rp, rr));
+}
 template <bool NORM>
 __device__ __forceinline__ void chain_fk(int jt, V3 po, Q4 qo, V3 ax, float qj, Q4 qp, const M3& Rp, V3 xp, Q4& ql,
                                          V3& xl) {
-    Q4 qrel = qo;
-    V3 rr = po;
-    if (jt == MG_JOINT_REVOLUTE) qrel = qmul(qo, q_axis_angle(ax, qj));
-    else if (jt == MG_JOINT_PRISMATIC) rr = vadd(po, qrot(qo, vscale(ax, qj)));
-    ql = NORM ? qnormalize(qmul(qp, qrel)) : qmul(qp, qrel);
-    xl = vadd(xp, rmul(Rp, rr));
+    Q4 qrel;
+    V3 rr;
+    chain_rel(jt, po, qo, ax, qj, qrel, rr);
+    chain_fk_rel<NORM>(qrel, rr, qp, Rp, xp, ql, xl);
 }
 // joint l's motion axis about x0 (R: the link's rotation matrix)
 __device__ __forceinline__ SV chain_axis(int jt, V3 ax, const M3& R, V3 xl, V3 x0) {
@@ -556,6 +567,351 @@ __device__ __forceinline__ void chain_body(const MgStep& P, const MgArticArgs& A
     }
 }
 
+// ---- four lanes per chain (launches of at most one resident round) ----------
+// At the S2 size (4096 gimbals = 64 waves of one lane per gimbal on 1024 SIMDs)
+// the step is one wave's instruction stream (profiles/r05_sq_chain_4096.json:
+// 3,934 VALU per wave, 65 % of its quad-cycles issuing): the chain kernel runs
+// on four lanes per articulation instead, lane k of a quad owning link k.
+// Lane l forms joint l's rotation in its parent (chain_rel: the sin / cos
+// series) and the quad broadcasts them (DPP quad_perm); every lane then runs the
+// serial scan (poses, axes, velocities, bias accelerations) itself; lane l
+// forms link l's world inertia, bias force and its terms of the bias C and the
+// joint-space inertia M, the quad broadcasts the terms, and every lane adds
+// them in link order and solves, exactly as chain_body does. In the output pass lane l stores link l's rows (lane 0 the base's,
+// the root row and the DOF rows). The same operations on the same values in
+// the same order: bit-identical to chain_body and to the oracle's chain_step_.
+template <int CTRL>
+__device__ __forceinline__ float qdpp(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// lane k of each quad, to the whole quad (quad_perm [k, k, k, k])
+template <int K>
+__device__ __forceinline__ float qbc(float v) { return qdpp<K | (K << 2) | (K << 4) | (K << 6)>(v); }
+template <int K>
+__device__ __forceinline__ V3 qbc3(V3 v) { return v3(qbc<K>(v.x), qbc<K>(v.y), qbc<K>(v.z)); }
+template <int K>
+__device__ __forceinline__ SV qbcs(SV v) { return sv(qbc3<K>(v.w), qbc3<K>(v.v)); }
+template <int K>
+__device__ __forceinline__ RI qbci(const RI& I) {
+    RI r;
+    r.xx = qbc<K>(I.xx); r.yy = qbc<K>(I.yy); r.zz = qbc<K>(I.zz);
+    r.xy = qbc<K>(I.xy); r.xz = qbc<K>(I.xz); r.yz = qbc<K>(I.yz);
+    r.h = qbc3<K>(I.h);
+    r.m = qbc<K>(I.m);
+    return r;
+}
+template <int K>
+__device__ __forceinline__ Q4 qbcq(Q4 q) { return q4(qbc<K>(q.x), qbc<K>(q.y), qbc<K>(q.z), qbc<K>(q.w)); }
+
+// joint K's chain_rel from lane K (value selects: a ternary on Q4 / V3 objects
+// selects their addresses and puts them in scratch)
+template <int K>
+__device__ __forceinline__ void chain_rel_bc(int jt, Q4 qo, V3 po, Q4 a, V3 b, Q4& qr, V3& rr) {
+    qr = qo;
+    rr = po;
+    if (jt == MG_JOINT_REVOLUTE) qr = qbcq<K>(a);
+    else if (jt == MG_JOINT_PRISMATIC) rr = qbc3<K>(b);
+}
+// every joint's chain_rel at DOF positions q: lane k of the quad forms joint
+// k's (lanes 0 and k > D: joint 1's; its constants by per-lane loads: a
+// register-array select by the lane's link becomes a scratch lookup), the quad
+// broadcasts them
+struct ChainJoint {
+    int jt;
+    V3 po, ax;
+    Q4 qo;
+};
+__device__ __forceinline__ ChainJoint chain_joint(const MgArticArgs& AA, int l) {
+    const float* lf = AA.link_f + l * MG_LINK_F_N;
+    ChainJoint J;
+    J.po = v3(lf[0], lf[1], lf[2]);
+    J.qo = q4(lf[3], lf[4], lf[5], lf[6]);
+    J.ax = v3(lf[7], lf[8], lf[9]);
+    J.jt = AA.link_i[l * MG_LINK_I_N + 1];
+    return J;
+}
+template <int NL>
+__device__ __forceinline__ void chain_rels_q(const ChainJoint& Jm, int ml, const int (&jt)[NL], const V3 (&po)[NL],
+                                             const Q4 (&qo)[NL], const float* q, Q4 (&qr)[NL], V3 (&rr)[NL]) {
+    // the lane's DOF position: selects of register values (a select of two loads
+    // from one array is folded into a load at a selected index, which sends the
+    // array to LDS)
+    float qs[NL - 1];
+#pragma unroll
+    for (int d = 0; d < NL - 1; ++d) {
+        qs[d] = q[d];
+        asm volatile("" : "+v"(qs[d]));
+    }
+    float qm = qs[0];
+    if constexpr (NL > 2) qm = ml == 2 ? qs[1] : qm;
+    if constexpr (NL > 3) qm = ml == 3 ? qs[2] : qm;
+    Q4 a;
+    V3 b;
+    chain_rel(Jm.jt, Jm.po, Jm.qo, Jm.ax, qm, a, b);
+    chain_rel_bc<1>(jt[1], qo[1], po[1], a, b, qr[1], rr[1]);
+    if constexpr (NL > 2) chain_rel_bc<2>(jt[2], qo[2], po[2], a, b, qr[2], rr[2]);
+    if constexpr (NL > 3) chain_rel_bc<3>(jt[3], qo[3], po[3], a, b, qr[3], rr[3]);
+}
+// link K's terms of the bias C and the joint-space inertia M (from lane K of
+// the quad) added in link order: chain_body's accumulation, term for term
+template <int K, int D>
+__device__ __forceinline__ void chain_terms_q(const float (&ct)[D], const float (&mt)[D][D], float (&Cb)[D],
+                                              float (&M)[D][D]) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const float c = qbc<K>(ct[j]);
+        Cb[j] = j == K - 1 ? c : Cb[j] + c;
+#pragma unroll
+        for (int i = 0; i <= j; ++i) {
+            const float m = qbc<K>(mt[i][j]);
+            M[i][j] = j == K - 1 ? m : M[i][j] + m;
+        }
+    }
+}
+
+template <int NL, bool EXT, bool UNI, bool UDOF>
+__device__ __forceinline__ void chain_body_q(const MgStep& P, const MgArticArgs& AA) {
+    constexpr int D = NL - 1;
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    const int qd = threadIdx.x & 3;             // lane in the quad: this lane's link
+    const int a = t >> 2;
+    const bool live = a < AA.na;
+    const int* ai = AA.artic_i + (size_t)(live ? a : 0) * MG_ARTIC_I_N;
+    const int b0 = ai[0], d0 = ai[1], ls = ai[3];
+    const int nb = AA.nb, nd = AA.nd;
+    float* St = AA.state;
+    const float* pr = AA.dof_props;
+    const float h = P.h;
+    const int ml = qd >= 1 && qd <= D ? qd : 1;  // the link whose inertia / bias force this lane forms
+    const ChainJoint Jm = chain_joint(AA, ml);
+
+    V3 po[NL], ax[NL];
+    Q4 qo[NL];
+    int jt[NL];
+#pragma unroll
+    for (int l = 1; l < NL; ++l) {
+        const float* lf = AA.link_f + l * MG_LINK_F_N;
+        po[l] = v3(lf[0], lf[1], lf[2]);
+        qo[l] = q4(lf[3], lf[4], lf[5], lf[6]);
+        ax[l] = v3(lf[7], lf[8], lf[9]);
+        jt[l] = AA.link_i[l * MG_LINK_I_N + 1];
+    }
+    const V3 x0 = v3(fld(St, 0, nb, b0), fld(St, 1, nb, b0), fld(St, 2, nb, b0));
+    const Q4 q0 = qnormalize(q4(fld(St, 3, nb, b0), fld(St, 4, nb, b0), fld(St, 5, nb, b0), fld(St, 6, nb, b0)));
+    const M3 R0 = qmat(q0);
+    const float gflag = UNI ? AA.uni[MG_CHAIN_UNI_GRAV] : AA.tbf[fld(AA.body_tmpl, 0, 0, b0) * MG_TBODY_F_N + 4];
+    const V3 gw = gflag != 0.0f ? v3(P.g[0], P.g[1], P.g[2]) : v3(0.0f, 0.0f, 0.0f);
+    float qv[D], uv[D], arm[D];
+    ChainDof dc[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const int gd = d0 + d;
+        qv[d] = fld(AA.dof_pos, 0, 0, gd);
+        uv[d] = fld(AA.dof_vel, 0, 0, gd);
+        if constexpr (UDOF) {
+            const float* u = AA.uni + MG_CHAIN_UNI_DOF + 9 * d;
+            dc[d].mode = (int)u[0]; dc[d].kp = u[1]; dc[d].kd = u[2]; dc[d].eff = u[3]; dc[d].maxv = u[4];
+            dc[d].lo = u[5]; dc[d].hi = u[6]; dc[d].haslim = u[7] != 0.0f; arm[d] = u[8];
+        } else {
+            dc[d].mode = (int)fld(pr, 0, nd, gd); dc[d].kp = fld(pr, 1, nd, gd); dc[d].kd = fld(pr, 2, nd, gd);
+            dc[d].eff = fld(pr, 3, nd, gd); dc[d].maxv = fld(pr, 4, nd, gd); dc[d].lo = fld(pr, 5, nd, gd);
+            dc[d].hi = fld(pr, 6, nd, gd); dc[d].haslim = fld(pr, 7, nd, gd) != 0.0f; arm[d] = fld(pr, 8, nd, gd);
+        }
+        dc[d].tpos = fld(AA.dof_tpos, 0, 0, gd);
+        dc[d].tvel = fld(AA.dof_tvel, 0, 0, gd);
+        dc[d].force = fld(AA.dof_force, 0, 0, gd);
+        if (live && qd == 0) {   // fused target sets: write through (one lane of the quad)
+            if (AA.tpos_w) fld(AA.tpos_w, 0, 0, gd) = dc[d].tpos;
+            if (AA.tvel_w) fld(AA.tvel_w, 0, 0, gd) = dc[d].tvel;
+            if (AA.force_w) fld(AA.force_w, 0, 0, gd) = dc[d].force;
+        }
+    }
+    // this lane's link's mass constants
+    ChainLink lk;
+    if constexpr (UNI) {
+        const float* u = AA.uni + MG_CHAIN_UNI_LINK + 10 * (ml - 1);
+        lk.m = u[0];
+        lk.com = v3(u[1], u[2], u[3]);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) lk.ib[k] = u[4 + k];
+    } else {
+        lk = load_chain_link(AA.mass, nb, b0 + ml * ls);
+    }
+
+    for (int st = 0; st < P.substeps; ++st) {
+        SV xi[D];
+        // ---- the serial scan (every lane); the values of link ml kept aside
+        M3 Rm = R0;
+        V3 xm = x0;
+        SV vm = svzero(), am = svzero();
+        {
+            Q4 qr[NL];
+            V3 rr[NL];
+            chain_rels_q<NL>(Jm, ml, jt, po, qo, qv, qr, rr);
+            Q4 qp = q0;
+            M3 Rp = R0;
+            V3 xp = x0;
+            SV vp = svzero();
+            SV ap = sv(v3(0.0f, 0.0f, 0.0f), v3(-gw.x, -gw.y, -gw.z));
+#pragma unroll
+            for (int l = 1; l < NL; ++l) {
+                Q4 ql;
+                V3 xl;
+                chain_fk_rel<false>(qr[l], rr[l], qp, Rp, xp, ql, xl);
+                const M3 Rl = qmat(ql);
+                const SV x = chain_axis(jt[l], ax[l], Rl, xl, x0);
+                const SV vJ = svscale(x, uv[l - 1]);
+                const SV v = svadd(vp, vJ);
+                const SV acc = svadd(ap, crm_f(v, vJ));
+                xi[l - 1] = x;
+                if (l == ml) { Rm = Rl; xm = xl; vm = v; am = acc; }
+                qp = ql;
+                Rp = Rl;
+                xp = xl;
+                vp = v;
+                ap = acc;
+            }
+        }
+        // ---- link ml's rigid inertia about x0 and bias force (lane ml)
+        V3 cm;
+        const RI Im = world_ri(lk, Rm, xm, x0, cm);
+        SV fm = svadd(ri_mul(Im, am), crf_f(vm, ri_mul(Im, vm)));
+        if constexpr (EXT) {
+            const int b = b0 + ml * ls;
+            const V3 fe = v3(fld(AA.ext, 0, nb, b), fld(AA.ext, 1, nb, b), fld(AA.ext, 2, nb, b));
+            const V3 te = v3(fld(AA.ext, 3, nb, b), fld(AA.ext, 4, nb, b), fld(AA.ext, 5, nb, b));
+            fm = sv(vsub(fm.w, vadd(te, vcross(cm, fe))), vsub(fm.v, fe));
+        }
+        // ---- link ml's terms of C and M (lane ml; every j < D formed, j < ml used),
+        // then every link's from its lane, added in link order
+        float ct[D], mt[D][D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            ct[j] = sdot(xi[j], fm);
+            const SV Fm = ri_mul(Im, xi[j]);
+#pragma unroll
+            for (int i = 0; i <= j; ++i) mt[i][j] = sdot(xi[i], Fm);
+        }
+        float Cb[D];
+        float M[D][D];
+        chain_terms_q<1, D>(ct, mt, Cb, M);
+        if constexpr (D > 1) chain_terms_q<2, D>(ct, mt, Cb, M);
+        if constexpr (D > 2) chain_terms_q<3, D>(ct, mt, Cb, M);
+        // ---- drives and the solve; one re-solve with effort-limited drives
+        float qdd[D], tau0[D], imp[D], rhs[D];
+        bool xm_[D], xp_[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            xm_[d] = false;
+            xp_[d] = false;
+            chain_drive(dc[d], qv[d], uv[d], h, false, false, tau0[d], imp[d]);
+            rhs[d] = tau0[d] - Cb[d];
+        }
+        chain_solve<D>(M, arm, imp, rhs, qdd);
+        bool flip = false;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            if (dc[d].eff > 0.0f && imp[d] != 0.0f) {
+                const float actf = tau0[d] - imp[d] * qdd[d];
+                if (actf > dc[d].eff) { xm_[d] = true; xp_[d] = true; flip = true; }
+                else if (actf < -dc[d].eff) { xm_[d] = true; flip = true; }
+            }
+        }
+        if (__any(flip)) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                chain_drive(dc[d], qv[d], uv[d], h, xm_[d], xp_[d], tau0[d], imp[d]);
+                rhs[d] = tau0[d] - Cb[d];
+            }
+            chain_solve<D>(M, arm, imp, rhs, qdd);
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            float w = uv[d] + h * qdd[d];
+            if (dc[d].maxv > 0.0f) w = fminf(fmaxf(w, -dc[d].maxv), dc[d].maxv);
+            float x = qv[d] + h * w;
+            if (dc[d].haslim) {
+                if (x < dc[d].lo) { x = dc[d].lo; if (w < 0.0f) w = 0.0f; }
+                if (x > dc[d].hi) { x = dc[d].hi; if (w > 0.0f) w = 0.0f; }
+            }
+            qv[d] = x;
+            uv[d] = w;
+        }
+    }
+    if (!live) return;   // whole quads
+    // ---- outputs: DOF state (lane 0); link qd's state by forward kinematics (lane qd)
+    Q4 qr[NL];
+    V3 rr[NL];
+    chain_rels_q<NL>(Jm, ml, jt, po, qo, qv, qr, rr);   // the whole quad, before lanes leave
+    if (qd == 0) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            fld(AA.dof_pos, 0, 0, d0 + d) = qv[d];
+            fld(AA.dof_vel, 0, 0, d0 + d) = uv[d];
+        }
+        if (AA.out_dof) {
+            float* R = AA.out_dof + (size_t)d0 * 2;
+#pragma unroll
+            for (int d = 0; d < D; ++d) { R[2 * d] = qv[d]; R[2 * d + 1] = uv[d]; }
+        }
+    }
+    if (qd >= NL) return;
+    float r[MG_STATE_N] = {x0.x, x0.y, x0.z, q0.x, q0.y, q0.z, q0.w, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    {
+        Q4 qp = q0;
+        M3 Rp = R0;
+        V3 xp = x0;
+        SV vp = svzero();
+#pragma unroll
+        for (int l = 1; l < NL; ++l) {
+            Q4 ql;
+            V3 xl;
+            chain_fk_rel<true>(qr[l], rr[l], qp, Rp, xp, ql, xl);
+            const M3 Rl = qmat(ql);
+            const SV v = svadd(vp, svscale(chain_axis(jt[l], ax[l], Rl, xl, x0), uv[l - 1]));
+            if (l == qd) {
+                // COM velocity: v_O + w x (COM - x0) (lane qd's own link constants)
+                const V3 cw = vadd(vsub(xl, x0), rmul(Rl, lk.com));
+                const V3 vw = vadd(v.v, fcross(v.w, cw));
+                r[0] = xl.x; r[1] = xl.y; r[2] = xl.z;
+                r[3] = ql.x; r[4] = ql.y; r[5] = ql.z; r[6] = ql.w;
+                r[7] = vw.x; r[8] = vw.y; r[9] = vw.z;
+                r[10] = v.w.x; r[11] = v.w.y; r[12] = v.w.z;
+            }
+            qp = ql;
+            Rp = Rl;
+            xp = xl;
+            vp = v;
+        }
+    }
+    const int b = b0 + qd * ls;
+#pragma unroll
+    for (int k = 0; k < MG_STATE_N; ++k) fld(St, k, nb, b) = r[k];
+    if (AA.out_rb) {
+        float* R = AA.out_rb + (size_t)fld(AA.out_body, 0, 0, b) * MG_STATE_N;
+#pragma unroll
+        for (int k = 0; k < MG_STATE_N; ++k) R[k] = r[k];
+    }
+    if (qd == 0 && AA.out_root) {
+        const int rr = fld(AA.out_root_row, 0, 0, b0);
+        if (rr >= 0) {
+            float* R = AA.out_root + (size_t)rr * MG_STATE_N;
+#pragma unroll
+            for (int k = 0; k < MG_STATE_N; ++k) R[k] = r[k];
+        }
+    }
+}
+
+template <int NL, bool EXT, bool UNI>
+__global__ void __launch_bounds__(64, 2) k_artic_chain_q(MgStep P, MgArticArgs AA) {
+    if constexpr (UNI) {
+        if (AA.uni[MG_CHAIN_UNI_DOFOK] != 0.0f) chain_body_q<NL, EXT, true, true>(P, AA);
+        else chain_body_q<NL, EXT, true, false>(P, AA);
+    } else {
+        chain_body_q<NL, EXT, false, false>(P, AA);
+    }
+}
+
 // The DOF constants' uniformity is read at run time (AA.uni[MG_CHAIN_UNI_DOFOK],
 // one scalar load, the same branch for the whole launch): a hipGraph captured
 // while every instance shared them keeps stepping correctly after a
@@ -580,6 +936,27 @@ hipError_t mg_launch_artic_chain(const MgStep& P, const MgArticArgs& A, hipStrea
     if (A.na <= 0) return hipSuccess;
     if (!A.chain || A.nl < 2 || A.nl > 4) return hipErrorNotSupported;
     const int cb = (A.na + 63) / 64;
+#ifndef MG_CHAIN_QUAD_MAX
+#define MG_CHAIN_QUAD_MAX (64 * 1024)   // four lanes per chain up to this many lanes (one resident round)
+#endif
+    if ((long)A.na * 4 <= MG_CHAIN_QUAD_MAX) {
+        const int qb = (A.na * 4 + 63) / 64;
+#define MG_KQ(NL)                                                                                   \
+    do {                                                                                            \
+        if (A.ext) {                                                                                \
+            if (A.uni) MG_LAUNCH((k_artic_chain_q<NL, true, true>), dim3(qb), dim3(64), 0, s, P, A);  \
+            else MG_LAUNCH((k_artic_chain_q<NL, true, false>), dim3(qb), dim3(64), 0, s, P, A);       \
+        } else {                                                                                    \
+            if (A.uni) MG_LAUNCH((k_artic_chain_q<NL, false, true>), dim3(qb), dim3(64), 0, s, P, A); \
+            else MG_LAUNCH((k_artic_chain_q<NL, false, false>), dim3(qb), dim3(64), 0, s, P, A);      \
+        }                                                                                           \
+    } while (0)
+        if (A.nl == 2) MG_KQ(2);
+        else if (A.nl == 3) MG_KQ(3);
+        else MG_KQ(4);
+#undef MG_KQ
+        return hipGetLastError();
+    }
 #define MG_KC(NL)                                                                                 \
     do {                                                                                          \
         if (A.ext) {                                                                              \
