@@ -392,12 +392,14 @@ def gimbal_rate(n, steps, warmup, dev, use_graph=True):
     gym.destroy_sim(sim)
     ach = S2_BYTES_PER_ENV * n / (kms * 1e-3) / 1e9 if kms else None
     pmc, pmc_file = load_pmc("gimbal_%d" % n)
+    # four lanes per gimbal when the launch fits one resident round (mg_chain.hip MG_CHAIN_QUAD_MAX)
+    kname = "k_artic_chain_q<4>" if n * 4 <= 64 * 1024 else "k_artic_chain<4>"
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
             "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graphs is not None else "eager Python loop",
-            "kernel": "S2 articulation step (k_artic_chain<4>)", "kernel_ms_avg": kms, "kernel_ms_min": kmin,
+            "kernel": "S2 articulation step (%s)" % kname, "kernel_ms_avg": kms, "kernel_ms_min": kmin,
             "kernel_launches_timed": used, "algorithmic_bytes_per_env": S2_BYTES_PER_ENV,
             "kernel_achieved_GBs": ach,
-            "roofline": {"bound": "hbm", "kernel": "k_artic_chain<4>", "achieved": ach, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": (ach / HBM_PEAK_GBS) if ach else None,
                          "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None, "traffic_source": pmc_file,
                          "algorithmic_bytes_per_launch": S2_BYTES_PER_ENV * n,

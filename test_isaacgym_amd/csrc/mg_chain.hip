@@ -218,6 +218,26 @@ __device__ __forceinline__ void chain_solve(const float (&M)[D][D], const float*
     }
 }
 
+#ifndef MG_CHAIN_AFF
+#define MG_CHAIN_AFF 1
+#endif
+// instance a's first body, first DOF and link stride: computed for the
+// blocked layout (AA.aff: no dependent load ahead of the state loads), else
+// its artic_i row
+__device__ __forceinline__ void chain_row(const MgArticArgs& AA, int a, int nbody, int& b0, int& d0, int& ls) {
+    if (MG_CHAIN_AFF && AA.aff) {
+        const int blk = a >> 6;
+        b0 = AA.ab0 + blk * 64 * nbody + (a & 63);
+        ls = min(64, AA.na - blk * 64);
+        d0 = AA.ad0 + a * AA.ads;
+    } else {
+        const int* ai = AA.artic_i + (size_t)a * MG_ARTIC_I_N;
+        b0 = ai[0];
+        d0 = ai[1];
+        ls = ai[3];
+    }
+}
+
 // contiguous stores of n floats from registers; 16-B stores when dst is aligned
 template <int N>
 __device__ __forceinline__ void store_row(float* dst, const float (&v)[N]) {
@@ -246,6 +266,9 @@ __device__ __forceinline__ void chain_body(const MgStep& P, const MgArticArgs& A
     constexpr int D = NL - 1;
     const int a = blockIdx.x * 64 + threadIdx.x;
     const bool live = a < AA.na;
+    // the row is loaded here (a launch of several rounds hides the latency; the
+    // computed form's second path cost registers and scratch): chain_row is the
+    // quad kernel's
     const int* ai = AA.artic_i + (size_t)(live ? a : 0) * MG_ARTIC_I_N;
     const int b0 = ai[0], d0 = ai[1], ls = ai[3];   // link l: body b0 + l * ls (migym_capi.cpp)
     const int nb = AA.nb, nd = AA.nd;
@@ -676,8 +699,8 @@ __device__ __forceinline__ void chain_body_q(const MgStep& P, const MgArticArgs&
     const int qd = threadIdx.x & 3;             // lane in the quad: this lane's link
     const int a = t >> 2;
     const bool live = a < AA.na;
-    const int* ai = AA.artic_i + (size_t)(live ? a : 0) * MG_ARTIC_I_N;
-    const int b0 = ai[0], d0 = ai[1], ls = ai[3];
+    int b0, d0, ls;
+    chain_row(AA, live ? a : 0, NL, b0, d0, ls);
     const int nb = AA.nb, nd = AA.nd;
     float* St = AA.state;
     const float* pr = AA.dof_props;

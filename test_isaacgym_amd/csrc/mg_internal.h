@@ -42,7 +42,9 @@ struct MgStep {
 // bounding radius), then that shared mass row (MG_MASS_N floats)
 #define MG_TREC_N        (MG_TBODY_F_N + MG_SHAPE_STRIDE + MG_MASS_N)
 #define MG_TREC_MASS     (MG_TBODY_F_N + MG_SHAPE_STRIDE)
+#ifndef MG_TREC_LDS_MAX
 #define MG_TREC_LDS_MAX  (48 * 1024)
+#endif
 
 // Kernel argument block of the free-body step (SoA arrays, stride = nb).
 struct MgRigidArgs {
@@ -80,6 +82,10 @@ struct MgArticArgs {
     int          na;          // articulation instances in this launch
     int          nb, nd;      // SoA strides
     const int*   artic_i;     // [na][4] first_body, first_dof, tmpl, pad
+    // aff: instance a's row is computed, not loaded (migym_capi.cpp; the blocked
+    // chain layout): first body ab0 + (a / 64) * 64 * nbl + a % 64, link stride
+    // min(64, na - 64 (a / 64)), first DOF ad0 + a * ads
+    int          aff, ab0, ad0, ads;
     int          tmpl;        // template id handled by this launch
     int          nl, ndof;    // links / dofs of the template
     int          nbl;         // bodies of the template (nl minus virtual links; Jacobian rows)

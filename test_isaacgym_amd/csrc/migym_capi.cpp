@@ -69,6 +69,8 @@ struct ArticGroup {
     int nbody;                     // bodies per instance (nl minus the virtual links of ball joints)
     int offset, count;             // into the template-sorted instance list (all instances)
     int step_offset, step_count;   // into the list stepped by k_artic_chain / k_artic_lanes (uncoupled envs)
+    // the stepped instances' rows are affine in the instance (MgArticArgs::aff)
+    int aff = 0, aff_b0 = 0, aff_d0 = 0, aff_ds = 0;
 };
 
 // coupled envs (mg_env.hip) of one articulation template (tmpl -1: none)
@@ -848,6 +850,22 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     for (int i = 0; i < nb; ++i) perm[order[i]] = i;
     for (size_t k = 0; k < artic_sorted.size(); k += MG_ARTIC_I_N) artic_sorted[k] = perm[artic_sorted[k]];
     for (size_t k = 0; k < artic_step.size(); k += MG_ARTIC_I_N) artic_step[k] = perm[artic_step[k]];
+    // chain groups whose stepped rows follow the blocked layout from one base
+    // slot and one DOF stride: the kernel computes them (MgArticArgs::aff)
+    for (ArticGroup& g : s->groups) {
+        g.aff = 0;
+        if (!(g.chain && g.nl >= 2 && g.nl <= 4) || g.step_count == 0) continue;
+        const int* r0 = artic_step.data() + (size_t)g.step_offset * MG_ARTIC_I_N;
+        const int B = r0[0], D = r0[1];
+        const int DS = g.step_count > 1 ? r0[MG_ARTIC_I_N + 1] - D : 0;
+        bool ok = true;
+        for (int k = 0; k < g.step_count && ok; ++k) {
+            const int* r = r0 + (size_t)k * MG_ARTIC_I_N;
+            const int blk = k / 64, j = k % 64, cnt = std::min(64, g.step_count - blk * 64);
+            ok = r[0] == B + blk * 64 * g.nbody + j && r[3] == cnt && r[1] == D + k * DS;
+        }
+        if (ok) { g.aff = 1; g.aff_b0 = B; g.aff_d0 = D; g.aff_ds = DS; }
+    }
     // coupled env rows: internal slots, grouped by articulation template (-1 first)
     std::vector<int> env_flat;
     s->env_groups.clear();
@@ -1128,6 +1146,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.uni = g.uni_mass ? s->d_chain_uni + gi * MG_CHAIN_UNI_N : nullptr;
         A.na = g.step_count; A.nb = s->nb; A.nd = s->nd;
         A.artic_i = s->d_artic_step + (size_t)g.step_offset * MG_ARTIC_I_N;
+        A.aff = g.aff; A.ab0 = g.aff_b0; A.ad0 = g.aff_d0; A.ads = g.aff_ds;
         A.tmpl = g.tmpl; A.nl = g.nl; A.ndof = g.ndof; A.fixed_base = g.fixed_base; A.chain = g.chain; A.nbl = g.nbody;
         A.link_f = s->d_link_f + (size_t)g.first_link * MG_LINK_F_N;
         A.link_i = s->d_link_i + (size_t)g.first_link * MG_LINK_I_N;
