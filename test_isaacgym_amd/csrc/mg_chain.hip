@@ -40,6 +40,31 @@
 #include "mg_spatial.h"
 #include "mg_world.h"
 
+#ifdef MG_CHAIN_STAMPS
+// diagnostic build only (tools/kbench_gimbal_stamps.py): s_memtime stamps of
+// each quad-kernel wave at its phase boundaries, lane 0 -> g_chain_stamp[wave]
+#define MG_CHAIN_NSTAMP 8
+__device__ unsigned long long g_chain_stamp[4096][MG_CHAIN_NSTAMP];
+extern "C" int mg_debug_chain_stamps(unsigned long long* out, int nwaves) {
+    if (nwaves > 4096) nwaves = 4096;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_stamp), (size_t)nwaves * MG_CHAIN_NSTAMP * 8) == hipSuccess ? 0
+                                                                                                             : -1;
+}
+__device__ __forceinline__ unsigned long long chain_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define CSTAMP(k) do { const unsigned long long t_ = chain_stamp(); \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_chain_stamp[blockIdx.x][k] = t_; } while (0)
+#define CUSE(v) asm volatile("" ::"v"(v))
+#else
+#define CSTAMP(k) do { } while (0)
+#define CUSE(v) do { } while (0)
+#endif
+
 namespace {
 
 // compact rigid spatial inertia about x0 in world axes:
@@ -695,6 +720,7 @@ __device__ __forceinline__ void chain_terms_q(const float (&ct)[D], const float 
 template <int NL, bool EXT, bool UNI, bool UDOF>
 __device__ __forceinline__ void chain_body_q(const MgStep& P, const MgArticArgs& AA) {
     constexpr int D = NL - 1;
+    CSTAMP(0);
     const int t = blockIdx.x * 64 + threadIdx.x;
     const int qd = threadIdx.x & 3;             // lane in the quad: this lane's link
     const int a = t >> 2;
@@ -761,6 +787,8 @@ __device__ __forceinline__ void chain_body_q(const MgStep& P, const MgArticArgs&
         lk = load_chain_link(AA.mass, nb, b0 + ml * ls);
     }
 
+    CUSE(x0.x); CUSE(q0.w); CUSE(qv[0]); CUSE(uv[D - 1]); CUSE(dc[D - 1].tpos); CUSE(lk.m);
+    CSTAMP(1);   // inputs in registers
     for (int st = 0; st < P.substeps; ++st) {
         SV xi[D];
         // ---- the serial scan (every lane); the values of link ml kept aside
@@ -860,6 +888,8 @@ __device__ __forceinline__ void chain_body_q(const MgStep& P, const MgArticArgs&
             qv[d] = x;
             uv[d] = w;
         }
+        CUSE(qv[0]);
+        if (st == 0) CSTAMP(2); else CSTAMP(3);
     }
     if (!live) return;   // whole quads
     // ---- outputs: DOF state (lane 0); link qd's state by forward kinematics (lane qd)
@@ -907,22 +937,33 @@ __device__ __forceinline__ void chain_body_q(const MgStep& P, const MgArticArgs&
             vp = v;
         }
     }
+    CUSE(r[0]); CUSE(r[12]);
+    CSTAMP(4);   // output rows formed
     const int b = b0 + qd * ls;
+    // (the fused refresh's row indices loaded with the inputs instead measured
+    // the same: 9.88 vs 9.89 us at 4096 gimbals)
+    const int out_b = AA.out_rb ? fld(AA.out_body, 0, 0, b) : 0;
+    const int out_r = AA.out_root ? fld(AA.out_root_row, 0, 0, b0) : -1;
 #pragma unroll
     for (int k = 0; k < MG_STATE_N; ++k) fld(St, k, nb, b) = r[k];
     if (AA.out_rb) {
-        float* R = AA.out_rb + (size_t)fld(AA.out_body, 0, 0, b) * MG_STATE_N;
+        float* R = AA.out_rb + (size_t)out_b * MG_STATE_N;
 #pragma unroll
         for (int k = 0; k < MG_STATE_N; ++k) R[k] = r[k];
     }
     if (qd == 0 && AA.out_root) {
-        const int rr = fld(AA.out_root_row, 0, 0, b0);
+        const int rr = out_r;
         if (rr >= 0) {
             float* R = AA.out_root + (size_t)rr * MG_STATE_N;
 #pragma unroll
             for (int k = 0; k < MG_STATE_N; ++k) R[k] = r[k];
         }
     }
+    CSTAMP(5);   // stores issued
+#ifdef MG_CHAIN_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    CSTAMP(6);   // stores complete
+#endif
 }
 
 template <int NL, bool EXT, bool UNI>
