@@ -69,6 +69,7 @@ if has prof; then
     || { tail -20 gpurun_out/prof_$tag.log; exit 1; }
   tail -1 gpurun_out/prof_$tag.log | cut -c1-300
   f=$(find gpurun_out/prof_$tag -name '*kernel_stats.csv' | head -1); cut -c1-150 "$f" | head -16
+  find gpurun_out/prof_$tag -name '*kernel_trace.csv' -delete   # the summary is kept (gpurun_out <= 64 MiB)
 fi
 if has pmc; then
   # FETCH_SIZE and WRITE_SIZE in separate runs (one counter block each, no trace
@@ -80,9 +81,9 @@ if has pmc; then
         > gpurun_out/pmc_${c}_$n.log 2>&1 || { tail -20 gpurun_out/pmc_${c}_$n.log; exit 1; }
     done
   done
-  for n in ${PMC_GIMBAL_SIZES:-262144}; do          # S2: k_artic_chain (tools/kbench_gimbal.py)
+  for n in ${PMC_GIMBAL_SIZES:-262144}; do          # S2: k_artic_chain (tools/kbench_gimbal.py, fused as bench.py)
     for c in FETCH_SIZE WRITE_SIZE; do
-      timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmcg_${c}_$n -o run --output-format csv -- \
+      MIGYM_KB_FUSED=1 timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmcg_${c}_$n -o run --output-format csv -- \
         python tools/kbench_gimbal.py $n > gpurun_out/pmcg_${c}_$n.log 2>&1 || { tail -20 gpurun_out/pmcg_${c}_$n.log; exit 1; }
     done
   done
