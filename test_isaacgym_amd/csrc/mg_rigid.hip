@@ -39,6 +39,32 @@
 #include "mg_internal.h"
 #include "mg_math.h"
 
+#ifdef MG_RIGID1_STAMPS
+// diagnostic build only (tools/kbench_rigid_stamps.py): s_memtime stamps of
+// each k_rigid_step1 wave at its phase boundaries, lane 0 -> g_rigid_stamp[wave]
+#define MG_RIGID1_NSTAMP 18
+__device__ unsigned long long g_rigid_stamp[4096][MG_RIGID1_NSTAMP];
+extern "C" int mg_debug_rigid_stamps(unsigned long long* out, int nwaves) {
+    if (nwaves > 4096) nwaves = 4096;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rigid_stamp), (size_t)nwaves * MG_RIGID1_NSTAMP * 8) == hipSuccess
+               ? 0
+               : -1;
+}
+__device__ __forceinline__ unsigned long long rigid_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define RSTAMP(k) do { const unsigned long long t_ = rigid_stamp(); \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_rigid_stamp[blockIdx.x][k] = t_; } while (0)
+#define RUSE(v) asm volatile("" ::"v"(v))
+#else
+#define RSTAMP(k) do { } while (0)
+#define RUSE(v) do { } while (0)
+#endif
+
 namespace {
 
 // ---- ground basis: general (n, t1, t2) or the +Z specialisation -----------
@@ -602,7 +628,13 @@ __device__ __forceinline__ void tgs_zp(const MgStep& P, NRow (&sl)[4], ARow (&an
     f2 DW = pk2(dth.x, dth.y), DZ = pk2(dth.z, dx.z), DV = pk2(dx.x, dx.y);
     // the packed operands are named values, not arrays: an array of pairs built
     // lane by lane was kept in scratch (a memory round trip per substep)
-    const f2 S0a = pk2(sl[0].s0, sl[1].s0), S0b = pk2(sl[2].s0, sl[3].s0);
+    float s0r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // register copies: the pairs of loads were built through scratch
+        s0r[j] = sl[j].s0;
+        asm volatile("" : "+v"(s0r[j]));
+    }
+    const f2 S0a = pk2(s0r[0], s0r[1]), S0b = pk2(s0r[2], s0r[3]);
     const f2 RYa = pk2(sl[0].r.y, sl[1].r.y), RYb = pk2(sl[2].r.y, sl[3].r.y);
     const f2 NRXa = pk2(-sl[0].r.x, -sl[1].r.x), NRXb = pk2(-sl[2].r.x, -sl[3].r.x);
     // separations of slots (2h, 2h+1): s0 + dx.z + dth.x r.y - dth.y r.x (BasisZ::ps)
@@ -735,6 +767,8 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
         }
     }
 
+    RUSE(R.cnt); RUSE(R.aA[1].z);
+    RSTAMP(2);   // patch record read
     q = qnormalize(q);
     for (int st = 0; st < P.substeps; ++st) {
         const S3 Iw = sym_rdrt(qmat(inertia_frame(q, iq)), invI);
@@ -755,6 +789,8 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
             if (w2 > max_av2) w = vscale(w, sqrtf(max_av2 / w2));
         }
 
+        RUSE(v.x); RUSE(w.z); RUSE(xc.x);
+        if (st < 2) RSTAMP(3 + 6 * st);   // free-flight velocity, Iw, COM
         // 2. ground contacts: candidate k of the shape -> slot k
         NRow sl[4];
         bool on[4];
@@ -780,6 +816,8 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
                     cp[k] = p;
                 }
             });
+        RUSE(sl[0].s0); RUSE(sl[3].r.z);
+        if (st < 2) RSTAMP(4 + 6 * st);   // candidates
         bool any = false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) any = any || on[j];
@@ -793,6 +831,8 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
             R.cnt = 0;
         }
 
+        RUSE(R.cnt);
+        if (st < 2) RSTAMP(5 + 6 * st);   // patch update
         // 3. TGS (skipped by a wave in which no body touches the ground)
         V3 dx = v3(0.0f, 0.0f, 0.0f), dth = v3(0.0f, 0.0f, 0.0f);
         if (__any(any)) {
@@ -840,6 +880,8 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
             // anchors exerts no yaw torque), and the two saturate at mu N together
             const float share = R.cnt == 2 ? 0.5f : 1.0f;
             const int nit = P.npos + P.nvel;
+            RUSE(an[1].k2); RUSE(sl[3].kn);
+            if (st < 2) RSTAMP(6 + 6 * st);   // row constants, anchor rows
             if constexpr (B::kPacked && PACK) {
                 tgs_zp(P, sl, an, share * mu, e, v, w, dx, dth, invm, c01, c02, c11, c12);
             } else
@@ -906,10 +948,14 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
             }
         }
 
+        RUSE(dx.x); RUSE(dth.z);
+        if (st < 2) RSTAMP(7 + 6 * st);   // solver sweeps (or free flight)
         // 4. pose update (centre of mass moves by the integrated delta)
         const V3 xc1 = vadd(xc, dx);
         q = qintegrate(q, dth);
         x = origin_from_com(xc1, q, com);
+        RUSE(x.x); RUSE(q.w);
+        if (st < 2) RSTAMP(8 + 6 * st);   // pose update
     }
     // the patch for the next step: the anchor count always, the anchors while held
     if (gp && has_shape) {
@@ -942,6 +988,7 @@ __global__ void __launch_bounds__(64, UPZ && WIDE ? MG_RIGID1_WIDE_WAVES : (UPZ 
 k_rigid_step1(MgStep P, MgRigidArgs A) {
     extern __shared__ float s_trec[];
     const int i = (WIDE ? gridDim.x - 1 - blockIdx.x : blockIdx.x) * 64 + threadIdx.x;
+    RSTAMP(0);
     const bool live = i < A.nf;
     const int b = A.free_ids ? A.free_ids[live ? i : A.nf - 1] : (live ? i : A.nf - 1);
     const int nb = A.nb;
@@ -997,6 +1044,8 @@ k_rigid_step1(MgStep P, MgRigidArgs A) {
     const Q4 iq = q4(mr[4], mr[5], mr[6], mr[7]);
     const V3 com = v3(mr[8], mr[9], mr[10]);
     V3 fsum = v3(0.0f, 0.0f, 0.0f);
+    RUSE(x.x); RUSE(q.w); RUSE(w.z); RUSE(invm); RUSE(com.z); RUSE(T[4]);
+    RSTAMP(1);   // state, template record, mass row in registers
     // this body's ground-patch record (slot b of the SoA [MG_FP_N][gstride] table)
     // and its LDS copy during the frame
     float* gp = live && A.gpatch ? A.gpatch + b : nullptr;
@@ -1049,6 +1098,11 @@ k_rigid_step1(MgStep P, MgRigidArgs A) {
                 for (int k = 0; k < MG_STATE_N; ++k) Ro[k] = o[k];
             }
         }
+        RSTAMP(15);   // all stores issued
+#ifdef MG_RIGID1_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        RSTAMP(16);   // stores complete
+#endif
     } else if (A.out_rb || A.out_root) {   // launch-uniform
         // Wide launches are issue-bound, and the rows are 52-B AoS records, every
         // other one per wave (the wave holds one template: UAVs or cars): written
