@@ -490,6 +490,9 @@ __device__ __forceinline__ void rigid_body(const B& G, const MgStep& P, const Mg
 }
 
 // ---- single-shape bodies: k_rigid_step1 ------------------------------------
+#ifndef MG_RIGID1_SHAPE_REGS
+#define MG_RIGID1_SHAPE_REGS 1
+#endif
 // Friction is PhysX's patch friction, as in the coupled
 // step (§3.6.1): the body-ground pair's contacts form one patch whose friction
 // acts at up to two anchors, each fixed on the body (body frame) and on the
@@ -511,70 +514,70 @@ struct GPatch {
 };
 // Anchors are placed by candidate index during the scan and turned into body
 // copies (qrot_inv(q, p - x)) once per slot after it, from the scan points w0 /
-// w1 (the candidate each slot ended with): the oracle's gpatch_update_ values,
-// without a rotation per placement inside divergent branches. The normal test
-// takes only the normal component of the rotated patch normal (G.dn: for the +Z
-// ground one component of qrot; the same value as the oracle's dot product).
+// w1 (the candidate each slot ended with): the oracle's gpatch_update_ values.
+// The normal test takes only the normal component of the rotated patch normal
+// (G.dn: for the +Z ground one component of qrot; the same value as the
+// oracle's dot product).
+// Branch-free: every candidate value is formed on every lane and the oracle's
+// branches become selects (the lanes of a wave hold different contact states,
+// so the branches diverged and the wave paid every side plus the exec-mask
+// bookkeeping: ~2.9k cycles per substep of a vehicle wave, tools/
+// kbench_rigid_stamps.py). The values selected are the ones the branches
+// computed, by the same operations, so results are unchanged.
 template <class B>
 __device__ __forceinline__ void ground_patch_update(const B& G, GPatch& R, V3 x, Q4 q, V3 n0, const V3 (&p)[4],
                                                     const float (&s0)[4], const bool (&on)[4], float fot,
                                                     float corr) {
     const float c2 = corr * corr;
+    const V3 z3 = v3(0.0f, 0.0f, 0.0f);
     int cnt = R.cnt;
-    if (cnt > 0 && G.dn(qrot(q, R.nA)) < MG_FP_NORMAL_COS) cnt = 0;
+    const float nd = G.dn(qrot(q, R.nA));
+    if (cnt > 0 && nd < MG_FP_NORMAL_COS) cnt = 0;
+    // held anchors: kept while the body's copy stays within the correlation
+    // distance of the ground's
+    const V3 wa0 = vadd(x, qrot(q, R.aA[0]));
+    const V3 wa1 = vadd(x, qrot(q, R.aA[1]));
+    const V3 d0v = vsub(wa0, R.aB[0]), d1v = vsub(wa1, R.aB[1]);
+    const bool k0 = 0 < cnt && vdot(d0v, d0v) <= c2;
+    const bool k1 = 1 < cnt && vdot(d1v, d1v) <= c2;
     GPatch N;
-    N.cnt = 0;
-    N.aA[0] = N.aA[1] = N.aB[0] = N.aB[1] = v3(0.0f, 0.0f, 0.0f);
-    V3 w0 = v3(0.0f, 0.0f, 0.0f), w1 = v3(0.0f, 0.0f, 0.0f);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        if (k < cnt) {
-            const V3 wa = vadd(x, qrot(q, R.aA[k]));
-            const V3 d = vsub(wa, R.aB[k]);
-            if (vdot(d, d) <= c2) {
-                if (N.cnt == 0) { N.aA[0] = R.aA[k]; N.aB[0] = R.aB[k]; w0 = wa; }
-                else { N.aA[1] = R.aA[k]; N.aB[1] = R.aB[k]; }
-                N.cnt = N.cnt + 1;
-            }
-        }
-    }
-    const int kept = N.cnt;
+    N.aA[0] = vsel(k0, R.aA[0], vsel(k1, R.aA[1], z3));
+    N.aB[0] = vsel(k0, R.aB[0], vsel(k1, R.aB[1], z3));
+    N.aA[1] = vsel(k0 && k1, R.aA[1], z3);
+    N.aB[1] = vsel(k0 && k1, R.aB[1], z3);
+    V3 w0 = vsel(k0, wa0, vsel(k1, wa1, z3));
+    V3 w1 = z3;
+    const int kept = (k0 ? 1 : 0) + (k1 ? 1 : 0);
+    // growth from this substep's contacts in slot order (only while fewer than
+    // two anchors are held): the first, then one farther than the correlation
+    // distance, then a candidate replacing whichever end spreads the pair most
     int nc = kept;
-    if (nc < 2) {
-        float dd = 0.0f;
-        int sel0 = -1, sel1 = -1;
+    float dd = 0.0f;
+    bool set0 = false, set1 = false;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (on[j] && s0[j] <= fot) {
-                const V3 pj = p[j];
-                if (nc == 0) {
-                    sel0 = j; w0 = pj; nc = 1;
-                } else if (nc == 1) {
-                    const V3 d = vsub(pj, w0);
-                    const float d2 = vdot(d, d);
-                    if (d2 > c2) { sel1 = j; w1 = pj; dd = d2; nc = 2; }
-                } else {
-                    const V3 e0 = vsub(pj, w0), e1 = vsub(pj, w1);
-                    const float d0 = vdot(e0, e0), d1 = vdot(e1, e1);
-                    if (d0 > d1) {
-                        if (d0 > dd) { sel1 = j; w1 = pj; dd = d0; }
-                    } else if (d1 > dd) {
-                        sel0 = j; w0 = pj; dd = d1;
-                    }
-                }
-            }
-        }
-        if (sel0 >= 0) {
-            N.aA[0] = qrot_inv(q, vsub(w0, x));
-            N.aB[0] = w0;
-        }
-        if (sel1 >= 0) {
-            N.aA[1] = qrot_inv(q, vsub(w1, x));
-            N.aB[1] = w1;
-        }
-        N.cnt = nc;
+    for (int j = 0; j < 4; ++j) {
+        const bool c = kept < 2 && on[j] && s0[j] <= fot;
+        const V3 pj = p[j];
+        const V3 e0 = vsub(pj, w0), e1 = vsub(pj, w1);
+        const float dj0 = vdot(e0, e0), dj1 = vdot(e1, e1);
+        const bool a0 = c && nc == 0;
+        const bool a1 = c && nc == 1 && dj0 > c2;
+        const bool a2 = c && nc == 2 && dj0 > dj1 && dj0 > dd;
+        const bool a3 = c && nc == 2 && !(dj0 > dj1) && dj1 > dd;
+        const bool to0 = a0 || a3, to1 = a1 || a2;
+        dd = (a1 || a2) ? dj0 : (a3 ? dj1 : dd);
+        w0 = vsel(to0, pj, w0);
+        w1 = vsel(to1, pj, w1);
+        set0 = set0 || to0;
+        set1 = set1 || to1;
+        nc = a0 ? 1 : (a1 ? 2 : nc);
     }
-    N.nA = kept > 0 ? R.nA : qrot_inv(q, n0);
+    N.aA[0] = vsel(set0, qrot_inv(q, vsub(w0, x)), N.aA[0]);
+    N.aB[0] = vsel(set0, w0, N.aB[0]);
+    N.aA[1] = vsel(set1, qrot_inv(q, vsub(w1, x)), N.aA[1]);
+    N.aB[1] = vsel(set1, w1, N.aB[1]);
+    N.cnt = nc;
+    N.nA = vsel(kept > 0, R.nA, qrot_inv(q, n0));
     // the stored record changes unless every held anchor was kept in place and
     // none was placed (a resting body: most steps)
     N.dirty = R.dirty || !(kept == R.cnt && nc == kept);
@@ -729,10 +732,17 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
                                             V3& w, V3& fsum, float invm, V3 invI, Q4 iq, V3 com, bool has_ext,
                                             V3 fext, V3 text, const float* hulls, float* gp, int gstride) {
     const float lin_damp = T[0], ang_damp = T[1], max_lv = T[2], max_av = T[3], grav_on = T[4];
-    // the shape record stays in the template record (LDS when staged) and is
-    // read by each substep's candidate search: registers are scarcer than LDS
-    // reads at three waves per SIMD
+    // the shape record: wide launches read it from the template record (LDS
+    // when staged) in each substep's candidate search — registers are scarcer
+    // than LDS reads at three waves per SIMD; a one-round launch (PACK) keeps it
+    // in registers (the LDS reads were on each substep's dependency chain)
+    float shr[MG_SHAPE_STRIDE];
     const float* sh = T + MG_TBODY_F_N;
+    if constexpr (PACK && MG_RIGID1_SHAPE_REGS) {
+#pragma unroll
+        for (int k = 0; k < 14; ++k) shr[k] = sh[k];
+        sh = shr;
+    }
     const bool has_shape = P.has_ground && sh[0] >= 0.0f;
     const float rho = sh[13];   // bounding radius about the body origin (< 0: none)
     const float h = P.h;
@@ -809,12 +819,13 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
         const bool far = rho >= 0.0f && clear - rho > P.contact_offset + 1e-3f * (1.0f + fabsf(clear) + rho);
         if (__any(has_shape && !far) && has_shape)
             shape_candidates(G, P, sh, q, x, hulls, [&](int k, V3 p, float sep, float, float) {
-                if (sep < P.contact_offset) {
-                    on[k] = true;
-                    sl[k].r = vsub(p, xc);
-                    sl[k].s0 = sep - P.rest_offset;
-                    cp[k] = p;
-                }
+                // selects, not a branch: the candidates of a wave's bodies pass
+                // the test on different lanes
+                const bool c = sep < P.contact_offset;
+                on[k] = on[k] || c;
+                sl[k].r = vsel(c, vsub(p, xc), sl[k].r);
+                sl[k].s0 = c ? sep - P.rest_offset : sl[k].s0;
+                cp[k] = vsel(c, p, cp[k]);
             });
         RUSE(sl[0].s0); RUSE(sl[3].r.z);
         if (st < 2) RSTAMP(4 + 6 * st);   // candidates
@@ -850,16 +861,13 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
                 const bool act = a < R.cnt;
-                V3 r = v3(0.0f, 0.0f, 0.0f);
-                float e1 = 0.0f, e2 = 0.0f;
-                if (act) {
-                    const V3 wa = vadd(x, qrot(q, R.aA[a]));
-                    const V3 dr = vsub(wa, R.aB[a]);
-                    const float kd = 0.8f * P.inv_h;
-                    r = vsub(wa, xc);
-                    e1 = fminf(fmaxf(-G.d1(dr) * kd, -P.max_depen), P.max_depen);
-                    e2 = fminf(fmaxf(-G.d2(dr) * kd, -P.max_depen), P.max_depen);
-                }
+                // formed on every lane, selected (a divergent branch cost more)
+                const V3 wa = vadd(x, qrot(q, R.aA[a]));
+                const V3 dr = vsub(wa, R.aB[a]);
+                const float kd = 0.8f * P.inv_h;
+                const V3 r = vsel(act, vsub(wa, xc), v3(0.0f, 0.0f, 0.0f));
+                const float e1 = act ? fminf(fmaxf(-G.d1(dr) * kd, -P.max_depen), P.max_depen) : 0.0f;
+                const float e2 = act ? fminf(fmaxf(-G.d2(dr) * kd, -P.max_depen), P.max_depen) : 0.0f;
                 an[a].r = r;
                 an[a].I1 = G.iw1(Iw, r);
                 an[a].I2 = G.iw2(Iw, r);
@@ -970,15 +978,16 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
     }
 }
 
-// __launch_bounds__(64, 3): at most 168 VGPRs, so three waves share a SIMD in
-// large launches (the Gauss-Seidel chains are latency-bound: more resident
-// waves, not more lanes, fill the SIMD); free of scratch at that budget. The
-// packed-pair variant of one-round launches spills 24 B/lane at 168 VGPRs; a
-// two-wave budget (171 VGPRs, no scratch) measured slower on the same box
-// (4096 envs: min 9.96 vs 9.20 us, tools/kbench.py A/B, r03), so it keeps three.
-// The general ground basis needs more registers: two waves.
+// Wide launches: __launch_bounds__(64, 3), at most 168 VGPRs, so three waves
+// share a SIMD (the Gauss-Seidel chains are latency-bound: more resident waves,
+// not more lanes, fill the SIMD); free of scratch at that budget. One-round
+// launches (the packed solver, the shape record in registers): two waves, 175
+// VGPRs and no scratch — at three waves the shape record spilled 36 B/lane
+// (4096 envs: 13.2 us against 13.5 with the record in LDS and 13.5 at either
+// budget, same-box A/B, profiles/r05_ab_rigid_shape_regs.jsonl). The general
+// ground basis needs more registers: two waves.
 #ifndef MG_RIGID1_ROUND_WAVES
-#define MG_RIGID1_ROUND_WAVES 3
+#define MG_RIGID1_ROUND_WAVES 2
 #endif
 #ifndef MG_RIGID1_WIDE_WAVES
 #define MG_RIGID1_WIDE_WAVES 3
