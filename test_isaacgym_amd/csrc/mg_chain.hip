@@ -286,16 +286,27 @@ __device__ __forceinline__ void store_row(float* dst, const float (&v)[N]) {
 // (AA.uni, migym_capi.cpp; fixed after upload); UDOF: and its DOF properties
 // (wave-uniform scalar loads instead of per-lane loads and per-lane inertia
 // set-up: no VGPRs for them). s_rows / s_root: the kernel's LDS row staging.
-template <int NL, bool EXT, bool UNI, bool UDOF>
+template <int NL, bool EXT, bool UNI, bool UDOF, bool AFF>
 __device__ __forceinline__ void chain_body(const MgStep& P, const MgArticArgs& AA, float* s_rows, float* s_root) {
     constexpr int D = NL - 1;
     const int a = blockIdx.x * 64 + threadIdx.x;
     const bool live = a < AA.na;
-    // the row is loaded here (a launch of several rounds hides the latency; the
-    // computed form's second path cost registers and scratch): chain_row is the
-    // quad kernel's
-    const int* ai = AA.artic_i + (size_t)(live ? a : 0) * MG_ARTIC_I_N;
-    const int b0 = ai[0], d0 = ai[1], ls = ai[3];   // link l: body b0 + l * ls (migym_capi.cpp)
+    // link l: body b0 + l * ls (migym_capi.cpp); AFF (a launch-time choice, so
+    // only one form is compiled into each kernel): computed from the blocked
+    // layout, and the fused refresh's rows too — no dependent index load at
+    // either end of the frame
+    int b0, d0, ls;
+    if constexpr (AFF) {
+        const int ai = live ? a : 0, blk = ai >> 6;
+        b0 = AA.ab0 + blk * 64 * NL + (ai & 63);
+        ls = min(64, AA.na - blk * 64);
+        d0 = AA.ad0 + ai * AA.ads;
+    } else {
+        const int* ai = AA.artic_i + (size_t)(live ? a : 0) * MG_ARTIC_I_N;
+        b0 = ai[0];
+        d0 = ai[1];
+        ls = ai[3];
+    }
     const int nb = AA.nb, nd = AA.nd;
     float* St = AA.state;
     const float* pr = AA.dof_props;
@@ -499,10 +510,16 @@ __device__ __forceinline__ void chain_body(const MgStep& P, const MgArticArgs& A
     constexpr int RW = NL * MG_STATE_N;            // floats of one articulation's rows
     bool wave_tr = false, root_tr = false;
     if (AA.out_rb) {
-        const int g0 = fld(AA.out_body, 0, 0, b0);
-        contiguous = true;
+        int g0;
+        if constexpr (AFF) {
+            g0 = AA.og0 + a * NL;
+            contiguous = true;
+        } else {
+            g0 = fld(AA.out_body, 0, 0, b0);
+            contiguous = true;
 #pragma unroll
-        for (int l = 1; l < NL; ++l) contiguous = contiguous && fld(AA.out_body, 0, 0, b0 + l * ls) == g0 + l;
+            for (int l = 1; l < NL; ++l) contiguous = contiguous && fld(AA.out_body, 0, 0, b0 + l * ls) == g0 + l;
+        }
         orb = AA.out_rb + (size_t)g0 * MG_STATE_N;
         // wave-uniform: every lane live, and a launch wider than the SIMDs can hold
         // in one round (a latency-bound launch pays the LDS round trip: 4096
@@ -569,7 +586,7 @@ __device__ __forceinline__ void chain_body(const MgStep& P, const MgArticArgs& A
                 }
             }
             if (l == 0 && AA.out_root) {
-                const int rr = fld(AA.out_root_row, 0, 0, b0);
+                const int rr = AFF ? AA.or0 + a : fld(AA.out_root_row, 0, 0, b0);
                 // the wave's base rows one contiguous block as well: through LDS
                 const int rr0 = __builtin_amdgcn_readfirstlane(rr);
                 root_tr = wave_tr && __all(rr >= 0 && rr == rr0 + (int)threadIdx.x) &&
@@ -587,7 +604,8 @@ __device__ __forceinline__ void chain_body(const MgStep& P, const MgArticArgs& A
     }
     if (wave_tr) {   // wave-uniform
         __syncthreads();
-        float* wb = AA.out_rb + (size_t)__builtin_amdgcn_readfirstlane(fld(AA.out_body, 0, 0, b0)) * MG_STATE_N;
+        float* wb = AA.out_rb + (size_t)__builtin_amdgcn_readfirstlane(AFF ? AA.og0 + a * NL
+                                                                           : fld(AA.out_body, 0, 0, b0)) * MG_STATE_N;
         constexpr int N4 = 16 * RW;                 // float4s of the wave's block (64 * RW / 4)
 #pragma unroll
         for (int j = 0; j < (N4 + 63) / 64; ++j) {
@@ -596,7 +614,8 @@ __device__ __forceinline__ void chain_body(const MgStep& P, const MgArticArgs& A
                 *reinterpret_cast<float4*>(wb + 4 * f4) = *reinterpret_cast<const float4*>(s_rows + 4 * f4);
         }
         if (root_tr) {   // wave-uniform
-            float* wr = AA.out_root + (size_t)__builtin_amdgcn_readfirstlane(fld(AA.out_root_row, 0, 0, b0)) *
+            float* wr = AA.out_root + (size_t)__builtin_amdgcn_readfirstlane(AFF ? AA.or0 + a
+                                                                                 : fld(AA.out_root_row, 0, 0, b0)) *
                                           MG_STATE_N;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {   // 64 x 13 floats = 208 float4s
@@ -981,15 +1000,15 @@ __global__ void __launch_bounds__(64, 2) k_artic_chain_q(MgStep P, MgArticArgs A
 // while every instance shared them keeps stepping correctly after a
 // set_actor_dof_properties makes one differ, as the per-lane
 // path reads d_dof_props in place.
-template <int NL, bool EXT, bool UNI>
+template <int NL, bool EXT, bool UNI, bool AFF>
 __global__ void __launch_bounds__(64, MG_CHAIN_WAVES) k_artic_chain(MgStep P, MgArticArgs AA) {
     __shared__ __align__(16) float s_rows[64 * NL * MG_STATE_N];
     __shared__ __align__(16) float s_root[64 * MG_STATE_N];
     if constexpr (UNI) {
-        if (AA.uni[MG_CHAIN_UNI_DOFOK] != 0.0f) chain_body<NL, EXT, true, true>(P, AA, s_rows, s_root);
-        else chain_body<NL, EXT, true, false>(P, AA, s_rows, s_root);
+        if (AA.uni[MG_CHAIN_UNI_DOFOK] != 0.0f) chain_body<NL, EXT, true, true, AFF>(P, AA, s_rows, s_root);
+        else chain_body<NL, EXT, true, false, AFF>(P, AA, s_rows, s_root);
     } else {
-        chain_body<NL, EXT, false, false>(P, AA, s_rows, s_root);
+        chain_body<NL, EXT, false, false, false>(P, AA, s_rows, s_root);
     }
 }
 
@@ -1021,16 +1040,21 @@ hipError_t mg_launch_artic_chain(const MgStep& P, const MgArticArgs& A, hipStrea
 #undef MG_KQ
         return hipGetLastError();
     }
-#define MG_KC(NL)                                                                                 \
-    do {                                                                                          \
-        if (A.ext) {                                                                              \
-            if (A.uni) MG_LAUNCH((k_artic_chain<NL, true, true>), dim3(cb), dim3(64), 0, s, P, A);  \
-            else MG_LAUNCH((k_artic_chain<NL, true, false>), dim3(cb), dim3(64), 0, s, P, A);       \
-        } else {                                                                                  \
-            if (A.uni) MG_LAUNCH((k_artic_chain<NL, false, true>), dim3(cb), dim3(64), 0, s, P, A); \
-            else MG_LAUNCH((k_artic_chain<NL, false, false>), dim3(cb), dim3(64), 0, s, P, A);      \
-        }                                                                                         \
+#define MG_KC(NL)                                                                                       \
+    do {                                                                                                \
+        if (A.ext) {                                                                                    \
+            if (A.uni && aff) MG_LAUNCH((k_artic_chain<NL, true, true, true>), dim3(cb), dim3(64), 0, s, P, A);   \
+            else if (A.uni) MG_LAUNCH((k_artic_chain<NL, true, true, false>), dim3(cb), dim3(64), 0, s, P, A);    \
+            else MG_LAUNCH((k_artic_chain<NL, true, false, false>), dim3(cb), dim3(64), 0, s, P, A);              \
+        } else {                                                                                        \
+            if (A.uni && aff) MG_LAUNCH((k_artic_chain<NL, false, true, true>), dim3(cb), dim3(64), 0, s, P, A);  \
+            else if (A.uni) MG_LAUNCH((k_artic_chain<NL, false, true, false>), dim3(cb), dim3(64), 0, s, P, A);   \
+            else MG_LAUNCH((k_artic_chain<NL, false, false, false>), dim3(cb), dim3(64), 0, s, P, A);             \
+        }                                                                                               \
     } while (0)
+    // the computed-row form when the upload found the rows affine (and the
+    // fused refresh's rows too, when it writes them)
+    const bool aff = MG_CHAIN_AFF && A.aff && ((A.out_rb == nullptr && A.out_root == nullptr) || A.out_aff);
     if (A.nl == 2) MG_KC(2);
     else if (A.nl == 3) MG_KC(3);
     else MG_KC(4);

@@ -86,6 +86,9 @@ struct MgArticArgs {
     // chain layout): first body ab0 + (a / 64) * 64 * nbl + a % 64, link stride
     // min(64, na - 64 (a / 64)), first DOF ad0 + a * ads
     int          aff, ab0, ad0, ads;
+    // out_aff: instance a's fused-refresh rows too — link l's rigid-body row og0
+    // + a nl + l, its actor-root row or0 + a (k_artic_chain<..., AFF>)
+    int          out_aff, og0, or0;
     int          tmpl;        // template id handled by this launch
     int          nl, ndof;    // links / dofs of the template
     int          nbl;         // bodies of the template (nl minus virtual links; Jacobian rows)

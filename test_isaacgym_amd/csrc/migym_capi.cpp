@@ -69,8 +69,11 @@ struct ArticGroup {
     int nbody;                     // bodies per instance (nl minus the virtual links of ball joints)
     int offset, count;             // into the template-sorted instance list (all instances)
     int step_offset, step_count;   // into the list stepped by k_artic_chain / k_artic_lanes (uncoupled envs)
-    // the stepped instances' rows are affine in the instance (MgArticArgs::aff)
+    // the stepped instances' rows are affine in the instance (MgArticArgs::aff),
+    // and so are their fused-refresh rows (out_aff: rigid-body row og0 + a nl +
+    // l, actor row or0 + a)
     int aff = 0, aff_b0 = 0, aff_d0 = 0, aff_ds = 0;
+    int out_aff = 0, out_g0 = 0, out_r0 = 0;
 };
 
 // coupled envs (mg_env.hip) of one articulation template (tmpl -1: none)
@@ -1030,6 +1033,20 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         HIP_TRY(h2d(s->d_slot_global, order.data(), (size_t)nb * sizeof(int)));
         HIP_TRY(dalloc(&s->d_slot_actor, (size_t)std::max(nb, 1)));
         HIP_TRY(h2d(s->d_slot_actor, slot_actor.data(), (size_t)nb * sizeof(int)));
+        // chain groups whose fused-refresh rows are affine in the instance
+        for (ArticGroup& g : s->groups) {
+            g.out_aff = 0;
+            if (!g.aff) continue;
+            const int* r0 = artic_step.data() + (size_t)g.step_offset * MG_ARTIC_I_N;
+            const int G0 = order[r0[0]], A0 = slot_actor[r0[0]];
+            bool ok = A0 >= 0;
+            for (int k = 0; k < g.step_count && ok; ++k) {
+                const int* r = r0 + (size_t)k * MG_ARTIC_I_N;
+                ok = slot_actor[r[0]] == A0 + k;
+                for (int l = 0; l < g.nl && ok; ++l) ok = order[r[0] + l * r[3]] == G0 + k * g.nl + l;
+            }
+            if (ok) { g.out_aff = 1; g.out_g0 = G0; g.out_r0 = A0; }
+        }
         long long covered = s->nf1 == s->nf_rigid && s->nf_rigid == s->nf ? s->nf1 : -1;
         for (const ArticGroup& g : s->groups) {
             if (covered < 0) break;
@@ -1147,6 +1164,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.na = g.step_count; A.nb = s->nb; A.nd = s->nd;
         A.artic_i = s->d_artic_step + (size_t)g.step_offset * MG_ARTIC_I_N;
         A.aff = g.aff; A.ab0 = g.aff_b0; A.ad0 = g.aff_d0; A.ads = g.aff_ds;
+        A.out_aff = g.out_aff; A.og0 = g.out_g0; A.or0 = g.out_r0;
         A.tmpl = g.tmpl; A.nl = g.nl; A.ndof = g.ndof; A.fixed_base = g.fixed_base; A.chain = g.chain; A.nbl = g.nbody;
         A.link_f = s->d_link_f + (size_t)g.first_link * MG_LINK_F_N;
         A.link_i = s->d_link_i + (size_t)g.first_link * MG_LINK_I_N;
