@@ -959,10 +959,12 @@ __device__ __forceinline__ void chain_body_q(const MgStep& P, const MgArticArgs&
     CUSE(r[0]); CUSE(r[12]);
     CSTAMP(4);   // output rows formed
     const int b = b0 + qd * ls;
-    // (the fused refresh's row indices loaded with the inputs instead measured
-    // the same: 9.88 vs 9.89 us at 4096 gimbals)
-    const int out_b = AA.out_rb ? fld(AA.out_body, 0, 0, b) : 0;
-    const int out_r = AA.out_root ? fld(AA.out_root_row, 0, 0, b0) : -1;
+    // the fused refresh's rows: computed when the upload found them affine
+    // (loading the indices with the inputs instead measured the same as at the
+    // end: 9.88 vs 9.89 us at 4096 gimbals)
+    const bool oaff = MG_CHAIN_AFF && AA.aff && AA.out_aff;
+    const int out_b = AA.out_rb ? (oaff ? AA.og0 + a * NL + qd : fld(AA.out_body, 0, 0, b)) : 0;
+    const int out_r = AA.out_root ? (oaff ? AA.or0 + a : fld(AA.out_root_row, 0, 0, b0)) : -1;
 #pragma unroll
     for (int k = 0; k < MG_STATE_N; ++k) fld(St, k, nb, b) = r[k];
     if (AA.out_rb) {
