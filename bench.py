@@ -150,6 +150,12 @@ def kernel_stats(sim, n_launches, run):
     used = N.lib.mg_step_time_stats(sim.native, min(n_launches, 256), ctypes.byref(avg), ctypes.byref(lo), None)
     if used <= 0:
         return None, None, 0
+    # a simulate with more launches than the library's timer slots would sum
+    # only the first kKern kernels: refuse the number, loudly
+    missed = N.lib.mg_step_untimed_launches(sim.native, int(used))
+    if missed != 0:
+        raise RuntimeError("kernel timing: %d launch(es) per simulate ran untimed (mg_step_untimed_launches); "
+                           "the summed kernel time would undercount" % missed)
     return avg.value, lo.value, int(used)
 
 

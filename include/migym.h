@@ -376,13 +376,28 @@ float       mg_last_step_ms(mg_sim* sim);
  * start / stop events, the interval rocprofv3 reports for the kernel). Returns
  * the count used, or < 0. */
 int32_t     mg_step_time_stats(mg_sim* sim, int32_t n, float* avg_ms, float* min_ms, float* max_ms);
-/* Diagnostics: copy n floats of the coupled step's per-env contact tables (what
- * the narrow-phase launch k_env_np handed to k_env_step in the last substep
- * run) from float offset `off` to host memory `dst`; synchronises the device.
- * A group's envs are consecutive records of 8 + 24 MAXCT floats (MAXCT 16, 48
- * for 64-lane envs) starting at the group's first coupled row x
- * mg_env_ctab_floats(). */
-int32_t     mg_debug_copy_ctab(mg_sim* sim, int64_t off, int32_t n, float* dst);
+/* Replaces no reference interface (diagnostics of this build): how many kernel
+ * launches the most launch-heavy of the last n timed simulate() calls (at most
+ * 256) made past the timer's slots — launches run untimed, whose durations
+ * mg_step_time_stats' sums leave out (0: every kernel was timed). Or < 0. */
+int32_t     mg_step_untimed_launches(mg_sim* sim, int32_t n);
+/* Diagnostics: coupled env k's contact table (k = the k-th coupled env in env
+ * order; in the Franka scene every env is coupled, so k is the env index) as
+ * the narrow-phase launch k_env_np handed it to k_env_step in the last substep
+ * run: 8 header floats ([0] contacts, [1] anchors, ints by bit pattern), MAXCT
+ * contact records of 10 floats (participant a, b as int bits, point, normal,
+ * separation, restitution), MAXCT anchor records of 14 floats, MAXCT 16 in a
+ * 16-lane group and 48 in a 64-lane group. Copies into dst (cap floats at
+ * least the record) and returns the record's length in floats, 8 + 24 MAXCT;
+ * synchronises the device. < 0 on error. */
+int32_t     mg_debug_copy_env_ctab(mg_sim* sim, int32_t k, float* dst, int32_t cap);
+/* Diagnostics: per articulation group (up to cap / MG_DEBUG_GROUP_N groups)
+ * the facts that pick its kernel form (mg_chain.hip): links, instances stepped
+ * alone, serial chain, shared link masses (UNI), shared DOF properties, rows
+ * affine in the instance (AFF), fused-refresh rows affine, refresh fusion
+ * possible for the sim. Returns the number of groups, < 0 on error. */
+#define MG_DEBUG_GROUP_N 8
+int32_t     mg_debug_artic_groups(mg_sim* sim, int32_t* out, int32_t cap);
 int         mg_env_ctab_floats(void);
 int         mg_env_carry_floats(void);
 /* Number of bodies advanced by the free-body kernel / articulations by the

@@ -594,10 +594,20 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                  * its diagonal anchors exerts no yaw torque; the two saturate at
                  * mu N together) */
                 share = R.cnt == 2 ? 0.5f : 1.0f;
+                /* sweep order (round 6): a position sweep solves the anchors'
+                 * rows, then the normal rows, so the velocity it integrates is the
+                 * one non-penetration had the last word on; only the first one
+                 * opens with the normal rows (the anchors' budget needs a normal
+                 * impulse). A velocity sweep is normal, anchor, normal rows. With
+                 * the normal rows first in every position sweep (rounds 3-5) the
+                 * anchors' rows left a rotation about the line through the two
+                 * anchors in the integrated velocity: a vehicle pushed at 0.9
+                 * mu m g across that line crept at ~13 mm/s, held by anchors that
+                 * never clamped (tests/test_ground_patch_kat.py, yawed pushes). */
                 for (it = 0; it < P->npos + P->nvel; ++it) {
                     const int pos = it < P->npos, last = it == P->npos + P->nvel - 1;
                     float psum;
-                    for (j = 0; j < 4; ++j) {
+                    for (j = 0; j < 4 && (it == 0 || !pos); ++j) {
                         const float sj = b_ps(&B, sl[j].s0, dx, dth, sl[j].r);
                         contact_normal(&B, &sl[j], &v, &w, invm, &Iw,
                                        pos ? pos_target_(P, sj) : vel_target_(P, sj, sl[j].e, sl[j].vn0));
@@ -626,9 +636,9 @@ static void rigid_body_step(const step_t* P, const mg_model* m, int b, float* st
                             }
                         }
                     }
-                    /* the last position sweep and the velocity sweeps end with the
-                     * normal rows again (as the coupled step, §3.6.1) */
-                    if (it >= P->npos - 1) {
+                    /* every sweep ends with the normal rows (same targets: dx, dth
+                     * are unchanged within a sweep) */
+                    {
                         for (j = 0; j < 4; ++j) {
                             const float sj = b_ps(&B, sl[j].s0, dx, dth, sl[j].r);
                             contact_normal(&B, &sl[j], &v, &w, invm, &Iw,

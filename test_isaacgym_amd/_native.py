@@ -25,6 +25,7 @@ MG_DOFPROP_N = 12
 MG_LINK_F_N = 16
 MG_LINK_I_N = 4
 MG_ARTIC_I_N = 4
+MG_DEBUG_GROUP_N = 8       # include/migym.h mg_debug_artic_groups
 MG_ATMPL_I_N = 4
 MG_ACOLL_N = 4
 
@@ -140,7 +141,9 @@ def _load():
         "mg_num_free_bodies": (i32, [vp]),
         "mg_num_articulations": (i32, [vp]),
         "mg_num_coupled_envs": (i32, [vp]),
-        "mg_debug_copy_ctab": (i32, [vp, ctypes.c_int64, i32, vp]),
+        "mg_debug_copy_env_ctab": (i32, [vp, i32, vp, i32]),
+        "mg_debug_artic_groups": (i32, [vp, vp, i32]),
+        "mg_step_untimed_launches": (i32, [vp, i32]),
         "mg_env_ctab_floats": (i32, []),
         "mg_env_carry_floats": (i32, []),
         "mg_set_render_bodies": (i32, [vp, vp, vp, vp]),
@@ -171,7 +174,7 @@ EXPORTED_SYMBOLS = (
     "mg_num_articulations",
     "mg_num_coupled_envs", "mg_refresh_jacobian_mass_matrix",
     "mg_set_render_bodies", "mg_snapshot_render_state", "mg_render_cameras", "mg_last_render_ms",
-    "mg_debug_copy_ctab", "mg_env_ctab_floats", "mg_env_carry_floats",
+    "mg_debug_copy_env_ctab", "mg_debug_artic_groups", "mg_step_untimed_launches", "mg_env_ctab_floats", "mg_env_carry_floats",
 )
 
 

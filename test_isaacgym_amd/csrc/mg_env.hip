@@ -2502,3 +2502,4 @@ hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s
 // need (migym_capi.cpp allocates them per coupled env at the widest group's size)
 extern "C" int mg_env_carry_floats(void) { return carry_n<64>(); }
 extern "C" int mg_env_ctab_floats(void) { return ct_n<MG_ENV_MAXCT_WIDE>(); }
+int mg_env_ctab_record_floats(int wide) { return wide ? ct_n<MG_ENV_MAXCT_WIDE>() : ct_n<MG_ENV_MAXCT>(); }

@@ -250,6 +250,7 @@ struct MgKernelTimer {
     hipEvent_t* start;
     hipEvent_t* stop;
     int cap, used;
+    int missed;   // launches past `cap`, run untimed (mg_step_untimed_launches)
 };
 extern thread_local MgKernelTimer* mg_timer;
 #define MG_LAUNCH(kernel, grid, block, shmem, stream, ...)                                               \
@@ -260,6 +261,7 @@ extern thread_local MgKernelTimer* mg_timer;
                                   t_->stop[t_->used], 0, __VA_ARGS__);                                  \
             t_->used++;                                                                                 \
         } else {                                                                                        \
+            if (t_) t_->missed++;                                                                       \
             hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                        \
         }                                                                                               \
     } while (0)
@@ -269,6 +271,7 @@ hipError_t mg_launch_render(const MgRenderArgs& A, int nblocks, hipStream_t s);
 hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s);
 extern "C" int mg_env_carry_floats(void);   // per-env record sizes of the coupled step (mg_env.hip)
 extern "C" int mg_env_ctab_floats(void);
+int mg_env_ctab_record_floats(int wide);   // one env's contact table in a 16- / 64-lane group
 hipError_t mg_launch_rigid_step(const MgStep& P, const MgRigidArgs& A, hipStream_t s);
 hipError_t mg_launch_artic_step(const MgStep& P, const MgArticArgs& A, hipStream_t s);
 hipError_t mg_launch_artic_lanes(const MgStep& P, const MgArticArgs& A, hipStream_t s);

@@ -7,9 +7,11 @@
 //   2. contact generation against the ground plane (box corners, sphere and
 //      capsule end caps within contact_offset), at most MG_MAX_CONTACTS slots;
 //   3. TGS: npos position iterations of length h/npos, each a Gauss-Seidel pass
-//      over the normal rows (speculative / depenetration target) then over the
+//      over the normal rows (speculative / depenetration target) and the
 //      friction rows (Coulomb pyramid, PhysX-style), followed by integrating the
-//      body's motion delta; then nvel velocity iterations with the bias removed;
+//      body's motion delta; then nvel velocity iterations with the bias removed
+//      (single-shape bodies: the patch's anchor rows then the normal rows, the
+//      first and the velocity sweeps opening with the normal rows too);
 //   4. pose update: com += sum of iteration deltas, q = exp(dtheta) q.
 // Envs are independent and (test10_servo_vecenv.py:317,323: group=i, filter=-1)
 // the two actors of an env do not collide, so lanes never communicate: no
@@ -689,17 +691,20 @@ __device__ __forceinline__ void tgs_zp(const MgStep& P, NRow (&sl)[4], ARow (&an
     };
     const f2 nsub = bc2(-P.inv_sub), psub = bc2(P.sub);
     const int nit = P.npos + P.nvel;
+    // sweep order (round 6, as the oracle): a position sweep is the anchors'
+    // rows then the normal rows (non-penetration has the last word before the
+    // velocity is integrated); only the first opens with the normal rows
     for (int it = 0; it < P.npos; ++it) {
         const f2 t0 = sep(0) * nsub, t1 = sep(1) * nsub;   // -s / sub of each slot
         const float tg[4] = {fminf(t0.x, P.max_depen), fminf(t0.y, P.max_depen), fminf(t1.x, P.max_depen),
                              fminf(t1.y, P.max_depen)};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) normal(j, tg[j]);
-        anchors(true, it == nit - 1);
-        if (it == P.npos - 1) {   // the closing normal pass (same targets: dx, dth unchanged)
+        if (it == 0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) normal(j, tg[j]);
         }
+        anchors(true, it == nit - 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) normal(j, tg[j]);   // same targets: dx, dth unchanged
         DV = pfma(V, psub, DV);
         DW = pfma(W, psub, DW);
         DZ = pfma(Z, psub, DZ);
@@ -902,7 +907,10 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
                         row_normal1(G, sl[j], v, w, invm, pos ? pos_target(P, sj) : vel_target(P, sj, e, sl[j].vn0));
                     }
                 };
-                normals();
+                // sweep order (round 6, oracle rigid_body_step): a position
+                // sweep is the anchors' rows then the normal rows; the first
+                // and the velocity sweeps open with the normal rows as well
+                if (it == 0 || !pos) normals();
                 // the patch's normal impulse (slot order)
                 const float mun = mu * (((sl[0].ln + sl[1].ln) + sl[2].ln) + sl[3].ln);
 #pragma unroll
@@ -930,9 +938,7 @@ __device__ __forceinline__ void rigid_body1(const B& G, const MgStep& P, const f
                         w = fmad3(w, an[a].I2, dl);
                     }
                 }
-                // the last position sweep and the velocity sweeps end with the
-                // normal rows again (the coupled step's order)
-                if (it >= P.npos - 1) normals();
+                normals();   // every sweep ends with the normal rows
                 if (pos) {
                     dx = fmad3(dx, v, P.sub);
                     dth = fmad3(dth, w, P.sub);

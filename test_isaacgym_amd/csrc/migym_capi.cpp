@@ -79,6 +79,7 @@ struct ArticGroup {
 // coupled envs (mg_env.hip) of one articulation template (tmpl -1: none)
 struct EnvGroup {
     int tmpl, first_link, nl, ndof, floating;
+    int wide;            // 64 lanes per env (mg_env.hip k_env_step<32, 64>), else 16
     int max_free;        // most free bodies of one env of the group (velocity slots)
     int offset, count;   // rows of d_env
 };
@@ -204,7 +205,12 @@ struct mg_sim {
     hipEvent_t ring_b[kRing] = {}, ring_e[kRing] = {};
     hipEvent_t kern_b[kRing][kKern] = {}, kern_e[kRing][kKern] = {};
     int kern_n[kRing] = {};
+    int kern_miss[kRing] = {};    // launches of that simulate past kKern (untimed)
     long long ring_n = 0;
+    // coupled env k (env order) -> its row of d_env and the float offset /
+    // length of its contact-table record (mg_debug_copy_env_ctab)
+    std::vector<long long> cenv_ctab_off;
+    std::vector<int> cenv_ctab_n;
 };
 
 namespace {
@@ -872,12 +878,15 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     // coupled env rows: internal slots, grouped by articulation template (-1 first)
     std::vector<int> env_flat;
     s->env_groups.clear();
+    s->cenv_ctab_off.assign(env_rows.size(), -1);
+    s->cenv_ctab_n.assign(env_rows.size(), 0);
     // (and by lane width: an env of more than 16 links or velocity slots runs
     // 64 lanes wide, mg_env.hip; the oracle decides per env the same way)
     for (int t = -1; t < m->num_artic_tmpls; ++t)
     for (int wide = 0; wide < 2; ++wide) {
         EnvGroup g{};
         g.tmpl = t;
+        g.wide = wide;
         if (t >= 0) {
             g.first_link = m->artic_tmpl_i[t * MG_ATMPL_I_N + 0];
             g.nl = m->artic_tmpl_i[t * MG_ATMPL_I_N + 1];
@@ -895,6 +904,10 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
             for (int i = 0; i < row[2]; ++i) row[3 + i] = perm[row[3 + i]];
             for (int i = 0; i < row[7]; ++i) row[8 + i] = perm[row[8 + i]];
             env_flat.insert(env_flat.end(), row.begin(), row.end());
+            // k_env_np writes env j of the group at the group's base + j records
+            s->cenv_ctab_off[r] = (long long)g.offset * mg_env_ctab_floats() +
+                                  (long long)g.count * mg_env_ctab_record_floats(wide);
+            s->cenv_ctab_n[r] = mg_env_ctab_record_floats(wide);
             g.count++;
         }
         if (g.count > 0) s->env_groups.push_back(g);
@@ -1258,6 +1271,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         if (timed) {
             HIP_TRY(hipEventRecord(s->ev_end, st));
             s->kern_n[slot] = timer.used;
+            s->kern_miss[slot] = timer.missed;
             s->ring_n++;
         }
         s->timed_step = timed;
@@ -1352,18 +1366,45 @@ int32_t mg_step_time_stats(mg_sim* s, int32_t n, float* avg_ms, float* min_ms, f
     return n;
 }
 
-// diagnostics (tools/diag_franka_env.py): n floats of the coupled step's
-// contact tables (k_env_np's output of the last substep run) from float offset
-// `off` (a group's envs are consecutive records of 8 + 24 MAXCT floats from
-// its offset x mg_env_ctab_floats(); MAXCT 16, or 48 in 64-lane groups)
-int32_t mg_debug_copy_ctab(mg_sim* s, int64_t off, int32_t n, float* dst) {
-    if (!s || !s->uploaded || !s->d_env_ctab || off < 0 || n < 0 || !dst) return fail(MG_ERR_ARG, "bad arguments");
-    const int64_t total = (int64_t)std::max(s->n_coupled, 1) * mg_env_ctab_floats();
-    if (off + n > total) return fail(MG_ERR_ARG, "range beyond the contact tables");
+int32_t mg_step_untimed_launches(mg_sim* s, int32_t n) {
+    if (!s || n <= 0) return fail(MG_ERR_ARG, "bad arguments");
+    if (s->ring_n == 0) return fail(MG_ERR_STATE, "no simulate() recorded");
+    const long long avail = s->ring_n < mg_sim::kRing ? s->ring_n : mg_sim::kRing;
+    if (n > avail) n = (int32_t)avail;
+    int32_t most = 0;
+    for (int32_t k = 0; k < n; ++k) {
+        const int slot = (int)((s->ring_n - 1 - k) % mg_sim::kRing);
+        most = std::max(most, s->kern_miss[slot]);
+    }
+    return most;
+}
+
+// diagnostics (tests/test_franka_gpu.py, tools/diag_franka_env.py): coupled
+// env k's contact table (k_env_np's output of the last substep run): the
+// group's base and record size are the library's, so callers hard-code neither
+int32_t mg_debug_copy_env_ctab(mg_sim* s, int32_t k, float* dst, int32_t cap) {
+    if (!s || !s->uploaded || !s->d_env_ctab || !dst) return fail(MG_ERR_ARG, "bad arguments");
+    if (k < 0 || k >= (int32_t)s->cenv_ctab_off.size()) return fail(MG_ERR_ARG, "no such coupled env");
+    const int32_t n = s->cenv_ctab_n[k];
+    if (cap < n) return fail(MG_ERR_ARG, "dst holds fewer floats than the env's contact table");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(dst, s->d_env_ctab + off, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
-    return MG_OK;
+    HIP_TRY(hipMemcpy(dst, s->d_env_ctab + s->cenv_ctab_off[k], (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+    return n;
+}
+
+// diagnostics (tests/test_step_out_chain_gpu.py): per articulation group the
+// facts that choose its chain-kernel form (mg_chain.hip mg_launch_artic_chain)
+int32_t mg_debug_artic_groups(mg_sim* s, int32_t* out, int32_t cap) {
+    if (!s || !s->uploaded || (!out && cap > 0)) return fail(MG_ERR_ARG, "bad arguments");
+    const int32_t n = (int32_t)s->groups.size();
+    for (int32_t i = 0; i < n && (i + 1) * MG_DEBUG_GROUP_N <= cap; ++i) {
+        const ArticGroup& g = s->groups[i];
+        int32_t* r = out + (size_t)i * MG_DEBUG_GROUP_N;
+        r[0] = g.nl; r[1] = g.step_count; r[2] = g.chain; r[3] = g.uni_mass ? 1 : 0;
+        r[4] = g.uni_dof ? 1 : 0; r[5] = g.aff; r[6] = g.out_aff; r[7] = s->step_out_ok ? 1 : 0;
+    }
+    return n;
 }
 
 int32_t mg_num_free_bodies(mg_sim* s) { return s ? s->nf : 0; }

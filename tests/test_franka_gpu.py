@@ -139,7 +139,7 @@ def test_franka_pick_lifts_cubes(gym, n):
     # overlaps the table's (top at 0.4 m, half extents 0.3 / 0.5 m, cube half
     # size 0.0225 m) must not rest below the top. A cube at rest below the top
     # beside the table must be carried by the robot: the contacts the narrow
-    # phase handed to the step (mg_debug_copy_ctab) include one between the
+    # phase handed to the step (mg_debug_copy_env_ctab) include one between the
     # cube and a link of the arm. The one such cube at 4096 envs (env 3043,
     # tools/diag_franka_env.py, profiles/r05_diag_franka.jsonl) was knocked off
     # the table's edge and rests on the forearm (links 4 and 5), pressed
@@ -171,15 +171,18 @@ def test_franka_pick_lifts_cubes(gym, n):
 def _env_contacts(sim, e):
     """Env e's contacts of the last substep as k_env_np handed them to the step
     (participants a, b: link l, free body 64 + k, static 80 + s, ground -1;
-    separation): mg_debug_copy_ctab on the 16-lane group's records."""
+    separation): mg_debug_copy_env_ctab (every env of the scene is coupled, so
+    env e is coupled env e; the library sizes the record)."""
     import ctypes
     from test_isaacgym_amd import _native as N
-    ct_n = 8 + 16 * 24
-    buf = (ctypes.c_float * ct_n)()
-    N.check(N.lib.mg_debug_copy_ctab(sim.native, e * ct_n, ct_n, buf), "mg_debug_copy_ctab")
-    a = np.frombuffer(buf, np.float32)
+    cap = N.lib.mg_env_ctab_floats()
+    buf = (ctypes.c_float * cap)()
+    n = N.lib.mg_debug_copy_env_ctab(sim.native, e, buf, cap)
+    N.check(n if n < 0 else 0, "mg_debug_copy_env_ctab")
+    maxct = (n - 8) // 24
+    a = np.frombuffer(buf, np.float32)[:n]
     ib = a.view(np.int32)
-    return [(int(ib[8 + 10 * c]), int(ib[9 + 10 * c]), float(a[16 + 10 * c])) for c in range(min(int(ib[0]), 16))]
+    return [(int(ib[8 + 10 * c]), int(ib[9 + 10 * c]), float(a[16 + 10 * c])) for c in range(min(int(ib[0]), maxct))]
 
 
 def test_franka_jacobian_mass_matrix_float64(gym):

@@ -69,13 +69,20 @@ def test_free_fall_semi_implicit_euler(gym):
 
 def test_resting_box_contact_force(gym):
     """A 1 m box (1000 kg) dropped flat from 0.1 m settles on its face:
-    z = 0.5 +- 1e-3, |v| < 1e-3, net contact force = m g within 0.1 %."""
+    z = 0.5 +- 1e-3, the pose static (< 1 um over the last 100 frames), net
+    contact force = m g within 0.1 %. The state's velocity is the last
+    velocity sweep's Gauss-Seidel residual: |v|, |w| < 2e-3
+    (1.07e-3 with round 6's sweep order, 2e-4 with round 5's, whose position
+    sweeps let a pushed body creep: tests/test_ground_patch_kat.py)."""
     sim = _sim(gym)
     p, m, st = _one(gym, sim, gym.create_box(sim, 1, 1, 1, gymapi.AssetOptions()),
                     gymapi.Transform(gymapi.Vec3(0, 0, 0.6)))
-    cf = _run(p, m, st, 240)
+    _run(p, m, st, 140)
+    pose = st[0, :7].copy()
+    cf = _run(p, m, st, 100)
     assert abs(st[0, 2] - 0.5) < 1e-3
-    assert np.all(np.abs(st[0, 7:13]) < 1e-3)
+    assert np.all(np.abs(st[0, :7] - pose) < 1e-6), st[0, :7] - pose
+    assert np.all(np.abs(st[0, 7:13]) < 2e-3)
     np.testing.assert_allclose(cf[0], [0, 0, 1000 * 9.8], rtol=1e-3, atol=1.0)
 
 

@@ -355,3 +355,110 @@ def test_gimbal_wide_launch_rows_through_lds(gym):
     assert torch.equal(rba[roots], ra)
     for sim, _ in sims:
         gym.destroy_sim(sim)
+
+
+def _gimbal_box_scene(gym, n, box_every, heavy_every=0):
+    """gimbal_scene's gimbals (fixed base at (0, 2, 3), POS drives kp 50, kd 5)
+    with a free 0.2 m box created after the gimbal in every `box_every`-th env
+    (filter 1 against the gimbal's 1: no contacts, so the box steps alone on the
+    ground in k_rigid_step1). The boxes' rows interleave the gimbals' rows in
+    the rigid-body and root tensors, so the fused refresh's rows are not affine
+    in the instance (out_aff 0); every `heavy_every`-th env's gimbal links get
+    1.5x their mass (the link mass rows then differ: UNI 0)."""
+    sp = gymapi.SimParams()
+    sp.substeps = 2
+    sp.dt = 1.0 / 60.0
+    sp.up_axis = gymapi.UP_AXIS_Z
+    sp.gravity = gymapi.Vec3(0.0, 0.0, -9.8)
+    sp.physx.solver_type = 1
+    sp.physx.num_position_iterations = 4
+    sp.physx.num_velocity_iterations = 1
+    sp.use_gpu_pipeline = True
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim, plane)
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    opts.default_dof_drive_mode = gymapi.DOF_MODE_POS
+    gimbal = gym.load_asset(sim, scenes.ASSET_ROOT, "servo/gimbal.urdf", opts)
+    box = gym.create_box(sim, 0.2, 0.2, 0.2, gymapi.AssetOptions())
+    per_row = int(math.sqrt(n))
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-1, -1, -1), gymapi.Vec3(1, 1, 1), per_row)
+        h = gym.create_actor(env, gimbal, gymapi.Transform(gymapi.Vec3(0.0, 2.0, 3.0)), "gimbal", i, 1)
+        props = gym.get_actor_dof_properties(env, h)
+        props["driveMode"][:] = gymapi.DOF_MODE_POS
+        props["stiffness"][:] = 50.0
+        props["damping"][:] = 5.0
+        gym.set_actor_dof_properties(env, h, props)
+        if heavy_every and i % heavy_every == 0:
+            bp = gym.get_actor_rigid_body_properties(env, h)
+            for b in bp:
+                b.mass = b.mass * 1.5
+            gym.set_actor_rigid_body_properties(env, h, bp, True)
+        if i % box_every == 0:
+            gym.create_actor(env, box, gymapi.Transform(gymapi.Vec3(0.5, 0.0, 0.3)), "box", i, 1)
+    return sim
+
+
+def _artic_groups(sim):
+    import ctypes
+    buf = (ctypes.c_int32 * (8 * N.MG_DEBUG_GROUP_N))()
+    ng = N.lib.mg_debug_artic_groups(sim.native, buf, len(buf))
+    assert ng >= 0, N.last_error()
+    a = np.frombuffer(buf, np.int32).reshape(-1, N.MG_DEBUG_GROUP_N)[:ng]
+    keys = ("nl", "step_count", "chain", "uni_mass", "uni_dof", "aff", "out_aff", "step_out_ok")
+    return [dict(zip(keys, map(int, r))) for r in a]
+
+
+@pytest.mark.parametrize("heavy_every", [0, 7], ids=["uni", "nonuni"])
+def test_gimbal_nonaffine_one_lane_forms(gym, heavy_every):
+    """the one-lane chain kernel's forms without computed
+    rows (k_artic_chain<4, 0, UNI, AFF = 0>) on the GPU. 65,536 + 64 x 5 + 23
+    gimbals (a launch wider than one resident round, so full contiguous waves
+    take the LDS row path; the last wave partly filled) interleaved with free
+    boxes in every 997th env (waves that straddle a box store their rows lane
+    by lane). `uni`: fused (STEP_FUSION_ALL) -> <4,0,1,0> (out_aff 0), unfused
+    -> <4,0,1,1>; `nonuni` (every 7th gimbal 1.5x heavier): <4,0,0,0> both
+    ways. Fused and unfused DOF, rigid-body and root tensors agree bit for bit,
+    and both equal oracle.step (gimbals and boxes)."""
+    n, steps = 65536 + 64 * 5 + 23, 2
+    tg = scenes.gimbal_targets(n, steps, DEV, seed=29)
+    sims = []
+    for fusion in (gymapi.STEP_FUSION_ALL, 0):
+        sim = _gimbal_box_scene(gym, n, 997, heavy_every)
+        gym.prepare_sim(sim)
+        gym.set_step_fusion(sim, fusion)
+        sims.append((sim, _tensors(gym, sim)))
+    (sa, (ra, rba, da)), (sb, (rb_, rbb, db)) = sims
+    grp = [g for g in _artic_groups(sa) if g["step_count"] > 0]
+    assert len(grp) == 1, grp
+    g = grp[0]
+    assert (g["nl"], g["step_count"], g["chain"]) == (4, n, 1), g
+    assert g["uni_mass"] == (0 if heavy_every else 1), g
+    assert g["aff"] == 1 and g["out_aff"] == 0 and g["step_out_ok"] == 1, g
+    assert N.lib.mg_step_out_supported(sa.native) == 1
+    p, m = sa.mg_params(), sa.mg_model()
+    st = sa.model_arrays["body_state0"].copy()
+    ds = sa.model_arrays["dof_state0"].copy()
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+    tg_h = tg.cpu().numpy()
+    for k in range(steps):
+        for sim, _ in sims:
+            gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tg[k]))
+            gym.simulate(sim)
+            gym.refresh_dof_state_tensor(sim)
+            gym.refresh_rigid_body_state_tensor(sim)
+            gym.refresh_actor_root_state_tensor(sim)
+        tgt[:, 0] = tg_h[k]
+        oracle.step(p, m, st, ds, tgt=tgt)
+        torch.cuda.synchronize()
+        assert torch.equal(da, db) and torch.equal(rba, rbb) and torch.equal(ra, rb_), "step %d: fused != unfused" % k
+    assert np.abs(ds[:, 1]).max() > 0.05
+    assert np.array_equal(da.cpu().numpy(), ds), "max |diff| %g" % np.abs(da.cpu().numpy() - ds).max()
+    assert np.array_equal(rba.cpu().numpy(), st), "max |diff| %g" % np.abs(rba.cpu().numpy() - st).max()
+    roots = torch.as_tensor(sa.model_arrays["actor_root_body"], device=DEV, dtype=torch.long)
+    assert torch.equal(rba[roots], ra)
+    for sim, _ in sims:
+        gym.destroy_sim(sim)

@@ -6,7 +6,7 @@ below the table top beside it. A second, identical run (the step is
 deterministic) then logs the selected envs frame by frame around their worst
 frame: DOF positions against their limits, the penetration depth, the net
 contact forces of cube / hand / fingers, and the contacts k_env_np handed to
-the step (mg_debug_copy_ctab: participants, separation, normal).
+the step (mg_debug_copy_env_ctab: participants, separation, normal).
 Usage: python tools/diag_franka_env.py [n] [frames] [env ...]"""
 import ctypes
 import json
@@ -24,7 +24,6 @@ from test_isaacgym_amd import _native as N  # noqa: E402
 from test_franka_gpu import _setup, _control  # noqa: E402
 import franka_geom as FG  # noqa: E402
 
-CT_N = 8 + 16 * 24           # the 16-lane group's contact-table record (mg_env.hip ct_n<16>)
 NAMES = {64: "cube", 80: "table", -1: "ground"}
 
 
@@ -37,11 +36,13 @@ def who(p):
 
 
 def contacts(sim, e):
-    buf = (ctypes.c_float * CT_N)()
-    N.check(N.lib.mg_debug_copy_ctab(sim.native, e * CT_N, CT_N, buf), "mg_debug_copy_ctab")
-    a = np.frombuffer(buf, np.float32)
+    cap = N.lib.mg_env_ctab_floats()
+    buf = (ctypes.c_float * cap)()
+    n = N.lib.mg_debug_copy_env_ctab(sim.native, e, buf, cap)   # every env of the scene is coupled
+    N.check(n if n < 0 else 0, "mg_debug_copy_env_ctab")
+    a = np.frombuffer(buf, np.float32)[:n]
     ib = a.view(np.int32)
-    nct = min(int(ib[0]), 16)
+    nct = min(int(ib[0]), (n - 8) // 24)
     out = []
     for c in range(nct):
         r = 8 + c * 10
