@@ -498,8 +498,12 @@ def franka_rate(n, steps, warmup, dev, use_graph=True):
            "roofline": {"bound": "hbm", "kernel": "k_env_np + k_env_step (one frame)", "achieved": ach,
                         "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": (ach / HBM_PEAK_GBS) if ach else None,
-                        "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None, "traffic_source": pmc_file,
-                        "algorithmic_bytes_per_launch": S3_BYTES_PER_ENV * n,
+                        # per frame (the summed launches the roofline prices); older summaries kept
+                        # the per-frame value under hbm_bytes_per_launch
+                        "traffic": (pmc.get("hbm_bytes_per_frame", pmc.get("hbm_bytes_per_launch"))
+                                    if pmc else None), "traffic_unit": "bytes per frame", "traffic_source": pmc_file,
+                        "traffic_read_factor_borrowed": pmc.get("read_factor_borrowed", True) if pmc else None,
+                        "algorithmic_bytes_per_frame": S3_BYTES_PER_ENV * n,
                         "algorithmic_bytes_per_env": S3_BYTES_PER_ENV,
                         "note": "SURVEY.md §8d S3: 5,844 B per env-step (rigid-body refresh, DOF state, targets and "
                                 "efforts, Jacobian, mass matrix, DOF / body constants, contact warm-start state) "

@@ -63,10 +63,14 @@ def frame_kernels(f, nf, w, envs, out, kernels, per_frame, bpe, factor_from):
         parts[k] = {"fetch_kib_raw": f[key], "write_kib_raw": w[wk], "launches": nf[key],
                     "hbm_bytes_per_launch": f[key] * 1024.0 * factor + w[wk] * 1024.0}
     total = per_frame * sum(p["hbm_bytes_per_launch"] for p in parts.values())
+    # per FRAME, under its own key: bench.py prices the S3 roofline on
+    # the frame's summed kernels, so its `traffic` is this value
     res = {"envs": envs, "kernel": " + ".join(kernels), "launches_per_frame_each": per_frame, "per_kernel": parts,
-           "read_factor_calibrated": factor, "calibration": "from %s (%s)" % (factor_from, cal["calibration"]),
-           "hbm_bytes_per_launch": total, "hbm_bytes_note": "per frame (all the frame's coupled-step launches)",
-           "algorithmic_bytes_per_launch": bpe * envs}
+           "read_factor_calibrated": factor, "read_factor_borrowed": True,
+           "calibration": "borrowed from %s (%s): no kernel of known read volume runs in the S3 benchmark, so the "
+                          "FETCH_SIZE factor of the same GPU session's S1 calibration kernel (dword SoA loads) "
+                          "is applied" % (factor_from, cal["calibration"]),
+           "hbm_bytes_per_frame": total, "algorithmic_bytes_per_frame": bpe * envs}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -92,6 +92,13 @@ constexpr int carry_link0() { return MG_CARRY_HDR + MG_CARRY_LANE * G; }
 // substep's start (forward kinematics of its integrated q, the same operations
 // the next launches would run) in the carry record, so the next substep's
 // k_env_np and k_env_step read them instead of each running the kinematic scan
+// MG_ENV_SWEEP_ANF (experiment): a position sweep solves the anchors' rows then
+// the normal rows (only the first opens with the normal rows), the free-body
+// kernel's order since round 6 (mg_rigid.hip); 0: normal, anchor rows, the
+// last position sweep and the velocity sweeps closing with the normal rows
+#ifndef MG_ENV_SWEEP_ANF
+#define MG_ENV_SWEEP_ANF 0
+#endif
 #ifndef MG_ENV_FK_CARRY
 #define MG_ENV_FK_CARRY 1
 #endif
@@ -2005,7 +2012,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
                     }
                 }
             };
-            normal_pass();
+            if (!MG_ENV_SWEEP_ANF || it == 0 || !pos) normal_pass();
             // each patch's normal impulse: running sums in contact order,
             // restarting at the contact that opens a patch
             {
@@ -2050,7 +2057,7 @@ __global__ void __launch_bounds__(64) k_env_step(MgStep P, MgEnvArgs A) {
             // rows again: a friction bound the size of a grip cannot drag a body
             // into a unilateral contact that eight Gauss-Seidel sweeps would not
             // converge
-            if (it >= P.npos - 1) normal_pass();
+            if (it >= P.npos - 1 || MG_ENV_SWEEP_ANF) normal_pass();
             if (pos) dp = dp + uv * P.sub;
         }
         if (ln == 0) {

@@ -128,7 +128,8 @@ def test_franka_pick_lifts_cubes(gym, n):
     stats = {"n": n, "worst_mm": round(1e3 * float(worst.max()), 2), "worst_env": int(worst.argmax()),
              "envs_past_1mm": int((worst > off).sum()), "envs_past_5mm": int((worst > 0.005).sum()),
              "longest_run_past_1mm": int(worst_run[0].max()), "longest_run_past_5mm": int(worst_run[1].max()),
-             "last_frame_worst_mm": round(1e3 * float(d.max()), 2)}
+             "last_frame_worst_mm": round(1e3 * float(d.max()), 2),
+             "lifted_frac": round(float((maxz > 0.55).float().mean()), 4)}
     print("hull-in-table:", stats)
     assert stats["worst_mm"] < 30.0, stats
     assert stats["longest_run_past_5mm"] <= 3, stats

@@ -50,7 +50,7 @@ def contacts(sim, e):
     return int(ib[0]), int(ib[1]), out
 
 
-def run(n, frames, watch=(), around=None):
+def run(n, frames, watch=(), around=None, around_run=False):
     gym = gymapi.acquire_gym()
     sim, info, rb, dof, jac, mm, ctl = _setup(gym, n)
     ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))
@@ -63,17 +63,26 @@ def run(n, frames, watch=(), around=None):
     worst = torch.zeros(n, dtype=torch.float64, device="cuda:0")
     worst_f = torch.zeros(n, dtype=torch.int64, device="cuda:0")
     log = {e: [] for e in watch}
+    run_1mm = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+    best_run = torch.zeros_like(run_1mm)
+    best_run_end = torch.zeros_like(run_1mm)
+    acts = {e: [] for e in watch}   # the controller's targets / efforts (tools/replay_franka_env.py)
     for f in range(frames):
         gym.simulate(sim)
         gym.fetch_results(sim, True)
-        _control(gym, sim, info, rb, dof, jac, mm, ctl, n)
+        pa, ea = _control(gym, sim, info, rb, dof, jac, mm, ctl, n)
         gym.refresh_net_contact_force_tensor(sim)
         d = FG.penetration_depth(A, rb, hulls, bi - 1)
         upd = d > worst
         worst = torch.where(upd, d, worst)
         worst_f = torch.where(upd, torch.full_like(worst_f, f), worst_f)
+        run_1mm = torch.where(d > 0.001, run_1mm + 1, torch.zeros_like(run_1mm))
+        longer = run_1mm > best_run
+        best_run = torch.where(longer, run_1mm, best_run)
+        best_run_end = torch.where(longer, torch.full_like(best_run_end, f), best_run_end)
         for e in watch:
-            if around is not None and abs(f - around[e]) > 12:
+            acts[e].append(np.stack([pa.view(n, 9)[e].cpu().numpy(), ea.view(n, 9)[e].cpu().numpy()]))
+            if around is not None and abs(f - around[e]) > 12 and not (around_run and float(d[e]) > 0.0005):
                 continue
             q = dof[:, 0].view(n, 9)[e]
             nct, nanc, cl = contacts(sim, e)
@@ -91,6 +100,8 @@ def run(n, frames, watch=(), around=None):
     overlap = (rel[:, 0].abs() < 0.3225) & (rel[:, 1].abs() < 0.5225)
     loose = ((z > 0.3) & (z < 0.4175) & still & ~overlap).nonzero().flatten().tolist()
     gym.destroy_sim(sim)
+    run.runs = (best_run.cpu().numpy(), best_run_end.cpu().numpy())
+    run.acts = {e: np.stack(a) for e, a in acts.items()}
     return worst.cpu().numpy(), worst_f.cpu().numpy(), loose, log
 
 
@@ -105,10 +116,16 @@ def main():
                "depth_mm_quantiles": {q: round(1e3 * float(np.quantile(worst, q)), 3) for q in (0.5, 0.9, 0.99, 1.0)},
                "deepest": [(int(e), round(1e3 * float(worst[e]), 2), int(wf[e])) for e in order[:8]],
                "loose_cubes": loose}
+    runs, run_end = run.runs
+    by_run = np.argsort(-runs)
+    summary["longest_runs_past_1mm"] = [(int(e), int(runs[e]), int(run_end[e])) for e in by_run[:8]]
     print(json.dumps(summary), flush=True)
-    watch = [int(x) for x in sys.argv[3:]] or (loose[:3] + [int(order[0])])
+    watch = [int(x) for x in sys.argv[3:]] or (loose[:3] + [int(order[0]), int(by_run[0])])
     around = {e: (int(wf[e]) if e not in loose else frames - 6) for e in watch}
-    _, _, _, log = run(n, frames, watch, around)
+    _, _, _, log = run(n, frames, watch, around, around_run=True)
+    out = os.environ.get("DIAG_ACTIONS")
+    if out:   # the watched envs' per-frame actions, for a CPU replay on the oracle
+        np.savez_compressed(out, envs=np.array(watch), acts=np.stack([run.acts[e] for e in watch]))
     for e in watch:
         print(json.dumps({"env": e, "worst_depth_mm": round(1e3 * float(worst[e]), 3), "worst_frame": int(wf[e]),
                           "log": log[e]}), flush=True)
