@@ -19,11 +19,13 @@ semantics of an attached camera (world frame, the attachment dropped).
 Tolerances: leg tips and bounding box within TIP_TOL px (1 px is ~5 mm at the
 ant's distance); the simulated feet's end-sphere centres within FOOT_TOL m of
 the triangulated ones. Measured: our ant twists — all four hips
-turn ~11 degrees and the torso yaws between frames 100 and 140 — a slowly
-growing mode of the symmetric rest pose that Isaac Gym's images do not show
-(CPU PhysX puts a resting articulation to sleep after 0.4 s; this build has
-no sleeping); the twist moves the tips by up to 4 px, which TIP_TOL admits,
-and the state before it matches within 3 px.
+turn ~11 degrees and the torso yaws between frames 100 and 140 — a growing mode
+of the symmetric rest pose that Isaac Gym's images do not show; the twist moves
+the tips by up to 4 px, which TIP_TOL admits, and is bounded as its own number
+(HIP_TWIST_TOL). Round 6's ablations on the oracle: the rest
+pose with point feet and ankles at their limits is an unstable equilibrium
+(the torso drops 3.5 mm as it twists), the friction anchors' drift closing
+sets the growth rate, and no variant tried brings every image within 2 px.
 The CPU test runs the C restatement (physics + renderer); the GPU test runs
 the device path, bit for bit against the restatement, and the same checks.
 """
@@ -46,6 +48,10 @@ from make_dr_fixture import features  # noqa: E402  (the fixture's own feature e
 TIP_TOL = 4          # px
 BBOX_TOL = 4         # px
 FOOT_TOL = 0.012     # m
+# the twist this build shows and Isaac Gym's images do not, as a
+# number of its own: the four hips settle at 11.1-11.6 degrees by
+# frame 150 and stay; a change that lets the mode grow further fails here
+HIP_TWIST_TOL = 12.5  # deg
 FEET = {2: (0.4, 0.4, 0.0), 4: (-0.4, 0.4, 0.0), 6: (-0.4, -0.4, 0.0), 8: (0.4, -0.4, 0.0)}  # foot capsule ends
 
 
@@ -134,6 +140,7 @@ def test_oracle_ant_rest_matches_isaac_gym_dr_images(gym):
     # ankles at their limits, the torso off the ground on its feet
     assert np.allclose(np.abs(np.degrees(ds[1::2, 0])), 30.0, atol=0.05)
     assert 0.35 < st[0, 1] < 0.38
+    assert np.abs(np.degrees(ds[0::2, 0])).max() <= HIP_TWIST_TOL, np.degrees(ds[0::2, 0])
     print("worst tip / bbox error px:", worst)
 
 
@@ -173,3 +180,4 @@ def test_gpu_ant_rest_matches_isaac_gym_dr_images(gym):
             _check_image(key, fx["images"][key], seg)
     d = np.abs(_foot_centres(st) - np.array(fx["foot_centres"]))
     assert d[:, [0, 2]].max() <= FOOT_TOL, d
+    assert np.abs(np.degrees(ds[0::2, 0])).max() <= HIP_TWIST_TOL, np.degrees(ds[0::2, 0])

@@ -91,9 +91,13 @@ def test_franka_pick_parity_bitexact(gym):
 @pytest.mark.parametrize("n", [256, 4096])
 def test_franka_pick_lifts_cubes(gym, n):
     """Config 3 (examples/franka_cube_ik_osc.py --num_envs 4096) at 256 and at
-    the full 4096 envs, 600 frames (10 s) of the script's loop: most cubes are
-    grasped and lifted above 0.55 m (the script drops them at 0.6 m, :405),
-    state stays finite, no cube sinks into the table or the ground."""
+    the full 4096 envs, 600 frames (10 s) of the script's loop: at least 88 % of
+    the cubes are grasped and lifted above 0.55 m (the script drops them at
+    0.6 m, :405; measured round 6: 93.8 % at 256 envs, 91.6 % at 4096,
+    profiles/r06_franka_stats.log), state stays finite, no cube sinks into the
+    table or the ground, and hand / finger hulls do not stay inside the table.
+    Parity unpinned: no reference output shows a grasp or a hull's depth in the
+    table; these bounds pin this build's behaviour."""
     frames = 600
     sim, info, rb, dof, jac, mm, ctl = _setup(gym, n)
     maxz = torch.zeros(n, device=DEV)
@@ -122,20 +126,31 @@ def test_franka_pick_lifts_cubes(gym, n):
     # the table by up to a substep's travel before its first contact exists (no
     # speculative contacts; tools/diag_franka_env.py: 160 of 4096 envs pass 1 mm
     # in some frame, the deepest 17.6 mm, a hand driven down at a cube on the
-    # floor), and a hand the controller presses onto the table top (up to
-    # ~4 kN) rests a little inside it (the position sweeps' residual); the
-    # contact rows keep both shallow and short.
+    # floor; 31 pass 5 mm, each for at most 2 frames). One arm in 4096 (env 2581,
+    # profiles/r06_diag_franka.jsonl) wedges below the table top at a corner —
+    # the hand against the -y face, finger A the -x face, finger B pressed down
+    # on the top at ~480 N by the OSC torques — and that finger rests 1.32 mm in
+    # for the remaining 390 frames. Measured cause (round 6 A/B, DESIGN.md
+    # §3.6.1): the sweep order, normal rows then the anchors' rows, with only the
+    # last position sweep closing on the normal rows: the velocity integrated in
+    # the earlier sweeps is the one the friction rows left, under a steady load
+    # a fixed overlap. Closing every sweep on the normal rows ends every run past
+    # 1 mm within 2 frames, but the fingers' normal rows then undo the grip's
+    # friction (15 % of the cubes lifted), so the order stays and the bound is
+    # on how many envs hold such an overlap.
     stats = {"n": n, "worst_mm": round(1e3 * float(worst.max()), 2), "worst_env": int(worst.argmax()),
              "envs_past_1mm": int((worst > off).sum()), "envs_past_5mm": int((worst > 0.005).sum()),
              "longest_run_past_1mm": int(worst_run[0].max()), "longest_run_past_5mm": int(worst_run[1].max()),
              "last_frame_worst_mm": round(1e3 * float(d.max()), 2),
              "lifted_frac": round(float((maxz > 0.55).float().mean()), 4)}
     print("hull-in-table:", stats)
-    assert stats["worst_mm"] < 30.0, stats
-    assert stats["longest_run_past_5mm"] <= 3, stats
-    assert stats["last_frame_worst_mm"] <= 5.0, stats
+    stats["envs_run_past_1mm_over_40"] = int((worst_run[0] > 40).sum())
+    assert stats["worst_mm"] < 20.0, stats                          # measured 17.63 (4096), 6.97 (256)
+    assert stats["longest_run_past_5mm"] <= 3, stats                # measured 2 / 1
+    assert stats["last_frame_worst_mm"] <= 5.0, stats               # measured 3.56 / 0.69
+    assert stats["envs_run_past_1mm_over_40"] <= max(n // 1000, 1), stats   # the wedged arm above
     frac = float((maxz > 0.55).float().mean())
-    assert frac >= 0.5, "only %.2f of the cubes were lifted" % frac
+    assert frac >= 0.88, "only %.4f of the cubes were lifted" % frac
     # nothing sinks through the table or the ground. A cube whose footprint
     # overlaps the table's (top at 0.4 m, half extents 0.3 / 0.5 m, cube half
     # size 0.0225 m) must not rest below the top. A cube at rest below the top
