@@ -44,6 +44,15 @@ MESH_PROXIES = {
 SPHERE, BOX, CAPSULE, CONVEX = 0, 1, 2, 3
 MJCF_MAX_JOINT_VELOCITY = 100.0      # PhysX's default articulation joint speed limit (rad/s, m/s)
 HULL_MAX_VERTS, HULL_MAX_FACES = 32, 64          # MG_HULL_MAX_VERTS / _FACES (include/migym.h)
+# Per-mesh caps for measurements with a library built with larger MG_HULL_MAX_*
+# (the Franka hand at 64 vertices and at its full 102):
+# MIGYM_HULL_CAPS="hand.obj=64/128,finger.obj=128/256" (mesh file name =
+# vertices / faces). Unset: every mesh at the defaults above.
+HULL_CAPS = {}
+for _item in filter(None, os.environ.get("MIGYM_HULL_CAPS", "").split(",")):
+    _name, _caps = _item.split("=")
+    _v, _f = _caps.split("/")
+    HULL_CAPS[_name.strip()] = (int(_v), int(_f))
 
 
 def _quat_from_rpy(r, p, y):
@@ -140,7 +149,7 @@ def _farthest_points(pts, k):
     return pts[sorted(idx)]
 
 
-def make_hull(verts, max_verts=HULL_MAX_VERTS):
+def make_hull(verts, max_verts=HULL_MAX_VERTS, max_faces=None):
     """Convex hull of a vertex cloud, at most max_verts vertices; coplanar
     triangles merged into one face plane. Mass properties by tetrahedra from
     the vertex centroid."""
@@ -161,7 +170,7 @@ def make_hull(verts, max_verts=HULL_MAX_VERTS):
             if not match:
                 planes.append(np.array([n[0], n[1], n[2], d]))
             tri_plane.append(match[0] if match else len(planes) - 1)
-        if len(planes) <= HULL_MAX_FACES or nv <= 8:
+        if len(planes) <= (HULL_MAX_FACES if max_faces is None else max_faces) or nv <= 8:
             break
         nv -= 2
     o = hv.mean(0)
@@ -570,11 +579,12 @@ _HULL_CACHE = {}
 def mesh_shape(verts, p, q, source):
     """A collision mesh (vertices in the geometry frame p, q) as a convex-hull
     shape whose origin is the hull's box centre; None for a degenerate mesh."""
-    key = (np.asarray(verts, dtype=np.float64).tobytes(),)
+    caps = HULL_CAPS.get(os.path.basename(str(source).split(":")[-1]), (HULL_MAX_VERTS, None))
+    key = (np.asarray(verts, dtype=np.float64).tobytes(), caps)
     hull = _HULL_CACHE.get(key)
     if hull is None:
         try:
-            hull = make_hull(verts)
+            hull = make_hull(verts, caps[0], caps[1])
         except Exception:                 # flat / degenerate cloud (scipy QhullError)
             return None
         c = 0.5 * (hull.verts.min(0) + hull.verts.max(0))

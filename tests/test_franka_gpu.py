@@ -9,6 +9,8 @@ expressions in the same order, no FMA contraction on either side).
 Physics: the pick loop lifts cubes (the script's whole point), and the
 Jacobian / mass matrix match float64 textbook kinematics (tests/kinematics64.py).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -23,8 +25,14 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
+# MIGYM_FRANKA_ASSET (measurements only): another proxy,
+# e.g. franka_hand64/franka_proxy.urdf with MIGYM_HULL_CAPS and a library built
+# with larger MG_HULL_MAX_*; unset, the in-tree asset
+FRANKA_ASSET = os.environ.get("MIGYM_FRANKA_ASSET", "franka/franka_proxy.urdf")
+
+
 def _setup(gym, n, seed=42):
-    sim, info = scenes.franka_scene(gym, n, use_gpu_pipeline=True, seed=seed)
+    sim, info = scenes.franka_scene(gym, n, use_gpu_pipeline=True, seed=seed, asset_file=FRANKA_ASSET)
     gym.prepare_sim(sim)
     rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
     dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))

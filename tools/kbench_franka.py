@@ -21,7 +21,7 @@ from test_isaacgym_amd import _native as N, franka_control, scenes  # noqa: E402
 
 def run(n, warm=150, steps=100):
     gym = gymapi.acquire_gym()
-    sim, info = scenes.franka_scene(gym, n)
+    sim, info = scenes.franka_scene(gym, n, asset_file=os.environ.get("MIGYM_FRANKA_ASSET", "franka/franka_proxy.urdf"))
     gym.prepare_sim(sim)
     N.lib.mg_set_kernel_timing(sim.native, 1)
     rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
