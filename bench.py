@@ -180,7 +180,7 @@ def fuse_in_capture(sim):
 def load_pmc(name):
     """Committed rocprofv3 PMC summary (profiles/<round>_pmc_<name>.json, newest
     round first, written by profiles/collect_pmc.py): (dict, file) or (None, None)."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", "%s_pmc_%s.json" % (rnd, name))
         if os.path.exists(path):
             with open(path) as f:
