@@ -416,6 +416,38 @@ int32_t     mg_num_articulations(mg_sim* sim);
  * and every env holding a floating-base articulation). */
 int32_t     mg_num_coupled_envs(mg_sim* sim);
 
+/* ---- the S3 cube-pick controller on the device (csrc/mg_ctrl.hip) ----
+ * Replaces the per-frame torch controller of examples/franka_cube_ik_osc.py
+ * :348-410 (its grasp state machine, control_osc :59-79 / control_ik :51-56
+ * and the gripper targets :403-407) for n envs, one launch, reading the sim's
+ * own tensors in place: rigid-body rows (13 floats), DOF state rows (pos, vel),
+ * the end-effector Jacobian block and the 7x7 mass-matrix block of each env at
+ * element strides (a view such as jacobian[:, hand - 1, :, :7] needs no copy).
+ * Writes the (n, 9) rows the script hands to set_dof_position_target_tensor /
+ * set_dof_actuation_force_tensor: OSC sets effort[:, :7] and pos[:, 7:9], IK
+ * pos[:, :9]; other entries are left as they are (the script's zeros). */
+typedef struct mg_cube_pick_args {
+    int32_t        n;              /* envs */
+    int32_t        osc;            /* 1: operational-space control, 0: damped least-squares IK */
+    const float*   rb;             /* rigid-body state rows (num_bodies, 13) */
+    const int32_t* box_row;        /* (n) rows of the cubes */
+    const int32_t* hand_row;       /* (n) rows of the hands */
+    const float*   dof;            /* DOF state rows (num_dofs, 2) */
+    const int32_t* dof_row0;       /* (n) first of the env's 9 DOF rows */
+    const float*   jac;            /* env e's 6 x 7 block: jac[e jac_se + r jac_sr + c jac_sc] */
+    int64_t        jac_se, jac_sr, jac_sc;
+    const float*   mm;             /* env e's 7 x 7 block, likewise */
+    int64_t        mm_se, mm_sr, mm_sc;
+    const float*   init_pos;       /* (n, 3) the hands' start positions (:252-253) */
+    const float*   init_rot;       /* (n, 4) and orientations */
+    const float*   default_dof_pos;/* (9) null-space target (:187-191) */
+    uint8_t*       hand_restart;   /* (n) the script's hand_restart flags (kept across frames) */
+    float*         pos_action;     /* (n, 9) */
+    float*         effort_action;  /* (n, 9) */
+    float          kp, kd, kp_null, kd_null, damping, grasp_offset, box_size;
+} mg_cube_pick_args;
+int32_t     mg_cube_pick_step(const mg_cube_pick_args* args, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -150,6 +150,7 @@ def _load():
         "mg_snapshot_render_state": (i32, [vp, vp]),
         "mg_render_cameras": (i32, [vp, vp, i32, vp]),
         "mg_last_render_ms": (ctypes.c_float, [vp]),
+        "mg_cube_pick_step": (i32, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -174,7 +175,7 @@ EXPORTED_SYMBOLS = (
     "mg_num_articulations",
     "mg_num_coupled_envs", "mg_refresh_jacobian_mass_matrix",
     "mg_set_render_bodies", "mg_snapshot_render_state", "mg_render_cameras", "mg_last_render_ms",
-    "mg_debug_copy_env_ctab", "mg_debug_artic_groups", "mg_step_untimed_launches", "mg_env_ctab_floats", "mg_env_carry_floats",
+    "mg_debug_copy_env_ctab", "mg_debug_artic_groups", "mg_step_untimed_launches", "mg_cube_pick_step", "mg_env_ctab_floats", "mg_env_carry_floats",
 )
 
 

@@ -370,20 +370,24 @@ __device__ __forceinline__ void coop_edges(const CShape& X, const CShape& Y, flo
         }
     }
 }
-// X's vertices (i = ln + 16 k, at most 2 per lane) against Y's planes, into the
-// lane's queue (order idbase + i); both vertices loaded before either is tested
+// X's vertices (i = ln + G k, at most MG_HULL_MAX_VERTS / G per lane: 2 at the
+// default 32-vertex cap on 16 lanes) against Y's planes, into the lane's queue
+// (order idbase + i); all the lane's vertices loaded before any is tested.
+// (Round 6: the bound was a literal 2, so a build with a larger vertex cap
+// skipped the vertices past 32 G / 16 while the oracle tested them.)
 template <int G>
 __device__ __forceinline__ void coop_vertices(const CShape& X, const CShape& Y, float margin, bool onY, int idbase,
                                               int ln, CandQ& Q, V3& lo, V3& hi) {
+    constexpr int CV_PER_LANE = (MG_HULL_MAX_VERTS + G - 1) / G;
     const int nv = cvx_nv(X);
-    V3 vw[2];
+    V3 vw[CV_PER_LANE];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < CV_PER_LANE; ++k) {
         const int i = ln + G * k;
         vw[k] = cvx_vertex(X, i < nv ? i : nv - 1);
     }
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < CV_PER_LANE; ++k) {
         const int i = ln + G * k;
         if (i < nv) {
             const V3 v = vw[k];

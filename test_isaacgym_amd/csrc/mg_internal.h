@@ -268,6 +268,7 @@ extern thread_local MgKernelTimer* mg_timer;
 
 // launchers (defined in the .hip files)
 hipError_t mg_launch_render(const MgRenderArgs& A, int nblocks, hipStream_t s);
+hipError_t mg_launch_cube_pick(const mg_cube_pick_args& A, hipStream_t s);
 hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s);
 extern "C" int mg_env_carry_floats(void);   // per-env record sizes of the coupled step (mg_env.hip)
 extern "C" int mg_env_ctab_floats(void);

@@ -1407,6 +1407,20 @@ int32_t mg_debug_artic_groups(mg_sim* s, int32_t* out, int32_t cap) {
     return n;
 }
 
+// the S3 cube-pick controller (csrc/mg_ctrl.hip): independent of any sim, on
+// the caller's stream (torch's current stream: ordered with the refreshes that
+// filled its inputs and the sets that read its outputs)
+int32_t mg_cube_pick_step(const mg_cube_pick_args* a, void* stream) {
+    if (!a || a->n < 0) return fail(MG_ERR_ARG, "bad arguments");
+    if (a->n == 0) return MG_OK;
+    if (!a->rb || !a->box_row || !a->hand_row || !a->dof || !a->dof_row0 || !a->jac || (a->osc && !a->mm) ||
+        !a->init_pos || !a->init_rot || !a->default_dof_pos || !a->hand_restart || !a->pos_action ||
+        !a->effort_action)
+        return fail(MG_ERR_ARG, "null tensor");
+    HIP_TRY(mg_launch_cube_pick(*a, (hipStream_t)stream));
+    return MG_OK;
+}
+
 int32_t mg_num_free_bodies(mg_sim* s) { return s ? s->nf : 0; }
 int32_t mg_num_articulations(mg_sim* s) { return s ? s->nartic : 0; }
 int32_t mg_num_coupled_envs(mg_sim* s) { return s ? s->n_coupled : 0; }

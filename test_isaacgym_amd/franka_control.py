@@ -4,16 +4,40 @@ The reference script computes, every frame, from the refreshed rigid-body,
 DOF, Jacobian and mass-matrix tensors (:336-346): the grasp state machine
 (:348-401), an operational-space (OSC, :59-79) or damped-least-squares IK
 (:51-56) arm command, and gripper targets (:403-407). This module restates that
-loop as batched torch ops on the sim device so the S3 bench and the parity tests
-drive the engine exactly as the script does, without the viewer. The math
-follows the cited lines; names follow the script.
+loop so the S3 bench and the parity tests drive the engine exactly as the
+script does, without the viewer. The math follows the cited lines; names
+follow the script.
+
+Two implementations behind one step(): on a HIP device, one kernel launch
+(csrc/mg_ctrl.hip through mg_cube_pick_step: one lane per env, the inverses as
+Cholesky solves in registers; round 6), and the batched torch ops the kernel
+replaced (`fused=False`, and on the CPU), ~150 launches per frame. The two
+agree to float32 rounding (tests/test_franka_ctrl_gpu.py).
 """
+import ctypes
 import math
 
 import numpy as np
 import torch
 
 from .torch_utils import quat_conjugate, quat_mul
+
+
+class _CubePickArgs(ctypes.Structure):
+    """include/migym.h mg_cube_pick_args."""
+    _fields_ = [("n", ctypes.c_int32), ("osc", ctypes.c_int32),
+                ("rb", ctypes.c_void_p), ("box_row", ctypes.c_void_p), ("hand_row", ctypes.c_void_p),
+                ("dof", ctypes.c_void_p), ("dof_row0", ctypes.c_void_p),
+                ("jac", ctypes.c_void_p), ("jac_se", ctypes.c_int64), ("jac_sr", ctypes.c_int64),
+                ("jac_sc", ctypes.c_int64),
+                ("mm", ctypes.c_void_p), ("mm_se", ctypes.c_int64), ("mm_sr", ctypes.c_int64),
+                ("mm_sc", ctypes.c_int64),
+                ("init_pos", ctypes.c_void_p), ("init_rot", ctypes.c_void_p), ("default_dof_pos", ctypes.c_void_p),
+                ("hand_restart", ctypes.c_void_p), ("pos_action", ctypes.c_void_p),
+                ("effort_action", ctypes.c_void_p),
+                ("kp", ctypes.c_float), ("kd", ctypes.c_float), ("kp_null", ctypes.c_float),
+                ("kd_null", ctypes.c_float), ("damping", ctypes.c_float), ("grasp_offset", ctypes.c_float),
+                ("box_size", ctypes.c_float)]
 
 
 def _inv(a):
@@ -74,9 +98,13 @@ class CubePick:
     and set_dof_actuation_force_tensor (:409-410)."""
 
     def __init__(self, num_envs, init_pos, init_rot, default_dof_pos, device, controller="osc",
-                 box_size=0.045, damping=0.05, kp=150.0, kp_null=10.0):
+                 box_size=0.045, damping=0.05, kp=150.0, kp_null=10.0, fused=None):
         self.n = num_envs
         self.device = device
+        # fused: the one-kernel controller (csrc/mg_ctrl.hip) on a HIP device;
+        # None = there by default, False = the batched torch ops
+        self.fused = (torch.device(device).type == "cuda") if fused is None else bool(fused)
+        self._args = None
         self.controller = controller
         self.box_size = box_size
         self.damping = damping
@@ -118,10 +146,57 @@ class CubePick:
         u = u + _bmm(self.eye7 - _bmm(j_t, j_eef_inv), u_null)
         return u.squeeze(-1)
 
+    def _fused_args(self, rb_states, dof_pos, dof_vel, j_eef, mm, box_idxs, hand_idxs):
+        """The kernel's arguments for these tensors (built on the first call and
+        kept while the same tensors come back: a captured hipGraph replays the
+        pointers)."""
+        key = (rb_states.data_ptr(), dof_pos.data_ptr(), j_eef.data_ptr(), mm.data_ptr(), box_idxs.data_ptr(),
+               hand_idxs.data_ptr())
+        if self._args is not None and self._args[0] == key:
+            return self._args[1]
+        n = self.n
+        ok = (rb_states.dtype == torch.float32 and rb_states.is_contiguous() and rb_states.shape[1] == 13 and
+              dof_pos.shape == (n, 9, 1) and dof_pos.stride(1) == 2 and dof_pos.stride(0) % 2 == 0 and
+              dof_vel.data_ptr() == dof_pos.data_ptr() + 4 and dof_vel.stride() == dof_pos.stride() and
+              j_eef.shape == (n, 6, 7) and mm.shape == (n, 7, 7) and j_eef.dtype == torch.float32 and
+              mm.dtype == torch.float32)
+        if not ok:
+            raise ValueError("CubePick(fused=True): rb_states (nb, 13) contiguous, dof_pos / dof_vel the (n, 9, 1) "
+                             "views of the DOF state's two columns, j_eef (n, 6, 7) and mm (n, 7, 7) float32 views")
+        box_row = box_idxs.to(torch.int32).contiguous()
+        hand_row = hand_idxs.to(torch.int32).contiguous()
+        dof_row0 = torch.arange(n, dtype=torch.int32, device=rb_states.device) * (dof_pos.stride(0) // 2)
+        a = _CubePickArgs()
+        a.n = n
+        a.osc = 1 if self.controller == "osc" else 0
+        a.rb = rb_states.data_ptr()
+        a.box_row, a.hand_row, a.dof_row0 = box_row.data_ptr(), hand_row.data_ptr(), dof_row0.data_ptr()
+        a.dof = dof_pos.data_ptr()
+        a.jac = j_eef.data_ptr()
+        a.jac_se, a.jac_sr, a.jac_sc = j_eef.stride()
+        a.mm = mm.data_ptr()
+        a.mm_se, a.mm_sr, a.mm_sc = mm.stride()
+        a.init_pos, a.init_rot = self.init_pos.data_ptr(), self.init_rot.data_ptr()
+        a.default_dof_pos = self.default_dof_pos.data_ptr()
+        a.hand_restart = self.hand_restart.data_ptr()
+        a.pos_action, a.effort_action = self.pos_action.data_ptr(), self.effort_action.data_ptr()
+        a.kp, a.kd, a.kp_null, a.kd_null = self.kp, self.kd, self.kp_null, self.kd_null
+        a.damping = self.damping
+        a.grasp_offset = 0.11 if self.controller == "ik" else 0.10
+        a.box_size = self.box_size
+        self._args = (key, a, (box_row, hand_row, dof_row0))   # the index tensors live with the args
+        return a
+
     def step(self, rb_states, dof_pos, dof_vel, j_eef, mm, box_idxs, hand_idxs):
         """One controller frame (franka_cube_ik_osc.py:348-407).
         rb_states (num_bodies, 13); dof_pos / dof_vel (n, 9, 1); j_eef (n, 6, 7);
         mm (n, 7, 7); box_idxs / hand_idxs: long tensors of body rows."""
+        if self.fused:
+            from . import _native as N
+            a = self._fused_args(rb_states, dof_pos, dof_vel, j_eef, mm, box_idxs, hand_idxs)
+            stream = torch.cuda.current_stream(rb_states.device).cuda_stream
+            N.check(N.lib.mg_cube_pick_step(ctypes.byref(a), ctypes.c_void_p(stream)), "mg_cube_pick_step")
+            return self.pos_action, self.effort_action
         box_pos = rb_states[box_idxs, :3]
         box_rot = rb_states[box_idxs, 3:7]
         hand_pos = rb_states[hand_idxs, :3]

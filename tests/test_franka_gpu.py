@@ -69,7 +69,9 @@ def test_franka_env_classification(gym):
 def test_franka_pick_parity_bitexact(gym):
     """64 envs, 240 frames of the OSC pick loop (approach, grasp contacts,
     lift): GPU state == oracle state after every frame."""
-    n, frames = 64, 240
+    # MIGYM_PARITY_ENVS / _FRAMES: a longer run for measurements (DESIGN.md §6)
+    n = int(os.environ.get("MIGYM_PARITY_ENVS", "64"))
+    frames = int(os.environ.get("MIGYM_PARITY_FRAMES", "240"))
     sim, info, rb, dof, jac, mm, ctl = _setup(gym, n)
     p, m = sim.mg_params(), sim.mg_model()
     A = sim.model_arrays

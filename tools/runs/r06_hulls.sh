@@ -15,7 +15,7 @@ tag=${1:-r06f}
 run_setting() {   # name lib asset caps
   local v=$1
   export MIGYM_LIB=$2 MIGYM_FRANKA_ASSET=$3 MIGYM_HULL_CAPS=$4
-  timeout -k 10 300 python -u -m pytest tests/test_franka_gpu.py -k "parity_bitexact" -v --timeout 280 \
+  MIGYM_PARITY_ENVS=${PARITY_ENVS:-64} MIGYM_PARITY_FRAMES=${PARITY_FRAMES:-240} timeout -k 10 400 python -u -m pytest tests/test_franka_gpu.py -k "parity_bitexact" -v --timeout 380 \
     --timeout-method thread > gpurun_out/hull_parity_${v}_$tag.log 2>&1 || { tail -20 gpurun_out/hull_parity_${v}_$tag.log; return 1; }
   tail -1 gpurun_out/hull_parity_${v}_$tag.log
   KB_FRAMES=600 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/hull_kf_${v}_$tag -o run \
