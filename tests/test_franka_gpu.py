@@ -136,8 +136,11 @@ def test_franka_pick_lifts_cubes(gym, n):
     # the table by up to a substep's travel before its first contact exists (no
     # speculative contacts; tools/diag_franka_env.py: 160 of 4096 envs pass 1 mm
     # in some frame, the deepest 17.6 mm, a hand driven down at a cube on the
-    # floor; 31 pass 5 mm, each for at most 2 frames). One arm in 4096 (env 2581,
-    # profiles/r06_diag_franka.jsonl) wedges below the table top at a corner —
+    # floor; 31 pass 5 mm, each for at most 2 frames). With the torch controller's
+    # trajectories one arm in 4096 (env 2581, profiles/r06_diag_franka.jsonl;
+    # the one-kernel controller's, the default since round 6, differ in float32
+    # rounding and have no such arm: longest run 18 frames) wedged below the
+    # table top at a corner —
     # the hand against the -y face, finger A the -x face, finger B pressed down
     # on the top at ~480 N by the OSC torques — and that finger rests 1.32 mm in
     # for the remaining 390 frames. Measured cause (round 6 A/B, DESIGN.md
