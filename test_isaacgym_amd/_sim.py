@@ -494,6 +494,12 @@ class Sim:
         self.tensors["rb"] = torch.from_numpy(A["body_state0"].copy()).to(dev)
         self.tensors["dof"] = torch.from_numpy(A["dof_state0"].copy()).to(dev)
         self.tensors["ncf"] = torch.zeros((self.num_bodies, 3), dtype=torch.float32, device=dev)
+        if dev.type == "cpu" and N.device_count() > 0 and torch.cuda.is_available():
+            # the CPU pipeline's host tensors (test10's mode) in page-locked memory:
+            # every refresh is a D2H copy and every set an H2D copy, which then go
+            # straight over PCIe instead of through the runtime's staging buffer
+            for k in ("root", "rb", "dof", "ncf"):
+                self.tensors[k] = self.tensors[k].pin_memory()
         if N.device_count() > 0:
             handle = N.lib.mg_create_sim(self.compute_device, ctypes.byref(self.mg_params()))
             if not handle:
