@@ -415,6 +415,11 @@ int32_t     mg_num_articulations(mg_sim* sim);
  * touch each other under the actor_coll rule, e.g. the Franka cube-pick scene,
  * and every env holding a floating-base articulation). */
 int32_t     mg_num_coupled_envs(mg_sim* sim);
+/* Number of those stepped as free-body piles (csrc/mg_pile.hip, DESIGN.md
+ * §3.10): more than two free bodies, no articulation — the 30-ball pyramid per
+ * env of examples/1080_balls_of_solitude.py:96-136. Replaces no reference entry
+ * point of its own: gym.simulate (test10_servo_vecenv.py:380) steps them. */
+int32_t     mg_num_pile_envs(mg_sim* sim);
 
 /* ---- the S3 cube-pick controller on the device (csrc/mg_ctrl.hip) ----
  * Replaces the per-frame torch controller of examples/franka_cube_ik_osc.py

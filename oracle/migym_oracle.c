@@ -815,6 +815,7 @@ static int dof_ball_(const float* LF, const int* LI, int L, int d) {
 }
 
 #include "migym_oracle_env.c"
+#include "migym_oracle_pile.c"
 #include "migym_oracle_render.c"
 
 /* ---- serial chains: mg_chain.hip k_artic_chain, op for
@@ -1222,7 +1223,11 @@ int oracle_step(const mg_sim_params* p, const mg_model* m, float* state, float* 
     for (k = 0; k < ne; ++k) {
         const int first = envs[k].art_body >= 0 ? envs[k].art_body : envs[k].free_b[0];
         if (first < body_begin || first >= body_end) continue;
-        if (env_step_(&P, m, &envs[k], state, dof, tgt, props, ext, cforce, fcache) != 0) { rc = -1; goto done; }
+        if ((envs[k].pile ? pile_step_(&P, m, &envs[k], state, ext, cforce)
+                          : env_step_(&P, m, &envs[k], state, dof, tgt, props, ext, cforce, fcache)) != 0) {
+            rc = -1;
+            goto done;
+        }
     }
     for (k = 0; k < m->num_artics; ++k) {
         const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;
@@ -1264,7 +1269,9 @@ int oracle_step_mt(const mg_sim_params* p, const mg_model* m, float* state, floa
             int k, b;
 #pragma omp for schedule(dynamic, 16)
             for (k = 0; k < ne; ++k)
-                if (env_step_(&P, m, &envs[k], state, dof, tgt, props, ext, cforce, fcache) != 0) bad = 1;
+                if ((envs[k].pile ? pile_step_(&P, m, &envs[k], state, ext, cforce)
+                                  : env_step_(&P, m, &envs[k], state, dof, tgt, props, ext, cforce, fcache)) != 0)
+                    bad = 1;
 #pragma omp for schedule(static)
             for (k = 0; k < m->num_artics; ++k) {
                 const int* ai = m->artic_i + (size_t)k * MG_ARTIC_I_N;

@@ -779,9 +779,13 @@ static void ground_pair_(const step_t* P, const cshape_t* s, pair_t* o) {
 }
 
 /* env description, as the library's env_i row but with global body ids */
+#define OP_MAXB 64   /* free bodies of a pile env (mg_internal.h MG_PILE_MAXB; migym_oracle_pile.c) */
 typedef struct {
     int art_body, art_dof, art_tmpl, nf, free_b[OE_MAXF], ns, stat_b[OE_MAXS], mask;
     int env;   /* model env index (friction patch cache row) */
+    /* a pile env (more than OE_MAXF free bodies, no articulation): its free
+     * bodies pb and their actors pact, the static bodies' actors sact */
+    int pile, np, pb[OP_MAXB], pact[OP_MAXB], sact[OE_MAXS];
 } oenv_t;
 
 #define OE_GM 64      /* lanes of a wide env (mg_env.hip: G = 16, or 64 above 16 links / slots) */
@@ -1743,7 +1747,7 @@ static int classify_envs_(const mg_model* m, oenv_t* envs, char* owned) {
         free(fill);
     }
     for (e = 0; e < nenv; ++e) {
-        int art[2], fr[OE_MAXF + 1], stc[OE_MAXS + 1], nart = 0, nf = 0, ns = 0, i, j, coupled = 0, mask = 0;
+        int art[2], fr[OP_MAXB + 1], stc[OE_MAXS + 1], nart = 0, nf = 0, ns = 0, i, j, coupled = 0, mask = 0;
         int nart_all = 0, nf_all = 0, ns_all = 0, x;
         oenv_t* ev = &envs[n];
         for (x = start[e]; x < start[e + 1]; ++x) {
@@ -1751,7 +1755,7 @@ static int classify_envs_(const mg_model* m, oenv_t* envs, char* owned) {
             const int kind = m->body_kind[r0];
             a = list[x];
             if (kind == MG_BODY_LINK) { if (nart < 2) art[nart++] = a; nart_all++; }
-            else if (kind == MG_BODY_FREE) { if (nf <= OE_MAXF) fr[nf++] = a; nf_all++; }
+            else if (kind == MG_BODY_FREE) { if (nf <= OP_MAXB) fr[nf++] = a; nf_all++; }
             else { if (ns <= OE_MAXS) stc[ns++] = a; ns_all++; }
         }
         for (i = 0; i < nf; ++i) {
@@ -1768,9 +1772,27 @@ static int classify_envs_(const mg_model* m, oenv_t* envs, char* owned) {
             }
         }
         if (!coupled) continue;
-        if (nart_all > 1 || nf_all > OE_MAXF || ns_all > OE_MAXS) { n = -1; break; }
         ev->art_body = -1; ev->art_dof = 0; ev->art_tmpl = -1;
         ev->env = e;
+        ev->pile = 0;
+        if (nart_all == 0 && nf_all > OE_MAXF) {   /* a pile env (migym_oracle_pile.c) */
+            if (nf_all > OP_MAXB || ns_all > OE_MAXS) { n = -1; break; }
+            ev->pile = 1;
+            ev->np = nf;
+            for (i = 0; i < nf; ++i) {
+                ev->pact[i] = fr[i];
+                ev->pb[i] = m->actor_root_body[fr[i]];
+                owned[ev->pb[i]] = 1;
+            }
+            ev->nf = 0;
+            ev->free_b[0] = ev->pb[0];
+            ev->ns = ns;
+            for (i = 0; i < ns; ++i) { ev->sact[i] = stc[i]; ev->stat_b[i] = m->actor_root_body[stc[i]]; }
+            ev->mask = 0;
+            n++;
+            continue;
+        }
+        if (nart_all > 1 || nf_all > OE_MAXF || ns_all > OE_MAXS) { n = -1; break; }
         if (nart == 1) {
             const int r0 = m->actor_root_body[art[0]];
             for (i = 0; i < m->num_artics; ++i) {

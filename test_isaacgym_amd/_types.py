@@ -71,6 +71,25 @@ MESH_COLLISION = 1
 MESH_VISUAL = 2
 MESH_VISUAL_AND_COLLISION = 3
 
+# viewer keyboard inputs (gymapi.KeyboardInput; subscribe_viewer_keyboard_event,
+# examples/1080_balls_of_solitude.py:88). The viewer is headless and raises no
+# events, so only their distinctness matters; the values are this build's.
+KeyboardInput = int
+KEY_SPACE = 32
+KEY_APOSTROPHE, KEY_COMMA, KEY_MINUS, KEY_PERIOD, KEY_SLASH = 39, 44, 45, 46, 47
+for _i in range(10):
+    globals()["KEY_%d" % _i] = 48 + _i
+for _i in range(26):
+    globals()["KEY_" + chr(65 + _i)] = 65 + _i
+KEY_ESCAPE, KEY_ENTER, KEY_TAB, KEY_BACKSPACE, KEY_INSERT, KEY_DEL = 256, 257, 258, 259, 260, 261
+KEY_RIGHT, KEY_LEFT, KEY_DOWN, KEY_UP, KEY_PAGE_UP, KEY_PAGE_DOWN, KEY_HOME, KEY_END = (262, 263, 264, 265, 266,
+                                                                                        267, 268, 269)
+for _i in range(1, 13):
+    globals()["KEY_F%d" % _i] = 289 + _i
+KEY_LEFT_SHIFT, KEY_LEFT_CONTROL, KEY_LEFT_ALT, KEY_RIGHT_SHIFT, KEY_RIGHT_CONTROL, KEY_RIGHT_ALT = (340, 341, 342,
+                                                                                                    344, 345, 346)
+del _i
+
 RIGID_BODY_NONE = 0
 RIGID_BODY_DISABLE_GRAVITY = 1
 RIGID_BODY_DISABLE_SIMULATION = 2

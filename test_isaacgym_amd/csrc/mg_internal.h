@@ -200,6 +200,36 @@ struct MgEnvArgs {
     float*       ctab;        // [ne][ctab] this substep's contacts and anchors (k_env_np -> k_env_step)
 };
 
+// Free-body pile step (mg_pile.hip): a coupled env with more
+// than MG_ENV_MAXF free bodies and no articulation, one wavefront per env, lane
+// k = free body k. pile_i rows (MG_PILE_I_N int32): [0] first entry of the env's
+// free bodies in pile_body (internal slots), [1] their count nb <= MG_PILE_MAXB,
+// [2] first candidate pair, [3] pair count, [4] static bodies ns <= MG_ENV_MAXS,
+// [5..8] their internal slots. Pairs ([4] int32): a (free body 0..nb-1), shape
+// of a, b (free body, MG_PILE_ST0 + static body s, -1 the ground), shape of b.
+#define MG_PILE_I_N      12
+#define MG_PILE_MAXB     64
+#define MG_PILE_ST0      64
+#define MG_PILE_MAXAP    128     // active pairs (with contacts) per substep
+#define MG_PILE_MAXPT    256     // contact points per substep
+#define MG_PILE_MAXPAIRS 8192    // candidate shape pairs per env
+struct MgPileArgs {
+    int          ne;          // pile envs
+    int          nb;          // SoA stride
+    const int*   pile_i;      // [ne][MG_PILE_I_N]
+    const int*   pile_body;   // free bodies' internal slots
+    const int*   pairs;       // [..][4]
+    float*       state;
+    const float* mass;
+    const int*   body_tmpl;
+    const float* tbf;
+    const float* shapes;
+    const float* hulls;
+    const float* shape_obb;   // [num_shapes][MG_OBB_N] (pair screen)
+    const float* ext;         // [6][nb] or null
+    float*       cforce;      // [3][nb]
+};
+
 // Camera render (mg_render.hip). One device record per camera; a camera's
 // pixels are cut into linear runs of MG_RENDER_RUN pixels (row-major), one run
 // per workgroup; blk0 = first workgroup of the camera (prefix over cameras).
@@ -270,6 +300,7 @@ extern thread_local MgKernelTimer* mg_timer;
 hipError_t mg_launch_render(const MgRenderArgs& A, int nblocks, hipStream_t s);
 hipError_t mg_launch_cube_pick(const mg_cube_pick_args& A, hipStream_t s);
 hipError_t mg_launch_env_step(const MgStep& P, const MgEnvArgs& A, hipStream_t s);
+hipError_t mg_launch_pile_step(const MgStep& P, const MgPileArgs& A, hipStream_t s);
 extern "C" int mg_env_carry_floats(void);   // per-env record sizes of the coupled step (mg_env.hip)
 extern "C" int mg_env_ctab_floats(void);
 int mg_env_ctab_record_floats(int wide);   // one env's contact table in a 16- / 64-lane group

@@ -170,6 +170,12 @@ struct mg_sim {
     float* d_env_ctab = nullptr;     // [n_coupled][mg_env_ctab_floats] contacts of one substep (k_env_np -> k_env_step)
     int n_coupled = 0;
     std::vector<EnvGroup> env_groups;
+    // free-body piles (mg_pile.hip): coupled envs of more than MG_ENV_MAXF free
+    // bodies and no articulation, one wavefront each
+    int n_pile = 0;
+    int* d_pile_i = nullptr;      // [n_pile][MG_PILE_I_N]
+    int* d_pile_body = nullptr;   // their free bodies' internal slots
+    int* d_pile_pairs = nullptr;  // [..][4] candidate shape pairs (env-local participants)
 
     float* d_stage = nullptr;     // host-transfer staging (floats)
     size_t stage_n = 0;
@@ -390,7 +396,7 @@ void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls, s->d_shape_obb,
                     s->d_actor_root, s->d_root_row, s->d_slot_global, s->d_slot_actor, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
                     s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_chain_uni, s->d_fp_mask, s->d_env_carry, s->d_env_ctab, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
-                    s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
+                    s->d_pile_i, s->d_pile_body, s->d_pile_pairs, s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -550,6 +556,10 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     std::vector<std::array<int, MG_ENV_I_N>> env_rows;   // global body ids, converted below
     std::vector<int> env_tmpl;
     std::vector<int> pairs;                              // [..][4] shape pairs of the coupled envs
+    // pile envs (mg_pile.hip): rows with global body ids (converted below),
+    // the free bodies, their candidate pairs
+    std::vector<std::array<int, MG_PILE_I_N>> pile_rows;
+    std::vector<int> pile_body, pile_pairs;
     if (m->actor_coll && na > 0) {
         for (int a = 0; a + 1 < na; ++a)
             if (m->actor_root_body[a + 1] <= m->actor_root_body[a])
@@ -596,6 +606,61 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                     coupled = true;
             }
             if (!coupled) continue;
+            if (art.empty() && fr.size() > MG_ENV_MAXF) {
+                // a pile (mg_pile.hip): lane k = free body k; pairs
+                // per free body k and shape of k: the ground, the static bodies it
+                // may touch, the later free bodies it may touch
+                if (fr.size() > MG_PILE_MAXB || stc.size() > MG_ENV_MAXS)
+                    return fail(MG_ERR_UNSUPPORTED,
+                                "env %d: %zu free / %zu static bodies in contact range; a pile env supports %d / %d",
+                                e, fr.size(), stc.size(), MG_PILE_MAXB, MG_ENV_MAXS);
+                std::array<int, MG_PILE_I_N> row;
+                row.fill(0);
+                row[0] = (int)pile_body.size();
+                row[1] = (int)fr.size();
+                row[2] = (int)(pile_pairs.size() / 4);
+                row[4] = (int)stc.size();
+                for (size_t t = 0; t < stc.size(); ++t) row[5 + t] = m->actor_root_body[stc[t]];
+                for (int f : fr) {
+                    pile_body.push_back(m->actor_root_body[f]);
+                    coupled_body[m->actor_root_body[f]] = 1;
+                }
+                const bool ground = s->params.has_ground != 0;
+                auto shp = [m](int b, int* s0, int* ns) {
+                    const int* t = m->tmpl_body_i + (size_t)m->body_tmpl[b] * MG_TBODY_I_N;
+                    *s0 = t[0];
+                    *ns = t[1];
+                };
+                for (int k = 0; k < (int)fr.size(); ++k) {
+                    int sa0, nsa;
+                    shp(m->actor_root_body[fr[k]], &sa0, &nsa);
+                    for (int sa = sa0; sa < sa0 + nsa; ++sa) {
+                        auto push = [&](int b, int sb) {
+                            pile_pairs.push_back(k); pile_pairs.push_back(sa);
+                            pile_pairs.push_back(b); pile_pairs.push_back(sb);
+                        };
+                        if (ground) push(-1, -1);
+                        for (int t = 0; t < (int)stc.size(); ++t) {
+                            if (!collide(fr[k], stc[t])) continue;
+                            int sb0, nsb;
+                            shp(m->actor_root_body[stc[t]], &sb0, &nsb);
+                            for (int sb = sb0; sb < sb0 + nsb; ++sb) push(MG_PILE_ST0 + t, sb);
+                        }
+                        for (int j = k + 1; j < (int)fr.size(); ++j) {
+                            if (!collide(fr[k], fr[j])) continue;
+                            int sb0, nsb;
+                            shp(m->actor_root_body[fr[j]], &sb0, &nsb);
+                            for (int sb = sb0; sb < sb0 + nsb; ++sb) push(j, sb);
+                        }
+                    }
+                }
+                row[3] = (int)(pile_pairs.size() / 4) - row[2];
+                if (row[3] > MG_PILE_MAXPAIRS)
+                    return fail(MG_ERR_UNSUPPORTED, "env %d: %d candidate shape pairs; a pile env supports %d", e,
+                                row[3], MG_PILE_MAXPAIRS);
+                pile_rows.push_back(row);
+                continue;
+            }
             if (art.size() > 1 || fr.size() > MG_ENV_MAXF || stc.size() > MG_ENV_MAXS)
                 return fail(MG_ERR_UNSUPPORTED,
                             "env %d: %zu articulations / %zu free / %zu static bodies in contact range; the "
@@ -913,6 +978,10 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         if (g.count > 0) s->env_groups.push_back(g);
     }
     s->n_coupled = (int)env_rows.size();
+    s->n_pile = (int)pile_rows.size();
+    for (auto& r : pile_rows)
+        for (int t = 0; t < r[4]; ++t) r[5 + t] = perm[r[5 + t]];
+    for (int& b : pile_body) b = perm[b];
     std::vector<int> root_int(na), tmpl_int(nb);
     for (int a = 0; a < na; ++a) root_int[a] = perm[m->actor_root_body[a]];
     for (int i = 0; i < nb; ++i) tmpl_int[i] = m->body_tmpl[order[i]];
@@ -1027,7 +1096,8 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         // free-body kernel (internal slots 0..nf1-1), and that kernel steps all
         // free bodies (no multi-shape ones, no articulations, no coupled envs)
         std::vector<int> row(nb, -1);
-        bool ok = s->nf1 == s->nf_rigid && s->nf_rigid == s->nf && s->nartic == 0 && s->n_coupled == 0 && na > 0;
+        bool ok = s->nf1 == s->nf_rigid && s->nf_rigid == s->nf && s->nartic == 0 && s->n_coupled == 0 &&
+                  s->n_pile == 0 && na > 0;
         for (int a = 0; a < na && ok; ++a) {
             const int slot = root_int[a];
             ok = slot >= 0 && slot < s->nf1 && row[slot] < 0;
@@ -1067,7 +1137,7 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
             if (!(g.chain && g.nl >= 2 && g.nl <= 4) || g.step_count != g.count) covered = -1;
             else covered += (long long)g.step_count * g.nbody;
         }
-        s->step_out_ok = s->n_coupled == 0 && nb > 0 && covered == nb;
+        s->step_out_ok = s->n_coupled == 0 && s->n_pile == 0 && nb > 0 && covered == nb;
     }
     HIP_TRY(h2d(s->d_actor_dof, m->actor_dof, (size_t)(na + 1) * sizeof(int)));
     HIP_TRY(hipMemset(s->d_cforce, 0, (size_t)nb * 3 * sizeof(float)));
@@ -1087,6 +1157,16 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     HIP_TRY(h2d(s->d_artic_step, artic_step.data(), artic_step.size() * sizeof(int)));
     HIP_TRY(h2d(s->d_env, env_flat.data(), env_flat.size() * sizeof(int)));
     HIP_TRY(h2d(s->d_pairs, pairs.data(), pairs.size() * sizeof(int)));
+    if (s->n_pile > 0) {
+        std::vector<int> flat;
+        for (const auto& r : pile_rows) flat.insert(flat.end(), r.begin(), r.end());
+        HIP_TRY(dalloc(&s->d_pile_i, flat.size()));
+        HIP_TRY(h2d(s->d_pile_i, flat.data(), flat.size() * sizeof(int)));
+        HIP_TRY(dalloc(&s->d_pile_body, pile_body.size()));
+        HIP_TRY(h2d(s->d_pile_body, pile_body.data(), pile_body.size() * sizeof(int)));
+        HIP_TRY(dalloc(&s->d_pile_pairs, std::max<size_t>(pile_pairs.size(), 4)));
+        if (!pile_pairs.empty()) HIP_TRY(h2d(s->d_pile_pairs, pile_pairs.data(), pile_pairs.size() * sizeof(int)));
+    }
     {   // no friction patch yet: every pair starts without anchors
         const size_t np = std::max<size_t>(pairs.size() / 4, 1), nm = (size_t)std::max(s->n_coupled, 1) * MG_FP_W;
         HIP_TRY(dalloc(&s->d_fpatch, np * MG_FP_N));
@@ -1226,6 +1306,17 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.cforce = s->d_cforce;
         hipError_t e = mg_launch_env_step(P, A, st);
         if (e != hipSuccess) return fail(MG_ERR_DEVICE, "coupled env step launch: %s", hipGetErrorString(e));
+    }
+    if (s->n_pile > 0) {
+        MgPileArgs A{};
+        A.ne = s->n_pile; A.nb = s->nb;
+        A.pile_i = s->d_pile_i; A.pile_body = s->d_pile_body; A.pairs = s->d_pile_pairs;
+        A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl; A.tbf = s->d_tbf;
+        A.shapes = s->d_shapes; A.hulls = s->d_hulls; A.shape_obb = s->d_shape_obb;
+        A.ext = s->ext_pending ? s->d_ext : nullptr;
+        A.cforce = s->d_cforce;
+        hipError_t e = mg_launch_pile_step(P, A, st);
+        if (e != hipSuccess) return fail(MG_ERR_DEVICE, "pile step launch: %s", hipGetErrorString(e));
     }
     if (s->nf_rigid > 0) {
         MgRigidArgs A{};
@@ -1424,6 +1515,7 @@ int32_t mg_cube_pick_step(const mg_cube_pick_args* a, void* stream) {
 int32_t mg_num_free_bodies(mg_sim* s) { return s ? s->nf : 0; }
 int32_t mg_num_articulations(mg_sim* s) { return s ? s->nartic : 0; }
 int32_t mg_num_coupled_envs(mg_sim* s) { return s ? s->n_coupled : 0; }
+int32_t mg_num_pile_envs(mg_sim* s) { return s ? s->n_pile : 0; }
 
 int32_t mg_refresh_actor_root_state(mg_sim* s, float* dst, int32_t dst_host, void* stream) {
     if (!s) return fail(MG_ERR_ARG, "null sim");

@@ -451,6 +451,73 @@ def ant_scene(gym, num_envs, use_gpu_pipeline=True, device=0, asset_root=None, a
     return sim, {"num_bodies": nb, "envs": envs, "actors": actors, "asset": asset}
 
 
+# ------------------------------------------------------------ S6 ball piles
+def ball_pile_sim_params(use_gpu_pipeline=True):
+    """examples/1080_balls_of_solitude.py:41-53: Isaac Gym's default (y-up) sim,
+    dt 1/60, 1 substep, PhysX TGS 4/1."""
+    sp = gymapi.SimParams()
+    sp.substeps = 1
+    sp.physx.solver_type = 1
+    sp.physx.num_position_iterations = 4
+    sp.physx.num_velocity_iterations = 1
+    sp.use_gpu_pipeline = use_gpu_pipeline
+    return sp
+
+
+def ball_pyramid_poses(n=4, radius=0.2):
+    """The pyramid of examples/1080_balls_of_solitude.py:102-132: layers of
+    n x n, (n-1) x (n-1), ... balls spaced 2.5 radii, the bottom layer at
+    y = 1.5 + 4 - 0.75 m (30 balls for n = 4), env-local (x, y, z)."""
+    out = []
+    spacing = 2.5 * radius
+    min_coord = -0.5 * (n - 1) * spacing
+    y = min_coord + 4
+    while n > 0:
+        z = min_coord
+        for _ in range(n):
+            x = min_coord
+            for _ in range(n):
+                out.append((x, 1.5 + y, z))
+                x += spacing
+            z += spacing
+        y += spacing
+        n -= 1
+        min_coord = -0.5 * (n - 1) * spacing
+    return out
+
+
+def ball_pile_scene(gym, num_envs, use_gpu_pipeline=True, device=0, asset_root=None, mode="env",
+                    sim_params=None, n=4):
+    """S6: examples/1080_balls_of_solitude.py:29-136 — per env a pyramid of 30
+    assets/urdf/ball.urdf balls (0.2 m, 0.5 kg), env spacing 1.25, sqrt(n) envs
+    per row. mode "env" (the script's default): group i, filter 0, so the balls
+    of an env collide with each other — a pile env; "none"
+    (--no_collisions): group 0, filter 1, only the ground. Returns (sim, envs)."""
+    sim = gym.create_sim(device, device, gymapi.SIM_PHYSX, sim_params or ball_pile_sim_params(use_gpu_pipeline))
+    gym.add_ground(sim, gymapi.PlaneParams())
+    ball = gym.load_asset(sim, asset_root or ASSET_ROOT, "urdf/ball.urdf", gymapi.AssetOptions())
+    if ball is None:
+        raise RuntimeError("failed to load ball.urdf")
+    per_row = max(int(math.sqrt(num_envs)), 1)
+    spacing = 1.25
+    lower, upper = gymapi.Vec3(-spacing, 0.0, -spacing), gymapi.Vec3(spacing, spacing, spacing)
+    poses = ball_pyramid_poses(n)
+    rng = np.random.RandomState(17)
+    envs = []
+    for i in range(num_envs):
+        env = gym.create_env(sim, lower, upper, per_row)
+        envs.append(env)
+        c = 0.5 + 0.5 * rng.random_sample(3)
+        for p in poses:
+            pose = gymapi.Transform()
+            pose.p = gymapi.Vec3(*p)
+            pose.r = gymapi.Quat(0, 0, 0, 1)
+            group, filt = (i, 0) if mode == "env" else (0, 1)
+            a = gym.create_actor(env, ball, pose, None, group, filt)
+            gym.set_rigid_body_color(env, a, 0, gymapi.MESH_VISUAL_AND_COLLISION, gymapi.Vec3(*c))
+    return sim, envs
+
+
 # ------------------------------------------------------ domain randomization
 DR_CAM_POS = (0.0, 3.0, 3.0)
 DR_CAM_TARGET = (0.0, 0.0, -1.0)

@@ -152,3 +152,35 @@ def test_joint_monkey_humanoid_setup(monkeypatch):
     env, h = ns["envs"][0], ns["actor_handles"][0]
     fr = gym.get_dof_frame(env, gym.get_actor_dof_handle(env, h, 0))
     assert abs((fr.axis.x ** 2 + fr.axis.y ** 2 + fr.axis.z ** 2) - 1.0) < 1e-6
+
+
+@pytest.mark.skipif(has_gpu(), reason="CPU-container variant")
+@pytest.mark.parametrize("mode", ["", "--no_collisions"])
+def test_1080_balls_of_solitude_setup(monkeypatch, mode):
+    """examples/1080_balls_of_solitude.py unmodified (36 envs x 30 balls): by
+    default group i, filter 0 — every env a pile, the same
+    packed scene as scenes.ball_pile_scene, stepped on the oracle here; with
+    --no_collisions (group 0, filter 1) the balls are uncoupled free bodies."""
+    import numpy as np
+    import oracle
+    from test_isaacgym_amd import gymapi as G, scenes
+    path = os.path.join(REFERENCE, "examples", "1080_balls_of_solitude.py")
+    monkeypatch.setattr(sys, "argv", [path] + ([mode] if mode else []))
+    ns, err = _exec_script(path, os.path.join(REFERENCE, "examples"), monkeypatch)
+    assert err is not None
+    gym, sim = ns["gym"], ns["sim"]
+    assert len(ns["envs"]) == 36 and gym.get_sim_rigid_body_count(sim) == 1080
+    assert ns["initial_state"].shape == (1080,)
+    A = sim.model_arrays
+    if mode:
+        assert (A["actor_coll"][:, 1:3] == [0, 1]).all()
+    else:
+        assert (A["actor_coll"][:, 1] == np.repeat(np.arange(36), 30)).all() and (A["actor_coll"][:, 2] == 0).all()
+    ref_sim, _ = scenes.ball_pile_scene(G.acquire_gym(), 36, use_gpu_pipeline=False, mode="env" if not mode else "none")
+    R = ref_sim.build_model()
+    assert np.array_equal(R["body_state0"], A["body_state0"])
+    p, m = sim.mg_params(), sim.mg_model()
+    st, dof = A["body_state0"].copy(), A["dof_state0"].copy()
+    for _ in range(90):
+        oracle.step(p, m, st, dof)
+    assert st[:, 1].min() > 0.19 and np.isfinite(st).all()
