@@ -58,6 +58,12 @@ STEP_BYTES_PER_ENV = 688         # whole tensor-API step
 S2_BYTES_PER_ENV = 532           # SURVEY.md §8d S2 (servo-arm gimbal)
 S2_LARGE_N = 262144
 S3_BYTES_PER_ENV = 5844          # SURVEY.md §8d S3 (Franka cube pick, the whole tensor-API step)
+# S6 ball piles (examples/1080_balls_of_solitude.py): per ball
+# and simulate, state in 52 + out 52 + mass properties 44 + net contact force
+# 12 (SURVEY §8d's per-body pricing; the shape and the pair list are template
+# data shared by every env, read through L2), x 30 balls
+S6_BALLS = 30
+S6_BYTES_PER_ENV = S6_BALLS * (52 + 52 + 44 + 12)
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 KERNEL_TIMED_LAUNCHES = 128      # eager launches with dispatch timestamps (ring holds 256)
 GRAPH_CHUNK_MAX = 64             # tensor-API steps captured per hipGraph at most (amortizes the graph launch)
@@ -81,6 +87,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-gimbal", action="store_true", help="skip the secondary S2 servo-arm measurement")
     ap.add_argument("--no-franka", action="store_true", help="skip the secondary S3 Franka cube-pick measurement")
     ap.add_argument("--no-cameras", action="store_true", help="skip the secondary S5 camera-render measurement")
+    ap.add_argument("--no-piles", action="store_true", help="skip the secondary S6 ball-pile measurement")
+    ap.add_argument("--pile-envs", type=int, default=ENVS_PER_GPU, help="envs of the S6 ball-pile leg")
     ap.add_argument("--no-large-n", action="store_true", help="skip the 262,144-env S1 kernel leg")
     ap.add_argument("--no-default-legs", action="store_true",
                     help="skip the S1 library-default (fusion off) and CPU-pipeline legs")
@@ -277,6 +285,16 @@ def _cpu_scene(leg, n):
         def hook(st, tgt, k):
             tgt[:, 0] = tg[k % len(tg)]
         return sim, hook, tgt
+    if leg == "s6":
+        sim, _ = scenes.ball_pile_scene(gym, n, use_gpu_pipeline=False)
+        sim.build_model()
+        p, m = sim.mg_params(), sim.mg_model()
+        import oracle
+        st0 = sim.model_arrays["body_state0"]
+        dof0 = sim.model_arrays["dof_state0"].copy()
+        for _ in range(90):   # the GPU leg times the collapsed piles: drop them first
+            oracle.step_threads(p, m, st0, dof0, max(1, cpu_threads()[1]))
+        return sim, (lambda st, tgt, k: None), None
     sim, info = scenes.franka_scene(gym, n, use_gpu_pipeline=False)
     sim.build_model()
     nd = sim.model_arrays["dof_state0"].shape[0]
@@ -328,6 +346,7 @@ def cpu_baseline(seconds=10.0):
     s1 = cpu_leg("s1", n, seconds, [(usable, seconds * 0.4), (1, seconds * 0.2)] + extra)
     s2 = cpu_leg("s2", n, seconds, [(usable, seconds * 0.3)] + extra)
     s3 = cpu_leg("s3", n, seconds, [(usable, seconds * 0.5)] + extra)
+    s6 = cpu_leg("s6", n, seconds, [(usable, seconds * 0.3)])
 
     def leg(r, what):
         v, steps, el = r[usable]
@@ -344,8 +363,10 @@ def cpu_baseline(seconds=10.0):
                         "with os.cpu_count() threads, throttled by that quota",
                 "s2": leg(s2, "%d simulate() steps of 4096 3-DOF gimbals under random PD targets (S2)" % s2[usable][1]),
                 "s3": leg(s3, "%d simulate() steps of 4096 Franka cube-pick envs holding their default DOF "
-                              "targets (S3 physics only; the OSC controller is not in the oracle)" % s3[usable][1])})
-    out["sample"] = out["sample"] + "; S2 and S3 under s2 / s3"
+                              "targets (S3 physics only; the OSC controller is not in the oracle)" % s3[usable][1]),
+                "s6": leg(s6, "%d simulate() steps of 4096 envs of 1080_balls_of_solitude.py's 30-ball pyramid, "
+                              "after 90 frames of collapse (S6)" % s6[usable][1])})
+    out["sample"] = out["sample"] + "; S2, S3 and S6 under s2 / s3 / s6"
     return out
 
 
@@ -600,6 +621,75 @@ def camera_rate(n, steps, warmup, dev, use_graph=True, width=1600, height=900):
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": pmc_file},
             "env0_non_sky_fraction": lit, "sampled_cameras_non_sky_fraction": lit_all}
+
+
+def pile_rate(n, steps, warmup, dev, use_graph=True):
+    """S6 ball piles: examples/1080_balls_of_solitude.py's scene at n envs (30
+    balls per env in one collision group, y-up, 1 substep, TGS 4/1; the script
+    runs 36) — every env a pile stepped by k_pile_step. One
+    step = simulate -> fetch_results -> refresh the rigid-body tensor. Timed
+    from the pyramids' collapse on (the warm-up drops them: 60 frames to the
+    ground), replayed as hipGraphs."""
+    import torch
+    from isaacgym import gymapi, gymtorch
+    from test_isaacgym_amd import _native as N, scenes
+    gym = gymapi.acquire_gym()
+    sim, envs = scenes.ball_pile_scene(gym, n, use_gpu_pipeline=True, device=dev.index or 0)
+    gym.prepare_sim(sim)
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+
+    def step():
+        gym.simulate(sim)
+        gym.fetch_results(sim, False)
+        gym.refresh_rigid_body_state_tensor(sim)
+
+    for _ in range(warmup):
+        step()
+    kms, kmin, used = kernel_stats(sim, 100, lambda: [step() for _ in range(100)])
+    graph, chunk = None, graph_chunk(steps, 16)
+    if use_graph:
+        try:
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for _ in range(chunk):
+                    step()
+            graph.replay()
+        except Exception as ex:
+            print("*** bench: S6 hipGraph capture failed (%s); timing the eager loop" % ex, file=sys.stderr)
+            graph = None
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    if graph is not None:
+        for _ in range(steps // chunk):
+            graph.replay()
+    else:
+        for _ in range(steps):
+            step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    y = rb[:, 1].view(n, S6_BALLS)
+    ach = S6_BYTES_PER_ENV * n / (kms * 1e-3) / 1e9 if kms else None
+    pmc, pmc_file = load_pmc("pile_%d" % n)
+    out = {"envs": n, "bodies": n * S6_BALLS, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps,
+           "kernel": "k_pile_step (one launch per simulate)", "kernel_ms_avg": kms, "kernel_ms_min": kmin,
+           "kernel_launches_timed": used, "pile_envs": int(N.lib.mg_num_pile_envs(sim.native)),
+           "roofline": {"bound": "hbm", "kernel": "k_pile_step", "achieved": ach, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": (ach / HBM_PEAK_GBS) if ach else None,
+                        "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None, "traffic_source": pmc_file,
+                        "algorithmic_bytes_per_env": S6_BYTES_PER_ENV,
+                        "note": "30 balls x (state in 52 + out 52 + mass 44 + contact force 12 B); the kernel is "
+                                "bound by its per-env serial work (narrow phase of 465 candidate pairs, the "
+                                "colouring, the colour-by-colour sweeps), not by HBM: DESIGN.md §3.10"},
+           "balls_height_range_m": [float(y.min()), float(y.max())],
+           "timed_loop": ("hipGraph replay, %d steps per graph" % chunk) if graph is not None else "eager Python loop"}
+    gym.destroy_sim(sim)
+    return out
 
 
 def s1_rate(n, steps, dev, use_graph=True, fused=True, seed=1, unfused_kernel=False):
@@ -986,6 +1076,8 @@ def main():
             out["s3_franka"] = franka_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
         if not args.no_cameras:
             out["s5_cameras"] = camera_rate(args.camera_envs, min(args.steps, 100), 10, dev, not args.eager)
+        if not args.no_piles:
+            out["s6_piles"] = pile_rate(args.pile_envs, min(args.steps, 300), 90, dev, not args.eager)
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

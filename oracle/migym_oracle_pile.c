@@ -60,14 +60,21 @@ static int pile_pairs_(const mg_model* m, const oenv_t* ev, int ground, epair_t*
     return n;
 }
 
-/* relative velocity of A over B along d at lever arms ra, rb (mg_pile.hip rel_d) */
-static float op_rel_(v3_t d, v3_t ra, v3_t rb, v3_t va, v3_t wa, v3_t vb, v3_t wb) {
-    return (dot3(d, va) + dot3(cross3(ra, d), wa)) - (dot3(d, vb) + dot3(cross3(rb, d), wb));
+/* relative velocity of A over B along d at lever arms ra, rb (mg_pile.hip
+ * pair_constants); B static or the ground (dynb 0): A's terms only */
+static float op_rel_(int dynb, v3_t d, v3_t ra, v3_t rb, v3_t va, v3_t wa, v3_t vb, v3_t wb) {
+    const float ua = dot3(d, va) + dot3(cross3(ra, d), wa);
+    return dynb ? ua - (dot3(d, vb) + dot3(cross3(rb, d), wb)) : ua;
 }
 /* 1 / effective mass of a row along d (mg_pile.hip row_k) */
-static float op_k_(v3_t d, v3_t ra, v3_t rb, float ima, float imb, const s3_t* Ia, const s3_t* Ib) {
-    const v3_t ca = cross3(ra, d), cb = cross3(rb, d);
-    return 1.0f / (((ima + imb) + dot3(ca, symmul_(*Ia, ca))) + dot3(cb, symmul_(*Ib, cb)));
+static float op_k_(int dynb, v3_t d, v3_t ra, v3_t rb, float ima, float imb, const s3_t* Ia, const s3_t* Ib) {
+    const v3_t ca = cross3(ra, d);
+    const float ka = ima + dot3(ca, symmul_(*Ia, ca));
+    if (!dynb) return 1.0f / ka;
+    {
+        const v3_t cb = cross3(rb, d);
+        return 1.0f / ((ka + imb) + dot3(cb, symmul_(*Ib, cb)));
+    }
 }
 
 typedef struct {
@@ -77,9 +84,29 @@ typedef struct {
     float invm[OP_MAXB];
 } pbody_t;
 
-/* the velocities a pair's rows act on: A's, and B's (zero and never stored
- * back for a static body or the ground) */
-typedef struct { float ima, imb; s3_t Ia, Ib; v3_t dxa, dta, dxb, dtb, va, wa, vb, wb; } prow_t;
+/* the velocities a pair's rows act on: A's, and B's when B is a free body
+ * (dynb); against a static body or the ground a row has A's terms only */
+typedef struct { int dynb; float ima, imb; s3_t Ia, Ib; v3_t dxa, dta, dxb, dtb, va, wa, vb, wb; } prow_t;
+
+/* A's (and B's) part of a row along d at lever arms ra, rb: the relative
+ * velocity (mg_pile.hip rel_v) and the relative motion over the substep */
+static float op_relv_(const prow_t* R, v3_t d, v3_t ca, v3_t cb) {
+    const float ua = dot3(d, R->va) + dot3(ca, R->wa);
+    return R->dynb ? ua - (dot3(d, R->vb) + dot3(cb, R->wb)) : ua;
+}
+static float op_reld_(const prow_t* R, v3_t d, v3_t ca, v3_t cb) {
+    const float ua = dot3(d, R->dxa) + dot3(ca, R->dta);
+    return R->dynb ? ua - (dot3(d, R->dxb) + dot3(cb, R->dtb)) : ua;
+}
+/* apply impulse dl along d: A gets +dl, B -dl */
+static void op_apply_(prow_t* R, v3_t d, v3_t ca, v3_t cb, float dl) {
+    R->va = fmad3_(R->va, d, dl * R->ima);
+    R->wa = fmad3_(R->wa, symmul_(R->Ia, ca), dl);
+    if (R->dynb) {
+        R->vb = fmad3_(R->vb, d, -(dl * R->imb));
+        R->wb = fmad3_(R->wb, symmul_(R->Ib, cb), -dl);
+    }
+}
 
 /* the pair's normal rows, point order (mg_pile.hip normal_rows) */
 static void op_normal_rows_(const step_t* P, const pap_t* pr, ppt_t* pt, prow_t* R, int pos) {
@@ -87,16 +114,13 @@ static void op_normal_rows_(const step_t* P, const pap_t* pr, ppt_t* pt, prow_t*
     for (j = 0; j < pr->pn; ++j) {
         ppt_t* c = &pt[pr->pt0 + j];
         const v3_t ca = cross3(c->ra, c->n), cb = cross3(c->rb, c->n);
-        const float s = c->s0 + ((dot3(c->n, R->dxa) + dot3(ca, R->dta)) - (dot3(c->n, R->dxb) + dot3(cb, R->dtb)));
+        const float s = c->s0 + op_reld_(R, c->n, ca, cb);
         const float tgt = pos ? pos_target_(P, s) : vel_target_(P, s, pr->e, c->vn0);
-        const float vn = (dot3(c->n, R->va) + dot3(ca, R->wa)) - (dot3(c->n, R->vb) + dot3(cb, R->wb));
+        const float vn = op_relv_(R, c->n, ca, cb);
         const float nl = fmaxf(fmaf(c->kn, tgt - vn, c->ln), 0.0f);
         const float dl = nl - c->ln;
         c->ln = nl;
-        R->va = fmad3_(R->va, c->n, dl * R->ima);
-        R->wa = fmad3_(R->wa, symmul_(R->Ia, ca), dl);
-        R->vb = fmad3_(R->vb, c->n, -(dl * R->imb));
-        R->wb = fmad3_(R->wb, symmul_(R->Ib, cb), -dl);
+        op_apply_(R, c->n, ca, cb, dl);
     }
 }
 
@@ -113,16 +137,12 @@ static void op_friction_rows_(const step_t* P, const pap_t* pr, ppt_t* pt, prow_
             const v3_t t = r == 0 ? c->t1 : c->t2;
             const float kt = r == 0 ? c->kt1 : c->kt2, lt = r == 0 ? c->lt1 : c->lt2;
             const v3_t ca = cross3(c->ra, t), cb = cross3(c->rb, t);
-            const float vt = (dot3(t, R->va) + dot3(ca, R->wa)) - (dot3(t, R->vb) + dot3(cb, R->wb));
-            const float dr = (dot3(t, R->dxa) + dot3(ca, R->dta)) - (dot3(t, R->dxb) + dot3(cb, R->dtb));
-            const float ft = pos ? -dr * P->inv_sub : 0.0f;
+            const float vt = op_relv_(R, t, ca, cb);
+            const float ft = pos ? -op_reld_(R, t, ca, cb) * P->inv_sub : 0.0f;
             const float nl = clamp_sym_(fmaf(kt, ft - vt, lt), lim);
             const float d = nl - lt;
             if (r == 0) c->lt1 = nl; else c->lt2 = nl;
-            R->va = fmad3_(R->va, t, d * R->ima);
-            R->wa = fmad3_(R->wa, symmul_(R->Ia, ca), d);
-            R->vb = fmad3_(R->vb, t, -(d * R->imb));
-            R->wb = fmad3_(R->wb, symmul_(R->Ib, cb), -d);
+            op_apply_(R, t, ca, cb, d);
         }
     }
 }
@@ -137,6 +157,7 @@ static void op_solve_pair_(const step_t* P, const pap_t* pr, ppt_t* pt, pbody_t*
     const int a = pr->a, b = pr->b, dynb = b >= 0 && b < OP_ST0;
     const v3_t z = V(0.0f, 0.0f, 0.0f);
     prow_t R;
+    R.dynb = dynb;
     R.ima = B->invm[a]; R.Ia = B->Iw[a];
     R.dxa = B->dx[a]; R.dta = B->dth[a]; R.va = B->v[a]; R.wa = B->w[a];
     if (dynb) {
@@ -274,10 +295,10 @@ static int pile_step_(const step_t* P, const mg_model* m, const oenv_t* ev, floa
             for (j = 0; j < pr->pn; ++j) {
                 ppt_t* c = &W.pt[pr->pt0 + j];
                 tangents_(c->n, &c->t1, &c->t2);
-                c->kn = op_k_(c->n, c->ra, c->rb, ima, imb, &Ia, &Ib);
-                c->kt1 = op_k_(c->t1, c->ra, c->rb, ima, imb, &Ia, &Ib);
-                c->kt2 = op_k_(c->t2, c->ra, c->rb, ima, imb, &Ia, &Ib);
-                c->vn0 = op_rel_(c->n, c->ra, c->rb, va, wa, vb, wb);
+                c->kn = op_k_(dynb, c->n, c->ra, c->rb, ima, imb, &Ia, &Ib);
+                c->kt1 = op_k_(dynb, c->t1, c->ra, c->rb, ima, imb, &Ia, &Ib);
+                c->kt2 = op_k_(dynb, c->t2, c->ra, c->rb, ima, imb, &Ia, &Ib);
+                c->vn0 = op_rel_(dynb, c->n, c->ra, c->rb, va, wa, vb, wb);
                 c->ln = 0.0f; c->lt1 = 0.0f; c->lt2 = 0.0f;
             }
         }

@@ -205,20 +205,28 @@ struct MgEnvArgs {
 // k = free body k. pile_i rows (MG_PILE_I_N int32): [0] first entry of the env's
 // free bodies in pile_body (internal slots), [1] their count nb <= MG_PILE_MAXB,
 // [2] first candidate pair, [3] pair count, [4] static bodies ns <= MG_ENV_MAXS,
-// [5..8] their internal slots. Pairs ([4] int32): a (free body 0..nb-1), shape
-// of a, b (free body, MG_PILE_ST0 + static body s, -1 the ground), shape of b.
+// [5..8] their internal slots, [9] first entry of its local shape slots in
+// `slots`, [10] their count <= MG_PILE_MAXSH. A local shape slot ([2] int32):
+// participant (free body k, or MG_PILE_ST0 + static body s), shape record —
+// the free bodies' shapes in body order, then the static bodies'. A candidate
+// pair (uint32): local slot of A | local slot of B << 8 (MG_PILE_GROUND: the
+// ground plane), in the oracle's pair order. Envs built alike share their slot
+// table and pair list.
 #define MG_PILE_I_N      12
 #define MG_PILE_MAXB     64
 #define MG_PILE_ST0      64
 #define MG_PILE_MAXAP    128     // active pairs (with contacts) per substep
 #define MG_PILE_MAXPT    256     // contact points per substep
 #define MG_PILE_MAXPAIRS 8192    // candidate shape pairs per env
+#define MG_PILE_MAXSH    128     // local shape slots per env
+#define MG_PILE_GROUND   255
 struct MgPileArgs {
     int          ne;          // pile envs
     int          nb;          // SoA stride
     const int*   pile_i;      // [ne][MG_PILE_I_N]
     const int*   pile_body;   // free bodies' internal slots
-    const int*   pairs;       // [..][4]
+    const unsigned* pairs;    // packed candidate pairs
+    const int*   slots;       // [..][2] local shape slots
     float*       state;
     const float* mass;
     const int*   body_tmpl;

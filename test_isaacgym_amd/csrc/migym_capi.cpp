@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstring>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "mg_internal.h"
@@ -175,7 +176,8 @@ struct mg_sim {
     int n_pile = 0;
     int* d_pile_i = nullptr;      // [n_pile][MG_PILE_I_N]
     int* d_pile_body = nullptr;   // their free bodies' internal slots
-    int* d_pile_pairs = nullptr;  // [..][4] candidate shape pairs (env-local participants)
+    unsigned* d_pile_pairs = nullptr;  // packed candidate pairs (local shape slots, mg_internal.h)
+    int* d_pile_slots = nullptr;  // [..][2] local shape slots: participant, shape
 
     float* d_stage = nullptr;     // host-transfer staging (floats)
     size_t stage_n = 0;
@@ -396,7 +398,7 @@ void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls, s->d_shape_obb,
                     s->d_actor_root, s->d_root_row, s->d_slot_global, s->d_slot_actor, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
                     s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_chain_uni, s->d_fp_mask, s->d_env_carry, s->d_env_ctab, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
-                    s->d_pile_i, s->d_pile_body, s->d_pile_pairs, s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
+                    s->d_pile_i, s->d_pile_body, s->d_pile_pairs, s->d_pile_slots, s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -559,7 +561,11 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
     // pile envs (mg_pile.hip): rows with global body ids (converted below),
     // the free bodies, their candidate pairs
     std::vector<std::array<int, MG_PILE_I_N>> pile_rows;
-    std::vector<int> pile_body, pile_pairs;
+    std::vector<int> pile_body, pile_slots;
+    std::vector<unsigned> pile_pairs;
+    // envs built alike (the same shapes, filters and order) share one slot table
+    // and pair list: 4096 pyramids read one 2 KB list through L2
+    std::map<std::pair<std::vector<int>, std::vector<unsigned>>, std::pair<int, int>> pile_list_at;
     if (m->actor_coll && na > 0) {
         for (int a = 0; a + 1 < na; ++a)
             if (m->actor_root_body[a + 1] <= m->actor_root_body[a])
@@ -618,7 +624,6 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                 row.fill(0);
                 row[0] = (int)pile_body.size();
                 row[1] = (int)fr.size();
-                row[2] = (int)(pile_pairs.size() / 4);
                 row[4] = (int)stc.size();
                 for (size_t t = 0; t < stc.size(); ++t) row[5 + t] = m->actor_root_body[stc[t]];
                 for (int f : fr) {
@@ -631,33 +636,63 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
                     *s0 = t[0];
                     *ns = t[1];
                 };
+                // local shape slots: the free bodies' shapes in body order, then the statics'
+                std::vector<int> slots;
+                std::vector<int> first_slot(fr.size() + stc.size());
+                for (size_t k = 0; k < fr.size() + stc.size(); ++k) {
+                    const bool st = k >= fr.size();
+                    int sb0, nsb;
+                    shp(m->actor_root_body[st ? stc[k - fr.size()] : fr[k]], &sb0, &nsb);
+                    first_slot[k] = (int)slots.size() / 2;
+                    for (int sb = sb0; sb < sb0 + nsb; ++sb) {
+                        slots.push_back(st ? MG_PILE_ST0 + (int)(k - fr.size()) : (int)k);
+                        slots.push_back(sb);
+                    }
+                }
+                if ((int)slots.size() / 2 > MG_PILE_MAXSH)
+                    return fail(MG_ERR_UNSUPPORTED, "env %d: %zu collision shapes; a pile env supports %d", e,
+                                slots.size() / 2, MG_PILE_MAXSH);
+                std::vector<unsigned> plist;
                 for (int k = 0; k < (int)fr.size(); ++k) {
                     int sa0, nsa;
                     shp(m->actor_root_body[fr[k]], &sa0, &nsa);
                     for (int sa = sa0; sa < sa0 + nsa; ++sa) {
-                        auto push = [&](int b, int sb) {
-                            pile_pairs.push_back(k); pile_pairs.push_back(sa);
-                            pile_pairs.push_back(b); pile_pairs.push_back(sb);
+                        const unsigned la = (unsigned)(first_slot[k] + (sa - sa0));
+                        auto push = [&](int owner, int sb, int sb0) {
+                            plist.push_back(la | (unsigned)(first_slot[owner] + (sb - sb0)) << 8);
                         };
-                        if (ground) push(-1, -1);
+                        if (ground) plist.push_back(la | (unsigned)MG_PILE_GROUND << 8);
                         for (int t = 0; t < (int)stc.size(); ++t) {
                             if (!collide(fr[k], stc[t])) continue;
                             int sb0, nsb;
                             shp(m->actor_root_body[stc[t]], &sb0, &nsb);
-                            for (int sb = sb0; sb < sb0 + nsb; ++sb) push(MG_PILE_ST0 + t, sb);
+                            for (int sb = sb0; sb < sb0 + nsb; ++sb) push((int)fr.size() + t, sb, sb0);
                         }
                         for (int j = k + 1; j < (int)fr.size(); ++j) {
                             if (!collide(fr[k], fr[j])) continue;
                             int sb0, nsb;
                             shp(m->actor_root_body[fr[j]], &sb0, &nsb);
-                            for (int sb = sb0; sb < sb0 + nsb; ++sb) push(j, sb);
+                            for (int sb = sb0; sb < sb0 + nsb; ++sb) push(j, sb, sb0);
                         }
                     }
                 }
-                row[3] = (int)(pile_pairs.size() / 4) - row[2];
+                row[3] = (int)plist.size();
+                row[10] = (int)slots.size() / 2;
                 if (row[3] > MG_PILE_MAXPAIRS)
                     return fail(MG_ERR_UNSUPPORTED, "env %d: %d candidate shape pairs; a pile env supports %d", e,
                                 row[3], MG_PILE_MAXPAIRS);
+                auto key = std::make_pair(slots, plist);
+                auto it = pile_list_at.find(key);
+                if (it != pile_list_at.end()) {
+                    row[2] = it->second.first;
+                    row[9] = it->second.second;
+                } else {
+                    row[2] = (int)pile_pairs.size();
+                    row[9] = (int)pile_slots.size() / 2;
+                    pile_list_at.emplace(std::move(key), std::make_pair(row[2], row[9]));
+                    pile_pairs.insert(pile_pairs.end(), plist.begin(), plist.end());
+                    pile_slots.insert(pile_slots.end(), slots.begin(), slots.end());
+                }
                 pile_rows.push_back(row);
                 continue;
             }
@@ -1164,8 +1199,11 @@ int32_t mg_upload_model(mg_sim* s, const mg_model* m) {
         HIP_TRY(h2d(s->d_pile_i, flat.data(), flat.size() * sizeof(int)));
         HIP_TRY(dalloc(&s->d_pile_body, pile_body.size()));
         HIP_TRY(h2d(s->d_pile_body, pile_body.data(), pile_body.size() * sizeof(int)));
-        HIP_TRY(dalloc(&s->d_pile_pairs, std::max<size_t>(pile_pairs.size(), 4)));
-        if (!pile_pairs.empty()) HIP_TRY(h2d(s->d_pile_pairs, pile_pairs.data(), pile_pairs.size() * sizeof(int)));
+        HIP_TRY(dalloc(&s->d_pile_pairs, std::max<size_t>(pile_pairs.size(), 1)));
+        if (!pile_pairs.empty())
+            HIP_TRY(h2d(s->d_pile_pairs, pile_pairs.data(), pile_pairs.size() * sizeof(unsigned)));
+        HIP_TRY(dalloc(&s->d_pile_slots, std::max<size_t>(pile_slots.size(), 2)));
+        if (!pile_slots.empty()) HIP_TRY(h2d(s->d_pile_slots, pile_slots.data(), pile_slots.size() * sizeof(int)));
     }
     {   // no friction patch yet: every pair starts without anchors
         const size_t np = std::max<size_t>(pairs.size() / 4, 1), nm = (size_t)std::max(s->n_coupled, 1) * MG_FP_W;
@@ -1310,7 +1348,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     if (s->n_pile > 0) {
         MgPileArgs A{};
         A.ne = s->n_pile; A.nb = s->nb;
-        A.pile_i = s->d_pile_i; A.pile_body = s->d_pile_body; A.pairs = s->d_pile_pairs;
+        A.pile_i = s->d_pile_i; A.pile_body = s->d_pile_body; A.pairs = s->d_pile_pairs; A.slots = s->d_pile_slots;
         A.state = s->d_state; A.mass = s->d_mass; A.body_tmpl = s->d_body_tmpl; A.tbf = s->d_tbf;
         A.shapes = s->d_shapes; A.hulls = s->d_hulls; A.shape_obb = s->d_shape_obb;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
