@@ -159,3 +159,64 @@ def test_ball_pyramid_4096_gpu(gym):
             gym.refresh_rigid_body_state_tensor(sim)
             gym.refresh_net_contact_force_tensor(sim)
             _check(k, rb, ncf, st, cf)
+
+
+def test_piles_beside_other_env_kinds_gpu(gym):
+    """Pile envs in one sim with every other kind of env — coupled envs of
+    two free bodies (k_env_step), uncoupled free bodies (k_rigid_step1) and
+    fixed-base articulations (the chain kernel) — each stepped by its own
+    kernel over the shared SoA state: all bit-exact against the oracle."""
+    from test_isaacgym_amd import _native as N, scenes as SC
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, PS.sim_params(True))
+    plane = gymapi.PlaneParams()
+    plane.normal = gymapi.Vec3(0, 0, 1)
+    gym.add_ground(sim, plane)
+    ball = gym.create_sphere(sim, 0.05, gymapi.AssetOptions())
+    box = gym.create_box(sim, 0.1, 0.1, 0.1, gymapi.AssetOptions())
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    opts.default_dof_drive_mode = gymapi.DOF_MODE_POS
+    gimbal = gym.load_asset(sim, SC.ASSET_ROOT, "servo/gimbal.urdf", opts)
+    kinds = []
+    for i in range(24):
+        env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 6)
+        k = i % 4
+        kinds.append(k)
+        if k == 0:       # a pile: 5 balls in a column
+            for j in range(5):
+                gym.create_actor(env, ball, gymapi.Transform(gymapi.Vec3(0.01 * j, 0, 0.1 + 0.12 * j)), None, i, 0)
+        elif k == 1:     # two boxes, one on the other: a coupled env (k_env_step)
+            gym.create_actor(env, box, gymapi.Transform(gymapi.Vec3(0, 0, 0.05)), None, i, 0)
+            gym.create_actor(env, box, gymapi.Transform(gymapi.Vec3(0.02, 0, 0.2)), None, i, 0)
+        elif k == 2:     # free bodies that may not touch each other: uncoupled
+            for j in range(3):
+                gym.create_actor(env, box, gymapi.Transform(gymapi.Vec3(0.3 * j, 0, 0.3)), None, i, 1)
+        else:            # a fixed-base gimbal driven to a target
+            h = gym.create_actor(env, gimbal, gymapi.Transform(gymapi.Vec3(0, 2, 3)), None, i, 1)
+            props = gym.get_actor_dof_properties(env, h)
+            props["stiffness"][:] = 50.0
+            props["damping"][:] = 5.0
+            gym.set_actor_dof_properties(env, h, props)
+    gym.prepare_sim(sim)
+    assert N.lib.mg_num_pile_envs(sim.native) == 6
+    assert N.lib.mg_num_coupled_envs(sim.native) == 6             # k_env_step's envs (piles not counted)
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))
+    dofs = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    A = sim.model_arrays
+    st = A["body_state0"].copy()
+    dof = A["dof_state0"].copy()
+    nd = dof.shape[0]
+    tgt = np.zeros((nd, 3), np.float32)
+    tgt[:, 0] = np.tile(np.array([0.5, -0.4, 0.3], np.float32), nd // 3)
+    gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(torch.from_numpy(tgt[:, 0].copy()).cuda()))
+    for k in range(90):
+        gym.simulate(sim)
+        gym.fetch_results(sim, True)
+        cf = oracle.step(p, m, st, dof, tgt=tgt, props=A["dof_props"])
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_net_contact_force_tensor(sim)
+        gym.refresh_dof_state_tensor(sim)
+        _check(k, rb, ncf, st, cf)
+        assert np.array_equal(dofs.cpu().numpy(), dof), "frame %d: DOF state" % k
