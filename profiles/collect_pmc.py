@@ -30,7 +30,7 @@ def per_kernel(path, counter):
             continue
         name = r["Kernel_Name"]
         for key in ("k_rigid_step", "k_scatter_rows", "k_gather_rb_root", "k_gather_rows", "k_artic_step",
-                    "k_artic_chain", "k_env_step", "k_env_np"):
+                    "k_artic_chain", "k_env_step", "k_env_np", "k_pile_step"):
             if key in name:
                 name = key
         acc[name].append(float(r["Counter_Value"]))
