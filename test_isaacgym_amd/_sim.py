@@ -50,6 +50,38 @@ def _warn_multishape_friction(A):
               "plane (patch friction: single-shape free bodies and coupled envs; DESIGN.md §3.2.1)",
               file=sys.stderr)
 
+_warned_cross_env = [False]
+
+
+def _warn_cross_env_contacts(A):
+    """Contacts are simulated within an env only (every kernel steps an env on
+    its own): actors of different envs that share a collision
+    group (or use group -1) with filters that let them touch — e.g.
+    examples/1080_balls_of_solitude.py --all_collisions (group 0, filter 0) —
+    would collide in Isaac Gym once they meet. Said once, on stderr."""
+    if _warned_cross_env[0]:
+        return
+    ac = np.asarray(A["actor_coll"])
+    if len(ac) == 0:
+        return
+    env, grp, filt = ac[:, 0], ac[:, 1], ac[:, 2]
+    hit = False
+    # group -1 meets every group: its actors count with each group's
+    for g in np.unique(grp[grp >= 0]) if (grp >= 0).any() else [-1]:
+        sel = (grp == g) | (grp == -1)
+        if len(np.unique(env[sel])) > 1:
+            f = filt[sel]
+            # two of them may touch when some pair of filters shares no bit
+            uniq = np.unique(f)
+            if any((int(a) & int(b)) == 0 for i, a in enumerate(uniq) for b in uniq[i:]):
+                hit = True
+                break
+    if hit:
+        _warned_cross_env[0] = True
+        print("*** migym: actors of different envs share a collision group and may touch; contacts are simulated "
+              "within each env only (DESIGN.md §3.6, §6)", file=sys.stderr)
+
+
 class Env:
     __slots__ = ("sim", "index", "lower", "upper", "per_row", "origin", "actors", "num_bodies", "num_dofs",
                  "cameras")
@@ -489,6 +521,7 @@ class Sim:
             return
         A = self.build_model()
         _warn_multishape_friction(A)
+        _warn_cross_env_contacts(A)
         dev = self.device
         self.tensors["root"] = torch.from_numpy(A["body_state0"][A["actor_root_body"]].copy()).to(dev)
         self.tensors["rb"] = torch.from_numpy(A["body_state0"].copy()).to(dev)

@@ -217,3 +217,24 @@ def test_mixed_pile_settles(gym, tmp_path):
 
     _run(sim, 360, every=rec)
     assert all(b <= a * 1.001 for a, b in zip(ke, ke[1:])), ke
+
+
+def test_cross_env_collisions_are_warned(gym, capsys):
+    """--all_collisions (group 0, filter 0 in every env): Isaac Gym lets balls
+    of different envs collide; this build steps each env on its own and says
+    so once on stderr (the per-env modes stay silent)."""
+    from test_isaacgym_amd import _sim
+    _sim._warned_cross_env[0] = False
+    for mode, warned in (("env", False), ("none", False)):
+        sim, _ = scenes.ball_pile_scene(gym, 2, use_gpu_pipeline=False, mode=mode)
+        _sim._warn_cross_env_contacts(sim.build_model())
+        assert ("different envs" in capsys.readouterr().err) == warned
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, scenes.ball_pile_sim_params(False))
+    gym.add_ground(sim, gymapi.PlaneParams())
+    ball = gym.create_sphere(sim, 0.1, gymapi.AssetOptions())
+    for i in range(2):
+        env = gym.create_env(sim, gymapi.Vec3(-1, 0, -1), gymapi.Vec3(1, 1, 1), 2)
+        for k in range(3):
+            gym.create_actor(env, ball, gymapi.Transform(gymapi.Vec3(0.3 * k, 1, 0)), None, 0, 0)
+    _sim._warn_cross_env_contacts(sim.build_model())
+    assert "different envs" in capsys.readouterr().err
