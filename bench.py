@@ -816,7 +816,8 @@ def s1_cpu_pipeline_rate(n, steps, warmup):
     el = time.perf_counter() - t0
     gym.destroy_sim(sim)
     return {"envs": n, "env_steps_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps, "steps": steps,
-            "pipeline": "CPU (host state tensors, H2D set / D2H refresh, fetch_results(sim, True))",
+            "pipeline": "CPU (host state tensors: H2D set; fetch_results(sim, True) stages the refreshed kinds in one "
+                        "D2H round trip, mg_fetch_host_state; the refreshes copy from it)",
             "timed_loop": "eager Python loop (host tensors)",
             "bytes_over_pcie_per_step": n * 2 * 13 * 4 * 3}
 

@@ -199,6 +199,16 @@ int32_t     mg_upload_model(mg_sim* sim, const mg_model* model);
 int32_t     mg_simulate(mg_sim* sim, void* stream);
 /* gym.fetch_results(sim, wait) (:381): waits for the last simulate when wait. */
 int32_t     mg_fetch_results(mg_sim* sim, int32_t wait);
+/* gym.fetch_results(sim, True) in the CPU pipeline (test10_servo_vecenv.py:381,
+ * host state tensors): waits for the last simulate and copies the current state
+ * into one host buffer with a single synchronisation. Layout of dst (tensor row
+ * orders): [na][13] actor roots, [nb][13] rigid bodies, [nd][2] DOF states,
+ * [nb][3] net contact forces; `parts` bit k asks for part k (0 roots, 1 rigid
+ * bodies, 2 DOFs, 3 contact forces; 0: wait only). The refresh_*_tensor calls
+ * that follow (:394-396) are then host copies from it while no simulate or state
+ * set intervenes (the Python layer tracks that), instead of a device round trip
+ * each. Not while the stream is being captured. */
+int32_t     mg_fetch_host_state(mg_sim* sim, float* dst, int32_t parts, void* stream);
 
 /* ---- tensor API: refresh (state -> user tensor) ----------------------------
  * gym.refresh_actor_root_state_tensor (:394), refresh_rigid_body_state_tensor

@@ -198,6 +198,13 @@ class Sim:
         # state epoch: bumped by simulate and every state setter; the mass matrix
         # computed alongside the Jacobian is reused while the epoch is unchanged
         self.epoch = 0
+        # CPU pipeline: the host state staged by fetch_results(sim, True) and the
+        # epoch it belongs to (gymapi.Gym._refresh serves refreshes from it)
+        self.host_stage = None
+        self.host_stage_offsets = {}
+        self.host_stage_epoch = -1
+        self.host_stage_parts = 0      # kinds refreshed so far: staged by the next waiting fetch
+        self.host_staged = 0           # kinds the last waiting fetch staged
         self.held_src = []     # fused sets: (tensor, torch version at the set, setter), until the next simulate
         # step fusion (gym.set_step_fusion; opt-in, MIGYM_STEP_FUSION sets the default)
         self.fusion = int(os.environ.get("MIGYM_STEP_FUSION", "0") or 0) & 31
@@ -533,6 +540,12 @@ class Sim:
             # straight over PCIe instead of through the runtime's staging buffer
             for k in ("root", "rb", "dof", "ncf"):
                 self.tensors[k] = self.tensors[k].pin_memory()
+            # fetch_results(sim, True) stages the whole state here in one round
+            # trip (mg_fetch_host_state); the refreshes copy from it
+            sizes = [self.tensors[k].numel() for k in ("root", "rb", "dof", "ncf")]
+            offs = np.cumsum([0] + sizes)
+            self.host_stage_offsets = {k: int(offs[i]) for i, k in enumerate(("root", "rb", "dof", "ncf"))}
+            self.host_stage = torch.empty(int(offs[-1]), dtype=torch.float32).pin_memory()
         if N.device_count() > 0:
             handle = N.lib.mg_create_sim(self.compute_device, ctypes.byref(self.mg_params()))
             if not handle:

@@ -1419,6 +1419,41 @@ int32_t mg_fetch_results(mg_sim* s, int32_t wait) {
     return MG_OK;
 }
 
+int32_t mg_fetch_host_state(mg_sim* s, float* dst, int32_t parts, void* stream) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    if (!s->uploaded) return fail(MG_ERR_STATE, "sim has no uploaded model");
+    if (!dst && parts) return fail(MG_ERR_ARG, "null destination");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(s->device));
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(st, &cap));
+    if (cap != hipStreamCaptureStatusNone) return fail(MG_ERR_STATE, "mg_fetch_host_state while capturing");
+    if (int rc_ = flush_root(s, st)) return rc_;
+    // [na][13] roots, [nb][13] bodies, [nd][2] DOFs, [nb][3] contact forces; the
+    // parts asked for are gathered and the span covering them copied at once
+    const size_t off[5] = {0, (size_t)s->na * MG_STATE_N, (size_t)(s->na + s->nb) * MG_STATE_N,
+                           (size_t)(s->na + s->nb) * MG_STATE_N + (size_t)s->nd * 2,
+                           (size_t)(s->na + s->nb) * MG_STATE_N + (size_t)s->nd * 2 + (size_t)s->nb * 3};
+    int rc = ensure_stage(s, off[4], 0);
+    if (rc) return rc;
+    int lo = -1, hi = -1;
+    for (int k = 0; k < 4; ++k) {
+        if (!((parts >> k) & 1) || off[k + 1] == off[k]) continue;
+        if (lo < 0) lo = k;
+        hi = k;
+        float* d = s->d_stage + off[k];
+        if (k == 0) HIP_TRY(mg_launch_gather_rows(s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, d, st));
+        if (k == 1) HIP_TRY(mg_launch_gather_rows(s->d_state, s->nb, MG_STATE_N, s->d_perm, s->nb, d, st));
+        if (k == 2) HIP_TRY(mg_launch_gather_rows(s->d_dof, s->nd, 2, nullptr, s->nd, d, st));
+        if (k == 3) HIP_TRY(mg_launch_gather_rows(s->d_cforce, s->nb, 3, s->d_perm, s->nb, d, st));
+    }
+    if (lo >= 0)
+        HIP_TRY(hipMemcpyAsync(dst + off[lo], s->d_stage + off[lo], (off[hi + 1] - off[lo]) * sizeof(float),
+                               hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return MG_OK;
+}
+
 int32_t mg_set_fusion(mg_sim* s, int32_t flags) {
     if (!s) return fail(MG_ERR_ARG, "null sim");
     const int32_t prev = s->fusion;

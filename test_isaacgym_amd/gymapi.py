@@ -104,6 +104,10 @@ def _check_held(sim, what, kinds=None):
     sim.held_src = keep
 
 
+# mg_fetch_host_state part bits of the state tensors
+_STAGE_BIT = {"root": 1, "rb": 2, "dof": 4, "ncf": 8}
+
+
 class Gym:
     def __init__(self):
         self._sims = []
@@ -184,8 +188,20 @@ class Gym:
         return sim.fusion
 
     def fetch_results(self, sim, wait=True):
+        """test10_servo_vecenv.py:381. In the CPU pipeline a waiting fetch also
+        stages the state kinds refreshed so far (one device round trip), so the
+        refreshes after it are host copies (include/migym.h mg_fetch_host_state)."""
         if sim.native:
-            N.check(N.lib.mg_fetch_results(sim.native, 1 if wait else 0), "mg_fetch_results")
+            if wait and sim.host_stage is not None:
+                # CPU pipeline: the state the refreshes will copy — the kinds
+                # refreshed so far — staged in one device round trip
+                # (mg_fetch_host_state) as the wait
+                N.check(N.lib.mg_fetch_host_state(sim.native, sim.host_stage.data_ptr(), sim.host_stage_parts,
+                                                  sim.stream()), "mg_fetch_host_state")
+                sim.host_stage_epoch = sim.epoch
+                sim.host_staged = sim.host_stage_parts
+            else:
+                N.check(N.lib.mg_fetch_results(sim.native, 1 if wait else 0), "mg_fetch_results")
         return True
 
     def get_sim_time(self, sim):
@@ -862,7 +878,16 @@ class Gym:
                     "mg_bind_refresh_targets")
         if key == "dof" and sim.dof_out_version is not None and t._version != sim.dof_out_version:
             N.check(N.lib.mg_bind_dof_refresh_target(h, t.data_ptr()), "mg_bind_dof_refresh_target")
-        N.check(fn(h, t.data_ptr(), 1 if t.device.type == "cpu" else 0, sim.stream()), what)
+        bit = _STAGE_BIT[key]
+        if t.device.type == "cpu" and sim.host_stage_epoch == sim.epoch and sim.host_staged & bit:
+            # CPU pipeline after fetch_results(sim, True): no simulate and no
+            # state set since the staged copy — a host copy, no device round trip
+            o = sim.host_stage_offsets[key]
+            t.view(-1).copy_(sim.host_stage[o:o + t.numel()])
+        else:
+            N.check(fn(h, t.data_ptr(), 1 if t.device.type == "cpu" else 0, sim.stream()), what)
+            if t.device.type == "cpu":
+                sim.host_stage_parts |= bit      # stage this kind at the next fetch_results(sim, True)
         # the tensor now holds the sim state, whether this refresh launched a
         # gather or was served by the step / the paired gather: a later in-place
         # write makes the next refresh rebind and gather again, as Isaac Gym's

@@ -1,0 +1,57 @@
+"""test10_servo_vecenv.py's own mode, the CPU pipeline (host state tensors,
+SURVEY.md §0.7, BASELINE config 2), on the device: fetch_results(sim, True)
+stages the whole state in one round trip (mg_fetch_host_state) and the
+refresh_*_tensor calls that follow copy from it — unless a simulate or a
+state set intervened, which sends the refresh back to the device. Checked bit
+for bit against the oracle every step, including a set between fetch and
+refresh (the refresh must show the set's state, not the staged one)."""
+import numpy as np
+import pytest
+import torch
+
+from isaacgym import gymapi, gymtorch
+from test_isaacgym_amd import scenes
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def test_cpu_pipeline_staged_refreshes_gpu(gym):
+    n = 256
+    sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=False)
+    gym.prepare_sim(sim)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    ncf = gymtorch.wrap_tensor(gym.acquire_net_contact_force_tensor(sim))
+    assert root.device.type == "cpu" and sim.host_stage is not None
+    p, m = sim.mg_params(), sim.mg_model()
+    A = sim.model_arrays
+    st = A["body_state0"].copy()
+    dof = A["dof_state0"].copy()
+    roots = A["actor_root_body"]
+    acts = scenes.servo_actions(n, 8, "cpu", seed=4)
+    gym.refresh_actor_root_state_tensor(sim)
+    for k in range(40):
+        root[:, 3:10] = acts[k % 8]
+        assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        st[roots, 3:10] = acts[k % 8].numpy()
+        gym.simulate(sim)
+        gym.fetch_results(sim, True)
+        cf = oracle.step(p, m, st, dof)
+        assert sim.host_stage_epoch == sim.epoch
+        if k % 10 == 5:
+            # a set between fetch and refresh (every root from the host tensor,
+            # still holding the previous refresh, one of them moved): the
+            # refresh shows the set's state, not the staged one
+            root[0, 0:3] = torch.tensor([1.0, 2.0, 150.0])
+            assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+            st[roots] = root.numpy()
+            assert sim.host_stage_epoch != sim.epoch
+        gym.refresh_actor_root_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        gym.refresh_net_contact_force_tensor(sim)
+        gym.refresh_dof_state_tensor(sim)
+        assert np.array_equal(rb.numpy(), st), "step %d: rigid-body tensor" % k
+        assert np.array_equal(root.numpy(), st[roots]), "step %d: root tensor" % k
+        if k % 10 != 5:
+            assert np.array_equal(ncf.numpy(), cf), "step %d: net contact force" % k
