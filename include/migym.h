@@ -54,15 +54,14 @@ extern "C" {
  * (x, y, z), then nf face planes (n.x, n.y, n.z, d) with unit outward n and
  * n . x <= d inside, then ne edges (vertex index pairs; ne <= 3 MG_HULL_MAX_VERTS) */
 #define MG_HULL_HEADER     4
-/* the caps are the importer's defaults (test_isaacgym_amd/_assets.py); a build may
- * raise them (-DMG_HULL_MAX_VERTS=128 -DMG_HULL_MAX_FACES=256: the finer-hull
- * measurement of DESIGN.md §5, round 6) with the importer's caps raised to match */
-#ifndef MG_HULL_MAX_VERTS
-#define MG_HULL_MAX_VERTS 32
-#endif
-#ifndef MG_HULL_MAX_FACES
-#define MG_HULL_MAX_FACES 64
-#endif
+/* the library's caps are PhysX's convex-mesh cooking limits (255 vertices, 255
+ * polygons); the importer reduces a collision mesh to 32 vertices / 64 faces by
+ * default (test_isaacgym_amd/_assets.py, MIGYM_HULL_CAPS raises that per mesh).
+ * The per-env narrow phase walks a hull's vertices and edges in chunks (32
+ * vertices / 96 edges on 16 lanes), so a hull past the importer's default costs
+ * more chunks, not a rebuild. */
+#define MG_HULL_MAX_VERTS 255
+#define MG_HULL_MAX_FACES 255
 
 /* body kinds (mg_model.body_kind) */
 #define MG_BODY_FREE      0   /* single-body dynamic actor: free-body kernel */

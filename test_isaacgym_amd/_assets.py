@@ -20,8 +20,8 @@ Reference behaviour this mirrors (SURVEY.md §2 "URDF/MJCF/mesh importer", §8a 
     vehicle, assets/urdf/uav/urdf/rq-1-predator-mae-uav.urdf:4-7) keeps the mass
     and takes the shape inertia scaled to it.
 Meshes: a collision mesh that exists becomes its convex hull (MG_SHAPE_CONVEX,
-as PhysX cooks a convex mesh from it), reduced to at most MG_HULL_MAX_VERTS
-vertices by farthest-point sampling of the hull vertices; its mass properties
+as PhysX cooks a convex mesh from it), reduced to at most HULL_MAX_VERTS (32;
+MIGYM_HULL_CAPS per mesh, up to PhysX's 255) vertices by farthest-point sampling of the hull vertices; its mass properties
 are the hull's at AssetOptions.density. The servo scene's two meshes are missing
 from the reference (.MISSING_LARGE_BLOBS:7-8); they get the frozen box proxies
 of MESH_PROXIES, expressed in the body frame.
@@ -43,16 +43,17 @@ MESH_PROXIES = {
 
 SPHERE, BOX, CAPSULE, CONVEX = 0, 1, 2, 3
 MJCF_MAX_JOINT_VELOCITY = 100.0      # PhysX's default articulation joint speed limit (rad/s, m/s)
-HULL_MAX_VERTS, HULL_MAX_FACES = 32, 64          # MG_HULL_MAX_VERTS / _FACES (include/migym.h)
-# Per-mesh caps for measurements with a library built with larger MG_HULL_MAX_*
-# (the Franka hand at 64 vertices and at its full 102):
-# MIGYM_HULL_CAPS="hand.obj=64/128,finger.obj=128/256" (mesh file name =
-# vertices / faces). Unset: every mesh at the defaults above.
+# the importer's default hull size; the library takes hulls up to PhysX's own
+# limits (255 vertices / 255 faces: MG_HULL_MAX_VERTS / _FACES, include/migym.h)
+HULL_MAX_VERTS, HULL_MAX_FACES = 32, 64
+# Per-mesh caps (the Franka hand at 64 vertices and at its
+# full 102): MIGYM_HULL_CAPS="hand.obj=64/128,finger.obj=128/255" (mesh file
+# name = vertices / faces, each at most 255). Unset: every mesh at the defaults.
 HULL_CAPS = {}
 for _item in filter(None, os.environ.get("MIGYM_HULL_CAPS", "").split(",")):
     _name, _caps = _item.split("=")
     _v, _f = _caps.split("/")
-    HULL_CAPS[_name.strip()] = (int(_v), int(_f))
+    HULL_CAPS[_name.strip()] = (min(int(_v), 255), min(int(_f), 255))
 
 
 def _quat_from_rpy(r, p, y):

@@ -30,7 +30,7 @@ MG_ATMPL_I_N = 4
 MG_ACOLL_N = 4
 
 MG_SHAPE_SPHERE, MG_SHAPE_BOX, MG_SHAPE_CAPSULE, MG_SHAPE_CONVEX = 0, 1, 2, 3
-MG_HULL_HEADER, MG_HULL_MAX_VERTS, MG_HULL_MAX_FACES = 4, 32, 64   # include/migym.h defaults
+MG_HULL_HEADER, MG_HULL_MAX_VERTS, MG_HULL_MAX_FACES = 4, 255, 255   # include/migym.h
 MG_BODY_FREE, MG_BODY_STATIC, MG_BODY_LINK = 0, 1, 2
 
 _f32p = ctypes.POINTER(ctypes.c_float)

@@ -331,10 +331,19 @@ __device__ __forceinline__ unsigned long long grp_ballot(bool b, int gi) {
     if constexpr (G == 64) return __ballot(b);
     return (__ballot(b) >> (gi * G)) & 0xFFFFull;
 }
+// the cooperative hull loops' chunk: MG_NP_HULL_CHUNK vertices (3x as many
+// edges) per pass of the group, the importer's default hull in one pass; a finer
+// hull (up to MG_HULL_MAX_VERTS) takes more passes, in index order
+#ifndef MG_NP_HULL_CHUNK
+#define MG_NP_HULL_CHUNK 32
+#endif
+// B's vertex candidates order after every vertex of A (coop_convex_convex)
+#define MG_NP_BVERT_ORDER 256
+static_assert(MG_NP_BVERT_ORDER > MG_HULL_MAX_VERTS, "vertex order keys of A and B overlap");
 // X's edges against Y on the group, into each lane's queue (order = edge index).
-// A lane's edges (e = ln + 16 k, at most 3 MG_HULL_MAX_VERTS / 16 = 6) in two
-// batches of 3: all the batch's edge ids, then all its endpoints are loaded
-// before any is tested (two dependent round trips per batch, not two per edge)
+// A lane's edges (e = base + ln + G k, 6 per chunk on 16 lanes) in batches of
+// 3: all the batch's edge ids, then all its endpoints are loaded before any is
+// tested (two dependent round trips per batch, not two per edge)
 template <int G>
 __device__ __forceinline__ void coop_edges(const CShape& X, const CShape& Y, float margin, bool onY, V3 lo, V3 hi,
                                            int ln, CandQ& Q) {
@@ -343,62 +352,66 @@ __device__ __forceinline__ void coop_edges(const CShape& X, const CShape& Y, flo
     float ry;
     if (!cvx_edges_gate(X, Y, margin, lo, hi, t, M, ry)) return;
     const int ne = cvx_ne(X);
-    constexpr int CE_PER_LANE = (3 * MG_HULL_MAX_VERTS + G - 1) / G;
+    constexpr int CE_PER_LANE = (3 * MG_NP_HULL_CHUNK + G - 1) / G;
+    for (int base = 0; base < ne; base += G * CE_PER_LANE) {
 #pragma unroll
-    for (int k0 = 0; k0 < CE_PER_LANE; k0 += 3) {
-        if (ln + G * k0 >= ne) break;
-        int ia[3], ib[3];
-        V3 la[3], lb[3];
+        for (int k0 = 0; k0 < CE_PER_LANE; k0 += 3) {
+            if (base + ln + G * k0 >= ne) break;
+            int ia[3], ib[3];
+            V3 la[3], lb[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int e = ln + G * (k0 + k);
-            cvx_edge_ids(X, e < ne ? e : ne - 1, ia[k], ib[k]);
-        }
+            for (int k = 0; k < 3; ++k) {
+                const int e = base + ln + G * (k0 + k);
+                cvx_edge_ids(X, e < ne ? e : ne - 1, ia[k], ib[k]);
+            }
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            la[k] = cvx_vertex_l(X, ia[k]);
-            lb[k] = cvx_vertex_l(X, ib[k]);
-        }
+            for (int k = 0; k < 3; ++k) {
+                la[k] = cvx_vertex_l(X, ia[k]);
+                lb[k] = cvx_vertex_l(X, ib[k]);
+            }
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int e = ln + G * (k0 + k);
-            if (e < ne) {
-                Deep4 T;
-                T.n = 0;
-                cvx_edge_one(Y, margin, onY, t, M, ry, la[k], lb[k], T);
-                if (T.n) candq_add(Q, T.s[0], e, T.p[0], T.nrm[0]);
+            for (int k = 0; k < 3; ++k) {
+                const int e = base + ln + G * (k0 + k);
+                if (e < ne) {
+                    Deep4 T;
+                    T.n = 0;
+                    cvx_edge_one(Y, margin, onY, t, M, ry, la[k], lb[k], T);
+                    if (T.n) candq_add(Q, T.s[0], e, T.p[0], T.nrm[0]);
+                }
             }
         }
     }
 }
-// X's vertices (i = ln + G k, at most MG_HULL_MAX_VERTS / G per lane: 2 at the
-// default 32-vertex cap on 16 lanes) against Y's planes, into the lane's queue
-// (order idbase + i); all the lane's vertices loaded before any is tested.
-// (Round 6: the bound was a literal 2, so a build with a larger vertex cap
-// skipped the vertices past 32 G / 16 while the oracle tested them.)
+// X's vertices (i = base + ln + G k: 2 per lane per chunk on 16 lanes) against
+// Y's planes, into the lane's queue (order idbase + i); all the chunk's vertices
+// loaded before any is tested. (Round 6: the bound was a literal 2, so a build
+// with a larger vertex cap skipped the vertices past 32 while the oracle tested
+// them; now any hull up to MG_HULL_MAX_VERTS, chunk by chunk.)
 template <int G>
 __device__ __forceinline__ void coop_vertices(const CShape& X, const CShape& Y, float margin, bool onY, int idbase,
                                               int ln, CandQ& Q, V3& lo, V3& hi) {
-    constexpr int CV_PER_LANE = (MG_HULL_MAX_VERTS + G - 1) / G;
+    constexpr int CV_PER_LANE = (MG_NP_HULL_CHUNK + G - 1) / G;
     const int nv = cvx_nv(X);
-    V3 vw[CV_PER_LANE];
+    for (int base = 0; base < nv; base += G * CV_PER_LANE) {
+        V3 vw[CV_PER_LANE];
 #pragma unroll
-    for (int k = 0; k < CV_PER_LANE; ++k) {
-        const int i = ln + G * k;
-        vw[k] = cvx_vertex(X, i < nv ? i : nv - 1);
-    }
+        for (int k = 0; k < CV_PER_LANE; ++k) {
+            const int i = base + ln + G * k;
+            vw[k] = cvx_vertex(X, i < nv ? i : nv - 1);
+        }
 #pragma unroll
-    for (int k = 0; k < CV_PER_LANE; ++k) {
-        const int i = ln + G * k;
-        if (i < nv) {
-            const V3 v = vw[k];
-            aabb_add(lo, hi, mtmul(Y.R, vsub(v, Y.c)));
-            int f;
-            const float sv = cvx_sd(Y, v, f, 0.0f, margin);     // cvx_vertex_one's candidate
-            if (sv < margin) {
-                const V3 n = cvx_normal(Y, f);
-                if (onY) candq_add(Q, sv, idbase + i, vsub(v, vscale(n, sv)), vscale(n, -1.0f));
-                else candq_add(Q, sv, idbase + i, v, n);
+        for (int k = 0; k < CV_PER_LANE; ++k) {
+            const int i = base + ln + G * k;
+            if (i < nv) {
+                const V3 v = vw[k];
+                aabb_add(lo, hi, mtmul(Y.R, vsub(v, Y.c)));
+                int f;
+                const float sv = cvx_sd(Y, v, f, 0.0f, margin);     // cvx_vertex_one's candidate
+                if (sv < margin) {
+                    const V3 n = cvx_normal(Y, f);
+                    if (onY) candq_add(Q, sv, idbase + i, vsub(v, vscale(n, sv)), vscale(n, -1.0f));
+                    else candq_add(Q, sv, idbase + i, v, n);
+                }
             }
         }
     }
@@ -414,7 +427,7 @@ __device__ __forceinline__ void coop_convex_convex(const CShape& A, const CShape
     Q.n = 0;
     V3 loA = v3(1e30f, 1e30f, 1e30f), hiA = v3(-1e30f, -1e30f, -1e30f), loB = loA, hiB = hiA;
     coop_vertices<G>(A, B, margin, false, 0, ln, Q, loA, hiA);     // A's vertices by B's planes
-    coop_vertices<G>(B, A, margin, true, 64, ln, Q, loB, hiB);     // B's vertices by A's planes
+    coop_vertices<G>(B, A, margin, true, MG_NP_BVERT_ORDER, ln, Q, loB, hiB);     // B's vertices by A's planes
     PH_SUB(12);
     if (grp_ballot<G>(Q.n > 0, gi) == 0ull) {
         // no vertex candidate: edge crossings (convex_convex's order of passes)
