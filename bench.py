@@ -1064,23 +1064,43 @@ def main():
         if gather_leg:
             out["allgather"] = gather_leg
     if world == 1:
+        # the secondary legs, each announced on stderr with its wall time (the one
+        # JSON line stays the only stdout; a long default run keeps printing)
+        legs = []
         if not args.no_large_n:
-            out["large_n"] = large_n_rate(args.large_n, 64, dev, not args.eager)
+            legs.append(("large_n", lambda: large_n_rate(args.large_n, 64, dev, not args.eager)))
         if not args.no_default_legs:
-            out["s1_default"] = s1_rate(ENVS_PER_GPU, min(args.steps, 300), dev, not args.eager, fused=False, seed=3)
-            out["s1_cpu_pipeline"] = s1_cpu_pipeline_rate(1024, 100, 10)
+            legs.append(("s1_default", lambda: s1_rate(ENVS_PER_GPU, min(args.steps, 300), dev, not args.eager,
+                                                       fused=False, seed=3)))
+            legs.append(("s1_cpu_pipeline", lambda: s1_cpu_pipeline_rate(1024, 100, 10)))
         if not args.no_gimbal:
-            out["s2_servo_arm"] = gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
+            legs.append(("s2_servo_arm", lambda: gimbal_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev,
+                                                             not args.eager)))
             if not args.no_large_n:
-                out["s2_servo_arm"]["large_n"] = gimbal_rate(S2_LARGE_N, 64, 10, dev, not args.eager)
+                legs.append(("s2_servo_arm.large_n", lambda: gimbal_rate(S2_LARGE_N, 64, 10, dev, not args.eager)))
         if not args.no_franka:
-            out["s3_franka"] = franka_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev, not args.eager)
+            legs.append(("s3_franka", lambda: franka_rate(ENVS_PER_GPU, min(args.steps, 300), 30, dev,
+                                                          not args.eager)))
         if not args.no_cameras:
-            out["s5_cameras"] = camera_rate(args.camera_envs, min(args.steps, 100), 10, dev, not args.eager)
+            legs.append(("s5_cameras", lambda: camera_rate(args.camera_envs, min(args.steps, 100), 10, dev,
+                                                           not args.eager)))
         if not args.no_piles:
-            out["s6_piles"] = pile_rate(args.pile_envs, min(args.steps, 300), 90, dev, not args.eager)
+            legs.append(("s6_piles", lambda: pile_rate(args.pile_envs, min(args.steps, 300), 90, dev,
+                                                       not args.eager)))
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            legs.append(("cpu_baseline", lambda: cpu_baseline(args.cpu_seconds)))
+        leg_s = {}
+        for name, fn in legs:
+            t_leg = time.perf_counter()
+            res = fn()
+            if "." in name:
+                a, b = name.split(".")
+                out[a][b] = res
+            else:
+                out[name] = res
+            leg_s[name] = round(time.perf_counter() - t_leg, 2)
+            print("bench: %s done in %.1f s" % (name, leg_s[name]), file=sys.stderr, flush=True)
+        out["leg_wall_s"] = leg_s
     if rank == 0:
         print(json.dumps(out), flush=True)
     gym.destroy_sim(sim)
