@@ -9,7 +9,11 @@ bank's rows for its envs and steps `frames` frames through the gymapi tensor
 API (test10_servo_vecenv.py:376-456), then the ranks all-gather their root and
 rigid-body state tensors and rank 0 saves them to <out>_root.npy / <out>_rb.npy.
 
-usage: _shard_worker_gpu.py <envs per rank> <frames> <out prefix>
+With backend "nccl" (one rank only: RCCL refuses two ranks on one device) the
+same job runs over RCCL, so sharding.all_gather_rows takes its device branch
+(all_gather_into_tensor), the one the 8-GPU node runs.
+
+usage: _shard_worker_gpu.py <envs per rank> <frames> <out prefix> [gloo|nccl]
 """
 import os
 import sys
@@ -24,9 +28,14 @@ import torch.distributed as dist  # noqa: E402
 
 def main():
     n, frames, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
+    backend = sys.argv[4] if len(sys.argv) > 4 else "gloo"
     torch.cuda.set_device(0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo")
+    assert dist.get_backend() == backend
+    rank, world = dist.get_rank(), dist.get_world_size()
     from isaacgym import gymapi, gymtorch
     from test_isaacgym_amd import scenes, sharding
     gym = gymapi.acquire_gym()

@@ -56,6 +56,25 @@ def test_config4_sharded_equals_single_sim(tmp_path):
     assert np.array_equal(g_rb, want_rb), "rb max |diff| %g" % np.abs(g_rb - want_rb).max()
 
 
+def test_config4_rccl_rank_equals_single_sim(tmp_path):
+    """The RCCL path of the sharded job: one rank over backend "nccl" (RCCL
+    allows one rank per device, and the box has one), so the all-gather of
+    the root / rigid-body tensors goes through all_gather_into_tensor on the
+    device (sharding.all_gather_rows' RCCL branch, what config 4 runs on the
+    8-GPU node). 4096 envs, 20 frames: equal to one sim, bit for bit."""
+    out = str(tmp_path / "rccl")
+    n, frames = ENVS_PER_RANK, 20
+    rc, codes = launch.spawn_ranks([os.path.join(HERE, "_shard_worker_gpu.py"), str(n), str(frames), out, "nccl"],
+                                   1, timeout=300)
+    assert rc == 0, codes
+    g_root, g_rb = np.load(out + "_root.npy"), np.load(out + "_rb.npy")
+    gym = gymapi.acquire_gym()
+    sim, root, rb = _single_sim(gym, n, frames)
+    want_root, want_rb = root.cpu().numpy(), rb.cpu().numpy()
+    gym.destroy_sim(sim)
+    assert np.array_equal(g_root, want_root) and np.array_equal(g_rb, want_rb)
+
+
 def test_config4_single_sim_step_matches_oracle():
     """32768 envs (65536 bodies, 1024 waves of k_rigid_step1): 5 frames of
     random teleports from the initial state, the oracle stepping alongside (its

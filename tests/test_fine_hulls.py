@@ -12,7 +12,9 @@ edges past the first chunk, and the vertex tests cover both hulls past index
 64 (the old order key of B's vertices); it comes to rest crosswise. The importer's caps are raised
 for the two meshes (test_isaacgym_amd/_assets.py HULL_CAPS, MIGYM_HULL_CAPS).
 CPU: the importer keeps every vertex and the oracle's prism lands on the other
-one; GPU: k_env_np / k_env_step bit for bit the oracle, 64 envs.
+one; GPU: k_env_np / k_env_step bit for bit the oracle, 64 envs. And a pile
+(mg_pile.hip, serial hull tests per pair): three free 200-vertex prisms
+stacked crosswise on the 240-vertex one, bit for bit.
 """
 import math
 import os
@@ -49,7 +51,7 @@ def fine_caps(monkeypatch):
     monkeypatch.setitem(_assets.HULL_CAPS, "rod_b.obj", (255, 255))
 
 
-def _scene(gym, d, n, gpu, seed=0):
+def _scene(gym, d, n, gpu, seed=0, stack=1):
     sp = gymapi.SimParams()
     sp.up_axis = gymapi.UP_AXIS_Z
     sp.gravity = gymapi.Vec3(0, 0, -9.8)
@@ -73,8 +75,11 @@ def _scene(gym, d, n, gpu, seed=0):
         env = gym.create_env(sim, gymapi.Vec3(-0.5, -0.5, 0), gymapi.Vec3(0.5, 0.5, 1), 8)
         dx, dy = (rng.uniform(-0.01, 0.01, size=2) if i else (0.0, 0.0))
         gym.create_actor(env, base, gymapi.Transform(gymapi.Vec3(0, 0, 0.2), gymapi.Quat()), "base", i, 0)
-        gym.create_actor(env, rod, gymapi.Transform(gymapi.Vec3(dx, dy, 0.2 + 2 * R + 0.02), gymapi.Quat()),
-                         "rod", i, 0)
+        for k in range(stack):
+            # stack > 1: alternately crosswise (a quarter turn about z every other rod)
+            q = gymapi.Quat.from_axis_angle(gymapi.Vec3(0, 0, 1), 0.5 * math.pi * (k % 2))
+            gym.create_actor(env, rod, gymapi.Transform(gymapi.Vec3(dx, dy, 0.2 + 2 * R * (k + 1) + 0.02 * (k + 1)), q),
+                             "rod%d" % k, i, 0)
     return sim, base, rod
 
 
@@ -124,3 +129,29 @@ def test_fine_hulls_parity_gpu(gym, tmp_path, fine_caps):
             assert np.array_equal(got, st), "frame %d: max |diff| %g" % (f, np.abs(got - st).max())
     gym.refresh_net_contact_force_tensor(sim)
     assert np.array_equal(ncf.cpu().numpy(), cf)
+
+
+@pytest.mark.gpu
+def test_fine_hulls_pile_parity_gpu(gym, tmp_path, fine_caps):
+    """The pile step (k_pile_step: more than two free bodies, no articulation)
+    with 200- / 240-vertex hulls: 64 envs of three prisms dropped in a
+    crosswise stack on the fixed one, 90 frames, bit for bit the oracle."""
+    from test_isaacgym_amd import _native as N
+    n, steps = 64, 90
+    sim, *_ = _scene(gym, str(tmp_path), n, True, seed=5, stack=3)
+    gym.prepare_sim(sim)
+    assert N.lib.mg_num_pile_envs(sim.native) == n
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    st = sim.model_arrays["body_state0"].copy()
+    for f in range(steps):
+        gym.simulate(sim)
+        oracle.step(p, m, st, np.zeros((0, 2), np.float32))
+        if f % 15 == 14 or f == steps - 1:
+            gym.refresh_rigid_body_state_tensor(sim)
+            got = rb.cpu().numpy()
+            assert np.all(np.isfinite(got))
+            assert np.array_equal(got, st), "frame %d: max |diff| %g" % (f, np.abs(got - st).max())
+    # the stack topples onto the ground (rounding), but no rod passes into it
+    rods = np.arange(st.shape[0]) % 4 != 0
+    assert np.all(st[rods, 2] > R - 0.003)
