@@ -75,7 +75,7 @@ if has pmc; then
   # FETCH_SIZE and WRITE_SIZE in separate runs (one counter block each, no trace
   # domains combined); profiles/collect_pmc.py turns the CSVs into per-launch bytes
   for n in ${PMC_SIZES:-4096 262144}; do
-    B="python bench.py --envs $n --steps 48 --warmup 5 --repeats 1 --pmc-calibrate --no-cpu-baseline --no-gimbal --no-franka --no-cameras --no-large-n --no-default-legs"
+    B="python bench.py --envs $n --steps 48 --warmup 5 --repeats 1 --pmc-calibrate --no-cpu-baseline --no-gimbal --no-franka --no-cameras --no-large-n --no-default-legs --no-piles"
     for c in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmc_${c}_$n -o run --output-format csv -- $B \
         > gpurun_out/pmc_${c}_$n.log 2>&1 || { tail -20 gpurun_out/pmc_${c}_$n.log; exit 1; }
