@@ -133,6 +133,10 @@ class Actor:
         self.body_colors = {}
         self.body_segs = {}
         self.scale = 1.0
+        # root (linear, angular) velocity set while the scene is still being
+        # built (set_rigid_linear_velocity before prepare_sim,
+        # examples/body_physics_props.py:128-130): the initial state's root row
+        self.init_vel = None
 
     @property
     def num_bodies(self):
@@ -363,6 +367,8 @@ class Sim:
             for b in range(nba):
                 st[g0 + b, 0:3] = ps[b]
                 st[g0 + b, 3:7] = qs[b]
+            if a.init_vel is not None:
+                st[g0, 7:13] = a.init_vel
             bkey = (id(asset), id(a.mass_props), id(a.shape_props))
             blk = blocks.get(bkey)
             if blk is None:

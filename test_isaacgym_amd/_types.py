@@ -90,6 +90,34 @@ KEY_LEFT_SHIFT, KEY_LEFT_CONTROL, KEY_LEFT_ALT, KEY_RIGHT_SHIFT, KEY_RIGHT_CONTR
                                                                                                     344, 345, 346)
 del _i
 
+# viewer mouse inputs (gymapi.MouseInput; subscribe_viewer_mouse_event,
+# examples/projectiles.py:68): headless viewer, values this build's
+MouseInput = int
+(MOUSE_LEFT_BUTTON, MOUSE_RIGHT_BUTTON, MOUSE_MIDDLE_BUTTON, MOUSE_FORWARD_BUTTON, MOUSE_BACK_BUTTON,
+ MOUSE_SCROLL_RIGHT, MOUSE_SCROLL_LEFT, MOUSE_SCROLL_UP, MOUSE_SCROLL_DOWN,
+ MOUSE_MOVE_RIGHT, MOUSE_MOVE_LEFT, MOUSE_MOVE_UP, MOUSE_MOVE_DOWN) = range(13)
+
+
+def _enum(name, *members):
+    """A pybind11-style enum type over this module's int constants: Isaac Gym
+    scripts spell both gymapi.UP_AXIS_Z and gymapi.UpAxis.UP_AXIS_Z
+    (examples/test_graphics_up.py:43,108); both are the same int here."""
+    g = globals()
+    return type(name, (int,), {m: g[m] for m in members})
+
+
+SimType = _enum("SimType", "SIM_PHYSX", "SIM_FLEX")
+UpAxis = _enum("UpAxis", "UP_AXIS_Y", "UP_AXIS_Z")
+DofDriveMode = _enum("DofDriveMode", "DOF_MODE_NONE", "DOF_MODE_POS", "DOF_MODE_VEL", "DOF_MODE_EFFORT")
+DofType = _enum("DofType", "DOF_INVALID", "DOF_ROTATION", "DOF_TRANSLATION")
+JointType = _enum("JointType", "JOINT_INVALID", "JOINT_FIXED", "JOINT_REVOLUTE", "JOINT_PRISMATIC", "JOINT_BALL",
+                  "JOINT_PLANAR", "JOINT_FLOATING")
+CoordinateSpace = _enum("CoordinateSpace", "ENV_SPACE", "LOCAL_SPACE", "GLOBAL_SPACE")
+ImageType = _enum("ImageType", "IMAGE_COLOR", "IMAGE_DEPTH", "IMAGE_SEGMENTATION", "IMAGE_OPTICAL_FLOW")
+CameraFollowMode = _enum("CameraFollowMode", "FOLLOW_POSITION", "FOLLOW_TRANSFORM")
+KeyboardInput = _enum("KeyboardInput", *[k for k in list(globals()) if k.startswith("KEY_")])
+MouseInput = _enum("MouseInput", *[k for k in list(globals()) if k.startswith("MOUSE_")])
+
 RIGID_BODY_NONE = 0
 RIGID_BODY_DISABLE_GRAVITY = 1
 RIGID_BODY_DISABLE_SIMULATION = 2

@@ -694,22 +694,54 @@ class Gym:
             rows[:, 3 + k] = st["pose"]["r"][n]
         return rows
 
+    def _pending_rows(self, actors):
+        """Body-state rows of actors whose sim is still being built: the
+        initial poses by forward kinematics (the state prepare_sim starts
+        from), zero velocities but a root velocity set before it."""
+        rows = []
+        for a in actors:
+            ps, qs = a.env.sim.actor_world_body_poses(a)
+            r = np.zeros((a.num_bodies, 13), dtype=np.float32)
+            r[:, 0:3] = np.asarray(ps, dtype=np.float64)
+            r[:, 3:7] = np.asarray(qs, dtype=np.float64)
+            if a.init_vel is not None:
+                r[0, 7:13] = a.init_vel
+            rows.append(r)
+        return np.concatenate(rows, 0) if rows else np.zeros((0, 13), dtype=np.float32)
+
     def get_actor_rigid_body_states(self, env, handle, flags=_T.STATE_ALL):
         a = self._actor(env, handle)
+        if not env.sim.finalized:           # during scene building: no state read finalizes the sim
+            return self._rb_struct(self._pending_rows([a]))
         rb, _ = self._host_state(env.sim)
         return self._rb_struct(rb[a.global_body:a.global_body + a.num_bodies])
 
     def get_env_rigid_body_states(self, env, flags=_T.STATE_ALL):
+        if not env.sim.finalized:
+            return self._rb_struct(self._pending_rows(env.actors))
         rb, _ = self._host_state(env.sim)
         first = env.actors[0].global_body if env.actors else 0
         return self._rb_struct(rb[first:first + env.num_bodies])
 
     def get_sim_rigid_body_states(self, sim, flags=_T.STATE_ALL):
+        if not sim.finalized:
+            return self._rb_struct(self._pending_rows([a for e in sim.envs for a in e.actors]))
         rb, _ = self._host_state(sim)
         return self._rb_struct(rb)
 
     def _set_root_rows(self, sim, actors_rows):
-        """Teleport actor roots: [(actor, row13)] through the indexed root setter."""
+        """Teleport actor roots: [(actor, row13)] through the indexed root setter.
+        While the scene is being built (no prepare_sim, no tensor access yet) the
+        row becomes the actor's creation pose and initial root velocity instead,
+        so actors can still be added afterwards (examples/body_physics_props.py
+        sets velocities between create_actor calls)."""
+        if not sim.finalized:
+            for a, row in actors_rows:
+                o = a.env.origin
+                a.pose = Transform(Vec3(float(row[0] - o[0]), float(row[1] - o[1]), float(row[2] - o[2])),
+                                   Quat(float(row[3]), float(row[4]), float(row[5]), float(row[6])))
+                a.init_vel = np.array(row[7:13], dtype=np.float32)
+            return True
         sim.finalize()
         full = np.zeros((sim.num_actors, 13), dtype=np.float32)
         idx = np.zeros(len(actors_rows), dtype=np.int32)
@@ -744,6 +776,10 @@ class Gym:
         if flags & _T.STATE_VEL:
             cur["vel"] = new["vel"]
         rows = self._rb_rows(cur)
+        if not sim.finalized:        # the pending rows' order: env by env, actor by actor
+            acts = [a for e in sim.envs for a in e.actors]
+            first = np.cumsum([0] + [a.num_bodies for a in acts])
+            return self._set_root_rows(sim, [(a, rows[first[k]]) for k, a in enumerate(acts)])
         return self._set_root_rows(sim, [(a, rows[a.global_body]) for a in sim.actors])
 
     def set_rigid_linear_velocity(self, env, body_handle, vel):

@@ -184,3 +184,47 @@ def test_1080_balls_of_solitude_setup(monkeypatch, mode):
     for _ in range(90):
         oracle.step(p, m, st, dof)
     assert st[:, 1].min() > 0.19 and np.isfinite(st).all()
+
+
+@pytest.mark.skipif(has_gpu(), reason="CPU-container variant")
+def test_body_physics_props_setup(monkeypatch):
+    """examples/body_physics_props.py unmodified: shape properties and root
+    velocities are set between create_actor calls (:117-131), so the per-actor
+    state setters work while the scene is still being built (they become the
+    initial state, gymapi._set_root_rows) instead of freezing it. The three
+    frictionless boxes start at 2 m/s along +z; on the oracle they slide on."""
+    import numpy as np
+    import oracle
+    path = os.path.join(REFERENCE, "examples", "body_physics_props.py")
+    ns, err = _exec_script(path, os.path.join(REFERENCE, "examples"), monkeypatch)
+    assert err is not None
+    gym, sim, envs = ns["gym"], ns["sim"], ns["envs"]
+    assert len(envs) == ns["num_envs"]
+    A = sim.model_arrays
+    st = A["body_state0"].copy()
+    moving = [gym.get_actor_rigid_body_index(envs[0], h, 0, 2) for h in ns["actor_handles"][:3]]
+    assert np.array_equal(st[moving, 7:10], np.tile([0.0, 0.0, 2.0], (3, 1)).astype(np.float32))
+    z0 = st[moving, 2].copy()
+    p, m = sim.mg_params(), sim.mg_model()
+    dof = A["dof_state0"].copy()
+    for _ in range(30):
+        oracle.step(p, m, st, dof)
+    assert np.all(st[moving, 2] - z0 > 0.3) and np.isfinite(st).all()
+
+
+@pytest.mark.skipif(has_gpu(), reason="CPU-container variant")
+def test_graphics_up_and_projectiles_setup(monkeypatch):
+    """examples/test_graphics_up.py (gymapi.UpAxis.UP_AXIS_Z, the pybind-style
+    enum spelling) and examples/projectiles.py (viewer mouse events,
+    gymapi.MOUSE_LEFT_BUTTON) set up unmodified up to their first simulate."""
+    from test_isaacgym_amd import gymapi as G
+    path = os.path.join(REFERENCE, "examples", "test_graphics_up.py")
+    monkeypatch.setattr(sys, "argv", [path, "--up_axis_z"])
+    ns, err = _exec_script(path, os.path.join(REFERENCE, "examples"), monkeypatch)
+    assert err is not None and len(ns["envs"]) == ns["num_envs"]
+    assert G.UpAxis.UP_AXIS_Z == G.UP_AXIS_Z and G.UpAxis.UP_AXIS_Y == G.UP_AXIS_Y
+    path = os.path.join(REFERENCE, "examples", "projectiles.py")
+    monkeypatch.setattr(sys, "argv", [path])
+    ns, err = _exec_script(path, os.path.join(REFERENCE, "examples"), monkeypatch)
+    assert err is not None and len(ns["envs"]) == ns["num_envs"]
+    assert ns["gym"].get_sim_actor_count(ns["sim"]) == ns["num_envs"] + len(ns["projectiles"])
