@@ -132,6 +132,7 @@ class Actor:
         self.mass_props = asset.mass_props        # copy-on-write (set_actor_rigid_body_properties)
         self.body_colors = {}
         self.body_segs = {}
+        self.body_textures = {}
         self.scale = 1.0
         # root (linear, angular) velocity set while the scene is still being
         # built (set_rigid_linear_velocity before prepare_sim,
@@ -219,6 +220,7 @@ class Sim:
         self._renderer = None
         self.cam_version = 0       # bumped by every camera change (render tables are rebuilt)
         self.render_version = 0    # bumped by body colour / segmentation changes
+        self.textures = []          # create_texture_from_file / _buffer: the handle is the index
 
     @property
     def renderer(self):

@@ -13,6 +13,7 @@ MIGYM_VIEWER_FRAMES draws, so the reference scripts' loops end (§8b last row).
 """
 import ctypes
 import math
+import os
 import sys
 import time
 
@@ -868,8 +869,28 @@ class Gym:
         self._actor(env, handle).body_segs[body_index] = int(seg)
         env.sim.render_version += 1
 
+    # textures (examples/domain_randomization.py:91,179, graphics.py:100): handles
+    # are kept per body, but the camera renderer draws a body in its colour
+    # (set_rigid_body_color) — texture sampling is not modelled
+    def create_texture_from_file(self, sim, filename):
+        if not os.path.isfile(filename):
+            print("*** migym: texture file %s not found" % filename, file=sys.stderr)
+            return -1
+        sim.textures.append(os.path.abspath(filename))
+        return len(sim.textures) - 1
+
+    def create_texture_from_buffer(self, sim, width, height, pixels):
+        sim.textures.append((int(width), int(height)))
+        return len(sim.textures) - 1
+
+    def free_texture(self, sim, tex):
+        return None
+
     def set_rigid_body_texture(self, env, handle, body_index, mesh_type, tex):
-        pass
+        self._actor(env, handle).body_textures[body_index] = int(tex)
+
+    def get_rigid_body_texture(self, env, handle, body_index, mesh_type):
+        return self._actor(env, handle).body_textures.get(body_index, -1)
 
     def set_actor_scale(self, env, handle, scale):
         self._actor(env, handle).scale = float(scale)

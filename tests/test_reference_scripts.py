@@ -228,3 +228,24 @@ def test_graphics_up_and_projectiles_setup(monkeypatch):
     ns, err = _exec_script(path, os.path.join(REFERENCE, "examples"), monkeypatch)
     assert err is not None and len(ns["envs"]) == ns["num_envs"]
     assert ns["gym"].get_sim_actor_count(ns["sim"]) == ns["num_envs"] + len(ns["projectiles"])
+
+
+@pytest.mark.skipif(has_gpu(), reason="CPU-container variant")
+def test_domain_randomization_setup_matches_restated_scene(monkeypatch):
+    """examples/domain_randomization.py unmodified (textures: handles kept, the
+    renderer draws body colours) sets up to its first simulate, and its packed
+    model is the one tests/test_dr_fixture.py steps: scenes.dr_ant_scene, the
+    restatement the DR pin runs on the GPU box (where the reference is absent),
+    array for array."""
+    import numpy as np
+    from test_isaacgym_amd import gymapi as G, scenes
+    path = os.path.join(REFERENCE, "examples", "domain_randomization.py")
+    ns, err = _exec_script(path, os.path.join(REFERENCE, "examples"), monkeypatch)
+    assert err is not None
+    gym, sim = ns["gym"], ns["sim"]
+    assert len(ns["loaded_texture_handle_list"]) > 0 and min(ns["loaded_texture_handle_list"]) >= 0
+    A = sim.model_arrays
+    ref_sim = scenes.dr_ant_scene(G.acquire_gym(), 1)[0]
+    R = ref_sim.build_model()
+    for k in ("body_state0", "body_mass", "shapes", "dof_state0", "dof_props", "actor_coll"):
+        assert np.array_equal(A[k], R[k]), k
