@@ -249,3 +249,24 @@ def test_domain_randomization_setup_matches_restated_scene(monkeypatch):
     R = ref_sim.build_model()
     for k in ("body_state0", "body_mass", "shapes", "dof_state0", "dof_props", "actor_coll"):
         assert np.array_equal(A[k], R[k]), k
+
+
+SETUP_ONLY = [("asset_info.py", []), ("convex_decomposition.py", []), ("dof_controls.py", []),
+              ("large_mass_ratio.py", []), ("spherical_joint.py", []), ("transforms.py", []),
+              ("multiple_camera_envs.py", []), ("graphics.py", []), ("graphics_materials.py", []),
+              ("apply_forces.py", ["--pipeline", "cpu"]), ("apply_forces_at_pos.py", ["--pipeline", "cpu"]),
+              ("franka_osc.py", ["--pipeline", "cpu"])]
+
+
+@pytest.mark.skipif(has_gpu(), reason="CPU-container variant")
+@pytest.mark.parametrize("script,args", SETUP_ONLY, ids=[s for s, _ in SETUP_ONLY])
+def test_example_sets_up_unmodified(monkeypatch, script, args):
+    """More reference examples run their whole scene setup against the package
+    and stop only at the first call that needs the device (gym.simulate, a
+    refresh or a render: MigymError, there is no CPU engine) — no missing API,
+    no other exception on the way."""
+    path = os.path.join(REFERENCE, "examples", script)
+    monkeypatch.setattr(sys, "argv", [path] + args)
+    ns, err = _exec_script(path, os.path.join(REFERENCE, "examples"), monkeypatch)
+    assert err is not None and "HIP device" in str(err)
+    assert ns["sim"] is not None and ns["gym"].get_env_count(ns["sim"]) > 0
