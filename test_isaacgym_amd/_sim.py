@@ -65,15 +65,32 @@ def _warn_cross_env_contacts(A):
     if len(ac) == 0:
         return
     env, grp, filt = ac[:, 0], ac[:, 1], ac[:, 2]
+
+    def touch(fs):        # some pair of filters (a pair may be one actor's twice) shares no bit
+        fs = np.unique(fs)
+        return any((int(a) & int(b)) == 0 for i, a in enumerate(fs) for b in fs[i:])
+
+    # group -1 meets every group: its actors count with each group's. Sorted
+    # once (O(n log n): 262,144 envs of one group each used to take minutes)
+    m = grp == -1
+    em, fm = np.unique(env[m]), np.unique(filt[m])
     hit = False
-    # group -1 meets every group: its actors count with each group's
-    for g in np.unique(grp[grp >= 0]) if (grp >= 0).any() else [-1]:
-        sel = (grp == g) | (grp == -1)
-        if len(np.unique(env[sel])) > 1:
-            f = filt[sel]
-            # two of them may touch when some pair of filters shares no bit
-            uniq = np.unique(f)
-            if any((int(a) & int(b)) == 0 for i, a in enumerate(uniq) for b in uniq[i:]):
+    if not (~m).any():
+        hit = len(em) > 1 and touch(fm)
+    else:
+        g, e, f = grp[~m], env[~m], filt[~m]
+        order = np.lexsort((e, g))
+        g, e, f = g[order], e[order], f[order]
+        ug, start = np.unique(g, return_index=True)
+        bounds = list(start[1:]) + [len(g)]
+        first_env, last_env = e[start], e[np.asarray(bounds) - 1]
+        multi = first_env != last_env                 # the group itself spans envs
+        if len(em) > 1:
+            multi[:] = True
+        elif len(em) == 1:
+            multi |= (first_env != em[0]) | (last_env != em[0])
+        for k in np.nonzero(multi)[0]:
+            if touch(np.concatenate([f[start[k]:bounds[k]], fm])):
                 hit = True
                 break
     if hit:

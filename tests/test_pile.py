@@ -238,3 +238,30 @@ def test_cross_env_collisions_are_warned(gym, capsys):
             gym.create_actor(env, ball, gymapi.Transform(gymapi.Vec3(0.3 * k, 1, 0)), None, 0, 0)
     _sim._warn_cross_env_contacts(sim.build_model())
     assert "different envs" in capsys.readouterr().err
+
+
+def test_cross_env_warning_group_minus_one_and_scale(capsys):
+    """The warning's group rules straight on actor_coll rows (env, group,
+    filter): group -1 meets every group; filter bits shared by every pair keep
+    it silent; and the check is O(n log n) — test10's layout at 262,144 envs
+    (group i, filter -1) takes well under a second (it took ~90 s to
+    prepare_sim when the check was quadratic)."""
+    import time
+    from test_isaacgym_amd import _sim
+
+    def warned(rows):
+        _sim._warned_cross_env[0] = False
+        _sim._warn_cross_env_contacts({"actor_coll": np.asarray(rows, dtype=np.int32)})
+        return "different envs" in capsys.readouterr().err
+
+    assert not warned([[0, 0, 0], [1, 1, 0]])                 # one env per group
+    assert warned([[0, 0, 0], [1, -1, 0]])                    # group -1 joins group 0 across envs
+    assert not warned([[0, 0, 1], [1, -1, 1]])                # ... but their filters share a bit
+    assert warned([[0, -1, 0], [1, -1, 2]])                   # only group -1, two envs, no shared bit
+    assert not warned([[0, -1, 0], [0, -1, 0]])               # only group -1, one env
+    assert warned([[0, 3, 1], [0, -1, 2], [1, 3, 1]])         # group 3 spans envs; filters 1 and 2 share none
+    n = 262144
+    rows = np.stack([np.repeat(np.arange(n), 2), np.repeat(np.arange(n), 2), -np.ones(2 * n, np.int64)], 1)
+    t0 = time.perf_counter()
+    assert not warned(rows)
+    assert time.perf_counter() - t0 < 2.0
