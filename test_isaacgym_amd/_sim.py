@@ -53,6 +53,18 @@ def _warn_multishape_friction(A):
 _warned_cross_env = [False]
 
 
+def _scaled_hull_record(r, s):
+    """An MG_HULL record (include/migym.h) scaled by s about the shape origin:
+    vertices and plane offsets times s; normals and edges unchanged."""
+    r = np.array(r, dtype=np.float32)
+    nv, nf = int(r[0]), int(r[1])
+    h = N.MG_HULL_HEADER
+    r[h:h + 3 * nv] = (r[h:h + 3 * nv].astype(np.float64) * s).astype(np.float32)
+    d = h + 3 * nv + 4 * np.arange(nf) + 3
+    r[d] = (r[d].astype(np.float64) * s).astype(np.float32)
+    return r
+
+
 def _warn_cross_env_contacts(A):
     """Contacts are simulated within an env only (every kernel steps an env on
     its own): actors of different envs that share a collision
@@ -327,7 +339,7 @@ class Sim:
             d = asset.dof_of_body(b)
             qj = float(a.dof_state[d, 0]) if d >= 0 else 0.0
             qrel = j.q.copy()
-            rr = j.p.copy()
+            rr = j.p * a.scale
             for k, pj in enumerate(j.pre):      # pre-hinges of a multi-joint body, in order
                 th = float(a.dof_state[d + k, 0])
                 s, c = np.sin(0.5 * th), np.cos(0.5 * th)
@@ -346,7 +358,7 @@ class Sim:
                     e = np.array([*(th / t * np.sin(0.5 * t)), np.cos(0.5 * t)])
                     qrel = _qmul(qrel, e)
             elif j.type == T.JOINT_PRISMATIC:
-                rr = j.p + _qmat(j.q) @ (j.axis * qj)
+                rr = j.p * a.scale + _qmat(j.q) @ (j.axis * qj)
             pp, pq = ps[j.parent], qs[j.parent]
             qn = _qmul(pq, qrel)
             qs.append(qn / np.linalg.norm(qn))
@@ -388,7 +400,8 @@ class Sim:
                 st[g0 + b, 3:7] = qs[b]
             if a.init_vel is not None:
                 st[g0, 7:13] = a.init_vel
-            bkey = (id(asset), id(a.mass_props), id(a.shape_props))
+            sc = a.scale                   # set_actor_scale: geometry and joint frames (mass props already scaled)
+            bkey = (id(asset), id(a.mass_props), id(a.shape_props), sc)
             blk = blocks.get(bkey)
             if blk is None:
                 bm = np.zeros((nba, N.MG_MASS_N), dtype=np.float32)
@@ -405,7 +418,7 @@ class Sim:
                     sidx = sum(len(x.shapes) for x in asset.bodies[:b])
                     mats = tuple((a.shape_props[sidx + k].friction, a.shape_props[sidx + k].restitution)
                                  for k in range(len(body.shapes)))
-                    key = (id(asset), b, mats)
+                    key = (id(asset), b, mats, sc)
                     if key not in tb_key:
                         tb_key[key] = len(tbf)
                         tbf.append([opts.linear_damping, opts.angular_damping, opts.max_linear_velocity,
@@ -414,15 +427,18 @@ class Sim:
                         for k, sh in enumerate(body.shapes):
                             rec = np.zeros(N.MG_SHAPE_STRIDE, dtype=np.float32)
                             rec[0] = sh.type
-                            rec[1:1 + len(sh.size)] = sh.size
+                            rec[1:1 + len(sh.size)] = np.asarray(sh.size, dtype=np.float64) * sc
                             if sh.type == N.MG_SHAPE_CONVEX:
-                                if id(sh.hull) not in hull_off:
+                                hk = (id(sh.hull), sc)
+                                if hk not in hull_off:
                                     r = sh.hull.record()
-                                    hull_off[id(sh.hull)] = nhull
+                                    if sc != 1.0:
+                                        r = _scaled_hull_record(r, sc)
+                                    hull_off[hk] = nhull
                                     hulls.append(r)
                                     nhull += len(r)
-                                rec[2] = hull_off[id(sh.hull)]
-                            rec[4:7] = sh.p
+                                rec[2] = hull_off[hk]
+                            rec[4:7] = np.asarray(sh.p, dtype=np.float64) * sc
                             rec[7:11] = sh.q
                             rec[11] = mats[k][0]
                             rec[12] = mats[k][1]
@@ -447,8 +463,9 @@ class Sim:
                                    p["lower"], p["upper"], 1.0 if p["hasLimits"] else 0.0, p["armature"],
                                    p["friction"]]
             if multi:
-                if id(asset) not in atmpl_key:
-                    atmpl_key[id(asset)] = len(atmpl)
+                akey = (id(asset), sc)
+                if akey not in atmpl_key:
+                    atmpl_key[akey] = len(atmpl)
                     atmpl.append([len(lf), len(asset.bodies), asset.num_dofs, 1 if opts.fix_base_link else 0])
                     nl0 = len(lf)
                     link_of = []          # body -> its kernel link (local)
@@ -467,7 +484,7 @@ class Sim:
                             f = np.zeros(N.MG_LINK_F_N, dtype=np.float32)
                             f[3:7] = (0, 0, 0, 1)
                             if k == 0:
-                                f[0:3] = j.p
+                                f[0:3] = j.p * sc
                                 f[3:7] = j.q
                             f[7:10] = pj.axis
                             lf.append(f)
@@ -482,7 +499,7 @@ class Sim:
                                 f = np.zeros(N.MG_LINK_F_N, dtype=np.float32)
                                 f[3:7] = (0, 0, 0, 1)
                                 if k == 0:
-                                    f[0:3] = j.p
+                                    f[0:3] = j.p * sc
                                     f[3:7] = j.q
                                 f[7 + k] = 1.0
                                 f[10] = k + 1     # place in the ball: the first link turns by exp(th)
@@ -493,7 +510,7 @@ class Sim:
                             f = np.zeros(N.MG_LINK_F_N, dtype=np.float32)
                             f[3:7] = (0, 0, 0, 1)
                             if not j.pre:
-                                f[0:3] = j.p
+                                f[0:3] = j.p * sc
                                 f[3:7] = j.q
                             f[7:10] = j.axis
                             li.append([parent, j.type if j.type in (T.JOINT_FIXED, T.JOINT_REVOLUTE,
@@ -501,7 +518,7 @@ class Sim:
                             lf.append(f)
                         link_of.append(len(lf) - 1 - nl0)
                     atmpl[-1][1] = len(lf) - nl0
-                artic.append([a.global_body, a.global_dof, atmpl_key[id(asset)], 0])
+                artic.append([a.global_body, a.global_dof, atmpl_key[akey], 0])
         self.model_arrays = dict(
             body_state0=st, body_mass=mass, body_kind=kind, body_tmpl=btmpl,
             tmpl_body_f=np.array(tbf, dtype=np.float32).reshape(-1, N.MG_TBODY_F_N),

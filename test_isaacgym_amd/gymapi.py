@@ -893,8 +893,23 @@ class Gym:
         return self._actor(env, handle).body_textures.get(body_index, -1)
 
     def set_actor_scale(self, env, handle, scale):
-        self._actor(env, handle).scale = float(scale)
-        return abs(scale - 1.0) < 1e-6
+        """examples/actor_scaling.py:126. Scales the actor's collision geometry
+        and joint frames by `scale` and its mass properties with them (mass by
+        scale^3, inertia by scale^5, centres of mass by scale), as a body of the
+        same density would. Before prepare_sim only: the packed model is frozen
+        after it (returns False, said on stderr)."""
+        a = self._actor(env, handle)
+        scale = float(scale)
+        if env.sim.finalized:
+            print("*** migym: actor scale is frozen after prepare_sim", file=sys.stderr)
+            return False
+        if not scale > 0.0:
+            return False
+        r = scale / a.scale
+        if r != 1.0:
+            a.mass_props = [_assets.MassProps(mp.mass * r ** 3, mp.com * r, mp.inertia * r ** 5) for mp in a.mass_props]
+            a.scale = scale
+        return True
 
     def get_actor_scale(self, env, handle):
         return self._actor(env, handle).scale
