@@ -1342,10 +1342,29 @@ class Gym:
         return Tensor(_render.image_tensor(sim, cam, image_type))
 
     def write_camera_image_to_file(self, sim, env, handle, image_type, filename):
+        """examples/domain_randomization.py:192 (--save_images): the last render
+        of the camera as a PNG — color as RGBA, depth as 16-bit millimetres of
+        -depth (Isaac Gym's depth is negative along the view axis; 0 = no hit),
+        segmentation as 16-bit ids. False when the image cannot be written."""
+        from PIL import Image
+        img = self.get_camera_image(sim, env, handle, image_type)
+        try:
+            if image_type == _T.IMAGE_COLOR:
+                h = img.shape[0]
+                Image.fromarray(np.ascontiguousarray(img.reshape(h, -1, 4)), "RGBA").save(filename)
+            elif image_type == _T.IMAGE_DEPTH:
+                d = np.nan_to_num(-np.asarray(img, dtype=np.float64), posinf=0.0, neginf=0.0)
+                Image.fromarray(np.clip(np.rint(d * 1000.0), 0, 65535).astype(np.uint16)).save(filename)
+            else:
+                Image.fromarray(np.clip(np.asarray(img), 0, 65535).astype(np.uint16)).save(filename)
+        except OSError as e:
+            print("*** migym: cannot write %s: %s" % (filename, e), file=sys.stderr)
+            return False
         return True
 
     def write_viewer_image_to_file(self, viewer, filename):
-        return True
+        """The viewer is headless (no window, nothing drawn): no image to write."""
+        return False
 
 
 def sim_num(sim, what):

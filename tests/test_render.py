@@ -211,7 +211,7 @@ def test_render_servo_cameras_gpu_bitexact(gym):
 
 
 @pytest.mark.gpu
-def test_get_camera_image_shows_the_render_snapshot(gym):
+def test_get_camera_image_shows_the_render_snapshot(gym, tmp_path):
     """test11 calls set_actor_root_state_tensor between render_all_camera_sensors
     and get_camera_image (:388,456,459): the image is the rendered snapshot."""
     n = 4
@@ -247,6 +247,15 @@ def test_get_camera_image_shows_the_render_snapshot(gym):
     assert not np.array_equal(after, before[0])
     d = gym.get_camera_image(sim, envs[0], 0, gymapi.IMAGE_DEPTH)
     assert d.dtype == np.float32 and np.isneginf(d[0]).all()           # top row: sky
+    # write_camera_image_to_file (domain_randomization.py:192): the same render as PNG
+    from PIL import Image
+    fc, fd = str(tmp_path / "rgb.png"), str(tmp_path / "depth.png")
+    assert gym.write_camera_image_to_file(sim, envs[0], 0, gymapi.IMAGE_COLOR, fc)
+    assert gym.write_camera_image_to_file(sim, envs[0], 0, gymapi.IMAGE_DEPTH, fd)
+    assert np.array_equal(np.asarray(Image.open(fc)).reshape(36, 64 * 4), after)
+    mm = np.asarray(Image.open(fd)).astype(np.int64)
+    hit = np.isfinite(d)
+    assert (mm[~hit] == 0).all() and np.abs(mm[hit] - np.rint(-d[hit] * 1000.0)).max() <= 1
 
 
 @pytest.mark.gpu
