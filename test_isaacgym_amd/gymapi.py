@@ -1344,7 +1344,8 @@ class Gym:
     def write_camera_image_to_file(self, sim, env, handle, image_type, filename):
         """examples/domain_randomization.py:192 (--save_images): the last render
         of the camera as a PNG — color as RGBA, depth as 16-bit millimetres of
-        -depth (Isaac Gym's depth is negative along the view axis; 0 = no hit),
+        -depth (Isaac Gym's depth is negative along the view axis; 0 = no hit;
+        clipped at 65.535 m),
         segmentation as 16-bit ids. False when the image cannot be written."""
         from PIL import Image
         img = self.get_camera_image(sim, env, handle, image_type)

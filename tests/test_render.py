@@ -255,7 +255,8 @@ def test_get_camera_image_shows_the_render_snapshot(gym, tmp_path):
     assert np.array_equal(np.asarray(Image.open(fc)).reshape(36, 64 * 4), after)
     mm = np.asarray(Image.open(fd)).astype(np.int64)
     hit = np.isfinite(d)
-    assert (mm[~hit] == 0).all() and np.abs(mm[hit] - np.rint(-d[hit] * 1000.0)).max() <= 1
+    want = np.clip(np.rint(-d[hit].astype(np.float64) * 1000.0), 0, 65535)     # 16-bit: clipped at 65.535 m
+    assert (mm[~hit] == 0).all() and np.abs(mm[hit] - want).max() <= 1
 
 
 @pytest.mark.gpu
