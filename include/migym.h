@@ -206,7 +206,11 @@ int32_t     mg_fetch_results(mg_sim* sim, int32_t wait);
  * bodies, 2 DOFs, 3 contact forces; 0: wait only). The refresh_*_tensor calls
  * that follow (:394-396) are then host copies from it while no simulate or state
  * set intervenes (the Python layer tracks that), instead of a device round trip
- * each. Not while the stream is being captured. */
+ * each. Not while the stream is being captured. From the first call on, on a sim
+ * whose bodies are all stepped by kernels that write their own rows (as
+ * MG_FUSE_STEP_OUT), the step writes root / body / DOF rows into the sim's own
+ * device copy of this layout, and a fetch after a simulate with no state set
+ * since copies those parts without gathering them. */
 int32_t     mg_fetch_host_state(mg_sim* sim, float* dst, int32_t parts, void* stream);
 
 /* ---- tensor API: refresh (state -> user tensor) ----------------------------
@@ -231,7 +235,10 @@ int32_t     mg_refresh_net_contact_force(mg_sim* sim, float* dst, int32_t dst_ho
  * kernel (the scatter fused into the step), or by the scatter that any earlier
  * call reading the state issues first (refresh_*, set_rigid_body_state, an
  * indexed or host set, the render snapshot). The caller keeps such a src alive
- * and unmodified until then (the gymapi layer holds the tensor). */
+ * and unmodified until then (the gymapi layer holds the tensor). A host source
+ * (src_host) is copied at the call into the sim's page-locked buffer, so it may
+ * be overwritten at once; a full host set on such a sim is then read by the
+ * next mg_simulate's step kernel too (no scatter launch). */
 int32_t     mg_set_actor_root_state(mg_sim* sim, const float* src, int32_t src_host,
                                     const int32_t* idx, int32_t n_idx, void* stream);
 /* gym.set_rigid_body_state_tensor (test/test05_isaacgym_vel_batch.py:367-385):

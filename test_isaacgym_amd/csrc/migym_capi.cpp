@@ -181,6 +181,24 @@ struct mg_sim {
 
     float* d_stage = nullptr;     // host-transfer staging (floats)
     size_t stage_n = 0;
+    // CPU pipeline (host state tensors): a full host root set is copied here at the
+    // set call and read by the next step kernel (no scatter launch); and from the
+    // first mg_fetch_host_state on, the step kernels that write their own rows
+    // (step_out_ok) write root / rigid-body / DOF rows into d_host_out, laid out as
+    // the host stage, so the fetch copies them without gathering (ho_*_gen: the
+    // state generation they hold)
+    float* d_root_pend = nullptr;
+    // host sources are copied at the set call into this page-locked buffer (then
+    // sent in stream order), so the caller may overwrite its tensor right away —
+    // Isaac Gym's copy-at-set — even though the transfer itself is asynchronous;
+    // pin_ev: the last transfer out of it (waited on before it is refilled)
+    char* h_pin = nullptr;
+    size_t h_pin_n = 0;
+    hipEvent_t pin_ev = nullptr;
+    bool pin_ev_pending = false;
+    float* d_host_out = nullptr;
+    size_t host_out_n = 0;
+    long long ho_root_gen = -1, ho_rb_gen = -1, ho_dof_gen = -1;
     int* d_stage_idx = nullptr;
     size_t stage_idx_n = 0;
 
@@ -296,6 +314,32 @@ int refresh_rows(mg_sim* s, const float* soa, int stride, int ncol, const int* i
     return MG_OK;
 }
 
+// copy host data into the sim's page-locked buffer now and send it to the device
+// in stream order: n parts (src[k], bytes[k]) to dst[k]
+int pin_h2d(mg_sim* s, int n, const void* const* src, const size_t* bytes, void* const* dst, hipStream_t st) {
+    size_t total = 0;
+    for (int k = 0; k < n; ++k) total += (bytes[k] + 255) & ~(size_t)255;
+    if (total > s->h_pin_n) {
+        if (s->pin_ev_pending) HIP_TRY(hipEventSynchronize(s->pin_ev));
+        if (s->h_pin) (void)hipHostFree(s->h_pin);
+        s->h_pin = nullptr;
+        s->h_pin_n = 0;
+        HIP_TRY(hipHostMalloc((void**)&s->h_pin, total, hipHostMallocDefault));
+        s->h_pin_n = total;
+    }
+    if (!s->pin_ev) HIP_TRY(hipEventCreateWithFlags(&s->pin_ev, hipEventDisableTiming));
+    if (s->pin_ev_pending) HIP_TRY(hipEventSynchronize(s->pin_ev));   // the previous transfer left it
+    size_t at = 0;
+    for (int k = 0; k < n; ++k) {
+        std::memcpy(s->h_pin + at, src[k], bytes[k]);
+        HIP_TRY(hipMemcpyAsync(dst[k], s->h_pin + at, bytes[k], hipMemcpyHostToDevice, st));
+        at += (bytes[k] + 255) & ~(size_t)255;
+    }
+    HIP_TRY(hipEventRecord(s->pin_ev, st));
+    s->pin_ev_pending = true;
+    return MG_OK;
+}
+
 // stage a host source (and optional index list) to the device
 int stage_src(mg_sim* s, const float* src, int src_host, size_t nfloat, const int* idx, int n_idx,
               hipStream_t st, const float** dsrc, const int** didx) {
@@ -304,12 +348,12 @@ int stage_src(mg_sim* s, const float* src, int src_host, size_t nfloat, const in
     if (!src_host) return MG_OK;
     int rc = ensure_stage(s, nfloat, idx ? (size_t)n_idx : 0);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(s->d_stage, src, nfloat * sizeof(float), hipMemcpyHostToDevice, st));
+    const void* srcs[2] = {src, idx};
+    const size_t bytes[2] = {nfloat * sizeof(float), idx && n_idx > 0 ? (size_t)n_idx * sizeof(int) : 0};
+    void* dsts[2] = {s->d_stage, s->d_stage_idx};
+    if ((rc = pin_h2d(s, bytes[1] ? 2 : 1, srcs, bytes, dsts, st))) return rc;
     *dsrc = s->d_stage;
-    if (idx && n_idx > 0) {
-        HIP_TRY(hipMemcpyAsync(s->d_stage_idx, idx, (size_t)n_idx * sizeof(int), hipMemcpyHostToDevice, st));
-        *didx = s->d_stage_idx;
-    }
+    if (idx && n_idx > 0) *didx = s->d_stage_idx;
     return MG_OK;
 }
 
@@ -397,7 +441,7 @@ void shape_obb(const float* sh, const float* hulls, float* o) {
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls, s->d_shape_obb,
                     s->d_actor_root, s->d_root_row, s->d_slot_global, s->d_slot_actor, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
-                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_chain_uni, s->d_fp_mask, s->d_env_carry, s->d_env_ctab, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx,
+                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_chain_uni, s->d_fp_mask, s->d_env_carry, s->d_env_ctab, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx, s->d_root_pend, s->d_host_out,
                     s->d_pile_i, s->d_pile_body, s->d_pile_pairs, s->d_pile_slots, s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -453,6 +497,8 @@ void mg_destroy_sim(mg_sim* s) {
     }
     if (s->rev_b) (void)hipEventDestroy(s->rev_b);
     if (s->rev_e) (void)hipEventDestroy(s->rev_e);
+    if (s->pin_ev) (void)hipEventDestroy(s->pin_ev);
+    if (s->h_pin) (void)hipHostFree(s->h_pin);
     delete s;
 }
 
@@ -1285,6 +1331,12 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     const unsigned long long step_cid = capture_id(st);
     const bool step_out = (s->fusion & MG_FUSE_STEP_OUT) && fuse_here(s, step_cid) && s->step_out_ok &&
                           (s->bind_root || s->bind_rb || s->bind_dof);
+    // the CPU pipeline's output stage (mg_fetch_host_state): the same kernels
+    // write into the library's own buffer, so no caller-visible tensor changes
+    const bool host_out = !step_out && s->d_host_out && s->step_out_ok && step_cid == 0;
+    float* ho_root = host_out ? s->d_host_out : nullptr;
+    float* ho_rb = host_out ? s->d_host_out + (size_t)s->na * MG_STATE_N : nullptr;
+    float* ho_dof = host_out && s->nd ? s->d_host_out + (size_t)(s->na + s->nb) * MG_STATE_N : nullptr;
     for (size_t gi = 0; gi < s->groups.size(); ++gi) {
         const ArticGroup& g = s->groups[gi];
         if (g.step_count == 0) continue;
@@ -1306,10 +1358,10 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.dof_props = s->d_dof_props;
         A.ext = s->ext_pending ? s->d_ext : nullptr;
         A.cforce = s->d_cforce;
-        if (step_out) {   // chain groups only (s->step_out_ok)
-            A.out_rb = s->bind_rb;
-            A.out_root = s->bind_root;
-            A.out_dof = s->bind_dof;
+        if (step_out || host_out) {   // chain groups only (s->step_out_ok)
+            A.out_rb = step_out ? s->bind_rb : ho_rb;
+            A.out_root = step_out ? s->bind_root : ho_root;
+            A.out_dof = step_out ? s->bind_dof : ho_dof;
             A.out_body = s->d_slot_global;
             A.out_root_row = s->d_slot_actor;
         }
@@ -1371,9 +1423,9 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
             A.root_row = s->d_root_row;
             s->pend_root = nullptr;
         }
-        if (step_out) {
-            A.out_rb = s->bind_rb;
-            A.out_root = s->bind_root;
+        if (step_out || host_out) {
+            A.out_rb = step_out ? s->bind_rb : ho_rb;
+            A.out_root = step_out ? s->bind_root : ho_root;
             A.out_body = s->d_slot_global;     // internal slot -> global body
             A.out_root_row = s->d_slot_actor;
         }
@@ -1386,6 +1438,11 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     for (int k = 0; k < 3; ++k) s->pend_tgt[k] = nullptr;   // read (and written through) by the step
     s->state_gen++;
     s->dof_sgen++;
+    if (host_out) {
+        s->ho_root_gen = s->state_gen;
+        s->ho_rb_gen = s->state_gen;
+        s->ho_dof_gen = ho_dof ? s->dof_sgen : -1;
+    }
     if (step_out) {
         if (s->bind_root) { s->out_gen = s->state_gen; s->out_cap = step_cid; }
         if (s->bind_rb) { s->rb_gen = s->state_gen; s->rb_cap = step_cid; }
@@ -1434,21 +1491,30 @@ int32_t mg_fetch_host_state(mg_sim* s, float* dst, int32_t parts, void* stream) 
     const size_t off[5] = {0, (size_t)s->na * MG_STATE_N, (size_t)(s->na + s->nb) * MG_STATE_N,
                            (size_t)(s->na + s->nb) * MG_STATE_N + (size_t)s->nd * 2,
                            (size_t)(s->na + s->nb) * MG_STATE_N + (size_t)s->nd * 2 + (size_t)s->nb * 3};
-    int rc = ensure_stage(s, off[4], 0);
-    if (rc) return rc;
+    if (s->host_out_n < off[4]) {   // the output stage (simulate writes into it from now on)
+        if (s->d_host_out) (void)hipFree(s->d_host_out);
+        s->d_host_out = nullptr;
+        HIP_TRY(dalloc(&s->d_host_out, std::max<size_t>(off[4], 1)));
+        s->host_out_n = off[4];
+        s->ho_root_gen = s->ho_rb_gen = s->ho_dof_gen = -1;
+    }
     int lo = -1, hi = -1;
     for (int k = 0; k < 4; ++k) {
         if (!((parts >> k) & 1) || off[k + 1] == off[k]) continue;
         if (lo < 0) lo = k;
         hi = k;
-        float* d = s->d_stage + off[k];
-        if (k == 0) HIP_TRY(mg_launch_gather_rows(s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, d, st));
-        if (k == 1) HIP_TRY(mg_launch_gather_rows(s->d_state, s->nb, MG_STATE_N, s->d_perm, s->nb, d, st));
-        if (k == 2) HIP_TRY(mg_launch_gather_rows(s->d_dof, s->nd, 2, nullptr, s->nd, d, st));
+        float* d = s->d_host_out + off[k];
+        // parts the last simulate wrote there, with no state change since: no gather
+        if (k == 0 && s->ho_root_gen != s->state_gen)
+            HIP_TRY(mg_launch_gather_rows(s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, d, st));
+        if (k == 1 && s->ho_rb_gen != s->state_gen)
+            HIP_TRY(mg_launch_gather_rows(s->d_state, s->nb, MG_STATE_N, s->d_perm, s->nb, d, st));
+        if (k == 2 && s->ho_dof_gen != s->dof_sgen)
+            HIP_TRY(mg_launch_gather_rows(s->d_dof, s->nd, 2, nullptr, s->nd, d, st));
         if (k == 3) HIP_TRY(mg_launch_gather_rows(s->d_cforce, s->nb, 3, s->d_perm, s->nb, d, st));
     }
     if (lo >= 0)
-        HIP_TRY(hipMemcpyAsync(dst + off[lo], s->d_stage + off[lo], (off[hi + 1] - off[lo]) * sizeof(float),
+        HIP_TRY(hipMemcpyAsync(dst + off[lo], s->d_host_out + off[lo], (off[hi + 1] - off[lo]) * sizeof(float),
                                hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return MG_OK;
@@ -1658,6 +1724,20 @@ int32_t mg_set_actor_root_state(mg_sim* s, const float* src, int32_t src_host, c
         s->pend_root = src;   // read by the next simulate (a later full set replaces it)
         s->pend_root_cap = cid;
         s->last_set_deferred = 1;
+        return MG_OK;
+    }
+    if (src_host && !idx && s->roots_free && cid == 0) {
+        // CPU pipeline, full set: copied at the call into the library's own buffer
+        // (Isaac Gym's copy-at-set), read by the next simulate's step kernel like
+        // a fused device set — or by the scatter a reader of the state issues first
+        if (!s->d_root_pend) HIP_TRY(dalloc(&s->d_root_pend, (size_t)s->na * MG_STATE_N));
+        s->pend_root = nullptr;     // a later full set replaces an earlier deferred one
+        const void* srcs[1] = {src};
+        const size_t bytes[1] = {(size_t)s->na * MG_STATE_N * sizeof(float)};
+        void* dsts[1] = {s->d_root_pend};
+        if (int rc_ = pin_h2d(s, 1, srcs, bytes, dsts, st)) return rc_;
+        s->pend_root = s->d_root_pend;
+        s->pend_root_cap = 0;
         return MG_OK;
     }
     if (int rc_ = flush_root(s, st)) return rc_;

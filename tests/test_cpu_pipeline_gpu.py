@@ -55,3 +55,42 @@ def test_cpu_pipeline_staged_refreshes_gpu(gym):
         assert np.array_equal(root.numpy(), st[roots]), "step %d: root tensor" % k
         if k % 10 != 5:
             assert np.array_equal(ncf.numpy(), cf), "step %d: net contact force" % k
+
+
+def test_cpu_pipeline_copy_at_set_and_set_before_fetch_gpu(gym):
+    """The host root set is Isaac Gym's copy-at-set: the tensor is copied at
+    the call (into the library's page-locked buffer) and read by the next
+    simulate's step kernel, so overwriting the host tensor right after the set
+    changes nothing. And a set between simulate and fetch_results: the staged
+    state is the set's (the step's own output rows are stale then, so the
+    fetch gathers). Bit for bit the oracle."""
+    n = 128
+    sim, _ = scenes.servo_scene(gym, n, use_gpu_pipeline=False)
+    gym.prepare_sim(sim)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    p, m = sim.mg_params(), sim.mg_model()
+    A = sim.model_arrays
+    st = A["body_state0"].copy()
+    dof = A["dof_state0"].copy()
+    roots = A["actor_root_body"]
+    acts = scenes.servo_actions(n, 8, "cpu", seed=6)
+    gym.refresh_actor_root_state_tensor(sim)
+    for k in range(24):
+        root[:, 3:10] = acts[k % 8]
+        assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+        st[roots, 3:10] = acts[k % 8].numpy()
+        root.fill_(float("nan"))                 # overwritten right after the set
+        gym.simulate(sim)
+        oracle.step(p, m, st, dof)
+        if k % 6 == 3:
+            # a set after the simulate and before the fetch: the staged state is the set's
+            gym.refresh_actor_root_state_tensor(sim)        # (the tensor holds the state again)
+            root[1, 0:3] = torch.tensor([-3.0, 4.0, 120.0])
+            assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+            st[roots] = root.numpy()
+        gym.fetch_results(sim, True)
+        gym.refresh_actor_root_state_tensor(sim)
+        gym.refresh_rigid_body_state_tensor(sim)
+        assert np.array_equal(rb.numpy(), st), "step %d: rigid-body tensor" % k
+        assert np.array_equal(root.numpy(), st[roots]), "step %d: root tensor" % k
