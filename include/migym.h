@@ -212,6 +212,13 @@ int32_t     mg_fetch_results(mg_sim* sim, int32_t wait);
  * device copy of this layout, and a fetch after a simulate with no state set
  * since copies those parts without gathering them. */
 int32_t     mg_fetch_host_state(mg_sim* sim, float* dst, int32_t parts, void* stream);
+/* The sim's own host stage for mg_fetch_host_state: nfloat floats of page-locked
+ * host memory mapped into the device's address space, owned by the sim (freed by
+ * mg_destroy_sim; a larger request replaces it). Passed as mg_fetch_host_state's
+ * dst, the fetch is zero-copy: the step kernels write their rows into it over
+ * PCIe and the remaining parts are gathered straight into it — no device-to-host
+ * copy. NULL on failure (mg_last_error). */
+float*      mg_host_stage(mg_sim* sim, int64_t nfloat);
 
 /* ---- tensor API: refresh (state -> user tensor) ----------------------------
  * gym.refresh_actor_root_state_tensor (:394), refresh_rigid_body_state_tensor

@@ -143,6 +143,7 @@ def _load():
         "mg_num_coupled_envs": (i32, [vp]),
         "mg_num_pile_envs": (i32, [vp]),
         "mg_fetch_host_state": (i32, [vp, vp, i32, vp]),
+        "mg_host_stage": (vp, [vp, ctypes.c_int64]),
         "mg_debug_copy_env_ctab": (i32, [vp, i32, vp, i32]),
         "mg_debug_artic_groups": (i32, [vp, vp, i32]),
         "mg_step_untimed_launches": (i32, [vp, i32]),
@@ -175,7 +176,7 @@ EXPORTED_SYMBOLS = (
     "mg_refresh_jacobian", "mg_refresh_mass_matrix", "mg_set_kernel_timing", "mg_set_fusion", "mg_bind_refresh_targets",
     "mg_bind_dof_refresh_target", "mg_step_out_supported", "mg_last_set_deferred", "mg_discard_pending_sets", "mg_last_step_ms", "mg_step_time_stats", "mg_num_free_bodies",
     "mg_num_articulations",
-    "mg_num_coupled_envs", "mg_num_pile_envs", "mg_fetch_host_state", "mg_refresh_jacobian_mass_matrix",
+    "mg_num_coupled_envs", "mg_num_pile_envs", "mg_fetch_host_state", "mg_host_stage", "mg_refresh_jacobian_mass_matrix",
     "mg_set_render_bodies", "mg_snapshot_render_state", "mg_render_cameras", "mg_last_render_ms",
     "mg_debug_copy_env_ctab", "mg_debug_artic_groups", "mg_step_untimed_launches", "mg_cube_pick_step", "mg_env_ctab_floats", "mg_env_carry_floats",
 )

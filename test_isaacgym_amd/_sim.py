@@ -594,6 +594,15 @@ class Sim:
                 raise N.MigymError("mg_create_sim: " + N.last_error())
             self.native = handle
             N.check(N.lib.mg_upload_model(handle, ctypes.byref(self.mg_model())), "mg_upload_model")
+            if self.host_stage is not None and os.environ.get("MIGYM_HOST_STAGE", "mapped") != "copy":
+                # the sim's own device-mapped host stage (mg_host_stage): the
+                # waiting fetch is then zero-copy (the step writes its rows into it);
+                # MIGYM_HOST_STAGE=copy keeps a torch page-locked stage and a D2H copy
+                nst = int(self.host_stage.numel())
+                ptr = N.lib.mg_host_stage(handle, max(nst, 1))
+                if ptr:
+                    buf = (ctypes.c_float * max(nst, 1)).from_address(ptr)
+                    self.host_stage = torch.from_numpy(np.ctypeslib.as_array(buf))[:nst]
             # the persistent root / rigid-body tensors: a root refresh serves both
             # (mg_bind_refresh_targets, MG_FUSE_REFRESH)
             root, rb = self.tensors["root"], self.tensors["rb"]
@@ -636,5 +645,7 @@ class Sim:
 
     def destroy(self):
         if self.native:
+            self.host_stage = None          # the sim's own memory (mg_host_stage), freed with it
+            self.host_stage_epoch = -1
             N.lib.mg_destroy_sim(self.native)
             self.native = None

@@ -181,13 +181,12 @@ struct mg_sim {
 
     float* d_stage = nullptr;     // host-transfer staging (floats)
     size_t stage_n = 0;
-    // CPU pipeline (host state tensors): a full host root set is copied here at the
-    // set call and read by the next step kernel (no scatter launch); and from the
+    // CPU pipeline (host state tensors): a full host root set is read by the next
+    // step kernel (no scatter launch; h_root_in below); and from the
     // first mg_fetch_host_state on, the step kernels that write their own rows
     // (step_out_ok) write root / rigid-body / DOF rows into d_host_out, laid out as
     // the host stage, so the fetch copies them without gathering (ho_*_gen: the
     // state generation they hold)
-    float* d_root_pend = nullptr;
     // host sources are copied at the set call into this page-locked buffer (then
     // sent in stream order), so the caller may overwrite its tensor right away —
     // Isaac Gym's copy-at-set — even though the transfer itself is asynchronous;
@@ -198,6 +197,20 @@ struct mg_sim {
     bool pin_ev_pending = false;
     float* d_host_out = nullptr;
     size_t host_out_n = 0;
+    // zero-copy variants (mg_host_stage): the host stage itself, page-locked and
+    // mapped into the device's address space — the step kernels write their rows
+    // into it over PCIe and the fetch's remaining gathers do too (no copy); and
+    // a mapped input buffer the step kernel reads a host root set from
+    // (root_ev: its last reader, waited on before it is refilled)
+    float* h_stage = nullptr;
+    float* d_stage_alias = nullptr;
+    size_t h_stage_n = 0;
+    float* h_root_in = nullptr;
+    float* d_root_in_alias = nullptr;
+    hipEvent_t root_ev = nullptr;
+    bool root_ev_pending = false;
+    bool ho_alias = false;            // the last fetch staged into h_stage: the step writes there
+    const float* ho_written = nullptr;   // the stage the last simulate wrote (ho_*_gen refer to it)
     long long ho_root_gen = -1, ho_rb_gen = -1, ho_dof_gen = -1;
     int* d_stage_idx = nullptr;
     size_t stage_idx_n = 0;
@@ -376,6 +389,10 @@ int flush_root(mg_sim* s, hipStream_t st) {
     const float* src = s->pend_root;
     s->pend_root = nullptr;
     HIP_TRY(mg_launch_scatter_rows(src, MG_STATE_N, s->d_actor_root, nullptr, s->na, s->na, s->d_state, s->nb, st));
+    if (src == s->d_root_in_alias) {   // the mapped input buffer's reader
+        HIP_TRY(hipEventRecord(s->root_ev, st));
+        s->root_ev_pending = true;
+    }
     return MG_OK;
 }
 
@@ -441,7 +458,7 @@ void shape_obb(const float* sh, const float* hulls, float* o) {
 void free_all(mg_sim* s) {
     void* ptrs[] = {s->d_state, s->d_mass, s->d_body_tmpl, s->d_free_global, s->d_perm, s->d_tbf, s->d_trec, s->d_tbi, s->d_shapes, s->d_hulls, s->d_shape_obb,
                     s->d_actor_root, s->d_root_row, s->d_slot_global, s->d_slot_actor, s->d_body_actor, s->d_actor_dof, s->d_cforce, s->d_ext, s->d_dof, s->d_dof_tgt,
-                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_chain_uni, s->d_fp_mask, s->d_env_carry, s->d_env_ctab, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx, s->d_root_pend, s->d_host_out,
+                    s->d_dof_props, s->d_artic, s->d_artic_step, s->d_env, s->d_pairs, s->d_fpatch, s->d_gpatch, s->d_chain_uni, s->d_fp_mask, s->d_env_carry, s->d_env_ctab, s->d_link_f, s->d_link_i, s->d_stage, s->d_stage_idx, s->d_host_out,
                     s->d_pile_i, s->d_pile_body, s->d_pile_pairs, s->d_pile_slots, s->d_rstate, s->d_rshapes, s->d_env_shape_first, s->d_cams};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -499,6 +516,9 @@ void mg_destroy_sim(mg_sim* s) {
     if (s->rev_e) (void)hipEventDestroy(s->rev_e);
     if (s->pin_ev) (void)hipEventDestroy(s->pin_ev);
     if (s->h_pin) (void)hipHostFree(s->h_pin);
+    if (s->root_ev) (void)hipEventDestroy(s->root_ev);
+    if (s->h_root_in) (void)hipHostFree(s->h_root_in);
+    if (s->h_stage) (void)hipHostFree(s->h_stage);
     delete s;
 }
 
@@ -1333,10 +1353,11 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
                           (s->bind_root || s->bind_rb || s->bind_dof);
     // the CPU pipeline's output stage (mg_fetch_host_state): the same kernels
     // write into the library's own buffer, so no caller-visible tensor changes
-    const bool host_out = !step_out && s->d_host_out && s->step_out_ok && step_cid == 0;
-    float* ho_root = host_out ? s->d_host_out : nullptr;
-    float* ho_rb = host_out ? s->d_host_out + (size_t)s->na * MG_STATE_N : nullptr;
-    float* ho_dof = host_out && s->nd ? s->d_host_out + (size_t)(s->na + s->nb) * MG_STATE_N : nullptr;
+    float* ho_base = s->ho_alias ? s->d_stage_alias : s->d_host_out;
+    const bool host_out = !step_out && ho_base && s->step_out_ok && step_cid == 0;
+    float* ho_root = host_out ? ho_base : nullptr;
+    float* ho_rb = host_out ? ho_base + (size_t)s->na * MG_STATE_N : nullptr;
+    float* ho_dof = host_out && s->nd ? ho_base + (size_t)(s->na + s->nb) * MG_STATE_N : nullptr;
     for (size_t gi = 0; gi < s->groups.size(); ++gi) {
         const ArticGroup& g = s->groups[gi];
         if (g.step_count == 0) continue;
@@ -1418,9 +1439,11 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
         A.gstride = std::max(s->nf1, 1);
         A.ext = s->ext_pending ? s->d_ext : nullptr;
         A.cforce = s->d_cforce;
+        bool reads_root_in = false;
         if (s->pend_root) {   // the deferred root set, read by the step kernel
             A.root_src = s->pend_root;
             A.root_row = s->d_root_row;
+            reads_root_in = s->pend_root == s->d_root_in_alias;
             s->pend_root = nullptr;
         }
         if (step_out || host_out) {
@@ -1430,6 +1453,10 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
             A.out_root_row = s->d_slot_actor;
         }
         HIP_TRY(mg_launch_rigid_step(P, A, st));
+        if (reads_root_in) {
+            HIP_TRY(hipEventRecord(s->root_ev, st));
+            s->root_ev_pending = true;
+        }
     }
     if (int rc_ = flush_root(s, st)) return rc_;   // a root set with no free-body launch
     if (s->groups.empty() && s->env_groups.empty())
@@ -1439,6 +1466,7 @@ int32_t mg_simulate(mg_sim* s, void* stream) {
     s->state_gen++;
     s->dof_sgen++;
     if (host_out) {
+        s->ho_written = ho_base;
         s->ho_root_gen = s->state_gen;
         s->ho_rb_gen = s->state_gen;
         s->ho_dof_gen = ho_dof ? s->dof_sgen : -1;
@@ -1491,33 +1519,71 @@ int32_t mg_fetch_host_state(mg_sim* s, float* dst, int32_t parts, void* stream) 
     const size_t off[5] = {0, (size_t)s->na * MG_STATE_N, (size_t)(s->na + s->nb) * MG_STATE_N,
                            (size_t)(s->na + s->nb) * MG_STATE_N + (size_t)s->nd * 2,
                            (size_t)(s->na + s->nb) * MG_STATE_N + (size_t)s->nd * 2 + (size_t)s->nb * 3};
-    if (s->host_out_n < off[4]) {   // the output stage (simulate writes into it from now on)
+    // zero-copy when dst is the sim's own mapped stage (mg_host_stage): the parts
+    // the last simulate wrote are already there, the others are gathered into it
+    const bool alias = s->h_stage && dst == s->h_stage && s->h_stage_n >= off[4];
+    if (!alias && s->host_out_n < off[4]) {   // the output stage (simulate writes into it from now on)
         if (s->d_host_out) (void)hipFree(s->d_host_out);
         s->d_host_out = nullptr;
         HIP_TRY(dalloc(&s->d_host_out, std::max<size_t>(off[4], 1)));
         s->host_out_n = off[4];
-        s->ho_root_gen = s->ho_rb_gen = s->ho_dof_gen = -1;
+        if (s->ho_written && !s->ho_alias) s->ho_written = nullptr;
     }
+    s->ho_alias = alias;
+    float* base = alias ? s->d_stage_alias : s->d_host_out;
+    const bool fresh = s->ho_written == base;
     int lo = -1, hi = -1;
     for (int k = 0; k < 4; ++k) {
         if (!((parts >> k) & 1) || off[k + 1] == off[k]) continue;
         if (lo < 0) lo = k;
         hi = k;
-        float* d = s->d_host_out + off[k];
+        float* d = base + off[k];
         // parts the last simulate wrote there, with no state change since: no gather
-        if (k == 0 && s->ho_root_gen != s->state_gen)
+        if (k == 0 && !(fresh && s->ho_root_gen == s->state_gen))
             HIP_TRY(mg_launch_gather_rows(s->d_state, s->nb, MG_STATE_N, s->d_actor_root, s->na, d, st));
-        if (k == 1 && s->ho_rb_gen != s->state_gen)
+        if (k == 1 && !(fresh && s->ho_rb_gen == s->state_gen))
             HIP_TRY(mg_launch_gather_rows(s->d_state, s->nb, MG_STATE_N, s->d_perm, s->nb, d, st));
-        if (k == 2 && s->ho_dof_gen != s->dof_sgen)
+        if (k == 2 && !(fresh && s->ho_dof_gen == s->dof_sgen))
             HIP_TRY(mg_launch_gather_rows(s->d_dof, s->nd, 2, nullptr, s->nd, d, st));
         if (k == 3) HIP_TRY(mg_launch_gather_rows(s->d_cforce, s->nb, 3, s->d_perm, s->nb, d, st));
     }
-    if (lo >= 0)
+    if (lo >= 0 && !alias)
         HIP_TRY(hipMemcpyAsync(dst + off[lo], s->d_host_out + off[lo], (off[hi + 1] - off[lo]) * sizeof(float),
                                hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return MG_OK;
+}
+
+float* mg_host_stage(mg_sim* s, int64_t nfloat) {
+    if (!s || nfloat <= 0) { fail(MG_ERR_ARG, "null sim or empty stage"); return nullptr; }
+    if (s->h_stage && s->h_stage_n >= (size_t)nfloat) return s->h_stage;
+    if (hipSetDevice(s->device) != hipSuccess) { fail(MG_ERR_DEVICE, "hipSetDevice failed"); return nullptr; }
+    if (s->h_stage) {
+        (void)hipDeviceSynchronize();
+        (void)hipHostFree(s->h_stage);
+        s->h_stage = nullptr;
+        s->d_stage_alias = nullptr;
+        s->h_stage_n = 0;
+        s->ho_alias = false;
+        s->ho_written = nullptr;
+    }
+    float* h = nullptr;
+    if (hipHostMalloc((void**)&h, (size_t)nfloat * sizeof(float), hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess) {
+        fail(MG_ERR_DEVICE, "hipHostMalloc of the host stage failed");
+        return nullptr;
+    }
+    float* d = nullptr;
+    if (hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess || !d) {
+        (void)hipHostFree(h);
+        fail(MG_ERR_DEVICE, "hipHostGetDevicePointer of the host stage failed");
+        return nullptr;
+    }
+    std::memset(h, 0, (size_t)nfloat * sizeof(float));
+    s->h_stage = h;
+    s->d_stage_alias = d;
+    s->h_stage_n = (size_t)nfloat;
+    return h;
 }
 
 int32_t mg_set_fusion(mg_sim* s, int32_t flags) {
@@ -1730,13 +1796,17 @@ int32_t mg_set_actor_root_state(mg_sim* s, const float* src, int32_t src_host, c
         // CPU pipeline, full set: copied at the call into the library's own buffer
         // (Isaac Gym's copy-at-set), read by the next simulate's step kernel like
         // a fused device set — or by the scatter a reader of the state issues first
-        if (!s->d_root_pend) HIP_TRY(dalloc(&s->d_root_pend, (size_t)s->na * MG_STATE_N));
+        const size_t bytes = (size_t)s->na * MG_STATE_N * sizeof(float);
         s->pend_root = nullptr;     // a later full set replaces an earlier deferred one
-        const void* srcs[1] = {src};
-        const size_t bytes[1] = {(size_t)s->na * MG_STATE_N * sizeof(float)};
-        void* dsts[1] = {s->d_root_pend};
-        if (int rc_ = pin_h2d(s, 1, srcs, bytes, dsts, st)) return rc_;
-        s->pend_root = s->d_root_pend;
+        if (!s->h_root_in) {        // page-locked and device-mapped: the step kernel reads it over PCIe
+            HIP_TRY(hipHostMalloc((void**)&s->h_root_in, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+            HIP_TRY(hipHostGetDevicePointer((void**)&s->d_root_in_alias, s->h_root_in, 0));
+            HIP_TRY(hipEventCreateWithFlags(&s->root_ev, hipEventDisableTiming));
+        }
+        if (s->root_ev_pending) HIP_TRY(hipEventSynchronize(s->root_ev));   // its last reader is done
+        s->root_ev_pending = false;
+        std::memcpy(s->h_root_in, src, bytes);
+        s->pend_root = s->d_root_in_alias;
         s->pend_root_cap = 0;
         return MG_OK;
     }
