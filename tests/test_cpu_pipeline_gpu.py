@@ -94,3 +94,39 @@ def test_cpu_pipeline_copy_at_set_and_set_before_fetch_gpu(gym):
         gym.refresh_rigid_body_state_tensor(sim)
         assert np.array_equal(rb.numpy(), st), "step %d: rigid-body tensor" % k
         assert np.array_equal(root.numpy(), st[roots]), "step %d: root tensor" % k
+
+
+@pytest.mark.parametrize("kind", ["gimbal", "pile"])
+def test_cpu_pipeline_other_kernels_gpu(gym, kind):
+    """The zero-copy host stage with the other step kernels: the S2 gimbal
+    (k_artic_chain writes its body and DOF rows into the mapped stage itself;
+    DOF targets set from a host tensor every step) and the S6 ball pile
+    (k_pile_step: the fetch gathers into the mapped stage). Every step's
+    refreshed host tensors equal the oracle bit for bit."""
+    n, steps = 64, 30
+    if kind == "gimbal":
+        sim, _ = scenes.gimbal_scene(gym, n, use_gpu_pipeline=False)
+    else:
+        sim, _ = scenes.ball_pile_scene(gym, 8, use_gpu_pipeline=False)
+    gym.prepare_sim(sim)
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    assert rb.device.type == "cpu" and sim.host_stage is not None
+    p, m = sim.mg_params(), sim.mg_model()
+    A = sim.model_arrays
+    st, ds = A["body_state0"].copy(), A["dof_state0"].copy()
+    tgt = np.zeros((ds.shape[0], 3), np.float32)
+    tg = scenes.gimbal_targets(n, steps, "cpu", seed=8) if kind == "gimbal" else None
+    for k in range(steps):
+        if tg is not None:
+            t = tg[k].contiguous()
+            assert gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(t))
+            tgt[:, 0] = t.numpy()
+        gym.simulate(sim)
+        gym.fetch_results(sim, True)
+        oracle.step(p, m, st, ds, tgt=tgt)
+        gym.refresh_rigid_body_state_tensor(sim)
+        if ds.shape[0]:
+            gym.refresh_dof_state_tensor(sim)
+            assert np.array_equal(dof.numpy(), ds), "step %d: DOF tensor" % k
+        assert np.array_equal(rb.numpy(), st), "step %d: rigid-body tensor" % k
