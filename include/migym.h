@@ -327,6 +327,18 @@ int32_t     mg_snapshot_render_state(mg_sim* sim, void* stream);
 int32_t     mg_render_cameras(mg_sim* sim, const mg_camera* cams, int32_t n, void* stream);
 /* Duration in ms of the last mg_render_cameras launch (HIP events), -1 if none. */
 float       mg_last_render_ms(mg_sim* sim);
+/* gym.set_light_parameters(sim, 0, intensity, ambient, direction)
+ * (examples/domain_randomization.py:186): the directional light of later renders.
+ * A body's colour c is drawn as c * (ambient + color * max(n . dir, 0)) per
+ * channel (c * ambient in shadow); dir points towards the light (normalised
+ * here). NULL restores the default: ambient 0.3, color 0.7, dir (0.3, 0.2, 1)
+ * z-up / (0.3, 1, 0.2) y-up. The checker ground keeps its fixed colours. */
+typedef struct mg_light {
+    float dir[3];
+    float color[3];
+    float ambient[3];
+} mg_light;
+int32_t     mg_set_light(mg_sim* sim, const mg_light* light);
 
 /* ---- step fusion ------------------------------------------------------------
  * MG_FUSE_ROOT_SET: the deferred root-state set described above.

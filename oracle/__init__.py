@@ -172,15 +172,16 @@ def obb_apart(a, b, margin, hull_a=None, hull_b=None):
     return bool(L.oracle_obb_apart(a.ctypes.data, _ptr(ha), b.ctypes.data, _ptr(hb), float(margin)))
 
 
-def render(sim_params, state, body_tmpl, tbi, shapes, env_body_first, color, seg, cam, hulls=None):
+def render(sim_params, state, body_tmpl, tbi, shapes, env_body_first, color, seg, cam, hulls=None, light=None):
     """One camera on the host (oracle_render, migym_oracle_render.c): returns
     (rgba (H, W, 4) uint8, depth (H, W) f32, seg (H, W) int32). state is the
     rigid-body tensor [nb, 13] (global order); cam a _native.MgCamera (its
-    device pointers are ignored)."""
+    device pointers are ignored); light an _native.MgLight (mg_set_light) or
+    None for the default light."""
     L = lib()
     vp = ctypes.c_void_p
     L.oracle_render.restype = ctypes.c_int
-    L.oracle_render.argtypes = [vp] * 13
+    L.oracle_render.argtypes = [vp] * 14
     H, W = cam.height, cam.width
     rgba = np.zeros((H, W, 4), np.uint8)
     depth = np.zeros((H, W), np.float32)
@@ -192,7 +193,8 @@ def render(sim_params, state, body_tmpl, tbi, shapes, env_body_first, color, seg
     hl = np.ascontiguousarray(hulls if hulls is not None and len(hulls) else np.zeros(1), np.float32)
     ptrs = [a.ctypes.data for a in arrs]
     rc = L.oracle_render(ctypes.addressof(sim_params), ptrs[0], ptrs[1], ptrs[2], ptrs[3], hl.ctypes.data, ptrs[4],
-                         ptrs[5], ptrs[6], ctypes.addressof(cam), rgba.ctypes.data, depth.ctypes.data, sg.ctypes.data)
+                         ptrs[5], ptrs[6], ctypes.addressof(cam), rgba.ctypes.data, depth.ctypes.data, sg.ctypes.data,
+                         ctypes.addressof(light) if light is not None else None)
     if rc != 0:
         raise RuntimeError("oracle_render: too many shapes in the camera's env")
     return rgba, depth, sg

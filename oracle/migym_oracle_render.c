@@ -156,12 +156,13 @@ static unsigned q8_(float x) { return (unsigned)(fminf(fmaxf(x, 0.0f), 1.0f) * 2
  * [num_envs+1]; color [nb][3]; seg [nb]. Outputs may be NULL. */
 int oracle_render(const mg_sim_params* p, const float* state, const int32_t* body_tmpl, const int32_t* tbi,
                   const float* shapes, const float* hulls, const int32_t* env_body_first, const float* color,
-                  const int32_t* seg, const mg_camera* cam, uint8_t* rgba_out, float* depth_out, int32_t* seg_out) {
+                  const int32_t* seg, const mg_camera* cam, uint8_t* rgba_out, float* depth_out, int32_t* seg_out,
+                  const mg_light* light) {
     rws_t ws[MG_RENDER_MAX_SHAPES];
     int ns = 0, b, k, row, col;
     v3_t o, f, l, u, upv, leftv, fwdv, L, gn;
     q4_t q;
-    float ifx, ify, lx = 0.3f, ly = 0.2f, lz = 1.0f, inv, h0;
+    float ifx, ify, lx = 0.3f, ly = 0.2f, lz = 1.0f, inv, h0, lcol[3], amb[3];
     int up_axis = p->up_axis == 0 ? 0 : 1;
 
     /* the env's shapes in the world frame */
@@ -212,6 +213,11 @@ int oracle_render(const mg_sim_params* p, const float* state, const int32_t* bod
         fwdv = V(0.0f, 0.0f, -1.0f);
         ly = 1.0f; lz = 0.2f;
     }
+    for (k = 0; k < 3; ++k) { lcol[k] = 0.7f; amb[k] = 0.3f; }
+    if (light) {   /* mg_set_light (migym_capi.cpp mg_render_cameras) */
+        lx = light->dir[0]; ly = light->dir[1]; lz = light->dir[2];
+        for (k = 0; k < 3; ++k) { lcol[k] = light->color[k]; amb[k] = light->ambient[k]; }
+    }
     inv = 1.0f / sqrtf(lx * lx + ly * ly + lz * lz);
     L = V(lx * inv, ly * inv, lz * inv);
     f = qrot_(q, fwdv);
@@ -257,8 +263,10 @@ int oracle_render(const mg_sim_params* p, const float* state, const int32_t* bod
             for (j = 0; j < ns && !shadow; ++j) shadow = ray_shape_(ps, L, &ws[j], 0.0f, R_INF) < R_INF;
             if (hit >= 0) {
                 float lam = fmaxf(fdot_(n, L), 0.0f);
-                float kk = shadow ? 0.3f : fmaf(0.7f, lam, 0.3f);
-                rgba = q8_(ws[hit].r * kk) | (q8_(ws[hit].g * kk) << 8) | (q8_(ws[hit].b * kk) << 16) | 0xFF000000u;
+                float kr = shadow ? amb[0] : fmaf(lcol[0], lam, amb[0]);
+                float kg = shadow ? amb[1] : fmaf(lcol[1], lam, amb[1]);
+                float kb = shadow ? amb[2] : fmaf(lcol[2], lam, amb[2]);
+                rgba = q8_(ws[hit].r * kr) | (q8_(ws[hit].g * kg) << 8) | (q8_(ws[hit].b * kb) << 16) | 0xFF000000u;
                 sgv = ws[hit].seg;
             } else {
                 float uu = pp.x, vv = up_axis == 1 ? pp.y : pp.z;

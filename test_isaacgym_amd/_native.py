@@ -94,6 +94,11 @@ class MgCamera(ctypes.Structure):
     ]
 
 
+class MgLight(ctypes.Structure):
+    """mg_light (include/migym.h): the renderer's directional light."""
+    _fields_ = [("dir", ctypes.c_float * 3), ("color", ctypes.c_float * 3), ("ambient", ctypes.c_float * 3)]
+
+
 MG_RENDER_MAX_SHAPES = 64
 
 
@@ -152,6 +157,7 @@ def _load():
         "mg_set_render_bodies": (i32, [vp, vp, vp, vp]),
         "mg_snapshot_render_state": (i32, [vp, vp]),
         "mg_render_cameras": (i32, [vp, vp, i32, vp]),
+        "mg_set_light": (i32, [vp, vp]),
         "mg_last_render_ms": (ctypes.c_float, [vp]),
         "mg_cube_pick_step": (i32, [vp, vp]),
     }
@@ -177,7 +183,7 @@ EXPORTED_SYMBOLS = (
     "mg_bind_dof_refresh_target", "mg_step_out_supported", "mg_last_set_deferred", "mg_discard_pending_sets", "mg_last_step_ms", "mg_step_time_stats", "mg_num_free_bodies",
     "mg_num_articulations",
     "mg_num_coupled_envs", "mg_num_pile_envs", "mg_fetch_host_state", "mg_host_stage", "mg_refresh_jacobian_mass_matrix",
-    "mg_set_render_bodies", "mg_snapshot_render_state", "mg_render_cameras", "mg_last_render_ms",
+    "mg_set_render_bodies", "mg_snapshot_render_state", "mg_render_cameras", "mg_set_light", "mg_last_render_ms",
     "mg_debug_copy_env_ctab", "mg_debug_artic_groups", "mg_step_untimed_launches", "mg_cube_pick_step", "mg_env_ctab_floats", "mg_env_carry_floats",
 )
 

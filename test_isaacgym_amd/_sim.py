@@ -250,6 +250,7 @@ class Sim:
         self.cam_version = 0       # bumped by every camera change (render tables are rebuilt)
         self.render_version = 0    # bumped by body colour / segmentation changes
         self.textures = []          # create_texture_from_file / _buffer: the handle is the index
+        self.light = None           # set_light_parameters (an _native.MgLight), None: the default light
 
     @property
     def renderer(self):
@@ -613,6 +614,8 @@ class Sim:
             if dof.is_cuda and dof.numel():   # written by the step itself under STEP_FUSION_STEP_OUT
                 N.check(N.lib.mg_bind_dof_refresh_target(handle, dof.data_ptr()), "mg_bind_dof_refresh_target")
             N.lib.mg_set_fusion(handle, self.fusion)
+            if self.light is not None:
+                N.check(N.lib.mg_set_light(handle, ctypes.byref(self.light)), "mg_set_light")
             # actor DOF targets / props set before prepare
             self._push_dof_targets_all()
         self.finalized = True

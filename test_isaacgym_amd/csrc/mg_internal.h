@@ -277,6 +277,7 @@ struct MgRenderArgs {
     float               fwd[3], up[3], left[3];   // camera-frame view / up / left axes (local)
     int                 up_axis;           // 1: checker on (x, y); 0: on (x, z)
     float               light[3];          // unit direction towards the light
+    float               lcol[3], lamb[3];  // light colour and ambient per channel (mg_set_light)
 };
 
 // Kernel timing by dispatch timestamps: while mg_timer is set (by mg_simulate,

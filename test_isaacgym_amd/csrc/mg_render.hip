@@ -242,8 +242,10 @@ __device__ __forceinline__ void shade(const MgRenderArgs& A, const Cam& C, const
     }
     if (hit >= 0) {
         const float lam = fmaxf(fdot(n, L), 0.0f);
-        const float k = shadow ? 0.3f : fmaf(0.7f, lam, 0.3f);
-        rgba = q8(sws[hit].r * k) | (q8(sws[hit].g * k) << 8) | (q8(sws[hit].b * k) << 16) | 0xFF000000u;
+        const float kr = shadow ? A.lamb[0] : fmaf(A.lcol[0], lam, A.lamb[0]);
+        const float kg = shadow ? A.lamb[1] : fmaf(A.lcol[1], lam, A.lamb[1]);
+        const float kb = shadow ? A.lamb[2] : fmaf(A.lcol[2], lam, A.lamb[2]);
+        rgba = q8(sws[hit].r * kr) | (q8(sws[hit].g * kg) << 8) | (q8(sws[hit].b * kb) << 16) | 0xFF000000u;
         seg = sws[hit].seg;
     } else {
         const float uu = p.x, vv = A.up_axis == 1 ? p.y : p.z;

@@ -202,6 +202,8 @@ struct mg_sim {
     // into it over PCIe and the fetch's remaining gathers do too (no copy); and
     // a mapped input buffer the step kernel reads a host root set from
     // (root_ev: its last reader, waited on before it is refilled)
+    bool has_light = false;           // mg_set_light (else the default light)
+    mg_light light{};
     float* h_stage = nullptr;
     float* d_stage_alias = nullptr;
     size_t h_stage_n = 0;
@@ -1554,6 +1556,19 @@ int32_t mg_fetch_host_state(mg_sim* s, float* dst, int32_t parts, void* stream) 
     return MG_OK;
 }
 
+int32_t mg_set_light(mg_sim* s, const mg_light* light) {
+    if (!s) return fail(MG_ERR_ARG, "null sim");
+    if (!light) {
+        s->has_light = false;
+        return MG_OK;
+    }
+    const float* d = light->dir;
+    if (!(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] > 0.0f)) return fail(MG_ERR_ARG, "zero light direction");
+    s->light = *light;
+    s->has_light = true;
+    return MG_OK;
+}
+
 float* mg_host_stage(mg_sim* s, int64_t nfloat) {
     if (!s || nfloat <= 0) { fail(MG_ERR_ARG, "null sim or empty stage"); return nullptr; }
     if (s->h_stage && s->h_stage_n >= (size_t)nfloat) return s->h_stage;
@@ -2096,6 +2111,11 @@ int32_t mg_render_cameras(mg_sim* s, const mg_camera* cams, int32_t n, void* str
         A.up[0] = 0.0f; A.up[1] = 1.0f; A.up[2] = 0.0f;
         A.left[0] = -1.0f; A.left[1] = 0.0f; A.left[2] = 0.0f;
         ly = 1.0f; lz = 0.2f;
+    }
+    for (int k = 0; k < 3; ++k) { A.lcol[k] = 0.7f; A.lamb[k] = 0.3f; }
+    if (s->has_light) {
+        lx = s->light.dir[0]; ly = s->light.dir[1]; lz = s->light.dir[2];
+        for (int k = 0; k < 3; ++k) { A.lcol[k] = s->light.color[k]; A.lamb[k] = s->light.ambient[k]; }
     }
     const float inv = 1.0f / sqrtf(lx * lx + ly * ly + lz * lz);
     A.light[0] = lx * inv; A.light[1] = ly * inv; A.light[2] = lz * inv;

@@ -1240,7 +1240,23 @@ class Gym:
         pass
 
     def set_light_parameters(self, sim, light_index, intensity, ambient, direction):
-        pass
+        """examples/domain_randomization.py:186: the directional light of the
+        camera renders (include/migym.h mg_set_light): per channel, a body is
+        drawn as colour * (ambient + intensity * max(n . direction, 0)),
+        direction pointing towards the light. One light (index 0) is modelled."""
+        if light_index != 0:
+            print("*** migym: set_light_parameters: only light 0 is modelled", file=sys.stderr)
+            return
+        L = N.MgLight()
+        L.dir[:] = (direction.x, direction.y, direction.z)
+        L.color[:] = (intensity.x, intensity.y, intensity.z)
+        L.ambient[:] = (ambient.x, ambient.y, ambient.z)
+        if not (direction.x ** 2 + direction.y ** 2 + direction.z ** 2) > 0.0:
+            print("*** migym: set_light_parameters: zero direction", file=sys.stderr)
+            return
+        sim.light = L
+        if sim.native:
+            N.check(N.lib.mg_set_light(sim.native, ctypes.byref(L)), "mg_set_light")
 
     def draw_env_rigid_contacts(self, viewer, env, color, scale, flag):
         pass

@@ -46,7 +46,7 @@ def _oracle_image(sim, state, cam):
     first, color, seg = _render.body_render_arrays(sim)
     rec = _render.camera_record(sim, cam)
     return oracle.render(sim.mg_params(), state, A["body_tmpl"], A["tmpl_body_i"], A["shapes"], first, color, seg,
-                         rec, hulls=A["hulls"])
+                         rec, hulls=A["hulls"], light=sim.light)
 
 
 def _ball_features(rgba):
@@ -354,3 +354,45 @@ def test_render_config5_full_size_sampled_bitexact(gym):
         lit.append(float((imgs[e][0][..., :3].amax(-1) > 0).float().mean()))
     assert max(lit) > 0.05, lit
     gym.destroy_sim(sim)
+
+
+@pytest.mark.gpu
+def test_light_parameters_gpu_bitexact(gym):
+    """gym.set_light_parameters (examples/domain_randomization.py:186): a
+    coloured, dimmer light from the side changes the bodies' shading and the
+    shadows' direction (the checker's colours are fixed), bit for bit the
+    oracle renderer with the same light;
+    set_light_parameters before prepare_sim applies at prepare."""
+    n = 8
+    sim, envs, tens = _servo_with_cameras(gym, n, 96, 54)
+    gym.set_light_parameters(sim, 0, gymapi.Vec3(0.9, 0.5, 0.2), gymapi.Vec3(0.1, 0.15, 0.2),
+                             gymapi.Vec3(1.0, -0.5, 0.4))
+    gym.prepare_sim(sim)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    down = gymapi.Quat.from_euler_zyx(0.0, math.atan2(100.0, 10.0), 0.0)
+    gym.refresh_actor_root_state_tensor(sim)
+    root[0::2, 3:7] = torch.tensor([down.x, down.y, down.z, down.w], device=DEV)
+    root[:, 7:13] = 0.0
+    assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+    gym.simulate(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    gym.render_all_camera_sensors(sim)
+    st = rb.cpu().numpy()
+    lit = [t[0].cpu().numpy().copy() for t in tens]
+    for e in range(n):
+        _assert_same(sim, st, envs[e], 0, tens[e], "lit env %d" % e)
+    # the default light again: the bodies' shading changes (and the shadows move)
+    gym.set_light_parameters(sim, 0, gymapi.Vec3(0.7, 0.7, 0.7), gymapi.Vec3(0.3, 0.3, 0.3),
+                             gymapi.Vec3(0.3, 0.2, 1.0))
+    gym.render_all_camera_sensors(sim)
+    body_px = 0
+    for e in range(n):
+        seg = tens[e][2].cpu().numpy()
+        now = tens[e][0].cpu().numpy()
+        _assert_same(sim, st, envs[e], 0, tens[e], "default env %d" % e)
+        ground = seg == 0
+        body_px += int((~ground).sum())
+        if (~ground).any():
+            assert not np.array_equal(now[~ground], lit[e][~ground])
+    assert body_px > 0
