@@ -892,6 +892,26 @@ def _quat_between(a, b):
     return q / np.linalg.norm(q)
 
 
+def _mj_expand_includes(el, base_dir, depth=0):
+    """MJCF <include file="..."/> (open_ai_assets/hand/shadow_hand.xml:8-15): the
+    included file's top-level children (its root is a <mujoco> element) replace
+    the include element in place, recursively, paths relative to the including
+    file."""
+    if depth > 16:
+        raise ValueError("MJCF: <include> nested deeper than 16 levels")
+    out = []
+    for child in list(el):
+        if child.tag == "include":
+            path = os.path.join(base_dir, child.get("file", ""))
+            inc = ET.parse(path).getroot()
+            _mj_expand_includes(inc, os.path.dirname(path), depth + 1)
+            out.extend(list(inc))
+        else:
+            _mj_expand_includes(child, base_dir, depth)
+            out.append(child)
+    el[:] = out
+
+
 class _MjDefaults:
     """<default> attribute sets: the top level and named classes (one level of
     nesting inherits from its parent class)."""
@@ -977,11 +997,17 @@ def load_mjcf(asset_root, filename, options):
     if not os.path.exists(path):
         raise FileNotFoundError(path)
     root = ET.parse(path).getroot()
+    _mj_expand_includes(root, os.path.dirname(path))
     comp = root.find("compiler")
     angle_deg = comp is None or comp.get("angle", "degree") != "radian"
     k_ang = math.pi / 180.0 if angle_deg else 1.0
     defaults = _MjDefaults(root)
     warnings = []
+    # elements that would change the dynamics but are not modelled: said, not dropped silently
+    for tag, what in (("tendon", "tendons"), ("equality", "equality constraints")):
+        el = root.find(tag)
+        if el is not None and len(el):
+            warnings.append("MJCF %s: %d %s not modelled" % (os.path.basename(path), len(el), what))
     wb = root.find("worldbody")
     if wb is None:
         raise ValueError("MJCF %s: no <worldbody>" % path)

@@ -129,3 +129,39 @@ def test_convex_decomposition_of_a_concave_mesh(gym, tmp_path):
         assert np.any(h.equations @ np.append(gap, 1.0) > 1e-9), "a piece covers the gap"
     assert abs(vol - 7e-3) < 0.15 * 7e-3, vol
     assert ConvexHull(s1[0].hull.verts).volume > 8.5e-3        # the single hull: 9e-3, gap included
+
+
+def test_mjcf_include_and_unmodelled_elements(gym, tmp_path, capsys):
+    """MJCF <include file=.../> (open_ai_assets/hand/shadow_hand.xml:8-15): the
+    included file's top-level children replace the include, recursively and
+    relative to the including file; tendons / equality constraints, which this
+    build does not model, are said on stderr rather than dropped silently."""
+    sub = tmp_path / "parts"
+    sub.mkdir()
+    (sub / "robot.xml").write_text(textwrap.dedent('''\
+        <mujoco>
+          <body name="base" pos="0 0 1">
+            <geom type="box" size="0.1 0.1 0.1"/>
+            <include file="arm.xml"/>
+          </body>
+        </mujoco>'''))
+    (sub / "arm.xml").write_text(textwrap.dedent('''\
+        <mujoco>
+          <body name="arm" pos="0 0 0.3">
+            <joint name="j0" type="hinge" axis="0 1 0" range="-45 45"/>
+            <geom type="capsule" fromto="0 0 0 0 0 0.2" size="0.03"/>
+          </body>
+        </mujoco>'''))
+    (tmp_path / "top.xml").write_text(textwrap.dedent('''\
+        <mujoco model="inc">
+          <worldbody><include file="parts/robot.xml"/></worldbody>
+          <tendon><fixed name="t"><joint joint="j0" coef="1"/></fixed></tendon>
+        </mujoco>'''))
+    sim = gym.create_sim(0, 0, gymapi.SIM_PHYSX, gymapi.SimParams())
+    opts = gymapi.AssetOptions()
+    opts.fix_base_link = True
+    a = gym.load_asset(sim, str(tmp_path), "top.xml", opts)
+    assert a is not None
+    assert gym.get_asset_rigid_body_names(a) == ["base", "arm"]
+    assert gym.get_asset_dof_names(a) == ["j0"]
+    assert "1 tendons not modelled" in capsys.readouterr().err

@@ -255,7 +255,7 @@ SETUP_ONLY = [("asset_info.py", []), ("convex_decomposition.py", []), ("dof_cont
               ("large_mass_ratio.py", []), ("spherical_joint.py", []), ("transforms.py", []),
               ("multiple_camera_envs.py", []), ("graphics.py", []), ("graphics_materials.py", []),
               ("apply_forces.py", ["--pipeline", "cpu"]), ("apply_forces_at_pos.py", ["--pipeline", "cpu"]),
-              ("franka_osc.py", ["--pipeline", "cpu"])]
+              ("franka_osc.py", ["--pipeline", "cpu"]), ("actor_scaling.py", [])]
 
 
 @pytest.mark.skipif(has_gpu(), reason="CPU-container variant")
