@@ -186,7 +186,7 @@ class Renderer:
         self.snap = True
         self.frame += 1
         if self.batch is None or self.batch[2] != sim.cam_version:
-            tcams = [c for e in sim.envs for c in e.cameras if c.images]
+            tcams = [c for e in sim.envs for c in e.cameras if c.images and not c.destroyed]
             arr = (N.MgCamera * max(len(tcams), 1))(*[camera_record(sim, c, c.images) for c in tcams])
             self.batch = (arr, len(tcams), sim.cam_version)
         if self.batch[1]:

@@ -206,6 +206,7 @@ class CameraSensor:
         self.follow = T.FOLLOW_TRANSFORM
         self.transform = T.Transform()   # env-frame transform when not attached
         self.images = {}                 # IMAGE_* -> persistent device tensor (get_camera_image_gpu_tensor)
+        self.destroyed = False           # destroy_camera_sensor: no longer rendered (its handle stays taken)
 
 
 class Sim:

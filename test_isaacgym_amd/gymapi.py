@@ -1272,7 +1272,12 @@ class Gym:
         return cam.handle
 
     def destroy_camera_sensor(self, sim, env, handle):
-        pass
+        """The camera is no longer rendered and its images can no longer be read
+        (the other cameras keep their handles)."""
+        cam = env.cameras[handle]
+        cam.destroyed = True
+        cam.images = {}
+        sim.cam_version += 1
 
     def set_camera_location(self, handle, env, pos, target):
         """examples/interop_torch.py:111: env-frame position looking at target."""
@@ -1344,6 +1349,8 @@ class Gym:
     def get_camera_image(self, sim, env, handle, image_type):
         """test11_servo_vecenv_camerazoom.py:459: host image of the last render
         (color (H, W*4) uint8, depth (H, W) float32, segmentation (H, W) int32)."""
+        if env.cameras[handle].destroyed:
+            raise ValueError("camera %d of env %d was destroyed" % (handle, env.index))
         if image_type not in _render.IMAGE_KINDS:
             p = env.cameras[handle].props
             return np.zeros((p.height, p.width), dtype=np.float32)
