@@ -396,3 +396,48 @@ def test_light_parameters_gpu_bitexact(gym):
         if (~ground).any():
             assert not np.array_equal(now[~ground], lit[e][~ground])
     assert body_px > 0
+
+
+@pytest.mark.gpu
+def test_destroy_camera_sensor_gpu(gym):
+    """destroy_camera_sensor: the camera is no longer rendered (its image
+    tensor keeps the last render) and can no longer be read; the env's other
+    camera keeps its handle and is still rendered bit for bit."""
+    n = 2
+    sim, envs = scenes.servo_scene(gym, n)
+    props = gymapi.CameraProperties()
+    props.width, props.height = 48, 27
+    cams = []
+    for env in envs:
+        pair = []
+        for k in range(2):
+            c = gym.create_camera_sensor(env, props)
+            local = gymapi.Transform()
+            local.p = gymapi.Vec3(5, 0, 0)
+            gym.attach_camera_to_body(c, env, gym.get_actor_rigid_body_handle(env, 0, 0), local,
+                                      gymapi.FOLLOW_TRANSFORM)
+            pair.append(c)
+        cams.append(pair)
+    imgs = [[gymtorch.wrap_tensor(gym.get_camera_image_gpu_tensor(sim, envs[e], c, gymapi.IMAGE_COLOR))
+             for c in cams[e]] for e in range(n)]
+    gym.prepare_sim(sim)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    gym.simulate(sim)
+    gym.render_all_camera_sensors(sim)
+    first = imgs[0][1].clone()
+    gym.destroy_camera_sensor(sim, envs[0], cams[0][1])
+    gym.refresh_actor_root_state_tensor(sim)
+    down = gymapi.Quat.from_euler_zyx(0.0, 1.4, 0.0)
+    root[:, 3:7] = torch.tensor([down.x, down.y, down.z, down.w], device=DEV)
+    assert gym.set_actor_root_state_tensor(sim, gymtorch.unwrap_tensor(root))
+    gym.simulate(sim)
+    gym.refresh_rigid_body_state_tensor(sim)
+    gym.render_all_camera_sensors(sim)
+    assert torch.equal(imgs[0][1], first)                    # not rendered again
+    assert not torch.equal(imgs[0][0], first)                 # its sibling is
+    with pytest.raises(ValueError):
+        gym.get_camera_image(sim, envs[0], cams[0][1], gymapi.IMAGE_COLOR)
+    st = rb.cpu().numpy()
+    rgba, _, _ = _oracle_image(sim, st, envs[0].cameras[cams[0][0]])
+    assert np.array_equal(imgs[0][0].cpu().numpy(), rgba)
