@@ -1120,6 +1120,52 @@ class Gym:
             return False
         return True
 
+    def apply_rigid_body_force_at_pos_tensors(self, sim, forceTensor, posTensor=None, space=_T.ENV_SPACE):
+        """examples/apply_forces_at_pos.py:126: forces (num_bodies, 3) applied at
+        points (num_bodies, 3) during the next simulate — the same as the force
+        at the centre of mass plus the torque (p - c) x F. ENV_SPACE / GLOBAL_SPACE:
+        points in the rigid-body tensor's frame (the example passes the refreshed
+        body positions plus an offset); LOCAL_SPACE: force and point in the body
+        frame. No points: forces at the centres of mass."""
+        if posTensor is None:
+            return self.apply_rigid_body_force_tensors(sim, forceTensor, None, space)
+        sim.finalize()
+        h = sim.require_native("apply_rigid_body_force_at_pos_tensors")
+        F = _as_tensor_arg(forceTensor, "apply_rigid_body_force_at_pos_tensors")
+        P = _as_tensor_arg(posTensor, "apply_rigid_body_force_at_pos_tensors")
+        nb = sim.num_bodies
+        if (F.dtype != torch.float32 or P.dtype != torch.float32 or F.numel() != nb * 3 or P.numel() != nb * 3
+                or F.device != P.device):
+            print("*** migym: apply_rigid_body_force_at_pos_tensors: expected float32 tensors of %d x 3 on one "
+                  "device" % nb, file=sys.stderr)
+            return False
+        dev = F.device
+        F = F.reshape(nb, 3)
+        P = P.reshape(nb, 3)
+        # the bodies' current state (a gather into a scratch tensor: the caller's
+        # tensors are left alone) and their centres of mass in the body frame
+        st = torch.empty((nb, 13), dtype=torch.float32, device=dev)
+        N.check(N.lib.mg_refresh_rigid_body_state(h, st.data_ptr(), 1 if dev.type == "cpu" else 0, sim.stream()),
+                "apply_rigid_body_force_at_pos_tensors")
+        com = getattr(sim, "_com_local", None)
+        if com is None or com.device != dev:
+            com = torch.from_numpy(np.ascontiguousarray(sim.model_arrays["body_mass"][:, 8:11],
+                                                        dtype=np.float32)).to(dev)
+            sim._com_local = com
+        x, q = st[:, 0:3], st[:, 3:7]
+
+        def rot(v):           # q (x, y, z, w) applied to v
+            u, w = q[:, 0:3], q[:, 3:4]
+            t = 2.0 * torch.cross(u, v, dim=1)
+            return v + w * t + torch.cross(u, t, dim=1)
+
+        c = x + rot(com)
+        if space == _T.LOCAL_SPACE:
+            F = rot(F)
+            P = x + rot(P)
+        tau = torch.cross(P - c, F, dim=1)
+        return self.apply_rigid_body_force_tensors(sim, F.contiguous(), tau.contiguous(), _T.ENV_SPACE)
+
     def _artic_template(self, sim, actor_name):
         """(template id, asset) of the articulated actors named actor_name; the
         tensors cover every instance of that template, in actor order."""
